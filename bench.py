@@ -1,0 +1,193 @@
+"""ParkingModel train-step benchmark on MI355X (BASELINE.json metric).
+
+One step = one full training step of the reference's ParkingTrainingModule
+(trainer/pl_trainer.py:55-83): forward (4-cam EfficientNet encoder -> lift-splat -> BEV
+encoder -> fusion -> seg/depth heads -> control decoder), the control + segmentation + depth
+losses, backward, and the Adam(lr 1e-4, wd 1e-4) update (:116-121), fp32, on a synthetic
+B-sample batch (4 x 256x256 cameras) that is resident in HBM before timing.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+N>1 is launched by torch.distributed.run (one rank per GPU, RCCL over xGMI): each rank runs
+B samples per step (weak scaling) and gradients are all-reduced (the only exchange).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "e2e-parking-carla_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "train samples/sec (4-cam frames) at B=8, 1/2/4/8 MI355X; CPU-ref baseline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
+
+
+def lss_fwd_bytes(B, N=4, C=64, D=48, hw=1024, XY=40000):
+    """Algorithmic HBM bytes of one fused lift-splat forward launch:
+    read featT + prob once, write the C x X x Y BEV planes once, per sample."""
+    return 4 * B * (N * C * hw + N * D * hw + C * XY)
+
+
+class _Step(torch.nn.Module):
+    """Wraps training_step as forward so DistributedDataParallel can hook it."""
+
+    def __init__(self, mod):
+        super().__init__()
+        self.mod = mod
+
+    def forward(self, batch):
+        return self.mod.training_step(batch, 0)
+
+
+def device_batch(data, dev):
+    out = {}
+    for k, v in data.items():
+        # intrinsics/extrinsics stay on the host, as the dataloader / agent deliver them:
+        # the 3x3 rig algebra runs on the host (bit-exact with the reference CPU path)
+        out[k] = v if k in ("intrinsics", "extrinsics") else v.to(dev, non_blocking=False)
+    return out
+
+
+def cpu_baseline(batch, steps, threads):
+    """The oracle (CPU restatement of the reference, bit-identical to it in the build
+    container) running the same train step on the host cores."""
+    from oracle import parking_ref as O
+    from e2ep_amd import synthetic
+
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    m = O.ParkingModelRef(O.Cfg).train()
+    opt = O.make_optimizer(m)
+    data = synthetic.synthetic_batch(batch, seed=0)
+    O.train_step(m, opt, data)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        O.train_step(m, opt, data)
+    dt = time.perf_counter() - t0
+    return batch * steps / dt, dt
+
+
+def load_traffic(batch):
+    """HBM bytes per lss_fwd launch from the committed rocprofv3 PMC summary, or None."""
+    path = os.path.join(ROOT, "profiles", "lss_fwd_pmc.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        j = json.load(f)
+    if int(j.get("batch", -1)) != batch:
+        return None
+    return float(j["hbm_bytes_per_launch"])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="samples per GPU per step")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from e2ep_amd import _lib, synthetic, timing
+    from tool.config import default_cfg
+    from trainer.pl_trainer import ParkingTrainingModule
+
+    _lib.load()
+    torch.manual_seed(1234)  # identical initial weights on every rank
+    mod = ParkingTrainingModule(default_cfg()).to(dev).train()
+    # bev_encoder.layer4 is built but never run (reference model/bev_encoder.py:21,23-36):
+    # it never has a gradient, so it is kept out of the reducer and the optimizer step.
+    for p in mod.parking_model.bev_encoder.layer4.parameters():
+        p.requires_grad_(False)
+    opt = mod.configure_optimizers()["optimizer"]
+    step_mod = _Step(mod)
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        step_mod = DDP(step_mod, device_ids=[local], broadcast_buffers=False, bucket_cap_mb=32,
+                       gradient_as_bucket_view=True)
+
+    data = device_batch(synthetic.synthetic_batch(args.batch, seed=rank), dev)
+
+    def step():
+        loss = step_mod(data)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    timing.reset()
+    timing.enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timing.enable(False)
+    kern = timing.summary()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    samples = world * args.batch * args.steps
+    value = samples / elapsed
+
+    n_fwd, mean_ms, _ = kern.get("lss_fwd", (0, float("nan"), 0.0))
+    achieved = lss_fwd_bytes(args.batch) / (mean_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.batch)
+    roofline = {"kernel": "e2ep::k_lss_fwd (fused depth x feature outer product + pillar pooling)",
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "bytes_per_launch": lss_fwd_bytes(args.batch), "launch_ms": round(mean_ms, 5),
+                "launches": n_fwd}
+
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        v, dt = cpu_baseline(args.batch, args.cpu_steps, threads)
+        base = {"value": round(v, 4), "unit": "samples/s", "cores": threads, "kind": "port",
+                "sample": f"{args.cpu_steps} timed train steps (after 1 warm-up) of the oracle CPU "
+                          f"restatement at B={args.batch}, 4x256^2, fp32 ({dt:.1f} s)"}
+
+    if rank == 0:
+        line = {"metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "config": {"workload": "ParkingModel train step (fwd + control/seg/depth losses + bwd "
+                                       "+ Adam), 4 cams x 256x256, fp32, random init",
+                           "global_batch": world * args.batch, "batch_per_gpu": args.batch,
+                           "parallelism": f"dp{world}"},
+                "roofline": roofline, "cpu_baseline": base,
+                "final_loss": round(float(loss), 4)}
+        print(json.dumps(line), flush=True)
+        print("kernel timing (launches, mean ms, total ms):",
+              {k: (n, round(m, 4), round(t, 3)) for k, (n, m, t) in kern.items()}, file=sys.stderr)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,403 @@
+// Lift-splat kernels for gfx950: geometry + pillar index, counting-sort plan, fused
+// outer-product/pillar-pool forward, gather backward, transpose, target channel.
+//
+// Reference behaviour (qintonguav/e2e-parking-carla):
+//   model/bev_model.py:45-57   get_geometry        -> k_geom_index (bit-exact, fp32, no FMA)
+//   model/bev_model.py:59-71   outer product       -> fused into k_lss_fwd (never materialised)
+//   model/bev_model.py:74-107  proj_bev_feature    -> k_count/k_scan/k_fill/k_segsort + k_lss_fwd
+//   tool/geometry.py:285-317   VoxelsSumming       -> k_lss_fwd (direct per-pillar sum) /
+//                                                     k_lss_bwd (gather, no atomics)
+//   model/parking_model.py:28-46 add_target_bev    -> k_target_bev
+//
+// HBM layout: prob [B*N][D][hw], featT [B*N][hw][C] (pixel-major, 256-B rows at C=64),
+// bev [B][C..][X*Y] channel-major (the reference's output layout), gT [B][XY][C].
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace e2ep {
+
+// ------------------------------------------------------------------------------------------
+// geometry + pillar index: one thread per frustum point
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_geom_index(
+    const float *__restrict__ frustum, const float *__restrict__ combine,
+    const float *__restrict__ trans, float lo0, float lo1, float lo2, float r0, float r1,
+    float r2, int X, int Y, int Z, int DHW, long long total, int *__restrict__ pillar) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int bn = (int)(i / DHW);
+  const int f = (int)(i - (long long)bn * DHW);
+  const float u = frustum[3 * f + 0], v = frustum[3 * f + 1], d = frustum[3 * f + 2];
+  // points = (u*d, v*d, d)                                   (bev_model.py:51-52)
+  const float p0 = __fmul_rn(u, d), p1 = __fmul_rn(v, d), p2 = d;
+  const float *c = combine + 9 * bn;
+  const float *t = trans + 3 * bn;
+  // combine @ p, accumulated in k order, then + translation  (bev_model.py:54-55)
+  float xyz[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    float a = __fmul_rn(c[3 * r + 0], p0);
+    a = __fadd_rn(a, __fmul_rn(c[3 * r + 1], p1));
+    a = __fadd_rn(a, __fmul_rn(c[3 * r + 2], p2));
+    xyz[r] = __fadd_rn(a, t[r]);
+  }
+  // ((xyz - lo) / res).long(), mask on all three dims      (bev_model.py:85-90)
+  const float gx = truncf(__fdiv_rn(__fsub_rn(xyz[0], lo0), r0));
+  const float gy = truncf(__fdiv_rn(__fsub_rn(xyz[1], lo1), r1));
+  const float gz = truncf(__fdiv_rn(__fsub_rn(xyz[2], lo2), r2));
+  const bool ok = gx >= 0.f && gx < (float)X && gy >= 0.f && gy < (float)Y && gz >= 0.f &&
+                  gz < (float)Z;
+  pillar[i] = ok ? ((int)gx * (Y * Z) + (int)gy * Z + (int)gz) : -1;
+}
+
+// ------------------------------------------------------------------------------------------
+// plan: histogram -> exclusive scan -> fill -> per-pillar sort (deterministic order)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_count(const int *__restrict__ pillar, int P, int XYZ,
+                                               long long total, int *__restrict__ counts) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int q = pillar[i];
+  if (q >= 0) atomicAdd(&counts[(i / P) * XYZ + q], 1);
+}
+
+// one 1024-thread block per sample; offsets[b][0..XYZ] = exclusive scan of counts[b]
+__global__ void __launch_bounds__(1024) k_scan(const int *__restrict__ counts, int XYZ,
+                                               int *__restrict__ offsets,
+                                               int *__restrict__ cursor) {
+  __shared__ int part[1024];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int per = (XYZ + 1023) / 1024;
+  const int beg = min(t * per, XYZ), end = min(beg + per, XYZ);
+  const int *cnt = counts + (long long)b * XYZ;
+  int s = 0;
+  for (int i = beg; i < end; ++i) s += cnt[i];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+    int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;  // exclusive prefix of this thread's chunk
+  int *off = offsets + (long long)b * (XYZ + 1);
+  int *cur = cursor + (long long)b * XYZ;
+  for (int i = beg; i < end; ++i) {
+    off[i] = run;
+    cur[i] = run;
+    run += cnt[i];
+  }
+  if (t == 1023) off[XYZ] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_fill(const int *__restrict__ pillar, int P, int DHW,
+                                              int HW, int XYZ, long long total,
+                                              int *__restrict__ cursor,
+                                              int *__restrict__ order) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int q = pillar[i];
+  if (q < 0) return;
+  const long long b = i / P;
+  const int local = (int)(i - b * P);
+  const int n = local / DHW;
+  const int rem = local - n * DHW;
+  const int d = rem / HW;
+  const int pix = rem - d * HW;
+  const int slot = atomicAdd(&cursor[b * XYZ + q], 1);
+  order[b * P + slot] = (n << 24) | (d << 16) | pix;
+}
+
+// insertion sort of each pillar's segment: fixes the (atomic, racy) fill order
+__global__ void __launch_bounds__(256) k_segsort(const int *__restrict__ offsets, int P, int XYZ,
+                                                 int B, int *__restrict__ order) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * XYZ) return;
+  const long long b = i / XYZ;
+  const int q = (int)(i - b * XYZ);
+  const int *off = offsets + b * (XYZ + 1);
+  int *seg = order + b * P;
+  const int beg = off[q], end = off[q + 1];
+  for (int k = beg + 1; k < end; ++k) {
+    const int key = seg[k];
+    int j = k - 1;
+    while (j >= beg && seg[j] > key) {
+      seg[j + 1] = seg[j];
+      --j;
+    }
+    seg[j + 1] = key;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// fused forward: block = 64 consecutive pillars x 64 channels (4 waves x 16 channels);
+// lane owns one pillar and walks its sorted points; stores are 256-B coalesced per channel.
+// ------------------------------------------------------------------------------------------
+constexpr int FWD_CPW = 16;  // channels per wave
+
+__global__ void __launch_bounds__(256) k_lss_fwd(
+    const float *__restrict__ prob, const float *__restrict__ featT,
+    const int *__restrict__ offsets, const int *__restrict__ order, int N, int D, int HW,
+    int C, int XYZ, int P, float *__restrict__ bev, long long bev_bstride) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.y;
+  const int q = blockIdx.x * 64 + lane;
+  const int c0 = blockIdx.z * 64 + wave * FWD_CPW;
+  if (c0 >= C) return;  // wave-uniform
+  float acc[FWD_CPW];
+#pragma unroll
+  for (int j = 0; j < FWD_CPW; ++j) acc[j] = 0.f;
+  if (q < XYZ) {
+    const int *off = offsets + (long long)b * (XYZ + 1);
+    const int beg = off[q], end = off[q + 1];
+    const int *ord = order + (long long)b * P;
+    const bool vec = (C % 4 == 0) && (c0 + FWD_CPW <= C);
+    for (int k = beg; k < end; ++k) {
+      const int code = ord[k];
+      const int n = code >> 24, d = (code >> 16) & 255, pix = code & 65535;
+      const long long bn = (long long)b * N + n;
+      const float pr = prob[(bn * D + d) * HW + pix];
+      const float *fp = featT + (bn * HW + pix) * C + c0;
+      if (vec) {
+#pragma unroll
+        for (int j = 0; j < FWD_CPW; j += 4) {
+          const float4 f4 = *reinterpret_cast<const float4 *>(fp + j);
+          acc[j + 0] += pr * f4.x;
+          acc[j + 1] += pr * f4.y;
+          acc[j + 2] += pr * f4.z;
+          acc[j + 3] += pr * f4.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < FWD_CPW; ++j)
+          if (c0 + j < C) acc[j] += pr * fp[j];
+      }
+    }
+  }
+  if (q < XYZ) {
+    float *o = bev + (long long)b * bev_bstride + q;
+#pragma unroll
+    for (int j = 0; j < FWD_CPW; ++j)
+      if (c0 + j < C) o[(long long)(c0 + j) * XYZ] = acc[j];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward: wave per pixel (lane = channel), d-loop over the pixel's <=64 depth bins.
+// grad_feat accumulates in a register; grad_prob[d] = sum over lanes, done for all d at once
+// by a recursive-halving transposed reduction (63 shuffles per pixel instead of 6 per bin).
+// ------------------------------------------------------------------------------------------
+constexpr int BWD_PIX_PER_WAVE = 4;
+constexpr int BWD_WAVES = 4;
+constexpr int BWD_PIX = BWD_PIX_PER_WAVE * BWD_WAVES;  // pixels per block
+
+template <int HALF>
+__device__ __forceinline__ void halve(float *v, int lane) {
+  const bool upper = (lane & HALF) != 0;
+#pragma unroll
+  for (int j = 0; j < HALF; ++j) {
+    const float send = upper ? v[j] : v[j + HALF];
+    const float keep = upper ? v[j + HALF] : v[j];
+    v[j] = keep + __shfl_xor(send, HALF, 64);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_lss_bwd(
+    const float *__restrict__ gT, const float *__restrict__ prob,
+    const float *__restrict__ featT, const int *__restrict__ pillar, int N, int D, int HW,
+    int C, int XYZ, float *__restrict__ grad_prob, float *__restrict__ grad_feat) {
+  __shared__ float s_gp[64][BWD_PIX + 1];
+  __shared__ float s_gf[64][BWD_PIX + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bn = blockIdx.y;  // b*N + n
+  const int b = bn / N;
+  const int pix0 = blockIdx.x * BWD_PIX;
+  const bool lane_ok = lane < C;
+  for (int pp = 0; pp < BWD_PIX_PER_WAVE; ++pp) {
+    const int lp = wave * BWD_PIX_PER_WAVE + pp;  // local pixel
+    const int pix = pix0 + lp;
+    if (pix >= HW) break;  // wave-uniform
+    const float f = lane_ok ? featT[((long long)bn * HW + pix) * C + lane] : 0.f;
+    float gf = 0.f;
+    float v[64];
+#pragma unroll
+    for (int d = 0; d < 64; ++d) {
+      v[d] = 0.f;
+      if (d < D) {
+        const long long pidx = ((long long)bn * D + d) * HW + pix;
+        const int q = pillar[pidx];
+        if (q >= 0) {
+          const float g = lane_ok ? gT[((long long)b * XYZ + q) * C + lane] : 0.f;
+          gf += g * prob[pidx];
+          v[d] = g * f;
+        }
+      }
+    }
+    halve<32>(v, lane);
+    halve<16>(v, lane);
+    halve<8>(v, lane);
+    halve<4>(v, lane);
+    halve<2>(v, lane);
+    halve<1>(v, lane);
+    s_gp[lane][lp] = v[0];  // lane == d after the six halvings
+    s_gf[lane][lp] = gf;
+  }
+  __syncthreads();
+  // coalesced write-back: rows d / c, columns = this block's pixels
+  for (int e = threadIdx.x; e < 64 * BWD_PIX; e += 256) {
+    const int r = e / BWD_PIX, lp = e - r * BWD_PIX;
+    const int pix = pix0 + lp;
+    if (pix >= HW) continue;
+    if (r < D) grad_prob[((long long)bn * D + r) * HW + pix] = s_gp[r][lp];
+    if (r < C) grad_feat[((long long)bn * C + r) * HW + pix] = s_gf[r][lp];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// batched transpose through a padded 64x64 LDS tile
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_transpose(const float *__restrict__ in,
+                                                   long long in_bstride, int rows, int cols,
+                                                   float *__restrict__ out) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const float *src = in + (long long)b * in_bstride;
+  float *dst = out + (long long)b * rows * cols;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int gr = r0 + r, gc = c0 + tx;
+    if (gr < rows && gc < cols) tile[r][tx] = src[(long long)gr * cols + gc];
+  }
+  __syncthreads();
+  for (int c = ty; c < 64; c += 4) {
+    const int gc = c0 + c, gr = r0 + tx;
+    if (gr < rows && gc < cols) dst[(long long)gc * rows + gr] = tile[tx][c];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// target channel: block per sample, zero the plane and set the 8x8 square
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void py_slice(int s, int e, int L, int &lo, int &hi) {
+  if (s < 0) s += L;
+  if (s < 0) s = 0;
+  if (e < 0) e += L;
+  if (e < 0) e = 0;
+  lo = min(s, L);
+  hi = min(e, L);
+}
+
+__global__ void __launch_bounds__(256) k_target_bev(const float *__restrict__ tp,
+                                                    const float *__restrict__ noise, int X,
+                                                    int Y, float res_x, float res_y,
+                                                    float *__restrict__ out,
+                                                    long long out_bstride) {
+  const int b = blockIdx.x;
+  // x_pixel = int(h/2 + x/res), + int(rand*10 - 5)            (parking_model.py:33-37)
+  const float fx = __fadd_rn((float)X * 0.5f, __fdiv_rn(tp[3 * b + 0], res_x));
+  const float fy = __fadd_rn((float)Y * 0.5f, __fdiv_rn(tp[3 * b + 1], res_y));
+  const int nx = (int)truncf(__fsub_rn(__fmul_rn(noise[2 * b + 0], 10.f), 5.f));
+  const int ny = (int)truncf(__fsub_rn(__fmul_rn(noise[2 * b + 1], 10.f), 5.f));
+  const int px = (int)truncf(fx) + nx, py = (int)truncf(fy) + ny;
+  int xlo, xhi, ylo, yhi;
+  py_slice(px - 4, px + 4, X, xlo, xhi);
+  py_slice(py - 4, py + 4, Y, ylo, yhi);
+  float *o = out + (long long)b * out_bstride;
+  for (int i = threadIdx.x; i < X * Y; i += blockDim.x) {
+    const int x = i / Y, y = i - x * Y;
+    o[i] = (x >= xlo && x < xhi && y >= ylo && y < yhi) ? 1.f : 0.f;
+  }
+}
+
+}  // namespace e2ep
+
+using namespace e2ep;
+
+extern "C" {
+
+int e2ep_geom_index(const float *frustum, const float *combine, const float *trans,
+                    const float *lo, const float *res, int X, int Y, int Z, int B, int N, int D,
+                    int h, int w, int32_t *pillar, void *stream) {
+  E2EP_REQUIRE(B > 0 && N > 0 && D > 0 && h > 0 && w > 0 && X > 0 && Y > 0 && Z > 0, E2EP_EINVAL,
+               "e2ep_geom_index: non-positive shape");
+  E2EP_REQUIRE(lo && res, E2EP_EINVAL, "e2ep_geom_index: lo/res must be host arrays of 3");
+  const long long total = (long long)B * N * D * h * w;
+  hipLaunchKernelGGL(k_geom_index, dim3(cdiv(total, 256)), dim3(256), 0, as_stream(stream),
+                     frustum, combine, trans, lo[0], lo[1], lo[2], res[0], res[1], res[2], X, Y, Z,
+                     D * h * w, total, pillar);
+  return launch_status("e2ep_geom_index");
+}
+
+size_t e2ep_lss_plan_workspace(int B, int XYZ) { return (size_t)B * XYZ * sizeof(int); }
+
+int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int XYZ,
+                  int32_t *offsets, int32_t *order, void *workspace, void *stream) {
+  E2EP_REQUIRE(B > 0 && XYZ > 0, E2EP_EINVAL, "e2ep_lss_plan: bad shape");
+  E2EP_REQUIRE(N < 128 && D < 256 && h * w < 65536, E2EP_ERANGE,
+               "e2ep_lss_plan: packed point code needs N<128, D<256, h*w<65536 (got %d,%d,%d)", N,
+               D, h * w);
+  hipStream_t s = as_stream(stream);
+  int *cnt = static_cast<int *>(workspace);
+  const int P = N * D * h * w;
+  const long long total = (long long)B * P;
+  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)B * XYZ * sizeof(int), s);
+  if (e != hipSuccess) {
+    set_error("e2ep_lss_plan: memset: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  hipLaunchKernelGGL(k_count, dim3(cdiv(total, 256)), dim3(256), 0, s, pillar, P, XYZ, total, cnt);
+  // scan writes offsets and re-uses the count buffer as the fill cursor
+  hipLaunchKernelGGL(k_scan, dim3(B), dim3(1024), 0, s, cnt, XYZ, offsets, cnt);
+  hipLaunchKernelGGL(k_fill, dim3(cdiv(total, 256)), dim3(256), 0, s, pillar, P, D * h * w, h * w,
+                     XYZ, total, cnt, order);
+  hipLaunchKernelGGL(k_segsort, dim3(cdiv((long long)B * XYZ, 256)), dim3(256), 0, s, offsets, P,
+                     XYZ, B, order);
+  return launch_status("e2ep_lss_plan");
+}
+
+int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
+                 const int32_t *order, int B, int N, int D, int hw, int C, int XYZ, float *bev,
+                 long long bev_bstride, void *stream) {
+  E2EP_REQUIRE(B > 0 && N > 0 && D > 0 && hw > 0 && C > 0 && XYZ > 0, E2EP_EINVAL,
+               "e2ep_lss_fwd: bad shape");
+  E2EP_REQUIRE(((uintptr_t)featT & 15) == 0, E2EP_EINVAL, "e2ep_lss_fwd: featT must be 16-B aligned");
+  dim3 grid(cdiv(XYZ, 64), B, cdiv(C, 64));
+  hipLaunchKernelGGL(k_lss_fwd, grid, dim3(256), 0, as_stream(stream), prob, featT, offsets, order,
+                     N, D, hw, C, XYZ, N * D * hw, bev, bev_bstride);
+  return launch_status("e2ep_lss_fwd");
+}
+
+int e2ep_lss_bwd(const float *gT, const float *prob, const float *featT, const int32_t *pillar,
+                 int B, int N, int D, int hw, int C, int XYZ, float *grad_prob, float *grad_feat,
+                 void *stream) {
+  E2EP_REQUIRE(B > 0 && N > 0 && D > 0 && hw > 0 && C > 0 && XYZ > 0, E2EP_EINVAL,
+               "e2ep_lss_bwd: bad shape");
+  E2EP_REQUIRE(C <= 64 && D <= 64, E2EP_ERANGE, "e2ep_lss_bwd: needs C<=64, D<=64 (got %d,%d)", C, D);
+  dim3 grid(cdiv(hw, BWD_PIX), B * N);
+  hipLaunchKernelGGL(k_lss_bwd, grid, dim3(256), 0, as_stream(stream), gT, prob, featT, pillar, N, D,
+                     hw, C, XYZ, grad_prob, grad_feat);
+  return launch_status("e2ep_lss_bwd");
+}
+
+int e2ep_transpose(const float *in, long long in_bstride, int batch, int rows, int cols, float *out,
+                   void *stream) {
+  E2EP_REQUIRE(batch > 0 && rows > 0 && cols > 0 && batch < 65536, E2EP_EINVAL,
+               "e2ep_transpose: bad shape");
+  dim3 grid(cdiv(cols, 64), cdiv(rows, 64), batch);
+  hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, as_stream(stream), in, in_bstride, rows, cols,
+                     out);
+  return launch_status("e2ep_transpose");
+}
+
+int e2ep_target_bev(const float *target_point, const float *noise, int B, int X, int Y, float res_x,
+                    float res_y, float *out, long long out_bstride, void *stream) {
+  E2EP_REQUIRE(B > 0 && X > 0 && Y > 0, E2EP_EINVAL, "e2ep_target_bev: bad shape");
+  hipLaunchKernelGGL(k_target_bev, dim3(B), dim3(256), 0, as_stream(stream), target_point, noise, X,
+                     Y, res_x, res_y, out, out_bstride);
+  return launch_status("e2ep_target_bev");
+}
+
+}  // extern "C"

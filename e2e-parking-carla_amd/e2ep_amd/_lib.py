@@ -1,0 +1,76 @@
+"""ctypes binding of libe2ep_hip.so (C ABI: include/e2ep.h).
+
+The library is built in-tree by csrc/Makefile (or __graft_entry__.build()).  There is no
+fallback: if it is missing or fails to load, every op raises — the product path never
+silently degrades to PyTorch or CPU code.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads torch's libamdhip64 first, so the library binds to it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("E2EP_LIB", os.path.join(_HERE, "libe2ep_hip.so"))
+
+_p, _i, _i64, _f, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
+_fp3 = ctypes.POINTER(ctypes.c_float)
+
+# name -> (restype, argtypes); must match include/e2ep.h
+SIGNATURES = {
+    "e2ep_abi_version": (_i, []),
+    "e2ep_last_error": (ctypes.c_char_p, []),
+    "e2ep_geom_index": (_i, [_p, _p, _p, _fp3, _fp3, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
+    "e2ep_lss_plan_workspace": (_sz, [_i, _i]),
+    "e2ep_lss_plan": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
+    "e2ep_lss_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i64, _p]),
+    "e2ep_lss_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
+    "e2ep_transpose": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
+    "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
+}
+
+_LIB = None
+_ERR = None
+
+
+class E2EPError(RuntimeError):
+    pass
+
+
+def load():
+    """Load and bind the library once; raise E2EPError if it is not there."""
+    global _LIB, _ERR
+    if _LIB is not None:
+        return _LIB
+    if _ERR is not None:
+        raise _ERR
+    try:
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+    except (OSError, AttributeError) as e:
+        _ERR = E2EPError(f"libe2ep_hip.so unavailable ({LIB_PATH}): {e}. Build it with "
+                         f"`make -C e2e-parking-carla_amd/csrc` or __graft_entry__.build().")
+        raise _ERR
+    _LIB = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise E2EPError(f"{name} failed ({rc}): {lib.e2ep_last_error().decode()}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def host3(vals):
+    return (ctypes.c_float * 3)(*[float(v) for v in vals])

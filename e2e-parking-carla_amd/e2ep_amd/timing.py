@@ -1,0 +1,46 @@
+"""HIP-event timing of individual kernel launches, on the stream each kernel runs on.
+
+bench.py enables it over its timed region to measure the dominant kernel's average launch
+duration live (the `roofline.achieved` figure); it is off by default and then costs one
+boolean test per launch."""
+from collections import defaultdict
+from contextlib import contextmanager
+
+import torch
+
+_enabled = False
+_events = defaultdict(list)
+
+
+def enable(flag=True):
+    global _enabled
+    _enabled = flag
+
+
+def reset():
+    _events.clear()
+
+
+@contextmanager
+def region(name):
+    if not _enabled:
+        yield
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()  # records on torch's current stream == the stream the kernel is enqueued on
+    try:
+        yield
+    finally:
+        e.record()
+        _events[name].append((s, e))
+
+
+def summary():
+    """{name: (launches, mean_ms, total_ms)} — synchronises."""
+    torch.cuda.synchronize()
+    out = {}
+    for k, evs in _events.items():
+        t = [s.elapsed_time(e) for s, e in evs]
+        out[k] = (len(t), sum(t) / max(1, len(t)), sum(t))
+    return out

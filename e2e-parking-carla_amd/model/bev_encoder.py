@@ -1,0 +1,69 @@
+"""BEV encoder: bilinear 200->256, conv7x7/2 65->64, BN, ReLU, maxpool, ResNet-18 layer1-3.
+
+Mirrors reference model/bev_encoder.py:8-36 with torchvision-0.14.1 key names
+(conv1, bn1, layer1..layer4; BasicBlock conv1/bn1/conv2/bn2/downsample.{0,1}).  layer4 is
+constructed (its weights are part of the checkpoint contract) but, as in the reference,
+never run, so it receives no gradient and is excluded from the gradient all-reduce."""
+import torch
+from torch import nn
+
+from e2ep_amd import ops
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
+                                            nn.BatchNorm2d(cout))
+        self.stride = stride
+
+    def forward(self, x):
+        y = ops.bn_act(ops.conv2d(x, self.conv1.weight, None, self.stride, 1), self.bn1, "relu")
+        y = ops.bn_act(ops.conv2d(y, self.conv2.weight, None, 1, 1), self.bn2, None)
+        if self.downsample is not None:
+            x = ops.bn_act(ops.conv2d(x, self.downsample[0].weight, None, self.stride, 0),
+                           self.downsample[1], None)
+        return torch.relu(y + x)
+
+
+def _layer(cin, cout, stride):
+    return nn.Sequential(BasicBlock(cin, cout, stride), BasicBlock(cout, cout, 1))
+
+
+class BevEncoder(nn.Module):
+    def __init__(self, in_channel):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_channel + 1, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.max_pool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = _layer(64, 64, 1)
+        self.layer2 = _layer(64, 128, 2)
+        self.layer3 = _layer(128, 256, 2)
+        self.layer4 = _layer(256, 512, 2)
+        for m in self.modules():  # torchvision init, zero_init_residual=True
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        for m in self.modules():
+            if isinstance(m, BasicBlock):
+                nn.init.zeros_(m.bn2.weight)
+        self.conv1.reset_parameters()  # the reference's own conv1 keeps PyTorch's default init
+
+    def forward(self, x):
+        x = ops.resize(x, (256, 256))
+        x = ops.bn_act(ops.conv2d(x, self.conv1.weight, None, 2, 3), self.bn1, "relu")
+        x = ops.max_pool3s2(x)
+        x = self.layer3(self.layer2(self.layer1(x)))
+        return torch.flatten(x, 2)

@@ -1,0 +1,54 @@
+"""Control-token decoder: embedding + 4-layer transformer decoder + vocabulary projection.
+
+Mirrors reference model/control_predict.py:8-75 (keys: embedding, pos_embed, tf_decoder.*,
+output).  `forward` is the teacher-forced training path, `predict` one autoregressive step
+(pads to tf_de_tgt_dim-1 tokens and reads the logits at the last real position)."""
+import torch
+from torch import nn
+
+from e2ep_amd import transformer
+
+
+class ControlPredict(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        self.pad_idx = cfg.token_nums - 1
+        det = getattr(cfg, "deterministic", False)
+        self.embedding = nn.Embedding(cfg.token_nums, cfg.tf_de_dim)
+        self.pos_drop = nn.Dropout(0.0 if det else cfg.tf_de_dropout)
+        self.pos_embed = nn.Parameter(torch.randn(1, cfg.tf_de_tgt_dim - 1, cfg.tf_de_dim) * .02)
+        layer = nn.TransformerDecoderLayer(d_model=cfg.tf_de_dim, nhead=cfg.tf_de_heads,
+                                           dropout=0.0 if det else 0.1)
+        self.tf_decoder = nn.TransformerDecoder(layer, num_layers=cfg.tf_de_layers)
+        self.output = nn.Linear(cfg.tf_de_dim, cfg.token_nums)
+        for name, p in self.named_parameters():
+            if "pos_embed" not in name and p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+        nn.init.trunc_normal_(self.pos_embed, std=.02)
+
+    def create_mask(self, tgt):
+        """Causal float mask (0 on/below the diagonal, -inf above) + PAD key mask."""
+        L = tgt.shape[1]
+        causal = torch.full((L, L), float("-inf"), device=tgt.device).triu(1)
+        return causal, tgt == self.pad_idx
+
+    def decoder(self, encoder_out, tgt_embedding, tgt_mask, tgt_padding_mask):
+        return transformer.decoder(self.tf_decoder, tgt_embedding, encoder_out, tgt_mask,
+                                   tgt_padding_mask)
+
+    def forward(self, encoder_out, tgt):
+        tgt = tgt[:, :-1]
+        mask, pad = self.create_mask(tgt)
+        emb = self.pos_drop(self.embedding(tgt) + self.pos_embed)
+        return self.output(self.decoder(encoder_out, emb, mask, pad))
+
+    def predict(self, encoder_out, tgt):
+        length = tgt.size(1)
+        pad = torch.full((tgt.size(0), self.cfg.tf_de_tgt_dim - length - 1), self.pad_idx,
+                         dtype=torch.long, device=tgt.device)
+        tgt = torch.cat([tgt, pad], dim=1)
+        mask, padm = self.create_mask(tgt)
+        emb = self.embedding(tgt) + self.pos_embed
+        logits = self.output(self.decoder(encoder_out, emb, mask, padm))[:, length - 1, :]
+        return torch.softmax(logits, dim=-1).argmax(dim=-1).view(-1, 1)

@@ -1,0 +1,74 @@
+"""Camera-head conv blocks with the reference's module/key layout
+(reference model/convolutions.py:183-282: UpsamplingConcat, ASPPConv, ASPPPooling, ASPP,
+DeepLabHead — the only reachable classes of that file).  Forwards run on e2ep_amd ops."""
+import torch
+from torch import nn
+
+from e2ep_amd import ops
+
+
+def _conv_bn(cin, cout, k, pad=0, dil=1):
+    return [nn.Conv2d(cin, cout, k, padding=pad, dilation=dil, bias=False), nn.BatchNorm2d(cout),
+            nn.ReLU()]
+
+
+def _run_conv_bn_relu(seq, x):
+    conv, bn = seq[0], seq[1]
+    return ops.bn_act(ops.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation),
+                      bn, "relu")
+
+
+class ASPPConv(nn.Sequential):
+    def __init__(self, cin, cout, dilation):
+        super().__init__(*_conv_bn(cin, cout, 3, dilation, dilation))
+
+    def forward(self, x):
+        return _run_conv_bn_relu(self, x)
+
+
+class ASPPPooling(nn.Sequential):
+    def __init__(self, cin, cout):
+        super().__init__(nn.AdaptiveAvgPool2d(1), *_conv_bn(cin, cout, 1))
+
+    def forward(self, x):
+        g = _run_conv_bn_relu(self[1:], x.mean((2, 3), keepdim=True))
+        return ops.resize(g, x.shape[-2:])
+
+
+class ASPP(nn.Module):
+    def __init__(self, cin, rates, cout=256, p_drop=0.5):
+        super().__init__()
+        mods = [nn.Sequential(*_conv_bn(cin, cout, 1))]
+        mods += [ASPPConv(cin, cout, r) for r in rates]
+        mods.append(ASPPPooling(cin, cout))
+        self.convs = nn.ModuleList(mods)
+        self.project = nn.Sequential(*_conv_bn(len(mods) * cout, cout, 1), nn.Dropout(p_drop))
+
+    def forward(self, x):
+        branches = [_run_conv_bn_relu(self.convs[0], x)] + [m(x) for m in self.convs[1:]]
+        y = _run_conv_bn_relu(self.project, torch.cat(branches, 1))
+        return self.project[3](y)
+
+
+class DeepLabHead(nn.Sequential):
+    def __init__(self, cin, cout, hidden_channel=256, p_drop=0.5):
+        super().__init__(ASPP(cin, (12, 24, 36), hidden_channel, p_drop),
+                         nn.Conv2d(hidden_channel, hidden_channel, 3, padding=1, bias=False),
+                         nn.BatchNorm2d(hidden_channel), nn.ReLU(), nn.Conv2d(hidden_channel, cout, 1))
+
+    def forward(self, x):
+        y = self[0](x)
+        y = ops.bn_act(ops.conv2d(y, self[1].weight, None, 1, 1), self[2], "relu")
+        return ops.conv2d(y, self[4].weight, self[4].bias)
+
+
+class UpsamplingConcat(nn.Module):
+    def __init__(self, cin, cout, scale_factor=2):
+        super().__init__()
+        self.upsample = nn.Upsample(scale_factor=scale_factor, mode="bilinear", align_corners=False)
+        self.conv = nn.Sequential(*_conv_bn(cin, cout, 3, 1), *_conv_bn(cout, cout, 3, 1))
+
+    def forward(self, x_to_upsample, x):
+        y = torch.cat([x, ops.upsample2x(x_to_upsample)], 1)
+        y = _run_conv_bn_relu(self.conv[0:3], y)
+        return _run_conv_bn_relu(self.conv[3:6], y)

@@ -1,0 +1,38 @@
+"""Target/ego fusion: motion MLP + BEV tokens + positional embedding -> 4-layer transformer.
+
+Mirrors reference model/feature_fusion.py:8-51 (keys: tf_encoder.layers.i.*, pos_embed,
+motion_encoder.{0,2,4}).  The encoder layers stay `nn.TransformerEncoderLayer` modules so
+the closed-loop agent's attention hook (agent/parking_agent.py:71-80,266-268) keeps working;
+their arithmetic runs through e2ep_amd.transformer."""
+import torch
+from torch import nn
+
+from e2ep_amd import transformer
+
+
+class FeatureFusion(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        det = getattr(cfg, "deterministic", False)
+        layer = nn.TransformerEncoderLayer(d_model=cfg.tf_en_dim, nhead=cfg.tf_en_heads,
+                                           dropout=0.0 if det else 0.1)
+        self.tf_encoder = nn.TransformerEncoder(layer, num_layers=cfg.tf_en_layers,
+                                                enable_nested_tensor=False)
+        self.pos_embed = nn.Parameter(torch.randn(1, cfg.tf_en_bev_length, cfg.tf_en_dim) * .02)
+        self.pos_drop = nn.Dropout(0.0 if det else cfg.tf_en_dropout)
+        u = cfg.tf_en_bev_length // 4
+        self.motion_encoder = nn.Sequential(
+            nn.Linear(cfg.tf_en_motion_length, u), nn.ReLU(inplace=True),
+            nn.Linear(u, 2 * u), nn.ReLU(inplace=True),
+            nn.Linear(2 * u, cfg.tf_en_bev_length), nn.ReLU(inplace=True))
+        for name, p in self.named_parameters():
+            if "pos_embed" not in name and p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+        nn.init.trunc_normal_(self.pos_embed, std=.02)
+
+    def forward(self, bev_feature, ego_motion):
+        motion = self.motion_encoder(ego_motion).transpose(1, 2).expand(-1, -1, 2)
+        tokens = torch.cat([bev_feature.transpose(1, 2), motion], dim=2)
+        tokens = self.pos_drop(tokens + self.pos_embed)
+        return transformer.encoder(self.tf_encoder, tokens)

@@ -1,0 +1,75 @@
+"""ParkingModel — MI355X-native drop-in for reference model/parking_model.py:12-78.
+
+Same constructor (`ParkingModel(cfg)`), submodules (bev_model, bev_encoder, feature_fusion,
+control_predict, segmentation_head), state-dict keys (861) and methods (forward, predict,
+encoder, add_target_bev).  Differences are internal: the lift-splat pooling writes straight
+into a 65-channel BEV buffer whose last plane the target-point kernel fills, so the
+reference's torch.cat of the target channel (:45) and its per-sample Python loop (:39-43)
+disappear.  `noise` (optional, (B,2) in [0,1)) replaces the torch.rand_like draw (:36) for
+reproducible runs; by default it is drawn on the device exactly like the reference."""
+import torch
+from torch import nn
+
+from e2ep_amd import lss
+from model.bev_encoder import BevEncoder
+from model.bev_model import BevModel
+from model.control_predict import ControlPredict
+from model.feature_fusion import FeatureFusion
+from model.segmentation_head import SegmentationHead
+
+
+class ParkingModel(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.cfg = cfg
+        self.bev_model = BevModel(self.cfg)
+        self.bev_encoder = BevEncoder(self.cfg.bev_encoder_in_channel)
+        self.feature_fusion = FeatureFusion(self.cfg)
+        self.control_predict = ControlPredict(self.cfg)
+        self.segmentation_head = SegmentationHead(self.cfg)
+
+    def _noise(self, b, device, noise):
+        if noise is None:
+            return torch.rand((b, 2), dtype=torch.float, device=device)
+        return noise
+
+    def add_target_bev(self, bev_feature, target_point, noise=None):
+        """Append the target-point channel to a (B,C,X,Y) BEV tensor (reference API)."""
+        b, c, h, w = bev_feature.shape
+        out = torch.empty((b, c + 1, h, w), dtype=bev_feature.dtype, device=bev_feature.device)
+        out[:, :c] = bev_feature
+        lss.target_bev(out, c, target_point, self._noise(b, out.device, noise),
+                       self.cfg.bev_x_bound[2], self.cfg.bev_y_bound[2])
+        return out, out[:, c:].detach().clone()
+
+    def encoder(self, data, noise=None):
+        dev = self.bev_model.frustum.device
+        images = data["image"].to(dev, non_blocking=True)
+        target_point = data["target_point"].to(dev, non_blocking=True)
+        ego_motion = data["ego_motion"].to(dev, non_blocking=True)
+        b = images.shape[0]
+        # lift-splat into channels [0,64); target plane into channel 64 (fused concat)
+        bev, pred_depth = self.bev_model.calc_bev_feature(images, data["intrinsics"],
+                                                          data["extrinsics"], extra_channels=1)
+        c = bev.shape[1] - 1
+        lss.target_bev(bev, c, target_point, self._noise(b, dev, noise),
+                       self.cfg.bev_x_bound[2], self.cfg.bev_y_bound[2])
+        bev_target = bev[:, c:].detach()
+        bev_down_sample = self.bev_encoder(bev)
+        fuse_feature = self.feature_fusion(bev_down_sample, ego_motion)
+        pred_segmentation = self.segmentation_head(fuse_feature)
+        return fuse_feature, pred_segmentation, pred_depth, bev_target
+
+    def forward(self, data, noise=None):
+        fuse_feature, pred_segmentation, pred_depth, _ = self.encoder(data, noise)
+        gt = data["gt_control"].to(fuse_feature.device, non_blocking=True)
+        pred_control = self.control_predict(fuse_feature, gt)
+        return pred_control, pred_segmentation, pred_depth
+
+    def predict(self, data, noise=None):
+        fuse_feature, pred_segmentation, pred_depth, bev_target = self.encoder(data, noise)
+        toks = data["gt_control"].to(fuse_feature.device, non_blocking=True)
+        for _ in range(3):
+            nxt = self.control_predict.predict(fuse_feature, toks)
+            toks = torch.cat([toks, nxt], dim=1)
+        return toks, pred_segmentation, pred_depth, bev_target

@@ -1,0 +1,105 @@
+/*
+ * e2ep.h — C ABI of libe2ep_hip.so, the MI355X (gfx950) kernels behind the ParkingModel
+ * hot path of qintonguav/e2e-parking-carla.
+ *
+ * Conventions (every entry point):
+ *   - all array pointers are DEVICE pointers owned by the caller; nothing is allocated inside;
+ *   - work is enqueued on the caller's hipStream_t (passed as void*), so every call can be
+ *     captured into a hipGraph; no host synchronisation happens inside;
+ *   - the return value is 0 on success, otherwise a hipError_t (>0) or an E2EP_E* code (<0);
+ *     e2ep_last_error() returns a thread-local message for the last failure;
+ *   - tensors are dense row-major fp32 unless stated; "stride" arguments are in elements.
+ *
+ * The reference is pure PyTorch (no native code), so each entry point
+ * replaces a PyTorch op chain; the citation names the reference code it stands in for.
+ */
+#ifndef E2EP_H
+#define E2EP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define E2EP_EINVAL (-1) /* bad shape / argument */
+#define E2EP_ERANGE (-2) /* shape outside what the kernel supports */
+
+int e2ep_abi_version(void);
+const char *e2ep_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Lift-splat
+ * ------------------------------------------------------------------------------------- */
+
+/* Ego-frame geometry + integer pillar index of every frustum point.
+ * Replaces BevModel.get_geometry (model/bev_model.py:45-57) and the voxelisation / mask /
+ * rank of proj_bev_feature (model/bev_model.py:85-95).
+ *   frustum [D,h,w,3]  (the module's `frustum` parameter; u, v, depth)
+ *   combine [B*N,3,3] = R(E^-1) K^-1,  trans [B*N,3] = t(E^-1)   (computed as the reference does)
+ *   lo[3] = bev_start_pos - bev_res/2,  res[3] = bev_res  (HOST arrays, read at call time),
+ *   X,Y,Z = bev_dim
+ *   out pillar [B*N*D*h*w] int32: x*Y*Z + y*Z + z, or -1 where the point is masked.
+ * Bit-exact with the reference's fp32 CPU path: sequential non-fused multiply/add, IEEE
+ * division, truncation toward zero (Tensor.long()). */
+int e2ep_geom_index(const float *frustum, const float *combine, const float *trans,
+                    const float *lo, const float *res, int X, int Y, int Z,
+                    int B, int N, int D, int h, int w, int32_t *pillar, void *stream);
+
+/* Bytes of int32 workspace e2ep_lss_plan needs: B*X*Y*Z*4. */
+size_t e2ep_lss_plan_workspace(int B, int XYZ);
+
+/* Counting sort of kept points by pillar (replaces the mask / argsort / cumsum-boundary
+ * bookkeeping of model/bev_model.py:86-99 and tool/geometry.py:292-300).
+ *   pillar [B*P] (P = N*D*h*w) from e2ep_geom_index
+ *   offsets [B*(XYZ+1)]: points of pillar q of sample b are order[b*P + offsets[b*(XYZ+1)+q] ..
+ *                        offsets[b*(XYZ+1)+q+1])
+ *   order   [B*P] packed point codes (n<<24 | d<<16 | h*w index), ascending within a pillar,
+ *           so every later sum has a fixed, run-to-run identical order.
+ * Limits: N < 128, D < 256, h*w < 65536. */
+int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int XYZ,
+                  int32_t *offsets, int32_t *order, void *workspace, void *stream);
+
+/* Fused depth-distribution x feature outer product + pillar sum-pooling, forward.
+ * Replaces encoder_forward's outer product/permute (model/bev_model.py:64-71) and
+ * proj_bev_feature's gather / VoxelsSumming / scatter (model/bev_model.py:74-107,
+ * tool/geometry.py:289-305).  The (B,N,D,h,w,C) outer product is never materialised.
+ *   prob  [B*N, D, h*w]   softmax depth distribution
+ *   featT [B*N, h*w, C]   camera features, pixel-major (see e2ep_transpose)
+ *   bev   out: bev[b*bev_bstride + c*XYZ + q] for c < C, every q written (zeros included).
+ */
+int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
+                 const int32_t *order, int B, int N, int D, int hw, int C, int XYZ,
+                 float *bev, long long bev_bstride, void *stream);
+
+/* Backward of e2ep_lss_fwd (replaces VoxelsSumming.backward, tool/geometry.py:307-317, and
+ * the autograd of the outer product).  Gather formulation, no atomics, deterministic:
+ *   grad_prob[p] = sum_c gT[q(p), c] * feat[pix(p), c]
+ *   grad_feat[pix, c] = sum_d gT[q(pix,d), c] * prob[pix, d]
+ *   gT    [B, XYZ, C]   grad of bev, pillar-major (see e2ep_transpose)
+ *   featT [B*N, h*w, C]
+ *   pillar [B*N*D*h*w] from e2ep_geom_index
+ *   out grad_prob [B*N, D, h*w], grad_feat [B*N, C, h*w]
+ * Limits: C <= 64, D <= 64. */
+int e2ep_lss_bwd(const float *gT, const float *prob, const float *featT, const int32_t *pillar,
+                 int B, int N, int D, int hw, int C, int XYZ, float *grad_prob,
+                 float *grad_feat, void *stream);
+
+/* Batched 2-D transpose: out[b][c][r] = in[b*in_bstride + r*cols + c], r < rows, c < cols;
+ * out batch stride rows*cols.  Used to produce featT / gT above. */
+int e2ep_transpose(const float *in, long long in_bstride, int batch, int rows, int cols,
+                   float *out, void *stream);
+
+/* Target-point channel (replaces ParkingModel.add_target_bev, model/parking_model.py:28-46).
+ *   target_point [B,3] (x m, y m, yaw);  noise [B,2] uniform [0,1) (the rand_like draw)
+ *   px = int(X/2 + x/res_x) + int(noise0*10-5), py likewise; out plane [X,Y] of sample b at
+ *   out + b*out_bstride is zeroed and the 8x8 square [px-4,px+4) x [py-4,py+4) set to 1 with
+ *   Python slice semantics (negative bounds wrap, then clamp). */
+int e2ep_target_bev(const float *target_point, const float *noise, int B, int X, int Y,
+                    float res_x, float res_y, float *out, long long out_bstride, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* E2EP_H */

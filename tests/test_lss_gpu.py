@@ -1,0 +1,148 @@
+"""Lift-splat HIP kernels vs the oracle / golden vectors (MI355X)."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import golden, max_scaled, meta, rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _plan_from_golden(g, B=1, lo=None, res=None):
+    from e2ep_amd import lss
+    g4 = golden("geometry_4cam_256.npz")
+    comb = torch.from_numpy(g["combine"])[None].expand(B, -1, -1, -1).contiguous()
+    trans = torch.from_numpy(g["trans"])[None].expand(B, -1, -1).contiguous()
+    return lss.build_plan(torch.from_numpy(g["frustum"]), comb, trans, g4["lo"].tolist(),
+                          g4["res"].tolist(), g4["dim"].tolist(), DEV)
+
+
+def test_pillar_index_bit_exact_4cam():
+    g = golden("geometry_4cam_256.npz")
+    plan = _plan_from_golden(g)
+    got = plan.pillar.view(g["pillar"].shape).cpu().numpy()
+    assert np.array_equal(got, g["pillar"])
+
+
+def test_pillar_index_bit_exact_hires_6cam():
+    g = golden("geometry_6cam_512.npz")
+    plan = _plan_from_golden(g)
+    got = plan.pillar.cpu().numpy().astype(np.int32)
+    assert hashlib.sha256(got.tobytes()).hexdigest() == meta()["geometry_6cam_512"]["pillar_sha256"]
+
+
+def test_rig_transforms_match_reference_bits():
+    from e2ep_amd import lss, synthetic
+    g = golden("geometry_4cam_256.npz")
+    K, E = synthetic.rig()
+    comb, trans = lss.rig_transforms(K[None].to(DEV), E[None].to(DEV))
+    assert np.array_equal(comb[0].numpy(), g["combine"]) and np.array_equal(trans[0].numpy(), g["trans"])
+
+
+def test_plan_invariants_batch_of_different_rigs():
+    """Counting sort: per-pillar counts, ascending codes within a pillar, every kept point once."""
+    from e2ep_amd import lss, synthetic
+    g4 = golden("geometry_4cam_256.npz")
+    K, E = synthetic.rig()
+    E2 = E.clone()
+    E2[:, :3, 3] += torch.tensor([0.13, -0.07, 0.02])  # second sample: shifted rig
+    comb, trans = lss.rig_transforms(torch.stack([K, K]), torch.stack([E, E2]))
+    plan = lss.build_plan(torch.from_numpy(g4["frustum"]), comb, trans, g4["lo"].tolist(),
+                          g4["res"].tolist(), [200, 200, 1], DEV)
+    pil = plan.pillar.view(2, -1).cpu().numpy()
+    off = plan.offsets.view(2, -1).cpu().numpy()
+    order = plan.order.view(2, -1).cpu().numpy()
+    P = pil.shape[1]
+    for b in range(2):
+        kept = pil[b][pil[b] >= 0]
+        cnt = np.bincount(kept, minlength=40000)
+        assert np.array_equal(np.diff(off[b]), cnt)
+        codes = order[b][: off[b][-1]]
+        n, d, pix = codes >> 24, (codes >> 16) & 255, codes & 65535
+        flat = n * (48 * 1024) + d * 1024 + pix
+        assert np.array_equal(np.sort(flat), np.nonzero(pil[b] >= 0)[0])
+        assert np.array_equal(pil[b][flat], np.repeat(np.arange(40000), cnt))
+        for q in np.nonzero(cnt > 1)[0][:2000]:
+            seg = codes[off[b][q]:off[b][q + 1]]
+            assert np.all(np.diff(seg) > 0)
+    assert not np.array_equal(pil[0], pil[1])
+
+
+def _lss_inputs(m):
+    B, N, D, h, w, C = m["shape"]
+    gl = torch.Generator().manual_seed(m["seed"])
+    logits = torch.randn(B * N, D, h, w, generator=gl) * m["logit_scale"]
+    feat = torch.randn(B * N, C, h, w, generator=gl)
+    gout = torch.randn(B, C, 200, 200, generator=gl)
+    return logits.softmax(1), feat, gout
+
+
+def test_lss_fwd_bwd_matches_reference_golden():
+    """Reference VoxelsSumming path (golden) vs fused HIP kernel at C=4.  Tolerances follow
+    SURVEY.md §8c: the reference's own cumsum trick carries ~1e-6 abs noise."""
+    from e2ep_amd import lss
+    g = golden("geometry_4cam_256.npz")
+    ref = golden("lss_c4.npz")
+    prob, feat, gout = _lss_inputs(meta()["lss_c4"])
+    plan = _plan_from_golden(g)
+    p = prob.to(DEV).requires_grad_(True)
+    f = feat.to(DEV).requires_grad_(True)
+    bev = lss.lift_splat(p, f, plan)
+    bev.backward(gout.to(DEV))
+    assert max_scaled(bev, ref["bev"]) < 1e-4 and rel_l2(bev, ref["bev"]) < 1e-4
+    assert rel_l2(p.grad, ref["grad_prob"]) < 1e-5
+    assert rel_l2(f.grad, ref["grad_feat"]) < 1e-5
+
+
+def test_lss_full_channels_vs_oracle_and_determinism():
+    """C=64 (product width), B=2: HIP vs the oracle's reference-order splat; bitwise repeatable."""
+    from e2ep_amd import lss
+    from oracle import parking_ref as O
+    g = golden("geometry_4cam_256.npz")
+    B, N, D, h, w, C = 2, 4, 48, 32, 32, 64
+    gl = torch.Generator().manual_seed(11)
+    prob = (torch.randn(B * N, D, h, w, generator=gl) * 3).softmax(1)
+    feat = torch.randn(B * N, C, h, w, generator=gl)
+    gout = torch.randn(B, C + 1, 200, 200, generator=gl)
+    plan = _plan_from_golden(g, B)
+    outs = []
+    for _ in range(2):
+        p = prob.to(DEV).requires_grad_(True)
+        f = feat.to(DEV).requires_grad_(True)
+        bev = lss.lift_splat(p, f, plan, C + 1)
+        bev[:, C].zero_()
+        bev.backward(gout.to(DEV))
+        outs.append((bev[:, :C].detach().cpu(), p.grad.cpu(), f.grad.cpu()))
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1])), "not run-to-run deterministic"
+    po = prob.clone().requires_grad_(True)
+    fo = feat.clone().requires_grad_(True)
+    outer = (po.unsqueeze(1) * fo.unsqueeze(2)).view(B, N, C, D, h, w).permute(0, 1, 3, 4, 5, 2)
+    xyz = torch.from_numpy(g["xyz"])[None].expand(B, -1, -1, -1, -1, -1)
+    res = torch.from_numpy(g["res"])
+    ref = O.splat(xyz, outer, res, torch.from_numpy(g["lo"]) + res / 2.0, torch.from_numpy(g["dim"]))
+    ref.backward(gout[:, :C])
+    bev, gp, gf = outs[0]
+    assert max_scaled(bev, ref) < 1e-4 and rel_l2(bev, ref) < 1e-5
+    assert rel_l2(gp, po.grad) < 1e-5 and rel_l2(gf, fo.grad) < 1e-5
+    # cells with no points are exactly zero, as in the reference
+    assert torch.equal(bev[ref == 0], torch.zeros_like(bev[ref == 0]))
+
+
+@pytest.mark.parametrize("xy", [(1.23, -2.71), (9.8, 9.9), (-9.97, -9.6), (-12.0, 3.0), (15.0, -15.0),
+                                (0.0, 0.0), (-10.4, -10.45), (-11.0, 5.0)])
+def test_target_bev_matches_reference_semantics(xy):
+    from e2ep_amd import lss
+    from oracle import parking_ref as O
+    B = 3
+    tp = torch.tensor([[xy[0], xy[1], 30.0]] * B)
+    noise = torch.tensor([[0.0, 0.999], [0.5, 0.05], [0.93, 0.41]])
+    m = O.ParkingModelRef.__new__(O.ParkingModelRef)
+    m.cfg = O.Cfg
+    _, ref = O.ParkingModelRef.add_target_bev(m, torch.zeros(B, 2, 200, 200), tp, noise)
+    out = torch.full((B, 3, 200, 200), 7.0, device=DEV)
+    lss.target_bev(out, 2, tp, noise, 0.1, 0.1)
+    assert torch.equal(out[:, 2:].cpu(), ref)
+    assert (out[:, :2] == 7.0).all()
