@@ -312,6 +312,61 @@ __global__ void __launch_bounds__(256) k_target_bev(const float *__restrict__ tp
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// rig algebra on the device: combine = R(E^-1) K^-1, trans = t(E^-1)   (bev_model.py:46-53)
+// fp64 Gauss-Jordan with partial pivoting, rounded once to fp32: deterministic on every host
+// (the reference's fp32 LAPACK result varies by host CPU ISA in the last ulp).
+// ------------------------------------------------------------------------------------------
+template <int M>
+__device__ void inv_gj(const double *a_in, double *inv) {
+  double a[M][M], r[M][M];
+  for (int i = 0; i < M; ++i)
+    for (int j = 0; j < M; ++j) {
+      a[i][j] = a_in[i * M + j];
+      r[i][j] = i == j ? 1.0 : 0.0;
+    }
+  for (int c = 0; c < M; ++c) {
+    int piv = c;
+    for (int i = c + 1; i < M; ++i)
+      if (fabs(a[i][c]) > fabs(a[piv][c])) piv = i;
+    if (piv != c)
+      for (int j = 0; j < M; ++j) {
+        double t = a[c][j]; a[c][j] = a[piv][j]; a[piv][j] = t;
+        t = r[c][j]; r[c][j] = r[piv][j]; r[piv][j] = t;
+      }
+    const double d = a[c][c];
+    for (int j = 0; j < M; ++j) { a[c][j] /= d; r[c][j] /= d; }
+    for (int i = 0; i < M; ++i) {
+      if (i == c) continue;
+      const double f = a[i][c];
+      if (f == 0.0) continue;
+      for (int j = 0; j < M; ++j) { a[i][j] -= f * a[c][j]; r[i][j] -= f * r[c][j]; }
+    }
+  }
+  for (int i = 0; i < M; ++i)
+    for (int j = 0; j < M; ++j) inv[i * M + j] = r[i][j];
+}
+
+__global__ void k_rig(const float *__restrict__ K, const float *__restrict__ E, int BN,
+                      float *__restrict__ combine, float *__restrict__ trans) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= BN) return;
+  double k[9], e[16], ki[9], ei[16];
+  for (int j = 0; j < 9; ++j) k[j] = K[9 * i + j];
+  for (int j = 0; j < 16; ++j) e[j] = E[16 * i + j];
+  inv_gj<3>(k, ki);
+  inv_gj<4>(e, ei);
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) {
+      double acc = 0.0;
+      for (int t = 0; t < 3; ++t) acc += ei[4 * r + t] * ki[3 * t + c];
+      combine[9 * i + 3 * r + c] = (float)acc;
+    }
+    trans[3 * i + r] = (float)ei[4 * r + 3];
+  }
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -329,6 +384,14 @@ int e2ep_geom_index(const float *frustum, const float *combine, const float *tra
                      frustum, combine, trans, lo[0], lo[1], lo[2], res[0], res[1], res[2], X, Y, Z,
                      D * h * w, total, pillar);
   return launch_status("e2ep_geom_index");
+}
+
+int e2ep_rig_transforms(const float *K, const float *E, int BN, float *combine, float *trans,
+                        void *stream) {
+  E2EP_REQUIRE(BN > 0, E2EP_EINVAL, "e2ep_rig_transforms: BN must be positive");
+  hipLaunchKernelGGL(k_rig, dim3(cdiv(BN, 64)), dim3(64), 0, as_stream(stream), K, E, BN, combine,
+                     trans);
+  return launch_status("e2ep_rig_transforms");
 }
 
 size_t e2ep_lss_plan_workspace(int B, int XYZ) { return (size_t)B * XYZ * sizeof(int); }

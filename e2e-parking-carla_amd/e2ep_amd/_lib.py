@@ -19,6 +19,7 @@ _fp3 = ctypes.POINTER(ctypes.c_float)
 SIGNATURES = {
     "e2ep_abi_version": (_i, []),
     "e2ep_last_error": (ctypes.c_char_p, []),
+    "e2ep_rig_transforms": (_i, [_p, _p, _i, _p, _p, _p]),
     "e2ep_geom_index": (_i, [_p, _p, _p, _fp3, _fp3, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_lss_plan_workspace": (_sz, [_i, _i]),
     "e2ep_lss_plan": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p]),

@@ -24,10 +24,23 @@ def plan_cache_enabled():
     return os.environ.get("E2EP_PLAN_CACHE", "1") != "0"
 
 
-def rig_transforms(intrinsics, extrinsics):
-    """combine = R(E^-1) K^-1 and trans = t(E^-1), computed on the host in fp32 exactly as the
-    reference's CPU path does (model/bev_model.py:46-53), so the pillar index is bit-exact.
-    Returns CPU tensors (B,N,3,3), (B,N,3)."""
+def rig_transforms(intrinsics, extrinsics, device):
+    """combine = R(E^-1) K^-1 and trans = t(E^-1) (model/bev_model.py:46-53) on the device
+    (e2ep_rig_transforms: fp64 Gauss-Jordan, one fp32 rounding; deterministic on any host).
+    Returns device tensors (B,N,3,3), (B,N,3)."""
+    K = intrinsics.detach().to(device=device, dtype=torch.float32).contiguous()
+    E = extrinsics.detach().to(device=device, dtype=torch.float32).contiguous()
+    B, N = K.shape[:2]
+    combine = torch.empty(B, N, 3, 3, dtype=torch.float32, device=device)
+    trans = torch.empty(B, N, 3, dtype=torch.float32, device=device)
+    _lib.call("e2ep_rig_transforms", _lib.ptr(K), _lib.ptr(E), B * N, _lib.ptr(combine),
+              _lib.ptr(trans), _lib.stream())
+    return combine, trans
+
+
+def rig_transforms_host(intrinsics, extrinsics):
+    """The reference's own fp32 CPU algebra (torch.inverse + matmul), for comparisons: its last
+    ulp depends on the host CPU's LAPACK kernels.  Returns CPU tensors."""
     K = intrinsics.detach().float().cpu()
     E = extrinsics.detach().float().cpu()
     inv_e = torch.inverse(E)

@@ -61,7 +61,7 @@ class BevModel(nn.Module):
         """Pillar plan for this batch's rig.  The plan is a pure function of (frustum, K, E);
         when K and E are host tensors (the dataloader / agent case) it is memoised on their
         bytes, since the CARLA rig is constant.  E2EP_PLAN_CACHE=0
-        rebuilds it every call (5 kernel launches + the 3x3 host algebra)."""
+        rebuilds it every call (6 kernel launches, no host synchronisation)."""
         if self._host_consts is None:
             self._host_consts = self._consts()
         lo, res, dims = self._host_consts
@@ -72,7 +72,7 @@ class BevModel(nn.Module):
                    extrinsics.detach().float().contiguous().numpy().tobytes())
             if key == self._plan_key and self._plan is not None:
                 return self._plan
-        combine, trans = lss.rig_transforms(intrinsics, extrinsics)
+        combine, trans = lss.rig_transforms(intrinsics, extrinsics, device)
         plan = lss.build_plan(self.frustum, combine, trans, lo, res, dims, device)
         if key is not None:
             self._plan_key, self._plan = key, plan

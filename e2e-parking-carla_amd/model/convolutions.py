@@ -12,8 +12,8 @@ def _conv_bn(cin, cout, k, pad=0, dil=1):
             nn.ReLU()]
 
 
-def _run_conv_bn_relu(seq, x):
-    conv, bn = seq[0], seq[1]
+def _run_conv_bn_relu(seq, x, first=0):
+    conv, bn = seq[first], seq[first + 1]
     return ops.bn_act(ops.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation),
                       bn, "relu")
 
@@ -31,7 +31,7 @@ class ASPPPooling(nn.Sequential):
         super().__init__(nn.AdaptiveAvgPool2d(1), *_conv_bn(cin, cout, 1))
 
     def forward(self, x):
-        g = _run_conv_bn_relu(self[1:], x.mean((2, 3), keepdim=True))
+        g = _run_conv_bn_relu(self, x.mean((2, 3), keepdim=True), first=1)
         return ops.resize(g, x.shape[-2:])
 
 
@@ -70,5 +70,5 @@ class UpsamplingConcat(nn.Module):
 
     def forward(self, x_to_upsample, x):
         y = torch.cat([x, ops.upsample2x(x_to_upsample)], 1)
-        y = _run_conv_bn_relu(self.conv[0:3], y)
-        return _run_conv_bn_relu(self.conv[3:6], y)
+        y = _run_conv_bn_relu(self.conv, y, 0)
+        return _run_conv_bn_relu(self.conv, y, 3)

@@ -33,6 +33,13 @@ const char *e2ep_last_error(void);
  * Lift-splat
  * ------------------------------------------------------------------------------------- */
 
+/* Rig algebra (model/bev_model.py:46-53): combine [BN,3,3] = R(E^-1) K^-1, trans [BN,3] = t(E^-1)
+ * from K [BN,3,3], E [BN,4,4].  fp64 Gauss-Jordan (partial pivoting), one rounding to fp32:
+ * deterministic on every host, whereas the reference's fp32 CPU torch.inverse differs by host
+ * ISA in the last ulp (tests/test_lss_gpu.py documents the effect on the pillar index). */
+int e2ep_rig_transforms(const float *K, const float *E, int BN, float *combine, float *trans,
+                        void *stream);
+
 /* Ego-frame geometry + integer pillar index of every frustum point.
  * Replaces BevModel.get_geometry (model/bev_model.py:45-57) and the voxelisation / mask /
  * rank of proj_bev_feature (model/bev_model.py:85-95).

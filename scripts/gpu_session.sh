@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel-trace profile.
+# Every GPU step has its own time limit; a crash / abort / timeout stops the script
+# (test failures, rc=1, do not).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/session.log
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/session.log
+  tail -5 "$OUT/$name.log" | tee -a $OUT/session.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-pytest,smoke,bench,prof}
+[[ $STEPS == *pytest* ]] && run pytest_gpu 600 python -m pytest tests -x -q -m gpu
+[[ $STEPS == *smoke* ]]  && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+[[ $STEPS == *bench* ]]  && run bench 600 python bench.py --steps 20 --warmup 5
+[[ $STEPS == *prof* ]]   && run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 --no-cpu-baseline
+exit 0

@@ -34,12 +34,34 @@ def test_pillar_index_bit_exact_hires_6cam():
     assert hashlib.sha256(got.tobytes()).hexdigest() == meta()["geometry_6cam_512"]["pillar_sha256"]
 
 
-def test_rig_transforms_match_reference_bits():
-    from e2ep_amd import lss, synthetic
+def _pillar_from_rig(K, E, frustum):
+    from e2ep_amd import lss
+    g4 = golden("geometry_4cam_256.npz")
+    comb, trans = lss.rig_transforms(K[None], E[None], DEV)
+    plan = lss.build_plan(torch.from_numpy(frustum), comb, trans, g4["lo"].tolist(), g4["res"].tolist(),
+                          g4["dim"].tolist(), DEV)
+    return comb[0].cpu().numpy(), plan.pillar.cpu().numpy().astype(np.int32)
+
+
+def test_device_rig_algebra_reproduces_reference_pillars_4cam():
+    """End to end from K,E: the device rig algebra (fp64, deterministic) lands within a few ulp (fp32 LU error, measured 11) of
+    the reference's fp32 LAPACK combine and gives the reference's pillar table bit for bit."""
     g = golden("geometry_4cam_256.npz")
-    K, E = synthetic.rig()
-    comb, trans = lss.rig_transforms(K[None].to(DEV), E[None].to(DEV))
-    assert np.array_equal(comb[0].numpy(), g["combine"]) and np.array_equal(trans[0].numpy(), g["trans"])
+    comb, pil = _pillar_from_rig(torch.from_numpy(g["K"]), torch.from_numpy(g["E"]), g["frustum"])
+    ulp = np.abs(comb.view(np.int32).astype(np.int64) - g["combine"].view(np.int32).astype(np.int64))
+    assert ulp[np.abs(g["combine"]) > 1e-6].max() <= 16  # fp32 LU vs fp64 GJ: measured 11
+    assert np.array_equal(pil, g["pillar"].reshape(-1))
+
+
+def test_device_rig_algebra_hires_6cam_band():
+    """6-cam 512^2: the reference's own fp32 combine is host-ISA dependent in the last ulp and
+    a handful of the 1.18M points sit within an ulp of a cell edge; bound that band."""
+    g = golden("geometry_6cam_512.npz")
+    from oracle import geom_c
+    g4 = golden("geometry_4cam_256.npz")
+    ref = geom_c.geom_index(g["frustum"], g["combine"], g["trans"], g4["lo"], g4["res"], g4["dim"]).reshape(-1)
+    _, pil = _pillar_from_rig(torch.from_numpy(g["K"]), torch.from_numpy(g["E"]), g["frustum"])
+    assert (pil != ref).sum() <= 16
 
 
 def test_plan_invariants_batch_of_different_rigs():
@@ -49,7 +71,7 @@ def test_plan_invariants_batch_of_different_rigs():
     K, E = synthetic.rig()
     E2 = E.clone()
     E2[:, :3, 3] += torch.tensor([0.13, -0.07, 0.02])  # second sample: shifted rig
-    comb, trans = lss.rig_transforms(torch.stack([K, K]), torch.stack([E, E2]))
+    comb, trans = lss.rig_transforms(torch.stack([K, K]), torch.stack([E, E2]), DEV)
     plan = lss.build_plan(torch.from_numpy(g4["frustum"]), comb, trans, g4["lo"].tolist(),
                           g4["res"].tolist(), [200, 200, 1], DEV)
     pil = plan.pillar.view(2, -1).cpu().numpy()
@@ -125,8 +147,20 @@ def test_lss_full_channels_vs_oracle_and_determinism():
     ref = O.splat(xyz, outer, res, torch.from_numpy(g["lo"]) + res / 2.0, torch.from_numpy(g["dim"]))
     ref.backward(gout[:, :C])
     bev, gp, gf = outs[0]
-    assert max_scaled(bev, ref) < 1e-4 and rel_l2(bev, ref) < 1e-5
+    assert max_scaled(bev, ref) < 1e-4 and rel_l2(bev, ref) < 1e-4
     assert rel_l2(gp, po.grad) < 1e-5 and rel_l2(gf, fo.grad) < 1e-5
+    # against an exact fp64 segmented sum the direct per-pillar sum is far tighter than the
+    # reference's cumsum-difference
+    pil = torch.from_numpy(g["pillar"]).reshape(-1).long()
+    keep = pil >= 0
+    exact = torch.zeros(B, 40000, C, dtype=torch.float64)
+    for b in range(B):
+        pts = (prob[b * N:(b + 1) * N].double().permute(0, 2, 3, 1).unsqueeze(-1)
+               * feat[b * N:(b + 1) * N].double().permute(0, 2, 3, 1).unsqueeze(-2))  # n,h,w,D,C
+        pts = pts.permute(0, 3, 1, 2, 4).reshape(-1, C)
+        exact[b].index_add_(0, pil[keep], pts[keep])
+    exact = exact.permute(0, 2, 1).reshape(B, C, 200, 200)
+    assert rel_l2(bev, exact) < 5e-7 and rel_l2(ref, exact) > rel_l2(bev, exact)
     # cells with no points are exactly zero, as in the reference
     assert torch.equal(bev[ref == 0], torch.zeros_like(bev[ref == 0]))
 
