@@ -27,6 +27,12 @@ SIGNATURES = {
     "e2ep_lss_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "e2ep_transpose": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
     "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
+    "e2ep_conv_table": (_i, [_p, _i, _p, _p]),
+    "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p]),
+    "e2ep_conv_dgrad": (_i, [_p, _p, _p, _p, _p, _p]),
+    "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),
+    "e2ep_conv_wgrad": (_i, [_p, _p, _p, _p, _i, _p, _p, _i, _p]),
+    "e2ep_bias_grad": (_i, [_p, _i, _i, _i, _p, _p]),
 }
 
 _LIB = None
@@ -71,6 +77,11 @@ def ptr(t):
 
 def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dims(vals):
+    """A host int32 array (kept alive by the caller for the duration of the call)."""
+    return (ctypes.c_int * len(vals))(*[int(v) for v in vals])
 
 
 def host3(vals):

@@ -106,6 +106,38 @@ int e2ep_transpose(const float *in, long long in_bstride, int batch, int rows, i
 int e2ep_target_bev(const float *target_point, const float *noise, int B, int X, int Y,
                     float res_x, float res_y, float *out, long long out_bstride, void *stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Convolution, NCHW fp32, implicit GEMM on the exact-f32 matrix cores (SURVEY.md §8a rows
+ * a8 (1x1/stem), a9, a11, a13).  Replaces torch.nn.Conv2d forward/backward in
+ * model/bev_encoder.py:13-34, model/segmentation_head.py:19-31,
+ * model/convolutions.py:183-282 and the efficientnet-pytorch 1x1 / stem convs.
+ *
+ * dims[15] = {N, Cin, H, W, Cout, R, S, P, Q, stride_h, stride_w, pad_top, pad_left,
+ *             dil_h, dil_w}; P, Q are the output size (so asymmetric "SAME" padding is just
+ * a bigger P/Q with implicit zero rows/cols at the bottom/right).  groups == 1.
+ * ------------------------------------------------------------------------------------- */
+
+/* Build the per-conv im2col k-table (int4[Cin*R*S], or int4[Cout*R*S] when dgrad != 0). */
+int e2ep_conv_table(const int *dims, int dgrad, void *table, void *stream);
+
+/* y[N,Cout,P,Q] = conv(x[N,Cin,H,W], w[Cout,Cin,R,S]) + bias (nullable); act 0 none, 1 relu. */
+int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const void *table,
+                  const int *dims, int act, float *y, void *stream);
+
+/* dx[N,Cin,H,W] = conv_transpose(gout[N,Cout,P,Q], w)   (table built with dgrad = 1). */
+int e2ep_conv_dgrad(const float *gout, const float *w, const void *table, const int *dims,
+                    float *dx, void *stream);
+
+/* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
+ * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of
+ * e2ep_conv_wgrad_workspace bytes) are summed in a fixed order: deterministic. */
+size_t e2ep_conv_wgrad_workspace(const int *dims, int splits);
+int e2ep_conv_wgrad(const float *gout, const float *x, const void *table, const int *dims,
+                    int splits, void *workspace, float *dw, int accumulate, void *stream);
+
+/* db[C] = sum over (n, p) of gout[N, C, HW]. */
+int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,71 @@
+"""e2ep implicit-GEMM conv (fp32 MFMA) vs an fp64 CPU reference of the same op, for every
+conv geometry family of the ParkingModel hot path."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (N, Cin, H, W, Cout, R, S, stride, pad(l,r,t,b), dil, bias, act)
+CASES = [
+    (2, 65, 64, 64, 64, 7, 7, 2, (3, 3, 3, 3), 1, False, 0),     # BEV conv1 (reduced H)
+    (2, 64, 16, 16, 64, 3, 3, 1, (1, 1, 1, 1), 1, False, 1),     # BasicBlock 3x3 (+relu)
+    (2, 64, 16, 16, 128, 3, 3, 2, (1, 1, 1, 1), 1, False, 0),    # layer2 stride-2
+    (2, 64, 16, 16, 128, 1, 1, 2, (0, 0, 0, 0), 1, False, 0),    # downsample 1x1/2
+    (4, 3, 32, 32, 48, 3, 3, 2, (0, 1, 0, 1), 1, False, 0),      # EfficientNet stem SAME pad
+    (4, 160, 16, 16, 64, 3, 3, 1, (12, 12, 12, 12), 12, False, 0),  # ASPP dilation 12
+    (4, 160, 16, 16, 64, 3, 3, 1, (24, 24, 24, 24), 24, False, 0),  # ASPP dilation 24
+    (4, 320, 16, 16, 64, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),    # ASPP project
+    (4, 64, 16, 16, 160, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),     # DeepLab last 1x1 + bias
+    (4, 216, 32, 32, 48, 3, 3, 1, (1, 1, 1, 1), 1, False, 0),    # UpsamplingConcat
+    (8, 144, 1, 1, 6, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),        # SE reduce (1x1 map)
+    (8, 6, 1, 1, 144, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),        # SE expand
+    (2, 64, 50, 50, 3, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),       # seg-head classifier
+    (3, 24, 33, 17, 40, 5, 5, 2, (2, 2, 2, 2), 1, False, 1),     # odd sizes, k5/s2
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_conv_fwd_bwd_vs_fp64(case):
+    from e2ep_amd import conv
+    N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5
+    b = torch.randn(Cout, generator=g) if has_b else None
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    bd = b.to(DEV).requires_grad_(True) if has_b else None
+    y = conv.conv2d(xd, wd, bd, (st, st), pad, (dil, dil), act)
+    gy = torch.randn(y.shape, generator=g)
+    y.backward(gy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    b64 = b.double().requires_grad_(True) if has_b else None
+    y64 = F.conv2d(F.pad(x64, pad), w64, b64, st, 0, dil)
+    if act:
+        y64 = torch.relu(y64)
+    y64.backward(gy.double())
+    assert y.shape == y64.shape
+    assert rel_l2(y, y64) < 2e-6
+    assert rel_l2(xd.grad, x64.grad) < 2e-6
+    assert rel_l2(wd.grad, w64.grad) < 2e-6
+    if has_b:
+        assert rel_l2(bd.grad, b64.grad) < 2e-6
+
+
+def test_conv_wgrad_deterministic():
+    from e2ep_amd import conv
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(8, 64, 32, 32, generator=g).to(DEV)
+    w = (torch.randn(64, 64, 3, 3, generator=g) / 24).to(DEV)
+    gy = torch.randn(8, 64, 32, 32, generator=g).to(DEV)
+    outs = []
+    for _ in range(2):
+        wd = w.clone().requires_grad_(True)
+        conv.conv2d(x, wd, None, (1, 1), (1, 1, 1, 1)).backward(gy)
+        outs.append(wd.grad.clone())
+    assert torch.equal(outs[0], outs[1])
