@@ -1,0 +1,199 @@
+// Depthwise (groups == channels, multiplier 1) conv for EfficientNet's MBConv
+// (efficientnet-pytorch 0.7.1 _depthwise_conv: k3/k5, stride 1/2, static SAME padding),
+// forward, data gradient (gather, no atomics) and weight gradient (fixed-order split
+// reduction), NCHW fp32, for gfx950.  Memory-bound: each kernel streams its input once.
+#include "common.h"
+
+namespace e2ep {
+
+struct DwGeom {
+  int N, C, H, W, K, P, Q, st, pt, pl;
+};
+
+// forward: one thread per output pixel; taps unrolled for the compile-time kernel size
+template <int K>
+__global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
+                                                const float *__restrict__ w, DwGeom g,
+                                                float *__restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)g.N * g.C * g.P * g.Q;
+  if (i >= total) return;
+  const int ox = (int)(i % g.Q);
+  const long long r = i / g.Q;
+  const int oy = (int)(r % g.P);
+  const long long nc = r / g.P;
+  const int c = (int)(nc % g.C);
+  const float *xp = x + nc * g.H * g.W;
+  const float *wp = w + c * K * K;
+  const int y0 = oy * g.st - g.pt, x0 = ox * g.st - g.pl;
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const int iy = y0 + a;
+    if ((unsigned)iy >= (unsigned)g.H) continue;
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const int ix = x0 + b;
+      if ((unsigned)ix < (unsigned)g.W) s += wp[a * K + b] * xp[iy * g.W + ix];
+    }
+  }
+  y[i] = s;
+}
+
+// data gradient: one thread per input pixel, gather the outputs whose window covers it
+template <int K>
+__global__ void __launch_bounds__(256) k_dw_dgrad(const float *__restrict__ gy,
+                                                  const float *__restrict__ w, DwGeom g,
+                                                  float *__restrict__ dx) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)g.N * g.C * g.H * g.W;
+  if (i >= total) return;
+  const int ix = (int)(i % g.W);
+  const long long r = i / g.W;
+  const int iy = (int)(r % g.H);
+  const long long nc = r / g.H;
+  const int c = (int)(nc % g.C);
+  const float *gp = gy + nc * g.P * g.Q;
+  const float *wp = w + c * K * K;
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const int ny = iy + g.pt - a;
+    if (ny < 0) continue;
+    const int oy = ny / g.st;
+    if (oy * g.st != ny || oy >= g.P) continue;
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const int nx = ix + g.pl - b;
+      if (nx < 0) continue;
+      const int ox = nx / g.st;
+      if (ox * g.st == nx && ox < g.Q) s += wp[a * K + b] * gp[oy * g.Q + ox];
+    }
+  }
+  dx[i] = s;
+}
+
+// weight gradient partials: grid (C, splits); each slice of (n, oy, ox) accumulates K*K taps
+template <int K>
+__global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
+                                                  const float *__restrict__ x, DwGeom g,
+                                                  int splits, float *__restrict__ part) {
+  const int c = blockIdx.x, sp = blockIdx.y;
+  const long long PQ = (long long)g.P * g.Q;
+  const long long tot = (long long)g.N * PQ;
+  const long long per = (tot + splits - 1) / splits;
+  const long long beg = sp * per, end = min(tot, beg + per);
+  float acc[K * K];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
+  for (long long i = beg + threadIdx.x; i < end; i += 256) {
+    const long long n = i / PQ;
+    const int pix = (int)(i - n * PQ);
+    const int oy = pix / g.Q, ox = pix - oy * g.Q;
+    const float gv = gy[(n * g.C + c) * PQ + pix];
+    const float *xp = x + (n * g.C + c) * g.H * g.W;
+    const int y0 = oy * g.st - g.pt, x0 = ox * g.st - g.pl;
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      const int iy = y0 + a;
+      const bool oky = (unsigned)iy < (unsigned)g.H;
+#pragma unroll
+      for (int b = 0; b < K; ++b) {
+        const int ix = x0 + b;
+        if (oky && (unsigned)ix < (unsigned)g.W) acc[a * K + b] += gv * xp[iy * g.W + ix];
+      }
+    }
+  }
+  __shared__ float red[4][K * K];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) {
+    const float v = wave_sum(acc[t]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][t] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < K * K) {
+    const int t = threadIdx.x;
+    part[((long long)c * splits + sp) * K * K + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  }
+}
+
+__global__ void k_dw_wgrad_finalize(const float *__restrict__ part, int C, int KK, int splits,
+                                    float *__restrict__ dw) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * KK) return;
+  const int c = i / KK, t = i - c * KK;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[((long long)c * splits + k) * KK + t];
+  dw[i] = s;
+}
+
+static int dw_splits(long long pixels, int C) {
+  long long want = (1024 + C - 1) / C;
+  long long cap = pixels / 2048;
+  long long s = want < cap ? want : cap;
+  return (int)(s < 1 ? 1 : (s > 128 ? 128 : s));
+}
+
+static DwGeom dw_geom(const int *d) {
+  DwGeom g;
+  g.N = d[0]; g.C = d[1]; g.H = d[2]; g.W = d[3]; g.K = d[4]; g.P = d[5]; g.Q = d[6];
+  g.st = d[7]; g.pt = d[8]; g.pl = d[9];
+  return g;
+}
+
+}  // namespace e2ep
+
+using namespace e2ep;
+
+#define DW_DISPATCH(KERNEL, GRID, ...)                                                        \
+  do {                                                                                        \
+    if (g.K == 3)                                                                             \
+      hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__);     \
+    else if (g.K == 5)                                                                        \
+      hipLaunchKernelGGL(KERNEL<5>, GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__);     \
+    else {                                                                                    \
+      set_error("depthwise conv: kernel size %d unsupported (3, 5)", g.K);                   \
+      return E2EP_ERANGE;                                                                     \
+    }                                                                                         \
+  } while (0)
+
+extern "C" {
+
+// dims[10] = {N, C, H, W, K, P, Q, stride, pad_top, pad_left}
+int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, float *y, void *stream) {
+  DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
+               "e2ep_dwconv_fwd: bad geometry");
+  const long long total = (long long)g.N * g.C * g.P * g.Q;
+  DW_DISPATCH(k_dw_fwd, dim3(cdiv(total, 256)), x, w, g, y);
+  return launch_status("e2ep_dwconv_fwd");
+}
+
+int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream) {
+  DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
+               "e2ep_dwconv_dgrad: bad geometry");
+  const long long total = (long long)g.N * g.C * g.H * g.W;
+  DW_DISPATCH(k_dw_dgrad, dim3(cdiv(total, 256)), gy, w, g, dx);
+  return launch_status("e2ep_dwconv_dgrad");
+}
+
+size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
+  DwGeom g = dw_geom(dims);
+  return (size_t)g.C * dw_splits((long long)g.N * g.P * g.Q, g.C) * g.K * g.K * sizeof(float);
+}
+
+int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, void *workspace, float *dw,
+                      void *stream) {
+  DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
+               "e2ep_dwconv_wgrad: bad geometry");
+  const int sp = dw_splits((long long)g.N * g.P * g.Q, g.C);
+  float *part = static_cast<float *>(workspace);
+  DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part);
+  hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0,
+                     as_stream(stream), part, g.C, g.K * g.K, sp, dw);
+  return launch_status("e2ep_dwconv_wgrad");
+}
+
+}  // extern "C"

@@ -1,0 +1,273 @@
+"""Autograd ops over the e2ep BN / resize / depthwise / pooling / SE kernels (csrc/bn.hip,
+resize.hip, dwconv.hip, pool.hip).  Each forward enqueues on torch's current HIP stream;
+each backward is the matching e2ep gradient kernel (no PyTorch arithmetic)."""
+import torch
+
+from . import _lib, timing
+
+ACT = {None: 0, "none": 0, "relu": 1, "swish": 2}
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.E2EPError("e2ep ops run on a HIP device only; got a CPU tensor")
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------------------------------
+# BatchNorm2d + activation (+ residual)
+# ------------------------------------------------------------------------------------------
+class _BnAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, rm, rv, train, momentum, eps, act):
+        x = x.contiguous()
+        res = res.contiguous() if res is not None else None
+        N, C, H, W = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
+        with timing.region("bn_fwd"):
+            _lib.call("e2ep_bn_fwd", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res),
+                      _lib.ptr(rm), _lib.ptr(rv), N, C, H, W, int(train), float(momentum),
+                      float(eps), act, _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(y), _lib.ptr(ws),
+                      _lib.stream())
+        ctx.save_for_backward(x, gamma, beta, res, mean, invstd)
+        ctx.train, ctx.act = train, act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, res, mean, invstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, C, H, W = x.shape
+        nig = ctx.needs_input_grad
+        dx = torch.empty_like(x) if nig[0] else None
+        dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
+        db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
+        dres = torch.empty_like(x) if (res is not None and nig[3]) else None
+        ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
+        with timing.region("bn_bwd"):
+            _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(mean), _lib.ptr(invstd),
+                      _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), N, C, H, W, int(ctx.train),
+                      ctx.act, _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws),
+                      _lib.stream())
+        return dx, dg, db, dres, None, None, None, None, None, None
+
+
+def batch_norm_act(x, bn, act=None, res=None):
+    """BatchNorm2d module `bn` (its train/eval mode, momentum, eps, running buffers) applied
+    to x, plus an optional residual, then the activation."""
+    _dev(x, res)
+    train = bn.training or not bn.track_running_stats
+    if bn.training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    return _BnAct.apply(x, bn.weight, bn.bias, res, rm if train else rm, rv, train, mom, bn.eps,
+                        ACT[act])
+
+
+class _Act(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _lib.call("e2ep_act_fwd", _lib.ptr(x), x.numel(), act, _lib.ptr(y), _lib.stream())
+        ctx.save_for_backward(x)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        _lib.call("e2ep_act_bwd", _lib.ptr(x), _lib.ptr(dy), x.numel(), ctx.act, _lib.ptr(dx),
+                  _lib.stream())
+        return dx, None
+
+
+def activation(x, act):
+    _dev(x)
+    return _Act.apply(x, ACT[act])
+
+
+# ------------------------------------------------------------------------------------------
+# bilinear resize (align_corners=False)
+# ------------------------------------------------------------------------------------------
+class _Resize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, Ho, Wo, sh, sw):
+        x = x.contiguous()
+        N, C, Hi, Wi = x.shape
+        y = torch.empty(N, C, Ho, Wo, dtype=torch.float32, device=x.device)
+        with timing.region("resize_fwd"):
+            _lib.call("e2ep_resize_fwd", _lib.ptr(x), N * C, Hi, Wi, Ho, Wo, sh, sw, _lib.ptr(y),
+                      Ho * Wo, _lib.stream())
+        ctx.meta = (N, C, Hi, Wi, Ho, Wo, sh, sw)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, Hi, Wi, Ho, Wo, sh, sw = ctx.meta
+        g = g.contiguous()
+        gx = torch.empty(N, C, Hi, Wi, dtype=torch.float32, device=g.device)
+        ws = _ws(N * C * Ho * Wi * 4, g.device)
+        with timing.region("resize_bwd"):
+            _lib.call("e2ep_resize_bwd", _lib.ptr(g), Ho * Wo, N * C, Hi, Wi, Ho, Wo, sh, sw,
+                      _lib.ptr(gx), 0, _lib.ptr(ws), _lib.stream())
+        return gx, None, None, None, None
+
+
+def resize(x, size=None, scale_factor=None):
+    """F.interpolate(x, size | scale_factor, mode='bilinear', align_corners=False)."""
+    _dev(x)
+    Hi, Wi = x.shape[-2:]
+    if scale_factor is not None:
+        Ho, Wo = int(Hi * scale_factor), int(Wi * scale_factor)
+        sh = sw = 1.0 / float(scale_factor)
+    else:
+        Ho, Wo = size
+        sh, sw = Hi / Ho, Wi / Wo
+    return _Resize.apply(x, int(Ho), int(Wo), float(sh), float(sw))
+
+
+# ------------------------------------------------------------------------------------------
+# depthwise conv
+# ------------------------------------------------------------------------------------------
+class _DwConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, dims):
+        x = x.contiguous()
+        w = w.contiguous()
+        N, C, H, W, K, P, Q = dims[:7]
+        y = torch.empty(N, C, P, Q, dtype=torch.float32, device=x.device)
+        d = _lib.dims(dims)
+        with timing.region("dwconv_fwd"):
+            _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(y), _lib.stream())
+        ctx.save_for_backward(x, w)
+        ctx.dims = dims
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        d = _lib.dims(ctx.dims)
+        s = _lib.stream()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            with timing.region("dwconv_dgrad"):
+                _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
+            with timing.region("dwconv_wgrad"):
+                _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(ws),
+                          _lib.ptr(dw), s)
+        return dx, dw, None
+
+
+def depthwise_conv2d(x, w, stride, pad):
+    """pad = (left, right, top, bottom); w [C, 1, K, K]."""
+    _dev(x)
+    N, C, H, W = x.shape
+    K = w.shape[-1]
+    l, r, t, b = pad
+    P = (H + t + b - K) // stride + 1
+    Q = (W + l + r - K) // stride + 1
+    return _DwConv.apply(x, w, (N, C, H, W, K, P, Q, stride, t, l))
+
+
+# ------------------------------------------------------------------------------------------
+# pooling / SE gate
+# ------------------------------------------------------------------------------------------
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty(N, C, P, Q, dtype=torch.float32, device=x.device)
+        arg = torch.empty(N, C, P, Q, dtype=torch.int8, device=x.device)
+        _lib.call("e2ep_maxpool3s2_fwd", _lib.ptr(x), N * C, H, W, _lib.ptr(y), _lib.ptr(arg),
+                  _lib.stream())
+        ctx.save_for_backward(arg)
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dx = torch.empty(N, C, H, W, dtype=torch.float32, device=gy.device)
+        _lib.call("e2ep_maxpool3s2_bwd", _lib.ptr(gy.contiguous()), _lib.ptr(arg), N * C, H, W,
+                  _lib.ptr(dx), _lib.stream())
+        return dx
+
+
+def max_pool3s2(x):
+    _dev(x)
+    return _MaxPool.apply(x)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty(N, C, 1, 1, dtype=torch.float32, device=x.device)
+        _lib.call("e2ep_avgpool_fwd", _lib.ptr(x), N * C, H * W, _lib.ptr(y), _lib.stream())
+        ctx.shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        N, C, H, W = ctx.shape
+        dx = torch.empty(N, C, H, W, dtype=torch.float32, device=gy.device)
+        _lib.call("e2ep_avgpool_bwd", _lib.ptr(gy.contiguous()), N * C, H * W, _lib.ptr(dx),
+                  _lib.stream())
+        return dx
+
+
+def global_avg_pool(x):
+    _dev(x)
+    return _AvgPool.apply(x)
+
+
+class _SeGate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a):
+        x = x.contiguous()
+        a = a.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty_like(x)
+        with timing.region("se_gate_fwd"):
+            _lib.call("e2ep_se_gate_fwd", _lib.ptr(x), _lib.ptr(a), N * C, H * W, _lib.ptr(y),
+                      _lib.stream())
+        ctx.save_for_backward(x, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, a = ctx.saved_tensors
+        N, C, H, W = x.shape
+        dx = torch.empty_like(x)
+        da = torch.empty_like(a)
+        with timing.region("se_gate_bwd"):
+            _lib.call("e2ep_se_gate_bwd", _lib.ptr(x), _lib.ptr(a), _lib.ptr(dy.contiguous()), N * C,
+                      H * W, _lib.ptr(dx), _lib.ptr(da), _lib.stream())
+        return dx, da
+
+
+def se_gate(x, a):
+    """x * sigmoid(a), a [N, C, 1, 1]."""
+    _dev(x, a)
+    return _SeGate.apply(x, a)

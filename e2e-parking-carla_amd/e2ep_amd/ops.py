@@ -1,77 +1,79 @@
 """Operator layer of the ParkingModel hot path on MI355X.
 
-Every model module calls these functions instead of torch.nn.functional.  Each one names
-the HIP kernel family that implements it (libe2ep_hip.so, include/e2ep.h); the few that are
-still MIOpen / hipBLASLt calls through PyTorch are listed in DESIGN.md §"Kernel coverage"
-with the round they move to HIP.
+Model modules call these functions instead of torch.nn.functional; every one of them runs
+an e2ep HIP kernel from libe2ep_hip.so (include/e2ep.h) — there is no PyTorch or CPU
+fallback, and a missing library raises.  What still runs as PyTorch/hipBLASLt work is
+listed in DESIGN.md ("Kernel coverage"): the transformer layers, the three losses, the
+depth softmax, and small elementwise glue (concat, residual adds outside BN, Adam).
 """
-import torch
-import torch.nn.functional as F
-
-from . import _lib
+from . import conv as _conv
+from . import nn_ops
 
 
 def _pad4(pad):
     if isinstance(pad, int):
         return (pad, pad, pad, pad)
-    if len(pad) == 2:
+    if len(pad) == 2:  # (ph, pw) torch convention
         return (pad[1], pad[1], pad[0], pad[0])
     return tuple(pad)
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
-    """NCHW convolution; padding is an int, (ph, pw) or (left, right, top, bottom)."""
-    l, r, t, b = _pad4(padding)
-    if l == r and t == b:
-        return F.conv2d(x, weight, bias, stride, (t, l), dilation, groups)
-    return F.conv2d(F.pad(x, (l, r, t, b)), weight, bias, stride, 0, dilation, groups)
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
 
 
-def _act(x, act):
-    if act is None:
-        return x
-    if act == "relu":
-        return F.relu(x)
-    if act == "swish":
-        return x * torch.sigmoid(x)
-    raise ValueError(act)
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None):
+    """NCHW convolution; padding is an int, (ph, pw) or (left, right, top, bottom).
+    groups == channels (depthwise) goes to the depthwise kernels, groups == 1 to the
+    implicit-GEMM MFMA kernels; act None | 'relu' is fused into the GEMM epilogue."""
+    pad = _pad4(padding)
+    if groups == 1:
+        return _conv.conv2d(x, weight, bias, _pair(stride), pad, _pair(dilation),
+                            nn_ops.ACT[act])
+    if groups == x.shape[1] and weight.shape[0] == groups and weight.shape[1] == 1 and bias is None \
+            and _pair(dilation) == (1, 1) and act is None:
+        s = _pair(stride)
+        assert s[0] == s[1]
+        return nn_ops.depthwise_conv2d(x, weight, s[0], pad)
+    raise NotImplementedError(f"e2ep conv2d: groups={groups} not on the hot path")
 
 
-def bn_act(x, bn, act=None):
-    """BatchNorm2d (train: batch statistics + running-stat update; eval: running stats) + act."""
-    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
-    y = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias,
-                     bn.training or not bn.track_running_stats, bn.momentum, bn.eps)
-    return _act(y, act)
+def bn_act(x, bn, act=None, res=None):
+    """BatchNorm2d (train: batch stats + running update; eval: running stats) [+ res] + act."""
+    return nn_ops.batch_norm_act(x, bn, act, res)
+
+
+def activation(x, act):
+    return nn_ops.activation(x, act)
 
 
 def squeeze_excite(x, reduce, expand):
-    g = F.adaptive_avg_pool2d(x, 1)
+    """efficientnet-pytorch MBConv SE: x * sigmoid(expand(swish(reduce(avgpool(x)))))."""
+    g = nn_ops.global_avg_pool(x)
     g = conv2d(g, reduce.weight, reduce.bias)
-    g = conv2d(g * torch.sigmoid(g), expand.weight, expand.bias)
-    return torch.sigmoid(g) * x
+    g = conv2d(nn_ops.activation(g, "swish"), expand.weight, expand.bias)
+    return nn_ops.se_gate(x, g)
 
 
 def drop_connect(x, p):
+    """efficientnet-pytorch drop_connect (training only): per-sample keep mask / keep."""
+    import torch
     keep = 1.0 - p
     mask = torch.floor(keep + torch.rand([x.shape[0], 1, 1, 1], dtype=x.dtype, device=x.device))
     return x / keep * mask
 
 
 def upsample2x(x):
-    return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+    return nn_ops.resize(x, scale_factor=2)
 
 
 def resize(x, size):
-    return F.interpolate(x, size=size, mode="bilinear", align_corners=False)
+    return nn_ops.resize(x, size=tuple(size))
 
 
 def max_pool3s2(x):
-    return F.max_pool2d(x, 3, 2, 1)
+    return nn_ops.max_pool3s2(x)
 
 
-def lib_loaded():
-    """True once libe2ep_hip.so is loaded (raises if it cannot be)."""
-    _lib.load()
-    return True
+def global_avg_pool(x):
+    return nn_ops.global_avg_pool(x)

@@ -28,11 +28,11 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         y = ops.bn_act(ops.conv2d(x, self.conv1.weight, None, self.stride, 1), self.bn1, "relu")
-        y = ops.bn_act(ops.conv2d(y, self.conv2.weight, None, 1, 1), self.bn2, None)
         if self.downsample is not None:
             x = ops.bn_act(ops.conv2d(x, self.downsample[0].weight, None, self.stride, 0),
                            self.downsample[1], None)
-        return torch.relu(y + x)
+        # relu(bn2(conv2(y)) + identity) as one fused BN/residual/activation kernel
+        return ops.bn_act(ops.conv2d(y, self.conv2.weight, None, 1, 1), self.bn2, "relu", res=x)
 
 
 def _layer(cin, cout, stride):

@@ -31,7 +31,7 @@ class ASPPPooling(nn.Sequential):
         super().__init__(nn.AdaptiveAvgPool2d(1), *_conv_bn(cin, cout, 1))
 
     def forward(self, x):
-        g = _run_conv_bn_relu(self, x.mean((2, 3), keepdim=True), first=1)
+        g = _run_conv_bn_relu(self, ops.global_avg_pool(x), first=1)
         return ops.resize(g, x.shape[-2:])
 
 

@@ -66,11 +66,11 @@ class MBConv(nn.Module):
             y = ops.bn_act(self._expand_conv(y), self._bn0, "swish")
         y = ops.bn_act(self._depthwise_conv(y), self._bn1, "swish")
         y = ops.squeeze_excite(y, self._se_reduce, self._se_expand)
+        if self.skip and not (drop_connect_rate and self.training):
+            return ops.bn_act(self._project_conv(y), self._bn2, None, res=x)  # fused skip add
         y = ops.bn_act(self._project_conv(y), self._bn2, None)
         if self.skip:
-            if drop_connect_rate and self.training:
-                y = ops.drop_connect(y, drop_connect_rate)
-            y = y + x
+            y = ops.drop_connect(y, drop_connect_rate) + x
         return y
 
 

@@ -30,9 +30,9 @@ class SegmentationHead(nn.Module):
             nn.ReLU(inplace=True), nn.Conv2d(c, self.seg_classes, kernel_size=1, padding=0))
 
     def top_down(self, x):
-        x = torch.relu(ops.conv2d(x, self.c5_conv.weight, self.c5_conv.bias))
+        x = ops.conv2d(x, self.c5_conv.weight, self.c5_conv.bias, act="relu")
         for conv in (self.up_conv5, self.up_conv4, self.up_conv3):
-            x = torch.relu(ops.conv2d(ops.upsample2x(x), conv.weight, conv.bias))
+            x = ops.conv2d(ops.upsample2x(x), conv.weight, conv.bias, act="relu")
         return ops.resize(x, (200, 200))
 
     def forward(self, fuse_feature):

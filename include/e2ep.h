@@ -138,6 +138,67 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const void *table, const 
 /* db[C] = sum over (n, p) of gout[N, C, HW]. */
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream);
 
+/* ---------------------------------------------------------------------------------------
+ * BatchNorm2d + activation (+ residual), NCHW fp32.
+ * Replaces BatchNorm2d(+ReLU / swish, + identity add) pairs of the reference model tree.
+ * act: 0 none, 1 relu, 2 swish (x * sigmoid(x)).  res (nullable) is added before act.
+ * train != 0: batch statistics (fp64 accumulation, fixed order), running stats updated in
+ * place with `momentum` (unbiased variance); train == 0: running statistics.
+ * mean / invstd [C] are outputs of fwd and inputs of bwd.  workspace: e2ep_bn_workspace.
+ * ------------------------------------------------------------------------------------- */
+size_t e2ep_bn_workspace(int N, int C, int H, int W);
+int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const float *res,
+                float *running_mean, float *running_var, int N, int C, int H, int W, int train,
+                float momentum, float eps, int act, float *mean, float *invstd, float *y,
+                void *workspace, void *stream);
+/* dx, dgamma, dbeta, dres (each nullable) from x, dy and the forward's mean/invstd. */
+int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
+                const float *gamma, const float *beta, const float *res, int N, int C, int H, int W,
+                int train, int act, float *dx, float *dgamma, float *dbeta, float *dres,
+                void *workspace, void *stream);
+/* Stand-alone activation (act as above) and its gradient w.r.t. the pre-activation x. */
+int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
+int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Bilinear resize, align_corners=False (F.interpolate / nn.Upsample semantics) over
+ * `planes` = N*C planes.  scale_* = 1/scale_factor when a factor is given, else In/Out.
+ * Replaces model/bev_encoder.py:24, model/segmentation_head.py:35-38,
+ * model/convolutions.py:197,238-240.  Backward is a deterministic two-pass gather.
+ * ------------------------------------------------------------------------------------- */
+int e2ep_resize_fwd(const float *x, int planes, int Hi, int Wi, int Ho, int Wo, float scale_h,
+                    float scale_w, float *y, long long y_pstride, void *stream);
+size_t e2ep_resize_bwd_workspace(int planes, int Ho, int Wi);
+int e2ep_resize_bwd(const float *g, long long g_pstride, int planes, int Hi, int Wi, int Ho,
+                    int Wo, float scale_h, float scale_w, float *gx, int accumulate,
+                    void *workspace, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Depthwise conv (EfficientNet MBConv _depthwise_conv; k 3 or 5, stride 1 or 2, static
+ * SAME padding).  dims[10] = {N, C, H, W, K, P, Q, stride, pad_top, pad_left}.
+ * ------------------------------------------------------------------------------------- */
+int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, float *y, void *stream);
+int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream);
+size_t e2ep_dwconv_wgrad_workspace(const int *dims);
+int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, void *workspace, float *dw,
+                      void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Pooling and squeeze-excitation gating.
+ * max-pool 3x3 / stride 2 / pad 1 (ResNet stem, model/bev_encoder.py:17,30) stores the
+ * winning tap index (int8) for its gather backward; global average pool per plane (ASPP
+ * pooling, SE squeeze); SE gate y = x * sigmoid(a[plane]).
+ * ------------------------------------------------------------------------------------- */
+int e2ep_maxpool3s2_fwd(const float *x, int planes, int H, int W, float *y, int8_t *arg,
+                        void *stream);
+int e2ep_maxpool3s2_bwd(const float *gy, const int8_t *arg, int planes, int H, int W, float *dx,
+                        void *stream);
+int e2ep_avgpool_fwd(const float *x, int planes, int HW, float *y, void *stream);
+int e2ep_avgpool_bwd(const float *gy, int planes, int HW, float *dx, void *stream);
+int e2ep_se_gate_fwd(const float *x, const float *a, int planes, int HW, float *y, void *stream);
+int e2ep_se_gate_bwd(const float *x, const float *a, const float *dy, int planes, int HW,
+                     float *dx, float *da, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

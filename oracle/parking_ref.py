@@ -446,7 +446,7 @@ def depth_labels(gt, d_bound=(0.5, 12.5, 0.25), down=8):
     g = torch.where(g == 0.0, 1e5 * torch.ones_like(g), g).min(-1).values
     g = (g - (d_bound[0] - d_bound[2])) / d_bound[2]
     g = torch.where((g < D + 1) & (g >= 0.0), g, torch.zeros_like(g))
-    return F.one_hot(g.long(), num_classes=D + 1).view(-1, D + 1)[:, 1:].float()
+    return F.one_hot(g.long(), num_classes=D + 1).view(-1, D + 1)[:, 1:].to(gt.dtype)
 
 
 def depth_loss(prob, gt):

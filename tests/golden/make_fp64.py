@@ -1,0 +1,62 @@
+"""fp64 companion of model_train_b2.npz: the oracle (bit-identical to the reference in fp32,
+tests/golden/make_golden.py) re-run with fp64 arithmetic everywhere except the integer
+pillar geometry (which stays fp32, as in the reference).
+
+Deterministic-train mode (BN batch statistics at B=2) is ill-conditioned: the reference's
+own fp32 result differs from this fp64 value by ~1e-3 on the segmentation logits and ~2 %
+on some weight gradients (the cumsum-difference pooling noise, SURVEY.md §0 fact 4, is
+amplified by batch-statistic BN).  Parity tests therefore measure both the product and the
+reference against this fp64 value.   Run: python tests/golden/make_fp64.py
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "e2e-parking-carla_amd")]
+
+from oracle import parking_ref as O  # noqa: E402
+from e2ep_amd import synthetic  # noqa: E402
+from weights import make_grad_probe_keys, make_state  # noqa: E402
+
+
+def oracle_model(dtype):
+    torch.manual_seed(0)
+    m = O.ParkingModelRef(O.Cfg, dropout=False)
+    m.load_state_dict(make_state(m.state_dict(), 1234))
+    keep = {k: v.detach().clone() for k, v in m.bev_model.named_parameters(recurse=False)}
+    m = m.to(dtype)
+    for k, v in keep.items():  # geometry constants stay fp32 (integer pillar index)
+        getattr(m.bev_model, k).data = v
+    return m
+
+
+def main():
+    torch.set_num_threads(8)
+    m = oracle_model(torch.float64).train()
+    data = synthetic.synthetic_batch(2, seed=5)
+    noise = synthetic.target_noise(2, seed=5)
+    d = {k: (v.double() if v.is_floating_point() and k not in ("intrinsics", "extrinsics") else v)
+         for k, v in data.items()}
+    losses, (pc, ps, pd) = O.train_losses(m, d, noise)
+    losses["train_loss"].backward()
+    fx = {"loss_control": np.float64(losses["control_loss"].item()),
+          "loss_seg": np.float64(losses["segmentation_loss"].item()),
+          "loss_depth": np.float64(losses["depth_loss"].item()),
+          "pred_control": pc.detach().numpy(), "seg_norm": np.float64(ps.detach().norm()),
+          "seg_slice": ps.detach()[:, :, 90:110, 90:110].numpy(),
+          "depth_norm": np.float64(pd.detach().norm()), "depth_slice": pd.detach()[:, :, 10:14].numpy()}
+    params = dict(m.named_parameters())
+    for k in make_grad_probe_keys(params.keys()):
+        g = params[k].grad.reshape(-1)
+        fx["gnorm::" + k] = np.float64(g.norm())
+        fx["gslice::" + k] = g[:4096].numpy()
+    np.savez_compressed(os.path.join(HERE, "model_train_b2_fp64.npz"), **fx)
+    print("wrote model_train_b2_fp64.npz")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+"""e2ep BN / resize / depthwise / pooling / SE kernels vs an fp64 CPU reference of the same
+PyTorch op (values, gradients, running statistics)."""
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _g(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+@pytest.mark.parametrize("train", [True, False])
+@pytest.mark.parametrize("act", [None, "relu", "swish"])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("shape", [(4, 24, 32, 32), (3, 7, 5, 9), (32, 6, 1, 1)])
+def test_bn_act(train, act, res, shape):
+    from e2ep_amd import nn_ops
+    g = _g(sum(shape) + 3 * train)
+    x = torch.randn(*shape, generator=g) * 2 + 0.5
+    r = torch.randn(*shape, generator=g) if res else None
+    dy = torch.randn(*shape, generator=g)
+    C = shape[1]
+    bn = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3)
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.3 * torch.randn(C, generator=g))
+        bn.bias.copy_(0.2 * torch.randn(C, generator=g))
+        bn.running_mean.copy_(0.1 * torch.randn(C, generator=g))
+        bn.running_var.copy_(0.5 + torch.rand(C, generator=g))
+    bn64 = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3).double()
+    bn64.load_state_dict(bn.state_dict())
+    bn.train(train), bn64.train(train)
+    bnd = bn.to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    rd = r.to(DEV).requires_grad_(True) if res else None
+    y = nn_ops.batch_norm_act(xd, bnd, act, rd)
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    r64 = r.double().requires_grad_(True) if res else None
+    z = bn64(x64) + (r64 if res else 0)
+    y64 = {None: z, "relu": torch.relu(z) if act == "relu" else z, "swish": z * torch.sigmoid(z)}[act]
+    if act == "relu":
+        y64 = torch.relu(z)
+    y64.backward(dy.double())
+    assert rel_l2(y, y64) < 1e-6
+    assert rel_l2(xd.grad, x64.grad) < 1e-5
+    assert rel_l2(bnd.weight.grad, bn64.weight.grad) < 1e-5
+    assert rel_l2(bnd.bias.grad, bn64.bias.grad) < 1e-5
+    if res:
+        assert rel_l2(rd.grad, r64.grad) < 1e-6
+    assert rel_l2(bnd.running_mean, bn64.running_mean) < 1e-6
+    assert rel_l2(bnd.running_var, bn64.running_var) < 1e-6
+    assert int(bnd.num_batches_tracked) == int(bn64.num_batches_tracked)
+
+
+@pytest.mark.parametrize("case", [((8, 65, 200, 200), (256, 256), None), ((4, 64, 16, 16), None, 2),
+                                  ((2, 64, 128, 128), (200, 200), None), ((32, 64, 1, 1), (16, 16), None),
+                                  ((3, 5, 17, 9), (40, 7), None)])
+def test_resize(case):
+    from e2ep_amd import nn_ops
+    shape, size, sf = case
+    g = _g(shape[2] + shape[3])
+    x = torch.randn(*shape, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    y = nn_ops.resize(xd, size=size, scale_factor=sf)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    y64 = F.interpolate(x64, size=size, scale_factor=sf, mode="bilinear", align_corners=False)
+    y64.backward(dy.double())
+    assert y.shape == y64.shape
+    assert rel_l2(y, y64) < 1e-6
+    assert rel_l2(xd.grad, x64.grad) < 1e-6
+
+
+@pytest.mark.parametrize("case", [(4, 144, 64, 64, 3, 2, (0, 1, 0, 1)), (4, 48, 32, 32, 3, 1, (1, 1, 1, 1)),
+                                  (4, 192, 32, 32, 5, 2, (2, 2, 2, 2)), (2, 672, 16, 16, 5, 1, (2, 2, 2, 2)),
+                                  (3, 8, 13, 11, 3, 2, (0, 1, 0, 1))])
+def test_depthwise(case):
+    from e2ep_amd import ops
+    N, C, H, W, K, s, pad = case
+    g = _g(C + H)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, 1, K, K, generator=g) / K
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    y = ops.conv2d(xd, wd, None, s, pad, 1, groups=C)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    y64 = F.conv2d(F.pad(x64, pad), w64, None, s, 0, 1, C)
+    y64.backward(dy.double())
+    assert y.shape == y64.shape
+    assert rel_l2(y, y64) < 1e-6
+    assert rel_l2(xd.grad, x64.grad) < 1e-6
+    assert rel_l2(wd.grad, w64.grad) < 1e-5
+
+
+def test_maxpool_avgpool_segate():
+    from e2ep_amd import nn_ops
+    g = _g(5)
+    x = torch.randn(2, 16, 33, 64, generator=g)
+    x[0, 0, :4, :4] = 1.0  # ties: first maximum wins
+    xd = x.to(DEV).requires_grad_(True)
+    y = nn_ops.max_pool3s2(xd)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    y64 = F.max_pool2d(x64, 3, 2, 1)
+    y64.backward(dy.double())
+    assert torch.equal(y.cpu().double(), y64) and rel_l2(xd.grad, x64.grad) < 1e-7
+    # global average pool + SE gate
+    a = torch.randn(2, 16, 1, 1, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    ad = a.to(DEV).requires_grad_(True)
+    out = nn_ops.se_gate(xd, ad) + nn_ops.global_avg_pool(xd)
+    dy = torch.randn(out.shape, generator=g)
+    out.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    a64 = a.double().requires_grad_(True)
+    o64 = x64 * torch.sigmoid(a64) + x64.mean((2, 3), keepdim=True)
+    o64.backward(dy.double())
+    assert rel_l2(out, o64) < 1e-6 and rel_l2(xd.grad, x64.grad) < 1e-6 and rel_l2(ad.grad, a64.grad) < 1e-6
