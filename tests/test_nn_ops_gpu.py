@@ -74,8 +74,12 @@ def test_resize(case):
     y64 = F.interpolate(x64, size=size, scale_factor=sf, mode="bilinear", align_corners=False)
     y64.backward(dy.double())
     assert y.shape == y64.shape
-    assert rel_l2(y, y64) < 1e-6
-    assert rel_l2(xd.grad, x64.grad) < 1e-6
+    # coordinates are computed in fp32 as PyTorch's own fp32 kernel does: compare to that
+    # tightly, and to fp64 (different interpolation weights in the last bits) loosely
+    y32 = F.interpolate(x, size=size, scale_factor=sf, mode="bilinear", align_corners=False)
+    assert rel_l2(y, y32) < 1e-6
+    assert rel_l2(y, y64) < 2e-5
+    assert rel_l2(xd.grad, x64.grad) < 2e-5
 
 
 @pytest.mark.parametrize("case", [(4, 144, 64, 64, 3, 2, (0, 1, 0, 1)), (4, 48, 32, 32, 3, 1, (1, 1, 1, 1)),
