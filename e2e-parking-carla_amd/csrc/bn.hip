@@ -42,21 +42,21 @@ __global__ void __launch_bounds__(256) k_bn_stats(const float *__restrict__ x, i
                                                   int HW, int splits, long long per,
                                                   double *__restrict__ part) {
   const int c = blockIdx.x, sp = blockIdx.y;
-  const long long tot = (long long)N * HW;
-  const long long beg = sp * per, end = min(tot, beg + per);
+  const int tot = N * HW;
+  const int beg = sp * (int)per, end = min(tot, beg + (int)per);
   double s = 0.0, q = 0.0;
   if ((HW & 3) == 0) {
     // vectorised: slices never straddle an image when per % 4 == 0 and HW % 4 == 0
-    for (long long i = beg + threadIdx.x * 4; i < end; i += 1024) {
-      const long long n = i / HW, p = i - n * HW;
-      const float4 v = *reinterpret_cast<const float4 *>(x + (n * C + c) * HW + p);
+    for (int i = beg + threadIdx.x * 4; i < end; i += 1024) {
+      const int n = i / HW, p = i - n * HW;
+      const float4 v = *reinterpret_cast<const float4 *>(x + ((size_t)n * C + c) * HW + p);
       s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
       q += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
     }
   } else {
-    for (long long i = beg + threadIdx.x; i < end; i += 256) {
-      const long long n = i / HW, p = i - n * HW;
-      const double v = x[(n * C + c) * HW + p];
+    for (int i = beg + threadIdx.x; i < end; i += 256) {
+      const int n = i / HW, p = i - n * HW;
+      const double v = x[((size_t)n * C + c) * HW + p];
       s += v;
       q += v * v;
     }
@@ -116,11 +116,12 @@ __global__ void __launch_bounds__(256) k_bn_apply(const float *__restrict__ x,
                                                   const float *__restrict__ gamma,
                                                   const float *__restrict__ beta,
                                                   const float *__restrict__ res, int C, int HW,
-                                                  long long total, int act, float *__restrict__ y) {
-  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i >= total) return;
+                                                  int act, float *__restrict__ y) {
+  const int q = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (q >= HW) return;
+  const int c = blockIdx.y % C;
+  const size_t i = (size_t)blockIdx.y * HW + q;
   if ((HW & 3) == 0) {
-    const int c = (int)((i / HW) % C);
     const float sc = invstd[c] * (gamma ? gamma[c] : 1.f);
     const float sh = (beta ? beta[c] : 0.f) - mean[c] * sc;
     float4 v = *reinterpret_cast<const float4 *>(x + i);
@@ -131,8 +132,7 @@ __global__ void __launch_bounds__(256) k_bn_apply(const float *__restrict__ x,
     v.w = act_fwd(v.w * sc + sh + r.w, act);
     *reinterpret_cast<float4 *>(y + i) = v;
   } else {
-    for (int j = 0; j < 4 && i + j < total; ++j) {
-      const int c = (int)(((i + j) / HW) % C);
+    for (int j = 0; j < 4 && q + j < HW; ++j) {
       const float sc = invstd[c] * (gamma ? gamma[c] : 1.f);
       const float sh = (beta ? beta[c] : 0.f) - mean[c] * sc;
       y[i + j] = act_fwd(x[i + j] * sc + sh + (res ? res[i + j] : 0.f), act);
@@ -147,15 +147,15 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
     const float *__restrict__ beta, const float *__restrict__ res, int N, int C, int HW,
     int splits, int act, double *__restrict__ part) {
   const int c = blockIdx.x, sp = blockIdx.y;
-  const long long tot = (long long)N * HW;
-  const long long per = (tot + splits - 1) / splits;
-  const long long beg = sp * per, end = min(tot, beg + per);
+  const int tot = N * HW;
+  const int per = (tot + splits - 1) / splits;
+  const int beg = sp * per, end = min(tot, beg + per);
   const float mu = mean[c], is = invstd[c];
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   double s = 0.0, q = 0.0;
-  for (long long i = beg + threadIdx.x; i < end; i += 256) {
-    const long long n = i / HW, p = i - n * HW;
-    const long long off = (n * C + c) * HW + p;
+  for (int i = beg + threadIdx.x; i < end; i += 256) {
+    const int n = i / HW, p = i - n * HW;
+    const size_t off = ((size_t)n * C + c) * HW + p;
     const float xh = (x[off] - mu) * is;
     const float dz = dy[off] * act_bwd(xh * g + b + (res ? res[off] : 0.f), act);
     s += dz;
@@ -198,11 +198,12 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(
     const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res, const double *__restrict__ sums,
-    int C, int HW, long long total, long long cnt, int act, int train, float *__restrict__ dx,
+    int C, int HW, long long cnt, int act, int train, float *__restrict__ dx,
     float *__restrict__ dres) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c = (int)((i / HW) % C);
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= HW) return;
+  const int c = blockIdx.y % C;
+  const size_t i = (size_t)blockIdx.y * HW + q;
   const float mu = mean[c], is = invstd[c];
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   const float xh = (x[i] - mu) * is;
@@ -253,7 +254,8 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
                 float *running_mean, float *running_var, int N, int C, int H, int W, int train,
                 float momentum, float eps, int act, float *mean, float *invstd, float *y,
                 void *workspace, void *stream) {
-  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0, E2EP_EINVAL, "e2ep_bn_fwd: bad shape");
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && N * C <= 65535 &&
+                   (long long)N * H * W < (1LL << 31), E2EP_EINVAL, "e2ep_bn_fwd: bad shape");
   E2EP_REQUIRE(act >= 0 && act <= 2, E2EP_EINVAL, "e2ep_bn_fwd: act must be 0/1/2");
   hipStream_t s = as_stream(stream);
   const int HW = H * W;
@@ -274,9 +276,8 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
     hipLaunchKernelGGL(k_bn_eval_stats, dim3(cdiv(C, 64)), dim3(64), 0, s, running_mean, running_var,
                        C, eps, mean, invstd);
   }
-  const long long total = (long long)N * C * HW;
-  hipLaunchKernelGGL(k_bn_apply, dim3(cdiv(cdiv(total, 4), 256)), dim3(256), 0, s, x, mean, invstd,
-                     gamma, beta, res, C, HW, total, act, y);
+  hipLaunchKernelGGL(k_bn_apply, dim3(cdiv(cdiv(HW, 4), 256), N * C), dim3(256), 0, s, x, mean,
+                     invstd, gamma, beta, res, C, HW, act, y);
   return launch_status("e2ep_bn_fwd");
 }
 
@@ -284,7 +285,8 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
                 const float *gamma, const float *beta, const float *res, int N, int C, int H, int W,
                 int train, int act, float *dx, float *dgamma, float *dbeta, float *dres,
                 void *workspace, void *stream) {
-  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0, E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && N * C <= 65535 &&
+                   (long long)N * H * W < (1LL << 31), E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
   hipStream_t s = as_stream(stream);
   const int HW = H * W;
   const long long per = (long long)N * HW;
@@ -295,10 +297,9 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
                      res, N, C, HW, sp, act, part);
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(64), 0, s, part, C, sp, dgamma, dbeta,
                      sums);
-  const long long total = (long long)N * C * HW;
   if (dx || dres)
-    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(cdiv(total, 256)), dim3(256), 0, s, x, dy, mean, invstd,
-                       gamma, beta, res, sums, C, HW, total, per, act, train, dx, dres);
+    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(cdiv(HW, 256), N * C), dim3(256), 0, s, x, dy, mean,
+                       invstd, gamma, beta, res, sums, C, HW, per, act, train, dx, dres);
   return launch_status("e2ep_bn_bwd");
 }
 

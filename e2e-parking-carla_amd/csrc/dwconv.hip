@@ -15,15 +15,12 @@ template <int K>
 __global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
                                                 const float *__restrict__ w, DwGeom g,
                                                 float *__restrict__ y) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)g.N * g.C * g.P * g.Q;
-  if (i >= total) return;
-  const int ox = (int)(i % g.Q);
-  const long long r = i / g.Q;
-  const int oy = (int)(r % g.P);
-  const long long nc = r / g.P;
-  const int c = (int)(nc % g.C);
-  const float *xp = x + nc * g.H * g.W;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.P * g.Q) return;
+  const int nc = blockIdx.y;
+  const int c = nc % g.C;
+  const int oy = i / g.Q, ox = i - oy * g.Q;
+  const float *xp = x + (size_t)nc * g.H * g.W;
   const float *wp = w + c * K * K;
   const int y0 = oy * g.st - g.pt, x0 = ox * g.st - g.pl;
   float s = 0.f;
@@ -37,7 +34,7 @@ __global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
       if ((unsigned)ix < (unsigned)g.W) s += wp[a * K + b] * xp[iy * g.W + ix];
     }
   }
-  y[i] = s;
+  y[(size_t)nc * g.P * g.Q + i] = s;
 }
 
 // data gradient: one thread per input pixel, gather the outputs whose window covers it
@@ -45,15 +42,12 @@ template <int K>
 __global__ void __launch_bounds__(256) k_dw_dgrad(const float *__restrict__ gy,
                                                   const float *__restrict__ w, DwGeom g,
                                                   float *__restrict__ dx) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)g.N * g.C * g.H * g.W;
-  if (i >= total) return;
-  const int ix = (int)(i % g.W);
-  const long long r = i / g.W;
-  const int iy = (int)(r % g.H);
-  const long long nc = r / g.H;
-  const int c = (int)(nc % g.C);
-  const float *gp = gy + nc * g.P * g.Q;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= g.H * g.W) return;
+  const int nc = blockIdx.y;
+  const int c = nc % g.C;
+  const int iy = i / g.W, ix = i - iy * g.W;
+  const float *gp = gy + (size_t)nc * g.P * g.Q;
   const float *wp = w + c * K * K;
   float s = 0.f;
 #pragma unroll
@@ -70,7 +64,7 @@ __global__ void __launch_bounds__(256) k_dw_dgrad(const float *__restrict__ gy,
       if (ox * g.st == nx && ox < g.Q) s += wp[a * K + b] * gp[oy * g.Q + ox];
     }
   }
-  dx[i] = s;
+  dx[(size_t)nc * g.H * g.W + i] = s;
 }
 
 // weight gradient partials: grid (C, splits); each slice of (n, oy, ox) accumulates K*K taps
@@ -79,19 +73,19 @@ __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
                                                   const float *__restrict__ x, DwGeom g,
                                                   int splits, float *__restrict__ part) {
   const int c = blockIdx.x, sp = blockIdx.y;
-  const long long PQ = (long long)g.P * g.Q;
-  const long long tot = (long long)g.N * PQ;
-  const long long per = (tot + splits - 1) / splits;
-  const long long beg = sp * per, end = min(tot, beg + per);
+  const int PQ = g.P * g.Q;
+  const int tot = g.N * PQ;
+  const int per = (tot + splits - 1) / splits;
+  const int beg = sp * per, end = min(tot, beg + per);
   float acc[K * K];
 #pragma unroll
   for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
-  for (long long i = beg + threadIdx.x; i < end; i += 256) {
-    const long long n = i / PQ;
-    const int pix = (int)(i - n * PQ);
+  for (int i = beg + threadIdx.x; i < end; i += 256) {
+    const int n = i / PQ;
+    const int pix = i - n * PQ;
     const int oy = pix / g.Q, ox = pix - oy * g.Q;
-    const float gv = gy[(n * g.C + c) * PQ + pix];
-    const float *xp = x + (n * g.C + c) * g.H * g.W;
+    const float gv = gy[((size_t)n * g.C + c) * PQ + pix];
+    const float *xp = x + ((size_t)n * g.C + c) * g.H * g.W;
     const int y0 = oy * g.st - g.pt, x0 = ox * g.st - g.pl;
 #pragma unroll
     for (int a = 0; a < K; ++a) {
@@ -164,8 +158,8 @@ int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, float *y, v
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_fwd: bad geometry");
-  const long long total = (long long)g.N * g.C * g.P * g.Q;
-  DW_DISPATCH(k_dw_fwd, dim3(cdiv(total, 256)), x, w, g, y);
+  E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_fwd: N*C > 65535");
+  DW_DISPATCH(k_dw_fwd, dim3(cdiv(g.P * g.Q, 256), g.N * g.C), x, w, g, y);
   return launch_status("e2ep_dwconv_fwd");
 }
 
@@ -173,8 +167,8 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_dgrad: bad geometry");
-  const long long total = (long long)g.N * g.C * g.H * g.W;
-  DW_DISPATCH(k_dw_dgrad, dim3(cdiv(total, 256)), gy, w, g, dx);
+  E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_dgrad: N*C > 65535");
+  DW_DISPATCH(k_dw_dgrad, dim3(cdiv(g.H * g.W, 256), g.N * g.C), gy, w, g, dx);
   return launch_status("e2ep_dwconv_dgrad");
 }
 

@@ -28,34 +28,32 @@ __device__ __forceinline__ Tap tap(int o, float scale, int In) {
   return t;
 }
 
-__global__ void __launch_bounds__(256) k_resize_fwd(const float *__restrict__ x, int planes, int Hi,
-                                                    int Wi, int Ho, int Wo, float sh, float sw,
-                                                    float *__restrict__ y, long long y_pstride) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)planes * Ho * Wo;
-  if (i >= total) return;
-  const int ow = (int)(i % Wo);
-  const long long r = i / Wo;
-  const int oh = (int)(r % Ho);
-  const long long pl = r / Ho;
+// grid (ceil(Ho*Wo/256), planes); plane pl = n*C + c reads x + n*x_nstride + c*Hi*Wi and
+// writes y + n*y_nstride + c*Ho*Wo (so channel slices of bigger tensors need no copy)
+__global__ void __launch_bounds__(256) k_resize_fwd(const float *__restrict__ x, int C,
+                                                    long long x_nstride, int Hi, int Wi, int Ho,
+                                                    int Wo, float sh, float sw, float *__restrict__ y,
+                                                    long long y_nstride) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Ho * Wo) return;
+  const int pl = blockIdx.y;
+  const int n = pl / C, c = pl - n * C;
+  const int oh = i / Wo, ow = i - oh * Wo;
   const Tap th = tap(oh, sh, Hi), tw = tap(ow, sw, Wi);
-  const float *p = x + pl * Hi * Wi;
+  const float *p = x + n * x_nstride + (long long)c * Hi * Wi;
   const float v = th.l0 * (tw.l0 * p[th.i0 * Wi + tw.i0] + tw.l1 * p[th.i0 * Wi + tw.i1]) +
                   th.l1 * (tw.l0 * p[th.i1 * Wi + tw.i0] + tw.l1 * p[th.i1 * Wi + tw.i1]);
-  y[pl * y_pstride + (long long)oh * Wo + ow] = v;
+  y[n * y_nstride + (long long)c * Ho * Wo + i] = v;
 }
 
 // backward pass 1 (along W): t[pl, oh, j] = sum_{ow} w(ow -> j) g[pl, oh, ow]
 __global__ void __launch_bounds__(256) k_resize_bwd_w(const float *__restrict__ g, long long g_pstride,
                                                       int planes, int Ho, int Wo, int Wi, float sw,
                                                       float *__restrict__ t) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)planes * Ho * Wi;
-  if (i >= total) return;
-  const int j = (int)(i % Wi);
-  const long long r = i / Wi;  // pl * Ho + oh
-  const long long pl = r / Ho;
-  const int oh = (int)(r - pl * Ho);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Ho * Wi) return;
+  const int pl = blockIdx.y;
+  const int oh = i / Wi, j = i - oh * Wi;
   const float *gr = g + pl * g_pstride + (long long)oh * Wo;
   // outputs touching source j lie in a window around j / sw; recompute each tap exactly
   const float inv = 1.f / sw;
@@ -69,21 +67,19 @@ __global__ void __launch_bounds__(256) k_resize_bwd_w(const float *__restrict__ 
     if (tw.i0 == j) s += tw.l0 * gr[o];
     if (tw.i1 == j) s += tw.l1 * gr[o];
   }
-  t[i] = s;
+  t[(long long)pl * Ho * Wi + i] = s;
 }
 
 // backward pass 2 (along H): gx[pl, i, j] = sum_{oh} w(oh -> i) t[pl, oh, j]
 __global__ void __launch_bounds__(256) k_resize_bwd_h(const float *__restrict__ t, int planes, int Ho,
                                                       int Hi, int Wi, float sh,
                                                       float *__restrict__ gx, int accumulate) {
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)planes * Hi * Wi;
-  if (idx >= total) return;
-  const int j = (int)(idx % Wi);
-  const long long r = idx / Wi;
-  const long long pl = r / Hi;
-  const int i = (int)(r - pl * Hi);
-  const float *tp = t + pl * Ho * Wi + j;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Hi * Wi) return;
+  const int pl = blockIdx.y;
+  const int i = q / Wi, j = q - i * Wi;
+  const long long idx = (long long)pl * Hi * Wi + q;
+  const float *tp = t + (long long)pl * Ho * Wi + j;
   const float inv = 1.f / sh;
   int lo = (int)floorf(((float)i - 0.5f) * inv - 0.5f) - 2;
   int hi = (int)ceilf(((float)i + 1.5f) * inv - 0.5f) + 2;
@@ -104,13 +100,13 @@ using namespace e2ep;
 
 extern "C" {
 
-int e2ep_resize_fwd(const float *x, int planes, int Hi, int Wi, int Ho, int Wo, float scale_h,
-                    float scale_w, float *y, long long y_pstride, void *stream) {
-  E2EP_REQUIRE(planes > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, E2EP_EINVAL,
-               "e2ep_resize_fwd: bad shape");
-  const long long total = (long long)planes * Ho * Wo;
-  hipLaunchKernelGGL(k_resize_fwd, dim3(cdiv(total, 256)), dim3(256), 0, as_stream(stream), x, planes,
-                     Hi, Wi, Ho, Wo, scale_h, scale_w, y, y_pstride);
+int e2ep_resize_fwd(const float *x, int N, int C, long long x_nstride, int Hi, int Wi, int Ho,
+                    int Wo, float scale_h, float scale_w, float *y, long long y_nstride,
+                    void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && N * C <= 65535,
+               E2EP_EINVAL, "e2ep_resize_fwd: bad shape");
+  hipLaunchKernelGGL(k_resize_fwd, dim3(cdiv(Ho * Wo, 256), N * C), dim3(256), 0, as_stream(stream),
+                     x, C, x_nstride, Hi, Wi, Ho, Wo, scale_h, scale_w, y, y_nstride);
   return launch_status("e2ep_resize_fwd");
 }
 
@@ -125,12 +121,10 @@ int e2ep_resize_bwd(const float *g, long long g_pstride, int planes, int Hi, int
                "e2ep_resize_bwd: bad shape");
   hipStream_t s = as_stream(stream);
   float *t = static_cast<float *>(workspace);
-  const long long n1 = (long long)planes * Ho * Wi;
-  hipLaunchKernelGGL(k_resize_bwd_w, dim3(cdiv(n1, 256)), dim3(256), 0, s, g, g_pstride, planes, Ho,
-                     Wo, Wi, scale_w, t);
-  const long long n2 = (long long)planes * Hi * Wi;
-  hipLaunchKernelGGL(k_resize_bwd_h, dim3(cdiv(n2, 256)), dim3(256), 0, s, t, planes, Ho, Hi, Wi,
-                     scale_h, gx, accumulate);
+  hipLaunchKernelGGL(k_resize_bwd_w, dim3(cdiv(Ho * Wi, 256), planes), dim3(256), 0, s, g, g_pstride,
+                     planes, Ho, Wo, Wi, scale_w, t);
+  hipLaunchKernelGGL(k_resize_bwd_h, dim3(cdiv(Hi * Wi, 256), planes), dim3(256), 0, s, t, planes, Ho,
+                     Hi, Wi, scale_h, gx, accumulate);
   return launch_status("e2ep_resize_bwd");
 }
 

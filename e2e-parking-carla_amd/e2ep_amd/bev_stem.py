@@ -1,0 +1,74 @@
+"""BEV-encoder stem as one autograd op: bilinear 200->256 of the 64 pooled BEV channels and
+the target-point plane, then conv7x7/2 (65->64) — reference model/bev_encoder.py:24-27.
+
+Forward writes the two resizes straight into one (B, 65, 256, 256) buffer (no torch.cat of
+the target channel, reference model/parking_model.py:45).  Backward computes the data
+gradient for the 64 feature channels only (the target plane is a constant), resizes it
+back to 200x200 with the deterministic gather, and the weight gradient with the split-K
+kernel."""
+import torch
+
+from . import _lib, conv, timing
+
+
+class _BevStem(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, bev, tgt, w, size):
+        B, C, X, Y = bev.shape
+        H, W = size
+        assert bev.stride(3) == 1 and bev.stride(2) == Y and bev.stride(1) == X * Y
+        tgt = tgt.contiguous()
+        Cin = C + 1
+        x = torch.empty(B, Cin, H, W, dtype=torch.float32, device=bev.device)
+        s = _lib.stream()
+        sh, sw = X / H, Y / W
+        with timing.region("resize_fwd"):
+            _lib.call("e2ep_resize_fwd", _lib.ptr(bev), B, C, bev.stride(0), X, Y, H, W, sh, sw,
+                      _lib.ptr(x), Cin * H * W, s)
+            _lib.call("e2ep_resize_fwd", _lib.ptr(tgt), B, 1, X * Y, X, Y, H, W, sh, sw,
+                      _lib.ptr(x[:, C:]), Cin * H * W, s)
+        Cout, _, R, S = w.shape
+        P, Q = (H + 6 - R) // 2 + 1, (W + 6 - S) // 2 + 1
+        dims = (B, Cin, H, W, Cout, R, S, P, Q, 2, 2, 3, 3, 1, 1)
+        y = torch.empty(B, Cout, P, Q, dtype=torch.float32, device=bev.device)
+        with timing.region("conv_fwd"):
+            _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w.contiguous()), None,
+                      _lib.ptr(conv._table(dims, 0, x.device)), _lib.dims(dims), 0, _lib.ptr(y), s)
+        ctx.save_for_backward(x, w)
+        ctx.meta = (B, C, X, Y, H, W, sh, sw, dims)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        B, C, X, Y, H, W, sh, sw, dims = ctx.meta
+        gy = gy.contiguous()
+        s = _lib.stream()
+        d = _lib.dims(dims)
+        dbev = dw = None
+        if ctx.needs_input_grad[0]:
+            dres = torch.empty(B, C, H, W, dtype=torch.float32, device=gy.device)
+            with timing.region("conv_dgrad"):
+                _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w.contiguous()),
+                          _lib.ptr(conv._table(dims, 1, gy.device)), d, C, _lib.ptr(dres), s)
+            dbev = torch.empty(B, C, X, Y, dtype=torch.float32, device=gy.device)
+            ws = torch.empty(B * C * H * Y, dtype=torch.float32, device=gy.device)
+            with timing.region("resize_bwd"):
+                _lib.call("e2ep_resize_bwd", _lib.ptr(dres), H * W, B * C, X, Y, H, W, sh, sw,
+                          _lib.ptr(dbev), 0, _lib.ptr(ws), s)
+        if ctx.needs_input_grad[2]:
+            splits = _lib.load().e2ep_conv_wgrad_splits(d)
+            ws = torch.empty(splits * w.numel(), dtype=torch.float32, device=gy.device)
+            dw = torch.empty_like(w)
+            with timing.region("conv_wgrad"):
+                _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x),
+                          _lib.ptr(conv._table(dims, 0, gy.device)), d, splits, _lib.ptr(ws),
+                          _lib.ptr(dw), 0, s)
+        return dbev, None, dw, None
+
+
+def bev_stem(bev, tgt, weight, size=(256, 256)):
+    """conv7x7/2(resize(cat(bev, tgt)))  with bev (B,C,X,Y) [grad], tgt (B,1,X,Y) [const]."""
+    if not bev.is_cuda:
+        raise _lib.E2EPError("e2ep bev_stem runs on a HIP device only")
+    return _BevStem.apply(bev, tgt.detach(), weight, tuple(size))

@@ -1,9 +1,10 @@
 """Convolution autograd op over the e2ep implicit-GEMM kernels (csrc/conv.hip).
 
-conv2d(x, w, b, stride, padding(l,r,t,b), dilation, act) -> y, with backward through
-e2ep_conv_dgrad / e2ep_conv_wgrad / e2ep_bias_grad.  groups must be 1 (depthwise convs use
-e2ep_amd.dwconv).  The im2col k-tables are built once per geometry on the device and cached.
-"""
+conv2d(x, w, b, stride, padding(l,r,t,b), dilation, act, grad_channels) -> y, backward via
+e2ep_conv_dgrad (stride-phase tables) / e2ep_conv_wgrad (split pixel reduction) /
+e2ep_bias_grad.  1x1 convs on 1x1 maps run on e2ep_skinny_gemm.  groups must be 1
+(depthwise convs use e2ep_amd.nn_ops).  `grad_channels` limits the input gradient to the
+first channels (the BEV encoder's target-point channel is a constant: no gradient)."""
 import torch
 
 from . import _lib, timing
@@ -15,26 +16,17 @@ def _table(dims, dgrad, device):
     key = (tuple(dims), dgrad, str(device))
     t = _TABLES.get(key)
     if t is None:
-        n = (dims[4] if dgrad else dims[1]) * dims[5] * dims[6]
-        t = torch.empty(n * 4, dtype=torch.int32, device=device)
         d = _lib.dims(dims)
+        nbytes = _lib.load().e2ep_conv_table_bytes(d, int(dgrad))
+        t = torch.empty(max(nbytes // 4, 4), dtype=torch.int32, device=device)
         _lib.call("e2ep_conv_table", d, int(dgrad), _lib.ptr(t), _lib.stream())
         _TABLES[key] = t
     return t
 
 
-def _splits(dims):
-    N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
-    Kg = Cin * R * S
-    base = -(-Kg // 128) * -(-Cout // 64)
-    pix = N * P * Q
-    want = max(1, -(-512 // base))
-    return int(max(1, min(want, pix // 256, 64)))
-
-
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, dims, act):
+    def forward(ctx, x, w, b, dims, act, grad_channels):
         x = x.contiguous()
         w = w.contiguous()
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
@@ -43,7 +35,7 @@ class _Conv2d(torch.autograd.Function):
         with timing.region("conv_fwd"):
             _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b),
                       _lib.ptr(_table(dims, 0, x.device)), d, act, _lib.ptr(y), _lib.stream())
-        ctx.dims, ctx.act, ctx.has_bias = dims, act, b is not None
+        ctx.dims, ctx.act, ctx.has_bias, ctx.gc = dims, act, b is not None, grad_channels
         ctx.save_for_backward(x, w, y if act else None)
         return y
 
@@ -59,12 +51,18 @@ class _Conv2d(torch.autograd.Function):
         s = _lib.stream()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
+            gc = ctx.gc or Cin
+            dxg = torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device)
             with timing.region("conv_dgrad"):
                 _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w),
-                          _lib.ptr(_table(dims, 1, x.device)), d, _lib.ptr(dx), s)
+                          _lib.ptr(_table(dims, 1, x.device)), d, gc, _lib.ptr(dxg), s)
+            if gc == Cin:
+                dx = dxg
+            else:
+                dx = torch.zeros_like(x)
+                dx[:, :gc] = dxg
         if ctx.needs_input_grad[1]:
-            splits = _splits(dims)
+            splits = _lib.load().e2ep_conv_wgrad_splits(d)
             ws = torch.empty(splits * Cout * Cin * R * S, dtype=torch.float32, device=x.device)
             dw = torch.empty_like(w)
             with timing.region("conv_wgrad"):
@@ -74,10 +72,51 @@ class _Conv2d(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = torch.empty(Cout, dtype=torch.float32, device=x.device)
             _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db), s)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
-def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0):
+def _skinny(A, ai, ak, B, bk, bj, bias, Mi, Nj, K, out):
+    _lib.call("e2ep_skinny_gemm", _lib.ptr(A), ai, ak, _lib.ptr(B), bk, bj, _lib.ptr(bias), Mi, Nj,
+              K, _lib.ptr(out), _lib.stream())
+    return out
+
+
+class _Linear1x1(torch.autograd.Function):
+    """1x1 conv on a 1x1 map == linear layer y[n, m] = sum_k W[m, k] x[n, k] + b[m]."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        N, K = x.shape[0], x.shape[1]
+        M = w.shape[0]
+        x2 = x.reshape(N, K).contiguous()
+        w2 = w.reshape(M, K).contiguous()
+        y = torch.empty(N, M, dtype=torch.float32, device=x.device)
+        _skinny(x2, K, 1, w2, 1, K, b, N, M, K, y)
+        ctx.save_for_backward(x2, w2)
+        ctx.has_bias, ctx.wshape, ctx.xshape = b is not None, w.shape, x.shape
+        return y.view(N, M, 1, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w2 = ctx.saved_tensors
+        N, K = x2.shape
+        M = w2.shape[0]
+        g = gy.reshape(N, M).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _skinny(g, M, 1, w2, K, 1, None, N, K, M,
+                         torch.empty(N, K, dtype=torch.float32, device=g.device)).view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = _skinny(g, 1, M, x2, K, 1, None, M, K, N,
+                         torch.empty(M, K, dtype=torch.float32, device=g.device)).view(ctx.wshape)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            ones = torch.ones(N, dtype=torch.float32, device=g.device)
+            db = _skinny(ones, 0, 1, g, M, 1, None, 1, M, N,
+                         torch.empty(M, dtype=torch.float32, device=g.device))
+        return dx, dw, db
+
+
+def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0, grad_channels=None):
     """pad = (left, right, top, bottom); act 0 none, 1 relu (fused epilogue)."""
     if not x.is_cuda:
         raise _lib.E2EPError("e2ep conv2d runs on a HIP device only")
@@ -85,10 +124,12 @@ def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0
     Cout, cin_w, R, S = w.shape
     if cin_w != Cin:
         raise _lib.E2EPError(f"e2ep conv2d: groups must be 1 (w {tuple(w.shape)}, x {tuple(x.shape)})")
+    if H == 1 and W == 1 and R == 1 and S == 1 and act == 0 and not any(pad) and grad_channels is None:
+        return _Linear1x1.apply(x, w, b)
     sh, sw = stride
     dh, dw = dilation
     l, r, t, btm = pad
     P = (H + t + btm - dh * (R - 1) - 1) // sh + 1
     Q = (W + l + r - dw * (S - 1) - 1) // sw + 1
     dims = (N, Cin, H, W, Cout, R, S, P, Q, sh, sw, t, l, dh, dw)
-    return _Conv2d.apply(x, w, b, dims, act)
+    return _Conv2d.apply(x, w, b, dims, act, grad_channels)

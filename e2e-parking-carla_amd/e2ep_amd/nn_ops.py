@@ -108,8 +108,8 @@ class _Resize(torch.autograd.Function):
         N, C, Hi, Wi = x.shape
         y = torch.empty(N, C, Ho, Wo, dtype=torch.float32, device=x.device)
         with timing.region("resize_fwd"):
-            _lib.call("e2ep_resize_fwd", _lib.ptr(x), N * C, Hi, Wi, Ho, Wo, sh, sw, _lib.ptr(y),
-                      Ho * Wo, _lib.stream())
+            _lib.call("e2ep_resize_fwd", _lib.ptr(x), N, C, C * Hi * Wi, Hi, Wi, Ho, Wo, sh, sw,
+                      _lib.ptr(y), C * Ho * Wo, _lib.stream())
         ctx.meta = (N, C, Hi, Wi, Ho, Wo, sh, sw)
         return y
 

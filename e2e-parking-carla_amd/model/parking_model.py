@@ -48,14 +48,15 @@ class ParkingModel(nn.Module):
         target_point = data["target_point"].to(dev, non_blocking=True)
         ego_motion = data["ego_motion"].to(dev, non_blocking=True)
         b = images.shape[0]
-        # lift-splat into channels [0,64); target plane into channel 64 (fused concat)
         bev, pred_depth = self.bev_model.calc_bev_feature(images, data["intrinsics"],
-                                                          data["extrinsics"], extra_channels=1)
-        c = bev.shape[1] - 1
-        lss.target_bev(bev, c, target_point, self._noise(b, dev, noise),
+                                                          data["extrinsics"])
+        # target plane (model/parking_model.py:28-46) as its own constant tensor; the BEV
+        # encoder stem consumes (bev, target) without materialising their concatenation
+        X, Y = bev.shape[-2:]
+        bev_target = torch.empty((b, 1, X, Y), dtype=torch.float32, device=dev)
+        lss.target_bev(bev_target, 0, target_point, self._noise(b, dev, noise),
                        self.cfg.bev_x_bound[2], self.cfg.bev_y_bound[2])
-        bev_target = bev[:, c:].detach()
-        bev_down_sample = self.bev_encoder(bev)
+        bev_down_sample = self.bev_encoder.forward_split(bev, bev_target)
         fuse_feature = self.feature_fusion(bev_down_sample, ego_motion)
         pred_segmentation = self.segmentation_head(fuse_feature)
         return fuse_feature, pred_segmentation, pred_depth, bev_target

@@ -117,26 +117,37 @@ int e2ep_target_bev(const float *target_point, const float *noise, int B, int X,
  * a bigger P/Q with implicit zero rows/cols at the bottom/right).  groups == 1.
  * ------------------------------------------------------------------------------------- */
 
-/* Build the per-conv im2col k-table (int4[Cin*R*S], or int4[Cout*R*S] when dgrad != 0). */
+/* Build the per-conv im2col k-table (e2ep_conv_table_bytes bytes).  dgrad != 0 builds the
+ * stride-phase tables of the data gradient (only taps that land on an integral output
+ * coordinate for each input-pixel phase). */
+size_t e2ep_conv_table_bytes(const int *dims, int dgrad);
 int e2ep_conv_table(const int *dims, int dgrad, void *table, void *stream);
 
 /* y[N,Cout,P,Q] = conv(x[N,Cin,H,W], w[Cout,Cin,R,S]) + bias (nullable); act 0 none, 1 relu. */
 int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const void *table,
                   const int *dims, int act, float *y, void *stream);
 
-/* dx[N,Cin,H,W] = conv_transpose(gout[N,Cout,P,Q], w)   (table built with dgrad = 1). */
+/* dx[N,m_channels,H,W] = conv_transpose(gout[N,Cout,P,Q], w) restricted to the first
+ * m_channels input channels (table built with dgrad = 1); no zero taps at stride 2. */
 int e2ep_conv_dgrad(const float *gout, const float *w, const void *table, const int *dims,
-                    float *dx, void *stream);
+                    int m_channels, float *dx, void *stream);
 
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of
  * e2ep_conv_wgrad_workspace bytes) are summed in a fixed order: deterministic. */
+int e2ep_conv_wgrad_splits(const int *dims);
 size_t e2ep_conv_wgrad_workspace(const int *dims, int splits);
 int e2ep_conv_wgrad(const float *gout, const float *x, const void *table, const int *dims,
                     int splits, void *workspace, float *dw, int accumulate, void *stream);
 
 /* db[C] = sum over (n, p) of gout[N, C, HW]. */
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream);
+
+/* Skinny GEMM for tiny outputs: C[i*Nj + j] = sum_k A[i*ai + k*ak] * B[k*bk + j*bj]
+ * (+ bias[j]); one wave per output.  1x1 convs on 1x1 maps (squeeze-excitation) and small
+ * linears, forward and backward, via strides. */
+int e2ep_skinny_gemm(const float *A, int ai, int ak, const float *B, int bk, int bj,
+                     const float *bias, int Mi, int Nj, int K, float *C, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * BatchNorm2d + activation (+ residual), NCHW fp32.
@@ -166,8 +177,11 @@ int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *d
  * Replaces model/bev_encoder.py:24, model/segmentation_head.py:35-38,
  * model/convolutions.py:197,238-240.  Backward is a deterministic two-pass gather.
  * ------------------------------------------------------------------------------------- */
-int e2ep_resize_fwd(const float *x, int planes, int Hi, int Wi, int Ho, int Wo, float scale_h,
-                    float scale_w, float *y, long long y_pstride, void *stream);
+/* forward over N*C planes; plane (n, c) reads x + n*x_nstride + c*Hi*Wi and writes
+ * y + n*y_nstride + c*Ho*Wo, so channel slices of larger tensors are read/written in place. */
+int e2ep_resize_fwd(const float *x, int N, int C, long long x_nstride, int Hi, int Wi, int Ho,
+                    int Wo, float scale_h, float scale_w, float *y, long long y_nstride,
+                    void *stream);
 size_t e2ep_resize_bwd_workspace(int planes, int Ho, int Wi);
 int e2ep_resize_bwd(const float *g, long long g_pstride, int planes, int Hi, int Wi, int Ho,
                     int Wo, float scale_h, float scale_w, float *gx, int accumulate,

@@ -131,3 +131,25 @@ def test_maxpool_avgpool_segate():
     o64 = x64 * torch.sigmoid(a64) + x64.mean((2, 3), keepdim=True)
     o64.backward(dy.double())
     assert rel_l2(out, o64) < 1e-6 and rel_l2(xd.grad, x64.grad) < 1e-6 and rel_l2(ad.grad, a64.grad) < 1e-6
+
+
+def test_bev_stem_resize_conv_fused():
+    """bev_stem(bev, tgt, w) == conv7x7/2(resize(cat(bev, tgt))) with grads for bev and w."""
+    from e2ep_amd import bev_stem
+    g = _g(77)
+    bev = torch.randn(2, 64, 50, 50, generator=g)
+    tgt = (torch.rand(2, 1, 50, 50, generator=g) > 0.9).float()
+    w = torch.randn(64, 65, 7, 7, generator=g) / (65 * 49) ** 0.5
+    bd = bev.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    y = bev_stem.bev_stem(bd, tgt.to(DEV), wd, (64, 64))
+    gy = torch.randn(y.shape, generator=g)
+    y.backward(gy.to(DEV))
+    b64 = bev.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    x = F.interpolate(torch.cat([b64, tgt.double()], 1), size=(64, 64), mode="bilinear", align_corners=False)
+    y64 = F.conv2d(x, w64, None, 2, 3)
+    y64.backward(gy.double())
+    assert rel_l2(y, y64) < 2e-5
+    assert rel_l2(bd.grad, b64.grad) < 2e-5
+    assert rel_l2(wd.grad, w64.grad) < 2e-5
