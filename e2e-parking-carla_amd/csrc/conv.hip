@@ -1,9 +1,9 @@
 // NCHW fp32 convolution for gfx950 as implicit GEMM on the exact-f32 matrix cores
 // (v_mfma_f32_32x32x2_f32: f32 in, f32 accumulate, bitwise an fmaf chain).
 //
-//   forward      y[n,co,p]  = sum_k W[co,k] * xcol[k,(n,p)]            M=Cout N=n*P*Q K=Cin*R*S
-//   bwd-data     dx[n,ci,p] = sum_k W'[ci,k] * gcol[k,(n,p)]           M=Cin  N=n*H*W K=Cout*R*S
-//   bwd-weight   dW[co,k]   = sum_(n,p) g[n,co,p] * xcol[k,(n,p)]      M=Cout N=Cin*R*S K=n*P*Q
+//   forward      y[n,co,p]  = sum_(tap,ci) W[co,ci,tap] * x[n,ci,p+tap]       M=Cout  N=n*P*Q
+//   bwd-data     dx[n,ci,p] = sum_(tap,co) W[co,ci,tap] * g[n,co,(p-tap)/s]   M=Cin   N=n*H*W
+//   bwd-weight   dW[co,ci,tap] = sum_(n,p) g[n,co,p] * x[n,ci,p+tap]         M=Cout  N=taps*Cin
 //
 // Every conv of the hot path uses these kernels: BEV encoder (conv7x7/2 + ResNet-18 layers
 // 1-3), segmentation head, DeepLab/ASPP heads, UpsamplingConcat, EfficientNet 1x1
@@ -12,17 +12,17 @@
 // MBConv).  1x1 convs on 1x1 maps (squeeze-excitation) use the skinny-GEMM kernel at the end;
 // depthwise convs have their own memory-bound kernels (dwconv.hip).
 //
-// Tiling: 256 threads = 4 waves (2 x 2); block tile 64 (M) x BNT (N, 64 or 128), K-step 16,
-// each wave 32 x BNT/2 (one or two 32x32 accumulators sharing the A fragment).  A and B are
-// staged global -> registers -> LDS (double buffered, one barrier per K-step).  The im2col
-// gather is driven by per-conv k-tables (int4 {b_off, dy, dx, a_off}) built once on the
-// device, so the inner loop has no integer division:
-//   fwd:   iy = oy*sh - ph + dy,  ix = ox*sw - pw + dx
-//   dgrad: split by input-pixel phase (iy % sh, ix % sw); only the taps whose output
-//          coordinate is integral for that phase are in the phase's table, and
-//          qy = u + dy, qx = v + dx  (iy = py + sh*u) -- no zero taps at stride 2.
-// bwd-weight splits the pixel reduction over blocks and sums the fp32 partial slabs in a
-// fixed order: results are run-to-run deterministic.
+// K order is tap-outer / channel-inner: one K-step = one filter tap x 16 channels, so the
+// im2col bounds test is done once per pixel per K-step (not per element), channel rows are
+// a fixed stride apart, and no lookup table is needed.  The data gradient is split by
+// input-pixel phase (iy % sh, ix % sw): each phase only visits the taps that land on an
+// integral output coordinate (no zero taps at stride 2).
+//
+// Tiling: 256 threads = 4 waves (2 x 2); block tile 64 (M) x BNT (N, 64 or 128), each wave
+// 32 x BNT/2 (one or two 32x32 accumulators sharing the A fragment).  A and B are staged
+// global -> registers -> LDS (double buffered, one barrier per K-step) with branch-free
+// buffer loads (out-of-range offset -> 0).  Small grids split K; partial slabs are reduced
+// in a fixed order, so every result is run-to-run deterministic.
 #include <algorithm>
 
 #include "common.h"
@@ -31,9 +31,25 @@ namespace e2ep {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Branch-free guarded memory access: an invalid element gets an out-of-range byte offset,
+// which the buffer unit turns into a 0 load / a dropped store.  Descriptors are built from
+// kernel arguments only (wave-uniform: no waterfall loops).
+constexpr int OOR = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, long long bytes) {
+  const int nr = bytes >= 0x7fffffff ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, nr, 0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 0);
+}
+
 constexpr int BM = 64, BK = 16;
 constexpr int PADA = 4, PADB = 4;
 constexpr int MAXPH = 4;
+constexpr int MAXTAPS = 64;
 
 struct ConvGeom {
   int N;            // images
@@ -43,83 +59,94 @@ struct ConvGeom {
   int sh, sw, ph, pw, dh, dw;
 };
 
-struct Phases {  // dgrad phase decomposition
-  int n;
-  int py[MAXPH], px[MAXPH];     // phase offsets
-  int Hp[MAXPH], Wp[MAXPH];     // pixels of the phase
-  int k0[MAXPH], kn[MAXPH];     // table slice
-};
-
-// ------------------------------------------------------------------------------------------
-// k-tables
-// ------------------------------------------------------------------------------------------
-__global__ void k_conv_table_fwd(ConvGeom g, int4 *__restrict__ tab, int Kg) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= Kg) return;
-  const int RS = g.R * g.S;
-  const int c = k / RS, rs = k - c * RS, r = rs / g.S, s = rs - r * g.S;
-  tab[k] = make_int4(c * g.H * g.W, r * g.dh, s * g.dw, k);
-}
-
-// dgrad table of one phase (py, px): taps whose output coordinate is integral
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
-__global__ void k_conv_table_dgrad(ConvGeom g, int py, int px, int4 *__restrict__ tab) {
-  // single thread: deterministic compaction (tables are tiny and built once per geometry)
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int n = 0;
-  const int RS = g.R * g.S;
-  for (int co = 0; co < g.Cout; ++co)
-    for (int r = 0; r < g.R; ++r) {
-      const int ny = py + g.ph - r * g.dh;
-      if (((ny % g.sh) + g.sh) % g.sh) continue;
-      for (int s = 0; s < g.S; ++s) {
-        const int nx = px + g.pw - s * g.dw;
-        if (((nx % g.sw) + g.sw) % g.sw) continue;
-        tab[n++] = make_int4(co * g.P * g.Q, floordiv(ny, g.sh), floordiv(nx, g.sw),
-                             co * g.Cin * RS + r * g.S + s);
-      }
-    }
-}
-
 // ------------------------------------------------------------------------------------------
-// forward / bwd-data GEMM
+// forward (MODE 0) / data-gradient (MODE 1) implicit GEMM
 // ------------------------------------------------------------------------------------------
+// MODE 0: rows m = co, K channels c = ci, src = x [N,Cin,H,W], dst = y [N,Cout,P,Q];
+//         column pixel (oy,ox); tap (r,s): iy = oy*sh - ph + r*dh, ix = ox*sw - pw + s*dw.
+// MODE 1: rows m = ci, K channels c = co, src = g [N,Cout,P,Q], dst = dx [N,Cin,H,W];
+//         phase z = (py, px), column pixel (u,v) -> (iy, ix) = (py + sh*u, px + sw*v);
+//         tap (r,s) valid for the phase: qy = u + (py + ph - r*dh)/sh (exact), qx likewise.
 template <int MODE, int ACT, int BNT>
 __global__ void __launch_bounds__(256, 2) k_conv_gemm(
-    const float *__restrict__ A, int a_row_stride, const float *__restrict__ src,
-    const int4 *__restrict__ tab_all, const float *__restrict__ bias, float *__restrict__ dst,
-    ConvGeom g, int M, int Kfwd, Phases ph) {
+    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
+    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
   constexpr int NACC = BNT / 64;
+  constexpr int BROWS = 256 / BNT;  // B rows per pass (2 or 4)
+  constexpr int BPER = BK / BROWS;  // B loads per thread (8 or 4)
   __shared__ float As[2][BK][BM + PADA];
   __shared__ float Bs[2][BK][BNT + PADB];
+  __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
+  __shared__ int s_ntaps;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BNT;
+  const int split = blockIdx.z % splits, z = blockIdx.z / splits;
+  const int RS = g.R * g.S;
 
-  // phase (dgrad) or the single forward "phase"
-  int py = 0, px = 0, Hc, Wc, Kg;
-  const int4 *tab;
+  // phase / pixel space of the columns
+  int py = 0, px = 0, Hc, Wc;
   if (MODE == 0) {
-    Hc = g.P; Wc = g.Q; Kg = Kfwd; tab = tab_all;
+    Hc = g.P; Wc = g.Q;
   } else {
-    const int z = blockIdx.z;
-    py = ph.py[z]; px = ph.px[z]; Hc = ph.Hp[z]; Wc = ph.Wp[z];
-    Kg = ph.kn[z]; tab = tab_all + ph.k0[z];
+    py = z / g.sw; px = z % g.sw;
+    Hc = py < g.H ? (g.H - py + g.sh - 1) / g.sh : 0;
+    Wc = px < g.W ? (g.W - px + g.sw - 1) / g.sw : 0;
   }
-  const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;  // dst spatial
-  const int Hs = MODE == 0 ? g.H : g.P, Ws = MODE == 0 ? g.W : g.Q;  // src spatial
-  const int Cs = MODE == 0 ? g.Cin : g.Cout;
   const int HWc = Hc * Wc;
   const int Ntot = g.N * HWc;
   if (n0 >= Ntot) return;
 
-  // this thread's B-load column (constant over the K loop)
-  constexpr int BROWS = 256 / BNT;          // rows loaded per pass (2 or 4)
-  constexpr int BPER = BK / BROWS;          // loads per thread (8 or 4)
+  // tap table of this phase (tiny; built by one thread)
+  if (tid == 0) {
+    int n = 0;
+    for (int r = 0; r < g.R; ++r) {
+      int dy;
+      if (MODE == 0) {
+        dy = r * g.dh - g.ph;
+      } else {
+        const int ny = py + g.ph - r * g.dh;
+        if (((ny % g.sh) + g.sh) % g.sh) continue;
+        dy = floordiv(ny, g.sh);
+      }
+      for (int s = 0; s < g.S; ++s) {
+        int dx;
+        if (MODE == 0) {
+          dx = s * g.dw - g.pw;
+        } else {
+          const int nx = px + g.pw - s * g.dw;
+          if (((nx % g.sw) + g.sw) % g.sw) continue;
+          dx = floordiv(nx, g.sw);
+        }
+        s_tdy[n] = dy;
+        s_tdx[n] = dx;
+        s_trs[n] = r * g.S + s;
+        ++n;
+      }
+    }
+    s_ntaps = n;
+  }
+  __syncthreads();
+  const int ntaps = s_ntaps;
+  const int Kc = MODE == 0 ? g.Cin : g.Cout;  // channels summed per tap
+  const int csteps = (Kc + BK - 1) / BK;
+  const int ksteps_all = ntaps * csteps;
+  const int kbeg = split * kper;
+  const int kend = min(ksteps_all, kbeg + kper);
+  const int nk = max(0, kend - kbeg);
+
+  const int Hs = MODE == 0 ? g.H : g.P, Ws = MODE == 0 ? g.W : g.Q;  // src spatial
+  const int HWs = Hs * Ws;
+  const __amdgpu_buffer_rsrc_t rw = rsrc(w, 4LL * g.Cout * g.Cin * RS);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(src, 4LL * g.N * Kc * HWs);
+
+  // B-load column of this thread (fixed); its rows are wave-uniform
   const int bn = tid % BNT;
-  const int bk0 = tid / BNT;
+  const int bk0 = BNT == 128 ? (wave >> 1) : wave;
   const int ncol = n0 + bn;
   const bool col_ok = ncol < Ntot;
   int img = 0, cp = 0;
@@ -128,39 +155,40 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     cp = ncol - img * HWc;
   }
   const int cy = cp / Wc, cx = cp - cy * Wc;
-  const float *sbase = src + (size_t)img * Cs * Hs * Ws;
-  const int y0 = MODE == 0 ? cy * g.sh - g.ph : cy;
-  const int x0 = MODE == 0 ? cx * g.sw - g.pw : cx;
+  const int ybase = MODE == 0 ? cy * g.sh : cy;
+  const int xbase = MODE == 0 ? cx * g.sw : cx;
+  const int simg = img * Kc * HWs;
 
-  // this thread's A-load coordinates
+  // A-load row of this thread; its k rows (channels) are wave-uniform
   const int am = tid & (BM - 1);
-  const int ak0 = tid >> 6;  // 0..3
   const bool arow_ok = (m0 + am) < M;
-  const float *abase = A + (size_t)(m0 + am) * a_row_stride;
+  // fwd: W[m][c][rs] = w[m*Cin*RS + c*RS + rs];  dgrad: W[c][m][rs] = w[c*Cin*RS + m*RS + rs]
+  const int a_mstride = MODE == 0 ? g.Cin * RS : RS;
+  const int a_cstride = MODE == 0 ? RS : g.Cin * RS;
+  const int arow = (m0 + am) * a_mstride;
 
   float ra[4], rb[BPER];
-
-  auto load_tiles = [&](int k0) {
+  auto load_tiles = [&](int ks) {
+    const int tap = ks / csteps;                    // uniform
+    const int c0 = (ks - tap * csteps) * BK;
+    const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int k = k0 + ak0 + 4 * j;
-      ra[j] = (arow_ok && k < Kg) ? abase[tab[k].w] : 0.f;
+      const int c = c0 + wave + 4 * j;
+      ra[j] = bload(rw, (arow_ok && c < Kc) ? (arow + c * a_cstride + rs) * 4 : OOR);
     }
+    const int iy = ybase + dy, ix = xbase + dx;
+    const bool pix_ok = col_ok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
+    const int pofs = simg + iy * Ws + ix;
 #pragma unroll
     for (int j = 0; j < BPER; ++j) {
-      const int k = k0 + bk0 + BROWS * j;
-      float v = 0.f;
-      if (col_ok && k < Kg) {
-        const int4 t = tab[k];
-        const int iy = y0 + t.y, ix = x0 + t.z;
-        if ((unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws) v = sbase[t.x + iy * Ws + ix];
-      }
-      rb[j] = v;
+      const int c = c0 + bk0 + BROWS * j;
+      rb[j] = bload(rx, (pix_ok && c < Kc) ? (pofs + c * HWs) * 4 : OOR);
     }
   };
   auto store_tiles = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) As[buf][ak0 + 4 * j][am] = ra[j];
+    for (int j = 0; j < 4; ++j) As[buf][wave + 4 * j][am] = ra[j];
 #pragma unroll
     for (int j = 0; j < BPER; ++j) Bs[buf][bk0 + BROWS * j][bn] = rb[j];
   };
@@ -168,16 +196,15 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   f32x16 acc[NACC];
 #pragma unroll
   for (int t = 0; t < NACC; ++t) acc[t] = f32x16{0};
-  const int nk = (Kg + BK - 1) / BK;
   if (nk > 0) {
-    load_tiles(0);
+    load_tiles(kbeg);
     store_tiles(0);
   }
   __syncthreads();
   const int li = lane & 31, lk = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) load_tiles((kt + 1) * BK);
+    if (kt + 1 < nk) load_tiles(kbeg + kt + 1);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const float a = As[buf][kk + lk][32 * wm + li];
@@ -191,88 +218,112 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     __syncthreads();
   }
 
-  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // splits == 1: final values (bias, act) into dst[img][m][pixel];
+  // splits > 1:  raw partial sums into dst = part[split][m][n] (reduced by k_conv_reduce).
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, dst_bytes);
+  const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
   const int HWd = Hd * Wd;
 #pragma unroll
   for (int t = 0; t < NACC; ++t) {
     const int n = n0 + (BNT / 2) * wn + 32 * t + li;
-    if (n >= Ntot) continue;
-    const int im = n / HWc;
-    const int p = n - im * HWc;
-    int dp = p;
-    if (MODE == 1) {
-      const int u = p / Wc, v = p - u * Wc;
-      dp = (py + g.sh * u) * Wd + (px + g.sw * v);
+    const bool nok = n < Ntot;
+    int dbase, mstride;
+    if (splits == 1) {
+      const int im = n / HWc;
+      const int p = n - im * HWc;
+      int dp = p;
+      if (MODE == 1) {
+        const int u = p / Wc, v = p - u * Wc;
+        dp = (py + g.sh * u) * Wd + (px + g.sw * v);
+      }
+      dbase = im * M * HWd + dp;
+      mstride = HWd;
+    } else {
+      dbase = split * M * Ntot + n;
+      mstride = Ntot;
     }
-    float *dbase = dst + (size_t)im * M * HWd + dp;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
-      if (m < M) {
-        float v = acc[t][r];
-        if (bias) v += bias[m];
+      float v = acc[t][r];
+      if (splits == 1) {
+        if (bias) v += bias[min(m, M - 1)];
         if (ACT == 1) v = fmaxf(v, 0.f);
-        dbase[(size_t)m * HWd] = v;
       }
+      bstore(rd, (nok && m < M) ? (dbase + m * mstride) * 4 : OOR, v);
     }
   }
 }
 
+// split-K reduction (fixed order) + bias / relu epilogue:
+// out[img][m][p] = act(sum_s part[s][m][img*HW + p] + bias[m])
+__global__ void k_conv_reduce(const float *__restrict__ part, int splits, int M, int HW, int Ntot,
+                              const float *__restrict__ bias, int act, float *__restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= Ntot) return;
+  const int m = blockIdx.y;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[((size_t)k * M + m) * Ntot + n];
+  if (bias) s += bias[m];
+  if (act == 1) s = fmaxf(s, 0.f);
+  const int im = n / HW, p = n - im * HW;
+  out[((size_t)im * M + m) * HW + p] = s;
+}
+
 // ------------------------------------------------------------------------------------------
-// bwd-weight: dW[co,k] = sum over pixels of g[n,co,p] * xcol[k,(n,p)]; split over pixels.
-// Block tile 64 (co) x 128 (k), K-step = 16 pixels.  Partial slab per split.
+// bwd-weight: dW[co, ci, tap] = sum_(n,p) g[n,co,p] * x[n,ci,p+tap]; pixels split over
+// blocks.  Block tile 64 (co) x 64 (ci) for one tap, K-step = 16 pixels.  Partial slab per
+// split, reduced in fixed order.
 // ------------------------------------------------------------------------------------------
-constexpr int WBN = 128;
+constexpr int WBN = 64;
 
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
-    const float *__restrict__ gout, const float *__restrict__ x, const int4 *__restrict__ tab,
-    float *__restrict__ part, ConvGeom g, int Kg, int pix_per_split) {
-  __shared__ float As[2][BK][BM + PADA];  // As[pixel][co]
-  __shared__ float Bs[2][BK][WBN + PADB];  // Bs[pixel][k]
+    const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
+    ConvGeom g, int pix_per_split) {
+  __shared__ float As[2][BK][BM + PADA];   // As[pixel][co]
+  __shared__ float Bs[2][BK][WBN + PADB];  // Bs[pixel][ci]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * WBN;
+  const int cblocks = (g.Cin + WBN - 1) / WBN;
+  const int tap = blockIdx.x / cblocks;
+  const int ci0 = (blockIdx.x - tap * cblocks) * WBN;
+  const int r = tap / g.S, s = tap - r * g.S;
+  const int m0 = blockIdx.y * BM;
   const int split = blockIdx.z;
   const int PQ = g.P * g.Q;
   const int Ptot = g.N * PQ;
   const int pbeg = split * pix_per_split;
   const int pend = min(Ptot, pbeg + pix_per_split);
+  const int HW = g.H * g.W;
 
-  // thread -> pixel = tid & 15 (same pixel for its A and B loads), co/k rows = tid >> 4
+  // thread -> pixel = tid & 15 (same pixel for its A and B loads), co / ci rows = tid >> 4
   const int tp = tid & 15, trow = tid >> 4;
-  int4 tk[8];
-  bool kok[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = n0 + trow + 16 * j;
-    kok[j] = k < Kg;
-    tk[j] = kok[j] ? tab[k] : make_int4(0, 0, 0, 0);
-  }
-  // running (image, pixel) of this thread's pixel, advanced by BK per K-step (no division)
   int p_cur = pbeg + tp;
   int im = p_cur / max(PQ, 1), od = p_cur - im * PQ;
+  const int dy = r * g.dh - g.ph, dx = s * g.dw - g.pw;
 
-  float ra[4], rb[8];
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
+  float ra[4], rb[4];
   auto load_tiles = [&]() {
     const bool pok = p_cur < pend;
     const int oy = od / g.Q, ox = od - oy * g.Q;
+    const int gb = im * g.Cout * PQ + od;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int co = m0 + trow + 16 * j;
-      ra[j] = (pok && co < g.Cout) ? gout[((size_t)im * g.Cout + co) * PQ + od] : 0.f;
+      ra[j] = bload(rg, (pok && co < g.Cout) ? (gb + co * PQ) * 4 : OOR);
     }
-    const int y0 = oy * g.sh - g.ph, x0 = ox * g.sw - g.pw;
-    const float *xb = x + (size_t)im * g.Cin * g.H * g.W;
+    const int iy = oy * g.sh + dy, ix = ox * g.sw + dx;
+    const bool ok = pok && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    const int xb = im * g.Cin * HW + iy * g.W + ix;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = 0.f;
-      if (pok && kok[j]) {
-        const int iy = y0 + tk[j].y, ix = x0 + tk[j].z;
-        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-          v = xb[tk[j].x + iy * g.W + ix];
-      }
-      rb[j] = v;
+    for (int j = 0; j < 4; ++j) {
+      const int ci = ci0 + trow + 16 * j;
+      rb[j] = bload(rx, (ok && ci < g.Cin) ? (xb + ci * HW) * 4 : OOR);
     }
     p_cur += BK;
     od += BK;
@@ -285,10 +336,10 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 #pragma unroll
     for (int j = 0; j < 4; ++j) As[buf][tp][trow + 16 * j] = ra[j];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Bs[buf][tp][trow + 16 * j] = rb[j];
+    for (int j = 0; j < 4; ++j) Bs[buf][tp][trow + 16 * j] = rb[j];
   };
 
-  f32x16 acc0 = {0}, acc1 = {0};
+  f32x16 acc = {0};
   const int nk = (pend - pbeg + BK - 1) / BK;
   const int li = lane & 31, lk = lane >> 5;
   if (nk > 0) {
@@ -302,24 +353,22 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const float a = As[buf][kk + lk][32 * wm + li];
-      const float b0 = Bs[buf][kk + lk][64 * wn + li];
-      const float b1 = Bs[buf][kk + lk][64 * wn + 32 + li];
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
+      const float b = Bs[buf][kk + lk][32 * wn + li];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
     }
     if (kt + 1 < nk) store_tiles(buf ^ 1);
     __syncthreads();
   }
-  float *pbase = part + (size_t)split * g.Cout * Kg;
+  // part[split][co][ci][tap]  (the weight layout)
+  const int RS = g.R * g.S;
+  const int Kw = g.Cin * RS;
+  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
+  const int ci = ci0 + 32 * wn + li;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int k = n0 + 64 * wn + 32 * t + li;
-    if (k >= Kg) continue;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
-      if (co < g.Cout) pbase[(size_t)co * Kg + k] = t == 0 ? acc0[r] : acc1[r];
-    }
+  for (int rr = 0; rr < 16; ++rr) {
+    const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
+    const bool ok = co < g.Cout && ci < g.Cin;
+    bstore(rp, ok ? ((split * g.Cout + co) * Kw + ci * RS + tap) * 4 : OOR, acc[rr]);
   }
 }
 
@@ -383,13 +432,9 @@ static ConvGeom make_geom(const int *d) {
 static bool geom_ok(const ConvGeom &g) {
   return g.N > 0 && g.Cin > 0 && g.H > 0 && g.W > 0 && g.Cout > 0 && g.R > 0 && g.S > 0 &&
          g.P > 0 && g.Q > 0 && g.sh > 0 && g.sw > 0 && g.dh > 0 && g.dw > 0 && g.ph >= 0 &&
-         g.pw >= 0 && (long long)g.N * g.Cin * g.H * g.W < (1LL << 31) &&
-         (long long)g.N * g.Cout * g.P * g.Q < (1LL << 31);
+         g.pw >= 0 && g.R * g.S <= MAXTAPS && g.sh * g.sw <= MAXPH &&
+         4LL * g.N * g.Cin * g.H * g.W < (1LL << 31) && 4LL * g.N * g.Cout * g.P * g.Q < (1LL << 31);
 }
-
-// dgrad table layout: int4 entries of phase 0 .. phase n-1, each phase slice sized
-// Cout*R*S (upper bound); the count of phase (py, px) is Cout * nr(py) * ns(px).
-static int n_phases(const ConvGeom &g) { return g.sh * g.sw; }
 
 static int valid_taps(int p, int pad, int K, int dil, int st) {
   int n = 0;
@@ -400,109 +445,128 @@ static int valid_taps(int p, int pad, int K, int dil, int st) {
   return n;
 }
 
-static Phases make_phases(const ConvGeom &g, bool dgrad) {
-  Phases p;
-  p.n = n_phases(g);
-  const int cap = g.Cout * g.R * g.S;
-  for (int z = 0; z < p.n; ++z) {
-    p.py[z] = z / g.sw;
-    p.px[z] = z % g.sw;
-    p.Hp[z] = p.py[z] < g.H ? (g.H - p.py[z] + g.sh - 1) / g.sh : 0;
-    p.Wp[z] = p.px[z] < g.W ? (g.W - p.px[z] + g.sw - 1) / g.sw : 0;
-    p.k0[z] = z * cap;
-    p.kn[z] = dgrad ? g.Cout * valid_taps(p.py[z], g.ph, g.R, g.dh, g.sh) *
-                          valid_taps(p.px[z], g.pw, g.S, g.dw, g.sw)
-                    : 0;
+struct GemmPlan {
+  int bnt, splits, kper, nph;
+  long long ncols;  // columns of the largest phase
+};
+
+// Deterministic launch plan shared by the workspace query and the launch.
+static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
+  GemmPlan p;
+  const int Kc = mode == 0 ? g.Cin : g.Cout;
+  const int csteps = cdiv(Kc, BK);
+  int kmax;
+  p.nph = mode ? g.sh * g.sw : 1;
+  if (mode == 0) {
+    p.ncols = (long long)g.N * g.P * g.Q;
+    kmax = g.R * g.S * csteps;
+  } else {
+    p.ncols = 0;
+    kmax = 0;
+    for (int z = 0; z < p.nph; ++z) {
+      const int py = z / g.sw, px = z % g.sw;
+      const long long Hp = py < g.H ? (g.H - py + g.sh - 1) / g.sh : 0;
+      const long long Wp = px < g.W ? (g.W - px + g.sw - 1) / g.sw : 0;
+      p.ncols = std::max(p.ncols, (long long)g.N * Hp * Wp);
+      const int taps = valid_taps(py, g.ph, g.R, g.dh, g.sh) * valid_taps(px, g.pw, g.S, g.dw, g.sw);
+      kmax = std::max(kmax, taps * csteps);
+    }
   }
+  const long long mblocks = cdiv(M, BM);
+  p.bnt = cdiv(p.ncols, 128) * mblocks * p.nph >= 512 ? 128 : 64;
+  const long long blocks = cdiv(p.ncols, p.bnt) * mblocks * p.nph;
+  p.splits = 1;
+  if (blocks < 256 && p.nph == 1) {  // split K when the grid cannot fill the chip
+    int s = (int)((512 + blocks - 1) / blocks);
+    s = std::min(s, std::max(1, kmax / 4));
+    s = std::min(s, 32);
+    p.splits = std::max(1, s);
+  }
+  p.kper = cdiv(std::max(kmax, 1), p.splits);
+  if (p.splits > 1) p.splits = cdiv(kmax, p.kper);
   return p;
 }
 
-extern "C" {
-
-size_t e2ep_conv_table_bytes(const int *dims, int dgrad) {
-  ConvGeom g = make_geom(dims);
-  if (!dgrad) return (size_t)g.Cin * g.R * g.S * 16;
-  return (size_t)n_phases(g) * g.Cout * g.R * g.S * 16;
+static size_t gemm_workspace(const GemmPlan &p, int M) {
+  return p.splits > 1 ? (size_t)p.splits * M * p.ncols * sizeof(float) : 0;
 }
 
-int e2ep_conv_table(const int *dims, int dgrad, void *table, void *stream) {
-  ConvGeom g = make_geom(dims);
-  E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_table: bad geometry");
-  E2EP_REQUIRE(n_phases(g) <= MAXPH, E2EP_ERANGE, "e2ep_conv_table: stride product > %d", MAXPH);
-  hipStream_t s = as_stream(stream);
-  if (!dgrad) {
-    const int Kg = g.Cin * g.R * g.S;
-    hipLaunchKernelGGL(k_conv_table_fwd, dim3(cdiv(Kg, 256)), dim3(256), 0, s, g,
-                       static_cast<int4 *>(table), Kg);
-  } else {
-    int4 *ent = static_cast<int4 *>(table);
-    const int cap = g.Cout * g.R * g.S;
-    for (int z = 0; z < n_phases(g); ++z)
-      hipLaunchKernelGGL(k_conv_table_dgrad, dim3(1), dim3(64), 0, s, g, z / g.sw, z % g.sw,
-                         ent + (size_t)z * cap);
+static int launch_gemm(int mode, int act, const float *w, const float *src, const float *bias,
+                       float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
+                       hipStream_t s) {
+  const GemmPlan p = plan_gemm(mode, g, M);
+  dim3 grid(cdiv(p.ncols, p.bnt), cdiv(M, BM), p.nph * p.splits);
+  float *out = dst;
+  long long out_bytes = dst_bytes;
+  if (p.splits > 1) {
+    if (!workspace) {
+      set_error("conv: split-K plan needs a workspace (query the *_workspace entry point)");
+      return E2EP_EINVAL;
+    }
+    out = static_cast<float *>(workspace);
+    out_bytes = (long long)gemm_workspace(p, M);
   }
-  return launch_status("e2ep_conv_table");
-}
-
-static int launch_gemm(int mode, int act, const float *A, int a_stride, const float *src,
-                       const int4 *tab, const float *bias, float *dst, const ConvGeom &g, int M,
-                       int Kfwd, const Phases &ph, hipStream_t s) {
-  // columns of the largest phase / the forward output
-  long long ncols = 0;
-  if (mode == 0) {
-    ncols = (long long)g.N * g.P * g.Q;
-  } else {
-    for (int z = 0; z < ph.n; ++z) ncols = std::max(ncols, (long long)g.N * ph.Hp[z] * ph.Wp[z]);
-  }
-  const int mblocks = cdiv(M, BM);
-  // prefer the wide tile when it still yields >= 2 workgroups per CU
-  const bool wide = cdiv(ncols, 128) * mblocks * (mode ? ph.n : 1) >= 512;
-  const int bnt = wide ? 128 : 64;
-  dim3 grid(cdiv(ncols, bnt), mblocks, mode ? ph.n : 1);
-#define GEMM_LAUNCH(MD, AC, BT)                                                                   \
-  hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT>), grid, dim3(256), 0, s, A, a_stride, src, tab, bias, \
-                     dst, g, M, Kfwd, ph)
+#define GEMM_LAUNCH(MD, AC, BT)                                                              \
+  hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT>), grid, dim3(256), 0, s, w, src, bias, out,     \
+                     out_bytes, g, M, p.splits, p.kper)
+  const bool wide = p.bnt == 128;
   if (mode == 0 && act == 0) { if (wide) GEMM_LAUNCH(0, 0, 128); else GEMM_LAUNCH(0, 0, 64); }
   else if (mode == 0) { if (wide) GEMM_LAUNCH(0, 1, 128); else GEMM_LAUNCH(0, 1, 64); }
   else { if (wide) GEMM_LAUNCH(1, 0, 128); else GEMM_LAUNCH(1, 0, 64); }
 #undef GEMM_LAUNCH
+  if (p.splits > 1) {
+    const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
+    hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
+                       static_cast<const float *>(workspace), p.splits, M, HW, (int)p.ncols, bias,
+                       act, dst);
+  }
   return 0;
 }
 
-int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const void *table,
-                  const int *dims, int act, float *y, void *stream) {
+extern "C" {
+
+size_t e2ep_conv_fwd_workspace(const int *dims) {
+  ConvGeom g = make_geom(dims);
+  return gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout);
+}
+
+size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
+  ConvGeom g = make_geom(dims);
+  return gemm_workspace(plan_gemm(1, g, m_channels), m_channels);
+}
+
+int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
+                  float *y, void *workspace, void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_fwd: bad geometry");
   E2EP_REQUIRE(act == 0 || act == 1, E2EP_EINVAL, "e2ep_conv_fwd: act must be 0 (none) or 1 (relu)");
-  const int Kg = g.Cin * g.R * g.S;
-  Phases ph = make_phases(g, false);
-  launch_gemm(0, act, w, Kg, x, static_cast<const int4 *>(table), bias, y, g, g.Cout, Kg, ph,
-              as_stream(stream));
+  const int rc = launch_gemm(0, act, w, x, bias, y, 4LL * g.N * g.Cout * g.P * g.Q, g, g.Cout,
+                             workspace, as_stream(stream));
+  if (rc) return rc;
   return launch_status("e2ep_conv_fwd");
 }
 
-int e2ep_conv_dgrad(const float *gout, const float *w, const void *table, const int *dims,
-                    int m_channels, float *dx, void *stream) {
+int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels, float *dx,
+                    void *workspace, void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_dgrad: bad geometry");
   E2EP_REQUIRE(m_channels > 0 && m_channels <= g.Cin, E2EP_EINVAL,
                "e2ep_conv_dgrad: m_channels must be in [1, Cin]");
-  E2EP_REQUIRE(n_phases(g) <= MAXPH, E2EP_ERANGE, "e2ep_conv_dgrad: stride product > %d", MAXPH);
-  Phases ph = make_phases(g, true);
-  launch_gemm(1, 0, w, g.R * g.S, gout, static_cast<const int4 *>(table), nullptr, dx, g, m_channels, 0, ph, as_stream(stream));
+  const int rc = launch_gemm(1, 0, w, gout, nullptr, dx, 4LL * g.N * m_channels * g.H * g.W, g,
+                             m_channels, workspace, as_stream(stream));
+  if (rc) return rc;
   return launch_status("e2ep_conv_dgrad");
 }
 
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
-  const int Kg = g.Cin * g.R * g.S;
-  const long long base = (long long)cdiv(Kg, WBN) * cdiv(g.Cout, BM);
+  const long long base = (long long)g.R * g.S * cdiv(g.Cin, WBN) * cdiv(g.Cout, BM);
   const long long pix = (long long)g.N * g.P * g.Q;
   long long want = (1024 + base - 1) / base;
-  long long cap = pix / 128;
+  long long cap = pix / 256;
   long long s = want < cap ? want : cap;
   if (s < 1) s = 1;
-  if (s > 1024) s = 1024;
+  if (s > 256) s = 256;
   return (int)s;
 }
 
@@ -511,21 +575,19 @@ size_t e2ep_conv_wgrad_workspace(const int *dims, int splits) {
   return (size_t)splits * g.Cout * g.Cin * g.R * g.S * sizeof(float);
 }
 
-int e2ep_conv_wgrad(const float *gout, const float *x, const void *table, const int *dims,
-                    int splits, void *workspace, float *dw, int accumulate, void *stream) {
+int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,
+                    void *workspace, float *dw, int accumulate, void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g) && splits > 0, E2EP_EINVAL, "e2ep_conv_wgrad: bad geometry");
-  const int Kg = g.Cin * g.R * g.S;
   const int Ptot = g.N * g.P * g.Q;
   int per = (Ptot + splits - 1) / splits;
   per = (per + BK - 1) / BK * BK;
   const int used = (Ptot + per - 1) / per;
-  dim3 grid(cdiv(Kg, WBN), cdiv(g.Cout, BM), used);
+  dim3 grid(g.R * g.S * cdiv(g.Cin, WBN), cdiv(g.Cout, BM), used);
   hipStream_t s = as_stream(stream);
   float *part = static_cast<float *>(workspace);
-  hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, static_cast<const int4 *>(table),
-                     part, g, Kg, per);
-  const int n = g.Cout * Kg;
+  hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per);
+  const int n = g.Cout * g.Cin * g.R * g.S;
   hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 256)), dim3(256), 0, s, part, used, n, dw,
                      accumulate);
   return launch_status("e2ep_conv_wgrad");

@@ -30,10 +30,8 @@ class _BevStem(torch.autograd.Function):
         Cout, _, R, S = w.shape
         P, Q = (H + 6 - R) // 2 + 1, (W + 6 - S) // 2 + 1
         dims = (B, Cin, H, W, Cout, R, S, P, Q, 2, 2, 3, 3, 1, 1)
-        y = torch.empty(B, Cout, P, Q, dtype=torch.float32, device=bev.device)
-        with timing.region("conv_fwd"):
-            _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w.contiguous()), None,
-                      _lib.ptr(conv._table(dims, 0, x.device)), _lib.dims(dims), 0, _lib.ptr(y), s)
+        y = conv.conv_fwd(x, w.contiguous(), None, dims, 0,
+                          torch.empty(B, Cout, P, Q, dtype=torch.float32, device=bev.device))
         ctx.save_for_backward(x, w)
         ctx.meta = (B, C, X, Y, H, W, sh, sw, dims)
         return y
@@ -47,23 +45,15 @@ class _BevStem(torch.autograd.Function):
         d = _lib.dims(dims)
         dbev = dw = None
         if ctx.needs_input_grad[0]:
-            dres = torch.empty(B, C, H, W, dtype=torch.float32, device=gy.device)
-            with timing.region("conv_dgrad"):
-                _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w.contiguous()),
-                          _lib.ptr(conv._table(dims, 1, gy.device)), d, C, _lib.ptr(dres), s)
+            dres = conv.conv_dgrad(gy, w.contiguous(), dims, C,
+                                   torch.empty(B, C, H, W, dtype=torch.float32, device=gy.device))
             dbev = torch.empty(B, C, X, Y, dtype=torch.float32, device=gy.device)
             ws = torch.empty(B * C * H * Y, dtype=torch.float32, device=gy.device)
             with timing.region("resize_bwd"):
                 _lib.call("e2ep_resize_bwd", _lib.ptr(dres), H * W, B * C, X, Y, H, W, sh, sw,
                           _lib.ptr(dbev), 0, _lib.ptr(ws), s)
         if ctx.needs_input_grad[2]:
-            splits = _lib.load().e2ep_conv_wgrad_splits(d)
-            ws = torch.empty(splits * w.numel(), dtype=torch.float32, device=gy.device)
-            dw = torch.empty_like(w)
-            with timing.region("conv_wgrad"):
-                _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x),
-                          _lib.ptr(conv._table(dims, 0, gy.device)), d, splits, _lib.ptr(ws),
-                          _lib.ptr(dw), 0, s)
+            dw = conv.conv_wgrad(gy, x, dims, torch.empty_like(w))
         return dbev, None, dw, None
 
 

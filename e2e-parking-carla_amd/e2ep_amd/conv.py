@@ -1,7 +1,7 @@
 """Convolution autograd op over the e2ep implicit-GEMM kernels (csrc/conv.hip).
 
 conv2d(x, w, b, stride, padding(l,r,t,b), dilation, act, grad_channels) -> y, backward via
-e2ep_conv_dgrad (stride-phase tables) / e2ep_conv_wgrad (split pixel reduction) /
+e2ep_conv_dgrad (stride-phase split) / e2ep_conv_wgrad (split pixel reduction) /
 e2ep_bias_grad.  1x1 convs on 1x1 maps run on e2ep_skinny_gemm.  groups must be 1
 (depthwise convs use e2ep_amd.nn_ops).  `grad_channels` limits the input gradient to the
 first channels (the BEV encoder's target-point channel is a constant: no gradient)."""
@@ -9,19 +9,38 @@ import torch
 
 from . import _lib, timing
 
-_TABLES = {}
+
+def _ws(nbytes, device):
+    return torch.empty(nbytes // 4, dtype=torch.float32, device=device) if nbytes else None
 
 
-def _table(dims, dgrad, device):
-    key = (tuple(dims), dgrad, str(device))
-    t = _TABLES.get(key)
-    if t is None:
-        d = _lib.dims(dims)
-        nbytes = _lib.load().e2ep_conv_table_bytes(d, int(dgrad))
-        t = torch.empty(max(nbytes // 4, 4), dtype=torch.int32, device=device)
-        _lib.call("e2ep_conv_table", d, int(dgrad), _lib.ptr(t), _lib.stream())
-        _TABLES[key] = t
-    return t
+def conv_fwd(x, w, b, dims, act, y):
+    """Launch the forward conv into y (handles the split-K workspace)."""
+    d = _lib.dims(dims)
+    ws = _ws(_lib.load().e2ep_conv_fwd_workspace(d), x.device)
+    with timing.region("conv_fwd"):
+        _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, _lib.ptr(y),
+                  _lib.ptr(ws), _lib.stream())
+    return y
+
+
+def conv_dgrad(gy, w, dims, m_channels, dx):
+    d = _lib.dims(dims)
+    ws = _ws(_lib.load().e2ep_conv_dgrad_workspace(d, m_channels), gy.device)
+    with timing.region("conv_dgrad"):
+        _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, m_channels, _lib.ptr(dx),
+                  _lib.ptr(ws), _lib.stream())
+    return dx
+
+
+def conv_wgrad(gy, x, dims, dw):
+    d = _lib.dims(dims)
+    splits = _lib.load().e2ep_conv_wgrad_splits(d)
+    ws = torch.empty(splits * dw.numel(), dtype=torch.float32, device=gy.device)
+    with timing.region("conv_wgrad"):
+        _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws),
+                  _lib.ptr(dw), 0, _lib.stream())
+    return dw
 
 
 class _Conv2d(torch.autograd.Function):
@@ -30,11 +49,7 @@ class _Conv2d(torch.autograd.Function):
         x = x.contiguous()
         w = w.contiguous()
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
-        y = torch.empty(N, Cout, P, Q, dtype=torch.float32, device=x.device)
-        d = _lib.dims(dims)
-        with timing.region("conv_fwd"):
-            _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b),
-                      _lib.ptr(_table(dims, 0, x.device)), d, act, _lib.ptr(y), _lib.stream())
+        y = conv_fwd(x, w, b, dims, act, torch.empty(N, Cout, P, Q, dtype=torch.float32, device=x.device))
         ctx.dims, ctx.act, ctx.has_bias, ctx.gc = dims, act, b is not None, grad_channels
         ctx.save_for_backward(x, w, y if act else None)
         return y
@@ -47,28 +62,18 @@ class _Conv2d(torch.autograd.Function):
         gy = gy.contiguous()
         if ctx.act == 1:
             gy = torch.where(y > 0, gy, torch.zeros((), device=gy.device))
-        d = _lib.dims(dims)
         s = _lib.stream()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             gc = ctx.gc or Cin
-            dxg = torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device)
-            with timing.region("conv_dgrad"):
-                _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w),
-                          _lib.ptr(_table(dims, 1, x.device)), d, gc, _lib.ptr(dxg), s)
+            dxg = conv_dgrad(gy, w, dims, gc, torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device))
             if gc == Cin:
                 dx = dxg
             else:
                 dx = torch.zeros_like(x)
                 dx[:, :gc] = dxg
         if ctx.needs_input_grad[1]:
-            splits = _lib.load().e2ep_conv_wgrad_splits(d)
-            ws = torch.empty(splits * Cout * Cin * R * S, dtype=torch.float32, device=x.device)
-            dw = torch.empty_like(w)
-            with timing.region("conv_wgrad"):
-                _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x),
-                          _lib.ptr(_table(dims, 0, x.device)), d, splits, _lib.ptr(ws),
-                          _lib.ptr(dw), 0, s)
+            dw = conv_wgrad(gy, x, dims, torch.empty_like(w))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = torch.empty(Cout, dtype=torch.float32, device=x.device)
             _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db), s)

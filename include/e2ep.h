@@ -107,7 +107,8 @@ int e2ep_target_bev(const float *target_point, const float *noise, int B, int X,
                     float res_x, float res_y, float *out, long long out_bstride, void *stream);
 
 /* ---------------------------------------------------------------------------------------
- * Convolution, NCHW fp32, implicit GEMM on the exact-f32 matrix cores (SURVEY.md §8a rows
+ * Convolution, NCHW fp32, implicit GEMM on the exact-f32 matrix cores (K order: filter tap
+ * outer, 16-channel chunks inner; no im2col buffer, no lookup table) (SURVEY.md §8a rows
  * a8 (1x1/stem), a9, a11, a13).  Replaces torch.nn.Conv2d forward/backward in
  * model/bev_encoder.py:13-34, model/segmentation_head.py:19-31,
  * model/convolutions.py:183-282 and the efficientnet-pytorch 1x1 / stem convs.
@@ -117,28 +118,26 @@ int e2ep_target_bev(const float *target_point, const float *noise, int B, int X,
  * a bigger P/Q with implicit zero rows/cols at the bottom/right).  groups == 1.
  * ------------------------------------------------------------------------------------- */
 
-/* Build the per-conv im2col k-table (e2ep_conv_table_bytes bytes).  dgrad != 0 builds the
- * stride-phase tables of the data gradient (only taps that land on an integral output
- * coordinate for each input-pixel phase). */
-size_t e2ep_conv_table_bytes(const int *dims, int dgrad);
-int e2ep_conv_table(const int *dims, int dgrad, void *table, void *stream);
-
-/* y[N,Cout,P,Q] = conv(x[N,Cin,H,W], w[Cout,Cin,R,S]) + bias (nullable); act 0 none, 1 relu. */
-int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const void *table,
-                  const int *dims, int act, float *y, void *stream);
+/* y[N,Cout,P,Q] = conv(x[N,Cin,H,W], w[Cout,Cin,R,S]) + bias (nullable); act 0 none, 1 relu.
+ * Grids that cannot fill the chip split K; the partial sums then need a workspace of
+ * e2ep_conv_fwd_workspace bytes (0 = none needed; pass NULL) and are reduced in fixed order. */
+size_t e2ep_conv_fwd_workspace(const int *dims);
+int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
+                  float *y, void *workspace, void *stream);
 
 /* dx[N,m_channels,H,W] = conv_transpose(gout[N,Cout,P,Q], w) restricted to the first
- * m_channels input channels (table built with dgrad = 1); no zero taps at stride 2. */
-int e2ep_conv_dgrad(const float *gout, const float *w, const void *table, const int *dims,
-                    int m_channels, float *dx, void *stream);
+ * m_channels input channels; split by input-pixel stride phase, so no zero taps at stride 2. */
+size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels);
+int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels, float *dx,
+                    void *workspace, void *stream);
 
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of
  * e2ep_conv_wgrad_workspace bytes) are summed in a fixed order: deterministic. */
 int e2ep_conv_wgrad_splits(const int *dims);
 size_t e2ep_conv_wgrad_workspace(const int *dims, int splits);
-int e2ep_conv_wgrad(const float *gout, const float *x, const void *table, const int *dims,
-                    int splits, void *workspace, float *dw, int accumulate, void *stream);
+int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,
+                    void *workspace, float *dw, int accumulate, void *stream);
 
 /* db[C] = sum over (n, p) of gout[N, C, HW]. */
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream);
