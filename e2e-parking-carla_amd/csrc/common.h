@@ -24,6 +24,25 @@ inline int launch_status(const char *what) {
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// Branch-free guarded memory access.  `if (ok) v = p[i];` inside an unrolled loop makes
+// hipcc branch around every load and wait vmcnt(0) per element, serialising the loads; a
+// buffer load with an out-of-range byte offset instead returns 0 (a store is dropped), so
+// the guard becomes a select.  Descriptors must be built from wave-uniform values.
+constexpr int OOR = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, long long bytes) {
+  const int nr = bytes >= 0x7fffffff ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, nr, 0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ int bload_i(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 0);
+}
+
 // 64-lane wave helpers
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

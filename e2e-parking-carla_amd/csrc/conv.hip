@@ -31,21 +31,6 @@ namespace e2ep {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// Branch-free guarded memory access: an invalid element gets an out-of-range byte offset,
-// which the buffer unit turns into a 0 load / a dropped store.  Descriptors are built from
-// kernel arguments only (wave-uniform: no waterfall loops).
-constexpr int OOR = 0x7ffffff0;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, long long bytes) {
-  const int nr = bytes >= 0x7fffffff ? 0x7fffffff : (int)bytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, nr, 0x00020000);
-}
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 0);
-}
-
 constexpr int BM = 64, BK = 16;
 constexpr int PADA = 4, PADB = 4;
 constexpr int MAXPH = 4;
@@ -272,9 +257,10 @@ __global__ void k_conv_reduce(const float *__restrict__ part, int splits, int M,
 }
 
 // ------------------------------------------------------------------------------------------
-// bwd-weight: dW[co, ci, tap] = sum_(n,p) g[n,co,p] * x[n,ci,p+tap]; pixels split over
-// blocks.  Block tile 64 (co) x 64 (ci) for one tap, K-step = 16 pixels.  Partial slab per
-// split, reduced in fixed order.
+// bwd-weight: dW[co, col] = sum_(n,p) g[n,co,p] * x[n,ci,p+tap], col = ci*R*S + tap (the
+// weight layout); pixels split over blocks.  Block tile 64 (co) x 64 (col), K-step = 16
+// pixels; each thread's 4 columns keep (ci, dy, dx) in registers.  Partial slab per split,
+// reduced in fixed order.
 // ------------------------------------------------------------------------------------------
 constexpr int WBN = 64;
 
@@ -282,15 +268,14 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
     const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
     ConvGeom g, int pix_per_split) {
   __shared__ float As[2][BK][BM + PADA];   // As[pixel][co]
-  __shared__ float Bs[2][BK][WBN + PADB];  // Bs[pixel][ci]
+  __shared__ float Bs[2][BK][WBN + PADB];  // Bs[pixel][col]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
-  const int cblocks = (g.Cin + WBN - 1) / WBN;
-  const int tap = blockIdx.x / cblocks;
-  const int ci0 = (blockIdx.x - tap * cblocks) * WBN;
-  const int r = tap / g.S, s = tap - r * g.S;
+  const int RS = g.R * g.S;
+  const int Kw = g.Cin * RS;
+  const int n0 = blockIdx.x * WBN;
   const int m0 = blockIdx.y * BM;
   const int split = blockIdx.z;
   const int PQ = g.P * g.Q;
@@ -299,11 +284,23 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   const int pend = min(Ptot, pbeg + pix_per_split);
   const int HW = g.H * g.W;
 
-  // thread -> pixel = tid & 15 (same pixel for its A and B loads), co / ci rows = tid >> 4
+  // thread -> pixel = tid & 15 (same pixel for its A and B loads), co / col rows = tid >> 4
   const int tp = tid & 15, trow = tid >> 4;
+  int cofs[4], cdy[4], cdx[4];
+  bool cok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + trow + 16 * j;
+    cok[j] = col < Kw;
+    const int cc = cok[j] ? col : 0;
+    const int ci = cc / RS, tap = cc - ci * RS;
+    const int r = tap / g.S, s = tap - r * g.S;
+    cofs[j] = ci * HW;
+    cdy[j] = r * g.dh - g.ph;
+    cdx[j] = s * g.dw - g.pw;
+  }
   int p_cur = pbeg + tp;
   int im = p_cur / max(PQ, 1), od = p_cur - im * PQ;
-  const int dy = r * g.dh - g.ph, dx = s * g.dw - g.pw;
 
   const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
   const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
@@ -317,13 +314,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
       const int co = m0 + trow + 16 * j;
       ra[j] = bload(rg, (pok && co < g.Cout) ? (gb + co * PQ) * 4 : OOR);
     }
-    const int iy = oy * g.sh + dy, ix = ox * g.sw + dx;
-    const bool ok = pok && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-    const int xb = im * g.Cin * HW + iy * g.W + ix;
+    const int yb = oy * g.sh, xb0 = ox * g.sw;
+    const int xb = im * g.Cin * HW;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int ci = ci0 + trow + 16 * j;
-      rb[j] = bload(rx, (ok && ci < g.Cin) ? (xb + ci * HW) * 4 : OOR);
+      const int iy = yb + cdy[j], ix = xb0 + cdx[j];
+      const bool ok = pok && cok[j] && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      rb[j] = bload(rx, ok ? (xb + cofs[j] + iy * g.W + ix) * 4 : OOR);
     }
     p_cur += BK;
     od += BK;
@@ -359,27 +356,33 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
     if (kt + 1 < nk) store_tiles(buf ^ 1);
     __syncthreads();
   }
-  // part[split][co][ci][tap]  (the weight layout)
-  const int RS = g.R * g.S;
-  const int Kw = g.Cin * RS;
   const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
-  const int ci = ci0 + 32 * wn + li;
+  const int col = n0 + 32 * wn + li;
 #pragma unroll
   for (int rr = 0; rr < 16; ++rr) {
     const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
-    const bool ok = co < g.Cout && ci < g.Cin;
-    bstore(rp, ok ? ((split * g.Cout + co) * Kw + ci * RS + tap) * 4 : OOR, acc[rr]);
+    const bool ok = co < g.Cout && col < Kw;
+    bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[rr]);
   }
 }
 
-// fixed-order sum of the split slabs (+ optional accumulate into an existing gradient)
+// fixed-order sum of the split slabs (+ optional accumulate into an existing gradient).
+// 4 independent partial chains per thread (fixed assignment) keep loads in flight.
 __global__ void k_reduce_splits(const float *__restrict__ part, int splits, int n,
                                 float *__restrict__ out, int accumulate) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float s = accumulate ? out[i] : 0.f;
-  for (int k = 0; k < splits; ++k) s += part[(size_t)k * n + i];
-  out[i] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= splits; k += 4) {
+    s0 += part[(size_t)(k + 0) * n + i];
+    s1 += part[(size_t)(k + 1) * n + i];
+    s2 += part[(size_t)(k + 2) * n + i];
+    s3 += part[(size_t)(k + 3) * n + i];
+  }
+  for (; k < splits; ++k) s0 += part[(size_t)k * n + i];
+  const float s = (s0 + s1) + (s2 + s3);
+  out[i] = accumulate ? out[i] + s : s;
 }
 
 // per-channel bias gradient: db[c] = sum over (n, p) of g[n, c, p]  (one block per channel)
@@ -560,7 +563,7 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
 
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
-  const long long base = (long long)g.R * g.S * cdiv(g.Cin, WBN) * cdiv(g.Cout, BM);
+  const long long base = (long long)cdiv(g.Cin * g.R * g.S, WBN) * cdiv(g.Cout, BM);
   const long long pix = (long long)g.N * g.P * g.Q;
   long long want = (1024 + base - 1) / base;
   long long cap = pix / 256;
@@ -583,7 +586,7 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
   int per = (Ptot + splits - 1) / splits;
   per = (per + BK - 1) / BK * BK;
   const int used = (Ptot + per - 1) / per;
-  dim3 grid(g.R * g.S * cdiv(g.Cin, WBN), cdiv(g.Cout, BM), used);
+  dim3 grid(cdiv(g.Cin * g.R * g.S, WBN), cdiv(g.Cout, BM), used);
   hipStream_t s = as_stream(stream);
   float *part = static_cast<float *>(workspace);
   hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per);

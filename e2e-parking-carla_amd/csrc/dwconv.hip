@@ -10,8 +10,8 @@ struct DwGeom {
   int N, C, H, W, K, P, Q, st, pt, pl;
 };
 
-// forward: one thread per output pixel; taps unrolled for the compile-time kernel size
-template <int K>
+// forward: one thread per output pixel; taps unrolled; branch-free guarded loads
+template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
                                                 const float *__restrict__ w, DwGeom g,
                                                 float *__restrict__ y) {
@@ -20,25 +20,30 @@ __global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
   const int nc = blockIdx.y;
   const int c = nc % g.C;
   const int oy = i / g.Q, ox = i - oy * g.Q;
-  const float *xp = x + (size_t)nc * g.H * g.W;
+  const int HW = g.H * g.W;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x + (size_t)nc * HW, 4LL * HW);
   const float *wp = w + c * K * K;
-  const int y0 = oy * g.st - g.pt, x0 = ox * g.st - g.pl;
-  float s = 0.f;
+  const int y0 = oy * ST - g.pt, x0 = ox * ST - g.pl;
+  float v[K * K];
 #pragma unroll
   for (int a = 0; a < K; ++a) {
     const int iy = y0 + a;
-    if ((unsigned)iy >= (unsigned)g.H) continue;
 #pragma unroll
     for (int b = 0; b < K; ++b) {
       const int ix = x0 + b;
-      if ((unsigned)ix < (unsigned)g.W) s += wp[a * K + b] * xp[iy * g.W + ix];
+      const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      v[a * K + b] = bload(rx, ok ? (iy * g.W + ix) * 4 : OOR);
     }
   }
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) s += wp[t] * v[t];
   y[(size_t)nc * g.P * g.Q + i] = s;
 }
 
 // data gradient: one thread per input pixel, gather the outputs whose window covers it
-template <int K>
+// (branch-free: invalid taps read 0 through an out-of-range buffer offset)
+template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_dgrad(const float *__restrict__ gy,
                                                   const float *__restrict__ w, DwGeom g,
                                                   float *__restrict__ dx) {
@@ -47,28 +52,31 @@ __global__ void __launch_bounds__(256) k_dw_dgrad(const float *__restrict__ gy,
   const int nc = blockIdx.y;
   const int c = nc % g.C;
   const int iy = i / g.W, ix = i - iy * g.W;
-  const float *gp = gy + (size_t)nc * g.P * g.Q;
+  const int PQ = g.P * g.Q;
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gy + (size_t)nc * PQ, 4LL * PQ);
   const float *wp = w + c * K * K;
-  float s = 0.f;
+  float v[K * K];
 #pragma unroll
   for (int a = 0; a < K; ++a) {
     const int ny = iy + g.pt - a;
-    if (ny < 0) continue;
-    const int oy = ny / g.st;
-    if (oy * g.st != ny || oy >= g.P) continue;
+    const int oy = ny >= 0 ? ny / ST : -1;  // ST is a compile-time 1 or 2
+    const bool oky = ny >= 0 && oy * ST == ny && oy < g.P;
 #pragma unroll
     for (int b = 0; b < K; ++b) {
       const int nx = ix + g.pl - b;
-      if (nx < 0) continue;
-      const int ox = nx / g.st;
-      if (ox * g.st == nx && ox < g.Q) s += wp[a * K + b] * gp[oy * g.Q + ox];
+      const int ox = nx >= 0 ? nx / ST : -1;
+      const bool ok = oky && nx >= 0 && ox * ST == nx && ox < g.Q;
+      v[a * K + b] = bload(rg, ok ? (oy * g.Q + ox) * 4 : OOR);
     }
   }
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) s += wp[t] * v[t];
   dx[(size_t)nc * g.H * g.W + i] = s;
 }
 
 // weight gradient partials: grid (C, splits); each slice of (n, oy, ox) accumulates K*K taps
-template <int K>
+template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
                                                   const float *__restrict__ x, DwGeom g,
                                                   int splits, float *__restrict__ part) {
@@ -80,13 +88,15 @@ __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
   float acc[K * K];
 #pragma unroll
   for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
+  const int HW = g.H * g.W;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.C * HW);
   for (int i = beg + threadIdx.x; i < end; i += 256) {
     const int n = i / PQ;
     const int pix = i - n * PQ;
     const int oy = pix / g.Q, ox = pix - oy * g.Q;
     const float gv = gy[((size_t)n * g.C + c) * PQ + pix];
-    const float *xp = x + ((size_t)n * g.C + c) * g.H * g.W;
-    const int y0 = oy * g.st - g.pt, x0 = ox * g.st - g.pl;
+    const int xb = (n * g.C + c) * HW;
+    const int y0 = oy * ST - g.pt, x0 = ox * ST - g.pl;
 #pragma unroll
     for (int a = 0; a < K; ++a) {
       const int iy = y0 + a;
@@ -94,7 +104,8 @@ __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
 #pragma unroll
       for (int b = 0; b < K; ++b) {
         const int ix = x0 + b;
-        if (oky && (unsigned)ix < (unsigned)g.W) acc[a * K + b] += gv * xp[iy * g.W + ix];
+        const bool ok = oky && (unsigned)ix < (unsigned)g.W;
+        acc[a * K + b] += gv * bload(rx, ok ? (xb + iy * g.W + ix) * 4 : OOR);
       }
     }
   }
@@ -141,12 +152,16 @@ using namespace e2ep;
 
 #define DW_DISPATCH(KERNEL, GRID, ...)                                                        \
   do {                                                                                        \
-    if (g.K == 3)                                                                             \
-      hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__);     \
-    else if (g.K == 5)                                                                        \
-      hipLaunchKernelGGL(KERNEL<5>, GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__);     \
+    if (g.K == 3 && g.st == 1)                                                                \
+      hipLaunchKernelGGL((KERNEL<3, 1>), GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__); \
+    else if (g.K == 3 && g.st == 2)                                                           \
+      hipLaunchKernelGGL((KERNEL<3, 2>), GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__); \
+    else if (g.K == 5 && g.st == 1)                                                           \
+      hipLaunchKernelGGL((KERNEL<5, 1>), GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__); \
+    else if (g.K == 5 && g.st == 2)                                                           \
+      hipLaunchKernelGGL((KERNEL<5, 2>), GRID, dim3(256), 0, as_stream(stream), __VA_ARGS__); \
     else {                                                                                    \
-      set_error("depthwise conv: kernel size %d unsupported (3, 5)", g.K);                   \
+      set_error("depthwise conv: kernel %d / stride %d unsupported (k 3|5, s 1|2)", g.K, g.st); \
       return E2EP_ERANGE;                                                                     \
     }                                                                                         \
   } while (0)

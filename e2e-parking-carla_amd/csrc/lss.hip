@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(256) k_lss_bwd(
   const int b = bn / N;
   const int pix0 = blockIdx.x * BWD_PIX;
   const bool lane_ok = lane < C;
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gT, 4LL * gridDim.y / N * XYZ * C);
   for (int pp = 0; pp < BWD_PIX_PER_WAVE; ++pp) {
     const int lp = wave * BWD_PIX_PER_WAVE + pp;  // local pixel
     const int pix = pix0 + lp;
@@ -222,17 +223,16 @@ __global__ void __launch_bounds__(256) k_lss_bwd(
     const float f = lane_ok ? featT[((long long)bn * HW + pix) * C + lane] : 0.f;
     float gf = 0.f;
     float v[64];
+    // branch-free: masked points (q < 0) and idle lanes read 0 via an out-of-range offset
 #pragma unroll
     for (int d = 0; d < 64; ++d) {
       v[d] = 0.f;
-      if (d < D) {
+      if (d < D) {  // D is uniform
         const long long pidx = ((long long)bn * D + d) * HW + pix;
         const int q = pillar[pidx];
-        if (q >= 0) {
-          const float g = lane_ok ? gT[((long long)b * XYZ + q) * C + lane] : 0.f;
-          gf += g * prob[pidx];
-          v[d] = g * f;
-        }
+        const float g = bload(rg, (q >= 0 && lane_ok) ? ((b * XYZ + q) * C + lane) * 4 : OOR);
+        gf += g * prob[pidx];
+        v[d] = g * f;
       }
     }
     halve<32>(v, lane);

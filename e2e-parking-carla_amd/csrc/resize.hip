@@ -64,8 +64,8 @@ __global__ void __launch_bounds__(256) k_resize_bwd_w(const float *__restrict__ 
   float s = 0.f;
   for (int o = lo; o <= hi; ++o) {
     const Tap tw = tap(o, sw, Wi);
-    if (tw.i0 == j) s += tw.l0 * gr[o];
-    if (tw.i1 == j) s += tw.l1 * gr[o];
+    const float gv = gr[o];
+    s += (tw.i0 == j ? tw.l0 : 0.f) * gv + (tw.i1 == j ? tw.l1 : 0.f) * gv;
   }
   t[(long long)pl * Ho * Wi + i] = s;
 }
@@ -88,8 +88,8 @@ __global__ void __launch_bounds__(256) k_resize_bwd_h(const float *__restrict__ 
   float s = 0.f;
   for (int o = lo; o <= hi; ++o) {
     const Tap th = tap(o, sh, Hi);
-    if (th.i0 == i) s += th.l0 * tp[(long long)o * Wi];
-    if (th.i1 == i) s += th.l1 * tp[(long long)o * Wi];
+    const float tv = tp[(long long)o * Wi];
+    s += (th.i0 == i ? th.l0 : 0.f) * tv + (th.i1 == i ? th.l1 : 0.f) * tv;
   }
   gx[idx] = accumulate ? gx[idx] + s : s;
 }
