@@ -8,7 +8,9 @@ B-sample batch (4 x 256x256 cameras) that is resident in HBM bef
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
 N>1 is launched by torch.distributed.run (one rank per GPU, RCCL over xGMI): each rank runs
-B samples per step (weak scaling) and gradients are all-reduced (the only exchange).
+B samples per step (weak scaling) and the flat gradient buffer is all-reduced (the only
+exchange).  The step is captured into HIP graphs during warm-up (e2ep_amd.train.TrainStep;
+--eager disables capture).
 Rank 0 prints ONE JSON line.
 """
 import argparse
@@ -33,17 +35,6 @@ def lss_fwd_bytes(B, N=4, C=64, D=48, hw=1024, XY=40000):
     """Algorithmic HBM bytes of one fused lift-splat forward launch:
     read featT + prob once, write the C x X x Y BEV planes once, per sample."""
     return 4 * B * (N * C * hw + N * D * hw + C * XY)
-
-
-class _Step(torch.nn.Module):
-    """Wraps training_step as forward so DistributedDataParallel can hook it."""
-
-    def __init__(self, mod):
-        super().__init__()
-        self.mod = mod
-
-    def forward(self, batch):
-        return self.mod.training_step(batch, 0)
 
 
 def device_batch(data, dev):
@@ -94,6 +85,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="samples per GPU per step")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,6 +97,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from e2ep_amd import _lib, synthetic, timing
+    from e2ep_amd.train import TrainStep
     from tool.config import default_cfg
     from trainer.pl_trainer import ParkingTrainingModule
 
@@ -115,26 +108,16 @@ def main():
     # it never has a gradient, so it is kept out of the reducer and the optimizer step.
     for p in mod.parking_model.bev_encoder.layer4.parameters():
         p.requires_grad_(False)
-    opt = mod.configure_optimizers()["optimizer"]
-    step_mod = _Step(mod)
-    if world > 1:
-        from torch.nn.parallel import DistributedDataParallel as DDP
-        step_mod = DDP(step_mod, device_ids=[local], broadcast_buffers=False, bucket_cap_mb=32,
-                       gradient_as_bucket_view=True)
-
     data = device_batch(synthetic.synthetic_batch(args.batch, seed=rank), dev)
-
-    def step():
-        loss = step_mod(data)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        opt.step()
-        return loss
-
-    for _ in range(args.warmup):
-        step()
-    timing.reset()
-    timing.enable(True)
+    if world > 1:  # identical initial weights on every rank (DDP's init broadcast)
+        for t in list(mod.parameters()) + list(mod.buffers()):
+            dist.broadcast(t.data, 0)
+    # warm-up steps (the first ones also capture the step into HIP graphs)
+    step = TrainStep(mod, data, lr=mod.cfg.learning_rate, weight_decay=mod.cfg.weight_decay,
+                     world=world, graph=not args.eager, warmup=max(1, args.warmup))
+    if args.eager:
+        for _ in range(args.warmup):
+            step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -145,6 +128,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # per-kernel HIP-event timing: a few eager steps on the same stream after the timed
+    # region (graph replays cannot be bracketed per kernel from the host)
+    timing.reset()
+    timing.enable(True)
+    for _ in range(3):
+        step._fwd_bwd()
     timing.enable(False)
     kern = timing.summary()
     if world > 1:

@@ -32,9 +32,15 @@ def depth_onehot(gt, d_bound, down):
 
 
 def depth_bce(prob, gt, d_bound, down):
-    """loss/depth_loss.py:18-28: BCE on foreground cells, summed / max(1, #fg)."""
+    """loss/depth_loss.py:18-28: BCE on foreground cells, summed / max(1, #fg).
+
+    The reference selects the foreground rows with a boolean index (a data-dependent shape,
+    i.e. a device->host sync); here every row is evaluated and the background rows are
+    multiplied by 0, which gives the same sum without a sync (graph-capturable).  BCE keeps
+    PyTorch's log clamp at -100."""
     lab = depth_onehot(gt.to(prob.device), d_bound, down)
     D = lab.shape[1]
-    p = prob.permute(0, 2, 3, 1).contiguous().view(-1, D)
-    fg = lab.max(dim=1).values > 0.0
-    return F.binary_cross_entropy(p[fg], lab[fg], reduction="none").sum() / fg.sum().clamp(min=1.0)
+    p = prob.permute(0, 2, 3, 1).reshape(-1, D)
+    fg = (lab.max(dim=1).values > 0.0).to(prob.dtype)
+    ll = lab * torch.clamp(torch.log(p), min=-100.0) + (1 - lab) * torch.clamp(torch.log1p(-p), min=-100.0)
+    return -(ll.sum(dim=1) * fg).sum() / fg.sum().clamp(min=1.0)

@@ -1,8 +1,9 @@
 """HIP-event timing of individual kernel launches, on the stream each kernel runs on.
 
-bench.py enables it over its timed region to measure the dominant kernel's average launch
-duration live (the `roofline.achieved` figure); it is off by default and then costs one
-boolean test per launch."""
+bench.py enables it for a few eager steps right after its timed (graph-replayed) region to
+measure the dominant kernel's average launch duration live (the `roofline.achieved`
+figure); it is off by default and then costs one boolean test per launch.  Never enable it
+while a step is being captured into a HIP graph."""
 from collections import defaultdict
 from contextlib import contextmanager
 

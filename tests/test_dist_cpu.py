@@ -1,0 +1,67 @@
+"""N>1 data-parallel path of TrainStep on CPU: world_size 2 over gloo (127.0.0.1).
+
+Each rank steps its own half of the batch; the flat gradient buffer's single all-reduce of
+loss/world gradients must reproduce one step over the whole batch on one process
+(DistributedDataParallel semantics, reference pl_train.py:47 strategy 'ddp')."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _Tiny(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.conv = torch.nn.Conv2d(3, 4, 3, padding=1)
+        self.head = torch.nn.Linear(4, 2)
+        self.frozen = torch.nn.Linear(2, 2)  # no grad, like bev_encoder.layer4
+        for p in self.frozen.parameters():
+            p.requires_grad_(False)
+
+    def training_step(self, batch, idx=0):
+        h = self.conv(batch["x"]).relu().mean((2, 3))
+        return torch.nn.functional.mse_loss(self.head(h), batch["y"])
+
+
+def _data():
+    g = torch.Generator().manual_seed(5)
+    return {"x": torch.randn(4, 3, 8, 8, generator=g), "y": torch.randn(4, 2, generator=g)}
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from e2ep_amd.train import TrainStep
+    d = _data()
+    half = {k: v[rank * 2:(rank + 1) * 2] for k, v in d.items()}
+    m = _Tiny()
+    s = TrainStep(m, half, lr=1e-2, world=world, graph=False)
+    for _ in range(3):
+        s()
+    out[rank] = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    dist.destroy_process_group()
+
+
+def _port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def test_two_rank_step_equals_full_batch_step():
+    from e2ep_amd.train import TrainStep
+    ref = _Tiny()
+    s = TrainStep(ref, _data(), lr=1e-2, world=1, graph=False)
+    for _ in range(3):
+        s()
+    want = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_worker, args=(2, _port(), out), nprocs=2, join=True)
+        got0, got1 = out[0], out[1]
+    assert torch.equal(got0, got1)  # ranks stay in lock-step
+    assert torch.allclose(got0, want, rtol=1e-5, atol=1e-6)
+    assert torch.equal(ref.frozen.weight, _Tiny().frozen.weight)  # untouched
