@@ -367,6 +367,11 @@ __global__ void k_rig(const float *__restrict__ K, const float *__restrict__ E, 
   }
 }
 
+__global__ void k_zero_i32(int *p, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0;
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -406,11 +411,10 @@ int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int 
   int *cnt = static_cast<int *>(workspace);
   const int P = N * D * h * w;
   const long long total = (long long)B * P;
-  hipError_t e = hipMemsetAsync(cnt, 0, (size_t)B * XYZ * sizeof(int), s);
-  if (e != hipSuccess) {
-    set_error("e2ep_lss_plan: memset: %s", hipGetErrorString(e));
-    return (int)e;
-  }
+  // zero the counters with a kernel, not hipMemsetAsync: memset nodes do not replay
+  // correctly from captured HIP graphs on this stack (csrc/graph.hip)
+  hipLaunchKernelGGL(k_zero_i32, dim3(cdiv((long long)B * XYZ, 256)), dim3(256), 0, s, cnt,
+                     (long long)B * XYZ);
   hipLaunchKernelGGL(k_count, dim3(cdiv(total, 256)), dim3(256), 0, s, pillar, P, XYZ, total, cnt);
   // scan writes offsets and re-uses the count buffer as the fill cursor
   hipLaunchKernelGGL(k_scan, dim3(B), dim3(1024), 0, s, cnt, XYZ, offsets, cnt);

@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("E2EP_LIB", os.path.join(_HERE, "libe2ep_hip.so"))
 
 _p, _i, _i64, _f, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_size_t
+_d = ctypes.c_double
 _fp3 = ctypes.POINTER(ctypes.c_float)
 
 # name -> (restype, argtypes); must match include/e2ep.h
@@ -54,6 +55,10 @@ SIGNATURES = {
     "e2ep_avgpool_bwd": (_i, [_p, _i, _i, _p, _p]),
     "e2ep_se_gate_fwd": (_i, [_p, _p, _i, _i, _p, _p]),
     "e2ep_se_gate_bwd": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),
+    "e2ep_adam_chunk_elems": (_i, []),
+    "e2ep_adam_step": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _d, _d, _f, _p]),
+    "e2ep_grad_gather": (_i, [_p, _i, _p, _p, _p, _p]),
+    "e2ep_graph_replace_memsets": (_i, [_p, ctypes.POINTER(_i)]),
 }
 
 _LIB = None

@@ -1,54 +1,76 @@
 """Graph-captured training step for the ParkingModel (MI355X).
 
 The reference steps through PyTorch-Lightning eagerly (trainer/pl_trainer.py:55-83 +
-Adam at :116-121, DDP via pl_train.py:47).  Here one step — zero grads, forward, the three
-losses, backward and the Adam update — is captured once into a HIP graph and replayed, so
-the ~1,500 kernel launches of a step cost one launch from the host.
+Adam at :116-121, DDP via pl_train.py:47).  Here one step — forward, the three losses,
+backward and the Adam update — is captured once into HIP graphs and replayed, so the
+~1,500 kernel launches of a step cost a few launches from the host.
 
-Data parallelism (one process per GPU, RCCL over xGMI): gradients live in ONE flat fp32
-buffer (every parameter's .grad is a view into it), so the exchange is a single RCCL
-all-reduce of 78 MB per step between the captured backward graph and the captured optimizer
-graph; the loss is pre-scaled by 1/world so the all-reduce sum is the mean gradient
-(DistributedDataParallel semantics, without its per-bucket hooks).  bev_encoder.layer4 has
-no gradient (never run, reference model/bev_encoder.py:21) and is left out of the buffer.
+Optimizer: e2ep_amd.optim.FlatAdam (one fused launch over a flat parameter buffer; the
+gradients are read where autograd left them).
+
+Data parallelism (one process per GPU, RCCL over xGMI): after backward the gradients are
+gathered into one flat fp32 buffer (one launch), that buffer is all-reduced once per step
+(sum; the 1/world mean is folded into the Adam launch — DistributedDataParallel's averaging,
+without its per-bucket hooks), then the optimizer graph runs.  The all-reduce stays outside
+the graphs.  bev_encoder.layer4 has no gradient (never run, reference
+model/bev_encoder.py:21): callers freeze it so it is not part of the step.
+
+Graph replay order per step: g_bwd (fwd + losses + bwd) -> [g_gather -> all-reduce] -> g_opt.
+Graphs are captured through e2ep_amd.graphs.capture, which repairs memset nodes (they do
+not replay correctly on this ROCm stack) before instantiation.
 """
 import torch
 import torch.distributed as dist
 
+from . import graphs
+from .optim import FlatAdam
+
 
 class TrainStep:
     def __init__(self, module, batch, lr=1e-4, weight_decay=1e-4, world=1, graph=True,
-                 warmup=3):
+                 warmup=3, optimizer=None):
         self.module = module
         self.batch = batch
         self.world = world
         self.graph = graph
         self.params = [p for p in module.parameters() if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        for p in self.params:
-            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
-            off += p.numel()
-        self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay,
-                                    capturable=graph, foreach=True)
-        self.scale = 1.0 / world
+        self.opt = optimizer if optimizer is not None else FlatAdam(
+            self.params, lr=lr, weight_decay=weight_decay)
+        self.flat_grad = (torch.zeros(self.opt.numel, dtype=torch.float32,
+                                      device=self.params[0].device) if world > 1 else None)
         self.loss = None
-        self.g_bwd = self.g_opt = None
+        self.g_bwd = self.g_gather = self.g_opt = None
         if graph:
             self._capture(warmup)
 
-    # -- eager pieces ---------------------------------------------------------------------
+    # -- pieces ---------------------------------------------------------------------------
     def _fwd_bwd(self):
-        self.flat_grad.zero_()
+        self.opt.zero_grad(set_to_none=True)  # autograd hands its gradient tensors over
         loss = self.module.training_step(self.batch, 0)
-        (loss * self.scale if self.world > 1 else loss).backward()
+        loss.backward()
         return loss.detach()
+
+    def _gather(self):
+        if self.world > 1:
+            self.opt.gather_grads(self.flat_grad)
 
     def _allreduce(self):
         if self.world > 1:
             dist.all_reduce(self.flat_grad)
+
+    def _update(self):
+        if self.world > 1:
+            self.opt.step(self.flat_grad, 1.0 / self.world)
+        else:
+            self.opt.step()
+
+    def _eager(self):
+        loss = self._fwd_bwd()
+        self.opt.prepare()
+        self._gather()
+        self._allreduce()
+        self._update()
+        return loss
 
     # -- capture --------------------------------------------------------------------------
     def _capture(self, warmup):
@@ -56,17 +78,15 @@ class TrainStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self._fwd_bwd()
-                self._allreduce()
-                self.opt.step()
+                self._eager()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        self.g_bwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_bwd):
-            self.loss = self._fwd_bwd()
-        self.g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_opt, pool=self.g_bwd.pool()):
-            self.opt.step()
+        self.g_bwd, self.loss, self.memsets = graphs.capture(self._fwd_bwd)
+        # the captured gradients keep their (graph-pool) addresses on every replay
+        self.opt.prepare()
+        if self.world > 1:
+            self.g_gather, _, _ = graphs.capture(self._gather, pool=self.g_bwd.pool())
+        self.g_opt, _, _ = graphs.capture(self._update, pool=self.g_bwd.pool())
 
     def __call__(self, batch=None):
         """One training step; `batch` (optional) is copied into the captured input buffers."""
@@ -75,11 +95,11 @@ class TrainStep:
                 if torch.is_tensor(v) and torch.is_tensor(self.batch.get(k)) and self.batch[k].is_cuda:
                     self.batch[k].copy_(v, non_blocking=True)
         if not self.graph:
-            self.loss = self._fwd_bwd()
-            self._allreduce()
-            self.opt.step()
+            self.loss = self._eager()
             return self.loss
         self.g_bwd.replay()
-        self._allreduce()
+        if self.world > 1:
+            self.g_gather.replay()
+            self._allreduce()
         self.g_opt.replay()
         return self.loss

@@ -11,7 +11,7 @@ def encoder(stack, tokens):
     return stack(tokens.transpose(0, 1)).transpose(0, 1)
 
 
-def decoder(stack, tgt, memory, tgt_mask, tgt_key_padding_mask):
+def decoder(stack, tgt, memory, tgt_mask, tgt_key_padding_mask, tgt_is_causal=None):
     y = stack(tgt=tgt.transpose(0, 1), memory=memory.transpose(0, 1), tgt_mask=tgt_mask,
-              tgt_key_padding_mask=tgt_key_padding_mask)
+              tgt_key_padding_mask=tgt_key_padding_mask, tgt_is_causal=tgt_is_causal)
     return y.transpose(0, 1)

@@ -31,11 +31,16 @@ class ControlPredict(nn.Module):
         """Causal float mask (0 on/below the diagonal, -inf above) + PAD key mask."""
         L = tgt.shape[1]
         causal = torch.full((L, L), float("-inf"), device=tgt.device).triu(1)
+        self._causal_mask = causal
         return causal, tgt == self.pad_idx
 
     def decoder(self, encoder_out, tgt_embedding, tgt_mask, tgt_padding_mask):
+        # A mask made by create_mask is known to be causal: saying so skips torch's
+        # device->host comparison of the mask (a sync that also breaks HIP-graph capture);
+        # torch reaches the same decision (causal) by that comparison in the reference.
+        causal = True if tgt_mask is getattr(self, "_causal_mask", None) else None
         return transformer.decoder(self.tf_decoder, tgt_embedding, encoder_out, tgt_mask,
-                                   tgt_padding_mask)
+                                   tgt_padding_mask, causal)
 
     def forward(self, encoder_out, tgt):
         tgt = tgt[:, :-1]

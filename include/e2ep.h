@@ -212,6 +212,34 @@ int e2ep_se_gate_fwd(const float *x, const float *a, int planes, int HW, float *
 int e2ep_se_gate_bwd(const float *x, const float *a, const float *dy, int planes, int HW,
                      float *dx, float *da, void *stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Optimizer: fused Adam over one flat parameter buffer (replaces torch.optim.Adam configured
+ * at trainer/pl_trainer.py:116-121; torch Adam semantics: L2 weight decay added to the
+ * gradient, bias-corrected step, no amsgrad).
+ * chunks[4*n_chunks] = {tensor, start element, length (<= e2ep_adam_chunk_elems()), 0};
+ * offsets[tensor] = element offset of the tensor in the flat
+ * param / exp_avg / exp_avg_sq buffers (multiple of 4).  Gradients come from grad_ptrs
+ * (device array of per-tensor device addresses; 0 = no gradient, tensor not stepped) or,
+ * if grad_flat is non-null, from a flat buffer laid out like the parameters.  `step` is a
+ * device fp32 counter incremented by the call (graph-capturable: no host scalars change).
+ * ------------------------------------------------------------------------------------- */
+int e2ep_adam_chunk_elems(void);
+int e2ep_adam_step(const int *chunks, int n_chunks, const long long *offsets,
+                   const long long *grad_ptrs, const float *grad_flat, float *param, float *exp_avg,
+                   float *exp_avg_sq, float *step, double lr, double beta1, double beta2,
+                   double eps, double weight_decay, float grad_scale, void *stream);
+/* per-tensor gradients -> flat buffer (zeros for missing gradients), for one all-reduce */
+int e2ep_grad_gather(const int *chunks, int n_chunks, const long long *offsets,
+                     const long long *grad_ptrs, float *grad_flat, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * HIP-graph surgery: replace every memset node of a captured (not yet instantiated)
+ * hipGraph_t by an equivalent kernel node.  Memset nodes replay incorrectly after the first
+ * launch on this ROCm stack; PyTorch's reductions capture them.  `replaced` (optional)
+ * receives the number of nodes rewritten.
+ * ------------------------------------------------------------------------------------- */
+int e2ep_graph_replace_memsets(void *graph, int *replaced);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,34 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
+class _HostSGD:
+    """Host stand-in for FlatAdam's interface (prepare / gather_grads / step with a flat,
+    scaled gradient), so TrainStep's data-parallel orchestration runs on CPU ranks.  The
+    HIP optimizer itself is covered by tests/test_optim_gpu.py."""
+
+    def __init__(self, params, lr):
+        self.params, self.lr = list(params), lr
+        self.numel = sum(p.numel() for p in self.params)
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            p.grad = None
+
+    def prepare(self):
+        pass
+
+    def gather_grads(self, out):
+        out.copy_(torch.cat([p.grad.reshape(-1) for p in self.params]))
+
+    @torch.no_grad()
+    def step(self, grad_flat=None, grad_scale=1.0):
+        off = 0
+        for p in self.params:
+            g = p.grad if grad_flat is None else grad_flat[off:off + p.numel()].view_as(p)
+            p.sub_(self.lr * grad_scale * g)
+            off += p.numel()
+
+
 class _Tiny(torch.nn.Module):
     def __init__(self):
         super().__init__()
@@ -38,7 +66,8 @@ def _worker(rank, world, port, out):
     d = _data()
     half = {k: v[rank * 2:(rank + 1) * 2] for k, v in d.items()}
     m = _Tiny()
-    s = TrainStep(m, half, lr=1e-2, world=world, graph=False)
+    params = [p for p in m.parameters() if p.requires_grad]
+    s = TrainStep(m, half, world=world, graph=False, optimizer=_HostSGD(params, 1e-2))
     for _ in range(3):
         s()
     out[rank] = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
@@ -54,7 +83,8 @@ def _port():
 def test_two_rank_step_equals_full_batch_step():
     from e2ep_amd.train import TrainStep
     ref = _Tiny()
-    s = TrainStep(ref, _data(), lr=1e-2, world=1, graph=False)
+    params = [p for p in ref.parameters() if p.requires_grad]
+    s = TrainStep(ref, _data(), world=1, graph=False, optimizer=_HostSGD(params, 1e-2))
     for _ in range(3):
         s()
     want = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
