@@ -132,66 +132,119 @@ __global__ void __launch_bounds__(256) k_segsort(const int *__restrict__ offsets
 }
 
 // ------------------------------------------------------------------------------------------
-// fused forward: block = 64 consecutive pillars x 64 channels (4 waves x 16 channels);
-// lane owns one pillar and walks its sorted points; stores are 256-B coalesced per channel.
+// fused forward.  Block = 64 consecutive pillars of one sample x 64 channels; lane =
+// channel, so every point costs one broadcast depth probability and one coalesced 256-B
+// feature row (L2-resident: a sample's featT is 1 MB).  The block's points are contiguous
+// in `order`; the 4 waves split them at pillar boundaries into ~equal point counts, walk
+// them in sorted order (the same summation order as a sequential per-pillar sum), and
+// stage per-pillar sums in an LDS [channel][pillar] tile that is written out channel-major
+// with 256-B coalesced rows.  Codes and probabilities are gathered 64 points at a time
+// (lane = point) and broadcast with shuffles; feature rows are fetched FWD_UNROLL at a time
+// through a buffer descriptor (no per-load branch).  Block id -> (sample = id % B, tile =
+// id / B), so at B = 8 each XCD works on one sample and its featT stays in that XCD's L2.
 // ------------------------------------------------------------------------------------------
-constexpr int FWD_CPW = 16;  // channels per wave
+constexpr int FWD_TILE = 64;    // pillars per block
+constexpr int FWD_UNROLL = 8;   // feature rows in flight per wave
+
+__device__ __forceinline__ int first_ge(const int *O, int npil, int target, int lane) {
+  const bool ge = lane <= npil && O[lane] >= target;
+  const unsigned long long m = __ballot(ge);
+  return m ? __ffsll((long long)m) - 1 : npil;
+}
 
 __global__ void __launch_bounds__(256) k_lss_fwd(
     const float *__restrict__ prob, const float *__restrict__ featT,
-    const int *__restrict__ offsets, const int *__restrict__ order, int N, int D, int HW,
+    const int *__restrict__ offsets, const int *__restrict__ order, int B, int N, int D, int HW,
     int C, int XYZ, int P, float *__restrict__ bev, long long bev_bstride) {
+  __shared__ int O[FWD_TILE + 1];
+  __shared__ float tile[64][FWD_TILE + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.y;
-  const int q = blockIdx.x * 64 + lane;
-  const int c0 = blockIdx.z * 64 + wave * FWD_CPW;
-  if (c0 >= C) return;  // wave-uniform
-  float acc[FWD_CPW];
+  const int b = blockIdx.x % B, q0 = (blockIdx.x / B) * FWD_TILE;
+  const int c0 = blockIdx.y * 64;
+  const int npil = min(FWD_TILE, XYZ - q0);
+  const int *off = offsets + (long long)b * (XYZ + 1);
+  if ((int)threadIdx.x <= npil) O[threadIdx.x] = off[q0 + threadIdx.x];
+  __syncthreads();
+  const int base = O[0], T = O[npil] - base;
+  const int ps = wave == 0 ? 0 : first_ge(O, npil, base + (int)(((long long)wave * T) >> 2), lane);
+  const int pe = wave == 3 ? npil : first_ge(O, npil, base + (int)(((long long)(wave + 1) * T) >> 2), lane);
+  const int cc = c0 + lane;
+  const int *ord = order + (long long)b * P;
+  const __amdgpu_buffer_rsrc_t rf = rsrc(featT, 4LL * B * N * HW * C);
+  const int coff = cc < C ? cc * 4 : OOR;  // lanes past C read 0
+  const int HWC = HW * C;
+  int p = ps;
+  float acc = 0.f;
+  if (ps < pe) {
+    const int ke = O[pe];
+    int pend = O[p + 1];
+    for (int k0 = O[ps]; k0 < ke; k0 += 64) {
+      // lane-parallel gather of 64 point codes -> (feature row offset, probability)
+      const int k = k0 + lane;
+      int rowoff = 0;
+      float pr = 0.f;
+      if (k < ke) {
+        const int code = ord[k];
+        const int n = code >> 24, d = (code >> 16) & 255, pix = code & 65535;
+        const int bn = b * N + n;
+        pr = prob[((long long)bn * D + d) * HW + pix];
+        rowoff = (bn * HWC + pix * C) * 4;
+      }
+      const int cnt = min(64, ke - k0);
+      for (int j0 = 0; j0 < cnt; j0 += FWD_UNROLL) {
+        float f[FWD_UNROLL], w[FWD_UNROLL];
 #pragma unroll
-  for (int j = 0; j < FWD_CPW; ++j) acc[j] = 0.f;
-  if (q < XYZ) {
-    const int *off = offsets + (long long)b * (XYZ + 1);
-    const int beg = off[q], end = off[q + 1];
-    const int *ord = order + (long long)b * P;
-    const bool vec = (C % 4 == 0) && (c0 + FWD_CPW <= C);
-    for (int k = beg; k < end; ++k) {
-      const int code = ord[k];
-      const int n = code >> 24, d = (code >> 16) & 255, pix = code & 65535;
-      const long long bn = (long long)b * N + n;
-      const float pr = prob[(bn * D + d) * HW + pix];
-      const float *fp = featT + (bn * HW + pix) * C + c0;
-      if (vec) {
-#pragma unroll
-        for (int j = 0; j < FWD_CPW; j += 4) {
-          const float4 f4 = *reinterpret_cast<const float4 *>(fp + j);
-          acc[j + 0] += pr * f4.x;
-          acc[j + 1] += pr * f4.y;
-          acc[j + 2] += pr * f4.z;
-          acc[j + 3] += pr * f4.w;
+        for (int u = 0; u < FWD_UNROLL; ++u) {
+          const int ro = __shfl(rowoff, j0 + u, 64);
+          w[u] = __shfl(pr, j0 + u, 64);
+          f[u] = bload(rf, j0 + u < cnt ? ro + coff : OOR);
         }
-      } else {
 #pragma unroll
-        for (int j = 0; j < FWD_CPW; ++j)
-          if (c0 + j < C) acc[j] += pr * fp[j];
+        for (int u = 0; u < FWD_UNROLL; ++u) {
+          if (j0 + u >= cnt) break;
+          const int kk = k0 + j0 + u;
+          while (kk >= pend) {  // pillar p complete (wave-uniform)
+            tile[lane][p] = acc;
+            acc = 0.f;
+            ++p;
+            pend = O[p + 1];
+          }
+          acc += w[u] * f[u];
+        }
       }
     }
   }
-  if (q < XYZ) {
-    float *o = bev + (long long)b * bev_bstride + q;
-#pragma unroll
-    for (int j = 0; j < FWD_CPW; ++j)
-      if (c0 + j < C) o[(long long)(c0 + j) * XYZ] = acc[j];
+  for (; p < pe; ++p) {  // the last pillar and any empty ones
+    tile[lane][p] = acc;
+    acc = 0.f;
+  }
+  __syncthreads();
+  if (lane < npil) {
+    float *o = bev + (long long)b * bev_bstride + q0 + lane;
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      const int ch = wave * 16 + j;
+      if (c0 + ch < C) o[(long long)(c0 + ch) * XYZ] = tile[ch][lane];
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// backward: wave per pixel (lane = channel), d-loop over the pixel's <=64 depth bins.
-// grad_feat accumulates in a register; grad_prob[d] = sum over lanes, done for all d at once
-// by a recursive-halving transposed reduction (63 shuffles per pixel instead of 6 per bin).
+// backward: wave per pixel (lane = channel).  For one pixel of one camera, with q_d the
+// pillar of depth bin d and G the gathered gT rows:
+//   grad_feat[c] = sum_d prob[d] * G[d][c]      (register accumulation, d ascending)
+//   grad_prob[d] = sum_c G[d][c] * feat[c]      (cross-lane reduction)
+// The pixel's pillar indices and probabilities are loaded lane-parallel (lane = d) and
+// broadcast with shuffles; the gT rows are gathered BWD_CHUNK at a time (one coalesced 256-B
+// row per bin, all in flight together, masked bins read 0 through an out-of-range buffer
+// offset); the 16 per-lane products of a chunk are reduced across the wave with a
+// transposed halving (xor 8,4,2,1 keeps one value per lane, then xor 16,32), leaving
+// grad_prob[d0 + u] in lanes 16*k + u.  Results go through LDS for coalesced stores.
 // ------------------------------------------------------------------------------------------
 constexpr int BWD_PIX_PER_WAVE = 4;
 constexpr int BWD_WAVES = 4;
 constexpr int BWD_PIX = BWD_PIX_PER_WAVE * BWD_WAVES;  // pixels per block
+constexpr int BWD_CHUNK = 16;
 
 template <int HALF>
 __device__ __forceinline__ void halve(float *v, int lane) {
@@ -206,8 +259,8 @@ __device__ __forceinline__ void halve(float *v, int lane) {
 
 __global__ void __launch_bounds__(256) k_lss_bwd(
     const float *__restrict__ gT, const float *__restrict__ prob,
-    const float *__restrict__ featT, const int *__restrict__ pillar, int N, int D, int HW,
-    int C, int XYZ, float *__restrict__ grad_prob, float *__restrict__ grad_feat) {
+    const float *__restrict__ featT, const int *__restrict__ pillar, int B, int N, int D,
+    int HW, int C, int XYZ, float *__restrict__ grad_prob, float *__restrict__ grad_feat) {
   __shared__ float s_gp[64][BWD_PIX + 1];
   __shared__ float s_gf[64][BWD_PIX + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -215,33 +268,42 @@ __global__ void __launch_bounds__(256) k_lss_bwd(
   const int b = bn / N;
   const int pix0 = blockIdx.x * BWD_PIX;
   const bool lane_ok = lane < C;
-  const __amdgpu_buffer_rsrc_t rg = rsrc(gT, 4LL * gridDim.y / N * XYZ * C);
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gT, 4LL * B * XYZ * C);
+  const int rowbase = b * XYZ;
   for (int pp = 0; pp < BWD_PIX_PER_WAVE; ++pp) {
     const int lp = wave * BWD_PIX_PER_WAVE + pp;  // local pixel
     const int pix = pix0 + lp;
     if (pix >= HW) break;  // wave-uniform
     const float f = lane_ok ? featT[((long long)bn * HW + pix) * C + lane] : 0.f;
-    float gf = 0.f;
-    float v[64];
-    // branch-free: masked points (q < 0) and idle lanes read 0 via an out-of-range offset
-#pragma unroll
-    for (int d = 0; d < 64; ++d) {
-      v[d] = 0.f;
-      if (d < D) {  // D is uniform
-        const long long pidx = ((long long)bn * D + d) * HW + pix;
-        const int q = pillar[pidx];
-        const float g = bload(rg, (q >= 0 && lane_ok) ? ((b * XYZ + q) * C + lane) * 4 : OOR);
-        gf += g * prob[pidx];
-        v[d] = g * f;
-      }
+    int qd = -1;
+    float pd = 0.f;
+    if (lane < D) {
+      const long long pidx = ((long long)bn * D + lane) * HW + pix;
+      qd = pillar[pidx];
+      pd = prob[pidx];
     }
-    halve<32>(v, lane);
-    halve<16>(v, lane);
-    halve<8>(v, lane);
-    halve<4>(v, lane);
-    halve<2>(v, lane);
-    halve<1>(v, lane);
-    s_gp[lane][lp] = v[0];  // lane == d after the six halvings
+    float gf = 0.f, gp = 0.f;
+    for (int d0 = 0; d0 < D; d0 += BWD_CHUNK) {
+      float g[BWD_CHUNK];
+#pragma unroll
+      for (int u = 0; u < BWD_CHUNK; ++u) {
+        const int q = __shfl(qd, d0 + u, 64);  // -1 for d >= D (lanes past D hold -1)
+        g[u] = bload(rg, (q >= 0 && lane_ok) ? ((rowbase + q) * C + lane) * 4 : OOR);
+      }
+#pragma unroll
+      for (int u = 0; u < BWD_CHUNK; ++u) gf += __shfl(pd, d0 + u, 64) * g[u];
+#pragma unroll
+      for (int u = 0; u < BWD_CHUNK; ++u) g[u] *= f;
+      halve<8>(g, lane);
+      halve<4>(g, lane);
+      halve<2>(g, lane);
+      halve<1>(g, lane);
+      float t = g[0];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      if ((lane >> 4) == d0 / BWD_CHUNK) gp = t;  // lane d now holds grad_prob[d] (D <= 64)
+    }
+    s_gp[lane][lp] = gp;
     s_gf[lane][lp] = gf;
   }
   __syncthreads();
@@ -431,9 +493,11 @@ int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
   E2EP_REQUIRE(B > 0 && N > 0 && D > 0 && hw > 0 && C > 0 && XYZ > 0, E2EP_EINVAL,
                "e2ep_lss_fwd: bad shape");
   E2EP_REQUIRE(((uintptr_t)featT & 15) == 0, E2EP_EINVAL, "e2ep_lss_fwd: featT must be 16-B aligned");
-  dim3 grid(cdiv(XYZ, 64), B, cdiv(C, 64));
+  E2EP_REQUIRE(4LL * B * N * hw * C < 0x7fffffffLL, E2EP_ERANGE,
+               "e2ep_lss_fwd: featT over 2 GiB (32-bit buffer offsets)");
+  dim3 grid(cdiv(XYZ, FWD_TILE) * B, cdiv(C, 64));
   hipLaunchKernelGGL(k_lss_fwd, grid, dim3(256), 0, as_stream(stream), prob, featT, offsets, order,
-                     N, D, hw, C, XYZ, N * D * hw, bev, bev_bstride);
+                     B, N, D, hw, C, XYZ, N * D * hw, bev, bev_bstride);
   return launch_status("e2ep_lss_fwd");
 }
 
@@ -444,8 +508,10 @@ int e2ep_lss_bwd(const float *gT, const float *prob, const float *featT, const i
                "e2ep_lss_bwd: bad shape");
   E2EP_REQUIRE(C <= 64 && D <= 64, E2EP_ERANGE, "e2ep_lss_bwd: needs C<=64, D<=64 (got %d,%d)", C, D);
   dim3 grid(cdiv(hw, BWD_PIX), B * N);
-  hipLaunchKernelGGL(k_lss_bwd, grid, dim3(256), 0, as_stream(stream), gT, prob, featT, pillar, N, D,
-                     hw, C, XYZ, grad_prob, grad_feat);
+  E2EP_REQUIRE(4LL * B * XYZ * C < 0x7fffffffLL, E2EP_ERANGE,
+               "e2ep_lss_bwd: gT over 2 GiB (32-bit buffer offsets)");
+  hipLaunchKernelGGL(k_lss_bwd, grid, dim3(256), 0, as_stream(stream), gT, prob, featT, pillar, B,
+                     N, D, hw, C, XYZ, grad_prob, grad_feat);
   return launch_status("e2ep_lss_bwd");
 }
 
