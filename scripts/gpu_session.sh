@@ -17,7 +17,7 @@ run() {  # run <name> <timeout> <cmd...>
   return 0
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
-[[ $STEPS == *pytest* ]] && run pytest_gpu 600 python -m pytest tests -x -q -m gpu
+[[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
 [[ $STEPS == *smoke* ]]  && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]]  && run bench 600 python bench.py --steps 20 --warmup 5
 [[ $STEPS == *prof* ]]   && run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 --no-cpu-baseline
