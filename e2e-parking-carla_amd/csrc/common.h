@@ -39,6 +39,15 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int byte_off) {
 __device__ __forceinline__ int bload_i(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return (int)__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0);
 }
+// 16-B buffer load.  (__builtin_amdgcn_raw_buffer_load_b128 is lowered to a single dword
+// load by the ROCm 7.2 compiler, so the LLVM intrinsic is bound directly.)
+typedef float e2ep_f4 __attribute__((ext_vector_type(4)));
+__device__ e2ep_f4 e2ep_raw_buffer_load_v4f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
+                                              int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.v4f32");
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  const e2ep_f4 v = e2ep_raw_buffer_load_v4f32(r, byte_off, 0, 0);
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 0);
 }

@@ -132,7 +132,8 @@ __global__ void __launch_bounds__(256) k_segsort(const int *__restrict__ offsets
 }
 
 // ------------------------------------------------------------------------------------------
-// fused forward.  Block = 64 consecutive pillars of one sample x 64 channels; lane =
+// fused forward, general channel count (C % 4 != 0; the C = 64 product width uses
+// k_lss_fwd below).  Block = 64 consecutive pillars of one sample x 64 channels; lane =
 // channel, so every point costs one broadcast depth probability and one coalesced 256-B
 // feature row (L2-resident: a sample's featT is 1 MB).  The block's points are contiguous
 // in `order`; the 4 waves split them at pillar boundaries into ~equal point counts, walk
@@ -152,7 +153,7 @@ __device__ __forceinline__ int first_ge(const int *O, int npil, int target, int 
   return m ? __ffsll((long long)m) - 1 : npil;
 }
 
-__global__ void __launch_bounds__(256) k_lss_fwd(
+__global__ void __launch_bounds__(256) k_lss_fwd_narrow(
     const float *__restrict__ prob, const float *__restrict__ featT,
     const int *__restrict__ offsets, const int *__restrict__ order, int B, int N, int D, int HW,
     int C, int XYZ, int P, float *__restrict__ bev, long long bev_bstride) {
@@ -226,6 +227,201 @@ __global__ void __launch_bounds__(256) k_lss_fwd(
       const int ch = wave * 16 + j;
       if (c0 + ch < C) o[(long long)(c0 + ch) * XYZ] = tile[ch][lane];
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// fused forward, v2 (default).  Block = T consecutive pillars of one sample x 64 channels,
+// 16 groups of 16 lanes; a lane owns 4 channels, so one point's 256-B feature row is one
+// 16-B load per lane and a wave has 4 points' rows per load instruction (8 in flight per
+// group = 32 rows per wave).  The block's points (contiguous in `order`) are cut into 16
+// equal chunks at arbitrary positions, one per group, so every group does the same work
+// whatever the pillar sizes.  A group walks its chunk in sorted order, keeping one running
+// float4 sum (fma); on a pillar change it stores the sum into an LDS [channel][pillar] tile
+// (zeroed first, so empty pillars read 0).  The chunk's first pillar may have started in the
+// previous chunk: its partial sum goes to a per-group carry slot instead, and after a barrier
+// the 16 carries are added in group order — a fixed summation order, so the result is
+// deterministic.  Point codes are prefetched a batch ahead; codes and probabilities are
+// gathered lane-parallel (16 per group) and broadcast inside the 16-lane row with DPP
+// row_newbcast folded into the consuming instruction (no LDS traffic).  The tile is written
+// out channel-major with 16-B stores.  Block id -> (sample = id % B, tile = tiles[b][id / B]):
+// one sample per XCD at B = 8 (its 1 MB featT stays in that XCD's L2), heaviest tiles first.
+// Measured (rocprofv3, B = 8, 4 cams): 37 us vs 61 us for v1; per-block traces
+// (scripts/trace_lss_fwd.py) show a block lifetime of ~4 us fixed (offsets -> codes ->
+// rows round trips, 16 KB write-out) + ~25 ns per point: latency-bound, not HBM-bound.
+// ------------------------------------------------------------------------------------------
+
+template <int J>
+__device__ __forceinline__ int row_bcast(int v) {  // lane J of this lane's 16-lane row
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + J, 0xf, 0xf, true);
+}
+template <int J>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __builtin_bit_cast(float, row_bcast<J>(__builtin_bit_cast(int, v)));
+}
+
+// One 8-point step of a group's walk: lanes J0..J0+7 of the 16-lane row hold the batch's row
+// offsets / probabilities.  Slots past the chunk end carry probability 0 and row 0 (a valid
+// row), and their position is clamped to the chunk's last point, so they add exactly 0 and
+// never trigger a pillar change: no per-slot guards.
+template <int J0>
+__device__ __forceinline__ void fwd_step8(const __amdgpu_buffer_rsrc_t rf, int rowoff, float pr,
+                                          int lane_off, int kbase, int klast, int &p, int &pend,
+                                          const int *O, float4 &acc, bool &first, float *carry4,
+                                          int *carry_pg, float *tile_l, int TP, int lg) {
+  float4 f[8];
+  float w[8];
+#define E2EP_LD(U)                                               \
+  f[U] = bload4(rf, row_bcast<J0 + U>(rowoff) + lane_off);      \
+  w[U] = row_bcast<J0 + U>(pr);
+  E2EP_LD(0) E2EP_LD(1) E2EP_LD(2) E2EP_LD(3) E2EP_LD(4) E2EP_LD(5) E2EP_LD(6) E2EP_LD(7)
+#undef E2EP_LD
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (min(kbase + J0 + u, klast) >= pend) {  // pillar p complete (group-uniform)
+      if (first) {
+        *reinterpret_cast<float4 *>(carry4) = acc;
+        if (lg == 0) *carry_pg = p;
+        first = false;
+      } else {
+        tile_l[0 * TP + p] = acc.x;
+        tile_l[1 * TP + p] = acc.y;
+        tile_l[2 * TP + p] = acc.z;
+        tile_l[3 * TP + p] = acc.w;
+      }
+      acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      do {
+        ++p;
+        pend = O[p + 1];
+      } while (pend <= kbase + J0 + u);
+    }
+    acc.x = __builtin_fmaf(w[u], f[u].x, acc.x);
+    acc.y = __builtin_fmaf(w[u], f[u].y, acc.y);
+    acc.z = __builtin_fmaf(w[u], f[u].z, acc.z);
+    acc.w = __builtin_fmaf(w[u], f[u].w, acc.w);
+  }
+}
+
+__device__ long long *g_fwd_trace;  // diagnostics: per-block (start, end, hw id, points)
+
+template <int T, int NG>
+__global__ void __launch_bounds__(NG * 16) k_lss_fwd(
+    const float *__restrict__ prob, const float *__restrict__ featT,
+    const int *__restrict__ offsets, const int *__restrict__ order,
+    const int *__restrict__ tiles, int B, int N, int D, int HW, int C, int XYZ, int P,
+    float *__restrict__ bev, long long bev_bstride, int vec_out) {
+  constexpr int TP = T + 4;  // row pitch (16-B aligned rows)
+  constexpr int NTHR = NG * 16;
+  __shared__ int O[T + 1];
+  __shared__ __attribute__((aligned(16))) float tile[64 * TP];
+  __shared__ __attribute__((aligned(16))) float carry[NG][64];
+  __shared__ int carry_p[NG];
+  const int tid = threadIdx.x, g = tid >> 4, lg = tid & 15;
+  const long long t_start = __builtin_amdgcn_s_memrealtime();
+  const int b = blockIdx.x % B, rank = blockIdx.x / B;
+  const int ntiles = (XYZ + T - 1) / T;
+  const int q0 = (tiles && T == E2EP_LSS_TILE ? tiles[b * ntiles + rank] : rank) * T;
+  const int c0 = blockIdx.y * 64;
+  const int npil = min(T, XYZ - q0);
+  const int *off = offsets + (long long)b * (XYZ + 1);
+  for (int i = tid; i <= npil; i += NTHR) O[i] = off[q0 + i];
+  for (int i = tid; i < 16 * TP; i += NTHR)
+    reinterpret_cast<float4 *>(tile)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lg == 0) carry_p[g] = -1;
+  __syncthreads();
+  const int base = O[0], tot = O[npil] - base;
+  const int ks = base + (int)(((long long)g * tot) / NG);
+  const int ke = base + (int)(((long long)(g + 1) * tot) / NG);
+  if (ks < ke) {  // group-uniform
+    // p = the pillar holding point ks = #{j in [1, npil] : O[j] <= ks}
+    int cnt = 0;
+    for (int j = lg + 1; j <= npil; j += 16) cnt += O[j] <= ks;
+    cnt += __shfl_xor(cnt, 8, 64);
+    cnt += __shfl_xor(cnt, 4, 64);
+    cnt += __shfl_xor(cnt, 2, 64);
+    cnt += __shfl_xor(cnt, 1, 64);
+    int p = cnt, pend = O[p + 1];
+    bool first = true;
+    const int cc = c0 + 4 * lg;
+    // this lane's 16 B of a feature row; lanes past C read 0 (offset beyond the buffer)
+    const int lane_off = cc < C ? 4 * cc : 0x40000000;  // C % 4 == 0 (checked on the host)
+    const __amdgpu_buffer_rsrc_t rf = rsrc(featT, 4LL * B * N * HW * C);
+    const __amdgpu_buffer_rsrc_t rp = rsrc(prob, 4LL * B * N * D * HW);
+    const int HWC = HW * C, DHW = D * HW;
+    float *tile_l = tile + 4 * lg * TP;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    // point codes are prefetched one 16-point batch ahead (branch-free loads, so the
+    // compiler can leave the prefetch in flight)
+    const __amdgpu_buffer_rsrc_t ro_ = rsrc(order + (long long)b * P, 4LL * P);
+    int code_n = bload_i(ro_, ks + lg < ke ? (ks + lg) * 4 : OOR);
+    for (int k0 = ks; k0 < ke; k0 += 16) {
+      const int code = code_n;
+      const bool valid = k0 + lg < ke;
+      code_n = bload_i(ro_, k0 + 16 + lg < ke ? (k0 + 16 + lg) * 4 : OOR);
+      const int n = code >> 24, d = (code >> 16) & 255, pix = code & 65535;
+      const int bn = b * N + n;
+      const float pr = bload(rp, valid ? (bn * DHW + d * HW + pix) * 4 : OOR);
+      const int rowoff = valid ? (bn * HWC + pix * C) * 4 : 0;
+      const int klast = ke - 1;
+      fwd_step8<0>(rf, rowoff, pr, lane_off, k0, klast, p, pend, O, acc, first, &carry[g][4 * lg],
+                   &carry_p[g], tile_l, TP, lg);
+      if (k0 + 8 < ke)
+        fwd_step8<8>(rf, rowoff, pr, lane_off, k0, klast, p, pend, O, acc, first,
+                     &carry[g][4 * lg], &carry_p[g], tile_l, TP, lg);
+    }
+    if (first) {  // the chunk's last pillar
+      *reinterpret_cast<float4 *>(&carry[g][4 * lg]) = acc;
+      if (lg == 0) carry_p[g] = p;
+    } else {
+      tile_l[0 * TP + p] = acc.x;
+      tile_l[1 * TP + p] = acc.y;
+      tile_l[2 * TP + p] = acc.z;
+      tile_l[3 * TP + p] = acc.w;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // carries, in chunk order
+    for (int j = 0; j < NG; ++j) {
+      const int pc = carry_p[j];
+      if (pc >= 0) tile[tid * TP + pc] += carry[j][tid];
+    }
+  }
+  __syncthreads();
+  float *o = bev + (long long)b * bev_bstride + (long long)c0 * XYZ + q0;
+  const int nch = min(64, C - c0);
+  if (vec_out) {
+    constexpr int R4 = T / 4;  // float4 per tile row
+    for (int e = tid; e < 64 * R4; e += NTHR) {
+      const int ch = e / R4, i4 = e - ch * R4;
+      if (ch >= nch) break;
+      const int i = 4 * i4;
+      const float4 v = *reinterpret_cast<const float4 *>(&tile[ch * TP + i]);
+      float *dst = o + (long long)ch * XYZ + i;
+      if (i + 3 < npil) {
+        *reinterpret_cast<float4 *>(dst) = v;
+      } else {
+        if (i < npil) dst[0] = v.x;
+        if (i + 1 < npil) dst[1] = v.y;
+        if (i + 2 < npil) dst[2] = v.z;
+      }
+    }
+  } else {
+    for (int e = tid; e < 64 * T; e += NTHR) {
+      const int ch = e / T, i = e - ch * T;
+      if (ch >= nch) break;
+      if (i < npil) o[(long long)ch * XYZ + i] = tile[ch * TP + i];
+    }
+  }
+  if (g_fwd_trace && tid == 0) {
+    long long *r = g_fwd_trace + 4LL * (blockIdx.y * gridDim.x + blockIdx.x);
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    r[0] = t_start;
+    r[1] = __builtin_amdgcn_s_memrealtime();
+    r[2] = ((long long)xcc << 32) | hw;
+    r[3] = tot;
   }
 }
 
@@ -429,6 +625,26 @@ __global__ void k_rig(const float *__restrict__ K, const float *__restrict__ E, 
   }
 }
 
+// Tile schedule for k_lss_fwd: per sample, the T-pillar tiles ranked by point count,
+// heaviest first (ties by index), so the few dense tiles next to the ego vehicle (up to 5x
+// the mean) start at once instead of setting the kernel's tail.  One block per sample.
+constexpr int SCHED_MAX_TILES = 4096;
+__global__ void __launch_bounds__(1024) k_tile_schedule(const int *__restrict__ offsets, int XYZ,
+                                                        int T, int *__restrict__ tiles) {
+  __shared__ int cnt[SCHED_MAX_TILES];
+  const int b = blockIdx.x, nt = (XYZ + T - 1) / T;
+  const int *off = offsets + (long long)b * (XYZ + 1);
+  for (int t = threadIdx.x; t < nt; t += blockDim.x)
+    cnt[t] = off[min((t + 1) * T, XYZ)] - off[t * T];
+  __syncthreads();
+  for (int t = threadIdx.x; t < nt; t += blockDim.x) {
+    const int c = cnt[t];
+    int r = 0;
+    for (int u = 0; u < nt; ++u) r += cnt[u] > c || (cnt[u] == c && u < t);
+    tiles[(long long)b * nt + r] = t;
+  }
+}
+
 __global__ void k_zero_i32(int *p, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0;
@@ -463,8 +679,17 @@ int e2ep_rig_transforms(const float *K, const float *E, int BN, float *combine, 
 
 size_t e2ep_lss_plan_workspace(int B, int XYZ) { return (size_t)B * XYZ * sizeof(int); }
 
+int e2ep_debug_fwd_trace(void *dev_buf) {
+  long long *p = static_cast<long long *>(dev_buf);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_trace), &p, sizeof(p));
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int e2ep_lss_tiles(int XYZ) { return cdiv(XYZ, E2EP_LSS_TILE); }
+
 int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int XYZ,
-                  int32_t *offsets, int32_t *order, void *workspace, void *stream) {
+                  int32_t *offsets, int32_t *order, int32_t *tiles, void *workspace,
+                  void *stream) {
   E2EP_REQUIRE(B > 0 && XYZ > 0, E2EP_EINVAL, "e2ep_lss_plan: bad shape");
   E2EP_REQUIRE(N < 128 && D < 256 && h * w < 65536, E2EP_ERANGE,
                "e2ep_lss_plan: packed point code needs N<128, D<256, h*w<65536 (got %d,%d,%d)", N,
@@ -484,20 +709,34 @@ int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int 
                      XYZ, total, cnt, order);
   hipLaunchKernelGGL(k_segsort, dim3(cdiv((long long)B * XYZ, 256)), dim3(256), 0, s, offsets, P,
                      XYZ, B, order);
+  if (tiles) {
+    E2EP_REQUIRE(cdiv(XYZ, E2EP_LSS_TILE) <= SCHED_MAX_TILES, E2EP_ERANGE,
+                 "e2ep_lss_plan: %d tiles per sample exceed the scheduler's %d (pass tiles=NULL)",
+                 cdiv(XYZ, E2EP_LSS_TILE), SCHED_MAX_TILES);
+    hipLaunchKernelGGL(k_tile_schedule, dim3(B), dim3(1024), 0, s, offsets, XYZ, E2EP_LSS_TILE,
+                       tiles);
+  }
   return launch_status("e2ep_lss_plan");
 }
 
 int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
-                 const int32_t *order, int B, int N, int D, int hw, int C, int XYZ, float *bev,
-                 long long bev_bstride, void *stream) {
+                 const int32_t *order, const int32_t *tiles, int B, int N, int D, int hw, int C,
+                 int XYZ, float *bev, long long bev_bstride, void *stream) {
   E2EP_REQUIRE(B > 0 && N > 0 && D > 0 && hw > 0 && C > 0 && XYZ > 0, E2EP_EINVAL,
                "e2ep_lss_fwd: bad shape");
   E2EP_REQUIRE(((uintptr_t)featT & 15) == 0, E2EP_EINVAL, "e2ep_lss_fwd: featT must be 16-B aligned");
   E2EP_REQUIRE(4LL * B * N * hw * C < 0x7fffffffLL, E2EP_ERANGE,
                "e2ep_lss_fwd: featT over 2 GiB (32-bit buffer offsets)");
-  dim3 grid(cdiv(XYZ, FWD_TILE) * B, cdiv(C, 64));
-  hipLaunchKernelGGL(k_lss_fwd, grid, dim3(256), 0, as_stream(stream), prob, featT, offsets, order,
-                     B, N, D, hw, C, XYZ, N * D * hw, bev, bev_bstride);
+  if (C % 4 != 0) {  // general-width path: lane = channel
+    dim3 grid(cdiv(XYZ, FWD_TILE) * B, cdiv(C, 64));
+    hipLaunchKernelGGL(k_lss_fwd_narrow, grid, dim3(256), 0, as_stream(stream), prob, featT, offsets,
+                       order, B, N, D, hw, C, XYZ, N * D * hw, bev, bev_bstride);
+  } else {
+    const int vec = ((uintptr_t)bev & 15) == 0 && XYZ % 4 == 0 && bev_bstride % 4 == 0;
+    hipLaunchKernelGGL((k_lss_fwd<E2EP_LSS_TILE, 16>), dim3(cdiv(XYZ, E2EP_LSS_TILE) * B, cdiv(C, 64)),
+                       dim3(256), 0, as_stream(stream), prob, featT, offsets, order, tiles, B, N, D,
+                       hw, C, XYZ, N * D * hw, bev, bev_bstride, vec);
+  }
   return launch_status("e2ep_lss_fwd");
 }
 

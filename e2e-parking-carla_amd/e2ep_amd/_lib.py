@@ -23,8 +23,10 @@ SIGNATURES = {
     "e2ep_rig_transforms": (_i, [_p, _p, _i, _p, _p, _p]),
     "e2ep_geom_index": (_i, [_p, _p, _p, _fp3, _fp3, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_lss_plan_workspace": (_sz, [_i, _i]),
-    "e2ep_lss_plan": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
-    "e2ep_lss_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i64, _p]),
+    "e2ep_lss_tiles": (_i, [_i]),
+    "e2ep_debug_fwd_trace": (_i, [_p]),
+    "e2ep_lss_plan": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "e2ep_lss_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i64, _p]),
     "e2ep_lss_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "e2ep_transpose": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
     "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
@@ -94,6 +96,11 @@ def call(name, *args):
     rc = getattr(lib, name)(*args)
     if rc != 0:
         raise E2EPError(f"{name} failed ({rc}): {lib.e2ep_last_error().decode()}")
+
+
+def call_raw(name, *args):
+    """Call an entry point that returns a value rather than a status."""
+    return getattr(load(), name)(*args)
 
 
 def ptr(t):

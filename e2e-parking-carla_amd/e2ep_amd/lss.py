@@ -54,6 +54,7 @@ class LssPlan:
     pillar: torch.Tensor   # int32 [B*N*D*h*w], -1 = masked
     offsets: torch.Tensor  # int32 [B*(XYZ+1)]
     order: torch.Tensor    # int32 [B*N*D*h*w] packed point codes
+    tiles: torch.Tensor    # int32 [B*ntiles] forward tile schedule (heaviest first)
     B: int
     N: int
     D: int
@@ -87,10 +88,11 @@ def build_plan(frustum, combine, trans, lo, res, dims, device):
               _lib.host3(res), X, Y, Z, B, N, D, h, w, _lib.ptr(pillar), s)
     offsets = torch.empty(B * (XYZ + 1), dtype=torch.int32, device=device)
     order = torch.empty(B * P, dtype=torch.int32, device=device)
+    tiles = torch.empty(B * _lib.call_raw("e2ep_lss_tiles", XYZ), dtype=torch.int32, device=device)
     ws = torch.empty(B * XYZ, dtype=torch.int32, device=device)
     _lib.call("e2ep_lss_plan", _lib.ptr(pillar), B, N, D, h, w, XYZ, _lib.ptr(offsets),
-              _lib.ptr(order), _lib.ptr(ws), s)
-    return LssPlan(pillar, offsets, order, B, N, D, h, w, X, Y, Z)
+              _lib.ptr(order), _lib.ptr(tiles), _lib.ptr(ws), s)
+    return LssPlan(pillar, offsets, order, tiles, B, N, D, h, w, X, Y, Z)
 
 
 def transpose(x, rows, cols, batch, in_bstride=None):
@@ -112,7 +114,7 @@ class _LiftSplat(torch.autograd.Function):
         out = torch.empty(p.B, out_channels, p.X, p.Y, dtype=torch.float32, device=feat.device)
         with timing.region("lss_fwd"):
             _lib.call("e2ep_lss_fwd", _lib.ptr(prob), _lib.ptr(featT), _lib.ptr(p.offsets),
-                      _lib.ptr(p.order), p.B, p.N, p.D, hw, C, p.XYZ, _lib.ptr(out),
+                      _lib.ptr(p.order), _lib.ptr(p.tiles), p.B, p.N, p.D, hw, C, p.XYZ, _lib.ptr(out),
                       out_channels * p.XYZ, _lib.stream())
         ctx.save_for_backward(prob, featT)
         ctx.plan, ctx.C = plan, C

@@ -57,6 +57,10 @@ int e2ep_geom_index(const float *frustum, const float *combine, const float *tra
 /* Bytes of int32 workspace e2ep_lss_plan needs: B*X*Y*Z*4. */
 size_t e2ep_lss_plan_workspace(int B, int XYZ);
 
+/* Pillars per output tile of e2ep_lss_fwd, and tiles per sample (= ceil(XYZ / E2EP_LSS_TILE)). */
+#define E2EP_LSS_TILE 64
+int e2ep_lss_tiles(int XYZ);
+
 /* Counting sort of kept points by pillar (replaces the mask / argsort / cumsum-boundary
  * bookkeeping of model/bev_model.py:86-99 and tool/geometry.py:292-300).
  *   pillar [B*P] (P = N*D*h*w) from e2ep_geom_index
@@ -64,21 +68,30 @@ size_t e2ep_lss_plan_workspace(int B, int XYZ);
  *                        offsets[b*(XYZ+1)+q+1])
  *   order   [B*P] packed point codes (n<<24 | d<<16 | h*w index), ascending within a pillar,
  *           so every later sum has a fixed, run-to-run identical order.
- * Limits: N < 128, D < 256, h*w < 65536. */
+ *   tiles   [B*e2ep_lss_tiles(XYZ)] or NULL: per sample, the forward's output tiles ordered by
+ *           point count, heaviest first (a launch schedule; any permutation is correct).
+ * Limits: N < 128, D < 256, h*w < 65536; with tiles, e2ep_lss_tiles(XYZ) <= 4096. */
 int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int XYZ,
-                  int32_t *offsets, int32_t *order, void *workspace, void *stream);
+                  int32_t *offsets, int32_t *order, int32_t *tiles, void *workspace,
+                  void *stream);
 
 /* Fused depth-distribution x feature outer product + pillar sum-pooling, forward.
  * Replaces encoder_forward's outer product/permute (model/bev_model.py:64-71) and
  * proj_bev_feature's gather / VoxelsSumming / scatter (model/bev_model.py:74-107,
  * tool/geometry.py:289-305).  The (B,N,D,h,w,C) outer product is never materialised.
  *   prob  [B*N, D, h*w]   softmax depth distribution
- *   featT [B*N, h*w, C]   camera features, pixel-major (see e2ep_transpose)
+ *   featT [B*N, h*w, C]   camera features, pixel-major (see e2ep_transpose), 16-B aligned
+ *   offsets, order, tiles from e2ep_lss_plan (tiles may be NULL: natural tile order)
  *   bev   out: bev[b*bev_bstride + c*XYZ + q] for c < C, every q written (zeros included).
- */
+ * Each pillar is summed in a fixed order: deterministic, run to run. */
 int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
-                 const int32_t *order, int B, int N, int D, int hw, int C, int XYZ,
-                 float *bev, long long bev_bstride, void *stream);
+                 const int32_t *order, const int32_t *tiles, int B, int N, int D, int hw, int C,
+                 int XYZ, float *bev, long long bev_bstride, void *stream);
+
+/* Diagnostics only: when dev_buf != NULL every later e2ep_lss_fwd launch (C % 4 == 0 path)
+ * records per block {start, end (s_memrealtime, 100 MHz), XCC/HW id, points} as 4 int64 at
+ * dev_buf[4*block]; NULL turns it off.  Used by scripts/trace_lss_fwd.py. */
+int e2ep_debug_fwd_trace(void *dev_buf);
 
 /* Backward of e2ep_lss_fwd (replaces VoxelsSumming.backward, tool/geometry.py:307-317, and
  * the autograd of the outer product).  Gather formulation, no atomics, deterministic:

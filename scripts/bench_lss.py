@@ -31,6 +31,19 @@ def timeit(fn, iters):
     return ts[len(ts) // 2]
 
 
+def timeit_b2b(fn, iters):
+    """Mean of `iters` back-to-back launches between two events (launch gaps amortised)."""
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
@@ -58,7 +71,7 @@ def main():
 
     def fwd():
         _lib.call("e2ep_lss_fwd", _lib.ptr(prob), _lib.ptr(featT), _lib.ptr(plan.offsets),
-                  _lib.ptr(plan.order), B, N, D, hw, C, XY, _lib.ptr(bev), C * XY, _lib.stream())
+                  _lib.ptr(plan.order), None if os.environ.get("E2EP_NO_TILES") else _lib.ptr(plan.tiles), B, N, D, hw, C, XY, _lib.ptr(bev), C * XY, _lib.stream())
 
     def bwd():
         _lib.call("e2ep_lss_bwd", _lib.ptr(gT), _lib.ptr(prob), _lib.ptr(featT),
@@ -66,11 +79,10 @@ def main():
 
     fb = 4 * B * (N * C * hw + N * D * hw + C * XY)
     bb = 4 * B * (C * XY + 2 * N * C * hw + 2 * N * D * hw)
-    tf, tb = timeit(fwd, a.iters), timeit(bwd, a.iters)
-    print(f"lss_fwd B={B} N={N} {a.image}^2: {tf * 1e3:.1f} us  {fb / tf / 1e6:.0f} GB/s "
-          f"({fb / 1e6:.1f} MB algorithmic)")
-    print(f"lss_bwd B={B} N={N} {a.image}^2: {tb * 1e3:.1f} us  {bb / tb / 1e6:.0f} GB/s "
-          f"({bb / 1e6:.1f} MB algorithmic)")
+    for name, fn, nb in (("lss_fwd", fwd, fb), ("lss_bwd", bwd, bb)):
+        t1, t2 = timeit(fn, a.iters), timeit_b2b(fn, a.iters)
+        print(f"{name} B={B} N={N} {a.image}^2: single {t1 * 1e3:.1f} us ({nb / t1 / 1e6:.0f} GB/s), "
+              f"back-to-back {t2 * 1e3:.1f} us ({nb / t2 / 1e6:.0f} GB/s); {nb / 1e6:.1f} MB algorithmic")
 
 
 if __name__ == "__main__":

@@ -16,9 +16,10 @@ run() {  # run <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-STEPS=${STEPS:-pytest,smoke,bench,prof}
+STEPS=${STEPS:-pytest,smoke,bench,prof,pmc}
 [[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
 [[ $STEPS == *smoke* ]]  && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]]  && run bench 600 python bench.py --steps 20 --warmup 5
 [[ $STEPS == *prof* ]]   && run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 --no-cpu-baseline
+[[ $STEPS == *pmc* ]]    && run pmc_lss 600 bash scripts/pmc_lss.sh
 exit 0

@@ -91,6 +91,37 @@ def test_plan_invariants_batch_of_different_rigs():
             seg = codes[off[b][q]:off[b][q + 1]]
             assert np.all(np.diff(seg) > 0)
     assert not np.array_equal(pil[0], pil[1])
+    # forward tile schedule: a permutation per sample, heaviest tile first (ties by index)
+    T = 64
+    tiles = plan.tiles.view(2, -1).cpu().numpy()
+    for b in range(2):
+        nt = tiles.shape[1]
+        assert np.array_equal(np.sort(tiles[b]), np.arange(nt))
+        edges = np.minimum(np.arange(nt + 1) * T, 40000)
+        cnt = off[b][edges[1:]] - off[b][edges[:-1]]
+        assert np.array_equal(tiles[b], np.lexsort((np.arange(nt), -cnt)))
+
+
+def test_lss_fwd_schedule_does_not_change_result():
+    """Any tile order gives the bitwise-same BEV (each pillar's sum order is fixed); the
+    natural order (tiles=NULL) vs the heaviest-first schedule, C=64 and the C%4!=0 path."""
+    from e2ep_amd import _lib, lss
+    g = golden("geometry_4cam_256.npz")
+    B, N, D, hw = 2, 4, 48, 1024
+    plan = _plan_from_golden(g, B)
+    gl = torch.Generator().manual_seed(5)
+    prob = torch.rand(B * N, D, hw, generator=gl).to(DEV)
+    for C in (64, 12, 6):
+        featT = torch.randn(B * N, hw, C, generator=gl).to(DEV)
+        outs = []
+        for tiles in (plan.tiles, None):
+            bev = torch.full((B, C, 40000), float("nan"), device=DEV)
+            _lib.call("e2ep_lss_fwd", _lib.ptr(prob), _lib.ptr(featT), _lib.ptr(plan.offsets),
+                      _lib.ptr(plan.order), _lib.ptr(tiles), B, N, D, hw, C, 40000, _lib.ptr(bev),
+                      C * 40000, _lib.stream())
+            outs.append(bev.cpu())
+        assert torch.isfinite(outs[0]).all()
+        assert torch.equal(outs[0], outs[1])
 
 
 def _lss_inputs(m):
