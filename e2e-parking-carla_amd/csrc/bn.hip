@@ -37,185 +37,256 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
-// partial sums over a slice of the (n, hw) extent of channel c: grid (C, splits)
-__global__ void __launch_bounds__(256) k_bn_stats(const float *__restrict__ x, int N, int C,
-                                                  int HW, int splits, long long per,
-                                                  double *__restrict__ part) {
-  const int c = blockIdx.x, sp = blockIdx.y;
-  const int tot = N * HW;
-  const int beg = sp * (int)per, end = min(tot, beg + (int)per);
-  double s = 0.0, q = 0.0;
-  if ((HW & 3) == 0) {
-    // vectorised: slices never straddle an image when per % 4 == 0 and HW % 4 == 0
-    for (int i = beg + threadIdx.x * 4; i < end; i += 1024) {
-      const int n = i / HW, p = i - n * HW;
-      const float4 v = *reinterpret_cast<const float4 *>(x + ((size_t)n * C + c) * HW + p);
-      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
-      q += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
-    }
-  } else {
-    for (int i = beg + threadIdx.x; i < end; i += 256) {
-      const int n = i / HW, p = i - n * HW;
-      const double v = x[((size_t)n * C + c) * HW + p];
-      s += v;
-      q += v * v;
-    }
+// Channel-major iteration: channel c's data is N rows of HW floats at stride C*HW.  Kernels
+// walk it as one sequence of N*HWv vectors (VEC = 4 when HW % 4 == 0, else 1); vector t is
+// row n = t / HWv, column p = t % HWv.
+template <int VEC>
+struct Vec;
+template <>
+struct Vec<4> {
+  typedef float4 T;
+  static __device__ __forceinline__ float4 ld(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+  static __device__ __forceinline__ void st(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+  static __device__ __forceinline__ float get(const float4 &v, int i) {
+    return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
   }
+  static __device__ __forceinline__ void set(float4 &v, int i, float f) {
+    if (i == 0) v.x = f; else if (i == 1) v.y = f; else if (i == 2) v.z = f; else v.w = f;
+  }
+  static __device__ __forceinline__ float4 zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+};
+template <>
+struct Vec<1> {
+  typedef float T;
+  static __device__ __forceinline__ float ld(const float *p) { return *p; }
+  static __device__ __forceinline__ void st(float *p, float v) { *p = v; }
+  static __device__ __forceinline__ float get(const float &v, int) { return v; }
+  static __device__ __forceinline__ void set(float &v, int, float f) { v = f; }
+  static __device__ __forceinline__ float zero() { return 0.f; }
+};
+
+// fixed-order fp64 block reduction of two values (256 threads); result valid in every thread
+__device__ __forceinline__ void block_sum2(double &s, double &q) {
   __shared__ double rs[4], rq[4];
   s = wave_sum_d(s);
   q = wave_sum_d(q);
+  __syncthreads();  // rs/rq may still be read by a previous call
   if ((threadIdx.x & 63) == 0) {
     rs[threadIdx.x >> 6] = s;
     rq[threadIdx.x >> 6] = q;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    part[((long long)c * splits + sp) * 2 + 0] = (rs[0] + rs[1]) + (rs[2] + rs[3]);
-    part[((long long)c * splits + sp) * 2 + 1] = (rq[0] + rq[1]) + (rq[2] + rq[3]);
-  }
+  s = (rs[0] + rs[1]) + (rs[2] + rs[3]);
+  q = (rq[0] + rq[1]) + (rq[2] + rq[3]);
 }
 
-// mean / invstd per channel; running-stat update (momentum m): r = (1-m) r + m * stat
-__global__ void k_bn_finalize(const double *__restrict__ part, int C, int splits, long long cnt,
-                              float eps, float momentum, float *__restrict__ running_mean,
-                              float *__restrict__ running_var, float *__restrict__ mean,
-                              float *__restrict__ invstd) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int k = 0; k < splits; ++k) {
+// sum of channel c's `splits` partial pairs, fixed order (thread k takes entries k, k+256, ...)
+__device__ __forceinline__ void channel_partials(const double *__restrict__ part, int c,
+                                                 int splits, double &s, double &q) {
+  s = 0.0;
+  q = 0.0;
+  for (int k = threadIdx.x; k < splits; k += 256) {
     s += part[((long long)c * splits + k) * 2 + 0];
     q += part[((long long)c * splits + k) * 2 + 1];
   }
-  const double mu = s / (double)cnt;
-  double var = q / (double)cnt - mu * mu;
-  if (var < 0.0) var = 0.0;
-  mean[c] = (float)mu;
-  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (running_mean) {
-    const double unb = cnt > 1 ? var * (double)cnt / (double)(cnt - 1) : var;
-    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
-    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
-  }
+  block_sum2(s, q);
 }
 
-// eval-mode statistics from the running buffers
-__global__ void k_bn_eval_stats(const float *__restrict__ rm, const float *__restrict__ rv, int C,
-                                float eps, float *__restrict__ mean, float *__restrict__ invstd) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  mean[c] = rm[c];
-  invstd[c] = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+// drop-connect (efficientnet-pytorch, training): out = bn / keep * floor(keep + u[n])
+__device__ __forceinline__ float dc_scale(const float *dc_rand, float keep, int n, float z) {
+  return dc_rand ? __fmul_rn(__fdiv_rn(z, keep), floorf(__fadd_rn(keep, dc_rand[n]))) : z;
 }
 
-// y = act(gamma * (x - mean) * invstd + beta); grid covers N*C*HW/4 float4s (HW % 4 == 0)
-// or scalars otherwise.
-__global__ void __launch_bounds__(256) k_bn_apply(const float *__restrict__ x,
-                                                  const float *__restrict__ mean,
-                                                  const float *__restrict__ invstd,
-                                                  const float *__restrict__ gamma,
-                                                  const float *__restrict__ beta,
-                                                  const float *__restrict__ res, int C, int HW,
-                                                  int act, float *__restrict__ y) {
-  const int q = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (q >= HW) return;
-  const int c = blockIdx.y % C;
-  const size_t i = (size_t)blockIdx.y * HW + q;
-  if ((HW & 3) == 0) {
-    const float sc = invstd[c] * (gamma ? gamma[c] : 1.f);
-    const float sh = (beta ? beta[c] : 0.f) - mean[c] * sc;
-    float4 v = *reinterpret_cast<const float4 *>(x + i);
-    float4 r = res ? *reinterpret_cast<const float4 *>(res + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    v.x = act_fwd(v.x * sc + sh + r.x, act);
-    v.y = act_fwd(v.y * sc + sh + r.y, act);
-    v.z = act_fwd(v.z * sc + sh + r.z, act);
-    v.w = act_fwd(v.w * sc + sh + r.w, act);
-    *reinterpret_cast<float4 *>(y + i) = v;
-  } else {
-    for (int j = 0; j < 4 && q + j < HW; ++j) {
-      const float sc = invstd[c] * (gamma ? gamma[c] : 1.f);
-      const float sh = (beta ? beta[c] : 0.f) - mean[c] * sc;
-      y[i + j] = act_fwd(x[i + j] * sc + sh + (res ? res[i + j] : 0.f), act);
+// partial sums over a slice of channel c: grid (C, splits); slice = `per` vectors
+template <int VEC>
+__global__ void __launch_bounds__(256) k_bn_stats(const float *__restrict__ x, int N, int C,
+                                                  int HWv, int splits, int per,
+                                                  double *__restrict__ part) {
+  const int c = blockIdx.x, sp = blockIdx.y;
+  const int tot = N * HWv;
+  const int beg = sp * per, end = min(tot, beg + per);
+  double s = 0.0, q = 0.0;
+  for (int t = beg + threadIdx.x; t < end; t += 256) {
+    const int n = t / HWv, p = t - n * HWv;
+    const auto v = Vec<VEC>::ld(x + (((size_t)n * C + c) * HWv + p) * VEC);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const double d = Vec<VEC>::get(v, i);
+      s += d;
+      q += d * d;
     }
   }
+  block_sum2(s, q);
+  if (threadIdx.x == 0) {
+    part[((long long)c * splits + sp) * 2 + 0] = s;
+    part[((long long)c * splits + sp) * 2 + 1] = q;
+  }
 }
 
-// backward reduction: per channel, dz = dy * act'(z);  sums of dz and dz * xhat (fp64)
+// y = act(dc(gamma * (x - mean) * invstd + beta) + res); grid (C, chunks of `per` vectors).
+// Train: mean / invstd from the stats partials (fp64, biased variance); chunk 0 of each
+// channel publishes them and updates the running stats (unbiased variance).  Eval: from the
+// running stats.
+template <int VEC>
+__global__ void __launch_bounds__(256) k_bn_apply(
+    const float *__restrict__ x, const double *__restrict__ part, int splits, long long cnt,
+    float eps, float momentum, float *__restrict__ running_mean, float *__restrict__ running_var,
+    float *__restrict__ mean_out, float *__restrict__ invstd_out, const float *__restrict__ gamma,
+    const float *__restrict__ beta, const float *__restrict__ res,
+    const float *__restrict__ dc_rand, float dc_keep, int N, int C, int HWv, int per, int act,
+    float *__restrict__ y) {
+  const int c = blockIdx.x, j = blockIdx.y;
+  float mu, is;
+  if (part) {
+    double s, q;
+    channel_partials(part, c, splits, s, q);
+    const double m = s / (double)cnt;
+    double var = q / (double)cnt - m * m;
+    if (var < 0.0) var = 0.0;
+    mu = (float)m;
+    is = (float)(1.0 / sqrt(var + (double)eps));
+    if (j == 0 && threadIdx.x == 0) {
+      mean_out[c] = mu;
+      invstd_out[c] = is;
+      if (running_mean) {
+        const double unb = cnt > 1 ? var * (double)cnt / (double)(cnt - 1) : var;
+        running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * m);
+        running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+      }
+    }
+  } else {
+    mu = running_mean[c];
+    is = (float)(1.0 / sqrt((double)running_var[c] + (double)eps));
+    if (j == 0 && threadIdx.x == 0) {
+      mean_out[c] = mu;
+      invstd_out[c] = is;
+    }
+  }
+  const float sc = is * (gamma ? gamma[c] : 1.f);
+  const float sh = (beta ? beta[c] : 0.f) - mu * sc;
+  const int tot = N * HWv;
+  const int beg = j * per, end = min(tot, beg + per);
+  for (int t = beg + threadIdx.x; t < end; t += 256) {
+    const int n = t / HWv, p = t - n * HWv;
+    const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
+    auto v = Vec<VEC>::ld(x + off);
+    const auto r = res ? Vec<VEC>::ld(res + off) : Vec<VEC>::zero();
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const float z = dc_scale(dc_rand, dc_keep, n, Vec<VEC>::get(v, i) * sc + sh);
+      Vec<VEC>::set(v, i, act_fwd(z + Vec<VEC>::get(r, i), act));
+    }
+    Vec<VEC>::st(y + off, v);
+  }
+}
+
+// backward pieces shared by reduce and apply: from x, dy (and res / drop-connect), returns
+// xhat, dz (gradient at the activation input = dres) and dzb (gradient at the BN output)
+template <int VEC>
+struct BnBwdElem {
+  float mu, is, g, b;
+  const float *dc_rand;
+  float keep;
+  int act;
+  __device__ __forceinline__ void operator()(float xv, float dyv, float rv, int n, float &xh,
+                                             float &dz, float &dzb) const {
+    xh = (xv - mu) * is;
+    const float zb = xh * g + b;
+    dz = dyv * act_bwd(dc_scale(dc_rand, keep, n, zb) + rv, act);
+    dzb = dc_rand ? __fdiv_rn(__fmul_rn(dz, floorf(__fadd_rn(keep, dc_rand[n]))), keep) : dz;
+  }
+};
+
+// backward reduction: per channel sums of dzb and dzb * xhat (fp64); grid (C, splits)
+template <int VEC>
 __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
     const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
-    const float *__restrict__ beta, const float *__restrict__ res, int N, int C, int HW,
-    int splits, int act, double *__restrict__ part) {
+    const float *__restrict__ beta, const float *__restrict__ res,
+    const float *__restrict__ dc_rand, float dc_keep, int N, int C, int HWv, int splits, int per,
+    int act, double *__restrict__ part) {
   const int c = blockIdx.x, sp = blockIdx.y;
-  const int tot = N * HW;
-  const int per = (tot + splits - 1) / splits;
+  const int tot = N * HWv;
   const int beg = sp * per, end = min(tot, beg + per);
-  const float mu = mean[c], is = invstd[c];
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  const BnBwdElem<VEC> el{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f,
+                          dc_rand, dc_keep, act};
   double s = 0.0, q = 0.0;
-  for (int i = beg + threadIdx.x; i < end; i += 256) {
-    const int n = i / HW, p = i - n * HW;
-    const size_t off = ((size_t)n * C + c) * HW + p;
-    const float xh = (x[off] - mu) * is;
-    const float dz = dy[off] * act_bwd(xh * g + b + (res ? res[off] : 0.f), act);
-    s += dz;
-    q += (double)dz * xh;
+  for (int t = beg + threadIdx.x; t < end; t += 256) {
+    const int n = t / HWv, p = t - n * HWv;
+    const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
+    const auto xv = Vec<VEC>::ld(x + off);
+    const auto dv = Vec<VEC>::ld(dy + off);
+    const auto rv = res ? Vec<VEC>::ld(res + off) : Vec<VEC>::zero();
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float xh, dz, dzb;
+      el(Vec<VEC>::get(xv, i), Vec<VEC>::get(dv, i), Vec<VEC>::get(rv, i), n, xh, dz, dzb);
+      s += dzb;
+      q += (double)dzb * xh;
+    }
   }
-  __shared__ double rs[4], rq[4];
-  s = wave_sum_d(s);
-  q = wave_sum_d(q);
-  if ((threadIdx.x & 63) == 0) {
-    rs[threadIdx.x >> 6] = s;
-    rq[threadIdx.x >> 6] = q;
-  }
-  __syncthreads();
+  block_sum2(s, q);
   if (threadIdx.x == 0) {
-    part[((long long)c * splits + sp) * 2 + 0] = (rs[0] + rs[1]) + (rs[2] + rs[3]);
-    part[((long long)c * splits + sp) * 2 + 1] = (rq[0] + rq[1]) + (rq[2] + rq[3]);
+    part[((long long)c * splits + sp) * 2 + 0] = s;
+    part[((long long)c * splits + sp) * 2 + 1] = q;
   }
 }
 
-// dbeta[c] = sum dz, dgamma[c] = sum dz*xhat  (fixed-order combine of the slices)
-__global__ void k_bn_bwd_finalize(const double *__restrict__ part, int C, int splits,
-                                  float *__restrict__ dgamma, float *__restrict__ dbeta,
-                                  double *__restrict__ sums) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int k = 0; k < splits; ++k) {
-    s += part[((long long)c * splits + k) * 2 + 0];
-    q += part[((long long)c * splits + k) * 2 + 1];
+// dbeta[c] = sum dzb, dgamma[c] = sum dzb*xhat: only when no dx / dres is wanted
+__global__ void __launch_bounds__(256) k_bn_bwd_finalize(const double *__restrict__ part,
+                                                         int splits, float *__restrict__ dgamma,
+                                                         float *__restrict__ dbeta) {
+  const int c = blockIdx.x;
+  double s, q;
+  channel_partials(part, c, splits, s, q);
+  if (threadIdx.x == 0) {
+    if (dbeta) dbeta[c] = (float)s;
+    if (dgamma) dgamma[c] = (float)q;
   }
-  sums[2 * c] = s;
-  sums[2 * c + 1] = q;
-  if (dbeta) dbeta[c] = (float)s;
-  if (dgamma) dgamma[c] = (float)q;
 }
 
-// dx = gamma * invstd * (dz - (sum_dz + xhat * sum_dzxhat) / M)        (train)
-// dx = gamma * invstd * dz                                              (eval: train == 0)
+// dres = dz;  dx = gamma * invstd * (dzb - (sum_dzb + xhat * sum_dzbxhat) / M)   (train)
+//             dx = gamma * invstd * dzb                                          (eval)
+// grid (C, chunks); chunk 0 of each channel writes dgamma / dbeta.
+template <int VEC>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(
     const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
-    const float *__restrict__ beta, const float *__restrict__ res, const double *__restrict__ sums,
-    int C, int HW, long long cnt, int act, int train, float *__restrict__ dx,
-    float *__restrict__ dres) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= HW) return;
-  const int c = blockIdx.y % C;
-  const size_t i = (size_t)blockIdx.y * HW + q;
-  const float mu = mean[c], is = invstd[c];
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  const float xh = (x[i] - mu) * is;
-  const float dz = dy[i] * act_bwd(xh * g + b + (res ? res[i] : 0.f), act);
-  if (dres) dres[i] = dz;
-  float v = dz;
-  if (train) {
-    const float ms = (float)(sums[2 * c] / (double)cnt);
-    const float mq = (float)(sums[2 * c + 1] / (double)cnt);
-    v = dz - (ms + xh * mq);
+    const float *__restrict__ beta, const float *__restrict__ res,
+    const float *__restrict__ dc_rand, float dc_keep, const double *__restrict__ part,
+    int splits, long long cnt, int N, int C, int HWv, int per, int act, int train,
+    float *__restrict__ dx, float *__restrict__ dres, float *__restrict__ dgamma,
+    float *__restrict__ dbeta) {
+  const int c = blockIdx.x, j = blockIdx.y;
+  double s, q;
+  channel_partials(part, c, splits, s, q);
+  if (j == 0 && threadIdx.x == 0) {
+    if (dbeta) dbeta[c] = (float)s;
+    if (dgamma) dgamma[c] = (float)q;
   }
-  if (dx) dx[i] = g * is * v;
+  const float ms = (float)(s / (double)cnt), mq = (float)(q / (double)cnt);
+  const BnBwdElem<VEC> el{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f,
+                          dc_rand, dc_keep, act};
+  const float gis = el.g * el.is;
+  const int tot = N * HWv;
+  const int beg = j * per, end = min(tot, beg + per);
+  for (int t = beg + threadIdx.x; t < end; t += 256) {
+    const int n = t / HWv, p = t - n * HWv;
+    const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
+    const auto xv = Vec<VEC>::ld(x + off);
+    const auto dv = Vec<VEC>::ld(dy + off);
+    const auto rv = res ? Vec<VEC>::ld(res + off) : Vec<VEC>::zero();
+    auto ox = Vec<VEC>::zero(), orr = Vec<VEC>::zero();
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float xh, dz, dzb;
+      el(Vec<VEC>::get(xv, i), Vec<VEC>::get(dv, i), Vec<VEC>::get(rv, i), n, xh, dz, dzb);
+      Vec<VEC>::set(orr, i, dz);
+      Vec<VEC>::set(ox, i, gis * (train ? dzb - (ms + xh * mq) : dzb));
+    }
+    if (dres) Vec<VEC>::st(dres + off, orr);
+    if (dx) Vec<VEC>::st(dx + off, ox);
+  }
 }
 
 // elementwise activation forward/backward (for activations not fused into a BN)
@@ -239,6 +310,9 @@ static int bn_splits(long long per_channel, int C) {
   return (int)s;
 }
 
+// vectors per apply workgroup (4 per thread)
+constexpr int APPLY_PER = 1024;
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -247,59 +321,85 @@ extern "C" {
 
 size_t e2ep_bn_workspace(int N, int C, int H, int W) {
   const int sp = bn_splits((long long)N * H * W, C);
-  return (size_t)C * sp * 2 * sizeof(double) + (size_t)C * 2 * sizeof(double);
+  return (size_t)C * sp * 2 * sizeof(double);
 }
 
 int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const float *res,
-                float *running_mean, float *running_var, int N, int C, int H, int W, int train,
-                float momentum, float eps, int act, float *mean, float *invstd, float *y,
-                void *workspace, void *stream) {
-  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && N * C <= 65535 &&
-                   (long long)N * H * W < (1LL << 31), E2EP_EINVAL, "e2ep_bn_fwd: bad shape");
+                const float *dc_rand, float dc_keep, float *running_mean, float *running_var,
+                int N, int C, int H, int W, int train, float momentum, float eps, int act,
+                float *mean, float *invstd, float *y, void *workspace, void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
+               E2EP_EINVAL, "e2ep_bn_fwd: bad shape");
   E2EP_REQUIRE(act >= 0 && act <= 2, E2EP_EINVAL, "e2ep_bn_fwd: act must be 0/1/2");
+  E2EP_REQUIRE(train || (running_mean && running_var), E2EP_EINVAL,
+               "e2ep_bn_fwd: eval needs running stats");
+  E2EP_REQUIRE(!dc_rand || dc_keep > 0.f, E2EP_EINVAL, "e2ep_bn_fwd: drop-connect keep must be > 0");
   hipStream_t s = as_stream(stream);
   const int HW = H * W;
-  const long long per = (long long)N * HW;
+  const long long per_c = (long long)N * HW;
+  const bool v4 = (HW & 3) == 0;
+  const int HWv = v4 ? HW / 4 : HW;
+  const int totv = N * HWv;
+  double *part = nullptr;
+  int sp = 1;
   if (train) {
-    int sp = bn_splits(per, C);
-    long long pp = (per + sp - 1) / sp;
-    if ((HW & 3) == 0 && (pp & 3)) {  // keep vector slices aligned to whole float4s
-      pp = (pp + 3) & ~3LL;
-      sp = (int)((per + pp - 1) / pp);
-    }
-    double *part = static_cast<double *>(workspace);
-    hipLaunchKernelGGL(k_bn_stats, dim3(C, sp), dim3(256), 0, s, x, N, C, HW, sp, pp, part);
-    hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(C, 64)), dim3(64), 0, s, part, C, sp, per, eps,
-                       momentum, running_mean, running_var, mean, invstd);
-  } else {
-    E2EP_REQUIRE(running_mean && running_var, E2EP_EINVAL, "e2ep_bn_fwd: eval needs running stats");
-    hipLaunchKernelGGL(k_bn_eval_stats, dim3(cdiv(C, 64)), dim3(64), 0, s, running_mean, running_var,
-                       C, eps, mean, invstd);
+    sp = bn_splits(per_c, C);
+    const int per = cdiv(totv, sp);
+    sp = cdiv(totv, per);
+    part = static_cast<double *>(workspace);
+    if (v4)
+      hipLaunchKernelGGL(k_bn_stats<4>, dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
+    else
+      hipLaunchKernelGGL(k_bn_stats<1>, dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
   }
-  hipLaunchKernelGGL(k_bn_apply, dim3(cdiv(cdiv(HW, 4), 256), N * C), dim3(256), 0, s, x, mean,
-                     invstd, gamma, beta, res, C, HW, act, y);
+  const dim3 grid(C, cdiv(totv, APPLY_PER));
+  if (v4)
+    hipLaunchKernelGGL(k_bn_apply<4>, grid, dim3(256), 0, s, x, part, sp, per_c, eps, momentum,
+                       running_mean, running_var, mean, invstd, gamma, beta, res, dc_rand, dc_keep,
+                       N, C, HWv, APPLY_PER, act, y);
+  else
+    hipLaunchKernelGGL(k_bn_apply<1>, grid, dim3(256), 0, s, x, part, sp, per_c, eps, momentum,
+                       running_mean, running_var, mean, invstd, gamma, beta, res, dc_rand, dc_keep,
+                       N, C, HWv, APPLY_PER, act, y);
   return launch_status("e2ep_bn_fwd");
 }
 
 int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
-                const float *gamma, const float *beta, const float *res, int N, int C, int H, int W,
-                int train, int act, float *dx, float *dgamma, float *dbeta, float *dres,
-                void *workspace, void *stream) {
-  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && N * C <= 65535 &&
-                   (long long)N * H * W < (1LL << 31), E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
+                const float *gamma, const float *beta, const float *res, const float *dc_rand,
+                float dc_keep, int N, int C, int H, int W, int train, int act, float *dx,
+                float *dgamma, float *dbeta, float *dres, void *workspace, void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
+               E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
+  E2EP_REQUIRE(!dc_rand || dc_keep > 0.f, E2EP_EINVAL, "e2ep_bn_bwd: drop-connect keep must be > 0");
   hipStream_t s = as_stream(stream);
   const int HW = H * W;
-  const long long per = (long long)N * HW;
-  const int sp = bn_splits(per, C);
+  const long long per_c = (long long)N * HW;
+  const bool v4 = (HW & 3) == 0;
+  const int HWv = v4 ? HW / 4 : HW;
+  const int totv = N * HWv;
+  int sp = bn_splits(per_c, C);
+  const int per = cdiv(totv, sp);
+  sp = cdiv(totv, per);
   double *part = static_cast<double *>(workspace);
-  double *sums = part + (size_t)C * sp * 2;
-  hipLaunchKernelGGL(k_bn_bwd_reduce, dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                     res, N, C, HW, sp, act, part);
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(cdiv(C, 64)), dim3(64), 0, s, part, C, sp, dgamma, dbeta,
-                     sums);
-  if (dx || dres)
-    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(cdiv(HW, 256), N * C), dim3(256), 0, s, x, dy, mean,
-                       invstd, gamma, beta, res, sums, C, HW, per, act, train, dx, dres);
+  if (v4)
+    hipLaunchKernelGGL(k_bn_bwd_reduce<4>, dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd, gamma,
+                       beta, res, dc_rand, dc_keep, N, C, HWv, sp, per, act, part);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_reduce<1>, dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd, gamma,
+                       beta, res, dc_rand, dc_keep, N, C, HWv, sp, per, act, part);
+  if (dx || dres) {
+    const dim3 grid(C, cdiv(totv, APPLY_PER));
+    if (v4)
+      hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
+                         res, dc_rand, dc_keep, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
+                         dx, dres, dgamma, dbeta);
+    else
+      hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
+                         res, dc_rand, dc_keep, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
+                         dx, dres, dgamma, dbeta);
+  } else if (dgamma || dbeta) {
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(256), 0, s, part, sp, dgamma, dbeta);
+  }
   return launch_status("e2ep_bn_bwd");
 }
 

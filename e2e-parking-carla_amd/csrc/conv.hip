@@ -386,19 +386,35 @@ __global__ void k_reduce_splits(const float *__restrict__ part, int splits, int 
 }
 
 // per-channel bias gradient: db[c] = sum over (n, p) of g[n, c, p]  (one block per channel)
-__global__ void __launch_bounds__(256) k_bias_grad(const float *__restrict__ g, int N, int C,
-                                                   int HW, float *__restrict__ db) {
+__global__ void __launch_bounds__(1024) k_bias_grad(const float *__restrict__ g, int N, int C,
+                                                    int HW, float *__restrict__ db) {
+  // one workgroup per channel; its N rows of HW are walked as one sequence (float4 when
+  // HW % 4 == 0), fixed-order reduction
   const int c = blockIdx.x;
   float s = 0.f;
-  for (int n = 0; n < N; ++n) {
-    const float *p = g + ((size_t)n * C + c) * HW;
-    for (int i = threadIdx.x; i < HW; i += 256) s += p[i];
+  if ((HW & 3) == 0) {
+    const int HW4 = HW >> 2, tot = N * HW4;
+    for (int t = threadIdx.x; t < tot; t += 1024) {
+      const int n = t / HW4, p = t - n * HW4;
+      const float4 v = *reinterpret_cast<const float4 *>(g + ((size_t)n * C + c) * HW + 4 * p);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+  } else {
+    const int tot = N * HW;
+    for (int t = threadIdx.x; t < tot; t += 1024) {
+      const int n = t / HW, p = t - n * HW;
+      s += g[((size_t)n * C + c) * HW + p];
+    }
   }
-  __shared__ float red[4];
+  __shared__ float red[16];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) db[c] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    db[c] = t;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -598,7 +614,7 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
 
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && HW > 0, E2EP_EINVAL, "e2ep_bias_grad: bad shape");
-  hipLaunchKernelGGL(k_bias_grad, dim3(C), dim3(256), 0, as_stream(stream), gout, N, C, HW, db);
+  hipLaunchKernelGGL(k_bias_grad, dim3(C), dim3(1024), 0, as_stream(stream), gout, N, C, HW, db);
   return launch_status("e2ep_bias_grad");
 }
 

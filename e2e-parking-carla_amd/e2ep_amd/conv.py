@@ -115,9 +115,8 @@ class _Linear1x1(torch.autograd.Function):
             dw = _skinny(g, 1, M, x2, K, 1, None, M, K, N,
                          torch.empty(M, K, dtype=torch.float32, device=g.device)).view(ctx.wshape)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            ones = torch.ones(N, dtype=torch.float32, device=g.device)
-            db = _skinny(ones, 0, 1, g, M, 1, None, 1, M, N,
-                         torch.empty(M, dtype=torch.float32, device=g.device))
+            db = torch.empty(M, dtype=torch.float32, device=g.device)
+            _lib.call("e2ep_bias_grad", _lib.ptr(g), N, M, 1, _lib.ptr(db), _lib.stream())
         return dx, dw, db
 
 

@@ -23,7 +23,7 @@ def _ws(nbytes, device):
 # ------------------------------------------------------------------------------------------
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, rm, rv, train, momentum, eps, act):
+    def forward(ctx, x, gamma, beta, res, rm, rv, train, momentum, eps, act, dc_rand, dc_keep):
         x = x.contiguous()
         res = res.contiguous() if res is not None else None
         N, C, H, W = x.shape
@@ -33,16 +33,16 @@ class _BnAct(torch.autograd.Function):
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
         with timing.region("bn_fwd"):
             _lib.call("e2ep_bn_fwd", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res),
-                      _lib.ptr(rm), _lib.ptr(rv), N, C, H, W, int(train), float(momentum),
-                      float(eps), act, _lib.ptr(mean), _lib.ptr(invstd), _lib.ptr(y), _lib.ptr(ws),
-                      _lib.stream())
-        ctx.save_for_backward(x, gamma, beta, res, mean, invstd)
-        ctx.train, ctx.act = train, act
+                      _lib.ptr(dc_rand), float(dc_keep), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W,
+                      int(train), float(momentum), float(eps), act, _lib.ptr(mean),
+                      _lib.ptr(invstd), _lib.ptr(y), _lib.ptr(ws), _lib.stream())
+        ctx.save_for_backward(x, gamma, beta, res, mean, invstd, dc_rand)
+        ctx.train, ctx.act, ctx.dc_keep = train, act, dc_keep
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, gamma, beta, res, mean, invstd = ctx.saved_tensors
+        x, gamma, beta, res, mean, invstd, dc_rand = ctx.saved_tensors
         dy = dy.contiguous()
         N, C, H, W = x.shape
         nig = ctx.needs_input_grad
@@ -53,24 +53,72 @@ class _BnAct(torch.autograd.Function):
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
         with timing.region("bn_bwd"):
             _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(mean), _lib.ptr(invstd),
-                      _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), N, C, H, W, int(ctx.train),
-                      ctx.act, _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws),
-                      _lib.stream())
-        return dx, dg, db, dres, None, None, None, None, None, None
+                      _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), _lib.ptr(dc_rand),
+                      float(ctx.dc_keep), N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx),
+                      _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.stream())
+        return dx, dg, db, dres, None, None, None, None, None, None, None, None
 
 
-def batch_norm_act(x, bn, act=None, res=None):
+class BnCounters:
+    """num_batches_tracked bookkeeping for a whole model in one launch per forward.
+
+    BatchNorm2d increments its counter on every training forward.  The first training forward
+    of a model runs with per-layer increments while it records which BN layers ran (the
+    BEV encoder's layer4 never does, reference model/bev_encoder.py:21,23-36); later forwards
+    suppress the per-layer increments and add 1 to all recorded counters with one
+    torch._foreach_add_ — same counter values, ~100 fewer launches per step."""
+
+    def __init__(self):
+        self.recorded = None  # BN modules, in call order
+        self._log = None
+        self.batched = False
+
+    def __enter__(self):
+        if self.recorded is None:
+            self._log = []
+        else:
+            torch._foreach_add_([bn.num_batches_tracked for bn in self.recorded], 1)
+            self.batched = True
+        _COUNTERS.append(self)
+        return self
+
+    def __exit__(self, *exc):
+        _COUNTERS.pop()
+        if self.recorded is None and self._log is not None and not exc[0]:
+            self.recorded = self._log
+        self._log = None
+        self.batched = False
+        return False
+
+    def note(self, bn):
+        if self.batched:
+            return
+        bn.num_batches_tracked.add_(1)
+        if self._log is not None:
+            self._log.append(bn)
+
+
+_COUNTERS = []  # stack of active BnCounters (innermost last)
+
+
+def batch_norm_act(x, bn, act=None, res=None, dc_rand=None, dc_keep=1.0):
     """BatchNorm2d module `bn` (its train/eval mode, momentum, eps, running buffers) applied
-    to x, plus an optional residual, then the activation."""
-    _dev(x, res)
+    to x, then optional drop-connect (dc_rand: per-sample uniform draws, training only), an
+    optional residual, then the activation."""
+    _dev(x, res, dc_rand)
     train = bn.training or not bn.track_running_stats
     if bn.training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
+        if _COUNTERS:
+            _COUNTERS[-1].note(bn)
+        else:
+            bn.num_batches_tracked.add_(1)
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     mom = bn.momentum if bn.momentum is not None else 0.1
-    return _BnAct.apply(x, bn.weight, bn.bias, res, rm if train else rm, rv, train, mom, bn.eps,
-                        ACT[act])
+    if dc_rand is not None:
+        dc_rand = dc_rand.contiguous()
+    return _BnAct.apply(x, bn.weight, bn.bias, res, rm, rv, train, mom, bn.eps, ACT[act],
+                        dc_rand, dc_keep)
 
 
 class _Act(torch.autograd.Function):

@@ -38,9 +38,10 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=
     raise NotImplementedError(f"e2ep conv2d: groups={groups} not on the hot path")
 
 
-def bn_act(x, bn, act=None, res=None):
-    """BatchNorm2d (train: batch stats + running update; eval: running stats) [+ res] + act."""
-    return nn_ops.batch_norm_act(x, bn, act, res)
+def bn_act(x, bn, act=None, res=None, dc_rand=None, dc_keep=1.0):
+    """BatchNorm2d (train: batch stats + running update; eval: running stats)
+    [+ drop-connect] [+ res] + act."""
+    return nn_ops.batch_norm_act(x, bn, act, res, dc_rand, dc_keep)
 
 
 def activation(x, act):
@@ -53,14 +54,6 @@ def squeeze_excite(x, reduce, expand):
     g = conv2d(g, reduce.weight, reduce.bias)
     g = conv2d(nn_ops.activation(g, "swish"), expand.weight, expand.bias)
     return nn_ops.se_gate(x, g)
-
-
-def drop_connect(x, p):
-    """efficientnet-pytorch drop_connect (training only): per-sample keep mask / keep."""
-    import torch
-    keep = 1.0 - p
-    mask = torch.floor(keep + torch.rand([x.shape[0], 1, 1, 1], dtype=x.dtype, device=x.device))
-    return x / keep * mask
 
 
 def upsample2x(x):

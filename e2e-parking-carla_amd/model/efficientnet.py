@@ -60,18 +60,23 @@ class MBConv(nn.Module):
         self._project_conv = SameConv(mid, cout, 1, bias=False, size=math.ceil(size / stride))
         self._bn2 = nn.BatchNorm2d(cout, momentum=0.01, eps=1e-3)
 
-    def forward(self, x, drop_connect_rate=None):
+    def forward(self, x, drop_connect_rate=None, dc_rand=None):
+        """dc_rand: this block's per-sample uniform draws for drop-connect (training); drawn
+        here when not given (efficientnet-pytorch draws torch.rand([N,1,1,1]) per block)."""
         y = x
         if self.expand != 1:
             y = ops.bn_act(self._expand_conv(y), self._bn0, "swish")
         y = ops.bn_act(self._depthwise_conv(y), self._bn1, "swish")
         y = ops.squeeze_excite(y, self._se_reduce, self._se_expand)
-        if self.skip and not (drop_connect_rate and self.training):
-            return ops.bn_act(self._project_conv(y), self._bn2, None, res=x)  # fused skip add
-        y = ops.bn_act(self._project_conv(y), self._bn2, None)
-        if self.skip:
-            y = ops.drop_connect(y, drop_connect_rate) + x
-        return y
+        if not self.skip:
+            return ops.bn_act(self._project_conv(y), self._bn2, None)
+        if drop_connect_rate and self.training:
+            # bn2 -> x / keep * floor(keep + u) -> + inputs, fused into the BN kernels
+            if dc_rand is None:
+                dc_rand = torch.rand(x.shape[0], dtype=x.dtype, device=x.device)
+            return ops.bn_act(self._project_conv(y), self._bn2, None, res=x, dc_rand=dc_rand,
+                              dc_keep=1.0 - drop_connect_rate)
+        return ops.bn_act(self._project_conv(y), self._bn2, None, res=x)  # fused skip add
 
 
 class EfficientNetTrunk(nn.Module):
@@ -99,8 +104,12 @@ class EfficientNetTrunk(nn.Module):
         x = ops.bn_act(self._conv_stem(x), self._bn0, "swish")
         ends, prev = [], x
         n = len(self._blocks)
+        # all blocks' drop-connect draws in one launch (one row of N per block)
+        u = (torch.rand(n, x.shape[0], dtype=x.dtype, device=x.device)
+             if self.training and self.drop_connect_rate else None)
         for i, blk in enumerate(self._blocks):
-            x = blk(x, self.drop_connect_rate * i / n if self.drop_connect_rate else None)
+            x = blk(x, self.drop_connect_rate * i / n if self.drop_connect_rate else None,
+                    None if u is None else u[i])
             if prev.shape[2] > x.shape[2]:
                 ends.append(prev)
             prev = x

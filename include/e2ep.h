@@ -163,22 +163,28 @@ int e2ep_skinny_gemm(const float *A, int ai, int ak, const float *B, int bk, int
 
 /* ---------------------------------------------------------------------------------------
  * BatchNorm2d + activation (+ residual), NCHW fp32.
- * Replaces BatchNorm2d(+ReLU / swish, + identity add) pairs of the reference model tree.
- * act: 0 none, 1 relu, 2 swish (x * sigmoid(x)).  res (nullable) is added before act.
- * train != 0: batch statistics (fp64 accumulation, fixed order), running stats updated in
- * place with `momentum` (unbiased variance); train == 0: running statistics.
+ * Replaces BatchNorm2d(+ReLU / swish, + identity add) pairs of the reference model tree, and
+ * efficientnet-pytorch's drop_connect + skip add of MBConv (reference model/cam_encoder.py:70-72).
+ *   y = act(dc(gamma * (x - mean) * invstd + beta) + res)
+ * act: 0 none, 1 relu, 2 swish (x * sigmoid(x)); res (nullable) is added before act;
+ * dc(z) = z / dc_keep * floor(dc_keep + dc_rand[n]) when dc_rand [N] (uniform draws) is given,
+ * else z.  train != 0: batch statistics (fp64 accumulation, fixed order), running stats
+ * updated in place with `momentum` (unbiased variance); train == 0: running statistics.
  * mean / invstd [C] are outputs of fwd and inputs of bwd.  workspace: e2ep_bn_workspace.
+ * Two launches each way (statistics / reduction, then the elementwise pass, which also
+ * finishes the per-channel statistics): no separate finalize launch.
  * ------------------------------------------------------------------------------------- */
 size_t e2ep_bn_workspace(int N, int C, int H, int W);
 int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const float *res,
-                float *running_mean, float *running_var, int N, int C, int H, int W, int train,
-                float momentum, float eps, int act, float *mean, float *invstd, float *y,
-                void *workspace, void *stream);
-/* dx, dgamma, dbeta, dres (each nullable) from x, dy and the forward's mean/invstd. */
+                const float *dc_rand, float dc_keep, float *running_mean, float *running_var,
+                int N, int C, int H, int W, int train, float momentum, float eps, int act,
+                float *mean, float *invstd, float *y, void *workspace, void *stream);
+/* dx, dgamma, dbeta, dres (each nullable) from x, dy and the forward's mean/invstd; res and
+ * dc_rand / dc_keep as in the forward (dres = gradient at the activation input). */
 int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
-                const float *gamma, const float *beta, const float *res, int N, int C, int H, int W,
-                int train, int act, float *dx, float *dgamma, float *dbeta, float *dres,
-                void *workspace, void *stream);
+                const float *gamma, const float *beta, const float *res, const float *dc_rand,
+                float dc_keep, int N, int C, int H, int W, int train, int act, float *dx,
+                float *dgamma, float *dbeta, float *dres, void *workspace, void *stream);
 /* Stand-alone activation (act as above) and its gradient w.r.t. the pre-activation x. */
 int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);

@@ -77,3 +77,23 @@ def test_deterministic_train_step_matches_reference():
     for k in make_grad_probe_keys(params.keys()):
         gk = params[k].grad.reshape(-1)
         _within_reference_noise("grad " + k, gk[:4096], g32["gslice::" + k], g64["gslice::" + k])
+
+
+def test_bn_counters_batched_like_reference():
+    """num_batches_tracked after three training forwards (the first per-layer, later ones
+    batched into one launch): 3 on every BN that runs, 0 on the never-run bev_encoder.layer4
+    (reference model/bev_encoder.py:21,23-36); the drop-connect path (non-deterministic
+    config) runs too."""
+    from e2ep_amd import synthetic
+    from model.parking_model import ParkingModel
+    from tool.config import default_cfg
+    m = ParkingModel(default_cfg()).to(DEV).train()
+    data = synthetic.synthetic_batch(2, seed=1)
+    for _ in range(3):
+        with torch.no_grad():
+            pc, ps, pd = m(data)
+    assert torch.isfinite(pc).all() and torch.isfinite(ps).all() and torch.isfinite(pd).all()
+    counts = {k: int(v) for k, v in m.state_dict().items() if k.endswith("num_batches_tracked")}
+    assert len(counts) > 90
+    for k, v in counts.items():
+        assert v == (0 if k.startswith("bev_encoder.layer4.") else 3), k

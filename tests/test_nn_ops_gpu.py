@@ -58,6 +58,42 @@ def test_bn_act(train, act, res, shape):
     assert int(bnd.num_batches_tracked) == int(bn64.num_batches_tracked)
 
 
+@pytest.mark.parametrize("shape", [(8, 24, 16, 16), (6, 10, 5, 7)])
+def test_bn_drop_connect_fused(shape):
+    """MBConv tail in training: bn2 -> efficientnet-pytorch drop_connect (x / keep *
+    floor(keep + u)) -> + inputs, fused into the BN kernels; vs fp64 torch."""
+    from e2ep_amd import nn_ops
+    g = _g(sum(shape))
+    N, C = shape[:2]
+    x = torch.randn(*shape, generator=g) * 2 + 0.5
+    r = torch.randn(*shape, generator=g)
+    dy = torch.randn(*shape, generator=g)
+    u = torch.rand(N, generator=g)
+    keep = 0.8
+    bn = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3)
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.3 * torch.randn(C, generator=g))
+        bn.bias.copy_(0.2 * torch.randn(C, generator=g))
+    bn64 = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3).double()
+    bn64.load_state_dict(bn.state_dict())
+    bnd = bn.to(DEV).train()
+    xd = x.to(DEV).requires_grad_(True)
+    rd = r.to(DEV).requires_grad_(True)
+    y = nn_ops.batch_norm_act(xd, bnd, None, rd, dc_rand=u.to(DEV), dc_keep=keep)
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    r64 = r.double().requires_grad_(True)
+    mask = torch.floor(torch.tensor(keep, dtype=torch.float32) + u).double().view(N, 1, 1, 1)
+    assert 0 < mask.sum() < N or N < 8  # the draw exercises both kept and dropped samples
+    y64 = bn64(x64) / keep * mask + r64
+    y64.backward(dy.double())
+    assert rel_l2(y, y64) < 1e-6
+    assert rel_l2(xd.grad, x64.grad) < 1e-5
+    assert rel_l2(rd.grad, r64.grad) < 1e-6
+    assert rel_l2(bnd.weight.grad, bn64.weight.grad) < 1e-5
+    assert rel_l2(bnd.bias.grad, bn64.bias.grad) < 1e-5
+
+
 @pytest.mark.parametrize("case", [((8, 65, 200, 200), (256, 256), None), ((4, 64, 16, 16), None, 2),
                                   ((2, 64, 128, 128), (200, 200), None), ((32, 64, 1, 1), (16, 16), None),
                                   ((3, 5, 17, 9), (40, 7), None)])
