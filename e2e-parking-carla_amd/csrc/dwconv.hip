@@ -132,6 +132,152 @@ __global__ void k_dw_wgrad_finalize(const float *__restrict__ part, int C, int K
   dw[i] = s;
 }
 
+// ------------------------------------------------------------------------------------------
+// Strip kernels (Q % 4 == 0, Q <= 256): each wave owns one unit = (plane n*C+c, RO = 256/Q
+// consecutive output rows) and every lane 4 horizontally adjacent outputs, so a unit is
+// exactly 64 x 4 outputs.  The unit's input rows ((RO-1)*ST + K of them) are staged once in
+// LDS with float4 loads, zero-padded left/right (DW_PADL columns) and above/below, and each
+// lane reads its (3*ST + K) x K window from LDS: per output K*(3*ST+K)/4 LDS reads instead of
+// K*K global loads.  Weights are wave-uniform (scalar loads).  Forward; the stride-1 data
+// gradient is the same correlation with the filter flipped and pads K-1-pad (FLIP).
+// ------------------------------------------------------------------------------------------
+constexpr int DW_PADL = 4;  // left halo columns in LDS (>= max left pad 2, keeps rows 16-B aligned)
+
+struct DwStrip {
+  int RO, IR, WP, units_per_plane;  // out rows / unit, staged input rows, LDS row pitch
+};
+
+static DwStrip dw_strip(int K, int st, int W, int P, int Q) {
+  DwStrip d;
+  d.RO = 64 / (Q / 4);  // lanes past RO * (Q / 4) idle
+  d.IR = (d.RO - 1) * st + K;
+  d.WP = W + 2 * DW_PADL;
+  d.units_per_plane = (P + d.RO - 1) / d.RO;
+  return d;
+}
+
+// stage input rows [iy0, iy0 + IR) of plane `src` (H x W) into this wave's LDS buffer
+__device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, int W, int iy0,
+                                         int IR, int WP, float *lds, int lane) {
+  const int W4 = W >> 2;
+  for (int e = lane; e < IR * W4; e += 64) {
+    const int r = e / W4, j = e - r * W4;
+    const int iy = iy0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)iy < (unsigned)H) v = *reinterpret_cast<const float4 *>(src + (size_t)iy * W + 4 * j);
+    *reinterpret_cast<float4 *>(lds + r * WP + DW_PADL + 4 * j) = v;
+  }
+  // halo columns
+  for (int e = lane; e < IR * 2 * DW_PADL; e += 64) {
+    const int r = e / (2 * DW_PADL), j = e - r * (2 * DW_PADL);
+    lds[r * WP + (j < DW_PADL ? j : W + j)] = 0.f;
+  }
+}
+
+template <int K, int ST, bool FLIP>
+__global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
+                                                      const float *__restrict__ w, DwGeom g,
+                                                      DwStrip d, int units, float *__restrict__ y) {
+  extern __shared__ float dw_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int unit = blockIdx.x * 4 + wave;
+  float *lds = dw_lds + wave * d.IR * d.WP;
+  const bool active = unit < units;  // wave-uniform
+  int nc = 0, oy0 = 0;
+  if (active) {
+    nc = unit / d.units_per_plane;
+    oy0 = (unit - nc * d.units_per_plane) * d.RO;
+    dw_stage(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane);
+  }
+  __syncthreads();
+  if (!active) return;
+  const int c = nc % g.C;
+  float wr[K * K];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) wr[t] = w[c * K * K + (FLIP ? K * K - 1 - t : t)];
+  const int QL = g.Q >> 2;  // lanes per output row
+  const int ro = lane / QL, ox0 = 4 * (lane - ro * QL);
+  const int oy = oy0 + ro;
+  if (ro >= d.RO || oy >= g.P) return;
+  constexpr int NV = 3 * ST + K;
+  float o[4] = {0.f, 0.f, 0.f, 0.f};
+  const float *base = lds + (ro * ST) * d.WP + DW_PADL + ox0 * ST - g.pl;
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    float v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = base[a * d.WP + j];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int b = 0; b < K; ++b) o[u] = __builtin_fmaf(wr[a * K + b], v[u * ST + b], o[u]);
+  }
+  *reinterpret_cast<float4 *>(y + ((size_t)nc * g.P + oy) * g.Q + ox0) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// weight gradient partials over strip units: grid (C, splits); the block's waves walk the
+// channel's units (n, strip) of its slice; per lane K*K register accumulators, fixed-order
+// wave + block reduction.
+template <int K, int ST>
+__global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
+                                                        const float *__restrict__ x, DwGeom g,
+                                                        DwStrip d, int splits,
+                                                        float *__restrict__ part) {
+  extern __shared__ float dw_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x, sp = blockIdx.y;
+  float *lds = dw_lds + wave * d.IR * d.WP;
+  const int cunits = g.N * d.units_per_plane;  // units of this channel
+  const int per = (cunits + splits - 1) / splits;
+  const int beg = sp * per, end = min(cunits, beg + per);
+  const int QL = g.Q >> 2;
+  const int ro = lane / QL, ox0 = 4 * (lane - ro * QL);
+  constexpr int NV = 3 * ST + K;
+  float acc[K * K];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
+  // every wave runs the same number of rounds (barriers), idle slots stage nothing
+  for (int u0 = beg; u0 < end; u0 += 4) {
+    const int un = u0 + wave;
+    const bool active = un < end;
+    int n = 0, oy0 = 0;
+    if (active) {
+      n = un / d.units_per_plane;
+      oy0 = (un - n * d.units_per_plane) * d.RO;
+      dw_stage(x + ((size_t)n * g.C + c) * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane);
+    }
+    __syncthreads();
+    const int oy = oy0 + ro;
+    if (active && ro < d.RO && oy < g.P) {
+      const float4 gv4 = *reinterpret_cast<const float4 *>(gy + (((size_t)n * g.C + c) * g.P + oy) * g.Q + ox0);
+      const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
+      const float *base = lds + (ro * ST) * d.WP + DW_PADL + ox0 * ST - g.pl;
+#pragma unroll
+      for (int a = 0; a < K; ++a) {
+        float v[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[j] = base[a * d.WP + j];
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[a * K + b] = __builtin_fmaf(gv[u], v[u * ST + b], acc[a * K + b]);
+      }
+    }
+    __syncthreads();  // LDS reuse
+  }
+  __shared__ float red[4][K * K];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) {
+    const float v = wave_sum(acc[t]);
+    if (lane == 0) red[wave][t] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < K * K) {
+    const int t = threadIdx.x;
+    part[((long long)c * splits + sp) * K * K + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  }
+}
+
 static int dw_splits(long long pixels, int C) {
   long long want = (1024 + C - 1) / C;
   long long cap = pixels / 2048;
@@ -168,11 +314,37 @@ using namespace e2ep;
 
 extern "C" {
 
+static bool dw_strip_ok(const DwGeom &g) {
+  return g.Q % 4 == 0 && g.Q <= 256 && g.W % 4 == 0 && (g.K == 3 || g.K == 5) &&
+         (g.st == 1 || g.st == 2);
+}
+
+#define DW_STRIP_DISPATCH(KERNEL, FLIPARG, GRID, SHMEM, ...)                                    \
+  do {                                                                                         \
+    if (g.K == 3 && g.st == 1)                                                                 \
+      hipLaunchKernelGGL((KERNEL<3, 1 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+    else if (g.K == 3 && g.st == 2)                                                            \
+      hipLaunchKernelGGL((KERNEL<3, 2 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+    else if (g.K == 5 && g.st == 1)                                                            \
+      hipLaunchKernelGGL((KERNEL<5, 1 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+    else                                                                                       \
+      hipLaunchKernelGGL((KERNEL<5, 2 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+  } while (0)
+#define DW_NOFLIP , false
+#define DW_NONE
+
 // dims[10] = {N, C, H, W, K, P, Q, stride, pad_top, pad_left}
 int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, float *y, void *stream) {
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_fwd: bad geometry");
+  if (dw_strip_ok(g)) {
+    const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
+    const int units = g.N * g.C * d.units_per_plane;
+    DW_STRIP_DISPATCH(k_dw_fwd_strip, DW_NOFLIP, dim3(cdiv(units, 4)), 4 * d.IR * d.WP * 4, x, w, g,
+                      d, units, y);
+    return launch_status("e2ep_dwconv_fwd");
+  }
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_fwd: N*C > 65535");
   DW_DISPATCH(k_dw_fwd, dim3(cdiv(g.P * g.Q, 256), g.N * g.C), x, w, g, y);
   return launch_status("e2ep_dwconv_fwd");
@@ -182,14 +354,43 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_dgrad: bad geometry");
+  if (g.st == 1) {
+    // stride 1: dx = gy (P x Q) correlated with the flipped filter, pads K-1-pad, output H x W
+    DwGeom t = g;
+    t.H = g.P; t.W = g.Q; t.P = g.H; t.Q = g.W;
+    t.pt = g.K - 1 - g.pt; t.pl = g.K - 1 - g.pl;
+    if (dw_strip_ok(t) && t.pt >= 0 && t.pl >= 0 && t.pl <= DW_PADL) {
+      const DwStrip d = dw_strip(t.K, 1, t.W, t.P, t.Q);
+      const int units = t.N * t.C * d.units_per_plane;
+      if (t.K == 3)
+        hipLaunchKernelGGL((k_dw_fwd_strip<3, 1, true>), dim3(cdiv(units, 4)), dim3(256),
+                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx);
+      else
+        hipLaunchKernelGGL((k_dw_fwd_strip<5, 1, true>), dim3(cdiv(units, 4)), dim3(256),
+                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx);
+      return launch_status("e2ep_dwconv_dgrad");
+    }
+  }
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_dgrad: N*C > 65535");
   DW_DISPATCH(k_dw_dgrad, dim3(cdiv(g.H * g.W, 256), g.N * g.C), gy, w, g, dx);
   return launch_status("e2ep_dwconv_dgrad");
 }
 
+static int dw_wgrad_splits(const DwGeom &g) {
+  if (dw_strip_ok(g)) {
+    const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
+    const int cunits = g.N * d.units_per_plane;
+    int want = (2048 + g.C - 1) / g.C;           // ~2048 workgroups
+    int cap = (cunits + 7) / 8;                   // >= 8 units (2 per wave) each
+    int s = want < cap ? want : cap;
+    return s < 1 ? 1 : (s > 128 ? 128 : s);
+  }
+  return dw_splits((long long)g.N * g.P * g.Q, g.C);
+}
+
 size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
   DwGeom g = dw_geom(dims);
-  return (size_t)g.C * dw_splits((long long)g.N * g.P * g.Q, g.C) * g.K * g.K * sizeof(float);
+  return (size_t)g.C * dw_wgrad_splits(g) * g.K * g.K * sizeof(float);
 }
 
 int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, void *workspace, float *dw,
@@ -197,9 +398,15 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, void *wo
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_wgrad: bad geometry");
-  const int sp = dw_splits((long long)g.N * g.P * g.Q, g.C);
+  const int sp = dw_wgrad_splits(g);
   float *part = static_cast<float *>(workspace);
-  DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part);
+  if (dw_strip_ok(g)) {
+    const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
+    DW_STRIP_DISPATCH(k_dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
+                      sp, part);
+  } else {
+    DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part);
+  }
   hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0,
                      as_stream(stream), part, g.C, g.K * g.K, sp, dw);
   return launch_status("e2ep_dwconv_wgrad");

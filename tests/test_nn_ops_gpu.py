@@ -120,7 +120,10 @@ def test_resize(case):
 
 @pytest.mark.parametrize("case", [(4, 144, 64, 64, 3, 2, (0, 1, 0, 1)), (4, 48, 32, 32, 3, 1, (1, 1, 1, 1)),
                                   (4, 192, 32, 32, 5, 2, (2, 2, 2, 2)), (2, 672, 16, 16, 5, 1, (2, 2, 2, 2)),
-                                  (3, 8, 13, 11, 3, 2, (0, 1, 0, 1))])
+                                  (3, 8, 13, 11, 3, 2, (0, 1, 0, 1)), (2, 24, 128, 128, 3, 1, (1, 1, 1, 1)),
+                                  (2, 8, 128, 128, 3, 2, (0, 1, 0, 1)), (2, 32, 64, 64, 3, 1, (1, 1, 1, 1)),
+                                  (2, 40, 32, 32, 5, 1, (2, 2, 2, 2)), (3, 16, 16, 16, 3, 1, (1, 1, 1, 1)),
+                                  (2, 12, 24, 20, 5, 1, (2, 2, 2, 2))])
 def test_depthwise(case):
     from e2ep_amd import ops
     N, C, H, W, K, s, pad = case
