@@ -55,6 +55,8 @@ SIGNATURES = {
     "e2ep_maxpool3s2_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_avgpool_fwd": (_i, [_p, _i, _i, _p, _p]),
     "e2ep_avgpool_bwd": (_i, [_p, _i, _i, _p, _p]),
+    "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "e2ep_se_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "e2ep_se_gate_fwd": (_i, [_p, _p, _i, _i, _p, _p]),
     "e2ep_se_gate_bwd": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),
     "e2ep_adam_chunk_elems": (_i, []),

@@ -319,3 +319,55 @@ def se_gate(x, a):
     """x * sigmoid(a), a [N, C, 1, 1]."""
     _dev(x, a)
     return _SeGate.apply(x, a)
+
+
+# ------------------------------------------------------------------------------------------
+# squeeze-and-excitation (fused)
+# ------------------------------------------------------------------------------------------
+class _SqueezeExcite(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        sq = w1.shape[0]
+        dev = x.device
+        pooled = torch.empty(N, C, dtype=torch.float32, device=dev)
+        hpre = torch.empty(N, sq, dtype=torch.float32, device=dev)
+        a = torch.empty(N, C, dtype=torch.float32, device=dev)
+        y = torch.empty_like(x)
+        w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
+        with timing.region("se_fwd"):
+            _lib.call("e2ep_se_fwd", _lib.ptr(x), _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c),
+                      _lib.ptr(b2), N, C, H * W, sq, _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a),
+                      _lib.ptr(y), _lib.stream())
+        ctx.save_for_backward(x, w1c, w2c, pooled, hpre, a)
+        ctx.shapes = (w1.shape, w2.shape, b1 is not None, b2 is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w1c, w2c, pooled, hpre, a = ctx.saved_tensors
+        w1s, w2s, hb1, hb2 = ctx.shapes
+        N, C, H, W = x.shape
+        sq = w1c.shape[0]
+        nig = ctx.needs_input_grad
+        dev = x.device
+        dx = torch.empty_like(x) if nig[0] else None
+        dw1 = torch.empty(w1s, dtype=torch.float32, device=dev) if nig[1] else None
+        db1 = torch.empty(sq, dtype=torch.float32, device=dev) if (hb1 and nig[2]) else None
+        dw2 = torch.empty(w2s, dtype=torch.float32, device=dev) if nig[3] else None
+        db2 = torch.empty(C, dtype=torch.float32, device=dev) if (hb2 and nig[4]) else None
+        ws = torch.empty(2 * N * C + N * sq, dtype=torch.float32, device=dev)
+        with timing.region("se_bwd"):
+            _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(dy.contiguous()), _lib.ptr(w1c),
+                      _lib.ptr(w2c), _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), N, C, H * W,
+                      sq, _lib.ptr(dx), _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2),
+                      _lib.ptr(ws), _lib.stream())
+        return dx, dw1, db1, dw2, db2
+
+
+def squeeze_excite(x, w1, b1, w2, b2):
+    """x * sigmoid(w2 swish(w1 mean_hw(x) + b1) + b2): efficientnet-pytorch MBConv SE with the
+    two 1x1 convs (w1 [sq,C,1,1], w2 [C,sq,1,1]) on the pooled 1x1 map."""
+    _dev(x)
+    return _SqueezeExcite.apply(x, w1, b1, w2, b2)

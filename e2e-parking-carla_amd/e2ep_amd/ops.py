@@ -49,11 +49,9 @@ def activation(x, act):
 
 
 def squeeze_excite(x, reduce, expand):
-    """efficientnet-pytorch MBConv SE: x * sigmoid(expand(swish(reduce(avgpool(x)))))."""
-    g = nn_ops.global_avg_pool(x)
-    g = conv2d(g, reduce.weight, reduce.bias)
-    g = conv2d(nn_ops.activation(g, "swish"), expand.weight, expand.bias)
-    return nn_ops.se_gate(x, g)
+    """efficientnet-pytorch MBConv SE: x * sigmoid(expand(swish(reduce(avgpool(x))))), one
+    fused op (e2ep_se_fwd / e2ep_se_bwd)."""
+    return nn_ops.squeeze_excite(x, reduce.weight, reduce.bias, expand.weight, expand.bias)
 
 
 def upsample2x(x):

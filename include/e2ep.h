@@ -190,6 +190,25 @@ int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Squeeze-and-excitation of an MBConv block as one op (efficientnet-pytorch 0.7.1
+ * MBConvBlock._se_reduce / _swish / _se_expand / sigmoid gate, reference
+ * model/cam_encoder.py:69-73).  x, y [N,C,HW]; w1 [sq,C] b1 [sq] (_se_reduce), w2 [C,sq]
+ * b2 [C] (_se_expand), biases nullable:
+ *   pooled = mean_hw x; hpre = w1 pooled + b1; a = w2 swish(hpre) + b2; y = x * sigmoid(a)
+ * pooled [N,C], hpre [N,sq], a [N,C] are forward outputs the backward reads.
+ * Backward: dx = dy*sigmoid(a) + (w1^T (swish'(hpre) * (w2^T da))) / HW with
+ * da = sigmoid'(a) * sum_hw dy*x, and the four parameter gradients (each nullable), batch sums
+ * in sample order.  workspace: (2*N*C + N*sq) floats.  Limits: C <= 4096, sq <= 256.
+ * ------------------------------------------------------------------------------------- */
+int e2ep_se_fwd(const float *x, const float *w1, const float *b1, const float *w2,
+                const float *b2, int N, int C, int HW, int sq, float *pooled, float *hpre,
+                float *a, float *y, void *stream);
+int e2ep_se_bwd(const float *x, const float *dy, const float *w1, const float *w2,
+                const float *pooled, const float *hpre, const float *a, int N, int C, int HW,
+                int sq, float *dx, float *dw1, float *db1, float *dw2, float *db2,
+                float *workspace, void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Bilinear resize, align_corners=False (F.interpolate / nn.Upsample semantics) over
  * `planes` = N*C planes.  scale_* = 1/scale_factor when a factor is given, else In/Out.
  * Replaces model/bev_encoder.py:24, model/segmentation_head.py:35-38,

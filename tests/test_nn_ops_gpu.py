@@ -192,3 +192,30 @@ def test_bev_stem_resize_conv_fused():
     assert rel_l2(y, y64) < 2e-5
     assert rel_l2(bd.grad, b64.grad) < 2e-5
     assert rel_l2(wd.grad, w64.grad) < 2e-5
+
+
+@pytest.mark.parametrize("shape", [(8, 96, 16, 16, 6), (4, 40, 9, 7, 10), (32, 672, 16, 16, 28)])
+def test_squeeze_excite_fused(shape):
+    """Fused SE (pool -> 1x1 -> swish -> 1x1 -> sigmoid gate) vs fp64 torch, all gradients."""
+    from e2ep_amd import nn_ops
+    N, C, H, W, sq = shape
+    g = _g(C + sq)
+    x = torch.randn(N, C, H, W, generator=g)
+    w1 = torch.randn(sq, C, 1, 1, generator=g) / C ** 0.5
+    b1 = torch.randn(sq, generator=g) * 0.1
+    w2 = torch.randn(C, sq, 1, 1, generator=g) / sq ** 0.5
+    b2 = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(N, C, H, W, generator=g)
+    ts = [t.to(DEV).requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    y = nn_ops.squeeze_excite(*ts)
+    y.backward(dy.to(DEV))
+    rs = [t.double().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    p = F.adaptive_avg_pool2d(rs[0], 1)
+    h = F.conv2d(p, rs[1], rs[2])
+    h = h * torch.sigmoid(h)
+    a = F.conv2d(h, rs[3], rs[4])
+    y64 = rs[0] * torch.sigmoid(a)
+    y64.backward(dy.double())
+    assert rel_l2(y, y64) < 1e-6
+    for got, ref in zip(ts, rs):
+        assert rel_l2(got.grad, ref.grad) < 1e-5
