@@ -42,6 +42,7 @@ struct ConvGeom {
   int Cout, R, S;   // filter
   int P, Q;         // output spatial
   int sh, sw, ph, pw, dh, dw;
+  int wlayout;      // 0: [Cout][Cin][R*S] (PyTorch), 1: [R*S][Cout][Cin] (tap-major)
 };
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -144,23 +145,44 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   const int xbase = MODE == 0 ? cx * g.sw : cx;
   const int simg = img * Kc * HWs;
 
-  // A-load row of this thread; its k rows (channels) are wave-uniform
-  const int am = tid & (BM - 1);
+  // A-load row of this thread; its k rows (channels) are wave-uniform (dgrad).  Forward
+  // loads run along the weight's channel axis instead (thread = row tid/4, channels
+  // 4*(tid%4)..+3: float4 for 1x1 filters), so a wave touches 16 weight rows, not 64.
+  const int am = MODE == 0 ? (tid >> 2) : (tid & (BM - 1));
+  const int ac = MODE == 0 ? 4 * (tid & 3) : 0;
   const bool arow_ok = (m0 + am) < M;
-  // fwd: W[m][c][rs] = w[m*Cin*RS + c*RS + rs];  dgrad: W[c][m][rs] = w[c*Cin*RS + m*RS + rs]
-  const int a_mstride = MODE == 0 ? g.Cin * RS : RS;
-  const int a_cstride = MODE == 0 ? RS : g.Cin * RS;
+  // weight layout 0 (PyTorch [Cout][Cin][RS]):
+  //   fwd: W[m][c][rs] = w[m*Cin*RS + c*RS + rs];  dgrad: W[c][m][rs] = w[c*Cin*RS + m*RS + rs]
+  // weight layout 1 (tap-major [RS][Cout][Cin], contiguous along Cin for every tap):
+  //   fwd: w[rs*Cout*Cin + m*Cin + c];             dgrad: w[rs*Cout*Cin + c*Cin + m]
+  const bool tm = g.wlayout == 1;
+  const int a_mstride = MODE == 0 ? (tm ? g.Cin : g.Cin * RS) : (tm ? 1 : RS);
+  const int a_cstride = MODE == 0 ? (tm ? 1 : RS) : (tm ? g.Cin : g.Cin * RS);
+  const int a_tstride = tm ? g.Cout * g.Cin : 1;
+  const bool a_vec = MODE == 0 && a_cstride == 1 && (g.Cin & 3) == 0;
   const int arow = (m0 + am) * a_mstride;
 
   float ra[4], rb[BPER];
   auto load_tiles = [&](int ks) {
     const int tap = ks / csteps;                    // uniform
     const int c0 = (ks - tap * csteps) * BK;
-    const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap];
+    const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * a_tstride;
+    if (MODE == 0) {
+      const int c = c0 + ac;
+      if (a_vec) {
+        const float4 v = bload4(rw, (arow_ok && c < Kc) ? (arow + c + rs) * 4 : OOR);
+        ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
+      } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = c0 + wave + 4 * j;
-      ra[j] = bload(rw, (arow_ok && c < Kc) ? (arow + c * a_cstride + rs) * 4 : OOR);
+        for (int j = 0; j < 4; ++j)
+          ra[j] = bload(rw, (arow_ok && c + j < Kc) ? (arow + (c + j) * a_cstride + rs) * 4 : OOR);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + wave + 4 * j;
+        ra[j] = bload(rw, (arow_ok && c < Kc) ? (arow + c * a_cstride + rs) * 4 : OOR);
+      }
     }
     const int iy = ybase + dy, ix = xbase + dx;
     const bool pix_ok = col_ok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
@@ -173,7 +195,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   };
   auto store_tiles = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) As[buf][wave + 4 * j][am] = ra[j];
+    for (int j = 0; j < 4; ++j) As[buf][MODE == 0 ? ac + j : wave + 4 * j][am] = ra[j];
 #pragma unroll
     for (int j = 0; j < BPER; ++j) Bs[buf][bk0 + BROWS * j][bn] = rb[j];
   };
@@ -366,23 +388,116 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   }
 }
 
-// fixed-order sum of the split slabs (+ optional accumulate into an existing gradient).
-// 4 independent partial chains per thread (fixed assignment) keep loads in flight.
-__global__ void k_reduce_splits(const float *__restrict__ part, int splits, int n,
-                                float *__restrict__ out, int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int k = 0;
-  for (; k + 4 <= splits; k += 4) {
-    s0 += part[(size_t)(k + 0) * n + i];
-    s1 += part[(size_t)(k + 1) * n + i];
-    s2 += part[(size_t)(k + 2) * n + i];
-    s3 += part[(size_t)(k + 3) * n + i];
+// ------------------------------------------------------------------------------------------
+// bwd-weight of 1x1 / stride-1 / unpadded convs (the EfficientNet expand / project convs,
+// the BEV heads' 1x1s): dW[co][ci] = sum_q g[co][q] x[ci][q] over all pixels q.  No LDS, no
+// barrier in the main loop: each wave owns a 32 (co) x 32 (ci) tile and a pixel range, and
+// loads its MFMA operands straight from memory as float4s along the pixel axis — lane l
+// reads 4 consecutive pixels of row l%32 (g for A, x for B), and MFMA t of a group takes
+// element t of every lane (the K axis is reordered within each 8-pixel group; the sum is the
+// same and its order fixed).  The four waves of a block split the block's pixel range and
+// are summed in LDS in wave order; slabs per split are reduced by k_reduce_splits.
+// ------------------------------------------------------------------------------------------
+constexpr int W1_GROUPS = 4;  // 8-pixel groups per wave iteration (8 float4 loads in flight)
+
+static bool wgrad1x1_ok(const ConvGeom &g) {
+  return g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 &&
+         g.P == g.H && g.Q == g.W && (g.P * g.Q) % 8 == 0;
+}
+
+static int wgrad1x1_splits(const ConvGeom &g) {
+  const long long tiles = (long long)cdiv(g.Cout, 32) * cdiv(g.Cin, 32);
+  const long long pix = (long long)g.N * g.P * g.Q;
+  long long want = (2048 + tiles - 1) / tiles;   // ~2048 workgroups
+  long long cap = pix / 2048;                    // >= 16 loop iterations per wave
+  long long s = want < cap ? want : cap;
+  if (s < 1) s = 1;
+  if (s > 4096) s = 4096;
+  return (int)s;
+}
+
+__global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gout,
+                                                   const float *__restrict__ x,
+                                                   float *__restrict__ part, ConvGeom g,
+                                                   int splits, int groups_per_split) {
+  __shared__ float red[4][16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ntj = (g.Cin + 31) / 32;
+  const int ti = blockIdx.x / ntj, tj = blockIdx.x - ti * ntj;
+  const int split = blockIdx.y;
+  const int PQ = g.P * g.Q;
+  const int ngroups = g.N * PQ / 8;  // 8-pixel groups (never straddle an image: PQ % 8 == 0)
+  const int gb = split * groups_per_split;
+  const int ge = min(ngroups, gb + groups_per_split);
+  const int row = lane & 31, h = lane >> 5;
+  const int co = ti * 32 + row, ci = tj * 32 + row;
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * PQ);
+  const int gpq = PQ / 8;
+  f32x16 acc = {0};
+  // wave w takes groups gb + w*W1_GROUPS + 4*W1_GROUPS*i ...
+  for (int g0 = gb + wave * W1_GROUPS; g0 < ge; g0 += 4 * W1_GROUPS) {
+    float4 a[W1_GROUPS], b[W1_GROUPS];
+#pragma unroll
+    for (int u = 0; u < W1_GROUPS; ++u) {
+      const int grp = g0 + u;
+      const bool ok = grp < ge;
+      const int n = grp / gpq, p = (grp - n * gpq) * 8 + 4 * h;
+      a[u] = bload4(rg, (ok && co < g.Cout) ? (((n * g.Cout + co) * PQ) + p) * 4 : OOR);
+      b[u] = bload4(rx, (ok && ci < g.Cin) ? (((n * g.Cin + ci) * PQ) + p) * 4 : OOR);
+    }
+#pragma unroll
+    for (int u = 0; u < W1_GROUPS; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, b[u].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, b[u].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, b[u].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, b[u].w, acc, 0, 0, 0);
+    }
   }
-  for (; k < splits; ++k) s0 += part[(size_t)k * n + i];
-  const float s = (s0 + s1) + (s2 + s3);
-  out[i] = accumulate ? out[i] + s : s;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
+  __syncthreads();
+  // C layout: element r of lane l is (i, j) = ((r&3) + 8*(r>>2) + 4*(l>>5), l&31)
+  const int Kw = g.Cin;
+  for (int e = threadIdx.x; e < 16 * 64; e += 256) {
+    const int r = e >> 6, l = e & 63;
+    const int i = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = l & 31;
+    const int oc = ti * 32 + i, ic = tj * 32 + j;
+    if (oc < g.Cout && ic < g.Cin) {
+      const float v = (red[0][r][l] + red[1][r][l]) + (red[2][r][l] + red[3][r][l]);
+      part[((long long)split * g.Cout + oc) * Kw + ic] = v;
+    }
+  }
+}
+
+// fixed-order sum of the split slabs (+ optional accumulate into an existing gradient).
+// Block = 64 outputs x 16 split lanes: thread (o, r) sums splits r, r+16, ... with 4
+// independent chains, then the 16 lane sums are added in order through LDS.
+__global__ void __launch_bounds__(1024) k_reduce_splits(const float *__restrict__ part, int splits,
+                                                        int n, float *__restrict__ out,
+                                                        int accumulate) {
+  __shared__ float red[16][64];
+  const int o = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + o;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < n) {
+    int k = r;
+    for (; k + 48 < splits; k += 64) {
+      s0 += part[(size_t)(k + 0) * n + i];
+      s1 += part[(size_t)(k + 16) * n + i];
+      s2 += part[(size_t)(k + 32) * n + i];
+      s3 += part[(size_t)(k + 48) * n + i];
+    }
+    for (; k < splits; k += 16) s0 += part[(size_t)k * n + i];
+  }
+  red[r][o] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (r == 0 && i < n) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += red[j][o];
+    out[i] = accumulate ? out[i] + s : s;
+  }
 }
 
 // per-channel bias gradient: db[c] = sum over (n, p) of g[n, c, p]  (one block per channel)
@@ -445,6 +560,7 @@ static ConvGeom make_geom(const int *d) {
   g.N = d[0]; g.Cin = d[1]; g.H = d[2]; g.W = d[3];
   g.Cout = d[4]; g.R = d[5]; g.S = d[6]; g.P = d[7]; g.Q = d[8];
   g.sh = d[9]; g.sw = d[10]; g.ph = d[11]; g.pw = d[12]; g.dh = d[13]; g.dw = d[14];
+  g.wlayout = 0;
   return g;
 }
 
@@ -555,8 +671,10 @@ size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
 }
 
 int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
-                  float *y, void *workspace, void *stream) {
+                  int w_layout, float *y, void *workspace, void *stream) {
   ConvGeom g = make_geom(dims);
+  E2EP_REQUIRE(w_layout == 0 || w_layout == 1, E2EP_EINVAL, "e2ep_conv_fwd: w_layout must be 0 or 1");
+  g.wlayout = w_layout;
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_fwd: bad geometry");
   E2EP_REQUIRE(act == 0 || act == 1, E2EP_EINVAL, "e2ep_conv_fwd: act must be 0 (none) or 1 (relu)");
   const int rc = launch_gemm(0, act, w, x, bias, y, 4LL * g.N * g.Cout * g.P * g.Q, g, g.Cout,
@@ -565,9 +683,11 @@ int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *
   return launch_status("e2ep_conv_fwd");
 }
 
-int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels, float *dx,
-                    void *workspace, void *stream) {
+int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
+                    int w_layout, float *dx, void *workspace, void *stream) {
   ConvGeom g = make_geom(dims);
+  E2EP_REQUIRE(w_layout == 0 || w_layout == 1, E2EP_EINVAL, "e2ep_conv_dgrad: w_layout must be 0 or 1");
+  g.wlayout = w_layout;
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_dgrad: bad geometry");
   E2EP_REQUIRE(m_channels > 0 && m_channels <= g.Cin, E2EP_EINVAL,
                "e2ep_conv_dgrad: m_channels must be in [1, Cin]");
@@ -579,6 +699,7 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
 
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
+  if (wgrad1x1_ok(g)) return wgrad1x1_splits(g);
   const long long base = (long long)cdiv(g.Cin * g.R * g.S, WBN) * cdiv(g.Cout, BM);
   const long long pix = (long long)g.N * g.P * g.Q;
   long long want = (1024 + base - 1) / base;
@@ -598,6 +719,19 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
                     void *workspace, float *dw, int accumulate, void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g) && splits > 0, E2EP_EINVAL, "e2ep_conv_wgrad: bad geometry");
+  if (wgrad1x1_ok(g)) {
+    const int groups = g.N * g.P * g.Q / 8;
+    const int gps = cdiv(groups, splits);
+    const int used = cdiv(groups, gps);
+    hipStream_t s = as_stream(stream);
+    float *part = static_cast<float *>(workspace);
+    hipLaunchKernelGGL(k_wgrad_1x1, dim3(cdiv(g.Cout, 32) * cdiv(g.Cin, 32), used), dim3(256), 0, s,
+                       gout, x, part, g, used, gps);
+    const int n = g.Cout * g.Cin;
+    hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
+                       accumulate);
+    return launch_status("e2ep_conv_wgrad");
+  }
   const int Ptot = g.N * g.P * g.Q;
   int per = (Ptot + splits - 1) / splits;
   per = (per + BK - 1) / BK * BK;
@@ -607,7 +741,7 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
   float *part = static_cast<float *>(workspace);
   hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per);
   const int n = g.Cout * g.Cin * g.R * g.S;
-  hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 256)), dim3(256), 0, s, part, used, n, dw,
+  hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
                      accumulate);
   return launch_status("e2ep_conv_wgrad");
 }

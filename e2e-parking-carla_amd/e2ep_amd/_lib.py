@@ -31,9 +31,9 @@ SIGNATURES = {
     "e2ep_transpose": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
     "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
     "e2ep_conv_fwd_workspace": (_sz, [_p]),
-    "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p]),
+    "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _p]),
     "e2ep_conv_dgrad_workspace": (_sz, [_p, _i]),
-    "e2ep_conv_dgrad": (_i, [_p, _p, _p, _i, _p, _p, _p]),
+    "e2ep_conv_dgrad": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),
     "e2ep_conv_wgrad_splits": (_i, [_p]),
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),
     "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _p, _i, _p]),

@@ -30,23 +30,24 @@ class _BevStem(torch.autograd.Function):
         Cout, _, R, S = w.shape
         P, Q = (H + 6 - R) // 2 + 1, (W + 6 - S) // 2 + 1
         dims = (B, Cin, H, W, Cout, R, S, P, Q, 2, 2, 3, 3, 1, 1)
-        y = conv.conv_fwd(x, w.contiguous(), None, dims, 0,
-                          torch.empty(B, Cout, P, Q, dtype=torch.float32, device=bev.device))
-        ctx.save_for_backward(x, w)
+        wt = conv.tap_major(w)
+        y = conv.conv_fwd(x, wt, None, dims, 0,
+                          torch.empty(B, Cout, P, Q, dtype=torch.float32, device=bev.device), w_layout=1)
+        ctx.save_for_backward(x, w, wt)
         ctx.meta = (B, C, X, Y, H, W, sh, sw, dims)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w = ctx.saved_tensors
+        x, w, wt = ctx.saved_tensors
         B, C, X, Y, H, W, sh, sw, dims = ctx.meta
         gy = gy.contiguous()
         s = _lib.stream()
         d = _lib.dims(dims)
         dbev = dw = None
         if ctx.needs_input_grad[0]:
-            dres = conv.conv_dgrad(gy, w.contiguous(), dims, C,
-                                   torch.empty(B, C, H, W, dtype=torch.float32, device=gy.device))
+            dres = conv.conv_dgrad(gy, wt, dims, C,
+                                   torch.empty(B, C, H, W, dtype=torch.float32, device=gy.device), w_layout=1)
             dbev = torch.empty(B, C, X, Y, dtype=torch.float32, device=gy.device)
             ws = torch.empty(B * C * H * Y, dtype=torch.float32, device=gy.device)
             with timing.region("resize_bwd"):

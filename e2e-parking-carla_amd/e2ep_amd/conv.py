@@ -14,22 +14,33 @@ def _ws(nbytes, device):
     return torch.empty(nbytes // 4, dtype=torch.float32, device=device) if nbytes else None
 
 
-def conv_fwd(x, w, b, dims, act, y):
+def tap_major(w):
+    """[Cout,Cin,R,S] -> [R*S,Cout,Cin] (the kernels' w_layout 1); 1x1 filters unchanged."""
+    Cout, Cin, R, S = w.shape
+    if R * S == 1:
+        return w.contiguous()
+    out = torch.empty(R * S, Cout, Cin, dtype=torch.float32, device=w.device)
+    _lib.call("e2ep_transpose", _lib.ptr(w.contiguous()), Cout * Cin * R * S, 1, Cout * Cin, R * S,
+              _lib.ptr(out), _lib.stream())
+    return out
+
+
+def conv_fwd(x, w, b, dims, act, y, w_layout=0):
     """Launch the forward conv into y (handles the split-K workspace)."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_fwd_workspace(d), x.device)
     with timing.region("conv_fwd"):
-        _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, _lib.ptr(y),
-                  _lib.ptr(ws), _lib.stream())
+        _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
+                  _lib.ptr(y), _lib.ptr(ws), _lib.stream())
     return y
 
 
-def conv_dgrad(gy, w, dims, m_channels, dx):
+def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0):
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_dgrad_workspace(d, m_channels), gy.device)
     with timing.region("conv_dgrad"):
-        _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, m_channels, _lib.ptr(dx),
-                  _lib.ptr(ws), _lib.stream())
+        _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, m_channels, w_layout,
+                  _lib.ptr(dx), _lib.ptr(ws), _lib.stream())
     return dx
 
 
@@ -47,16 +58,18 @@ class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, dims, act, grad_channels):
         x = x.contiguous()
-        w = w.contiguous()
+        wt = tap_major(w)  # one small transpose per step for R*S > 1; shared with dgrad
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
-        y = conv_fwd(x, w, b, dims, act, torch.empty(N, Cout, P, Q, dtype=torch.float32, device=x.device))
+        y = conv_fwd(x, wt, b, dims, act, torch.empty(N, Cout, P, Q, dtype=torch.float32, device=x.device),
+                     w_layout=1)
         ctx.dims, ctx.act, ctx.has_bias, ctx.gc = dims, act, b is not None, grad_channels
-        ctx.save_for_backward(x, w, y if act else None)
+        ctx.save_for_backward(x, wt, y if act else None)
+        ctx.wshape = w.shape
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w, y = ctx.saved_tensors
+        x, wt, y = ctx.saved_tensors
         dims = ctx.dims
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
         gy = gy.contiguous()
@@ -66,14 +79,15 @@ class _Conv2d(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             gc = ctx.gc or Cin
-            dxg = conv_dgrad(gy, w, dims, gc, torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device))
+            dxg = conv_dgrad(gy, wt, dims, gc, torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device),
+                             w_layout=1)
             if gc == Cin:
                 dx = dxg
             else:
                 dx = torch.zeros_like(x)
                 dx[:, :gc] = dxg
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(gy, x, dims, torch.empty_like(w))
+            dw = conv_wgrad(gy, x, dims, torch.empty(ctx.wshape, dtype=torch.float32, device=x.device))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = torch.empty(Cout, dtype=torch.float32, device=x.device)
             _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db), s)

@@ -131,18 +131,22 @@ int e2ep_target_bev(const float *target_point, const float *noise, int B, int X,
  * a bigger P/Q with implicit zero rows/cols at the bottom/right).  groups == 1.
  * ------------------------------------------------------------------------------------- */
 
-/* y[N,Cout,P,Q] = conv(x[N,Cin,H,W], w[Cout,Cin,R,S]) + bias (nullable); act 0 none, 1 relu.
+/* y[N,Cout,P,Q] = conv(x[N,Cin,H,W], w) + bias (nullable); act 0 none, 1 relu.
+ * w_layout 0: w[Cout,Cin,R,S] (PyTorch); 1: tap-major w[R*S,Cout,Cin] (see e2ep_transpose),
+ * whose rows are contiguous along Cin for both the forward and the data gradient (16-B
+ * weight loads); the two coincide for 1x1 filters.
  * Grids that cannot fill the chip split K; the partial sums then need a workspace of
  * e2ep_conv_fwd_workspace bytes (0 = none needed; pass NULL) and are reduced in fixed order. */
 size_t e2ep_conv_fwd_workspace(const int *dims);
 int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
-                  float *y, void *workspace, void *stream);
+                  int w_layout, float *y, void *workspace, void *stream);
 
 /* dx[N,m_channels,H,W] = conv_transpose(gout[N,Cout,P,Q], w) restricted to the first
- * m_channels input channels; split by input-pixel stride phase, so no zero taps at stride 2. */
+ * m_channels input channels; split by input-pixel stride phase, so no zero taps at stride 2.
+ * w_layout as for e2ep_conv_fwd. */
 size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels);
-int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels, float *dx,
-                    void *workspace, void *stream);
+int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
+                    int w_layout, float *dx, void *workspace, void *stream);
 
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of

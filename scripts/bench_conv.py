@@ -1,0 +1,96 @@
+"""Per-shape timing of the e2ep implicit-GEMM conv kernels (fwd / dgrad / wgrad separately,
+back-to-back launches between HIP events) on the conv shapes of one ParkingModel train step.
+
+    python scripts/bench_conv.py [--record] [--top 30]
+--record runs the model once to (re)write scripts/conv_shapes.json."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "e2e-parking-carla_amd"), ROOT]
+import torch  # noqa: E402
+
+SHAPES = os.path.join(ROOT, "scripts", "conv_shapes.json")
+
+
+def record(batch):
+    from e2ep_amd import conv, synthetic
+    from tool.config import default_cfg
+    from trainer.pl_trainer import ParkingTrainingModule
+    seen = {}
+    orig = conv._Conv2d.apply
+
+    def rec(x, w, b, dims, act, gc):
+        key = json.dumps([list(dims), int(act), b is not None, gc])
+        seen[key] = seen.get(key, 0) + 1
+        return orig(x, w, b, dims, act, gc)
+
+    conv._Conv2d.apply = rec
+    mod = ParkingTrainingModule(default_cfg()).cuda().train()
+    data = synthetic.synthetic_batch(batch, seed=0)
+    mod.training_step(data, 0).backward()
+    conv._Conv2d.apply = orig
+    out = [{"dims": json.loads(k)[0], "act": json.loads(k)[1], "bias": json.loads(k)[2],
+            "grad_channels": json.loads(k)[3], "count": n} for k, n in seen.items()]
+    json.dump(out, open(SHAPES, "w"), indent=0)
+    return out
+
+
+def timeit(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--record", action="store_true")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--top", type=int, default=40)
+    a = ap.parse_args()
+    from e2ep_amd import _lib, conv
+    shapes = record(a.batch) if a.record or not os.path.exists(SHAPES) else json.load(open(SHAPES))
+    rows = []
+    tot = [0.0, 0.0, 0.0]
+    flops_tot = 0.0
+    for sh in shapes:
+        d = sh["dims"]
+        N, Cin, H, W, Cout, R, S, P, Q = d[:9]
+        x = torch.randn(N, Cin, H, W, device="cuda")
+        w = torch.randn(Cout, Cin, R, S, device="cuda")
+        gy = torch.randn(N, Cout, P, Q, device="cuda")
+        y = torch.empty_like(gy)
+        gc = sh["grad_channels"] or Cin
+        dx = torch.empty(N, gc, H, W, device="cuda")
+        dw = torch.empty_like(w)
+        fl = 2.0 * N * P * Q * Cout * Cin * R * S
+        wt = conv.tap_major(w)
+        tf = timeit(lambda: conv.conv_fwd(x, wt, None, d, sh["act"], y, w_layout=1))
+        td = timeit(lambda: conv.conv_dgrad(gy, wt, d, gc, dx, w_layout=1))
+        tw = timeit(lambda: conv.conv_wgrad(gy, x, d, dw))
+        n = sh["count"]
+        tot[0] += n * tf
+        tot[1] += n * td
+        tot[2] += n * tw
+        flops_tot += n * 3 * fl
+        rows.append((n * (tf + td + tw), n, d, tf, td, tw, fl))
+    rows.sort(key=lambda r: -r[0])
+    s = sum(tot)
+    print(f"conv per step: fwd {tot[0]:.2f} dgrad {tot[1]:.2f} wgrad {tot[2]:.2f} = {s:.2f} ms, "
+          f"{flops_tot / s / 1e9:.1f} TF/s over {len(rows)} shapes")
+    print(f"{'N,Cin,H,W -> Cout,RxS /st':>34} n |   fwd  dgrad  wgrad (ms) | TF/s f / d / w")
+    for tot_ms, n, d, tf, td, tw, fl in rows[:a.top]:
+        desc = f"{d[0]},{d[1]},{d[2]},{d[3]}->{d[4]},{d[5]}x{d[6]}/{d[9]}"
+        print(f"{desc:>34} {n:2d} | {tf:6.3f} {td:6.3f} {tw:6.3f} | {fl / tf / 1e9:5.1f} {fl / td / 1e9:5.1f} {fl / tw / 1e9:5.1f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,10 @@ CASES = [
     (8, 6, 1, 1, 144, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),        # SE expand
     (2, 64, 50, 50, 3, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),       # seg-head classifier
     (3, 24, 33, 17, 40, 5, 5, 2, (2, 2, 2, 2), 1, False, 1),     # odd sizes, k5/s2
+    (4, 24, 32, 32, 144, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),    # MBConv expand (1x1 wgrad path)
+    (3, 100, 8, 8, 70, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),      # 1x1, partial 32-tiles
+    (2, 336, 24, 24, 56, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),    # MBConv project
+    (2, 64, 20, 20, 3, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),       # 1x1 to 3 channels + bias
 ]
 
 
