@@ -611,8 +611,11 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
   p.bnt = cdiv(p.ncols, 128) * mblocks * p.nph >= 512 ? 128 : 64;
   const long long blocks = cdiv(p.ncols, p.bnt) * mblocks * p.nph;
   p.splits = 1;
-  if (blocks < 256 && p.nph == 1) {  // split K when the grid cannot fill the chip
-    int s = (int)((512 + blocks - 1) / blocks);
+  // split K when the grid cannot fill the chip twice over (measured best: aim at ~1024
+  // workgroups below 512, scripts/bench_conv.py)
+  const int target = 1024, thresh = 512;
+  if (blocks < thresh && p.nph == 1) {
+    int s = (int)((target + blocks - 1) / blocks);
     s = std::min(s, std::max(1, kmax / 4));
     s = std::min(s, 32);
     p.splits = std::max(1, s);

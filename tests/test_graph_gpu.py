@@ -58,3 +58,34 @@ def test_captured_bias_grad_replays():
         g.replay()
         torch.cuda.synchronize()
         assert torch.allclose(out["g"], ref, rtol=1e-6, atol=1e-9)
+
+
+def test_captured_predict_matches_eager():
+    """C5 path: ParkingModel.predict (B=1, eval) captured into one HIP graph replays the eager
+    result — control tokens identical, segmentation / depth bitwise equal (fixed noise)."""
+    from e2ep_amd import graphs, synthetic
+    from model.parking_model import ParkingModel
+    from tool.config import default_cfg
+    torch.manual_seed(0)
+    m = ParkingModel(default_cfg()).cuda().eval()
+    host = synthetic.synthetic_batch(1, seed=2)
+    host["gt_control"] = host["gt_control"][:, :1]
+    data = {k: (v if k in ("intrinsics", "extrinsics") else v.cuda()) for k, v in host.items()}
+    noise = synthetic.target_noise(1, seed=2).cuda()
+
+    def call():
+        with torch.no_grad():
+            return m.predict(data, noise)
+    ref = call()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        call()
+    torch.cuda.current_stream().wait_stream(s)
+    g, out, _ = graphs.capture(call)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out[0], ref[0])
+        assert torch.equal(out[1], ref[1]) and torch.equal(out[2], ref[2])
+        assert torch.equal(out[3], ref[3])
