@@ -35,6 +35,8 @@ def record(batch):
     out = [{"dims": json.loads(k)[0], "act": json.loads(k)[1], "bias": json.loads(k)[2],
             "grad_channels": json.loads(k)[3], "count": n} for k, n in seen.items()]
     json.dump(out, open(SHAPES, "w"), indent=0)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "conv_shapes.json"), "w"), indent=0)
     return out
 
 
