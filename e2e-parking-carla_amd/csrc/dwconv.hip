@@ -215,6 +215,54 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
   *reinterpret_cast<float4 *>(y + ((size_t)nc * g.P + oy) * g.Q + ox0) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// stride-2 data gradient over strip units: a wave owns RO = 64/(W/4) rows of dx of one plane,
+// each lane 4 adjacent dx pixels; the gy rows those rows read are staged in LDS.  For dx
+// pixel ix only taps b with (ix + pl - b) even contribute; ix0 is a multiple of 4, so the
+// parity of (u + pl - b) is compile-time given PLP = pl & 1.
+template <int K, int PLP>
+__global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restrict__ gy,
+                                                           const float *__restrict__ w, DwGeom g,
+                                                           int RO, int GR, int WPg,
+                                                           int units_per_plane, int units,
+                                                           float *__restrict__ dx) {
+  extern __shared__ float dw_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int unit = blockIdx.x * 4 + wave;
+  float *lds = dw_lds + wave * GR * WPg;
+  const bool active = unit < units;
+  int nc = 0, iy0 = 0, oyA = 0;
+  if (active) {
+    nc = unit / units_per_plane;
+    iy0 = (unit - nc * units_per_plane) * RO;
+    oyA = (iy0 + g.pt - (K - 1)) >> 1;  // floor division by 2
+    dw_stage(gy + (size_t)nc * g.P * g.Q, g.P, g.Q, oyA, GR, WPg, lds, lane);
+  }
+  __syncthreads();
+  if (!active) return;
+  const int c = nc % g.C;
+  float wr[K * K];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) wr[t] = w[c * K * K + t];
+  const int WL = g.W >> 2;
+  const int r = lane / WL, ix0 = 4 * (lane - r * WL);
+  const int iy = iy0 + r;
+  if (r >= RO || iy >= g.H) return;
+  const int xoff = (ix0 >> 1) + ((g.pl - PLP) >> 1) + DW_PADL;
+  float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const int ny = iy + g.pt - a;
+    if (ny & 1) continue;
+    const float *row = lds + ((ny >> 1) - oyA) * WPg + xoff;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int b = 0; b < K; ++b)
+        if (((u + PLP - b) & 1) == 0) o[u] = __builtin_fmaf(wr[a * K + b], row[(u + PLP - b) >> 1], o[u]);
+  }
+  *reinterpret_cast<float4 *>(dx + ((size_t)nc * g.H + iy) * g.W + ix0) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
 // weight gradient partials over strip units: grid (C, splits); the block's waves walk the
 // channel's units (n, strip) of its slice; per lane K*K register accumulators, fixed-order
 // wave + block reduction.
@@ -370,6 +418,25 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
                            4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx);
       return launch_status("e2ep_dwconv_dgrad");
     }
+  }
+  if (g.st == 2 && g.W % 4 == 0 && g.W <= 256 && g.Q % 4 == 0 && (g.K == 3 || g.K == 5) &&
+      g.pl <= 2 && g.pt <= 2) {
+    const int RO = 64 / (g.W / 4);
+    const int GR = ((RO - 1 + g.pt) >> 1) - ((g.pt - (g.K - 1)) >> 1) + 2;
+    const int WPg = g.Q + 2 * DW_PADL;
+    const int upp = (g.H + RO - 1) / RO, units = g.N * g.C * upp;
+    const size_t shm = 4 * GR * WPg * sizeof(float);
+    const dim3 grid(cdiv(units, 4));
+    const bool odd = g.pl & 1;
+    if (g.K == 3 && !odd)
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<3, 0>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+    else if (g.K == 3)
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<3, 1>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+    else if (!odd)
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<5, 0>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+    else
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<5, 1>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+    return launch_status("e2ep_dwconv_dgrad");
   }
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_dgrad: N*C > 65535");
   DW_DISPATCH(k_dw_dgrad, dim3(cdiv(g.H * g.W, 256), g.N * g.C), gy, w, g, dx);

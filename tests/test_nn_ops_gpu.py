@@ -123,7 +123,8 @@ def test_resize(case):
                                   (3, 8, 13, 11, 3, 2, (0, 1, 0, 1)), (2, 24, 128, 128, 3, 1, (1, 1, 1, 1)),
                                   (2, 8, 128, 128, 3, 2, (0, 1, 0, 1)), (2, 32, 64, 64, 3, 1, (1, 1, 1, 1)),
                                   (2, 40, 32, 32, 5, 1, (2, 2, 2, 2)), (3, 16, 16, 16, 3, 1, (1, 1, 1, 1)),
-                                  (2, 12, 24, 20, 5, 1, (2, 2, 2, 2))])
+                                  (2, 12, 24, 20, 5, 1, (2, 2, 2, 2)), (2, 16, 32, 32, 5, 2, (1, 2, 1, 2)),
+                                  (2, 8, 20, 24, 3, 2, (0, 1, 0, 1)), (2, 6, 64, 48, 5, 2, (2, 2, 2, 2))])
 def test_depthwise(case):
     from e2ep_amd import ops
     N, C, H, W, K, s, pad = case
