@@ -37,7 +37,27 @@ __global__ void __launch_bounds__(256) k_se_squeeze(const float *__restrict__ x,
   if ((threadIdx.x & 63) == 0) pooled[pl] = s / (float)HW;
 }
 
-// per sample n: hpre = W1 pooled + b1 (W1 [sq][C]);  a = W2 swish(hpre) + b2 (W2 [C][sq])
+// Block-wide sums of 16 per-thread values (fixed order: wave reduction, then waves 0..3).
+// Valid in red[0..15] after the call.
+__device__ __forceinline__ void block_sum16(float *v, float *red /* [4][16] */) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = wave_sum(v[j]);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) red[wave * 16 + j] = v[j];
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int j = threadIdx.x;
+    red[64 + j] = (red[j] + red[16 + j]) + (red[32 + j] + red[48 + j]);
+  }
+  __syncthreads();
+}
+
+// per sample n: hpre = W1 pooled + b1 (W1 [sq][C]);  a = W2 swish(hpre) + b2 (W2 [C][sq]).
+// grid (N, C-chunks of 256).  Every block recomputes the hidden vector with all 256 threads
+// (thread t takes channels t, t+256, ...; 16 hidden units at a time in registers, so its
+// loads are independent and coalesced), then its chunk of a (thread per c).
 __global__ void __launch_bounds__(256) k_se_mlp_fwd(const float *__restrict__ pooled,
                                                     const float *__restrict__ w1,
                                                     const float *__restrict__ b1,
@@ -45,24 +65,34 @@ __global__ void __launch_bounds__(256) k_se_mlp_fwd(const float *__restrict__ po
                                                     const float *__restrict__ b2, int C, int sq,
                                                     float *__restrict__ hpre,
                                                     float *__restrict__ a) {
-  __shared__ float sp[SE_MAXC], sh[SE_MAXSQ];
-  const int n = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = threadIdx.x; c < C; c += 256) sp[c] = pooled[(size_t)n * C + c];
-  __syncthreads();
-  for (int k = wave; k < sq; k += 4) {
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += w1[(size_t)k * C + c] * sp[c];
-    s = wave_sum(s);
-    if (lane == 0) {
-      const float v = s + (b1 ? b1[k] : 0.f);
-      hpre[(size_t)n * sq + k] = v;
-      sh[k] = v * sigm(v);
+  __shared__ float sh[SE_MAXSQ], red[80];
+  const int n = blockIdx.x;
+  const float *pn = pooled + (size_t)n * C;
+  for (int k0 = 0; k0 < sq; k0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float pv = pn[c];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (k0 + j < sq) v[j] += w1[(size_t)(k0 + j) * C + c] * pv;
+    }
+    block_sum16(v, red);
+    if (threadIdx.x < 16 && k0 + threadIdx.x < sq) {
+      const int k = k0 + threadIdx.x;
+      const float z = red[64 + threadIdx.x] + (b1 ? b1[k] : 0.f);
+      if (blockIdx.y == 0) hpre[(size_t)n * sq + k] = z;
+      sh[k] = z * sigm(z);
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c < C) {
     float s = b2 ? b2[c] : 0.f;
-    for (int k = 0; k < sq; ++k) s += w2[(size_t)c * sq + k] * sh[k];
+    const float *wr = w2 + (size_t)c * sq;
+#pragma unroll 8
+    for (int k = 0; k < sq; ++k) s += wr[k] * sh[k];
     a[(size_t)n * C + c] = s;
   }
 }
@@ -110,31 +140,43 @@ __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x,
   }
 }
 
-// per sample n: dh = W2^T da;  dhpre = dh * swish'(hpre);  dpooled = W1^T dhpre
+// per sample n: dh = W2^T da;  dhpre = dh * swish'(hpre);  dpooled = W1^T dhpre.
+// grid (N, C-chunks of 256); dh by all threads (channels strided over threads, 16 hidden
+// units at a time), then the block's chunk of dpooled (thread per c, coalesced W1 columns).
 __global__ void __launch_bounds__(256) k_se_mlp_bwd(const float *__restrict__ da,
                                                     const float *__restrict__ hpre,
                                                     const float *__restrict__ w1,
                                                     const float *__restrict__ w2, int C, int sq,
                                                     float *__restrict__ dhpre,
                                                     float *__restrict__ dpooled) {
-  __shared__ float sa[SE_MAXC], sd[SE_MAXSQ];
-  const int n = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = threadIdx.x; c < C; c += 256) sa[c] = da[(size_t)n * C + c];
-  __syncthreads();
-  for (int k = wave; k < sq; k += 4) {
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += w2[(size_t)c * sq + k] * sa[c];
-    s = wave_sum(s);
-    if (lane == 0) {
+  __shared__ float sd[SE_MAXSQ], red[80];
+  const int n = blockIdx.x;
+  const float *dn = da + (size_t)n * C;
+  for (int k0 = 0; k0 < sq; k0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float dv = dn[c];
+      const float *wr = w2 + (size_t)c * sq + k0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (k0 + j < sq) v[j] += wr[j] * dv;
+    }
+    block_sum16(v, red);
+    if (threadIdx.x < 16 && k0 + threadIdx.x < sq) {
+      const int k = k0 + threadIdx.x;
       const float z = hpre[(size_t)n * sq + k], sg = sigm(z);
-      const float v = s * (sg * (1.f + z * (1.f - sg)));
-      dhpre[(size_t)n * sq + k] = v;
-      sd[k] = v;
+      const float g = red[64 + threadIdx.x] * (sg * (1.f + z * (1.f - sg)));
+      if (blockIdx.y == 0) dhpre[(size_t)n * sq + k] = g;
+      sd[k] = g;
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c < C) {
     float s = 0.f;
+#pragma unroll 8
     for (int k = 0; k < sq; ++k) s += w1[(size_t)k * C + c] * sd[k];
     dpooled[(size_t)n * C + c] = s;
   }
@@ -155,10 +197,12 @@ __global__ void __launch_bounds__(256) k_se_wgrad(const float *__restrict__ pool
   float s = 0.f;
   if (i < n1) {
     const int k = i / C, c = i - k * C;
+#pragma unroll 8
     for (int n = 0; n < N; ++n) s += dhpre[(size_t)n * sq + k] * pooled[(size_t)n * C + c];
     if (dw1) dw1[i] = s;
   } else if (i < n1 + n2) {
     const int j = i - n1, c = j / sq, k = j - c * sq;
+#pragma unroll 8
     for (int n = 0; n < N; ++n) {
       const float z = hpre[(size_t)n * sq + k];
       s += da[(size_t)n * C + c] * (z * sigm(z));
@@ -166,10 +210,12 @@ __global__ void __launch_bounds__(256) k_se_wgrad(const float *__restrict__ pool
     if (dw2) dw2[j] = s;
   } else if (i < n1 + n2 + sq) {
     const int k = i - n1 - n2;
+#pragma unroll 8
     for (int n = 0; n < N; ++n) s += dhpre[(size_t)n * sq + k];
     if (db1) db1[k] = s;
   } else if (i < n1 + n2 + sq + C) {
     const int c = i - n1 - n2 - sq;
+#pragma unroll 8
     for (int n = 0; n < N; ++n) s += da[(size_t)n * C + c];
     if (db2) db2[c] = s;
   }
@@ -210,7 +256,8 @@ int e2ep_se_fwd(const float *x, const float *w1, const float *b1, const float *w
   hipStream_t s = as_stream(stream);
   const int planes = N * C;
   hipLaunchKernelGGL(k_se_squeeze, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, planes, HW, pooled);
-  hipLaunchKernelGGL(k_se_mlp_fwd, dim3(N), dim3(256), 0, s, pooled, w1, b1, w2, b2, C, sq, hpre, a);
+  hipLaunchKernelGGL(k_se_mlp_fwd, dim3(N, cdiv(C, 256)), dim3(256), 0, s, pooled, w1, b1, w2, b2, C,
+                     sq, hpre, a);
   const int vec = (HW & 3) == 0;
   const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
   hipLaunchKernelGGL(k_se_excite, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, a, HW, nvec, vec, y);
@@ -228,7 +275,8 @@ int e2ep_se_bwd(const float *x, const float *dy, const float *w1, const float *w
   const int planes = N * C;
   float *da = workspace, *dpooled = workspace + planes, *dhpre = workspace + 2 * planes;
   hipLaunchKernelGGL(k_se_da, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, dy, a, planes, HW, da);
-  hipLaunchKernelGGL(k_se_mlp_bwd, dim3(N), dim3(256), 0, s, da, hpre, w1, w2, C, sq, dhpre, dpooled);
+  hipLaunchKernelGGL(k_se_mlp_bwd, dim3(N, cdiv(C, 256)), dim3(256), 0, s, da, hpre, w1, w2, C, sq,
+                     dhpre, dpooled);
   if (dw1 || db1 || dw2 || db2) {
     const int outs = 2 * sq * C + sq + C;
     hipLaunchKernelGGL(k_se_wgrad, dim3(cdiv(outs, 256)), dim3(256), 0, s, pooled, hpre, da, dhpre,

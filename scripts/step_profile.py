@@ -8,10 +8,10 @@ import re
 
 
 def category(name):
-    for key, pat in (("conv fwd", r"k_conv_gemm<0"), ("conv dgrad", r"k_conv_gemm<1"),
-                     ("conv wgrad", r"k_conv_wgrad|k_reduce_splits"), ("bn", r"k_bn_"),
-                     ("depthwise", r"k_dw_"), ("hipBLASLt", r"Cijk_"), ("lift-splat", r"k_lss|k_transpose|k_target"),
-                     ("resize", r"k_resize"), ("se/pool", r"k_se_gate|k_avgpool|k_maxpool|k_skinny"),
+    for key, pat in (("conv fwd", r"k_conv_gemm<0|k_conv_reduce"), ("conv dgrad", r"k_conv_gemm<1"),
+                     ("conv wgrad", r"k_conv_wgrad|k_reduce_splits|k_wgrad_1x1"), ("bn", r"k_bn_"),
+                     ("depthwise", r"k_dw_"), ("hipBLASLt", r"Cijk_"), ("lift-splat", r"k_lss|k_target|k_tile"),
+                     ("resize", r"k_resize"), ("se/pool", r"k_se_|k_avgpool|k_maxpool|k_skinny"),
                      ("adam", r"k_adam"), ("torch", r"at::native|rocclr")):
         if re.search(pat, name):
             return key
