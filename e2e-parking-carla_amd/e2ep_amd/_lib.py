@@ -55,6 +55,9 @@ SIGNATURES = {
     "e2ep_maxpool3s2_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_avgpool_fwd": (_i, [_p, _i, _i, _p, _p]),
     "e2ep_avgpool_bwd": (_i, [_p, _i, _i, _p, _p]),
+    "e2ep_add_drop_ln_fwd": (_i, [_p, _p, _p, _f, _p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
+    "e2ep_add_drop_ln_bwd_workspace": (_sz, [_i, _i]),
+    "e2ep_add_drop_ln_bwd": (_i, [_p, _p, _p, _p, _p, _p, _f, _i, _i, _p, _p, _p, _p, _p, _p]),
     "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "e2ep_se_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
     "e2ep_se_gate_fwd": (_i, [_p, _p, _i, _i, _p, _p]),

@@ -371,3 +371,50 @@ def squeeze_excite(x, w1, b1, w2, b2):
     two 1x1 convs (w1 [sq,C,1,1], w2 [C,sq,1,1]) on the pooled 1x1 map."""
     _dev(x)
     return _SqueezeExcite.apply(x, w1, b1, w2, b2)
+
+
+# ------------------------------------------------------------------------------------------
+# residual add + dropout + LayerNorm (post-norm transformer layers)
+# ------------------------------------------------------------------------------------------
+class _AddDropLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, gamma, beta, u, p, eps):
+        a = a.contiguous()
+        b = b.contiguous()
+        E = a.shape[-1]
+        rows = a.numel() // E
+        x = torch.empty_like(a)
+        y = torch.empty_like(a)
+        mean = torch.empty(rows, dtype=torch.float32, device=a.device)
+        rstd = torch.empty_like(mean)
+        with timing.region("ln_fwd"):
+            _lib.call("e2ep_add_drop_ln_fwd", _lib.ptr(a), _lib.ptr(b), _lib.ptr(u), float(p),
+                      _lib.ptr(gamma), _lib.ptr(beta), rows, E, float(eps), _lib.ptr(x), _lib.ptr(y),
+                      _lib.ptr(mean), _lib.ptr(rstd), _lib.stream())
+        ctx.save_for_backward(x, mean, rstd, gamma, u)
+        ctx.p, ctx.rows, ctx.E = float(p), rows, E
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, gamma, u = ctx.saved_tensors
+        nig = ctx.needs_input_grad
+        da = torch.empty_like(x) if nig[0] else None
+        db = torch.empty_like(x) if nig[1] else None
+        dg = torch.empty_like(gamma) if (gamma is not None and nig[2]) else None
+        dbeta = torch.empty_like(gamma) if (gamma is not None and nig[3]) else None
+        ws = _ws(_lib.load().e2ep_add_drop_ln_bwd_workspace(ctx.rows, ctx.E), x.device)
+        with timing.region("ln_bwd"):
+            _lib.call("e2ep_add_drop_ln_bwd", _lib.ptr(dy.contiguous()), _lib.ptr(x), _lib.ptr(mean),
+                      _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(u), ctx.p, ctx.rows, ctx.E,
+                      _lib.ptr(da), _lib.ptr(db), _lib.ptr(dg), _lib.ptr(dbeta), _lib.ptr(ws),
+                      _lib.stream())
+        return da, db, dg, dbeta, None, None, None
+
+
+def add_drop_layer_norm(a, b, norm, p=0.0):
+    """norm(a + dropout_p(b)) for an nn.LayerNorm `norm` over the last dim, one fused op.
+    p > 0 draws the dropout mask with torch.rand_like (graph-capturable)."""
+    _dev(a, b)
+    u = torch.rand_like(b) if p > 0.0 else None
+    return _AddDropLN.apply(a, b, norm.weight, norm.bias, u, p, norm.eps)

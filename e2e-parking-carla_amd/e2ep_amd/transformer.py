@@ -1,17 +1,59 @@
 """Transformer encoder/decoder stacks of the fusion and control-decoder modules.
 
 d_model 258, 6 heads x 43, FFN 2048, post-norm, ReLU (reference model/feature_fusion.py:13-14,
-model/control_predict.py:19-20).  The layers are kept as torch.nn Transformer*Layer modules
-(state-dict keys and the agent's self_attn hook, agent/parking_agent.py:71-80); the arithmetic
-is routed here so the GEMMs/attention can run on e2ep kernels."""
+model/control_predict.py:19-20).  The layers stay torch.nn Transformer*Layer modules (state-dict
+keys and the agent's self_attn hook, agent/parking_agent.py:71-80); their forward is restated
+here with the same math and the same submodules, except that each "x + dropout(sublayer(x))
+-> LayerNorm" runs as one e2ep kernel (nn_ops.add_drop_layer_norm) instead of PyTorch's
+dropout + add + layer_norm (+ its slow gamma/beta backward).  The attention blocks and the
+linear layers are the modules' own (hipBLASLt GEMMs)."""
+import torch.nn.functional as F
+
+from . import nn_ops
+
+
+def _p(drop, training):
+    return drop.p if training else 0.0
+
+
+def _ff(layer, x):
+    return layer.linear2(layer.dropout(layer.activation(layer.linear1(x))))
+
+
+def encoder_layer(layer, x, mask=None, key_padding_mask=None):
+    """torch.nn.TransformerEncoderLayer.forward (norm_first=False), seq-first x (S, B, E)."""
+    assert not layer.norm_first
+    sa = layer.self_attn(x, x, x, attn_mask=mask, key_padding_mask=key_padding_mask,
+                         need_weights=False)[0]
+    x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
+    return nn_ops.add_drop_layer_norm(x, _ff(layer, x), layer.norm2, _p(layer.dropout2, layer.training))
+
+
+def decoder_layer(layer, x, memory, tgt_mask=None, tgt_key_padding_mask=None, tgt_is_causal=False):
+    """torch.nn.TransformerDecoderLayer.forward (norm_first=False), seq-first."""
+    assert not layer.norm_first
+    sa = layer.self_attn(x, x, x, attn_mask=tgt_mask, key_padding_mask=tgt_key_padding_mask,
+                         is_causal=bool(tgt_is_causal), need_weights=False)[0]
+    x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
+    ca = layer.multihead_attn(x, memory, memory, need_weights=False)[0]
+    x = nn_ops.add_drop_layer_norm(x, ca, layer.norm2, _p(layer.dropout2, layer.training))
+    return nn_ops.add_drop_layer_norm(x, _ff(layer, x), layer.norm3, _p(layer.dropout3, layer.training))
 
 
 def encoder(stack, tokens):
     """tokens (B, S, E) batch-first -> (B, S, E); the reference runs the stack seq-first."""
-    return stack(tokens.transpose(0, 1)).transpose(0, 1)
+    x = tokens.transpose(0, 1)
+    for layer in stack.layers:
+        x = encoder_layer(layer, x)
+    if stack.norm is not None:
+        x = stack.norm(x)
+    return x.transpose(0, 1)
 
 
 def decoder(stack, tgt, memory, tgt_mask, tgt_key_padding_mask, tgt_is_causal=None):
-    y = stack(tgt=tgt.transpose(0, 1), memory=memory.transpose(0, 1), tgt_mask=tgt_mask,
-              tgt_key_padding_mask=tgt_key_padding_mask, tgt_is_causal=tgt_is_causal)
-    return y.transpose(0, 1)
+    x, mem = tgt.transpose(0, 1), memory.transpose(0, 1)
+    for layer in stack.layers:
+        x = decoder_layer(layer, x, mem, tgt_mask, tgt_key_padding_mask, tgt_is_causal)
+    if stack.norm is not None:
+        x = stack.norm(x)
+    return x.transpose(0, 1)

@@ -213,6 +213,25 @@ int e2ep_se_bwd(const float *x, const float *dy, const float *w1, const float *w
                 float *workspace, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Residual add + dropout + LayerNorm of the post-norm transformer layers (torch
+ * TransformerEncoderLayer / TransformerDecoderLayer norm1..3 with dropout1..3; reference
+ * model/feature_fusion.py:13-14, model/control_predict.py:19-20), rows x E, E <= 512:
+ *   x = a + drop(b),  drop(b) = b * [u >= p] / (1 - p)  (u nullable: no dropout; b nullable)
+ *   y = (x - mean) * rstd * gamma + beta,  rstd = 1 / sqrt(biased var + eps)
+ * x (nullable), mean, rstd [rows] are saved for the backward, which returns da = dL/dx,
+ * db = da * [u >= p] / (1 - p) and gamma / beta gradients (fixed-order column sums;
+ * workspace e2ep_add_drop_ln_bwd_workspace bytes).
+ * ------------------------------------------------------------------------------------- */
+int e2ep_add_drop_ln_fwd(const float *a, const float *b, const float *u, float p,
+                         const float *gamma, const float *beta, int rows, int E, float eps,
+                         float *x, float *y, float *mean, float *rstd, void *stream);
+size_t e2ep_add_drop_ln_bwd_workspace(int rows, int E);
+int e2ep_add_drop_ln_bwd(const float *dy, const float *x, const float *mean, const float *rstd,
+                         const float *gamma, const float *u, float p, int rows, int E,
+                         float *da, float *db, float *dgamma, float *dbeta, void *workspace,
+                         void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Bilinear resize, align_corners=False (F.interpolate / nn.Upsample semantics) over
  * `planes` = N*C planes.  scale_* = 1/scale_factor when a factor is given, else In/Out.
  * Replaces model/bev_encoder.py:24, model/segmentation_head.py:35-38,

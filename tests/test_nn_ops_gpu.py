@@ -220,3 +220,27 @@ def test_squeeze_excite_fused(shape):
     assert rel_l2(y, y64) < 1e-6
     for got, ref in zip(ts, rs):
         assert rel_l2(got.grad, ref.grad) < 1e-5
+
+
+@pytest.mark.parametrize("rows,E,p", [(2048, 258, 0.1), (112, 258, 0.0), (37, 100, 0.5)])
+def test_add_dropout_layernorm_fused(rows, E, p):
+    """y = LayerNorm(a + dropout(b)) (transformer post-norm residual) vs fp64 torch, with the
+    dropout mask given by explicit uniforms; gradients of a, b, gamma, beta."""
+    from e2ep_amd import nn_ops
+    g = _g(rows + E)
+    a = torch.randn(rows, E, generator=g)
+    b = torch.randn(rows, E, generator=g)
+    u = torch.rand(rows, E, generator=g)
+    gamma = 1 + 0.2 * torch.randn(E, generator=g)
+    beta = 0.1 * torch.randn(E, generator=g)
+    dy = torch.randn(rows, E, generator=g)
+    ts = [t.to(DEV).requires_grad_(True) for t in (a, b, gamma, beta)]
+    y = nn_ops._AddDropLN.apply(ts[0], ts[1], ts[2], ts[3], u.to(DEV) if p > 0 else None, p, 1e-5)
+    y.backward(dy.to(DEV))
+    rs = [t.double().requires_grad_(True) for t in (a, b, gamma, beta)]
+    mask = (u >= p).double() / (1 - p) if p > 0 else torch.ones_like(u).double()
+    y64 = F.layer_norm(rs[0] + rs[1] * mask, (E,), rs[2], rs[3], 1e-5)
+    y64.backward(dy.double())
+    assert rel_l2(y, y64) < 1e-6
+    for got, ref in zip(ts, rs):
+        assert rel_l2(got.grad, ref.grad) < 1e-5
