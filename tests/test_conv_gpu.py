@@ -29,6 +29,9 @@ CASES = [
     (3, 100, 8, 8, 70, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),      # 1x1, partial 32-tiles
     (2, 336, 24, 24, 56, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),    # MBConv project
     (2, 64, 20, 20, 3, 1, 1, 1, (0, 0, 0, 0), 1, True, 0),       # 1x1 to 3 channels + bias
+    (2, 64, 24, 24, 64, 3, 3, 1, (1, 1, 1, 1), 1, False, 1),     # 3x3 s1 (tap wgrad path)
+    (2, 40, 16, 16, 24, 3, 3, 1, (2, 2, 2, 2), 2, False, 0),     # dilated 3x3, partial tiles
+    (2, 65, 20, 24, 48, 5, 5, 1, (2, 2, 2, 2), 1, True, 0),      # 5x5 s1
 ]
 
 
