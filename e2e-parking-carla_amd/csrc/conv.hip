@@ -162,8 +162,10 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   const bool a_vec = MODE == 0 && a_cstride == 1 && (g.Cin & 3) == 0;
   const int arow = (m0 + am) * a_mstride;
 
-  float ra[4], rb[BPER];
-  auto load_tiles = [&](int ks) {
+  // global -> register loads run two K-steps ahead of the MFMAs (two register sets), LDS
+  // is double buffered: one barrier per K-step, ~2 steps of MFMA work to cover a load
+  float ra0[4], rb0[BPER], ra1[4], rb1[BPER];
+  auto load_tiles = [&](int ks, float(&ra)[4], float(&rb)[BPER]) {
     const int tap = ks / csteps;                    // uniform
     const int c0 = (ks - tap * csteps) * BK;
     const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * a_tstride;
@@ -193,7 +195,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       rb[j] = bload(rx, (pix_ok && c < Kc) ? (pofs + c * HWs) * 4 : OOR);
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, const float(&ra)[4], const float(&rb)[BPER]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) As[buf][MODE == 0 ? ac + j : wave + 4 * j][am] = ra[j];
 #pragma unroll
@@ -203,15 +205,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   f32x16 acc[NACC];
 #pragma unroll
   for (int t = 0; t < NACC; ++t) acc[t] = f32x16{0};
-  if (nk > 0) {
-    load_tiles(kbeg);
-    store_tiles(0);
-  }
-  __syncthreads();
   const int li = lane & 31, lk = lane >> 5;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tiles(kbeg + kt + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const float a = As[buf][kk + lk][32 * wm + li];
@@ -221,7 +216,24 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) store_tiles(buf ^ 1);
+  };
+  if (nk > 0) {
+    load_tiles(kbeg, ra0, rb0);
+    store_tiles(0, ra0, rb0);
+  }
+  if (nk > 1) load_tiles(kbeg + 1, ra1, rb1);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    // buffer 0 holds step kt, registers 1 hold step kt+1
+    if (kt + 2 < nk) load_tiles(kbeg + kt + 2, ra0, rb0);
+    compute(0);
+    if (kt + 1 < nk) store_tiles(1, ra1, rb1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    // buffer 1 holds step kt+1, registers 0 hold step kt+2
+    if (kt + 3 < nk) load_tiles(kbeg + kt + 3, ra1, rb1);
+    compute(1);
+    if (kt + 2 < nk) store_tiles(0, ra0, rb0);
     __syncthreads();
   }
 
@@ -326,8 +338,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 
   const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
   const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
-  float ra[4], rb[4];
-  auto load_tiles = [&]() {
+  float ra0[4], rb0[4], ra1[4], rb1[4];  // two register sets: loads run two K-steps ahead
+  auto load_tiles = [&](float(&ra)[4], float(&rb)[4]) {
     const bool pok = p_cur < pend;
     const int oy = od / g.Q, ox = od - oy * g.Q;
     const int gb = im * g.Cout * PQ + od;
@@ -351,7 +363,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
       ++im;
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, const float(&ra)[4], const float(&rb)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) As[buf][tp][trow + 16 * j] = ra[j];
 #pragma unroll
@@ -361,21 +373,29 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   f32x16 acc = {0};
   const int nk = (pend - pbeg + BK - 1) / BK;
   const int li = lane & 31, lk = lane >> 5;
-  if (nk > 0) {
-    load_tiles();
-    store_tiles(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tiles();
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const float a = As[buf][kk + lk][32 * wm + li];
       const float b = Bs[buf][kk + lk][32 * wn + li];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles(buf ^ 1);
+  };
+  if (nk > 0) {
+    load_tiles(ra0, rb0);
+    store_tiles(0, ra0, rb0);
+  }
+  if (nk > 1) load_tiles(ra1, rb1);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    if (kt + 2 < nk) load_tiles(ra0, rb0);
+    compute(0);
+    if (kt + 1 < nk) store_tiles(1, ra1, rb1);
+    __syncthreads();
+    if (kt + 1 >= nk) break;
+    if (kt + 3 < nk) load_tiles(ra1, rb1);
+    compute(1);
+    if (kt + 2 < nk) store_tiles(0, ra0, rb0);
     __syncthreads();
   }
   const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
