@@ -55,22 +55,26 @@ __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : 
 // MODE 1: rows m = ci, K channels c = co, src = g [N,Cout,P,Q], dst = dx [N,Cin,H,W];
 //         phase z = (py, px), column pixel (u,v) -> (iy, ix) = (py + sh*u, px + sw*v);
 //         tap (r,s) valid for the phase: qy = u + (py + ph - r*dh)/sh (exact), qx likewise.
-template <int MODE, int ACT, int BNT>
+template <int MODE, int ACT, int BNT, int BMT = BM>
 __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
-  constexpr int NACC = BNT / 64;
-  constexpr int BROWS = 256 / BNT;  // B rows per pass (2 or 4)
-  constexpr int BPER = BK / BROWS;  // B loads per thread (8 or 4)
-  __shared__ float As[2][BK][BM + PADA];
+  // block tile BMT x BNT: BMT = 64 -> 2 x 2 waves of 32 x BNT/2; BMT = 32 (small-M layers:
+  // Cout or Cin 24..56) -> 1 x 4 waves of 32 x BNT/4, so no MFMA rows are padding
+  constexpr int WC = BMT == 64 ? BNT / 2 : BNT / 4;  // columns per wave
+  constexpr int NACC = WC / 32;
+  constexpr int BROWS = 256 / BNT;  // B rows per pass (1, 2 or 4)
+  constexpr int BPER = BK / BROWS;  // B loads per thread (16, 8 or 4)
+  constexpr int NA = BK * BMT / 256;  // A loads per thread (4 or 2)
+  __shared__ float As[2][BK][BMT + PADA];
   __shared__ float Bs[2][BK][BNT + PADB];
   __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
   __shared__ int s_ntaps;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BNT;
+  const int wm = BMT == 64 ? (wave & 1) : 0, wn = BMT == 64 ? (wave >> 1) : wave;
+  const int m0 = blockIdx.y * BMT, n0 = blockIdx.x * BNT;
   const int split = blockIdx.z % splits, z = blockIdx.z / splits;
   const int RS = g.R * g.S;
 
@@ -132,7 +136,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
 
   // B-load column of this thread (fixed); its rows are wave-uniform
   const int bn = tid % BNT;
-  const int bk0 = BNT == 128 ? (wave >> 1) : wave;
+  const int bk0 = tid / BNT;
   const int ncol = n0 + bn;
   const bool col_ok = ncol < Ntot;
   int img = 0, cp = 0;
@@ -148,8 +152,9 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   // A-load row of this thread; its k rows (channels) are wave-uniform (dgrad).  Forward
   // loads run along the weight's channel axis instead (thread = row tid/4, channels
   // 4*(tid%4)..+3: float4 for 1x1 filters), so a wave touches 16 weight rows, not 64.
-  const int am = MODE == 0 ? (tid >> 2) : (tid & (BM - 1));
-  const int ac = MODE == 0 ? 4 * (tid & 3) : 0;
+  const int am = MODE == 0 ? tid / (BK / NA) : (tid & (BMT - 1));
+  const int ac = MODE == 0 ? NA * (tid % (BK / NA)) : 0;
+  const int ak0 = tid / BMT;  // dgrad: this thread's first k row (then every 256/BMT)
   const bool arow_ok = (m0 + am) < M;
   // weight layout 0 (PyTorch [Cout][Cin][RS]):
   //   fwd: W[m][c][rs] = w[m*Cin*RS + c*RS + rs];  dgrad: W[c][m][rs] = w[c*Cin*RS + m*RS + rs]
@@ -159,13 +164,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   const int a_mstride = MODE == 0 ? (tm ? g.Cin : g.Cin * RS) : (tm ? 1 : RS);
   const int a_cstride = MODE == 0 ? (tm ? 1 : RS) : (tm ? g.Cin : g.Cin * RS);
   const int a_tstride = tm ? g.Cout * g.Cin : 1;
-  const bool a_vec = MODE == 0 && a_cstride == 1 && (g.Cin & 3) == 0;
+  const bool a_vec = NA == 4 && MODE == 0 && a_cstride == 1 && (g.Cin & 3) == 0;
   const int arow = (m0 + am) * a_mstride;
 
   // global -> register loads run two K-steps ahead of the MFMAs (two register sets), LDS
   // is double buffered: one barrier per K-step, ~2 steps of MFMA work to cover a load
-  float ra0[4], rb0[BPER], ra1[4], rb1[BPER];
-  auto load_tiles = [&](int ks, float(&ra)[4], float(&rb)[BPER]) {
+  float ra0[NA], rb0[BPER], ra1[NA], rb1[BPER];
+  auto load_tiles = [&](int ks, float(&ra)[NA], float(&rb)[BPER]) {
     const int tap = ks / csteps;                    // uniform
     const int c0 = (ks - tap * csteps) * BK;
     const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * a_tstride;
@@ -173,16 +178,16 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       const int c = c0 + ac;
       if (a_vec) {
         const float4 v = bload4(rw, (arow_ok && c < Kc) ? (arow + c + rs) * 4 : OOR);
-        ra[0] = v.x; ra[1] = v.y; ra[2] = v.z; ra[3] = v.w;
+        ra[0] = v.x; ra[1] = v.y; ra[NA > 2 ? 2 : 0] = v.z; ra[NA > 3 ? 3 : 0] = v.w;
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NA; ++j)
           ra[j] = bload(rw, (arow_ok && c + j < Kc) ? (arow + (c + j) * a_cstride + rs) * 4 : OOR);
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = c0 + wave + 4 * j;
+      for (int j = 0; j < NA; ++j) {
+        const int c = c0 + ak0 + (256 / BMT) * j;
         ra[j] = bload(rw, (arow_ok && c < Kc) ? (arow + c * a_cstride + rs) * 4 : OOR);
       }
     }
@@ -195,9 +200,9 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       rb[j] = bload(rx, (pix_ok && c < Kc) ? (pofs + c * HWs) * 4 : OOR);
     }
   };
-  auto store_tiles = [&](int buf, const float(&ra)[4], const float(&rb)[BPER]) {
+  auto store_tiles = [&](int buf, const float(&ra)[NA], const float(&rb)[BPER]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) As[buf][MODE == 0 ? ac + j : wave + 4 * j][am] = ra[j];
+    for (int j = 0; j < NA; ++j) As[buf][MODE == 0 ? ac + j : ak0 + (256 / BMT) * j][am] = ra[j];
 #pragma unroll
     for (int j = 0; j < BPER; ++j) Bs[buf][bk0 + BROWS * j][bn] = rb[j];
   };
@@ -212,7 +217,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       const float a = As[buf][kk + lk][32 * wm + li];
 #pragma unroll
       for (int t = 0; t < NACC; ++t) {
-        const float b = Bs[buf][kk + lk][(BNT / 2) * wn + 32 * t + li];
+        const float b = Bs[buf][kk + lk][WC * wn + 32 * t + li];
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
       }
     }
@@ -245,7 +250,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   const int HWd = Hd * Wd;
 #pragma unroll
   for (int t = 0; t < NACC; ++t) {
-    const int n = n0 + (BNT / 2) * wn + 32 * t + li;
+    const int n = n0 + WC * wn + 32 * t + li;
     const bool nok = n < Ntot;
     int dbase, mstride;
     if (splits == 1) {
@@ -601,7 +606,7 @@ static int valid_taps(int p, int pad, int K, int dil, int st) {
 }
 
 struct GemmPlan {
-  int bnt, splits, kper, nph;
+  int bm, bnt, splits, kper, nph;
   long long ncols;  // columns of the largest phase
 };
 
@@ -627,8 +632,12 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
       kmax = std::max(kmax, taps * csteps);
     }
   }
-  const long long mblocks = cdiv(M, BM);
-  p.bnt = cdiv(p.ncols, 128) * mblocks * p.nph >= 512 ? 128 : 64;
+  // 32-row tiles when 64-row tiles would pad M by more than 25 % (M = 24, 32, 96; measured:
+  // for smaller savings the wider tile's better reuse wins, scripts/bench_conv.py)
+  p.bm = 5LL * cdiv(M, 32) * 32 <= 4LL * cdiv(M, 64) * 64 ? 32 : 64;
+  const long long mblocks = cdiv(M, p.bm);
+  const int wide_n = p.bm == 64 ? 128 : 256;
+  p.bnt = cdiv(p.ncols, wide_n) * mblocks * p.nph >= 512 ? wide_n : wide_n / 2;
   const long long blocks = cdiv(p.ncols, p.bnt) * mblocks * p.nph;
   p.splits = 1;
   // split K when the grid cannot fill the chip twice over (measured best: aim at ~1024
@@ -653,7 +662,7 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
                        float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
                        hipStream_t s) {
   const GemmPlan p = plan_gemm(mode, g, M);
-  dim3 grid(cdiv(p.ncols, p.bnt), cdiv(M, BM), p.nph * p.splits);
+  dim3 grid(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
   float *out = dst;
   long long out_bytes = dst_bytes;
   if (p.splits > 1) {
@@ -664,13 +673,23 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     out = static_cast<float *>(workspace);
     out_bytes = (long long)gemm_workspace(p, M);
   }
-#define GEMM_LAUNCH(MD, AC, BT)                                                              \
-  hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT>), grid, dim3(256), 0, s, w, src, bias, out,     \
+#define GEMM_LAUNCH(MD, AC, BT, BMT)                                                         \
+  hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT>), grid, dim3(256), 0, s, w, src, bias, out, \
                      out_bytes, g, M, p.splits, p.kper)
-  const bool wide = p.bnt == 128;
-  if (mode == 0 && act == 0) { if (wide) GEMM_LAUNCH(0, 0, 128); else GEMM_LAUNCH(0, 0, 64); }
-  else if (mode == 0) { if (wide) GEMM_LAUNCH(0, 1, 128); else GEMM_LAUNCH(0, 1, 64); }
-  else { if (wide) GEMM_LAUNCH(1, 0, 128); else GEMM_LAUNCH(1, 0, 64); }
+#define GEMM_TILES(MD, AC)                                             \
+  do {                                                                 \
+    if (p.bm == 64) {                                                  \
+      if (p.bnt == 128) GEMM_LAUNCH(MD, AC, 128, 64);                  \
+      else GEMM_LAUNCH(MD, AC, 64, 64);                                \
+    } else {                                                           \
+      if (p.bnt == 256) GEMM_LAUNCH(MD, AC, 256, 32);                  \
+      else GEMM_LAUNCH(MD, AC, 128, 32);                               \
+    }                                                                  \
+  } while (0)
+  if (mode == 0 && act == 0) GEMM_TILES(0, 0);
+  else if (mode == 0) GEMM_TILES(0, 1);
+  else GEMM_TILES(1, 0);
+#undef GEMM_TILES
 #undef GEMM_LAUNCH
   if (p.splits > 1) {
     const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;

@@ -87,13 +87,15 @@ __global__ void __launch_bounds__(256) k_se_mlp_fwd(const float *__restrict__ po
     }
   }
   __syncthreads();
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (c < C) {
-    float s = b2 ? b2[c] : 0.f;
+  // a[c] for this block's 256 channels: wave per channel, lanes along the W2 row (coalesced)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cend = min(C, (blockIdx.y + 1) * 256);
+  for (int c = blockIdx.y * 256 + wave; c < cend; c += 4) {
     const float *wr = w2 + (size_t)c * sq;
-#pragma unroll 8
-    for (int k = 0; k < sq; ++k) s += wr[k] * sh[k];
-    a[(size_t)n * C + c] = s;
+    float s = 0.f;
+    for (int k = lane; k < sq; k += 64) s += wr[k] * sh[k];
+    s = wave_sum(s);
+    if (lane == 0) a[(size_t)n * C + c] = s + (b2 ? b2[c] : 0.f);
   }
 }
 
