@@ -180,6 +180,42 @@ __global__ void __launch_bounds__(256) k_bn_apply(
   }
 }
 
+// statistics only (for a consumer that applies the normalisation on load, e.g. the depthwise
+// conv): grid (C); mean / invstd, the folded scale / shift (sc = gamma * invstd,
+// sh = beta - mean * sc, the same arithmetic as k_bn_apply) and the running-stat update
+__global__ void __launch_bounds__(256) k_bn_finalize(
+    const double *__restrict__ part, int splits, long long cnt, float eps, float momentum,
+    float *__restrict__ running_mean, float *__restrict__ running_var, float *__restrict__ mean_out,
+    float *__restrict__ invstd_out, const float *__restrict__ gamma, const float *__restrict__ beta,
+    float *__restrict__ scale, float *__restrict__ shift) {
+  const int c = blockIdx.x;
+  float mu, is;
+  if (part) {
+    double s, q;
+    channel_partials(part, c, splits, s, q);
+    if (threadIdx.x != 0) return;
+    const double m = s / (double)cnt;
+    double var = q / (double)cnt - m * m;
+    if (var < 0.0) var = 0.0;
+    mu = (float)m;
+    is = (float)(1.0 / sqrt(var + (double)eps));
+    if (running_mean) {
+      const double unb = cnt > 1 ? var * (double)cnt / (double)(cnt - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * m);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+    }
+  } else {
+    if (threadIdx.x != 0) return;
+    mu = running_mean[c];
+    is = (float)(1.0 / sqrt((double)running_var[c] + (double)eps));
+  }
+  mean_out[c] = mu;
+  invstd_out[c] = is;
+  const float sc = is * (gamma ? gamma[c] : 1.f);
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - mu * sc;
+}
+
 // backward pieces shared by reduce and apply: from x, dy (and res / drop-connect), returns
 // xhat, dz (gradient at the activation input = dres) and dzb (gradient at the BN output)
 template <int VEC>
@@ -362,6 +398,38 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
                        running_mean, running_var, mean, invstd, gamma, beta, res, dc_rand, dc_keep,
                        N, C, HWv, APPLY_PER, act, y);
   return launch_status("e2ep_bn_fwd");
+}
+
+int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *running_mean,
+                  float *running_var, int N, int C, int H, int W, int train, float momentum,
+                  float eps, float *mean, float *invstd, float *scale, float *shift,
+                  void *workspace, void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
+               E2EP_EINVAL, "e2ep_bn_stats: bad shape");
+  E2EP_REQUIRE(train || (running_mean && running_var), E2EP_EINVAL,
+               "e2ep_bn_stats: eval needs running stats");
+  E2EP_REQUIRE(mean && invstd && scale && shift, E2EP_EINVAL, "e2ep_bn_stats: null output");
+  hipStream_t s = as_stream(stream);
+  const int HW = H * W;
+  const long long per_c = (long long)N * HW;
+  const bool v4 = (HW & 3) == 0;
+  const int HWv = v4 ? HW / 4 : HW;
+  const int totv = N * HWv;
+  double *part = nullptr;
+  int sp = 1;
+  if (train) {
+    sp = bn_splits(per_c, C);
+    const int per = cdiv(totv, sp);
+    sp = cdiv(totv, per);
+    part = static_cast<double *>(workspace);
+    if (v4)
+      hipLaunchKernelGGL(k_bn_stats<4>, dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
+    else
+      hipLaunchKernelGGL(k_bn_stats<1>, dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
+  }
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(256), 0, s, part, sp, per_c, eps, momentum,
+                     running_mean, running_var, mean, invstd, gamma, beta, scale, shift);
+  return launch_status("e2ep_bn_stats");
 }
 
 int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,

@@ -10,11 +10,25 @@ struct DwGeom {
   int N, C, H, W, K, P, Q, st, pt, pl;
 };
 
+// Optional input transform of the forward / weight-gradient kernels: the input is the raw
+// output of the preceding 1x1 conv and the kernel applies that layer's BatchNorm (per-channel
+// scale / shift from e2ep_bn_stats) and activation on load, so the normalised tensor is never
+// written (zero padding stays zero: it lives in the normalised space).
+struct DwIn {
+  const float *sc, *sh;  // [C] or null (identity)
+  int act;               // 0 none, 1 relu, 2 swish
+};
+__device__ __forceinline__ float dw_in(float v, float sc, float sh, int act) {
+  const float z = v * sc + sh;
+  return act == 2 ? z / (1.f + expf(-z)) : act == 1 ? fmaxf(z, 0.f) : z;
+}
+
 // forward: one thread per output pixel; taps unrolled; branch-free guarded loads
 template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
                                                 const float *__restrict__ w, DwGeom g,
-                                                float *__restrict__ y) {
+                                                float *__restrict__ y, const float *__restrict__ tsc,
+                                                const float *__restrict__ tsh, int tact) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= g.P * g.Q) return;
   const int nc = blockIdx.y;
@@ -33,6 +47,7 @@ __global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
       const int ix = x0 + b;
       const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
       v[a * K + b] = bload(rx, ok ? (iy * g.W + ix) * 4 : OOR);
+      if (tsc && ok) v[a * K + b] = dw_in(v[a * K + b], tsc[c], tsh[c], tact);
     }
   }
   float s = 0.f;
@@ -79,7 +94,9 @@ __global__ void __launch_bounds__(256) k_dw_dgrad(const float *__restrict__ gy,
 template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
                                                   const float *__restrict__ x, DwGeom g,
-                                                  int splits, float *__restrict__ part) {
+                                                  int splits, float *__restrict__ part,
+                                                  const float *__restrict__ tsc,
+                                                  const float *__restrict__ tsh, int tact) {
   const int c = blockIdx.x, sp = blockIdx.y;
   const int PQ = g.P * g.Q;
   const int tot = g.N * PQ;
@@ -105,7 +122,9 @@ __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
       for (int b = 0; b < K; ++b) {
         const int ix = x0 + b;
         const bool ok = oky && (unsigned)ix < (unsigned)g.W;
-        acc[a * K + b] += gv * bload(rx, ok ? (xb + iy * g.W + ix) * 4 : OOR);
+        float xv = bload(rx, ok ? (xb + iy * g.W + ix) * 4 : OOR);
+        if (tsc && ok) xv = dw_in(xv, tsc[c], tsh[c], tact);
+        acc[a * K + b] += gv * xv;
       }
     }
   }
@@ -158,13 +177,24 @@ static DwStrip dw_strip(int K, int st, int W, int P, int Q) {
 
 // stage input rows [iy0, iy0 + IR) of plane `src` (H x W) into this wave's LDS buffer
 __device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, int W, int iy0,
-                                         int IR, int WP, float *lds, int lane) {
+                                         int IR, int WP, float *lds, int lane,
+                                         DwIn tf = DwIn{nullptr, nullptr, 0}, int c = 0) {
   const int W4 = W >> 2;
+  const bool t = tf.sc != nullptr;
+  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
   for (int e = lane; e < IR * W4; e += 64) {
     const int r = e / W4, j = e - r * W4;
     const int iy = iy0 + r;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)iy < (unsigned)H) v = *reinterpret_cast<const float4 *>(src + (size_t)iy * W + 4 * j);
+    if ((unsigned)iy < (unsigned)H) {
+      v = *reinterpret_cast<const float4 *>(src + (size_t)iy * W + 4 * j);
+      if (t) {
+        v.x = dw_in(v.x, sc, sh, tf.act);
+        v.y = dw_in(v.y, sc, sh, tf.act);
+        v.z = dw_in(v.z, sc, sh, tf.act);
+        v.w = dw_in(v.w, sc, sh, tf.act);
+      }
+    }
     *reinterpret_cast<float4 *>(lds + r * WP + DW_PADL + 4 * j) = v;
   }
   // halo columns
@@ -177,7 +207,8 @@ __device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, i
 template <int K, int ST, bool FLIP>
 __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
                                                       const float *__restrict__ w, DwGeom g,
-                                                      DwStrip d, int units, float *__restrict__ y) {
+                                                      DwStrip d, int units, float *__restrict__ y,
+                                                      DwIn tf) {
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int unit = blockIdx.x * 4 + wave;
@@ -187,7 +218,8 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
   if (active) {
     nc = unit / d.units_per_plane;
     oy0 = (unit - nc * d.units_per_plane) * d.RO;
-    dw_stage(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane);
+    dw_stage(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane, tf,
+             nc % g.C);
   }
   __syncthreads();
   if (!active) return;
@@ -270,7 +302,7 @@ template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
                                                         const float *__restrict__ x, DwGeom g,
                                                         DwStrip d, int splits,
-                                                        float *__restrict__ part) {
+                                                        float *__restrict__ part, DwIn tf) {
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x, sp = blockIdx.y;
@@ -292,7 +324,8 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
     if (active) {
       n = un / d.units_per_plane;
       oy0 = (un - n * d.units_per_plane) * d.RO;
-      dw_stage(x + ((size_t)n * g.C + c) * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane);
+      dw_stage(x + ((size_t)n * g.C + c) * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds,
+               lane, tf, c);
     }
     __syncthreads();
     const int oy = oy0 + ro;
@@ -382,19 +415,24 @@ static bool dw_strip_ok(const DwGeom &g) {
 #define DW_NONE
 
 // dims[10] = {N, C, H, W, K, P, Q, stride, pad_top, pad_left}
-int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, float *y, void *stream) {
+int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float *in_scale,
+                    const float *in_shift, int in_act, float *y, void *stream) {
   DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(!in_scale == !in_shift && in_act >= 0 && in_act <= 2, E2EP_EINVAL,
+               "e2ep_dwconv_fwd: in_scale / in_shift both or neither, in_act 0..2");
+  const DwIn tf{in_scale, in_shift, in_act};
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_fwd: bad geometry");
   if (dw_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     const int units = g.N * g.C * d.units_per_plane;
     DW_STRIP_DISPATCH(k_dw_fwd_strip, DW_NOFLIP, dim3(cdiv(units, 4)), 4 * d.IR * d.WP * 4, x, w, g,
-                      d, units, y);
+                      d, units, y, tf);
     return launch_status("e2ep_dwconv_fwd");
   }
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_fwd: N*C > 65535");
-  DW_DISPATCH(k_dw_fwd, dim3(cdiv(g.P * g.Q, 256), g.N * g.C), x, w, g, y);
+  DW_DISPATCH(k_dw_fwd, dim3(cdiv(g.P * g.Q, 256), g.N * g.C), x, w, g, y, in_scale, in_shift,
+              in_act);
   return launch_status("e2ep_dwconv_fwd");
 }
 
@@ -412,10 +450,12 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
       const int units = t.N * t.C * d.units_per_plane;
       if (t.K == 3)
         hipLaunchKernelGGL((k_dw_fwd_strip<3, 1, true>), dim3(cdiv(units, 4)), dim3(256),
-                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx);
+                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx,
+                           DwIn{nullptr, nullptr, 0});
       else
         hipLaunchKernelGGL((k_dw_fwd_strip<5, 1, true>), dim3(cdiv(units, 4)), dim3(256),
-                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx);
+                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx,
+                           DwIn{nullptr, nullptr, 0});
       return launch_status("e2ep_dwconv_dgrad");
     }
   }
@@ -460,9 +500,12 @@ size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
   return (size_t)g.C * dw_wgrad_splits(g) * g.K * g.K * sizeof(float);
 }
 
-int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, void *workspace, float *dw,
-                      void *stream) {
+int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
+                      const float *in_shift, int in_act, void *workspace, float *dw, void *stream) {
   DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(!in_scale == !in_shift && in_act >= 0 && in_act <= 2, E2EP_EINVAL,
+               "e2ep_dwconv_wgrad: in_scale / in_shift both or neither, in_act 0..2");
+  const DwIn tf{in_scale, in_shift, in_act};
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_wgrad: bad geometry");
   const int sp = dw_wgrad_splits(g);
@@ -470,9 +513,9 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, void *wo
   if (dw_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     DW_STRIP_DISPATCH(k_dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
-                      sp, part);
+                      sp, part, tf);
   } else {
-    DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part);
+    DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part, in_scale, in_shift, in_act);
   }
   hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0,
                      as_stream(stream), part, g.C, g.K * g.K, sp, dw);

@@ -41,16 +41,17 @@ SIGNATURES = {
     "e2ep_skinny_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _i, _i, _i, _p, _p]),
     "e2ep_bn_workspace": (_sz, [_i, _i, _i, _i]),
     "e2ep_bn_fwd": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i, _p, _p, _p, _p, _p]),
+    "e2ep_bn_stats": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _p]),
     "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
     "e2ep_act_fwd": (_i, [_p, _i64, _i, _p, _p]),
     "e2ep_act_bwd": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_resize_fwd": (_i, [_p, _i, _i, _i64, _i, _i, _i, _i, _f, _f, _p, _i64, _p]),
     "e2ep_resize_bwd_workspace": (_sz, [_i, _i, _i]),
     "e2ep_resize_bwd": (_i, [_p, _i64, _i, _i, _i, _i, _i, _f, _f, _p, _i, _p, _p]),
-    "e2ep_dwconv_fwd": (_i, [_p, _p, _p, _p, _p]),
+    "e2ep_dwconv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p]),
     "e2ep_dwconv_dgrad": (_i, [_p, _p, _p, _p, _p]),
     "e2ep_dwconv_wgrad_workspace": (_sz, [_p]),
-    "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _p]),
+    "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p]),
     "e2ep_maxpool3s2_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p]),
     "e2ep_maxpool3s2_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_avgpool_fwd": (_i, [_p, _i, _i, _p, _p]),

@@ -101,17 +101,22 @@ class BnCounters:
 _COUNTERS = []  # stack of active BnCounters (innermost last)
 
 
-def batch_norm_act(x, bn, act=None, res=None, dc_rand=None, dc_keep=1.0):
-    """BatchNorm2d module `bn` (its train/eval mode, momentum, eps, running buffers) applied
-    to x, then optional drop-connect (dc_rand: per-sample uniform draws, training only), an
-    optional residual, then the activation."""
-    _dev(x, res, dc_rand)
-    train = bn.training or not bn.track_running_stats
+def _bn_train_and_count(bn):
+    """BatchNorm2d.forward's mode choice and num_batches_tracked increment."""
     if bn.training and bn.track_running_stats:
         if _COUNTERS:
             _COUNTERS[-1].note(bn)
         else:
             bn.num_batches_tracked.add_(1)
+    return bn.training or not bn.track_running_stats
+
+
+def batch_norm_act(x, bn, act=None, res=None, dc_rand=None, dc_keep=1.0):
+    """BatchNorm2d module `bn` (its train/eval mode, momentum, eps, running buffers) applied
+    to x, then optional drop-connect (dc_rand: per-sample uniform draws, training only), an
+    optional residual, then the activation."""
+    _dev(x, res, dc_rand)
+    train = _bn_train_and_count(bn)
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     mom = bn.momentum if bn.momentum is not None else 0.1
@@ -198,7 +203,8 @@ class _DwConv(torch.autograd.Function):
         y = torch.empty(N, C, P, Q, dtype=torch.float32, device=x.device)
         d = _lib.dims(dims)
         with timing.region("dwconv_fwd"):
-            _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(y), _lib.stream())
+            _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, None, None, 0, _lib.ptr(y),
+                      _lib.stream())
         ctx.save_for_backward(x, w)
         ctx.dims = dims
         return y
@@ -218,9 +224,70 @@ class _DwConv(torch.autograd.Function):
             dw = torch.empty_like(w)
             ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
             with timing.region("dwconv_wgrad"):
-                _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(ws),
-                          _lib.ptr(dw), s)
+                _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
+                          _lib.ptr(ws), _lib.ptr(dw), s)
         return dx, dw, None
+
+
+class _BnActDwConv(torch.autograd.Function):
+    """depthwise_conv(act(bn(x))) with the BN + activation applied while the depthwise
+    kernel stages its input: the normalised tensor is never stored (MBConv's
+    _bn0 -> swish -> _depthwise_conv, reference model/cam_encoder.py:70-72 via
+    efficientnet-pytorch MBConvBlock.forward).  Same arithmetic as batch_norm_act followed by
+    depthwise_conv2d."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, act, w, dims):
+        x = x.contiguous()
+        w = w.contiguous()
+        N, C, H, W, K, P, Q = dims[:7]
+        f32 = dict(dtype=torch.float32, device=x.device)
+        stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
+        ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
+        s = _lib.stream()
+        with timing.region("bn_fwd"):
+            _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
+                      _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
+                      _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
+                      _lib.ptr(stats[3]), _lib.ptr(ws), s)
+        y = torch.empty(N, C, P, Q, **f32)
+        d = _lib.dims(dims)
+        with timing.region("dwconv_fwd"):
+            _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(stats[2]),
+                      _lib.ptr(stats[3]), act, _lib.ptr(y), s)
+        ctx.save_for_backward(x, gamma, beta, w, stats)
+        ctx.dims, ctx.train, ctx.act = dims, train, act
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, gamma, beta, w, stats = ctx.saved_tensors
+        gy = gy.contiguous()
+        N, C, H, W = x.shape
+        d = _lib.dims(ctx.dims)
+        s = _lib.stream()
+        nig = ctx.needs_input_grad
+        dw = dx = dg = db = None
+        if nig[9]:
+            dw = torch.empty_like(w)
+            ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
+            with timing.region("dwconv_wgrad"):
+                _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(stats[2]),
+                          _lib.ptr(stats[3]), ctx.act, _lib.ptr(ws), _lib.ptr(dw), s)
+        if nig[0] or nig[1] or nig[2]:
+            dt = torch.empty_like(x)  # gradient at the activation output
+            with timing.region("dwconv_dgrad"):
+                _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s)
+            dx = torch.empty_like(x) if nig[0] else None
+            dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
+            db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
+            ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
+            with timing.region("bn_bwd"):
+                _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dt), _lib.ptr(stats[0]),
+                          _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
+                          N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx), _lib.ptr(dg),
+                          _lib.ptr(db), None, _lib.ptr(ws), s)
+        return dx, dg, db, None, None, None, None, None, None, dw, None
 
 
 def depthwise_conv2d(x, w, stride, pad):
@@ -232,6 +299,22 @@ def depthwise_conv2d(x, w, stride, pad):
     P = (H + t + b - K) // stride + 1
     Q = (W + l + r - K) // stride + 1
     return _DwConv.apply(x, w, (N, C, H, W, K, P, Q, stride, t, l))
+
+
+def bn_act_depthwise_conv2d(x, bn, act, w, stride, pad):
+    """depthwise_conv2d(batch_norm_act(x, bn, act), w, stride, pad) as one fused op."""
+    _dev(x)
+    train = _bn_train_and_count(bn)
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    N, C, H, W = x.shape
+    K = w.shape[-1]
+    l, r, t, b = pad
+    P = (H + t + b - K) // stride + 1
+    Q = (W + l + r - K) // stride + 1
+    return _BnActDwConv.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, ACT[act], w,
+                              (N, C, H, W, K, P, Q, stride, t, l))
 
 
 # ------------------------------------------------------------------------------------------
@@ -357,7 +440,7 @@ class _SqueezeExcite(torch.autograd.Function):
         db1 = torch.empty(sq, dtype=torch.float32, device=dev) if (hb1 and nig[2]) else None
         dw2 = torch.empty(w2s, dtype=torch.float32, device=dev) if nig[3] else None
         db2 = torch.empty(C, dtype=torch.float32, device=dev) if (hb2 and nig[4]) else None
-        ws = torch.empty(2 * N * C + N * sq, dtype=torch.float32, device=dev)
+        ws = torch.empty(2 * N * C + 17 * N * sq, dtype=torch.float32, device=dev)
         with timing.region("se_bwd"):
             _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(dy.contiguous()), _lib.ptr(w1c),
                       _lib.ptr(w2c), _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), N, C, H * W,

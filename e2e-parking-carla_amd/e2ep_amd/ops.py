@@ -44,6 +44,15 @@ def bn_act(x, bn, act=None, res=None, dc_rand=None, dc_keep=1.0):
     return nn_ops.batch_norm_act(x, bn, act, res, dc_rand, dc_keep)
 
 
+def bn_act_depthwise(x, bn, act, conv):
+    """conv(bn_act(x, bn, act)) for a depthwise SameConv `conv`, fused: the BN + activation
+    are applied while the depthwise kernel loads its input (MBConv _bn0 -> swish ->
+    _depthwise_conv); the normalised activation tensor is never written."""
+    s = _pair(conv.stride)
+    assert s[0] == s[1] and conv.groups == x.shape[1] and conv.bias is None
+    return nn_ops.bn_act_depthwise_conv2d(x, bn, act, conv.weight, s[0], _pad4(conv.same))
+
+
 def activation(x, act):
     return nn_ops.activation(x, act)
 

@@ -63,10 +63,12 @@ class MBConv(nn.Module):
     def forward(self, x, drop_connect_rate=None, dc_rand=None):
         """dc_rand: this block's per-sample uniform draws for drop-connect (training); drawn
         here when not given (efficientnet-pytorch draws torch.rand([N,1,1,1]) per block)."""
-        y = x
-        if self.expand != 1:
-            y = ops.bn_act(self._expand_conv(y), self._bn0, "swish")
-        y = ops.bn_act(self._depthwise_conv(y), self._bn1, "swish")
+        if self.expand != 1:  # _bn0 + swish applied inside the depthwise conv's input load
+            y = ops.bn_act_depthwise(self._expand_conv(x), self._bn0, "swish",
+                                     self._depthwise_conv)
+        else:
+            y = self._depthwise_conv(x)
+        y = ops.bn_act(y, self._bn1, "swish")
         y = ops.squeeze_excite(y, self._se_reduce, self._se_expand)
         if not self.skip:
             return ops.bn_act(self._project_conv(y), self._bn2, None)

@@ -183,6 +183,14 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
                 const float *dc_rand, float dc_keep, float *running_mean, float *running_var,
                 int N, int C, int H, int W, int train, float momentum, float eps, int act,
                 float *mean, float *invstd, float *y, void *workspace, void *stream);
+/* Statistics half of e2ep_bn_fwd (same fp64 reduction, same running-stat update) for a
+ * consumer that applies the normalisation on load (e2ep_dwconv_fwd / _wgrad in_scale,
+ * in_shift): writes mean / invstd [C] and the folded affine scale = gamma * invstd,
+ * shift = beta - mean * scale [C].  The backward is e2ep_bn_bwd on the same x. */
+int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *running_mean,
+                  float *running_var, int N, int C, int H, int W, int train, float momentum,
+                  float eps, float *mean, float *invstd, float *scale, float *shift,
+                  void *workspace, void *stream);
 /* dx, dgamma, dbeta, dres (each nullable) from x, dy and the forward's mean/invstd; res and
  * dc_rand / dc_keep as in the forward (dres = gradient at the activation input). */
 int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
@@ -202,7 +210,7 @@ int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *d
  * pooled [N,C], hpre [N,sq], a [N,C] are forward outputs the backward reads.
  * Backward: dx = dy*sigmoid(a) + (w1^T (swish'(hpre) * (w2^T da))) / HW with
  * da = sigmoid'(a) * sum_hw dy*x, and the four parameter gradients (each nullable), batch sums
- * in sample order.  workspace: (2*N*C + N*sq) floats.  Limits: C <= 4096, sq <= 256.
+ * in sample order.  workspace: (2*N*C + 17*N*sq) floats.  Limits: C <= 4096, sq <= 256.
  * ------------------------------------------------------------------------------------- */
 int e2ep_se_fwd(const float *x, const float *w1, const float *b1, const float *w2,
                 const float *b2, int N, int C, int HW, int sq, float *pooled, float *hpre,
@@ -251,11 +259,16 @@ int e2ep_resize_bwd(const float *g, long long g_pstride, int planes, int Hi, int
  * Depthwise conv (EfficientNet MBConv _depthwise_conv; k 3 or 5, stride 1 or 2, static
  * SAME padding).  dims[10] = {N, C, H, W, K, P, Q, stride, pad_top, pad_left}.
  * ------------------------------------------------------------------------------------- */
-int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, float *y, void *stream);
+/* in_scale / in_shift [C] (both or neither) and in_act (0 none, 1 relu, 2 swish): the conv
+ * input is act(x * in_scale + in_shift), i.e. the preceding BatchNorm + activation applied on
+ * load (e2ep_bn_stats); the zero padding is in the transformed space.  dgrad returns the
+ * gradient w.r.t. the transformed input (feed it to e2ep_bn_bwd with the same act). */
+int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float *in_scale,
+                    const float *in_shift, int in_act, float *y, void *stream);
 int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream);
 size_t e2ep_dwconv_wgrad_workspace(const int *dims);
-int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, void *workspace, float *dw,
-                      void *stream);
+int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
+                      const float *in_shift, int in_act, void *workspace, float *dw, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Pooling and squeeze-excitation gating.

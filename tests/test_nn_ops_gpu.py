@@ -146,6 +146,51 @@ def test_depthwise(case):
     assert rel_l2(wd.grad, w64.grad) < 1e-5
 
 
+@pytest.mark.parametrize("case", [(4, 144, 64, 64, 3, 2, (0, 1, 0, 1), True),
+                                  (2, 192, 32, 32, 5, 1, (2, 2, 2, 2), True),
+                                  (2, 40, 32, 32, 5, 2, (1, 2, 1, 2), False),
+                                  (3, 8, 13, 11, 3, 2, (0, 1, 0, 1), True),
+                                  (2, 6, 64, 48, 5, 2, (2, 2, 2, 2), True)])
+def test_bn_swish_depthwise_fused(case):
+    """MBConv _bn0 -> swish -> _depthwise_conv with the BN + swish applied inside the
+    depthwise input load (e2ep_bn_stats + dwconv in_scale/in_shift), train and eval, vs fp64
+    torch: output, x / gamma / beta / weight gradients and running statistics."""
+    from e2ep_amd import nn_ops
+    N, C, H, W, K, s, pad, train = case
+    g = _g(C + H + K)
+    x = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    w = torch.randn(C, 1, K, K, generator=g) / K
+    bn = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3)
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.3 * torch.randn(C, generator=g))
+        bn.bias.copy_(0.2 * torch.randn(C, generator=g))
+        bn.running_mean.copy_(0.1 * torch.randn(C, generator=g))
+        bn.running_var.copy_(0.5 + torch.rand(C, generator=g))
+    bn64 = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3).double()
+    bn64.load_state_dict(bn.state_dict())
+    bn.train(train), bn64.train(train)
+    bnd = bn.to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    y = nn_ops.bn_act_depthwise_conv2d(xd, bnd, "swish", wd, s, pad)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(DEV))
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    z = bn64(x64)
+    y64 = F.conv2d(F.pad(z * torch.sigmoid(z), pad), w64, None, s, 0, 1, C)
+    y64.backward(dy.double())
+    assert y.shape == y64.shape
+    assert rel_l2(y, y64) < 1e-6
+    assert rel_l2(xd.grad, x64.grad) < 1e-5
+    assert rel_l2(wd.grad, w64.grad) < 1e-5
+    assert rel_l2(bnd.weight.grad, bn64.weight.grad) < 1e-5
+    assert rel_l2(bnd.bias.grad, bn64.bias.grad) < 1e-5
+    assert rel_l2(bnd.running_mean, bn64.running_mean) < 1e-6
+    assert rel_l2(bnd.running_var, bn64.running_var) < 1e-6
+    assert int(bnd.num_batches_tracked) == int(bn64.num_batches_tracked)
+
+
 def test_maxpool_avgpool_segate():
     from e2ep_amd import nn_ops
     g = _g(5)
@@ -195,7 +240,8 @@ def test_bev_stem_resize_conv_fused():
     assert rel_l2(wd.grad, w64.grad) < 2e-5
 
 
-@pytest.mark.parametrize("shape", [(8, 96, 16, 16, 6), (4, 40, 9, 7, 10), (32, 672, 16, 16, 28)])
+@pytest.mark.parametrize("shape", [(8, 96, 16, 16, 6), (4, 40, 9, 7, 10), (32, 672, 16, 16, 28),
+                                   (32, 1632, 8, 8, 68), (5, 300, 3, 3, 75), (2, 4096, 2, 2, 256)])
 def test_squeeze_excite_fused(shape):
     """Fused SE (pool -> 1x1 -> swish -> 1x1 -> sigmoid gate) vs fp64 torch, all gradients."""
     from e2ep_amd import nn_ops
