@@ -181,14 +181,14 @@ __global__ void __launch_bounds__(256) k_bn_apply(
 }
 
 // statistics only (for a consumer that applies the normalisation on load, e.g. the depthwise
-// conv): grid (C); mean / invstd, the folded scale / shift (sc = gamma * invstd,
-// sh = beta - mean * sc, the same arithmetic as k_bn_apply) and the running-stat update
-__global__ void __launch_bounds__(256) k_bn_finalize(
-    const double *__restrict__ part, int splits, long long cnt, float eps, float momentum,
+// conv): mean / invstd, the folded scale / shift (sc = gamma * invstd, sh = beta - mean * sc,
+// the same arithmetic as k_bn_apply) and the running-stat update of channel c; every thread
+// of the block calls it (block-wide partial sum), thread 0 writes
+__device__ __forceinline__ void bn_finalize_channel(
+    int c, const double *__restrict__ part, int splits, long long cnt, float eps, float momentum,
     float *__restrict__ running_mean, float *__restrict__ running_var, float *__restrict__ mean_out,
     float *__restrict__ invstd_out, const float *__restrict__ gamma, const float *__restrict__ beta,
     float *__restrict__ scale, float *__restrict__ shift) {
-  const int c = blockIdx.x;
   float mu, is;
   if (part) {
     double s, q;
@@ -216,6 +216,41 @@ __global__ void __launch_bounds__(256) k_bn_finalize(
   shift[c] = (beta ? beta[c] : 0.f) - mu * sc;
 }
 
+// grid (C): eval (part == null) or a separate finalize after k_bn_stats
+__global__ void __launch_bounds__(256) k_bn_finalize(
+    const double *__restrict__ part, int splits, long long cnt, float eps, float momentum,
+    float *__restrict__ running_mean, float *__restrict__ running_var, float *__restrict__ mean_out,
+    float *__restrict__ invstd_out, const float *__restrict__ gamma, const float *__restrict__ beta,
+    float *__restrict__ scale, float *__restrict__ shift) {
+  bn_finalize_channel(blockIdx.x, part, splits, cnt, eps, momentum, running_mean, running_var,
+                      mean_out, invstd_out, gamma, beta, scale, shift);
+}
+
+// squeeze-excitation gate downstream of the activation (e2ep_bn_bwd gate_logit /
+// gate_dpooled): the gradient at the activation output is dy * sigmoid(logit[n,c]) +
+// dpooled[n,c] / HW (the SE op's dx, se.hip k_se_dx, formed here instead of stored)
+struct BnGate {
+  const float *logit, *dpooled;
+  float inv_hw;
+  __device__ __forceinline__ bool on() const { return logit != nullptr; }
+  __device__ __forceinline__ void coef(int n, int C, int c, float &s, float &d) const {
+    const int i = n * C + c;
+    s = 1.f / (1.f + expf(-logit[i]));
+    d = dpooled[i] * inv_hw;
+  }
+};
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T gate_dy(typename Vec<VEC>::T dv, const BnGate &gt,
+                                                        int n, int C, int c) {
+  if (gt.on()) {
+    float s, d;
+    gt.coef(n, C, c, s, d);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) Vec<VEC>::set(dv, i, Vec<VEC>::get(dv, i) * s + d);
+  }
+  return dv;
+}
+
 // backward pieces shared by reduce and apply: from x, dy (and res / drop-connect), returns
 // xhat, dz (gradient at the activation input = dres) and dzb (gradient at the BN output)
 template <int VEC>
@@ -239,8 +274,8 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
     const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
-    const float *__restrict__ dc_rand, float dc_keep, int N, int C, int HWv, int splits, int per,
-    int act, double *__restrict__ part) {
+    const float *__restrict__ dc_rand, float dc_keep, BnGate gt, int N, int C, int HWv,
+    int splits, int per, int act, double *__restrict__ part) {
   const int c = blockIdx.x, sp = blockIdx.y;
   const int tot = N * HWv;
   const int beg = sp * per, end = min(tot, beg + per);
@@ -251,7 +286,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
     const int n = t / HWv, p = t - n * HWv;
     const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
     const auto xv = Vec<VEC>::ld(x + off);
-    const auto dv = Vec<VEC>::ld(dy + off);
+    const auto dv = gate_dy<VEC>(Vec<VEC>::ld(dy + off), gt, n, C, c);
     const auto rv = res ? Vec<VEC>::ld(res + off) : Vec<VEC>::zero();
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -289,7 +324,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(
     const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
-    const float *__restrict__ dc_rand, float dc_keep, const double *__restrict__ part,
+    const float *__restrict__ dc_rand, float dc_keep, BnGate gt, const double *__restrict__ part,
     int splits, long long cnt, int N, int C, int HWv, int per, int act, int train,
     float *__restrict__ dx, float *__restrict__ dres, float *__restrict__ dgamma,
     float *__restrict__ dbeta) {
@@ -310,7 +345,7 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(
     const int n = t / HWv, p = t - n * HWv;
     const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
     const auto xv = Vec<VEC>::ld(x + off);
-    const auto dv = Vec<VEC>::ld(dy + off);
+    const auto dv = gate_dy<VEC>(Vec<VEC>::ld(dy + off), gt, n, C, c);
     const auto rv = res ? Vec<VEC>::ld(res + off) : Vec<VEC>::zero();
     auto ox = Vec<VEC>::zero(), orr = Vec<VEC>::zero();
 #pragma unroll
@@ -434,10 +469,14 @@ int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *
 
 int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
                 const float *gamma, const float *beta, const float *res, const float *dc_rand,
-                float dc_keep, int N, int C, int H, int W, int train, int act, float *dx,
-                float *dgamma, float *dbeta, float *dres, void *workspace, void *stream) {
+                float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
+                int H, int W, int train, int act, float *dx, float *dgamma, float *dbeta,
+                float *dres, void *workspace, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
                E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
+  E2EP_REQUIRE(!gate_logit == !gate_dpooled, E2EP_EINVAL,
+               "e2ep_bn_bwd: gate_logit / gate_dpooled both or neither");
+  const BnGate gt{gate_logit, gate_dpooled, 1.f / (float)(H * W)};
   E2EP_REQUIRE(!dc_rand || dc_keep > 0.f, E2EP_EINVAL, "e2ep_bn_bwd: drop-connect keep must be > 0");
   hipStream_t s = as_stream(stream);
   const int HW = H * W;
@@ -451,19 +490,19 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
   double *part = static_cast<double *>(workspace);
   if (v4)
     hipLaunchKernelGGL(k_bn_bwd_reduce<4>, dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd, gamma,
-                       beta, res, dc_rand, dc_keep, N, C, HWv, sp, per, act, part);
+                       beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
   else
     hipLaunchKernelGGL(k_bn_bwd_reduce<1>, dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd, gamma,
-                       beta, res, dc_rand, dc_keep, N, C, HWv, sp, per, act, part);
+                       beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
   if (dx || dres) {
     const dim3 grid(C, cdiv(totv, APPLY_PER));
     if (v4)
       hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                         res, dc_rand, dc_keep, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
+                         res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
                          dx, dres, dgamma, dbeta);
     else
       hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                         res, dc_rand, dc_keep, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
+                         res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
                          dx, dres, dgamma, dbeta);
   } else if (dgamma || dbeta) {
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(256), 0, s, part, sp, dgamma, dbeta);

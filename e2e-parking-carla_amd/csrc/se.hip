@@ -15,26 +15,48 @@ constexpr int SE_MAXC = 4096, SE_MAXSQ = 256;
 
 __device__ __forceinline__ float sigm(float v) { return 1.f / (1.f + expf(-v)); }
 
+// Optional input transform: when the SE input is the raw output of the depthwise conv, the
+// block's _bn1 + swish is applied on load, x -> swish(x * sc[c] + sh[c]) (sc / sh from
+// e2ep_bn_stats), so the activation tensor is never written.
+struct SeIn {
+  const float *sc, *sh;
+  int C;
+};
+__device__ __forceinline__ float se_in(float v, float sc, float sh, bool t) {
+  if (!t) return v;
+  const float z = v * sc + sh;
+  return z / (1.f + expf(-z));
+}
+__device__ __forceinline__ float4 se_in4(float4 v, float sc, float sh, bool t) {
+  return make_float4(se_in(v.x, sc, sh, t), se_in(v.y, sc, sh, t), se_in(v.z, sc, sh, t),
+                     se_in(v.w, sc, sh, t));
+}
+
 // sum over one plane (HW floats, float4 when HW % 4 == 0) by one wave
-__device__ __forceinline__ float plane_sum(const float *__restrict__ p, int HW, int lane) {
+__device__ __forceinline__ float plane_sum(const float *__restrict__ p, int HW, int lane,
+                                           float sc, float sh, bool t) {
   float s = 0.f;
   if ((HW & 3) == 0) {
     const int HW4 = HW >> 2;
     for (int i = lane; i < HW4; i += 64) {
-      const float4 v = reinterpret_cast<const float4 *>(p)[i];
+      const float4 v = se_in4(reinterpret_cast<const float4 *>(p)[i], sc, sh, t);
       s += (v.x + v.y) + (v.z + v.w);
     }
   } else {
-    for (int i = lane; i < HW; i += 64) s += p[i];
+    for (int i = lane; i < HW; i += 64) s += se_in(p[i], sc, sh, t);
   }
   return wave_sum(s);
 }
 
-__global__ void __launch_bounds__(256) k_se_squeeze(const float *__restrict__ x, int planes,
-                                                    int HW, float *__restrict__ pooled) {
+__global__ void __launch_bounds__(256) k_se_squeeze(const float *__restrict__ x, SeIn tf,
+                                                    int planes, int HW,
+                                                    float *__restrict__ pooled) {
   const int pl = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pl >= planes) return;
-  const float s = plane_sum(x + (size_t)pl * HW, HW, threadIdx.x & 63);
+  const bool t = tf.sc != nullptr;
+  const int c = pl % tf.C;
+  const float s = plane_sum(x + (size_t)pl * HW, HW, threadIdx.x & 63, t ? tf.sc[c] : 1.f,
+                            t ? tf.sh[c] : 0.f, t);
   if ((threadIdx.x & 63) == 0) pooled[pl] = s / (float)HW;
 }
 
@@ -92,40 +114,46 @@ __global__ void __launch_bounds__(256) k_se_logits(const float *__restrict__ hpr
 }
 
 // y = x * sigmoid(a[plane]); float4 stream (HW % 4 == 0) or scalar
-__global__ void __launch_bounds__(256) k_se_excite(const float *__restrict__ x,
+__global__ void __launch_bounds__(256) k_se_excite(const float *__restrict__ x, SeIn tf,
                                                    const float *__restrict__ a, int HW,
                                                    long long nvec, int vec,
                                                    float *__restrict__ y) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nvec) return;
+  const bool t = tf.sc != nullptr;
+  const long long pl = vec ? i / (HW >> 2) : i / HW;
+  const int c = (int)(pl % tf.C);
+  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
+  const float s = sigm(a[pl]);
   if (vec) {
-    const int HW4 = HW >> 2;
-    const float s = sigm(a[i / HW4]);
-    float4 v = reinterpret_cast<const float4 *>(x)[i];
+    float4 v = se_in4(reinterpret_cast<const float4 *>(x)[i], sc, sh, t);
     v.x *= s; v.y *= s; v.z *= s; v.w *= s;
     reinterpret_cast<float4 *>(y)[i] = v;
   } else {
-    y[i] = x[i] * sigm(a[i / HW]);
+    y[i] = se_in(x[i], sc, sh, t) * s;
   }
 }
 
 // da[plane] = s (1 - s) sum_hw dy * x      (wave per plane)
-__global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x,
+__global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn tf,
                                                const float *__restrict__ dy,
                                                const float *__restrict__ a, int planes, int HW,
                                                float *__restrict__ da) {
   const int pl = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (pl >= planes) return;
+  const bool t = tf.sc != nullptr;
+  const int c = pl % tf.C;
+  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
   const float *xp = x + (size_t)pl * HW, *gp = dy + (size_t)pl * HW;
   float acc = 0.f;
   if ((HW & 3) == 0) {
     for (int i = lane; i < (HW >> 2); i += 64) {
-      const float4 u = reinterpret_cast<const float4 *>(xp)[i];
+      const float4 u = se_in4(reinterpret_cast<const float4 *>(xp)[i], sc, sh, t);
       const float4 g = reinterpret_cast<const float4 *>(gp)[i];
       acc += (u.x * g.x + u.y * g.y) + (u.z * g.z + u.w * g.w);
     }
   } else {
-    for (int i = lane; i < HW; i += 64) acc += xp[i] * gp[i];
+    for (int i = lane; i < HW; i += 64) acc += se_in(xp[i], sc, sh, t) * gp[i];
   }
   acc = wave_sum(acc);
   if (lane == 0) {
@@ -253,36 +281,46 @@ using namespace e2ep;
 
 extern "C" {
 
-int e2ep_se_fwd(const float *x, const float *w1, const float *b1, const float *w2,
-                const float *b2, int N, int C, int HW, int sq, float *pooled, float *hpre,
-                float *a, float *y, void *stream) {
+int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, const float *w1,
+                const float *b1, const float *w2, const float *b2, int N, int C, int HW, int sq,
+                float *pooled, float *hpre, float *a, float *y, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && HW > 0 && sq > 0, E2EP_EINVAL, "e2ep_se_fwd: bad shape");
+  E2EP_REQUIRE(!x_scale == !x_shift, E2EP_EINVAL, "e2ep_se_fwd: x_scale / x_shift both or neither");
+  const SeIn tf{x_scale, x_shift, C};
   E2EP_REQUIRE(C <= SE_MAXC && sq <= SE_MAXSQ, E2EP_ERANGE, "e2ep_se_fwd: C %d > %d or sq %d > %d",
                C, SE_MAXC, sq, SE_MAXSQ);
   hipStream_t s = as_stream(stream);
   const int planes = N * C;
-  hipLaunchKernelGGL(k_se_squeeze, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, planes, HW, pooled);
+  hipLaunchKernelGGL(k_se_squeeze, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, planes, HW,
+                     pooled);
   hipLaunchKernelGGL(k_se_hidden, dim3(N, cdiv(sq, 4)), dim3(256), 0, s, pooled, w1, b1, C, sq,
                      hpre);
   hipLaunchKernelGGL(k_se_logits, dim3(cdiv(C, SE_CT), cdiv(N, SE_NT)), dim3(256),
                      (SE_CT * (sq + 1) + SE_NT * sq) * sizeof(float), s, hpre, w2, b2, N, C, sq, a);
   const int vec = (HW & 3) == 0;
   const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
-  hipLaunchKernelGGL(k_se_excite, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, a, HW, nvec, vec, y);
+  hipLaunchKernelGGL(k_se_excite, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, tf, a, HW, nvec, vec,
+                     y);
   return launch_status("e2ep_se_fwd");
 }
 
-int e2ep_se_bwd(const float *x, const float *dy, const float *w1, const float *w2,
-                const float *pooled, const float *hpre, const float *a, int N, int C, int HW,
-                int sq, float *dx, float *dw1, float *db1, float *dw2, float *db2,
-                float *workspace, void *stream) {
+int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, const float *dy,
+                const float *w1, const float *w2, const float *pooled, const float *hpre,
+                const float *a, int N, int C, int HW, int sq, float *dx, float *dpooled_out,
+                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && HW > 0 && sq > 0, E2EP_EINVAL, "e2ep_se_bwd: bad shape");
+  E2EP_REQUIRE(!x_scale == !x_shift, E2EP_EINVAL, "e2ep_se_bwd: x_scale / x_shift both or neither");
+  E2EP_REQUIRE(!(x_scale && dx), E2EP_EINVAL,
+               "e2ep_se_bwd: with an input transform dx is formed by e2ep_bn_bwd (gate_logit / "
+               "gate_dpooled); pass dx = NULL");
+  const SeIn tf{x_scale, x_shift, C};
   E2EP_REQUIRE(C <= SE_MAXC && sq <= SE_MAXSQ, E2EP_ERANGE, "e2ep_se_bwd: C %d > %d or sq %d > %d",
                C, SE_MAXC, sq, SE_MAXSQ);
   hipStream_t s = as_stream(stream);
   const int planes = N * C;
-  float *da = workspace, *dpooled = workspace + planes, *dhpre = workspace + 2 * planes;
-  hipLaunchKernelGGL(k_se_da, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, dy, a, planes, HW, da);
+  float *da = workspace, *dhpre = workspace + 2 * planes;
+  float *dpooled = dpooled_out ? dpooled_out : workspace + planes;
+  hipLaunchKernelGGL(k_se_da, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes, HW, da);
   float *dhp = workspace + 2 * planes + N * sq;
   const int spans = cdiv(C, SE_DH_SPAN);
   int KT = 1;

@@ -42,7 +42,7 @@ SIGNATURES = {
     "e2ep_bn_workspace": (_sz, [_i, _i, _i, _i]),
     "e2ep_bn_fwd": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i, _p, _p, _p, _p, _p]),
     "e2ep_bn_stats": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _p]),
-    "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
+    "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
     "e2ep_act_fwd": (_i, [_p, _i64, _i, _p, _p]),
     "e2ep_act_bwd": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_resize_fwd": (_i, [_p, _i, _i, _i64, _i, _i, _i, _i, _f, _f, _p, _i64, _p]),
@@ -59,8 +59,8 @@ SIGNATURES = {
     "e2ep_add_drop_ln_fwd": (_i, [_p, _p, _p, _f, _p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
     "e2ep_add_drop_ln_bwd_workspace": (_sz, [_i, _i]),
     "e2ep_add_drop_ln_bwd": (_i, [_p, _p, _p, _p, _p, _p, _f, _i, _i, _p, _p, _p, _p, _p, _p]),
-    "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
-    "e2ep_se_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p]),
+    "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "e2ep_se_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
     "e2ep_se_gate_fwd": (_i, [_p, _p, _i, _i, _p, _p]),
     "e2ep_se_gate_bwd": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),
     "e2ep_adam_chunk_elems": (_i, []),

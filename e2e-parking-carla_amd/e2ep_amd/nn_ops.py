@@ -18,6 +18,7 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+
 # ------------------------------------------------------------------------------------------
 # BatchNorm2d + activation (+ residual)
 # ------------------------------------------------------------------------------------------
@@ -54,7 +55,7 @@ class _BnAct(torch.autograd.Function):
         with timing.region("bn_bwd"):
             _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(mean), _lib.ptr(invstd),
                       _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), _lib.ptr(dc_rand),
-                      float(ctx.dc_keep), N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx),
+                      float(ctx.dc_keep), None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx),
                       _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.stream())
         return dx, dg, db, dres, None, None, None, None, None, None, None, None
 
@@ -285,7 +286,7 @@ class _BnActDwConv(torch.autograd.Function):
             with timing.region("bn_bwd"):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dt), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
-                          N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx), _lib.ptr(dg),
+                          None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx), _lib.ptr(dg),
                           _lib.ptr(db), None, _lib.ptr(ws), s)
         return dx, dg, db, None, None, None, None, None, None, dw, None
 
@@ -420,7 +421,7 @@ class _SqueezeExcite(torch.autograd.Function):
         y = torch.empty_like(x)
         w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
         with timing.region("se_fwd"):
-            _lib.call("e2ep_se_fwd", _lib.ptr(x), _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c),
+            _lib.call("e2ep_se_fwd", _lib.ptr(x), None, None, _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c),
                       _lib.ptr(b2), N, C, H * W, sq, _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a),
                       _lib.ptr(y), _lib.stream())
         ctx.save_for_backward(x, w1c, w2c, pooled, hpre, a)
@@ -442,11 +443,89 @@ class _SqueezeExcite(torch.autograd.Function):
         db2 = torch.empty(C, dtype=torch.float32, device=dev) if (hb2 and nig[4]) else None
         ws = torch.empty(2 * N * C + 17 * N * sq, dtype=torch.float32, device=dev)
         with timing.region("se_bwd"):
-            _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(dy.contiguous()), _lib.ptr(w1c),
-                      _lib.ptr(w2c), _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), N, C, H * W,
-                      sq, _lib.ptr(dx), _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2),
+            _lib.call("e2ep_se_bwd", _lib.ptr(x), None, None, _lib.ptr(dy.contiguous()),
+                      _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a),
+                      N, C, H * W, sq, _lib.ptr(dx), None, _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2),
                       _lib.ptr(ws), _lib.stream())
         return dx, dw1, db1, dw2, db2
+
+
+class _BnSwishSE(torch.autograd.Function):
+    """squeeze_excite(batch_norm_act(x, bn, 'swish'), ...) with the BN + swish applied on load
+    by the SE kernels (MBConv _bn1 -> swish -> SE, reference model/cam_encoder.py:69-73 via
+    efficientnet-pytorch MBConvBlock.forward): the activation tensor is never written, and
+    the backward forms its gradient inside the BN backward (gate_logit / gate_dpooled)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, w1, b1, w2, b2):
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        sq = w1.shape[0]
+        dev = x.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
+        ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
+        s = _lib.stream()
+        with timing.region("bn_fwd"):
+            _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
+                      _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
+                      _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
+                      _lib.ptr(stats[3]), _lib.ptr(ws), s)
+        pooled, hpre, a = torch.empty(N, C, **f32), torch.empty(N, sq, **f32), torch.empty(N, C, **f32)
+        y = torch.empty_like(x)
+        w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
+        with timing.region("se_fwd"):
+            _lib.call("e2ep_se_fwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
+                      _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c), _lib.ptr(b2), N, C, H * W, sq,
+                      _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), _lib.ptr(y), s)
+        ctx.save_for_backward(x, gamma, beta, stats, w1c, w2c, pooled, hpre, a)
+        ctx.shapes = (w1.shape, w2.shape, b1 is not None, b2 is not None)
+        ctx.train = train
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, stats, w1c, w2c, pooled, hpre, a = ctx.saved_tensors
+        w1s, w2s, hb1, hb2 = ctx.shapes
+        N, C, H, W = x.shape
+        sq = w1c.shape[0]
+        nig = ctx.needs_input_grad
+        dev = x.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        dy = dy.contiguous()
+        s = _lib.stream()
+        dw1 = torch.empty(w1s, **f32) if nig[8] else None
+        db1 = torch.empty(sq, **f32) if (hb1 and nig[9]) else None
+        dw2 = torch.empty(w2s, **f32) if nig[10] else None
+        db2 = torch.empty(C, **f32) if (hb2 and nig[11]) else None
+        dpooled = torch.empty(N, C, **f32)
+        ws = torch.empty(2 * N * C + 17 * N * sq, **f32)
+        with timing.region("se_bwd"):
+            _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
+                      _lib.ptr(dy), _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled),
+                      _lib.ptr(hpre), _lib.ptr(a), N, C, H * W, sq, None, _lib.ptr(dpooled),
+                      _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2), _lib.ptr(ws), s)
+        dx = torch.empty_like(x) if nig[0] else None
+        dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
+        db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
+        if dx is not None or dg is not None or db is not None:
+            bws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
+            with timing.region("bn_bwd"):
+                _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(stats[0]),
+                          _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
+                          _lib.ptr(a), _lib.ptr(dpooled), N, C, H, W, int(ctx.train), ACT["swish"],
+                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), None, _lib.ptr(bws), s)
+        return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2
+
+
+def bn_swish_squeeze_excite(x, bn, w1, b1, w2, b2):
+    """squeeze_excite(batch_norm_act(x, bn, 'swish'), w1, b1, w2, b2) as one fused op."""
+    _dev(x)
+    train = _bn_train_and_count(bn)
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    return _BnSwishSE.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, w1, b1, w2, b2)
 
 
 def squeeze_excite(x, w1, b1, w2, b2):

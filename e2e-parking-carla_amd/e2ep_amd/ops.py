@@ -63,6 +63,13 @@ def squeeze_excite(x, reduce, expand):
     return nn_ops.squeeze_excite(x, reduce.weight, reduce.bias, expand.weight, expand.bias)
 
 
+def bn_swish_squeeze_excite(x, bn, reduce, expand):
+    """squeeze_excite(bn_act(x, bn, 'swish'), reduce, expand) fused: BN + swish applied on
+    load by the SE kernels; the activation tensor is never stored."""
+    return nn_ops.bn_swish_squeeze_excite(x, bn, reduce.weight, reduce.bias, expand.weight,
+                                          expand.bias)
+
+
 def upsample2x(x):
     return nn_ops.resize(x, scale_factor=2)
 

@@ -68,8 +68,7 @@ class MBConv(nn.Module):
                                      self._depthwise_conv)
         else:
             y = self._depthwise_conv(x)
-        y = ops.bn_act(y, self._bn1, "swish")
-        y = ops.squeeze_excite(y, self._se_reduce, self._se_expand)
+        y = ops.bn_swish_squeeze_excite(y, self._bn1, self._se_reduce, self._se_expand)
         if not self.skip:
             return ops.bn_act(self._project_conv(y), self._bn2, None)
         if drop_connect_rate and self.training:

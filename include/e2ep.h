@@ -192,11 +192,15 @@ int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *
                   float eps, float *mean, float *invstd, float *scale, float *shift,
                   void *workspace, void *stream);
 /* dx, dgamma, dbeta, dres (each nullable) from x, dy and the forward's mean/invstd; res and
- * dc_rand / dc_keep as in the forward (dres = gradient at the activation input). */
+ * dc_rand / dc_keep as in the forward (dres = gradient at the activation input).
+ * gate_logit / gate_dpooled [N,C] (both or neither): the activation output fed a
+ * squeeze-excitation gate (e2ep_se_fwd with x_scale / x_shift), so the gradient at it is
+ * dy * sigmoid(gate_logit) + gate_dpooled / (H*W), formed on the fly from the gate's dy. */
 int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
                 const float *gamma, const float *beta, const float *res, const float *dc_rand,
-                float dc_keep, int N, int C, int H, int W, int train, int act, float *dx,
-                float *dgamma, float *dbeta, float *dres, void *workspace, void *stream);
+                float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
+                int H, int W, int train, int act, float *dx, float *dgamma, float *dbeta,
+                float *dres, void *workspace, void *stream);
 /* Stand-alone activation (act as above) and its gradient w.r.t. the pre-activation x. */
 int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);
@@ -211,14 +215,18 @@ int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *d
  * Backward: dx = dy*sigmoid(a) + (w1^T (swish'(hpre) * (w2^T da))) / HW with
  * da = sigmoid'(a) * sum_hw dy*x, and the four parameter gradients (each nullable), batch sums
  * in sample order.  workspace: (2*N*C + 17*N*sq) floats.  Limits: C <= 4096, sq <= 256.
+ * x_scale / x_shift [C] (both or neither): the SE input is swish(x * x_scale + x_shift),
+ * i.e. the block's _bn1 + swish applied on load to the raw depthwise output x (e2ep_bn_stats);
+ * then the backward leaves dx to e2ep_bn_bwd (pass dx = NULL, dpooled_out [N,C], and hand a
+ * and dpooled_out to e2ep_bn_bwd as gate_logit / gate_dpooled).
  * ------------------------------------------------------------------------------------- */
-int e2ep_se_fwd(const float *x, const float *w1, const float *b1, const float *w2,
-                const float *b2, int N, int C, int HW, int sq, float *pooled, float *hpre,
-                float *a, float *y, void *stream);
-int e2ep_se_bwd(const float *x, const float *dy, const float *w1, const float *w2,
-                const float *pooled, const float *hpre, const float *a, int N, int C, int HW,
-                int sq, float *dx, float *dw1, float *db1, float *dw2, float *db2,
-                float *workspace, void *stream);
+int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, const float *w1,
+                const float *b1, const float *w2, const float *b2, int N, int C, int HW, int sq,
+                float *pooled, float *hpre, float *a, float *y, void *stream);
+int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, const float *dy,
+                const float *w1, const float *w2, const float *pooled, const float *hpre,
+                const float *a, int N, int C, int HW, int sq, float *dx, float *dpooled_out,
+                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Residual add + dropout + LayerNorm of the post-norm transformer layers (torch

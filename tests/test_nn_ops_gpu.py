@@ -268,6 +268,51 @@ def test_squeeze_excite_fused(shape):
         assert rel_l2(got.grad, ref.grad) < 1e-5
 
 
+@pytest.mark.parametrize("case", [(8, 96, 16, 16, 6, True), (4, 40, 9, 7, 10, True),
+                                  (32, 672, 16, 16, 28, True), (5, 300, 3, 3, 75, False),
+                                  (2, 144, 64, 64, 6, True)])
+def test_bn_swish_se_fused(case):
+    """MBConv _bn1 -> swish -> SE with the BN + swish applied on load by the SE kernels
+    (e2ep_bn_stats + se x_scale/x_shift; backward through e2ep_bn_bwd gate_logit /
+    gate_dpooled), train and eval, vs fp64 torch: output, every gradient, running stats."""
+    from e2ep_amd import nn_ops
+    N, C, H, W, sq, train = case
+    g = _g(C + sq + H)
+    x = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    w1 = torch.randn(sq, C, 1, 1, generator=g) / C ** 0.5
+    b1 = torch.randn(sq, generator=g) * 0.1
+    w2 = torch.randn(C, sq, 1, 1, generator=g) / sq ** 0.5
+    b2 = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(N, C, H, W, generator=g)
+    bn = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3)
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.3 * torch.randn(C, generator=g))
+        bn.bias.copy_(0.2 * torch.randn(C, generator=g))
+        bn.running_mean.copy_(0.1 * torch.randn(C, generator=g))
+        bn.running_var.copy_(0.5 + torch.rand(C, generator=g))
+    bn64 = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3).double()
+    bn64.load_state_dict(bn.state_dict())
+    bn.train(train), bn64.train(train)
+    bnd = bn.to(DEV)
+    ts = [t.to(DEV).requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    y = nn_ops.bn_swish_squeeze_excite(ts[0], bnd, *ts[1:])
+    y.backward(dy.to(DEV))
+    rs = [t.double().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    z = bn64(rs[0])
+    u = z * torch.sigmoid(z)
+    h = F.conv2d(F.adaptive_avg_pool2d(u, 1), rs[1], rs[2])
+    a = F.conv2d(h * torch.sigmoid(h), rs[3], rs[4])
+    y64 = u * torch.sigmoid(a)
+    y64.backward(dy.double())
+    assert rel_l2(y, y64) < 1e-6
+    for got, ref in zip(ts, rs):
+        assert rel_l2(got.grad, ref.grad) < 1e-5
+    assert rel_l2(bnd.weight.grad, bn64.weight.grad) < 1e-5
+    assert rel_l2(bnd.bias.grad, bn64.bias.grad) < 1e-5
+    assert rel_l2(bnd.running_mean, bn64.running_mean) < 1e-6
+    assert rel_l2(bnd.running_var, bn64.running_var) < 1e-6
+
+
 @pytest.mark.parametrize("rows,E,p", [(2048, 258, 0.1), (112, 258, 0.0), (37, 100, 0.5)])
 def test_add_dropout_layernorm_fused(rows, E, p):
     """y = LayerNorm(a + dropout(b)) (transformer post-norm residual) vs fp64 torch, with the
