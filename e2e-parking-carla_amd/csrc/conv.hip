@@ -421,7 +421,9 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 // reads 4 consecutive pixels of row l%32 (g for A, x for B), and MFMA t of a group takes
 // element t of every lane (the K axis is reordered within each 8-pixel group; the sum is the
 // same and its order fixed).  The four waves of a block split the block's pixel range and
-// are summed in LDS in wave order; slabs per split are reduced by k_reduce_splits.
+// are summed in LDS in wave order; slabs per split are reduced by k_reduce_splits.  Wave
+// tiles are 32x32 or, when both channel counts fill them, 64x64 (four accumulators sharing
+// each loaded operand: half the L1/L2 operand traffic per MFMA).
 // ------------------------------------------------------------------------------------------
 constexpr int W1_GROUPS = 4;  // 8-pixel groups per wave iteration (8 float4 loads in flight)
 
@@ -430,8 +432,8 @@ static bool wgrad1x1_ok(const ConvGeom &g) {
          g.P == g.H && g.Q == g.W && (g.P * g.Q) % 8 == 0;
 }
 
-static int wgrad1x1_splits(const ConvGeom &g) {
-  const long long tiles = (long long)cdiv(g.Cout, 32) * cdiv(g.Cin, 32);
+static int wgrad1x1_splits_for(const ConvGeom &g, int to, int tc) {
+  const long long tiles = (long long)cdiv(g.Cout, to) * cdiv(g.Cin, tc);
   const long long pix = (long long)g.N * g.P * g.Q;
   long long want = (2048 + tiles - 1) / tiles;   // ~2048 workgroups
   long long cap = pix / 2048;                    // >= 16 loop iterations per wave
@@ -441,13 +443,35 @@ static int wgrad1x1_splits(const ConvGeom &g) {
   return (int)s;
 }
 
+// Wave tile rows per channel axis (Cout, Cin): 64 where that pads the axis at most 1/8 beyond
+// 32-row tiles, but only for large pixel counts whose 64-row grid still has >= 128 workgroups
+// (smaller problems are latency-bound and want the wider grid; scripts/bench_conv.py).
+static void wgrad1x1_tiles(const ConvGeom &g, int &to, int &tc) {
+  auto wide = [](int c) { return 8LL * cdiv(c, 64) * 64 <= 9LL * cdiv(c, 32) * 32; };
+  to = tc = 32;
+  if ((long long)g.N * g.P * g.Q < 65536) return;
+  const int wo = wide(g.Cout) ? 64 : 32, wc = wide(g.Cin) ? 64 : 32;
+  if ((long long)cdiv(g.Cout, wo) * cdiv(g.Cin, wc) * wgrad1x1_splits_for(g, wo, wc) < 128) return;
+  to = wo;
+  tc = wc;
+}
+
+static int wgrad1x1_splits(const ConvGeom &g) {
+  int to, tc;
+  wgrad1x1_tiles(g, to, tc);
+  return wgrad1x1_splits_for(g, to, tc);
+}
+
+template <int TI, int TJ>
 __global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gout,
                                                    const float *__restrict__ x,
                                                    float *__restrict__ part, ConvGeom g,
                                                    int splits, int groups_per_split) {
-  __shared__ float red[4][16][64];
+  // wave tile (32*TI co) x (32*TJ ci): TI*TJ accumulators share each loaded operand
+  constexpr int NT = TI * TJ;
+  __shared__ float red[NT * 16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ntj = (g.Cin + 31) / 32;
+  const int ntj = (g.Cin + 32 * TJ - 1) / (32 * TJ);
   const int ti = blockIdx.x / ntj, tj = blockIdx.x - ti * ntj;
   const int split = blockIdx.y;
   const int PQ = g.P * g.Q;
@@ -455,42 +479,64 @@ __global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gou
   const int gb = split * groups_per_split;
   const int ge = min(ngroups, gb + groups_per_split);
   const int row = lane & 31, h = lane >> 5;
-  const int co = ti * 32 + row, ci = tj * 32 + row;
+  const int co0 = ti * 32 * TI + row, ci0 = tj * 32 * TJ + row;
   const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
   const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * PQ);
   const int gpq = PQ / 8;
-  f32x16 acc = {0};
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{0};
   // wave w takes groups gb + w*W1_GROUPS + 4*W1_GROUPS*i ...
   for (int g0 = gb + wave * W1_GROUPS; g0 < ge; g0 += 4 * W1_GROUPS) {
-    float4 a[W1_GROUPS], b[W1_GROUPS];
+    float4 a[W1_GROUPS][TI], b[W1_GROUPS][TJ];
 #pragma unroll
     for (int u = 0; u < W1_GROUPS; ++u) {
       const int grp = g0 + u;
       const bool ok = grp < ge;
       const int n = grp / gpq, p = (grp - n * gpq) * 8 + 4 * h;
-      a[u] = bload4(rg, (ok && co < g.Cout) ? (((n * g.Cout + co) * PQ) + p) * 4 : OOR);
-      b[u] = bload4(rx, (ok && ci < g.Cin) ? (((n * g.Cin + ci) * PQ) + p) * 4 : OOR);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + 32 * i;
+        a[u][i] = bload4(rg, (ok && co < g.Cout) ? (((n * g.Cout + co) * PQ) + p) * 4 : OOR);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int ci = ci0 + 32 * j;
+        b[u][j] = bload4(rx, (ok && ci < g.Cin) ? (((n * g.Cin + ci) * PQ) + p) * 4 : OOR);
+      }
     }
 #pragma unroll
-    for (int u = 0; u < W1_GROUPS; ++u) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, b[u].x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, b[u].y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, b[u].z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, b[u].w, acc, 0, 0, 0);
-    }
+    for (int u = 0; u < W1_GROUPS; ++u)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          f32x16 &c = acc[i * TJ + j];
+          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].x, b[u][j].x, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].y, b[u][j].y, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].z, b[u][j].z, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].w, b[u][j].w, c, 0, 0, 0);
+        }
   }
+  // the four waves' tiles are summed in wave order through one LDS tile
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) red[wave][r][lane] = acc[r];
-  __syncthreads();
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          red[t * 16 + r][lane] = w == 0 ? acc[t][r] : red[t * 16 + r][lane] + acc[t][r];
+    __syncthreads();
+  }
   // C layout: element r of lane l is (i, j) = ((r&3) + 8*(r>>2) + 4*(l>>5), l&31)
   const int Kw = g.Cin;
-  for (int e = threadIdx.x; e < 16 * 64; e += 256) {
-    const int r = e >> 6, l = e & 63;
+  for (int e = threadIdx.x; e < NT * 16 * 64; e += 256) {
+    const int tr = e >> 6, l = e & 63;
+    const int t = tr >> 4, r = tr & 15;
     const int i = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = l & 31;
-    const int oc = ti * 32 + i, ic = tj * 32 + j;
+    const int oc = ti * 32 * TI + 32 * (t / TJ) + i, ic = tj * 32 * TJ + 32 * (t % TJ) + j;
     if (oc < g.Cout && ic < g.Cin) {
-      const float v = (red[0][r][l] + red[1][r][l]) + (red[2][r][l] + red[3][r][l]);
-      part[((long long)split * g.Cout + oc) * Kw + ic] = v;
+      part[((long long)split * g.Cout + oc) * Kw + ic] = red[tr][l];
     }
   }
 }
@@ -767,8 +813,16 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
     const int used = cdiv(groups, gps);
     hipStream_t s = as_stream(stream);
     float *part = static_cast<float *>(workspace);
-    hipLaunchKernelGGL(k_wgrad_1x1, dim3(cdiv(g.Cout, 32) * cdiv(g.Cin, 32), used), dim3(256), 0, s,
-                       gout, x, part, g, used, gps);
+    int to, tc;
+    wgrad1x1_tiles(g, to, tc);
+    const dim3 grid(cdiv(g.Cout, to) * cdiv(g.Cin, tc), used);
+#define W1_LAUNCH(TI, TJ) \
+  hipLaunchKernelGGL((k_wgrad_1x1<TI, TJ>), grid, dim3(256), 0, s, gout, x, part, g, used, gps)
+    if (to == 64 && tc == 64) W1_LAUNCH(2, 2);
+    else if (to == 64) W1_LAUNCH(2, 1);
+    else if (tc == 64) W1_LAUNCH(1, 2);
+    else W1_LAUNCH(1, 1);
+#undef W1_LAUNCH
     const int n = g.Cout * g.Cin;
     hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
                        accumulate);
