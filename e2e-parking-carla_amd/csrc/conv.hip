@@ -55,7 +55,7 @@ __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : 
 // MODE 1: rows m = ci, K channels c = co, src = g [N,Cout,P,Q], dst = dx [N,Cin,H,W];
 //         phase z = (py, px), column pixel (u,v) -> (iy, ix) = (py + sh*u, px + sw*v);
 //         tap (r,s) valid for the phase: qy = u + (py + ph - r*dh)/sh (exact), qx likewise.
-template <int MODE, int ACT, int BNT, int BMT = BM>
+template <int MODE, int ACT, int BNT, int BMT, bool AV>
 __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
 
   // B-load column of this thread (fixed); its rows are wave-uniform
   const int bn = tid % BNT;
-  const int bk0 = tid / BNT;
+  const int bk0 = __builtin_amdgcn_readfirstlane(tid / BNT);  // BNT >= 64: wave-uniform
   const int ncol = n0 + bn;
   const bool col_ok = ncol < Ntot;
   int img = 0, cp = 0;
@@ -154,7 +154,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   // 4*(tid%4)..+3: float4 for 1x1 filters), so a wave touches 16 weight rows, not 64.
   const int am = MODE == 0 ? tid / (BK / NA) : (tid & (BMT - 1));
   const int ac = MODE == 0 ? NA * (tid % (BK / NA)) : 0;
-  const int ak0 = tid / BMT;  // dgrad: this thread's first k row (then every 256/BMT)
+  // dgrad: this thread's first k row (then every 256/BMT); wave-uniform for BMT = 64
+  const int ak0 = BMT == 64 ? __builtin_amdgcn_readfirstlane(tid / BMT) : tid / BMT;
   const bool arow_ok = (m0 + am) < M;
   // weight layout 0 (PyTorch [Cout][Cin][RS]):
   //   fwd: W[m][c][rs] = w[m*Cin*RS + c*RS + rs];  dgrad: W[c][m][rs] = w[c*Cin*RS + m*RS + rs]
@@ -164,40 +165,61 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   const int a_mstride = MODE == 0 ? (tm ? g.Cin : g.Cin * RS) : (tm ? 1 : RS);
   const int a_cstride = MODE == 0 ? (tm ? 1 : RS) : (tm ? g.Cin : g.Cin * RS);
   const int a_tstride = tm ? g.Cout * g.Cin : 1;
-  const bool a_vec = NA == 4 && MODE == 0 && a_cstride == 1 && (g.Cin & 3) == 0;
+  // AV (host-checked): forward, tap-major weights, Cin % 4 == 0 -> one 16-B A load per thread
+  static_assert(!AV || (MODE == 0 && NA == 4), "AV: forward 64-row tiles only");
   const int arow = (m0 + am) * a_mstride;
+
+  // Guards without per-element branches: a disabled operand gets an offset >= the buffer's
+  // size (returns 0).  Per-thread conditions (pixel / row in range) pick the base offset once
+  // per K-step; per-row channel conditions are wave-uniform and pick the row term on the
+  // scalar unit; row terms are uniform strides, so each element costs one add.  Sums stay
+  // below 2^32: the base is < 2^31 and so is every row term.
+  const int nrw = (int)min(4LL * g.Cout * g.Cin * RS, 0x7fffffffLL);
+  const int nrx = (int)min(4LL * g.N * Kc * HWs, 0x7fffffffLL);
 
   // global -> register loads run two K-steps ahead of the MFMAs (two register sets), LDS
   // is double buffered: one barrier per K-step, ~2 steps of MFMA work to cover a load
   float ra0[NA], rb0[BPER], ra1[NA], rb1[BPER];
-  auto load_tiles = [&](int ks, float(&ra)[NA], float(&rb)[BPER]) {
-    const int tap = ks / csteps;                    // uniform
+  // Every call issues the same loads (steps past the range read zeros), so the loop has no
+  // branches around loads and the s_waitcnt before each LDS store waits only for the step
+  // being stored, not for the prefetch issued after it.
+  const int klast = kend - 1;
+  auto load_tiles = [&](int ks_in, float(&ra)[NA], float(&rb)[BPER]) {
+    const bool live = ks_in <= klast;                 // uniform
+    const int ks = min(ks_in, klast);
+    const int tap = ks / csteps;                      // uniform
     const int c0 = (ks - tap * csteps) * BK;
     const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * a_tstride;
     if (MODE == 0) {
       const int c = c0 + ac;
-      if (a_vec) {
-        const float4 v = bload4(rw, (arow_ok && c < Kc) ? (arow + c + rs) * 4 : OOR);
+      if (AV) {
+        const float4 v = bload4(rw, (live && arow_ok && c < Kc) ? (arow + c + rs) * 4 : OOR);
         ra[0] = v.x; ra[1] = v.y; ra[NA > 2 ? 2 : 0] = v.z; ra[NA > 3 ? 3 : 0] = v.w;
       } else {
+        const int abase = (live && arow_ok) ? (arow + rs) * 4 : nrw;
 #pragma unroll
         for (int j = 0; j < NA; ++j)
-          ra[j] = bload(rw, (arow_ok && c + j < Kc) ? (arow + (c + j) * a_cstride + rs) * 4 : OOR);
+          ra[j] = bload(rw, c + j < Kc ? abase + (c + j) * a_cstride * 4 : OOR);
       }
     } else {
+      // rows c0 + ak0 + (256/BMT) j: wave-uniform (ak0 = wave index for BMT = 64)
+      const int abase = (live && arow_ok) ? (arow + rs) * 4 : nrw;
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
         const int c = c0 + ak0 + (256 / BMT) * j;
-        ra[j] = bload(rw, (arow_ok && c < Kc) ? (arow + c * a_cstride + rs) * 4 : OOR);
+        const int rterm = c < Kc ? c * a_cstride * 4 : nrw;
+        ra[j] = bload(rw, abase + rterm);
       }
     }
     const int iy = ybase + dy, ix = xbase + dx;
-    const bool pix_ok = col_ok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
-    const int pofs = simg + iy * Ws + ix;
+    const bool pix_ok = live && col_ok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
+    // rows c0 + bk0 + BROWS j: wave-uniform (bk0 = tid / BNT, BNT >= 64)
+    const int bbase = pix_ok ? (simg + iy * Ws + ix) * 4 : nrx;
 #pragma unroll
     for (int j = 0; j < BPER; ++j) {
       const int c = c0 + bk0 + BROWS * j;
-      rb[j] = bload(rx, (pix_ok && c < Kc) ? (pofs + c * HWs) * 4 : OOR);
+      const int rterm = c < Kc ? c * HWs * 4 : nrx;
+      rb[j] = bload(rx, bbase + rterm);
     }
   };
   auto store_tiles = [&](int buf, const float(&ra)[NA], const float(&rb)[BPER]) {
@@ -225,21 +247,21 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   if (nk > 0) {
     load_tiles(kbeg, ra0, rb0);
     store_tiles(0, ra0, rb0);
-  }
-  if (nk > 1) load_tiles(kbeg + 1, ra1, rb1);
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    // buffer 0 holds step kt, registers 1 hold step kt+1
-    if (kt + 2 < nk) load_tiles(kbeg + kt + 2, ra0, rb0);
-    compute(0);
-    if (kt + 1 < nk) store_tiles(1, ra1, rb1);
+    load_tiles(kbeg + 1, ra1, rb1);
     __syncthreads();
-    if (kt + 1 >= nk) break;
-    // buffer 1 holds step kt+1, registers 0 hold step kt+2
-    if (kt + 3 < nk) load_tiles(kbeg + kt + 3, ra1, rb1);
-    compute(1);
-    if (kt + 2 < nk) store_tiles(0, ra0, rb0);
-    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      // buffer 0 holds step kt, registers 1 hold step kt+1
+      load_tiles(kbeg + kt + 2, ra0, rb0);
+      compute(0);
+      store_tiles(1, ra1, rb1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      // buffer 1 holds step kt+1, registers 0 hold step kt+2
+      load_tiles(kbeg + kt + 3, ra1, rb1);
+      compute(1);
+      store_tiles(0, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
@@ -386,22 +408,23 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
     }
   };
+  // unconditional loads (past the range they read zeros): exact s_waitcnt, see k_conv_gemm
   if (nk > 0) {
     load_tiles(ra0, rb0);
     store_tiles(0, ra0, rb0);
-  }
-  if (nk > 1) load_tiles(ra1, rb1);
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    if (kt + 2 < nk) load_tiles(ra0, rb0);
-    compute(0);
-    if (kt + 1 < nk) store_tiles(1, ra1, rb1);
+    load_tiles(ra1, rb1);
     __syncthreads();
-    if (kt + 1 >= nk) break;
-    if (kt + 3 < nk) load_tiles(ra1, rb1);
-    compute(1);
-    if (kt + 2 < nk) store_tiles(0, ra0, rb0);
-    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      load_tiles(ra0, rb0);
+      compute(0);
+      store_tiles(1, ra1, rb1);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      load_tiles(ra1, rb1);
+      compute(1);
+      store_tiles(0, ra0, rb0);
+      __syncthreads();
+    }
   }
   const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
   const int col = n0 + 32 * wn + li;
@@ -719,9 +742,15 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     out = static_cast<float *>(workspace);
     out_bytes = (long long)gemm_workspace(p, M);
   }
-#define GEMM_LAUNCH(MD, AC, BT, BMT)                                                         \
-  hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT>), grid, dim3(256), 0, s, w, src, bias, out, \
+  const bool av = mode == 0 && g.wlayout == 1 && (g.Cin & 3) == 0;
+#define GEMM_LAUNCH1(MD, AC, BT, BMT, V)                                                         \
+  hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V>), grid, dim3(256), 0, s, w, src, bias, out, \
                      out_bytes, g, M, p.splits, p.kper)
+#define GEMM_LAUNCH(MD, AC, BT, BMT)                                  \
+  do {                                                                \
+    if (MD == 0 && BMT == 64 && av) GEMM_LAUNCH1(MD, AC, BT, BMT, MD == 0 && BMT == 64); \
+    else GEMM_LAUNCH1(MD, AC, BT, BMT, false);                        \
+  } while (0)
 #define GEMM_TILES(MD, AC)                                             \
   do {                                                                 \
     if (p.bm == 64) {                                                  \
@@ -737,6 +766,7 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
   else GEMM_TILES(1, 0);
 #undef GEMM_TILES
 #undef GEMM_LAUNCH
+#undef GEMM_LAUNCH1
   if (p.splits > 1) {
     const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
     hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
