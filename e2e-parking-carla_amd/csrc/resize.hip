@@ -94,6 +94,62 @@ __global__ void __launch_bounds__(256) k_resize_bwd_h(const float *__restrict__ 
   gx[idx] = accumulate ? gx[idx] + s : s;
 }
 
+// Destinations o (along one axis) whose bilinear taps touch source index i, with their
+// weights (both taps' weights when i0 == i1), in increasing o.  The window scanned is the
+// exact preimage of [i - 1, i + 1) widened by one on each side: at most 2 / scale + 5
+// candidates, which callers keep <= RB_MAXT (scale >= 0.4: up to 2.5x upsampling).
+constexpr int RB_MAXT = 10;
+__device__ __forceinline__ int taps_into(int i, float scale, int In, int Out, int *os, float *ws) {
+  const float inv = 1.f / scale;
+  int lo = (int)floorf(((float)i - 0.5f) * inv - 0.5f) - 1;
+  int hi = (int)ceilf(((float)i + 1.5f) * inv - 0.5f) + 1;
+  lo = max(lo, 0);
+  hi = min(hi, Out - 1);
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < RB_MAXT; ++k) {
+    const int o = lo + k;
+    if (o <= hi) {
+      const Tap t = tap(o, scale, In);
+      const float w = (t.i0 == i ? t.l0 : 0.f) + (t.i1 == i ? t.l1 : 0.f);
+      if (t.i0 == i || t.i1 == i) {
+        os[n] = o;
+        ws[n] = w;
+        ++n;
+      }
+    }
+  }
+  return n;
+}
+
+// single-pass backward for moderate scales (destination windows of <= RB_MAXT per axis):
+// gx[pl, i, j] = sum_{oh, ow} wh(oh -> i) ww(ow -> j) g[pl, oh, ow], exact tap lists, one
+// thread per source pixel; g is read through the cache once per neighbourhood instead of
+// round-tripping an intermediate through HBM.
+__global__ void __launch_bounds__(256) k_resize_bwd_2d(const float *__restrict__ g,
+                                                       long long g_pstride, int Ho, int Wo,
+                                                       int Hi, int Wi, float sh, float sw,
+                                                       float *__restrict__ gx, int accumulate) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Hi * Wi) return;
+  const int pl = blockIdx.y;
+  const int i = q / Wi, j = q - i * Wi;
+  int oh[RB_MAXT], ow[RB_MAXT];
+  float wh[RB_MAXT], ww[RB_MAXT];
+  const int nh = taps_into(i, sh, Hi, Ho, oh, wh);
+  const int nw = taps_into(j, sw, Wi, Wo, ow, ww);
+  const float *gp = g + pl * g_pstride;
+  float s = 0.f;
+  for (int a = 0; a < nh; ++a) {
+    const float *gr = gp + (long long)oh[a] * Wo;
+    float r = 0.f;
+    for (int b = 0; b < nw; ++b) r += ww[b] * gr[ow[b]];
+    s += wh[a] * r;
+  }
+  const long long idx = (long long)pl * Hi * Wi + q;
+  gx[idx] = accumulate ? gx[idx] + s : s;
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -120,6 +176,11 @@ int e2ep_resize_bwd(const float *g, long long g_pstride, int planes, int Hi, int
   E2EP_REQUIRE(planes > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, E2EP_EINVAL,
                "e2ep_resize_bwd: bad shape");
   hipStream_t s = as_stream(stream);
+  if (2.f / scale_h + 5.f <= (float)RB_MAXT && 2.f / scale_w + 5.f <= (float)RB_MAXT) {
+    hipLaunchKernelGGL(k_resize_bwd_2d, dim3(cdiv(Hi * Wi, 256), planes), dim3(256), 0, s, g,
+                       g_pstride, Ho, Wo, Hi, Wi, scale_h, scale_w, gx, accumulate);
+    return launch_status("e2ep_resize_bwd");
+  }
   float *t = static_cast<float *>(workspace);
   hipLaunchKernelGGL(k_resize_bwd_w, dim3(cdiv(Ho * Wi, 256), planes), dim3(256), 0, s, g, g_pstride,
                      planes, Ho, Wo, Wi, scale_w, t);
