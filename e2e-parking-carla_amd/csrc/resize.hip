@@ -94,59 +94,73 @@ __global__ void __launch_bounds__(256) k_resize_bwd_h(const float *__restrict__ 
   gx[idx] = accumulate ? gx[idx] + s : s;
 }
 
-// Destinations o (along one axis) whose bilinear taps touch source index i, with their
-// weights (both taps' weights when i0 == i1), in increasing o.  The window scanned is the
-// exact preimage of [i - 1, i + 1) widened by one on each side: at most 2 / scale + 5
-// candidates, which callers keep <= RB_MAXT (scale >= 0.4: up to 2.5x upsampling).
-constexpr int RB_MAXT = 10;
-__device__ __forceinline__ int taps_into(int i, float scale, int In, int Out, int *os, float *ws) {
+// Destinations o along one axis whose bilinear taps touch source index i with a non-zero
+// weight have sources in (i - 1, i + 1): a run of at most ceil(2 / scale) consecutive
+// indices, <= 4 for scale >= 0.5.  axis_taps evaluates the six candidates from one before
+// the estimated run start exactly (the estimate is within one of the true start) and keeps
+// the four-wide window starting at the first non-zero weight; returns its first index.
+constexpr int RB_T = 4;
+__device__ __forceinline__ int axis_taps(int i, float scale, int In, int Out, float *w) {
   const float inv = 1.f / scale;
-  int lo = (int)floorf(((float)i - 0.5f) * inv - 0.5f) - 1;
-  int hi = (int)ceilf(((float)i + 1.5f) * inv - 0.5f) + 1;
-  lo = max(lo, 0);
-  hi = min(hi, Out - 1);
-  int n = 0;
+  const int c = max(0, (int)ceilf(((float)i - 0.5f) * inv - 0.5f)) - 1;
+  float v[RB_T + 2];
 #pragma unroll
-  for (int k = 0; k < RB_MAXT; ++k) {
-    const int o = lo + k;
-    if (o <= hi) {
+  for (int k = 0; k < RB_T + 2; ++k) {
+    const int o = c + k;
+    float x = 0.f;
+    if (o >= 0 && o < Out) {
       const Tap t = tap(o, scale, In);
-      const float w = (t.i0 == i ? t.l0 : 0.f) + (t.i1 == i ? t.l1 : 0.f);
-      if (t.i0 == i || t.i1 == i) {
-        os[n] = o;
-        ws[n] = w;
-        ++n;
-      }
+      x = (t.i0 == i ? t.l0 : 0.f) + (t.i1 == i ? t.l1 : 0.f);
     }
+    v[k] = x;
   }
-  return n;
+  const int sh = v[0] != 0.f ? 0 : v[1] != 0.f ? 1 : 2;
+#pragma unroll
+  for (int k = 0; k < RB_T; ++k) w[k] = sh == 0 ? v[k] : sh == 1 ? v[k + 1] : v[k + 2];
+  return c + sh;
 }
 
-// single-pass backward for moderate scales (destination windows of <= RB_MAXT per axis):
-// gx[pl, i, j] = sum_{oh, ow} wh(oh -> i) ww(ow -> j) g[pl, oh, ow], exact tap lists, one
-// thread per source pixel; g is read through the cache once per neighbourhood instead of
-// round-tripping an intermediate through HBM.
+// Single-pass backward for scales >= 0.5 (<= 2x upsampling): gx[pl, i, j] =
+// sum_{a,b < 4} wh[i][a] ww[j][b] g[pl, oh_i + a, ow_j + b].  A block owns an 8 x 32 source
+// tile of one plane; the per-row and per-column tap tables are built once in LDS, then
+// every thread does 16 cached loads — no intermediate through HBM, no per-pixel tap math.
+constexpr int RB_TH = 8, RB_TW = 32;
 __global__ void __launch_bounds__(256) k_resize_bwd_2d(const float *__restrict__ g,
                                                        long long g_pstride, int Ho, int Wo,
                                                        int Hi, int Wi, float sh, float sw,
                                                        float *__restrict__ gx, int accumulate) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= Hi * Wi) return;
-  const int pl = blockIdx.y;
-  const int i = q / Wi, j = q - i * Wi;
-  int oh[RB_MAXT], ow[RB_MAXT];
-  float wh[RB_MAXT], ww[RB_MAXT];
-  const int nh = taps_into(i, sh, Hi, Ho, oh, wh);
-  const int nw = taps_into(j, sw, Wi, Wo, ow, ww);
-  const float *gp = g + pl * g_pstride;
-  float s = 0.f;
-  for (int a = 0; a < nh; ++a) {
-    const float *gr = gp + (long long)oh[a] * Wo;
-    float r = 0.f;
-    for (int b = 0; b < nw; ++b) r += ww[b] * gr[ow[b]];
-    s += wh[a] * r;
+  __shared__ int s_oh[RB_TH], s_ow[RB_TW];
+  __shared__ float s_wh[RB_TH][RB_T], s_ww[RB_TW][RB_T];
+  const int tid = threadIdx.x;
+  const int i0 = blockIdx.y * RB_TH, j0 = blockIdx.x * RB_TW;
+  if (tid < RB_TH) {
+    float w[RB_T];
+    s_oh[tid] = axis_taps(min(i0 + tid, Hi - 1), sh, Hi, Ho, w);
+#pragma unroll
+    for (int k = 0; k < RB_T; ++k) s_wh[tid][k] = w[k];
+  } else if (tid >= 64 && tid < 64 + RB_TW) {
+    float w[RB_T];
+    const int c = tid - 64;
+    s_ow[c] = axis_taps(min(j0 + c, Wi - 1), sw, Wi, Wo, w);
+#pragma unroll
+    for (int k = 0; k < RB_T; ++k) s_ww[c][k] = w[k];
   }
-  const long long idx = (long long)pl * Hi * Wi + q;
+  __syncthreads();
+  const int r = tid / RB_TW, c = tid % RB_TW;
+  const int i = i0 + r, j = j0 + c;
+  if (i >= Hi || j >= Wi) return;
+  const float *gp = g + blockIdx.z * g_pstride;
+  const int ow = s_ow[c], oh = s_oh[r];
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < RB_T; ++a) {
+    const float *gr = gp + (long long)min(oh + a, Ho - 1) * Wo;
+    float t = 0.f;
+#pragma unroll
+    for (int b = 0; b < RB_T; ++b) t += s_ww[c][b] * gr[min(ow + b, Wo - 1)];
+    s += s_wh[r][a] * t;
+  }
+  const long long idx = ((long long)blockIdx.z * Hi + i) * Wi + j;
   gx[idx] = accumulate ? gx[idx] + s : s;
 }
 
@@ -176,9 +190,9 @@ int e2ep_resize_bwd(const float *g, long long g_pstride, int planes, int Hi, int
   E2EP_REQUIRE(planes > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, E2EP_EINVAL,
                "e2ep_resize_bwd: bad shape");
   hipStream_t s = as_stream(stream);
-  if (2.f / scale_h + 5.f <= (float)RB_MAXT && 2.f / scale_w + 5.f <= (float)RB_MAXT) {
-    hipLaunchKernelGGL(k_resize_bwd_2d, dim3(cdiv(Hi * Wi, 256), planes), dim3(256), 0, s, g,
-                       g_pstride, Ho, Wo, Hi, Wi, scale_h, scale_w, gx, accumulate);
+  if (scale_h >= 0.5f && scale_w >= 0.5f && planes <= 65535) {
+    hipLaunchKernelGGL(k_resize_bwd_2d, dim3(cdiv(Wi, RB_TW), cdiv(Hi, RB_TH), planes), dim3(256),
+                       0, s, g, g_pstride, Ho, Wo, Hi, Wi, scale_h, scale_w, gx, accumulate);
     return launch_status("e2ep_resize_bwd");
   }
   float *t = static_cast<float *>(workspace);

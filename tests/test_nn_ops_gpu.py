@@ -96,7 +96,7 @@ def test_bn_drop_connect_fused(shape):
 
 @pytest.mark.parametrize("case", [((8, 65, 200, 200), (256, 256), None), ((4, 64, 16, 16), None, 2),
                                   ((2, 64, 128, 128), (200, 200), None), ((32, 64, 1, 1), (16, 16), None),
-                                  ((3, 5, 17, 9), (40, 7), None)])
+                                  ((3, 5, 17, 9), (40, 7), None), ((2, 7, 50, 60), (40, 90), None)])
 def test_resize(case):
     from e2ep_amd import nn_ops
     shape, size, sf = case
