@@ -18,7 +18,8 @@ def _g(seed):
 @pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("act", [None, "relu", "swish"])
 @pytest.mark.parametrize("res", [False, True])
-@pytest.mark.parametrize("shape", [(4, 24, 32, 32), (3, 7, 5, 9), (32, 6, 1, 1)])
+@pytest.mark.parametrize("shape", [(4, 24, 32, 32), (3, 7, 5, 9), (32, 6, 1, 1),
+                                   (4, 160, 8, 8), (16, 128, 32, 32)])
 def test_bn_act(train, act, res, shape):
     from e2ep_amd import nn_ops
     g = _g(sum(shape) + 3 * train)
@@ -58,7 +59,7 @@ def test_bn_act(train, act, res, shape):
     assert int(bnd.num_batches_tracked) == int(bn64.num_batches_tracked)
 
 
-@pytest.mark.parametrize("shape", [(8, 24, 16, 16), (6, 10, 5, 7)])
+@pytest.mark.parametrize("shape", [(8, 24, 16, 16), (6, 10, 5, 7), (16, 136, 8, 8)])
 def test_bn_drop_connect_fused(shape):
     """MBConv tail in training: bn2 -> efficientnet-pytorch drop_connect (x / keep *
     floor(keep + u)) -> + inputs, fused into the BN kernels; vs fp64 torch."""
