@@ -645,6 +645,97 @@ __global__ void __launch_bounds__(256) k_skinny_gemm(const float *__restrict__ A
   if (lane == 0) C[o] = s + (bias ? bias[j] : 0.f);
 }
 
+// ------------------------------------------------------------------------------------------
+// Direct forward convolution for tiny reduction depth (Cin*R*S <= 32, R*S > 1) and
+// Cout <= 64: the EfficientNet stem (3 -> 48, 3x3/2).  As an implicit GEMM its K = 27 pads
+// to a 16-channel step per tap (9 MFMA K-steps for 27 useful products); directly it is one
+// pass over the input and the output (HBM-bound).
+// ------------------------------------------------------------------------------------------
+constexpr int DK = 32;  // max Cin*R*S
+
+__device__ __forceinline__ int dk_w_index(const ConvGeom &g, int co, int k) {
+  const int RS = g.R * g.S, ci = k / RS, rs = k - ci * RS;
+  return g.wlayout == 1 ? (rs * g.Cout + co) * g.Cin + ci : (co * g.Cin + ci) * RS + rs;
+}
+
+// im2col row of output pixel (oy, ox) of image img: xin[k], k = ci*R*S + r*S + s (zero pad)
+__device__ __forceinline__ void dk_gather(const ConvGeom &g, const __amdgpu_buffer_rsrc_t &rx,
+                                          int img, int oy, int ox, bool ok, float (&xin)[DK]) {
+  const int RS = g.R * g.S, K = g.Cin * RS;
+#pragma unroll
+  for (int k = 0; k < DK; ++k) {
+    const int ci = k / RS, rs = k - ci * RS, r = rs / g.S, sx = rs - r * g.S;
+    const int iy = oy * g.sh - g.ph + r * g.dh, ix = ox * g.sw - g.pw + sx * g.dw;
+    const bool in = ok && k < K && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+    xin[k] = bload(rx, in ? (((img * g.Cin + ci) * g.H + iy) * g.W + ix) * 4 : OOR);
+  }
+}
+
+// forward: thread per output pixel, all Cout channels in chunks of 16; weights [k][co] in LDS
+// (every lane reads the same word: broadcast)
+constexpr int DCO = 64, DCH = 16;
+__global__ void __launch_bounds__(256) k_conv_direct(const float *__restrict__ x,
+                                                     const float *__restrict__ w,
+                                                     const float *__restrict__ bias, ConvGeom g,
+                                                     int act, float *__restrict__ y) {
+  __shared__ float4 wl[DK][DCO / 4];
+  __shared__ float xs[DK][256];  // this block's im2col rows, k-major (thread-contiguous)
+  const int K = g.Cin * g.R * g.S;
+  for (int e = threadIdx.x; e < DK * DCO; e += 256) {
+    const int k = e / DCO, co = e - k * DCO;
+    reinterpret_cast<float *>(wl)[e] = (k < K && co < g.Cout) ? w[dk_w_index(g, co, k)] : 0.f;
+  }
+  const int PQ = g.P * g.Q;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  const bool ok = pix < g.N * PQ;
+  const int img = ok ? pix / PQ : 0, pq = ok ? pix - img * PQ : 0;
+  const int oy = pq / g.Q, ox = pq - oy * g.Q;
+  {
+    const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * g.H * g.W);
+    float xin[DK];
+    dk_gather(g, rx, img, oy, ox, ok, xin);
+#pragma unroll
+    for (int k = 0; k < DK; ++k) xs[k][threadIdx.x] = xin[k];
+  }
+  __syncthreads();
+  float *yp = y + (size_t)img * g.Cout * PQ + pq;
+#pragma unroll 1
+  for (int c0 = 0; c0 < g.Cout; c0 += DCH) {
+    float acc[DCH];
+#pragma unroll
+    for (int j = 0; j < DCH; ++j) acc[j] = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < K; ++k) {
+      const float xv = xs[k][threadIdx.x];
+#pragma unroll
+      for (int j4 = 0; j4 < DCH / 4; ++j4) {
+        const float4 wv = wl[k][c0 / 4 + j4];
+        acc[4 * j4 + 0] = __builtin_fmaf(xv, wv.x, acc[4 * j4 + 0]);
+        acc[4 * j4 + 1] = __builtin_fmaf(xv, wv.y, acc[4 * j4 + 1]);
+        acc[4 * j4 + 2] = __builtin_fmaf(xv, wv.z, acc[4 * j4 + 2]);
+        acc[4 * j4 + 3] = __builtin_fmaf(xv, wv.w, acc[4 * j4 + 3]);
+      }
+    }
+    if (ok) {
+#pragma unroll
+      for (int j = 0; j < DCH; ++j) {
+        const int co = c0 + j;
+        if (co < g.Cout) {
+          float v = acc[j] + (bias ? bias[co] : 0.f);
+          if (act == 1) v = fmaxf(v, 0.f);
+          yp[(size_t)co * PQ] = v;
+        }
+      }
+    }
+  }
+}
+
+// forward only (the weight gradient stays on the split-K GEMM: measured faster), and only
+// for R x S > 1 (a 1x1 with K <= 32 is already a plain GEMM with no tap padding)
+static bool direct_ok(const ConvGeom &g) {
+  return g.R * g.S > 1 && g.Cin * g.R * g.S <= DK && g.Cout <= DCO;
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -780,6 +871,7 @@ extern "C" {
 
 size_t e2ep_conv_fwd_workspace(const int *dims) {
   ConvGeom g = make_geom(dims);
+  if (direct_ok(g)) return 0;
   return gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout);
 }
 
@@ -795,6 +887,11 @@ int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *
   g.wlayout = w_layout;
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_fwd: bad geometry");
   E2EP_REQUIRE(act == 0 || act == 1, E2EP_EINVAL, "e2ep_conv_fwd: act must be 0 (none) or 1 (relu)");
+  if (direct_ok(g)) {
+    hipLaunchKernelGGL(k_conv_direct, dim3(cdiv((long long)g.N * g.P * g.Q, 256)), dim3(256), 0,
+                       as_stream(stream), x, w, bias, g, act, y);
+    return launch_status("e2ep_conv_fwd");
+  }
   const int rc = launch_gemm(0, act, w, x, bias, y, 4LL * g.N * g.Cout * g.P * g.Q, g, g.Cout,
                              workspace, as_stream(stream));
   if (rc) return rc;

@@ -35,6 +35,10 @@ CASES = [
     (4, 32, 128, 128, 192, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),  # 1x1 wgrad 64x32 wave tiles
     (4, 64, 128, 128, 24, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),   # 1x1 wgrad 32x64 wave tiles
     (4, 128, 128, 128, 120, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),  # 64x64 wave tiles, ragged Cout
+    (2, 2, 17, 19, 40, 3, 3, 1, (1, 1, 1, 1), 1, True, 1),       # direct path: K=18, bias+relu
+    (3, 24, 16, 16, 24, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),     # direct fwd 1x1 K=24
+    (2, 1, 30, 30, 64, 5, 5, 2, (2, 2, 2, 2), 1, False, 0),      # direct K=25, Cout=64, s2
+    (2, 3, 21, 23, 17, 3, 3, 1, (2, 2, 2, 2), 2, False, 0),      # direct, dilated, ragged Cout
 ]
 
 
