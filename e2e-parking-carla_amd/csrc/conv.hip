@@ -345,21 +345,26 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   const int pend = min(Ptot, pbeg + pix_per_split);
   const int HW = g.H * g.W;
 
-  // thread -> pixel = tid & 15 (same pixel for its A and B loads), co / col rows = tid >> 4
+  // thread -> pixel = tid & 15 (same pixel for its A and B loads), co / col rows = tid >> 4.
+  // Guards are branch-free: an invalid element gets an offset >= the buffer size (reads 0);
+  // per-column constants (channel plane + tap displacement) are folded once.
   const int tp = tid & 15, trow = tid >> 4;
-  int cofs[4], cdy[4], cdx[4];
-  bool cok[4];
+  const int nrg = (int)min(4LL * g.N * g.Cout * PQ, 0x7fffffffLL);
+  const int nrx = (int)min(4LL * g.N * g.Cin * HW, 0x7fffffffLL);
+  int cconst[4], cdy[4], cdx[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + trow + 16 * j;
-    cok[j] = col < Kw;
-    const int cc = cok[j] ? col : 0;
+    const int cc = col < Kw ? col : 0;
     const int ci = cc / RS, tap = cc - ci * RS;
     const int r = tap / g.S, s = tap - r * g.S;
-    cofs[j] = ci * HW;
     cdy[j] = r * g.dh - g.ph;
     cdx[j] = s * g.dw - g.pw;
+    cconst[j] = ci * HW + cdy[j] * g.W + cdx[j];
+    // an out-of-range column gets an impossible row displacement: never in bounds
+    if (col >= Kw) cdy[j] = -(1 << 29);
   }
+  const int arow = (m0 + trow) * PQ;  // gout row of this thread's first co
   int p_cur = pbeg + tp;
   int im = p_cur / max(PQ, 1), od = p_cur - im * PQ;
 
@@ -369,19 +374,19 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   auto load_tiles = [&](float(&ra)[4], float(&rb)[4]) {
     const bool pok = p_cur < pend;
     const int oy = od / g.Q, ox = od - oy * g.Q;
-    const int gb = im * g.Cout * PQ + od;
+    const int abase = pok ? (im * g.Cout * PQ + od + arow) * 4 : nrg;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int co = m0 + trow + 16 * j;
-      ra[j] = bload(rg, (pok && co < g.Cout) ? (gb + co * PQ) * 4 : OOR);
+      ra[j] = bload(rg, co < g.Cout ? abase + j * 16 * PQ * 4 : OOR);
     }
     const int yb = oy * g.sh, xb0 = ox * g.sw;
-    const int xb = im * g.Cin * HW;
+    const int pbase = im * g.Cin * HW + yb * g.W + xb0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int iy = yb + cdy[j], ix = xb0 + cdx[j];
-      const bool ok = pok && cok[j] && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-      rb[j] = bload(rx, ok ? (xb + cofs[j] + iy * g.W + ix) * 4 : OOR);
+      const bool ok = pok && (unsigned)(yb + cdy[j]) < (unsigned)g.H &&
+                      (unsigned)(xb0 + cdx[j]) < (unsigned)g.W;
+      rb[j] = bload(rx, ok ? (pbase + cconst[j]) * 4 : nrx);
     }
     p_cur += BK;
     od += BK;
