@@ -455,9 +455,14 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 // ------------------------------------------------------------------------------------------
 constexpr int W1_GROUPS = 4;  // 8-pixel groups per wave iteration (8 float4 loads in flight)
 
+// Used for large pixel counts with few channel pairs (the early EfficientNet stages, the
+// segmentation classifier); elsewhere the LDS-tiled k_conv_wgrad reads each operand row once
+// per 64x64 tile instead of once per 32x32 wave tile and is faster (scripts/bench_conv.py).
 static bool wgrad1x1_ok(const ConvGeom &g) {
+  const long long pix = (long long)g.N * g.P * g.Q;
   return g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 &&
-         g.P == g.H && g.Q == g.W && (g.P * g.Q) % 8 == 0;
+         g.P == g.H && g.Q == g.W && (g.P * g.Q) % 8 == 0 && pix >= 131072 &&
+         (pix >= 200000 || (long long)g.Cout * g.Cin <= 6144);
 }
 
 static int wgrad1x1_splits_for(const ConvGeom &g, int to, int tc) {

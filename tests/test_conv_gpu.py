@@ -32,9 +32,10 @@ CASES = [
     (2, 64, 24, 24, 64, 3, 3, 1, (1, 1, 1, 1), 1, False, 1),     # 3x3 s1 (tap wgrad path)
     (2, 40, 16, 16, 24, 3, 3, 1, (2, 2, 2, 2), 2, False, 0),     # dilated 3x3, partial tiles
     (2, 65, 20, 24, 48, 5, 5, 1, (2, 2, 2, 2), 1, True, 0),      # 5x5 s1
-    (4, 32, 128, 128, 192, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),  # 1x1 wgrad 64x32 wave tiles
-    (4, 64, 128, 128, 24, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),   # 1x1 wgrad 32x64 wave tiles
-    (4, 128, 128, 128, 120, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),  # 64x64 wave tiles, ragged Cout
+    (8, 32, 128, 128, 192, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),  # 1x1 wgrad 64x32 wave tiles
+    (16, 64, 128, 128, 24, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),  # 1x1 wgrad 32x64 wave tiles
+    (16, 64, 128, 128, 64, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),  # 1x1 wgrad 64x64 wave tiles
+    (4, 128, 32, 32, 120, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),   # 1x1 on the LDS-tiled wgrad
     (2, 2, 17, 19, 40, 3, 3, 1, (1, 1, 1, 1), 1, True, 1),       # direct path: K=18, bias+relu
     (3, 24, 16, 16, 24, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),     # direct fwd 1x1 K=24
     (2, 1, 30, 30, 64, 5, 5, 2, (2, 2, 2, 2), 1, False, 0),      # direct K=25, Cout=64, s2
