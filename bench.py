@@ -127,10 +127,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N>1 path on a one-GPU box: every rank on device 0, gloo all-reduce
+    # (E2EP_BENCH_REHEARSAL=1; never used for reported numbers)
+    rehearsal = os.environ.get("E2EP_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from e2ep_amd import _lib, synthetic, timing
     from e2ep_amd.train import TrainStep

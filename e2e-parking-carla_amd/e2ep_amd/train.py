@@ -40,6 +40,7 @@ class TrainStep:
                                       device=self.params[0].device) if world > 1 else None)
         self.loss = None
         self.g_bwd = self.g_gather = self.g_opt = None
+        self._host_sync = world > 1 and dist.get_backend() == "gloo"
         if graph:
             self._capture(warmup)
 
@@ -100,6 +101,10 @@ class TrainStep:
         self.g_bwd.replay()
         if self.world > 1:
             self.g_gather.replay()
+            if self._host_sync:
+                # gloo's CUDA all-reduce does not order itself after graph replays on this
+                # stack (it hangs); RCCL's does.  Only the gloo rehearsal path pays this.
+                torch.cuda.synchronize()
             self._allreduce()
         self.g_opt.replay()
         return self.loss
