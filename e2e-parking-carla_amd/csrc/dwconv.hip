@@ -175,6 +175,14 @@ static DwStrip dw_strip(int K, int st, int W, int P, int Q) {
   return d;
 }
 
+// Each wave of the strip kernels stages and reads only its own LDS region, so the staging
+// needs a wave-level fence, not a block barrier: the wave's LDS writes complete (lgkmcnt(0))
+// before any lane reads another lane's words, and the four waves of a block run decoupled.
+__device__ __forceinline__ void dw_wave_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt unconstrained
+  __builtin_amdgcn_wave_barrier();
+}
+
 // stage input rows [iy0, iy0 + IR) of plane `src` (H x W) into this wave's LDS buffer
 __device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, int W, int iy0,
                                          int IR, int WP, float *lds, int lane,
@@ -221,7 +229,7 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
     dw_stage(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane, tf,
              nc % g.C);
   }
-  __syncthreads();
+  dw_wave_sync();
   if (!active) return;
   const int c = nc % g.C;
   float wr[K * K];
@@ -269,7 +277,7 @@ __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restri
     oyA = (iy0 + g.pt - (K - 1)) >> 1;  // floor division by 2
     dw_stage(gy + (size_t)nc * g.P * g.Q, g.P, g.Q, oyA, GR, WPg, lds, lane);
   }
-  __syncthreads();
+  dw_wave_sync();
   if (!active) return;
   const int c = nc % g.C;
   float wr[K * K];
@@ -327,7 +335,7 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
       dw_stage(x + ((size_t)n * g.C + c) * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds,
                lane, tf, c);
     }
-    __syncthreads();
+    dw_wave_sync();
     const int oy = oy0 + ro;
     if (active && ro < d.RO && oy < g.P) {
       const float4 gv4 = *reinterpret_cast<const float4 *>(gy + (((size_t)n * g.C + c) * g.P + oy) * g.Q + ox0);
@@ -344,7 +352,7 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
           for (int u = 0; u < 4; ++u) acc[a * K + b] = __builtin_fmaf(gv[u], v[u * ST + b], acc[a * K + b]);
       }
     }
-    __syncthreads();  // LDS reuse
+    dw_wave_sync();  // LDS reuse
   }
   __shared__ float red[4][K * K];
 #pragma unroll
