@@ -50,13 +50,18 @@ class _BnAct(torch.autograd.Function):
         dx = torch.empty_like(x) if nig[0] else None
         dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
         db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
-        dres = torch.empty_like(x) if (res is not None and nig[3]) else None
+        # no activation: the residual's gradient is dy itself (y = dc(bn(x)) + res) — hand dy
+        # over instead of writing a copy
+        dres_is_dy = res is not None and nig[3] and ctx.act == 0
+        dres = torch.empty_like(x) if (res is not None and nig[3] and not dres_is_dy) else None
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
         with timing.region("bn_bwd"):
             _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(mean), _lib.ptr(invstd),
                       _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), _lib.ptr(dc_rand),
                       float(ctx.dc_keep), None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx),
                       _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.stream())
+        if dres_is_dy:
+            dres = dy
         return dx, dg, db, dres, None, None, None, None, None, None, None, None
 
 
