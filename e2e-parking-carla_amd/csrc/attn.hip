@@ -1,0 +1,466 @@
+// Fused multi-head attention (fp32) for the fusion encoder and the control decoder:
+// softmax(scale * Q K^T + mask) -> dropout -> @ V, forward and backward, reading Q/K/V
+// straight out of the in-projection output and writing O in the (S, B, E) layout the
+// out-projection consumes.  Replaces the inner part of torch.nn.MultiheadAttention as called
+// by the reference's TransformerEncoderLayer / TransformerDecoderLayer
+// (model/feature_fusion.py:13-14,48-50; model/control_predict.py:19-20,39-47): PyTorch runs
+// it there as bmm -> (mask add) -> safe softmax -> dropout -> bmm with the score tensor
+// written and re-read by ~10 launches per direction.
+//
+// Shapes on the path: encoder Sq = Sk = 256, decoder self Sq = Sk = 14 (causal + key
+// padding), decoder cross Sq = 14, Sk = 256; 6 heads x dh 43; B = 8.  Scores never leave the
+// chip.  Work per (query, key) pair is a few dh-long dot products, so this is vector-FMA
+// work on data held in LDS (a head's K/V is <= 90 KB), not MFMA: at dh = 43 and fp32 the
+// 32x32x2 MFMA tile would waste a third of the K dimension and the whole problem is
+// ~0.3 GFLOP per layer.
+//
+//   k_attn_fwd    block = (64-query tile, b*h); the head's K and V staged in LDS row-major
+//                 [key][DHP]; lane = query (q row in registers), 4 waves split the keys and
+//                 run an online softmax over 8-key groups; the 4 partial (max, sum, acc)
+//                 triples are merged in fixed wave order through LDS; O goes out through an
+//                 LDS tile as contiguous dh-float rows.  Also writes lse (log2 domain).
+//   k_attn_bwd_q  same tiling; recomputes P from lse, D_i = dO_i . O_i, and
+//                 dS = P (drop(dO V^T) - D); dQ = scale dS K (waves merged in fixed order).
+//   k_attn_bwd_kv block = (64-key tile, b*h); Q, dO, lse, D of the head staged in LDS;
+//                 lane = key (k, v, dk, dv rows in registers), 4 waves split the queries;
+//                 dV = P_drop^T dO, dK = scale dS^T Q.
+// Dropout: keep(b*h, i, j) = hash(seed, (bh*Sq + i)*Sk + j) >= p, scaled by 1/(1-p); the
+// seed is read from device memory (drawn by the caller each call, graph-capturable), so the
+// backward regenerates the same mask without storing it.
+#include "common.h"
+
+namespace e2ep {
+
+constexpr int ATT_SMAX = 256;  // max Sq / Sk (one head's K, V staged whole)
+constexpr int ATT_WAVES = 4;
+constexpr int ATT_TILE = 64;   // queries (fwd, bwd_q) or keys (bwd_kv) per block
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ uint32_t att_mix(uint32_t x) {  // 32-bit integer finaliser
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// dropout keep test for counter c: uniform 24-bit value >= p
+__device__ __forceinline__ bool att_keep(uint32_t seedmix, uint32_t c, float p) {
+  return (float)(att_mix(c ^ seedmix) >> 8) * (1.0f / 16777216.0f) >= p;
+}
+__device__ __forceinline__ uint32_t att_seedmix(const int *seed) {
+  return seed ? att_mix((uint32_t)seed[0] * 0x9e3779b9u + 0x632be5abu) : 0u;
+}
+
+template <int DHP>
+__device__ __forceinline__ float dot_lds(const float (&r)[DHP], const float *row) {
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int d = 0; d < DHP; d += 4) {
+    const float4 k = *reinterpret_cast<const float4 *>(row + d);
+    s0 = __builtin_fmaf(r[d], k.x, s0);
+    s1 = __builtin_fmaf(r[d + 1], k.y, s1);
+    s0 = __builtin_fmaf(r[d + 2], k.z, s0);
+    s1 = __builtin_fmaf(r[d + 3], k.w, s1);
+  }
+  return s0 + s1;
+}
+template <int DHP>
+__device__ __forceinline__ void axpy_lds(float (&acc)[DHP], float a, const float *row) {
+#pragma unroll
+  for (int d = 0; d < DHP; d += 4) {
+    const float4 v = *reinterpret_cast<const float4 *>(row + d);
+    acc[d] = __builtin_fmaf(a, v.x, acc[d]);
+    acc[d + 1] = __builtin_fmaf(a, v.y, acc[d + 1]);
+    acc[d + 2] = __builtin_fmaf(a, v.z, acc[d + 2]);
+    acc[d + 3] = __builtin_fmaf(a, v.w, acc[d + 3]);
+  }
+}
+
+struct AttnDims {
+  int B, H, Sq, Sk, dh;
+  int q_ss, q_sb, kv_ss, kv_sb, o_ss, o_sb;  // element strides (sequence, batch)
+  float scale, p;
+  int causal;
+};
+
+// stage rows [0, n) of a head's (S, B, E)-strided matrix into LDS as [n][DHP] (zero padded).
+// Loads go out STAGE_BATCH per thread before any LDS store (branch-free buffer loads; out of
+// range -> 0), so a head's 90 KB arrives in a few memory round trips, not one per element.
+constexpr int STAGE_BATCH = 32;
+template <int DHP>
+__device__ __forceinline__ void stage_rows(float *dst, const float *src, int n, int ss, int dh) {
+  const int total = n * DHP;
+  const __amdgpu_buffer_rsrc_t R = rsrc(src, 4LL * ((long long)(n - 1) * ss + dh));
+  for (int e0 = 0; e0 < total; e0 += ATT_WAVES * 64 * STAGE_BATCH) {
+    float t[STAGE_BATCH];
+#pragma unroll
+    for (int u = 0; u < STAGE_BATCH; ++u) {
+      const int e = e0 + u * ATT_WAVES * 64 + (int)threadIdx.x;
+      const int r = e / DHP, d = e - r * DHP;
+      t[u] = bload(R, (e < total && d < dh) ? 4 * (r * ss + d) : OOR);
+    }
+#pragma unroll
+    for (int u = 0; u < STAGE_BATCH; ++u) {
+      const int e = e0 + u * ATT_WAVES * 64 + (int)threadIdx.x;
+      if (e < total) dst[e] = t[u];
+    }
+  }
+}
+
+// one head row (dh floats at p) into registers, zero padded to DHP, times mul.  p differs per
+// lane, so no buffer descriptor (that would waterfall): padded slots re-read element dh-1
+// (always in bounds) and are zeroed by the multiplier, so the loads carry no branches.
+template <int DHP>
+__device__ __forceinline__ void load_row(float (&r)[DHP], const float *p, int dh, float mul) {
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) r[d] = p[min(d, dh - 1)] * (d < dh ? mul : 0.f);
+}
+
+// write an LDS tile [64][DHP] (rows r0.. of a head) to an (S, B, E)-strided matrix
+template <int DHP>
+__device__ __forceinline__ void store_rows(float *dst, const float *tile, int r0, int n, int ss,
+                                           int dh) {
+  const int nr = min(ATT_TILE, n - r0);
+  for (int e = threadIdx.x; e < nr * dh; e += ATT_WAVES * 64) {
+    const int r = e / dh, d = e - r * dh;
+    dst[(long long)(r0 + r) * ss + d] = tile[r * DHP + d];
+  }
+}
+
+template <int DHP>
+__global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
+    const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
+    const uint8_t *__restrict__ kpad, const int *__restrict__ seed, AttnDims a,
+    float *__restrict__ o, float *__restrict__ lse2) {
+  __shared__ __attribute__((aligned(16))) float sm[2 * ATT_SMAX * DHP];
+  __shared__ float smask[ATT_SMAX];
+  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  const int q0 = blockIdx.x * ATT_TILE;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float *sK = sm, *sV = sm + ATT_SMAX * DHP;
+  const long long kvoff = (long long)b * a.kv_sb + h * a.dh;
+  stage_rows<DHP>(sK, k + kvoff, a.Sk, a.kv_ss, a.dh);
+  stage_rows<DHP>(sV, v + kvoff, a.Sk, a.kv_ss, a.dh);
+  for (int j = threadIdx.x; j < a.Sk; j += ATT_WAVES * 64)
+    smask[j] = (kpad && kpad[(long long)b * a.Sk + j]) ? -INFINITY : 0.f;
+  const int i = q0 + lane;
+  const bool qvalid = i < a.Sq;
+  float qr[DHP];
+  const float qmul = a.scale * LOG2E;  // scores in the log2 domain
+  const float *qrow = q + (long long)b * a.q_sb + h * a.dh + (long long)min(i, a.Sq - 1) * a.q_ss;
+  load_row<DHP>(qr, qrow, a.dh, qmul);
+  __syncthreads();
+  const uint32_t sm_ = att_seedmix(seed);
+  const int chunk = (a.Sk + ATT_WAVES - 1) / ATT_WAVES;
+  const int j0 = w * chunk, j1 = min(a.Sk, j0 + chunk);
+  float m = -INFINITY, l = 0.f, acc[DHP];
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) acc[d] = 0.f;
+  const uint32_t cbase = ((uint32_t)bh * a.Sq + i) * a.Sk;
+  for (int jb = j0; jb < j1; jb += 8) {
+    float s[8];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = jb + u;
+      const int jl = min(j, j1 - 1);
+      const float x = dot_lds<DHP>(qr, sK + jl * DHP) + smask[jl];
+      s[u] = (j < j1 && !(a.causal && j > i)) ? x : -INFINITY;
+      bm = fmaxf(bm, s[u]);
+    }
+    const float mn = fmaxf(m, bm);
+    const float ms = mn == -INFINITY ? 0.f : mn;
+    const float corr = exp2f(m - ms);
+    m = mn;
+    l *= corr;
+#pragma unroll
+    for (int d = 0; d < DHP; ++d) acc[d] *= corr;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float pu = exp2f(s[u] - ms);
+      l += pu;
+      const int j = min(jb + u, j1 - 1);
+      const float pd = (a.p > 0.f && !att_keep(sm_, cbase + j, a.p)) ? 0.f : pu;
+      axpy_lds<DHP>(acc, pd, sV + j * DHP);
+    }
+  }
+  __syncthreads();  // K/V no longer needed: reuse sm for the merge
+  float *mrg = sm;  // [w][DHP + 2][64]
+  constexpr int MS = (DHP + 2) * 64;
+  mrg[w * MS + lane] = m;
+  mrg[w * MS + 64 + lane] = l;
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) mrg[w * MS + (d + 2) * 64 + lane] = acc[d];
+  __syncthreads();
+  // wave w merges dims [w*DHP/4, (w+1)*DHP/4) of query `lane` in fixed wave order
+  float M = -INFINITY;
+#pragma unroll
+  for (int x = 0; x < ATT_WAVES; ++x) M = fmaxf(M, mrg[x * MS + lane]);
+  const float Ms = M == -INFINITY ? 0.f : M;
+  float L = 0.f, f[ATT_WAVES];
+#pragma unroll
+  for (int x = 0; x < ATT_WAVES; ++x) {
+    f[x] = exp2f(mrg[x * MS + lane] - Ms);
+    L = __builtin_fmaf(mrg[x * MS + 64 + lane], f[x], L);
+  }
+  const float rinv = L > 0.f ? 1.f / (L * (1.f - a.p)) : 0.f;
+  constexpr int DPW = DHP / ATT_WAVES;
+  float outv[DPW];
+#pragma unroll
+  for (int t = 0; t < DPW; ++t) {
+    const int d = w * DPW + t;
+    float sacc = 0.f;
+#pragma unroll
+    for (int x = 0; x < ATT_WAVES; ++x) sacc = __builtin_fmaf(mrg[x * MS + (d + 2) * 64 + lane], f[x], sacc);
+    outv[t] = sacc * rinv;
+  }
+  if (w == 0 && qvalid) lse2[(long long)bh * a.Sq + i] = L > 0.f ? M + log2f(L) : INFINITY;
+  __syncthreads();
+  float *tile = sm + ATT_WAVES * MS;  // [64][DHP]
+#pragma unroll
+  for (int t = 0; t < DPW; ++t) tile[lane * DHP + w * DPW + t] = outv[t];
+  __syncthreads();
+  store_rows<DHP>(o + (long long)b * a.o_sb + h * a.dh, tile, q0, a.Sq, a.o_ss, a.dh);
+}
+
+template <int DHP>
+__global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_q(
+    const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
+    const float *__restrict__ o, const float *__restrict__ dout, const float *__restrict__ lse2,
+    const uint8_t *__restrict__ kpad, const int *__restrict__ seed, AttnDims a,
+    float *__restrict__ dq, float *__restrict__ Dbuf) {
+  __shared__ __attribute__((aligned(16))) float sm[2 * ATT_SMAX * DHP];
+  __shared__ float smask[ATT_SMAX];
+  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  const int q0 = blockIdx.x * ATT_TILE;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float *sK = sm, *sV = sm + ATT_SMAX * DHP;
+  const long long kvoff = (long long)b * a.kv_sb + h * a.dh;
+  stage_rows<DHP>(sK, k + kvoff, a.Sk, a.kv_ss, a.dh);
+  stage_rows<DHP>(sV, v + kvoff, a.Sk, a.kv_ss, a.dh);
+  for (int j = threadIdx.x; j < a.Sk; j += ATT_WAVES * 64)
+    smask[j] = (kpad && kpad[(long long)b * a.Sk + j]) ? -INFINITY : 0.f;
+  const int i = q0 + lane, ic = min(i, a.Sq - 1);
+  float qr[DHP], dor[DHP];
+  const float qmul = a.scale * LOG2E;
+  const float *qrow = q + (long long)b * a.q_sb + h * a.dh + (long long)ic * a.q_ss;
+  const long long orow = (long long)b * a.o_sb + h * a.dh + (long long)ic * a.o_ss;
+  float orr[DHP];
+  load_row<DHP>(qr, qrow, a.dh, qmul);
+  load_row<DHP>(dor, dout + orow, a.dh, 1.f);
+  load_row<DHP>(orr, o + orow, a.dh, 1.f);
+  float Di = 0.f;
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) Di = __builtin_fmaf(dor[d], orr[d], Di);
+  const float li = lse2[(long long)bh * a.Sq + ic];
+  __syncthreads();
+  const uint32_t sm_ = att_seedmix(seed);
+  const float rkeep = 1.f / (1.f - a.p);
+  const int chunk = (a.Sk + ATT_WAVES - 1) / ATT_WAVES;
+  const int j0 = w * chunk, j1 = min(a.Sk, j0 + chunk);
+  float acc[DHP];
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) acc[d] = 0.f;
+  const uint32_t cbase = ((uint32_t)bh * a.Sq + i) * a.Sk;
+  for (int j = j0; j < j1; ++j) {
+    const float s = dot_lds<DHP>(qr, sK + j * DHP) + smask[j];
+    const float pj = (a.causal && j > i) ? 0.f : exp2f(s - li);
+    const float dpd = dot_lds<DHP>(dor, sV + j * DHP);
+    const float dp = (a.p > 0.f && !att_keep(sm_, cbase + j, a.p)) ? 0.f : dpd * rkeep;
+    axpy_lds<DHP>(acc, pj * (dp - Di), sK + j * DHP);
+  }
+  __syncthreads();
+  constexpr int MS = DHP * 64;
+  float *mrg = sm;  // [w][DHP][64]
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) mrg[w * MS + d * 64 + lane] = acc[d];
+  __syncthreads();
+  constexpr int DPW = DHP / ATT_WAVES;
+  float outv[DPW];
+#pragma unroll
+  for (int t = 0; t < DPW; ++t) {
+    const int d = w * DPW + t;
+    float sacc = 0.f;
+#pragma unroll
+    for (int x = 0; x < ATT_WAVES; ++x) sacc += mrg[x * MS + d * 64 + lane];
+    outv[t] = sacc * a.scale;
+  }
+  if (w == 0 && i < a.Sq) Dbuf[(long long)bh * a.Sq + i] = Di;
+  __syncthreads();
+  float *tile = sm + ATT_WAVES * MS;
+#pragma unroll
+  for (int t = 0; t < DPW; ++t) tile[lane * DHP + w * DPW + t] = outv[t];
+  __syncthreads();
+  store_rows<DHP>(dq + (long long)b * a.q_sb + h * a.dh, tile, q0, a.Sq, a.q_ss, a.dh);
+}
+
+template <int DHP>
+__global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
+    const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
+    const float *__restrict__ dout, const float *__restrict__ lse2, const float *__restrict__ Dbuf,
+    const uint8_t *__restrict__ kpad, const int *__restrict__ seed, AttnDims a,
+    float *__restrict__ dk, float *__restrict__ dv) {
+  // staging [Sq][DHP] x 2 and the merge [w][2*DHP][64] share one buffer
+  constexpr int SMF = (2 * ATT_SMAX * DHP > ATT_WAVES * 128 * DHP) ? 2 * ATT_SMAX * DHP
+                                                                   : ATT_WAVES * 128 * DHP;
+  __shared__ __attribute__((aligned(16))) float sm[SMF];
+  __shared__ float slse[ATT_SMAX], sD[ATT_SMAX];
+  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  const int k0 = blockIdx.x * ATT_TILE;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float *sQ = sm, *sO = sm + ATT_SMAX * DHP;
+  stage_rows<DHP>(sQ, q + (long long)b * a.q_sb + h * a.dh, a.Sq, a.q_ss, a.dh);
+  stage_rows<DHP>(sO, dout + (long long)b * a.o_sb + h * a.dh, a.Sq, a.o_ss, a.dh);
+  for (int t = threadIdx.x; t < a.Sq; t += ATT_WAVES * 64) {
+    slse[t] = lse2[(long long)bh * a.Sq + t];
+    sD[t] = Dbuf[(long long)bh * a.Sq + t];
+  }
+  const int j = k0 + lane, jc = min(j, a.Sk - 1);
+  const bool kmasked = kpad && kpad[(long long)b * a.Sk + jc];
+  const long long krow = (long long)b * a.kv_sb + h * a.dh + (long long)jc * a.kv_ss;
+  float kr[DHP], vr[DHP], adk[DHP], adv[DHP];
+  const float kmul = a.scale * LOG2E;
+  load_row<DHP>(kr, k + krow, a.dh, kmul);
+  load_row<DHP>(vr, v + krow, a.dh, 1.f);
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) {
+    adk[d] = 0.f;
+    adv[d] = 0.f;
+  }
+  __syncthreads();
+  const uint32_t sm_ = att_seedmix(seed);
+  const float rkeep = 1.f / (1.f - a.p);
+  const int chunk = (a.Sq + ATT_WAVES - 1) / ATT_WAVES;
+  const int i0 = w * chunk, i1 = min(a.Sq, i0 + chunk);
+  for (int i = i0; i < i1; ++i) {
+    const float s = dot_lds<DHP>(kr, sQ + i * DHP);
+    const bool masked = kmasked || (a.causal && j > i);
+    const float pj = masked ? 0.f : exp2f(s - slse[i]);
+    const bool keep = !(a.p > 0.f) || att_keep(sm_, ((uint32_t)bh * a.Sq + i) * a.Sk + j, a.p);
+    const float pd = keep ? pj * rkeep : 0.f;
+    const float dpd = dot_lds<DHP>(vr, sO + i * DHP);
+    const float ds = pj * ((keep ? dpd * rkeep : 0.f) - sD[i]);
+    axpy_lds<DHP>(adv, pd, sO + i * DHP);
+    axpy_lds<DHP>(adk, ds, sQ + i * DHP);
+  }
+  __syncthreads();
+  constexpr int MS = 2 * DHP * 64;
+  float *mrg = sm;  // [w][2*DHP][64]
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) {
+    mrg[w * MS + d * 64 + lane] = adk[d];
+    mrg[w * MS + (DHP + d) * 64 + lane] = adv[d];
+  }
+  __syncthreads();
+  // wave w reduces columns [w*2*DHP/4, ...) of the 2*DHP (dk | dv) columns
+  constexpr int CPW = 2 * DHP / ATT_WAVES;
+  float outv[CPW];
+#pragma unroll
+  for (int t = 0; t < CPW; ++t) {
+    const int c = w * CPW + t;
+    float sacc = 0.f;
+#pragma unroll
+    for (int x = 0; x < ATT_WAVES; ++x) sacc += mrg[x * MS + c * 64 + lane];
+    outv[t] = c < DHP ? sacc * a.scale : sacc;
+  }
+  __syncthreads();
+  float *tile = sm;  // [64][2*DHP]: dk | dv
+#pragma unroll
+  for (int t = 0; t < CPW; ++t) tile[lane * 2 * DHP + w * CPW + t] = outv[t];
+  __syncthreads();
+  const int nr = min(ATT_TILE, a.Sk - k0);
+  const long long base = (long long)b * a.kv_sb + h * a.dh;
+  for (int e = threadIdx.x; e < nr * a.dh; e += ATT_WAVES * 64) {
+    const int r = e / a.dh, d = e - r * a.dh;
+    const long long off = base + (long long)(k0 + r) * a.kv_ss + d;
+    dk[off] = tile[r * 2 * DHP + d];
+    dv[off] = tile[r * 2 * DHP + DHP + d];
+  }
+}
+
+// keep mask as bytes [BH][Sq][Sk] (test/diagnostic entry)
+__global__ void k_attn_keep_mask(const int *seed, int BH, int Sq, int Sk, float p, uint8_t *out) {
+  const long long n = (long long)BH * Sq * Sk;
+  const uint32_t sm_ = att_seedmix(seed);
+  for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < n;
+       c += (long long)gridDim.x * blockDim.x)
+    out[c] = att_keep(sm_, (uint32_t)c, p) ? 1 : 0;
+}
+
+static int attn_check(const AttnDims &a, const char *who) {
+  E2EP_REQUIRE(a.B > 0 && a.H > 0 && a.Sq > 0 && a.Sk > 0 && a.dh > 0, E2EP_EINVAL, "%s: bad shape", who);
+  E2EP_REQUIRE(a.Sq <= ATT_SMAX && a.Sk <= ATT_SMAX && a.dh <= 64, E2EP_ERANGE,
+               "%s: Sq %d / Sk %d (max %d) or head dim %d (max 64) unsupported", who, a.Sq, a.Sk,
+               ATT_SMAX, a.dh);
+  E2EP_REQUIRE(a.p >= 0.f && a.p < 1.f, E2EP_EINVAL, "%s: dropout p %g outside [0, 1)", who, a.p);
+  E2EP_REQUIRE((long long)a.B * a.H * a.Sq * a.Sk < 0xffffffffLL, E2EP_ERANGE,
+               "%s: dropout counter space exceeds 32 bits", who);
+  return 0;
+}
+
+static AttnDims make_dims(int B, int H, int Sq, int Sk, int dh, int q_ss, int q_sb, int kv_ss,
+                          int kv_sb, int o_ss, int o_sb, float scale, int causal, float p) {
+  AttnDims a;
+  a.B = B; a.H = H; a.Sq = Sq; a.Sk = Sk; a.dh = dh;
+  a.q_ss = q_ss; a.q_sb = q_sb; a.kv_ss = kv_ss; a.kv_sb = kv_sb; a.o_ss = o_ss; a.o_sb = o_sb;
+  a.scale = scale; a.p = p; a.causal = causal;
+  return a;
+}
+
+}  // namespace e2ep
+
+using namespace e2ep;
+
+extern "C" {
+
+int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, int Sq, int Sk,
+                  int dh, int q_ss, int q_sb, int kv_ss, int kv_sb, int o_ss, int o_sb,
+                  float scale, int causal, const uint8_t *key_pad, float p, const int32_t *seed,
+                  float *o, float *lse, void *stream) {
+  const AttnDims a = make_dims(B, H, Sq, Sk, dh, q_ss, q_sb, kv_ss, kv_sb, o_ss, o_sb, scale, causal, p);
+  if (int rc = attn_check(a, "e2ep_attn_fwd")) return rc;
+  E2EP_REQUIRE(p == 0.f || seed, E2EP_EINVAL, "e2ep_attn_fwd: dropout needs a seed");
+  const dim3 grid(cdiv(Sq, ATT_TILE), B * H);
+  if (dh <= 44)
+    hipLaunchKernelGGL(k_attn_fwd<44>, grid, dim3(ATT_WAVES * 64), 0, as_stream(stream), q, k, v,
+                       key_pad, seed, a, o, lse);
+  else
+    hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(ATT_WAVES * 64), 0, as_stream(stream), q, k, v,
+                       key_pad, seed, a, o, lse);
+  return launch_status("e2ep_attn_fwd");
+}
+
+size_t e2ep_attn_bwd_workspace(int B, int H, int Sq) { return (size_t)B * H * Sq * sizeof(float); }
+
+int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o, const float *dout,
+                  const float *lse, int B, int H, int Sq, int Sk, int dh, int q_ss, int q_sb,
+                  int kv_ss, int kv_sb, int o_ss, int o_sb, float scale, int causal,
+                  const uint8_t *key_pad, float p, const int32_t *seed, float *dq, float *dk,
+                  float *dv, void *workspace, void *stream) {
+  const AttnDims a = make_dims(B, H, Sq, Sk, dh, q_ss, q_sb, kv_ss, kv_sb, o_ss, o_sb, scale, causal, p);
+  if (int rc = attn_check(a, "e2ep_attn_bwd")) return rc;
+  E2EP_REQUIRE(p == 0.f || seed, E2EP_EINVAL, "e2ep_attn_bwd: dropout needs a seed");
+  float *D = static_cast<float *>(workspace);
+  hipStream_t s = as_stream(stream);
+  const dim3 gq(cdiv(Sq, ATT_TILE), B * H), gk(cdiv(Sk, ATT_TILE), B * H), blk(ATT_WAVES * 64);
+  if (dh <= 44) {
+    hipLaunchKernelGGL(k_attn_bwd_q<44>, gq, blk, 0, s, q, k, v, o, dout, lse, key_pad, seed, a, dq, D);
+    hipLaunchKernelGGL(k_attn_bwd_kv<44>, gk, blk, 0, s, q, k, v, dout, lse, D, key_pad, seed, a, dk, dv);
+  } else {
+    hipLaunchKernelGGL(k_attn_bwd_q<64>, gq, blk, 0, s, q, k, v, o, dout, lse, key_pad, seed, a, dq, D);
+    hipLaunchKernelGGL(k_attn_bwd_kv<64>, gk, blk, 0, s, q, k, v, dout, lse, D, key_pad, seed, a, dk, dv);
+  }
+  return launch_status("e2ep_attn_bwd");
+}
+
+int e2ep_attn_keep_mask(const int32_t *seed, int BH, int Sq, int Sk, float p, uint8_t *out,
+                        void *stream) {
+  E2EP_REQUIRE(seed && BH > 0 && Sq > 0 && Sk > 0, E2EP_EINVAL, "e2ep_attn_keep_mask: bad args");
+  const long long n = (long long)BH * Sq * Sk;
+  hipLaunchKernelGGL(k_attn_keep_mask, dim3(min(cdiv(n, 256), 4096)), dim3(256), 0, as_stream(stream),
+                     seed, BH, Sq, Sk, p, out);
+  return launch_status("e2ep_attn_keep_mask");
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+"""torch.nn.MultiheadAttention forward (need_weights=False) on the fused e2ep attention core.
+
+The reference's transformer layers call `self_attn(x, x, x, ...)` / `multihead_attn(x, mem,
+mem)` (torch TransformerEncoderLayer / TransformerDecoderLayer, model/feature_fusion.py:13-14,
+model/control_predict.py:19-20).  Here the in-projection stays one hipBLASLt GEMM (packed
+Q|K|V for self-attention, Q and K|V for cross-attention), the attention core runs as
+e2ep_attn_fwd / e2ep_attn_bwd reading Q/K/V in place from that output (no head split
+copies, scores never written), and the out-projection is the module's own linear.
+
+`mha(mod, ...)` falls back to calling the module itself whenever the fused path would not be
+the same computation or would bypass something a caller installed: forward hooks or an
+instance-patched forward (the closed-loop agent's attention capture,
+agent/parking_agent.py:71-80,266-268), a float attn_mask not declared causal, bias_k /
+add_zero_attn, separate projection weights, or shapes outside the kernel's range.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib, timing
+
+MAX_SEQ = 256
+MAX_HEAD_DIM = 64
+
+
+class _Attn(torch.autograd.Function):
+    """O = dropout_p(softmax(scale Q K^T + mask)) V on (S, B, E)-strided Q/K/V.
+
+    `qb` holds Q at column offset 0 (row stride qb.shape[-1]); `kvb` holds K at column offset
+    `k_off` and V at `k_off + E`.  When kvb is None, K/V live in qb itself (packed QKV)."""
+
+    @staticmethod
+    def forward(ctx, qb, kvb, H, causal, key_pad, p, seed):
+        packed = kvb is None
+        kvt = qb if packed else kvb
+        Sq, B, Wq = qb.shape
+        Sk, _, Wkv = kvt.shape
+        E = Wq // 3 if packed else Wq
+        dh = E // H
+        k_off = E if packed else 0
+        o = torch.empty(Sq, B, E, dtype=qb.dtype, device=qb.device)
+        lse = torch.empty(B * H, Sq, dtype=torch.float32, device=qb.device)
+        kptr = kvt.data_ptr() + 4 * k_off
+        vptr = kptr + 4 * E
+        dims = (B, H, Sq, Sk, dh, B * Wq, Wq, B * Wkv, Wkv, B * E, E)
+        with timing.region("attn_fwd"):
+            _lib.call("e2ep_attn_fwd", _lib.ptr(qb), kptr, vptr, *dims, 1.0 / math.sqrt(dh),
+                      int(causal), _lib.ptr(key_pad), float(p), _lib.ptr(seed), _lib.ptr(o),
+                      _lib.ptr(lse), _lib.stream())
+        ctx.save_for_backward(qb, kvb, o, lse, key_pad, seed)
+        ctx.cfg = (packed, dims, E, k_off, causal, float(p))
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qb, kvb, o, lse, key_pad, seed = ctx.saved_tensors
+        packed, dims, E, k_off, causal, p = ctx.cfg
+        B, H, Sq = dims[0], dims[1], dims[2]
+        kvt = qb if packed else kvb
+        do = do.contiguous()
+        dqb = torch.empty_like(qb)
+        dkvb = None if packed else torch.empty_like(kvb)
+        dkvt = dqb if packed else dkvb
+        kptr = kvt.data_ptr() + 4 * k_off
+        dkptr = dkvt.data_ptr() + 4 * k_off
+        ws = torch.empty(_lib.call_raw("e2ep_attn_bwd_workspace", B, H, Sq) // 4,
+                         dtype=torch.float32, device=qb.device)
+        with timing.region("attn_bwd"):
+            _lib.call("e2ep_attn_bwd", _lib.ptr(qb), kptr, kptr + 4 * E, _lib.ptr(o), _lib.ptr(do),
+                      _lib.ptr(lse), *dims, 1.0 / math.sqrt(dims[4]), int(causal),
+                      _lib.ptr(key_pad), p, _lib.ptr(seed), _lib.ptr(dqb), dkptr, dkptr + 4 * E,
+                      _lib.ptr(ws), _lib.stream())
+        return dqb, dkvb, None, None, None, None, None
+
+
+def attention(qb, kvb, H, causal=False, key_pad=None, p=0.0, seed=None):
+    """Functional entry: see _Attn.  key_pad: bool (B, Sk) or None; seed: int32 (1,) device
+    tensor, drawn here when p > 0 and none is given."""
+    if p > 0.0 and seed is None:
+        seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=qb.device)
+    qb = qb.contiguous()
+    kvb = None if kvb is None else kvb.contiguous()
+    if key_pad is not None:
+        key_pad = key_pad.contiguous()
+        if key_pad.dtype != torch.bool:
+            raise TypeError("key_pad must be a bool mask (True = ignore key)")
+    return _Attn.apply(qb, kvb, H, bool(causal), key_pad, float(p), seed)
+
+
+def _fusable(mod, query, key, attn_mask, key_padding_mask, is_causal):
+    if key_padding_mask is not None and key_padding_mask.dtype != torch.bool:
+        return False
+    if mod._forward_hooks or mod._forward_pre_hooks or "forward" in mod.__dict__:
+        return False
+    if not mod._qkv_same_embed_dim or mod.batch_first or mod.bias_k is not None or mod.add_zero_attn:
+        return False
+    if attn_mask is not None and not is_causal:
+        return False
+    if not query.is_cuda or query.dtype != torch.float32 or query.dim() != 3:
+        return False
+    E, H = mod.embed_dim, mod.num_heads
+    return (E // H <= MAX_HEAD_DIM and query.shape[0] <= MAX_SEQ and key.shape[0] <= MAX_SEQ)
+
+
+def mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, is_causal=False):
+    """mod(query, key, value, attn_mask=..., key_padding_mask=..., need_weights=False)[0] for a
+    seq-first nn.MultiheadAttention, on the fused core when possible.  `is_causal` asserts
+    that attn_mask is the causal (-inf above the diagonal) mask, as torch's is_causal hint."""
+    if not _fusable(mod, query, key, attn_mask, key_padding_mask, is_causal):
+        return mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
+                   need_weights=False, is_causal=bool(is_causal) and attn_mask is not None)[0]
+    E, H = mod.embed_dim, mod.num_heads
+    W, bias = mod.in_proj_weight, mod.in_proj_bias
+    p = mod.dropout if mod.training else 0.0
+    if query is key and key is value:
+        qkv = F.linear(query, W, bias)
+        o = attention(qkv, None, H, is_causal, key_padding_mask, p)
+    else:
+        if key is not value:
+            return mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
+                       need_weights=False)[0]
+        q = F.linear(query, W[:E], None if bias is None else bias[:E])
+        kv = F.linear(key, W[E:], None if bias is None else bias[E:])
+        o = attention(q, kv, H, is_causal, key_padding_mask, p)
+    return F.linear(o, mod.out_proj.weight, mod.out_proj.bias)

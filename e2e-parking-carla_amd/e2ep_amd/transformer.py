@@ -5,11 +5,13 @@ model/control_predict.py:19-20).  The layers stay torch.nn Transformer*Layer mod
 keys and the agent's self_attn hook, agent/parking_agent.py:71-80); their forward is restated
 here with the same math and the same submodules, except that each "x + dropout(sublayer(x))
 -> LayerNorm" runs as one e2ep kernel (nn_ops.add_drop_layer_norm) instead of PyTorch's
-dropout + add + layer_norm (+ its slow gamma/beta backward).  The attention blocks and the
-linear layers are the modules' own (hipBLASLt GEMMs)."""
+dropout + add + layer_norm (+ its slow gamma/beta backward).  The attention core (QK^T, mask,
+softmax, dropout, PV and their backward) runs as e2ep kernels through attention.mha, which
+keeps the modules' own in/out projections (hipBLASLt GEMMs) and falls back to the module when
+a hook is installed (the agent's attention capture)."""
 import torch.nn.functional as F
 
-from . import nn_ops
+from . import attention, nn_ops
 
 
 def _p(drop, training):
@@ -23,8 +25,7 @@ def _ff(layer, x):
 def encoder_layer(layer, x, mask=None, key_padding_mask=None):
     """torch.nn.TransformerEncoderLayer.forward (norm_first=False), seq-first x (S, B, E)."""
     assert not layer.norm_first
-    sa = layer.self_attn(x, x, x, attn_mask=mask, key_padding_mask=key_padding_mask,
-                         need_weights=False)[0]
+    sa = attention.mha(layer.self_attn, x, x, x, attn_mask=mask, key_padding_mask=key_padding_mask)
     x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
     return nn_ops.add_drop_layer_norm(x, _ff(layer, x), layer.norm2, _p(layer.dropout2, layer.training))
 
@@ -32,10 +33,10 @@ def encoder_layer(layer, x, mask=None, key_padding_mask=None):
 def decoder_layer(layer, x, memory, tgt_mask=None, tgt_key_padding_mask=None, tgt_is_causal=False):
     """torch.nn.TransformerDecoderLayer.forward (norm_first=False), seq-first."""
     assert not layer.norm_first
-    sa = layer.self_attn(x, x, x, attn_mask=tgt_mask, key_padding_mask=tgt_key_padding_mask,
-                         is_causal=bool(tgt_is_causal), need_weights=False)[0]
+    sa = attention.mha(layer.self_attn, x, x, x, attn_mask=tgt_mask,
+                       key_padding_mask=tgt_key_padding_mask, is_causal=bool(tgt_is_causal))
     x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
-    ca = layer.multihead_attn(x, memory, memory, need_weights=False)[0]
+    ca = attention.mha(layer.multihead_attn, x, memory, memory)
     x = nn_ops.add_drop_layer_norm(x, ca, layer.norm2, _p(layer.dropout2, layer.training))
     return nn_ops.add_drop_layer_norm(x, _ff(layer, x), layer.norm3, _p(layer.dropout3, layer.training))
 

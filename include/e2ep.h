@@ -248,6 +248,34 @@ int e2ep_add_drop_ln_bwd(const float *dy, const float *x, const float *mean, con
                          void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Fused multi-head attention core, fp32: O = dropout_p(softmax(scale Q K^T + mask)) V per
+ * (batch, head), replacing the bmm / mask / softmax / dropout / bmm chain inside
+ * torch.nn.MultiheadAttention as the reference's transformer layers run it
+ * (model/feature_fusion.py:13-14,48-50; model/control_predict.py:19-20,39-47).
+ * Q, K, V, O are (S, B, E)-strided: row (s, b) of head h starts at
+ * base + s*ss + b*sb + h*dh (so Q/K/V are read in place from the in-projection output).
+ * Sq, Sk <= 256, dh <= 64.  causal masks key j > query i; key_pad (bool [B][Sk], may be NULL)
+ * masks keys; a fully masked row yields O = 0.  Dropout keep(bh, i, j) is a hash of *seed
+ * and the counter (bh*Sq + i)*Sk + j (seed: device int32, may be NULL when p == 0).
+ * lse: [B*H][Sq] row log-sum-exp (log2 domain, internal) for the backward.
+ * Backward writes dq (Q's layout) and dk, dv (K/V's layout); workspace
+ * e2ep_attn_bwd_workspace bytes.  e2ep_attn_keep_mask materialises the keep mask
+ * ([BH][Sq][Sk] bytes) for tests.
+ * ------------------------------------------------------------------------------------- */
+int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, int Sq, int Sk,
+                  int dh, int q_ss, int q_sb, int kv_ss, int kv_sb, int o_ss, int o_sb,
+                  float scale, int causal, const uint8_t *key_pad, float p, const int32_t *seed,
+                  float *o, float *lse, void *stream);
+size_t e2ep_attn_bwd_workspace(int B, int H, int Sq);
+int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o, const float *dout,
+                  const float *lse, int B, int H, int Sq, int Sk, int dh, int q_ss, int q_sb,
+                  int kv_ss, int kv_sb, int o_ss, int o_sb, float scale, int causal,
+                  const uint8_t *key_pad, float p, const int32_t *seed, float *dq, float *dk,
+                  float *dv, void *workspace, void *stream);
+int e2ep_attn_keep_mask(const int32_t *seed, int BH, int Sq, int Sk, float p, uint8_t *out,
+                        void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Bilinear resize, align_corners=False (F.interpolate / nn.Upsample semantics) over
  * `planes` = N*C planes.  scale_* = 1/scale_factor when a factor is given, else In/Out.
  * Replaces model/bev_encoder.py:24, model/segmentation_head.py:35-38,

@@ -1,0 +1,167 @@
+"""Fused attention core (e2ep_attn_fwd / e2ep_attn_bwd) vs torch.nn.MultiheadAttention.
+
+Shapes are the reference's transformer calls (model/feature_fusion.py:13-14: self-attention
+over 256 BEV tokens; model/control_predict.py:19-20: causal + key-padding self-attention over
+14 control tokens and cross-attention to the 256-token memory), d_model 258, 6 heads.
+Reference = the same module in fp64 on the CPU; tolerance rel-L2 <= 1e-4 (north_star) on the
+output and on every gradient.  Dropout is checked against an fp64 restatement that applies
+the kernel's own keep mask (e2ep_attn_keep_mask), so the mask is the only shared piece."""
+import math
+
+import pytest
+import torch
+from torch import nn
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+E, H = 258, 6
+
+
+def _module(seed):
+    torch.manual_seed(seed)
+    m = nn.MultiheadAttention(E, H, dropout=0.0)
+    with torch.no_grad():
+        m.in_proj_bias.normal_(0, 0.1)
+        m.out_proj.bias.normal_(0, 0.1)
+    return m
+
+
+def _grads(m, *xs):
+    return [x.grad for x in xs] + [m.in_proj_weight.grad, m.in_proj_bias.grad,
+                                   m.out_proj.weight.grad, m.out_proj.bias.grad]
+
+
+@pytest.mark.parametrize("case", ["enc_self", "dec_self", "dec_cross", "ragged"])
+def test_mha_matches_module(case):
+    from e2ep_amd import attention
+    g = torch.Generator().manual_seed(7)
+    B = 8
+    Sq, Sk = {"enc_self": (256, 256), "dec_self": (14, 14), "dec_cross": (14, 256),
+              "ragged": (77, 130)}[case]
+    m = _module(len(case))
+    m64 = _module(len(case)).double()
+    x = torch.randn(Sq, B, E, generator=g)
+    mem = torch.randn(Sk, B, E, generator=g)
+    dy = torch.randn(Sq, B, E, generator=g)
+    causal = case == "dec_self"
+    kpm = None
+    mask = None
+    if causal:
+        kpm = torch.zeros(B, Sk, dtype=torch.bool)
+        for b in range(B):
+            kpm[b, Sk - b:] = True  # sample b has b PAD tokens at the end
+        mask = torch.full((Sk, Sk), float("-inf")).triu(1)
+    self_attn = case in ("enc_self", "dec_self")
+    # reference (fp64, CPU)
+    xr = x.double().requires_grad_(True)
+    mr = xr if self_attn else mem.double().requires_grad_(True)
+    yr = m64(xr, mr, mr, attn_mask=None if mask is None else mask.double(), key_padding_mask=kpm,
+             need_weights=False)[0]
+    (yr * dy.double()).sum().backward()
+    # fused path
+    md = m.to(DEV)
+    xd = x.to(DEV).requires_grad_(True)
+    memd = xd if self_attn else mem.to(DEV).requires_grad_(True)
+    yd = attention.mha(md, xd, memd, memd, attn_mask=None if mask is None else mask.to(DEV),
+                       key_padding_mask=None if kpm is None else kpm.to(DEV), is_causal=causal)
+    (yd * dy.to(DEV)).sum().backward()
+    assert rel_l2(yd.detach().cpu(), yr) < 1e-4
+    ins = (xd,) if self_attn else (xd, memd)
+    ins_r = (xr,) if self_attn else (xr, mr)
+    for a, b in zip(_grads(md, *ins), _grads(m64, *ins_r)):
+        assert rel_l2(a.cpu(), b) < 1e-4
+
+
+def _ref_core(q, k, v, keep, p, causal, kpm):
+    """fp64 restatement: (B*H, S, dh) operands, keep mask [BH][Sq][Sk]."""
+    s = q @ k.transpose(1, 2) / math.sqrt(q.shape[-1])
+    BH, Sq, Sk = s.shape
+    if causal:
+        s = s.masked_fill(torch.ones(Sq, Sk, dtype=torch.bool).triu(1), float("-inf"))
+    if kpm is not None:
+        s = s.masked_fill(kpm.repeat_interleave(BH // kpm.shape[0], 0)[:, None, :], float("-inf"))
+    P = torch.softmax(s, -1).nan_to_num(0.0)
+    return (P * keep / (1 - p)) @ v
+
+
+@pytest.mark.parametrize("Sq,Sk,causal", [(256, 256, False), (14, 14, True), (14, 256, False)])
+def test_attention_dropout_matches_masked_reference(Sq, Sk, causal):
+    from e2ep_amd import _lib, attention
+    g = torch.Generator().manual_seed(11)
+    B, dh, p = 4, 43, 0.1
+    Ed = H * dh
+    qb = torch.randn(Sq, B, Ed, generator=g)
+    kvb = torch.randn(Sk, B, 2 * Ed, generator=g)
+    do = torch.randn(Sq, B, Ed, generator=g)
+    kpm = torch.zeros(B, Sk, dtype=torch.bool)
+    kpm[1, Sk - 3:] = True
+    seed = torch.tensor([12345], dtype=torch.int32, device=DEV)
+    keep = torch.empty(B * H, Sq, Sk, dtype=torch.uint8, device=DEV)
+    _lib.call("e2ep_attn_keep_mask", _lib.ptr(seed), B * H, Sq, Sk, p, _lib.ptr(keep), _lib.stream())
+    keep = keep.cpu().double()
+    assert abs(float(keep.mean()) - (1 - p)) < 0.01
+    qd = qb.to(DEV).requires_grad_(True)
+    kvd = kvb.to(DEV).requires_grad_(True)
+    o = attention.attention(qd, kvd, H, causal, kpm.to(DEV), p, seed)
+    (o * do.to(DEV)).sum().backward()
+
+    def heads(t):  # (S, B, H*dh) -> (B*H, S, dh)
+        S = t.shape[0]
+        return t.reshape(S, B, H, dh).permute(1, 2, 0, 3).reshape(B * H, S, dh)
+    qr = qb.double().requires_grad_(True)
+    kvr = kvb.double().requires_grad_(True)
+    orr = _ref_core(heads(qr), heads(kvr[..., :Ed]), heads(kvr[..., Ed:]), keep, p, causal, kpm)
+    orr = orr.reshape(B, H, Sq, dh).permute(2, 0, 1, 3).reshape(Sq, B, Ed)
+    (orr * do.double()).sum().backward()
+    assert rel_l2(o.detach().cpu(), orr) < 1e-4
+    assert rel_l2(qd.grad.cpu(), qr.grad) < 1e-4
+    assert rel_l2(kvd.grad.cpu(), kvr.grad) < 1e-4
+    # same seed -> same result (the backward regenerates the forward's mask)
+    o2 = attention.attention(qd.detach(), kvd.detach(), H, causal, kpm.to(DEV), p, seed)
+    assert torch.equal(o2, o.detach())
+
+
+def test_fully_masked_rows_are_zero():
+    from e2ep_amd import attention
+    B, S, dh = 2, 20, 43
+    qb = torch.randn(S, B, 3 * H * dh, device=DEV, requires_grad=True)
+    kpm = torch.zeros(B, S, dtype=torch.bool, device=DEV)
+    kpm[1] = True
+    o = attention.attention(qb, None, H, False, kpm)
+    assert torch.all(o[:, 1] == 0) and torch.isfinite(o).all()
+    o.sum().backward()
+    assert torch.isfinite(qb.grad).all()
+
+
+def test_hooked_module_falls_back():
+    """A forward hook (the agent's attention capture) must see the module's own call."""
+    from e2ep_amd import attention
+    m = _module(0).to(DEV)
+    seen = []
+    h = m.register_forward_hook(lambda mod, args, out: seen.append(out))
+    x = torch.randn(16, 2, E, device=DEV)
+    y = attention.mha(m, x, x, x)
+    h.remove()
+    assert len(seen) == 1
+    assert rel_l2(y.cpu(), attention.mha(m, x, x, x).cpu()) < 1e-5
+
+
+def test_graph_replay_draws_new_masks():
+    """Under HIP-graph replay the seed tensor is redrawn each replay (torch's graph-safe RNG),
+    so consecutive replays use different dropout masks."""
+    from e2ep_amd import attention
+    qb = torch.randn(64, 2, 3 * E, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        attention.attention(qb, None, H, p=0.1)
+    torch.cuda.current_stream().wait_stream(s)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        out = attention.attention(qb, None, H, p=0.1)
+    gr.replay()
+    a = out.clone()
+    gr.replay()
+    assert not torch.equal(a, out)
