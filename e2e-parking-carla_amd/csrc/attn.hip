@@ -33,7 +33,6 @@ namespace e2ep {
 
 constexpr int ATT_SMAX = 256;  // max Sq / Sk (one head's K, V staged whole)
 constexpr int ATT_WAVES = 4;
-constexpr int ATT_TILE = 64;   // queries (fwd, bwd_q) or keys (bwd_kv) per block
 constexpr float LOG2E = 1.4426950408889634f;
 
 __device__ __forceinline__ uint32_t att_mix(uint32_t x) {  // 32-bit integer finaliser
@@ -117,18 +116,27 @@ __device__ __forceinline__ void load_row(float (&r)[DHP], const float *p, int dh
   for (int d = 0; d < DHP; ++d) r[d] = p[min(d, dh - 1)] * (d < dh ? mul : 0.f);
 }
 
-// write an LDS tile [64][DHP] (rows r0.. of a head) to an (S, B, E)-strided matrix
-template <int DHP>
+// lanes-per-row butterfly merges (rows = queries or keys spread over L consecutive lanes)
+template <int L, int N>
+__device__ __forceinline__ void lane_sum(float (&x)[N]) {
+#pragma unroll
+  for (int off = L / 2; off > 0; off >>= 1)
+#pragma unroll
+    for (int d = 0; d < N; ++d) x[d] += __shfl_xor(x[d], off, 64);
+}
+
+// write an LDS tile [ROWS][DHP] (rows r0.. of a head) to an (S, B, E)-strided matrix
+template <int DHP, int ROWS>
 __device__ __forceinline__ void store_rows(float *dst, const float *tile, int r0, int n, int ss,
                                            int dh) {
-  const int nr = min(ATT_TILE, n - r0);
+  const int nr = min(ROWS, n - r0);
   for (int e = threadIdx.x; e < nr * dh; e += ATT_WAVES * 64) {
     const int r = e / dh, d = e - r * dh;
     dst[(long long)(r0 + r) * ss + d] = tile[r * DHP + d];
   }
 }
 
-template <int DHP>
+template <int DHP, int LPQ>
 __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
     const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
     const uint8_t *__restrict__ kpad, const int *__restrict__ seed, AttnDims a,
@@ -136,16 +144,16 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
   __shared__ __attribute__((aligned(16))) float sm[2 * ATT_SMAX * DHP];
   __shared__ float smask[ATT_SMAX];
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int q0 = blockIdx.x * ATT_TILE;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int QPW = 64 / LPQ;  // queries per block; LPQ lanes share a query's keys
+  const int q0 = blockIdx.x * QPW;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane & (LPQ - 1);
   float *sK = sm, *sV = sm + ATT_SMAX * DHP;
   const long long kvoff = (long long)b * a.kv_sb + h * a.dh;
   stage_rows<DHP>(sK, k + kvoff, a.Sk, a.kv_ss, a.dh);
   stage_rows<DHP>(sV, v + kvoff, a.Sk, a.kv_ss, a.dh);
   for (int j = threadIdx.x; j < a.Sk; j += ATT_WAVES * 64)
     smask[j] = (kpad && kpad[(long long)b * a.Sk + j]) ? -INFINITY : 0.f;
-  const int i = q0 + lane;
-  const bool qvalid = i < a.Sq;
+  const int i = q0 + lane / LPQ;
   float qr[DHP];
   const float qmul = a.scale * LOG2E;  // scores in the log2 domain
   const float *qrow = q + (long long)b * a.q_sb + h * a.dh + (long long)min(i, a.Sq - 1) * a.q_ss;
@@ -158,12 +166,12 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
 #pragma unroll
   for (int d = 0; d < DHP; ++d) acc[d] = 0.f;
   const uint32_t cbase = ((uint32_t)bh * a.Sq + i) * a.Sk;
-  for (int jb = j0; jb < j1; jb += 8) {
+  for (int jb = j0 + sub; jb < j1; jb += 8 * LPQ) {
     float s[8];
     float bm = -INFINITY;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int j = jb + u;
+      const int j = jb + u * LPQ;
       const int jl = min(j, j1 - 1);
       const float x = dot_lds<DHP>(qr, sK + jl * DHP) + smask[jl];
       s[u] = (j < j1 && !(a.causal && j > i)) ? x : -INFINITY;
@@ -180,18 +188,34 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
     for (int u = 0; u < 8; ++u) {
       const float pu = exp2f(s[u] - ms);
       l += pu;
-      const int j = min(jb + u, j1 - 1);
+      const int j = min(jb + u * LPQ, j1 - 1);
       const float pd = (a.p > 0.f && !att_keep(sm_, cbase + j, a.p)) ? 0.f : pu;
       axpy_lds<DHP>(acc, pd, sV + j * DHP);
     }
   }
-  __syncthreads();  // K/V no longer needed: reuse sm for the merge
-  float *mrg = sm;  // [w][DHP + 2][64]
-  constexpr int MS = (DHP + 2) * 64;
-  mrg[w * MS + lane] = m;
-  mrg[w * MS + 64 + lane] = l;
+  if (LPQ > 1) {  // merge the query's LPQ lane partials (same result in every lane)
 #pragma unroll
-  for (int d = 0; d < DHP; ++d) mrg[w * MS + (d + 2) * 64 + lane] = acc[d];
+    for (int off = LPQ / 2; off > 0; off >>= 1) {
+      const float mo = __shfl_xor(m, off, 64);
+      const float mn = fmaxf(m, mo);
+      const float ms = mn == -INFINITY ? 0.f : mn;
+      const float fs = exp2f(m - ms), fo = exp2f(mo - ms);
+      l = l * fs + __shfl_xor(l, off, 64) * fo;
+#pragma unroll
+      for (int d = 0; d < DHP; ++d) acc[d] = acc[d] * fs + __shfl_xor(acc[d], off, 64) * fo;
+      m = mn;
+    }
+  }
+  __syncthreads();  // K/V no longer needed: reuse sm for the merge
+  float *mrg = sm;  // [w][DHP + 2][64], column = query within the block
+  constexpr int MS = (DHP + 2) * 64;
+  if (sub == 0) {
+    const int c = lane / LPQ;
+    mrg[w * MS + c] = m;
+    mrg[w * MS + 64 + c] = l;
+#pragma unroll
+    for (int d = 0; d < DHP; ++d) mrg[w * MS + (d + 2) * 64 + c] = acc[d];
+  }
   __syncthreads();
   // wave w merges dims [w*DHP/4, (w+1)*DHP/4) of query `lane` in fixed wave order
   float M = -INFINITY;
@@ -215,16 +239,17 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
     for (int x = 0; x < ATT_WAVES; ++x) sacc = __builtin_fmaf(mrg[x * MS + (d + 2) * 64 + lane], f[x], sacc);
     outv[t] = sacc * rinv;
   }
-  if (w == 0 && qvalid) lse2[(long long)bh * a.Sq + i] = L > 0.f ? M + log2f(L) : INFINITY;
+  if (w == 0 && lane < QPW && q0 + lane < a.Sq)
+    lse2[(long long)bh * a.Sq + q0 + lane] = L > 0.f ? M + log2f(L) : INFINITY;
   __syncthreads();
   float *tile = sm + ATT_WAVES * MS;  // [64][DHP]
 #pragma unroll
   for (int t = 0; t < DPW; ++t) tile[lane * DHP + w * DPW + t] = outv[t];
   __syncthreads();
-  store_rows<DHP>(o + (long long)b * a.o_sb + h * a.dh, tile, q0, a.Sq, a.o_ss, a.dh);
+  store_rows<DHP, QPW>(o + (long long)b * a.o_sb + h * a.dh, tile, q0, a.Sq, a.o_ss, a.dh);
 }
 
-template <int DHP>
+template <int DHP, int LPQ>
 __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_q(
     const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
     const float *__restrict__ o, const float *__restrict__ dout, const float *__restrict__ lse2,
@@ -233,15 +258,16 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_q(
   __shared__ __attribute__((aligned(16))) float sm[2 * ATT_SMAX * DHP];
   __shared__ float smask[ATT_SMAX];
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int q0 = blockIdx.x * ATT_TILE;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int QPW = 64 / LPQ;
+  const int q0 = blockIdx.x * QPW;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane & (LPQ - 1);
   float *sK = sm, *sV = sm + ATT_SMAX * DHP;
   const long long kvoff = (long long)b * a.kv_sb + h * a.dh;
   stage_rows<DHP>(sK, k + kvoff, a.Sk, a.kv_ss, a.dh);
   stage_rows<DHP>(sV, v + kvoff, a.Sk, a.kv_ss, a.dh);
   for (int j = threadIdx.x; j < a.Sk; j += ATT_WAVES * 64)
     smask[j] = (kpad && kpad[(long long)b * a.Sk + j]) ? -INFINITY : 0.f;
-  const int i = q0 + lane, ic = min(i, a.Sq - 1);
+  const int i = q0 + lane / LPQ, ic = min(i, a.Sq - 1);
   float qr[DHP], dor[DHP];
   const float qmul = a.scale * LOG2E;
   const float *qrow = q + (long long)b * a.q_sb + h * a.dh + (long long)ic * a.q_ss;
@@ -263,18 +289,22 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_q(
 #pragma unroll
   for (int d = 0; d < DHP; ++d) acc[d] = 0.f;
   const uint32_t cbase = ((uint32_t)bh * a.Sq + i) * a.Sk;
-  for (int j = j0; j < j1; ++j) {
+  for (int j = j0 + sub; j < j1; j += LPQ) {
     const float s = dot_lds<DHP>(qr, sK + j * DHP) + smask[j];
     const float pj = (a.causal && j > i) ? 0.f : exp2f(s - li);
     const float dpd = dot_lds<DHP>(dor, sV + j * DHP);
     const float dp = (a.p > 0.f && !att_keep(sm_, cbase + j, a.p)) ? 0.f : dpd * rkeep;
     axpy_lds<DHP>(acc, pj * (dp - Di), sK + j * DHP);
   }
+  if (LPQ > 1) lane_sum<LPQ, DHP>(acc);
+  if (w == 0 && sub == 0 && i < a.Sq) Dbuf[(long long)bh * a.Sq + i] = Di;
   __syncthreads();
   constexpr int MS = DHP * 64;
-  float *mrg = sm;  // [w][DHP][64]
+  float *mrg = sm;  // [w][DHP][64], column = query within the block
+  if (sub == 0) {
 #pragma unroll
-  for (int d = 0; d < DHP; ++d) mrg[w * MS + d * 64 + lane] = acc[d];
+    for (int d = 0; d < DHP; ++d) mrg[w * MS + d * 64 + lane / LPQ] = acc[d];
+  }
   __syncthreads();
   constexpr int DPW = DHP / ATT_WAVES;
   float outv[DPW];
@@ -286,16 +316,15 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_q(
     for (int x = 0; x < ATT_WAVES; ++x) sacc += mrg[x * MS + d * 64 + lane];
     outv[t] = sacc * a.scale;
   }
-  if (w == 0 && i < a.Sq) Dbuf[(long long)bh * a.Sq + i] = Di;
   __syncthreads();
   float *tile = sm + ATT_WAVES * MS;
 #pragma unroll
   for (int t = 0; t < DPW; ++t) tile[lane * DHP + w * DPW + t] = outv[t];
   __syncthreads();
-  store_rows<DHP>(dq + (long long)b * a.q_sb + h * a.dh, tile, q0, a.Sq, a.q_ss, a.dh);
+  store_rows<DHP, QPW>(dq + (long long)b * a.q_sb + h * a.dh, tile, q0, a.Sq, a.q_ss, a.dh);
 }
 
-template <int DHP>
+template <int DHP, int LPK>
 __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
     const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
     const float *__restrict__ dout, const float *__restrict__ lse2, const float *__restrict__ Dbuf,
@@ -307,8 +336,9 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
   __shared__ __attribute__((aligned(16))) float sm[SMF];
   __shared__ float slse[ATT_SMAX], sD[ATT_SMAX];
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int k0 = blockIdx.x * ATT_TILE;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int KPW = 64 / LPK;  // keys per block; LPK lanes share a key's queries
+  const int k0 = blockIdx.x * KPW;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, sub = lane & (LPK - 1);
   float *sQ = sm, *sO = sm + ATT_SMAX * DHP;
   stage_rows<DHP>(sQ, q + (long long)b * a.q_sb + h * a.dh, a.Sq, a.q_ss, a.dh);
   stage_rows<DHP>(sO, dout + (long long)b * a.o_sb + h * a.dh, a.Sq, a.o_ss, a.dh);
@@ -316,7 +346,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
     slse[t] = lse2[(long long)bh * a.Sq + t];
     sD[t] = Dbuf[(long long)bh * a.Sq + t];
   }
-  const int j = k0 + lane, jc = min(j, a.Sk - 1);
+  const int j = k0 + lane / LPK, jc = min(j, a.Sk - 1);
   const bool kmasked = kpad && kpad[(long long)b * a.Sk + jc];
   const long long krow = (long long)b * a.kv_sb + h * a.dh + (long long)jc * a.kv_ss;
   float kr[DHP], vr[DHP], adk[DHP], adv[DHP];
@@ -333,7 +363,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
   const float rkeep = 1.f / (1.f - a.p);
   const int chunk = (a.Sq + ATT_WAVES - 1) / ATT_WAVES;
   const int i0 = w * chunk, i1 = min(a.Sq, i0 + chunk);
-  for (int i = i0; i < i1; ++i) {
+  for (int i = i0 + sub; i < i1; i += LPK) {
     const float s = dot_lds<DHP>(kr, sQ + i * DHP);
     const bool masked = kmasked || (a.causal && j > i);
     const float pj = masked ? 0.f : exp2f(s - slse[i]);
@@ -344,13 +374,20 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
     axpy_lds<DHP>(adv, pd, sO + i * DHP);
     axpy_lds<DHP>(adk, ds, sQ + i * DHP);
   }
+  if (LPK > 1) {
+    lane_sum<LPK, DHP>(adk);
+    lane_sum<LPK, DHP>(adv);
+  }
   __syncthreads();
   constexpr int MS = 2 * DHP * 64;
-  float *mrg = sm;  // [w][2*DHP][64]
+  float *mrg = sm;  // [w][2*DHP][64], column = key within the block
+  if (sub == 0) {
+    const int c = lane / LPK;
 #pragma unroll
-  for (int d = 0; d < DHP; ++d) {
-    mrg[w * MS + d * 64 + lane] = adk[d];
-    mrg[w * MS + (DHP + d) * 64 + lane] = adv[d];
+    for (int d = 0; d < DHP; ++d) {
+      mrg[w * MS + d * 64 + c] = adk[d];
+      mrg[w * MS + (DHP + d) * 64 + c] = adv[d];
+    }
   }
   __syncthreads();
   // wave w reduces columns [w*2*DHP/4, ...) of the 2*DHP (dk | dv) columns
@@ -369,7 +406,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
 #pragma unroll
   for (int t = 0; t < CPW; ++t) tile[lane * 2 * DHP + w * CPW + t] = outv[t];
   __syncthreads();
-  const int nr = min(ATT_TILE, a.Sk - k0);
+  const int nr = min(KPW, a.Sk - k0);
   const long long base = (long long)b * a.kv_sb + h * a.dh;
   for (int e = threadIdx.x; e < nr * a.dh; e += ATT_WAVES * 64) {
     const int r = e / a.dh, d = e - r * a.dh;
@@ -421,13 +458,18 @@ int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, 
   const AttnDims a = make_dims(B, H, Sq, Sk, dh, q_ss, q_sb, kv_ss, kv_sb, o_ss, o_sb, scale, causal, p);
   if (int rc = attn_check(a, "e2ep_attn_fwd")) return rc;
   E2EP_REQUIRE(p == 0.f || seed, E2EP_EINVAL, "e2ep_attn_fwd: dropout needs a seed");
-  const dim3 grid(cdiv(Sq, ATT_TILE), B * H);
-  if (dh <= 44)
-    hipLaunchKernelGGL(k_attn_fwd<44>, grid, dim3(ATT_WAVES * 64), 0, as_stream(stream), q, k, v,
-                       key_pad, seed, a, o, lse);
-  else
-    hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(ATT_WAVES * 64), 0, as_stream(stream), q, k, v,
-                       key_pad, seed, a, o, lse);
+  hipStream_t st = as_stream(stream);
+  const dim3 blk(ATT_WAVES * 64);
+  // short query sequences (the control decoder's 14 tokens): 4 lanes per query
+#define E2EP_ATT_FWD(DHP, LPQ)                                                                   \
+  hipLaunchKernelGGL((k_attn_fwd<DHP, LPQ>), dim3(cdiv(Sq, 64 / LPQ), B * H), blk, 0, st, q, k, v, \
+                     key_pad, seed, a, o, lse)
+  if (dh <= 44) {
+    if (Sq <= 16) E2EP_ATT_FWD(44, 4); else E2EP_ATT_FWD(44, 1);
+  } else {
+    if (Sq <= 16) E2EP_ATT_FWD(64, 4); else E2EP_ATT_FWD(64, 1);
+  }
+#undef E2EP_ATT_FWD
   return launch_status("e2ep_attn_fwd");
 }
 
@@ -443,14 +485,22 @@ int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o
   E2EP_REQUIRE(p == 0.f || seed, E2EP_EINVAL, "e2ep_attn_bwd: dropout needs a seed");
   float *D = static_cast<float *>(workspace);
   hipStream_t s = as_stream(stream);
-  const dim3 gq(cdiv(Sq, ATT_TILE), B * H), gk(cdiv(Sk, ATT_TILE), B * H), blk(ATT_WAVES * 64);
+  const dim3 blk(ATT_WAVES * 64);
+#define E2EP_ATT_BQ(DHP, LPQ)                                                                    \
+  hipLaunchKernelGGL((k_attn_bwd_q<DHP, LPQ>), dim3(cdiv(Sq, 64 / LPQ), B * H), blk, 0, s, q, k, v, \
+                     o, dout, lse, key_pad, seed, a, dq, D)
+#define E2EP_ATT_BKV(DHP, LPK)                                                                   \
+  hipLaunchKernelGGL((k_attn_bwd_kv<DHP, LPK>), dim3(cdiv(Sk, 64 / LPK), B * H), blk, 0, s, q, k, \
+                     v, dout, lse, D, key_pad, seed, a, dk, dv)
   if (dh <= 44) {
-    hipLaunchKernelGGL(k_attn_bwd_q<44>, gq, blk, 0, s, q, k, v, o, dout, lse, key_pad, seed, a, dq, D);
-    hipLaunchKernelGGL(k_attn_bwd_kv<44>, gk, blk, 0, s, q, k, v, dout, lse, D, key_pad, seed, a, dk, dv);
+    if (Sq <= 16) E2EP_ATT_BQ(44, 4); else E2EP_ATT_BQ(44, 1);
+    if (Sk <= 16) E2EP_ATT_BKV(44, 4); else E2EP_ATT_BKV(44, 1);
   } else {
-    hipLaunchKernelGGL(k_attn_bwd_q<64>, gq, blk, 0, s, q, k, v, o, dout, lse, key_pad, seed, a, dq, D);
-    hipLaunchKernelGGL(k_attn_bwd_kv<64>, gk, blk, 0, s, q, k, v, dout, lse, D, key_pad, seed, a, dk, dv);
+    if (Sq <= 16) E2EP_ATT_BQ(64, 4); else E2EP_ATT_BQ(64, 1);
+    if (Sk <= 16) E2EP_ATT_BKV(64, 4); else E2EP_ATT_BKV(64, 1);
   }
+#undef E2EP_ATT_BQ
+#undef E2EP_ATT_BKV
   return launch_status("e2ep_attn_bwd");
 }
 

@@ -33,19 +33,20 @@ def _grads(m, *xs):
                                    m.out_proj.weight.grad, m.out_proj.bias.grad]
 
 
-@pytest.mark.parametrize("case", ["enc_self", "dec_self", "dec_cross", "ragged"])
+@pytest.mark.parametrize("case", ["enc_self", "dec_self", "dec_cross", "ragged", "tiny_cross",
+                                  "dec_self_17"])
 def test_mha_matches_module(case):
     from e2ep_amd import attention
     g = torch.Generator().manual_seed(7)
     B = 8
     Sq, Sk = {"enc_self": (256, 256), "dec_self": (14, 14), "dec_cross": (14, 256),
-              "ragged": (77, 130)}[case]
+              "ragged": (77, 130), "tiny_cross": (5, 9), "dec_self_17": (17, 17)}[case]
     m = _module(len(case))
     m64 = _module(len(case)).double()
     x = torch.randn(Sq, B, E, generator=g)
     mem = torch.randn(Sk, B, E, generator=g)
     dy = torch.randn(Sq, B, E, generator=g)
-    causal = case == "dec_self"
+    causal = case.startswith("dec_self")
     kpm = None
     mask = None
     if causal:
@@ -53,7 +54,7 @@ def test_mha_matches_module(case):
         for b in range(B):
             kpm[b, Sk - b:] = True  # sample b has b PAD tokens at the end
         mask = torch.full((Sk, Sk), float("-inf")).triu(1)
-    self_attn = case in ("enc_self", "dec_self")
+    self_attn = case in ("enc_self", "dec_self", "dec_self_17")
     # reference (fp64, CPU)
     xr = x.double().requires_grad_(True)
     mr = xr if self_attn else mem.double().requires_grad_(True)
@@ -86,7 +87,8 @@ def _ref_core(q, k, v, keep, p, causal, kpm):
     return (P * keep / (1 - p)) @ v
 
 
-@pytest.mark.parametrize("Sq,Sk,causal", [(256, 256, False), (14, 14, True), (14, 256, False)])
+@pytest.mark.parametrize("Sq,Sk,causal", [(256, 256, False), (14, 14, True), (14, 256, False),
+                                                (16, 16, True), (17, 9, False)])
 def test_attention_dropout_matches_masked_reference(Sq, Sk, causal):
     from e2ep_amd import _lib, attention
     g = torch.Generator().manual_seed(11)
