@@ -34,6 +34,13 @@ namespace e2ep {
 constexpr int ATT_SMAX = 256;  // max Sq / Sk (one head's K, V staged whole)
 constexpr int ATT_WAVES = 4;
 constexpr float LOG2E = 1.4426950408889634f;
+#ifndef E2EP_ATT_KG
+#define E2EP_ATT_KG 4
+#endif
+constexpr int FWD_KG = E2EP_ATT_KG;  // keys per online-softmax rescale in the forward
+
+// 2^x on the hardware v_exp_f32 (arguments here are <= 0 or -inf; tiny results flush to 0)
+__device__ __forceinline__ float att_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ uint32_t att_mix(uint32_t x) {  // 32-bit integer finaliser
   x ^= x >> 16;
@@ -166,11 +173,11 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
 #pragma unroll
   for (int d = 0; d < DHP; ++d) acc[d] = 0.f;
   const uint32_t cbase = ((uint32_t)bh * a.Sq + i) * a.Sk;
-  for (int jb = j0 + sub; jb < j1; jb += 8 * LPQ) {
-    float s[8];
+  for (int jb = j0 + sub; jb < j1; jb += FWD_KG * LPQ) {
+    float s[FWD_KG];
     float bm = -INFINITY;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < FWD_KG; ++u) {
       const int j = jb + u * LPQ;
       const int jl = min(j, j1 - 1);
       const float x = dot_lds<DHP>(qr, sK + jl * DHP) + smask[jl];
@@ -179,14 +186,14 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
     }
     const float mn = fmaxf(m, bm);
     const float ms = mn == -INFINITY ? 0.f : mn;
-    const float corr = exp2f(m - ms);
+    const float corr = att_exp2(m - ms);
     m = mn;
     l *= corr;
 #pragma unroll
     for (int d = 0; d < DHP; ++d) acc[d] *= corr;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float pu = exp2f(s[u] - ms);
+    for (int u = 0; u < FWD_KG; ++u) {
+      const float pu = att_exp2(s[u] - ms);
       l += pu;
       const int j = min(jb + u * LPQ, j1 - 1);
       const float pd = (a.p > 0.f && !att_keep(sm_, cbase + j, a.p)) ? 0.f : pu;
@@ -199,7 +206,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
       const float mo = __shfl_xor(m, off, 64);
       const float mn = fmaxf(m, mo);
       const float ms = mn == -INFINITY ? 0.f : mn;
-      const float fs = exp2f(m - ms), fo = exp2f(mo - ms);
+      const float fs = att_exp2(m - ms), fo = att_exp2(mo - ms);
       l = l * fs + __shfl_xor(l, off, 64) * fo;
 #pragma unroll
       for (int d = 0; d < DHP; ++d) acc[d] = acc[d] * fs + __shfl_xor(acc[d], off, 64) * fo;
@@ -225,7 +232,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_fwd(
   float L = 0.f, f[ATT_WAVES];
 #pragma unroll
   for (int x = 0; x < ATT_WAVES; ++x) {
-    f[x] = exp2f(mrg[x * MS + lane] - Ms);
+    f[x] = att_exp2(mrg[x * MS + lane] - Ms);
     L = __builtin_fmaf(mrg[x * MS + 64 + lane], f[x], L);
   }
   const float rinv = L > 0.f ? 1.f / (L * (1.f - a.p)) : 0.f;
@@ -291,7 +298,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_q(
   const uint32_t cbase = ((uint32_t)bh * a.Sq + i) * a.Sk;
   for (int j = j0 + sub; j < j1; j += LPQ) {
     const float s = dot_lds<DHP>(qr, sK + j * DHP) + smask[j];
-    const float pj = (a.causal && j > i) ? 0.f : exp2f(s - li);
+    const float pj = (a.causal && j > i) ? 0.f : att_exp2(s - li);
     const float dpd = dot_lds<DHP>(dor, sV + j * DHP);
     const float dp = (a.p > 0.f && !att_keep(sm_, cbase + j, a.p)) ? 0.f : dpd * rkeep;
     axpy_lds<DHP>(acc, pj * (dp - Di), sK + j * DHP);
@@ -366,7 +373,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_kv(
   for (int i = i0 + sub; i < i1; i += LPK) {
     const float s = dot_lds<DHP>(kr, sQ + i * DHP);
     const bool masked = kmasked || (a.causal && j > i);
-    const float pj = masked ? 0.f : exp2f(s - slse[i]);
+    const float pj = masked ? 0.f : att_exp2(s - slse[i]);
     const bool keep = !(a.p > 0.f) || att_keep(sm_, ((uint32_t)bh * a.Sq + i) * a.Sk + j, a.p);
     const float pd = keep ? pj * rkeep : 0.f;
     const float dpd = dot_lds<DHP>(vr, sO + i * DHP);
