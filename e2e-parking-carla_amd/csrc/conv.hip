@@ -605,6 +605,49 @@ __global__ void __launch_bounds__(1024) k_reduce_splits(const float *__restrict_
 }
 
 // per-channel bias gradient: db[c] = sum over (n, p) of g[n, c, p]  (one block per channel)
+// Column sums of a row-major [rows][C] matrix (Linear bias gradients, reference
+// torch.nn.Linear backward inside the transformer layers): stage 1, block = 64 columns x 4
+// row lanes over one row chunk, coalesced 256-B row reads, fixed-order LDS reduction into
+// partial[chunk][C]; stage 2 sums the chunks in order.  Deterministic.
+constexpr int COLSUM_ROWS = 128;  // rows per chunk
+__global__ void __launch_bounds__(256) k_col_sum_partial(const float *__restrict__ g, int rows,
+                                                         int C, float *__restrict__ part) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * COLSUM_ROWS, r1 = min(rows, r0 + COLSUM_ROWS);
+  float s = 0.f;
+  if (c < C) {
+    float t[COLSUM_ROWS / 4];
+#pragma unroll
+    for (int u = 0; u < COLSUM_ROWS / 4; ++u) {
+      const int r = r0 + ty + 4 * u;
+      t[u] = r < r1 ? g[(long long)r * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < COLSUM_ROWS / 4; ++u) s += t[u];
+  }
+  __shared__ float red[4][64];
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C)
+    part[(long long)blockIdx.y * C + c] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+}
+
+__global__ void k_col_sum_final(const float *__restrict__ part, int chunks, int C,
+                                float *__restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k0 = 0; k0 < chunks; k0 += 16) {  // 16 independent loads in flight, summed in order
+    float t[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) t[u] = k0 + u < chunks ? part[(long long)(k0 + u) * C + c] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += t[u];
+  }
+  out[c] = s;
+}
+
 __global__ void __launch_bounds__(1024) k_bias_grad(const float *__restrict__ g, int N, int C,
                                                     int HW, float *__restrict__ db) {
   // one workgroup per channel; its N rows of HW are walked as one sequence (float4 when
@@ -977,6 +1020,21 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
   hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
                      accumulate);
   return launch_status("e2ep_conv_wgrad");
+}
+
+size_t e2ep_col_sum_workspace(int rows, int C) {
+  return (size_t)cdiv(rows, COLSUM_ROWS) * C * sizeof(float);
+}
+
+int e2ep_col_sum(const float *g, int rows, int C, float *out, void *workspace, void *stream) {
+  E2EP_REQUIRE(rows > 0 && C > 0 && workspace, E2EP_EINVAL, "e2ep_col_sum: bad args");
+  const int chunks = cdiv(rows, COLSUM_ROWS);
+  float *part = static_cast<float *>(workspace);
+  hipLaunchKernelGGL(k_col_sum_partial, dim3(cdiv(C, 64), chunks), dim3(256), 0,
+                     as_stream(stream), g, rows, C, part);
+  hipLaunchKernelGGL(k_col_sum_final, dim3(cdiv(C, 256)), dim3(256), 0, as_stream(stream), part,
+                     chunks, C, out);
+  return launch_status("e2ep_col_sum");
 }
 
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream) {

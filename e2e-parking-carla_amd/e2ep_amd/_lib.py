@@ -38,6 +38,8 @@ SIGNATURES = {
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),
     "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _p, _i, _p]),
     "e2ep_bias_grad": (_i, [_p, _i, _i, _i, _p, _p]),
+    "e2ep_col_sum_workspace": (_sz, [_i, _i]),
+    "e2ep_col_sum": (_i, [_p, _i, _i, _p, _p, _p]),
     "e2ep_skinny_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _i, _i, _i, _p, _p]),
     "e2ep_bn_workspace": (_sz, [_i, _i, _i, _i]),
     "e2ep_bn_fwd": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i, _p, _p, _p, _p, _p]),
@@ -63,7 +65,7 @@ SIGNATURES = {
     "e2ep_attn_bwd_workspace": (_sz, [_i, _i, _i]),
     "e2ep_attn_bwd": (_i, [_p] * 6 + [_i] * 11 + [_f, _i, _p, _f, _p, _p, _p, _p, _p, _p]),
     "e2ep_attn_keep_mask": (_i, [_p, _i, _i, _i, _f, _p, _p]),
-    "e2ep_se_fwd":(_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "e2ep_se_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
     "e2ep_se_gate_fwd": (_i, [_p, _p, _i, _i, _p, _p]),
     "e2ep_se_gate_bwd": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),

@@ -16,9 +16,8 @@ add_zero_attn, separate projection weights, or shapes outside the kernel's range
 import math
 
 import torch
-import torch.nn.functional as F
 
-from . import _lib, timing
+from . import _lib, nn_ops, timing
 
 MAX_SEQ = 256
 MAX_HEAD_DIM = 64
@@ -114,13 +113,13 @@ def mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, is_causal
     W, bias = mod.in_proj_weight, mod.in_proj_bias
     p = mod.dropout if mod.training else 0.0
     if query is key and key is value:
-        qkv = F.linear(query, W, bias)
+        qkv = nn_ops.linear(query, W, bias)
         o = attention(qkv, None, H, is_causal, key_padding_mask, p)
     else:
         if key is not value:
             return mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
                        need_weights=False)[0]
-        q = F.linear(query, W[:E], None if bias is None else bias[:E])
-        kv = F.linear(key, W[E:], None if bias is None else bias[E:])
+        q = nn_ops.linear(query, W[:E], None if bias is None else bias[:E])
+        kv = nn_ops.linear(key, W[E:], None if bias is None else bias[E:])
         o = attention(q, kv, H, is_causal, key_padding_mask, p)
-    return F.linear(o, mod.out_proj.weight, mod.out_proj.bias)
+    return nn_ops.linear(o, mod.out_proj.weight, mod.out_proj.bias)

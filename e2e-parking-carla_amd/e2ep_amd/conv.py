@@ -73,9 +73,11 @@ class _Conv2d(torch.autograd.Function):
         dims = ctx.dims
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
         gy = gy.contiguous()
-        if ctx.act == 1:
-            gy = torch.where(y > 0, gy, torch.zeros((), device=gy.device))
         s = _lib.stream()
+        if ctx.act == 1:  # ReLU gradient mask (y > 0 <=> pre-activation > 0), one e2ep launch
+            gm = torch.empty_like(gy)
+            _lib.call("e2ep_act_bwd", _lib.ptr(y), _lib.ptr(gy), gy.numel(), 1, _lib.ptr(gm), s)
+            gy = gm
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             gc = ctx.gc or Cin

@@ -2,6 +2,7 @@
 resize.hip, dwconv.hip, pool.hip).  Each forward enqueues on torch's current HIP stream;
 each backward is the matching e2ep gradient kernel (no PyTorch arithmetic)."""
 import torch
+import torch.nn.functional as F
 
 from . import _lib, timing
 
@@ -585,3 +586,44 @@ def add_drop_layer_norm(a, b, norm, p=0.0):
     _dev(a, b)
     u = torch.rand_like(b) if p > 0.0 else None
     return _AddDropLN.apply(a, b, norm.weight, norm.bias, u, p, norm.eps)
+
+
+# ------------------------------------------------------------------------------------------
+# nn.Linear with the bias gradient on e2ep_col_sum
+# ------------------------------------------------------------------------------------------
+class _Linear(torch.autograd.Function):
+    """y = x W^T + b.  Forward and the two backward GEMMs stay hipBLASLt (torch.mm); the bias
+    gradient (a column sum over all rows, which torch runs as a 3-8 workgroup reduction for
+    the transformer's 2048 x 258 gradients) is e2ep_col_sum."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        nig = ctx.needs_input_grad
+        g2 = gy.reshape(-1, gy.shape[-1])
+        dx = dw = db = None
+        if nig[0]:
+            dx = (g2 @ weight).view(x.shape)
+        if nig[1]:
+            dw = g2.t() @ x.reshape(-1, x.shape[-1])
+        if ctx.has_bias and nig[2]:
+            g2 = g2.contiguous()
+            rows, C = g2.shape
+            db = torch.empty(C, dtype=torch.float32, device=gy.device)
+            ws = _ws(_lib.load().e2ep_col_sum_workspace(rows, C), gy.device)
+            _lib.call("e2ep_col_sum", _lib.ptr(g2), rows, C, _lib.ptr(db), _lib.ptr(ws), _lib.stream())
+        return dx, dw, db
+
+
+def linear(x, weight, bias=None):
+    """F.linear(x, weight, bias) with an e2ep bias gradient (fp32 HIP tensors); other inputs
+    (CPU, other dtypes) go to F.linear itself."""
+    if not x.is_cuda or x.dtype != torch.float32 or (bias is None or not bias.requires_grad):
+        return F.linear(x, weight, bias)
+    return _Linear.apply(x, weight, bias)

@@ -9,7 +9,6 @@ dropout + add + layer_norm (+ its slow gamma/beta backward).  The attention core
 softmax, dropout, PV and their backward) runs as e2ep kernels through attention.mha, which
 keeps the modules' own in/out projections (hipBLASLt GEMMs) and falls back to the module when
 a hook is installed (the agent's attention capture)."""
-import torch.nn.functional as F
 
 from . import attention, nn_ops
 
@@ -19,7 +18,8 @@ def _p(drop, training):
 
 
 def _ff(layer, x):
-    return layer.linear2(layer.dropout(layer.activation(layer.linear1(x))))
+    h = layer.activation(nn_ops.linear(x, layer.linear1.weight, layer.linear1.bias))
+    return nn_ops.linear(layer.dropout(h), layer.linear2.weight, layer.linear2.bias)
 
 
 def encoder_layer(layer, x, mask=None, key_padding_mask=None):

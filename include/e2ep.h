@@ -159,6 +159,11 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
 /* db[C] = sum over (n, p) of gout[N, C, HW]. */
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream);
 
+/* out[C] = column sums of the row-major g[rows][C] (nn.Linear bias gradient), deterministic
+ * two-stage reduction; workspace e2ep_col_sum_workspace bytes. */
+size_t e2ep_col_sum_workspace(int rows, int C);
+int e2ep_col_sum(const float *g, int rows, int C, float *out, void *workspace, void *stream);
+
 /* Skinny GEMM for tiny outputs: C[i*Nj + j] = sum_k A[i*ai + k*ak] * B[k*bk + j*bj]
  * (+ bias[j]); one wave per output.  1x1 convs on 1x1 maps (squeeze-excitation) and small
  * linears, forward and backward, via strides. */

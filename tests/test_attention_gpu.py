@@ -167,3 +167,22 @@ def test_graph_replay_draws_new_masks():
     a = out.clone()
     gr.replay()
     assert not torch.equal(a, out)
+
+
+@pytest.mark.parametrize("rows,cin,cout", [(2048, 258, 2048), (2048, 2048, 258), (112, 258, 774),
+                                           (3, 5, 7), (1000, 64, 130)])
+def test_linear_bias_grad(rows, cin, cout):
+    """nn_ops.linear (e2ep_col_sum bias gradient) vs F.linear in fp64."""
+    from e2ep_amd import nn_ops
+    g = torch.Generator().manual_seed(rows + cout)
+    x = torch.randn(rows, cin, generator=g)
+    w = torch.randn(cout, cin, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g)
+    dy = torch.randn(rows, cout, generator=g)
+    ref = [t.double().requires_grad_(True) for t in (x, w, b)]
+    (torch.nn.functional.linear(*ref) * dy.double()).sum().backward()
+    dev = [t.to(DEV).requires_grad_(True) for t in (x, w, b)]
+    y = nn_ops.linear(*dev)
+    (y * dy.to(DEV)).sum().backward()
+    for a, r in zip(dev, ref):
+        assert rel_l2(a.grad.cpu(), r.grad) < 1e-5
