@@ -452,6 +452,57 @@ static AttnDims make_dims(int B, int H, int Sq, int Sk, int dh, int q_ss, int q_
   return a;
 }
 
+// ------------------------------------------------------------------------------------------
+// Feed-forward activation of the transformer layers: dropout_p(relu(x)) and its backward
+// (reference: linear1 -> relu -> dropout inside TransformerEncoderLayer/DecoderLayer._ff_block,
+// model/feature_fusion.py:13-14, model/control_predict.py:19-20).  One launch each way instead
+// of clamp + RNG fill + dropout (fwd) and dropout-mask scale + threshold (bwd).  The keep bit
+// of element c is att_keep(seed, c): the same hash as the attention dropout, regenerated in
+// the backward.  float4 per thread.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_relu_drop_fwd(const float4 *__restrict__ x, long long n4,
+                                                       float p, const int *__restrict__ seed,
+                                                       float4 *__restrict__ y) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const uint32_t sm_ = att_seedmix(seed);
+  const float sc = 1.f / (1.f - p);
+  const float4 v = x[i];
+  const uint32_t c = (uint32_t)(4 * i);
+  float4 o;
+  o.x = (p > 0.f && !att_keep(sm_, c, p)) ? 0.f : fmaxf(v.x, 0.f) * sc;
+  o.y = (p > 0.f && !att_keep(sm_, c + 1, p)) ? 0.f : fmaxf(v.y, 0.f) * sc;
+  o.z = (p > 0.f && !att_keep(sm_, c + 2, p)) ? 0.f : fmaxf(v.z, 0.f) * sc;
+  o.w = (p > 0.f && !att_keep(sm_, c + 3, p)) ? 0.f : fmaxf(v.w, 0.f) * sc;
+  y[i] = o;
+}
+
+__global__ void __launch_bounds__(256) k_relu_drop_bwd(const float4 *__restrict__ x,
+                                                       const float4 *__restrict__ dy, long long n4,
+                                                       float p, const int *__restrict__ seed,
+                                                       float4 *__restrict__ dx) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const uint32_t sm_ = att_seedmix(seed);
+  const float sc = 1.f / (1.f - p);
+  const float4 v = x[i], g = dy[i];
+  const uint32_t c = (uint32_t)(4 * i);
+  float4 o;
+  o.x = (v.x > 0.f && !(p > 0.f && !att_keep(sm_, c, p))) ? g.x * sc : 0.f;
+  o.y = (v.y > 0.f && !(p > 0.f && !att_keep(sm_, c + 1, p))) ? g.y * sc : 0.f;
+  o.z = (v.z > 0.f && !(p > 0.f && !att_keep(sm_, c + 2, p))) ? g.z * sc : 0.f;
+  o.w = (v.w > 0.f && !(p > 0.f && !att_keep(sm_, c + 3, p))) ? g.w * sc : 0.f;
+  dx[i] = o;
+}
+
+static int relu_drop_check(const void *x, long long n, float p, const int32_t *seed, const char *who) {
+  E2EP_REQUIRE(n > 0 && n % 4 == 0 && n < 0xffffffffLL, E2EP_EINVAL,
+               "%s: n = %lld must be a positive multiple of 4 below 2^32", who, n);
+  E2EP_REQUIRE(((uintptr_t)x & 15) == 0, E2EP_EINVAL, "%s: tensors must be 16-B aligned", who);
+  E2EP_REQUIRE(p >= 0.f && p < 1.f && (p == 0.f || seed), E2EP_EINVAL, "%s: bad dropout p / seed", who);
+  return 0;
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -518,6 +569,27 @@ int e2ep_attn_keep_mask(const int32_t *seed, int BH, int Sq, int Sk, float p, ui
   hipLaunchKernelGGL(k_attn_keep_mask, dim3(min(cdiv(n, 256), 4096)), dim3(256), 0, as_stream(stream),
                      seed, BH, Sq, Sk, p, out);
   return launch_status("e2ep_attn_keep_mask");
+}
+
+int e2ep_relu_dropout_fwd(const float *x, long long n, float p, const int32_t *seed, float *y,
+                          void *stream) {
+  if (int rc = relu_drop_check(x, n, p, seed, "e2ep_relu_dropout_fwd")) return rc;
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_relu_drop_fwd, dim3(cdiv(n4, 256)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4 *>(x), n4, p, seed, reinterpret_cast<float4 *>(y));
+  return launch_status("e2ep_relu_dropout_fwd");
+}
+
+int e2ep_relu_dropout_bwd(const float *x, const float *dy, long long n, float p,
+                          const int32_t *seed, float *dx, void *stream) {
+  if (int rc = relu_drop_check(x, n, p, seed, "e2ep_relu_dropout_bwd")) return rc;
+  E2EP_REQUIRE((((uintptr_t)dy | (uintptr_t)dx) & 15) == 0, E2EP_EINVAL,
+               "e2ep_relu_dropout_bwd: tensors must be 16-B aligned");
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(k_relu_drop_bwd, dim3(cdiv(n4, 256)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4 *>(x), reinterpret_cast<const float4 *>(dy), n4, p,
+                     seed, reinterpret_cast<float4 *>(dx));
+  return launch_status("e2ep_relu_dropout_bwd");
 }
 
 }  // extern "C"

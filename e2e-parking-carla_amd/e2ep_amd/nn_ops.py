@@ -627,3 +627,37 @@ def linear(x, weight, bias=None):
     if not x.is_cuda or x.dtype != torch.float32 or (bias is None or not bias.requires_grad):
         return F.linear(x, weight, bias)
     return _Linear.apply(x, weight, bias)
+
+
+# ------------------------------------------------------------------------------------------
+# transformer feed-forward activation: dropout_p(relu(x))
+# ------------------------------------------------------------------------------------------
+class _ReluDropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        y = torch.empty_like(x)
+        _lib.call("e2ep_relu_dropout_fwd", _lib.ptr(x), x.numel(), float(p), _lib.ptr(seed),
+                  _lib.ptr(y), _lib.stream())
+        ctx.save_for_backward(x, seed)
+        ctx.p = float(p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, seed = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        _lib.call("e2ep_relu_dropout_bwd", _lib.ptr(x), _lib.ptr(dy), x.numel(), ctx.p,
+                  _lib.ptr(seed), _lib.ptr(dx), _lib.stream())
+        return dx, None, None
+
+
+def relu_dropout(x, p=0.0, seed=None):
+    """dropout_p(relu(x)) as one e2ep launch each way (fp32 HIP tensor, numel % 4 == 0).
+    The mask is a hash of a per-call device seed (drawn here when p > 0 and none is given:
+    graph-capturable) and the element index."""
+    _dev(x)
+    x = x.contiguous()
+    if p > 0.0 and seed is None:
+        seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=x.device)
+    return _ReluDropout.apply(x, float(p), seed)

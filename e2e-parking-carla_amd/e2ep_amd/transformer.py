@@ -10,6 +10,9 @@ softmax, dropout, PV and their backward) runs as e2ep kernels through attention.
 keeps the modules' own in/out projections (hipBLASLt GEMMs) and falls back to the module when
 a hook is installed (the agent's attention capture)."""
 
+import torch
+import torch.nn.functional as F
+
 from . import attention, nn_ops
 
 
@@ -18,8 +21,12 @@ def _p(drop, training):
 
 
 def _ff(layer, x):
-    h = layer.activation(nn_ops.linear(x, layer.linear1.weight, layer.linear1.bias))
-    return nn_ops.linear(layer.dropout(h), layer.linear2.weight, layer.linear2.bias)
+    h = nn_ops.linear(x, layer.linear1.weight, layer.linear1.bias)
+    if layer.activation is F.relu and h.is_cuda and h.dtype == torch.float32 and h.numel() % 4 == 0:
+        h = nn_ops.relu_dropout(h, _p(layer.dropout, layer.training))  # one launch each way
+    else:
+        h = layer.dropout(layer.activation(h))
+    return nn_ops.linear(h, layer.linear2.weight, layer.linear2.bias)
 
 
 def encoder_layer(layer, x, mask=None, key_padding_mask=None):

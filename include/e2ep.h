@@ -279,6 +279,13 @@ int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o
                   float *dv, void *workspace, void *stream);
 int e2ep_attn_keep_mask(const int32_t *seed, int BH, int Sq, int Sk, float p, uint8_t *out,
                         void *stream);
+/* Transformer feed-forward activation y = dropout_p(relu(x)) over n floats (n % 4 == 0,
+ * 16-B aligned), and dx = dy * relu'(x) * keep / (1-p).  Keep bit of element c = the
+ * attention hash of (*seed, c) (e2ep_attn_keep_mask with BH = Sq = 1, Sk = n shows it). */
+int e2ep_relu_dropout_fwd(const float *x, long long n, float p, const int32_t *seed, float *y,
+                          void *stream);
+int e2ep_relu_dropout_bwd(const float *x, const float *dy, long long n, float p,
+                          const int32_t *seed, float *dx, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Bilinear resize, align_corners=False (F.interpolate / nn.Upsample semantics) over

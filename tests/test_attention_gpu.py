@@ -186,3 +186,28 @@ def test_linear_bias_grad(rows, cin, cout):
     (y * dy.to(DEV)).sum().backward()
     for a, r in zip(dev, ref):
         assert rel_l2(a.grad.cpu(), r.grad) < 1e-5
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_relu_dropout_matches_masked_reference(p):
+    """Feed-forward dropout(relu(x)) vs fp64 with the kernel's own keep mask (same hash as the
+    attention dropout: counters 0..n-1)."""
+    from e2ep_amd import _lib, nn_ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2048, 2048, generator=g)
+    dy = torch.randn(2048, 2048, generator=g)
+    seed = torch.tensor([777], dtype=torch.int32, device=DEV)
+    n = x.numel()
+    keep = torch.empty(n, dtype=torch.uint8, device=DEV)
+    _lib.call("e2ep_attn_keep_mask", _lib.ptr(seed), 1, 1, n, p, _lib.ptr(keep), _lib.stream())
+    keep = keep.cpu().double().view_as(x)
+    if p > 0:
+        assert abs(float(keep.mean()) - (1 - p)) < 0.002
+    xd = x.to(DEV).requires_grad_(True)
+    y = nn_ops.relu_dropout(xd, p, seed if p > 0 else None)
+    (y * dy.to(DEV)).sum().backward()
+    xr = x.double().requires_grad_(True)
+    yr = torch.relu(xr) * keep / (1 - p)
+    (yr * dy.double()).sum().backward()
+    assert rel_l2(y.detach().cpu(), yr) < 1e-6
+    assert rel_l2(xd.grad.cpu(), xr.grad) < 1e-6
