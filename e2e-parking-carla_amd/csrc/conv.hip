@@ -268,6 +268,9 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   // splits == 1: final values (bias, act) into dst[img][m][pixel];
   // splits > 1:  raw partial sums into dst = part[split][m][n] (reduced by k_conv_reduce).
   const __amdgpu_buffer_rsrc_t rd = rsrc(dst, dst_bytes);
+  // MODE 1: `bias` is an optional residual gradient in dst's layout, added to dx here (the
+  // skip connection's gradient, so autograd needs no separate accumulation kernel)
+  const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes : 0);
   const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
   const int HWd = Hd * Wd;
 #pragma unroll
@@ -293,11 +296,16 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
       float v = acc[t][r];
+      const int off = (nok && m < M) ? (dbase + m * mstride) * 4 : OOR;
       if (splits == 1) {
-        if (bias) v += bias[min(m, M - 1)];
-        if (ACT == 1) v = fmaxf(v, 0.f);
+        if (MODE == 0) {
+          if (bias) v += bias[min(m, M - 1)];
+          if (ACT == 1) v = fmaxf(v, 0.f);
+        } else if (bias) {
+          v += bload(rres, off);
+        }
       }
-      bstore(rd, (nok && m < M) ? (dbase + m * mstride) * 4 : OOR, v);
+      bstore(rd, off, v);
     }
   }
 }
@@ -305,7 +313,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
 // split-K reduction (fixed order) + bias / relu epilogue:
 // out[img][m][p] = act(sum_s part[s][m][img*HW + p] + bias[m])
 __global__ void k_conv_reduce(const float *__restrict__ part, int splits, int M, int HW, int Ntot,
-                              const float *__restrict__ bias, int act, float *__restrict__ out) {
+                              const float *__restrict__ bias, int act,
+                              const float *__restrict__ res, float *__restrict__ out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= Ntot) return;
   const int m = blockIdx.y;
@@ -314,7 +323,9 @@ __global__ void k_conv_reduce(const float *__restrict__ part, int splits, int M,
   if (bias) s += bias[m];
   if (act == 1) s = fmaxf(s, 0.f);
   const int im = n / HW, p = n - im * HW;
-  out[((size_t)im * M + m) * HW + p] = s;
+  const size_t o = ((size_t)im * M + m) * HW + p;
+  if (res) s += res[o];
+  out[o] = s;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -914,8 +925,8 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
   if (p.splits > 1) {
     const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
     hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
-                       static_cast<const float *>(workspace), p.splits, M, HW, (int)p.ncols, bias,
-                       act, dst);
+                       static_cast<const float *>(workspace), p.splits, M, HW, (int)p.ncols,
+                       mode == 0 ? bias : nullptr, act, mode == 1 ? bias : nullptr, dst);
   }
   return 0;
 }
@@ -951,18 +962,23 @@ int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *
   return launch_status("e2ep_conv_fwd");
 }
 
-int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
-                    int w_layout, float *dx, void *workspace, void *stream) {
+int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int m_channels,
+                        int w_layout, const float *res, float *dx, void *workspace, void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(w_layout == 0 || w_layout == 1, E2EP_EINVAL, "e2ep_conv_dgrad: w_layout must be 0 or 1");
   g.wlayout = w_layout;
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_dgrad: bad geometry");
   E2EP_REQUIRE(m_channels > 0 && m_channels <= g.Cin, E2EP_EINVAL,
                "e2ep_conv_dgrad: m_channels must be in [1, Cin]");
-  const int rc = launch_gemm(1, 0, w, gout, nullptr, dx, 4LL * g.N * m_channels * g.H * g.W, g,
+  const int rc = launch_gemm(1, 0, w, gout, res, dx, 4LL * g.N * m_channels * g.H * g.W, g,
                              m_channels, workspace, as_stream(stream));
   if (rc) return rc;
   return launch_status("e2ep_conv_dgrad");
+}
+
+int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
+                    int w_layout, float *dx, void *workspace, void *stream) {
+  return e2ep_conv_dgrad_acc(gout, w, dims, m_channels, w_layout, nullptr, dx, workspace, stream);
 }
 
 int e2ep_conv_wgrad_splits(const int *dims) {

@@ -35,12 +35,13 @@ def conv_fwd(x, w, b, dims, act, y, w_layout=0):
     return y
 
 
-def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0):
+def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0, res=None):
+    """dx = data gradient (+ res, a residual gradient in dx's layout, added in the epilogue)."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_dgrad_workspace(d, m_channels), gy.device)
     with timing.region("conv_dgrad"):
-        _lib.call("e2ep_conv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, m_channels, w_layout,
-                  _lib.ptr(dx), _lib.ptr(ws), _lib.stream())
+        _lib.call("e2ep_conv_dgrad_acc", _lib.ptr(gy), _lib.ptr(w), d, m_channels, w_layout,
+                  _lib.ptr(res), _lib.ptr(dx), _lib.ptr(ws), _lib.stream())
     return dx
 
 
@@ -56,7 +57,7 @@ def conv_wgrad(gy, x, dims, dw):
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, dims, act, grad_channels):
+    def forward(ctx, x, w, b, dims, act, grad_channels, skip=False):
         x = x.contiguous()
         wt = tap_major(w)  # one small transpose per step for R*S > 1; shared with dgrad
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
@@ -65,10 +66,13 @@ class _Conv2d(torch.autograd.Function):
         ctx.dims, ctx.act, ctx.has_bias, ctx.gc = dims, act, b is not None, grad_channels
         ctx.save_for_backward(x, wt, y if act else None)
         ctx.wshape = w.shape
-        return y
+        ctx.skip = skip
+        # skip: also hand x back, so the block's skip connection reads it from here and its
+        # gradient arrives in this backward, where the data-gradient epilogue adds it
+        return (y, x) if skip else y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, gskip=None):
         x, wt, y = ctx.saved_tensors
         dims = ctx.dims
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
@@ -81,10 +85,14 @@ class _Conv2d(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             gc = ctx.gc or Cin
+            res = gskip.contiguous() if (gskip is not None and gc == Cin) else None
             dxg = conv_dgrad(gy, wt, dims, gc, torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device),
-                             w_layout=1)
+                             w_layout=1, res=res)
             if gc == Cin:
                 dx = dxg
+            elif gskip is not None:  # channels past gc get only the skip gradient
+                dx = gskip.clone()
+                dx[:, :gc] += dxg
             else:
                 dx = torch.zeros_like(x)
                 dx[:, :gc] = dxg
@@ -93,7 +101,9 @@ class _Conv2d(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = torch.empty(Cout, dtype=torch.float32, device=x.device)
             _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db), s)
-        return dx, dw, db, None, None, None
+        if dx is None and gskip is not None and ctx.needs_input_grad[0]:
+            dx = gskip
+        return dx, dw, db, None, None, None, None
 
 
 def _skinny(A, ai, ak, B, bk, bj, bias, Mi, Nj, K, out):
@@ -136,8 +146,11 @@ class _Linear1x1(torch.autograd.Function):
         return dx, dw, db
 
 
-def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0, grad_channels=None):
-    """pad = (left, right, top, bottom); act 0 none, 1 relu (fused epilogue)."""
+def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0, grad_channels=None,
+           skip=False):
+    """pad = (left, right, top, bottom); act 0 none, 1 relu (fused epilogue).
+    skip=True returns (y, x_skip): use x_skip for the block's skip connection and its gradient
+    is added to this conv's input gradient inside the data-gradient kernel."""
     if not x.is_cuda:
         raise _lib.E2EPError("e2ep conv2d runs on a HIP device only")
     N, Cin, H, W = x.shape
@@ -145,11 +158,12 @@ def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0
     if cin_w != Cin:
         raise _lib.E2EPError(f"e2ep conv2d: groups must be 1 (w {tuple(w.shape)}, x {tuple(x.shape)})")
     if H == 1 and W == 1 and R == 1 and S == 1 and act == 0 and not any(pad) and grad_channels is None:
-        return _Linear1x1.apply(x, w, b)
+        y = _Linear1x1.apply(x, w, b)
+        return (y, x) if skip else y
     sh, sw = stride
     dh, dw = dilation
     l, r, t, btm = pad
     P = (H + t + btm - dh * (R - 1) - 1) // sh + 1
     Q = (W + l + r - dw * (S - 1) - 1) // sw + 1
     dims = (N, Cin, H, W, Cout, R, S, P, Q, sh, sw, t, l, dh, dw)
-    return _Conv2d.apply(x, w, b, dims, act, grad_channels)
+    return _Conv2d.apply(x, w, b, dims, act, grad_channels, bool(skip))

@@ -22,14 +22,16 @@ def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None):
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, act=None, skip=False):
     """NCHW convolution; padding is an int, (ph, pw) or (left, right, top, bottom).
     groups == channels (depthwise) goes to the depthwise kernels, groups == 1 to the
-    implicit-GEMM MFMA kernels; act None | 'relu' is fused into the GEMM epilogue."""
+    implicit-GEMM MFMA kernels; act None | 'relu' is fused into the GEMM epilogue.
+    skip=True (groups == 1): returns (y, x_skip), see e2ep_amd.conv.conv2d."""
     pad = _pad4(padding)
     if groups == 1:
         return _conv.conv2d(x, weight, bias, _pair(stride), pad, _pair(dilation),
-                            nn_ops.ACT[act])
+                            nn_ops.ACT[act], skip=skip)
+    assert not skip, "skip passthrough is for groups == 1 convs"
     if groups == x.shape[1] and weight.shape[0] == groups and weight.shape[1] == 1 and bias is None \
             and _pair(dilation) == (1, 1) and act is None:
         s = _pair(stride)

@@ -42,6 +42,11 @@ class SameConv(nn.Conv2d):
     def forward(self, x):
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.same, 1, self.groups)
 
+    def forward_skip(self, x):
+        """(conv(x), x_skip): x_skip feeds the block's skip connection; its gradient is added
+        inside this conv's data-gradient kernel (e2ep_conv_dgrad_acc)."""
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.same, 1, self.groups, skip=True)
+
 
 class MBConv(nn.Module):
     def __init__(self, cin, cout, k, stride, expand, size, first):
@@ -64,8 +69,11 @@ class MBConv(nn.Module):
         """dc_rand: this block's per-sample uniform draws for drop-connect (training); drawn
         here when not given (efficientnet-pytorch draws torch.rand([N,1,1,1]) per block)."""
         if self.expand != 1:  # _bn0 + swish applied inside the depthwise conv's input load
-            y = ops.bn_act_depthwise(self._expand_conv(x), self._bn0, "swish",
-                                     self._depthwise_conv)
+            if self.skip and x.is_cuda:
+                e, x = self._expand_conv.forward_skip(x)
+            else:
+                e = self._expand_conv(x)
+            y = ops.bn_act_depthwise(e, self._bn0, "swish", self._depthwise_conv)
         else:
             y = self._depthwise_conv(x)
         y = ops.bn_swish_squeeze_excite(y, self._bn1, self._se_reduce, self._se_expand)

@@ -147,6 +147,12 @@ int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *
 size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels);
 int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
                     int w_layout, float *dx, void *workspace, void *stream);
+/* e2ep_conv_dgrad plus a residual gradient res (dx's layout, may be NULL) added in the
+ * epilogue: dx = conv_transpose(gout, w) + res.  The skip connection around a block whose
+ * first conv reads the block input (MBConv expand conv, ResNet BasicBlock conv1) gets its
+ * input gradient in one pass instead of dgrad + an autograd accumulation add. */
+int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int m_channels,
+                        int w_layout, const float *res, float *dx, void *workspace, void *stream);
 
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of

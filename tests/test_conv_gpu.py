@@ -84,3 +84,40 @@ def test_conv_wgrad_deterministic():
         conv.conv2d(x, wd, None, (1, 1), (1, 1, 1, 1)).backward(gy)
         outs.append(wd.grad.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+# skip passthrough: the block input's skip-connection gradient is added inside the data
+# gradient kernel (e2ep_conv_dgrad_acc), both without split-K (large maps) and with it
+# (small maps -> k_conv_reduce adds it), plus the partial-channel (grad_channels) case.
+SKIP_CASES = [
+    (2, 24, 32, 32, 144, 1, 1, (0, 0, 0, 0), None),   # MBConv expand 1x1
+    (2, 64, 16, 16, 64, 3, 3, (1, 1, 1, 1), None),    # BasicBlock conv1 3x3
+    (2, 160, 8, 8, 960, 1, 1, (0, 0, 0, 0), None),    # small map: split-K data gradient
+    (2, 65, 16, 16, 64, 3, 3, (1, 1, 1, 1), 64),      # grad_channels < Cin
+]
+
+
+@pytest.mark.parametrize("case", SKIP_CASES, ids=[str(i) for i in range(len(SKIP_CASES))])
+def test_conv_skip_gradient_fused(case):
+    from e2ep_amd import conv
+    N, Cin, H, W, Cout, R, S, pad, gc = case
+    g = torch.Generator().manual_seed(17 + Cin)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    y, xs = conv.conv2d(xd, wd, None, (1, 1), pad, (1, 1), 0, grad_channels=gc, skip=True)
+    gy = torch.randn(y.shape, generator=g)
+    gs = torch.randn(x.shape, generator=g)
+    ((y * gy.to(DEV)).sum() + (xs * gs.to(DEV)).sum()).backward()
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    y64 = F.conv2d(F.pad(x64, pad), w64)
+    (y64 * gy.double()).sum().backward()
+    gx = x64.grad.clone()
+    if gc is not None:
+        gx[:, gc:] = 0
+    gx += gs.double()
+    assert rel_l2(y.detach().cpu(), y64) < 1e-5
+    assert rel_l2(xd.grad.cpu(), gx) < 1e-5
+    assert rel_l2(wd.grad.cpu(), w64.grad) < 1e-5
