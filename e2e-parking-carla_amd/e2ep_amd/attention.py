@@ -102,24 +102,30 @@ def _fusable(mod, query, key, attn_mask, key_padding_mask, is_causal):
     return (E // H <= MAX_HEAD_DIM and query.shape[0] <= MAX_SEQ and key.shape[0] <= MAX_SEQ)
 
 
-def mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, is_causal=False):
+def mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, is_causal=False,
+        skip=False):
     """mod(query, key, value, attn_mask=..., key_padding_mask=..., need_weights=False)[0] for a
     seq-first nn.MultiheadAttention, on the fused core when possible.  `is_causal` asserts
-    that attn_mask is the causal (-inf above the diagonal) mask, as torch's is_causal hint."""
+    that attn_mask is the causal (-inf above the diagonal) mask, as torch's is_causal hint.
+    skip=True returns (out, query_skip): the layer's residual reads query_skip, whose gradient
+    the query projection's input-gradient GEMM accumulates (nn_ops.linear)."""
     if not _fusable(mod, query, key, attn_mask, key_padding_mask, is_causal):
-        return mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
-                   need_weights=False, is_causal=bool(is_causal) and attn_mask is not None)[0]
+        out = mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
+                  need_weights=False, is_causal=bool(is_causal) and attn_mask is not None)[0]
+        return (out, query) if skip else out
     E, H = mod.embed_dim, mod.num_heads
     W, bias = mod.in_proj_weight, mod.in_proj_bias
     p = mod.dropout if mod.training else 0.0
     if query is key and key is value:
-        qkv = nn_ops.linear(query, W, bias)
+        qkv, qs = nn_ops.linear(query, W, bias, skip=True)
         o = attention(qkv, None, H, is_causal, key_padding_mask, p)
     else:
         if key is not value:
-            return mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
-                       need_weights=False)[0]
-        q = nn_ops.linear(query, W[:E], None if bias is None else bias[:E])
+            out = mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
+                      need_weights=False)[0]
+            return (out, query) if skip else out
+        q, qs = nn_ops.linear(query, W[:E], None if bias is None else bias[:E], skip=True)
         kv = nn_ops.linear(key, W[E:], None if bias is None else bias[E:])
         o = attention(q, kv, H, is_causal, key_padding_mask, p)
-    return nn_ops.linear(o, mod.out_proj.weight, mod.out_proj.bias)
+    out = nn_ops.linear(o, mod.out_proj.weight, mod.out_proj.bias)
+    return (out, qs) if skip else out

@@ -597,19 +597,25 @@ class _Linear(torch.autograd.Function):
     the transformer's 2048 x 258 gradients) is e2ep_col_sum."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, skip=False):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        return F.linear(x, weight, bias)
+        y = F.linear(x, weight, bias)
+        # skip: also hand x back for the layer's residual connection; that gradient is then
+        # accumulated by the input-gradient GEMM itself (addmm), not by an autograd add
+        return (y, x) if skip else y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, gskip=None):
         x, weight = ctx.saved_tensors
         nig = ctx.needs_input_grad
         g2 = gy.reshape(-1, gy.shape[-1])
         dx = dw = db = None
         if nig[0]:
-            dx = (g2 @ weight).view(x.shape)
+            if gskip is not None:
+                dx = torch.addmm(gskip.reshape(g2.shape[0], -1), g2, weight).view(x.shape)
+            else:
+                dx = (g2 @ weight).view(x.shape)
         if nig[1]:
             dw = g2.t() @ x.reshape(-1, x.shape[-1])
         if ctx.has_bias and nig[2]:
@@ -618,15 +624,17 @@ class _Linear(torch.autograd.Function):
             db = torch.empty(C, dtype=torch.float32, device=gy.device)
             ws = _ws(_lib.load().e2ep_col_sum_workspace(rows, C), gy.device)
             _lib.call("e2ep_col_sum", _lib.ptr(g2), rows, C, _lib.ptr(db), _lib.ptr(ws), _lib.stream())
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear(x, weight, bias=None):
+def linear(x, weight, bias=None, skip=False):
     """F.linear(x, weight, bias) with an e2ep bias gradient (fp32 HIP tensors); other inputs
-    (CPU, other dtypes) go to F.linear itself."""
+    (CPU, other dtypes) go to F.linear itself.  skip=True returns (y, x_skip): use x_skip for
+    the residual connection around this layer and its gradient joins dx inside the GEMM."""
     if not x.is_cuda or x.dtype != torch.float32 or (bias is None or not bias.requires_grad):
-        return F.linear(x, weight, bias)
-    return _Linear.apply(x, weight, bias)
+        y = F.linear(x, weight, bias)
+        return (y, x) if skip else y
+    return _Linear.apply(x, weight, bias, bool(skip))
 
 
 # ------------------------------------------------------------------------------------------

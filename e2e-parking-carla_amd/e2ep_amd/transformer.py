@@ -21,31 +21,37 @@ def _p(drop, training):
 
 
 def _ff(layer, x):
-    h = nn_ops.linear(x, layer.linear1.weight, layer.linear1.bias)
+    """(linear2(dropout(relu(linear1(x)))), x_skip) — x_skip carries the residual (see
+    nn_ops.linear skip)."""
+    h, xs = nn_ops.linear(x, layer.linear1.weight, layer.linear1.bias, skip=True)
     if layer.activation is F.relu and h.is_cuda and h.dtype == torch.float32 and h.numel() % 4 == 0:
         h = nn_ops.relu_dropout(h, _p(layer.dropout, layer.training))  # one launch each way
     else:
         h = layer.dropout(layer.activation(h))
-    return nn_ops.linear(h, layer.linear2.weight, layer.linear2.bias)
+    return nn_ops.linear(h, layer.linear2.weight, layer.linear2.bias), xs
 
 
 def encoder_layer(layer, x, mask=None, key_padding_mask=None):
     """torch.nn.TransformerEncoderLayer.forward (norm_first=False), seq-first x (S, B, E)."""
     assert not layer.norm_first
-    sa = attention.mha(layer.self_attn, x, x, x, attn_mask=mask, key_padding_mask=key_padding_mask)
+    sa, x = attention.mha(layer.self_attn, x, x, x, attn_mask=mask,
+                          key_padding_mask=key_padding_mask, skip=True)
     x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
-    return nn_ops.add_drop_layer_norm(x, _ff(layer, x), layer.norm2, _p(layer.dropout2, layer.training))
+    ff, x = _ff(layer, x)
+    return nn_ops.add_drop_layer_norm(x, ff, layer.norm2, _p(layer.dropout2, layer.training))
 
 
 def decoder_layer(layer, x, memory, tgt_mask=None, tgt_key_padding_mask=None, tgt_is_causal=False):
     """torch.nn.TransformerDecoderLayer.forward (norm_first=False), seq-first."""
     assert not layer.norm_first
-    sa = attention.mha(layer.self_attn, x, x, x, attn_mask=tgt_mask,
-                       key_padding_mask=tgt_key_padding_mask, is_causal=bool(tgt_is_causal))
+    sa, x = attention.mha(layer.self_attn, x, x, x, attn_mask=tgt_mask,
+                          key_padding_mask=tgt_key_padding_mask, is_causal=bool(tgt_is_causal),
+                          skip=True)
     x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
-    ca = attention.mha(layer.multihead_attn, x, memory, memory)
+    ca, x = attention.mha(layer.multihead_attn, x, memory, memory, skip=True)
     x = nn_ops.add_drop_layer_norm(x, ca, layer.norm2, _p(layer.dropout2, layer.training))
-    return nn_ops.add_drop_layer_norm(x, _ff(layer, x), layer.norm3, _p(layer.dropout3, layer.training))
+    ff, x = _ff(layer, x)
+    return nn_ops.add_drop_layer_norm(x, ff, layer.norm3, _p(layer.dropout3, layer.training))
 
 
 def encoder(stack, tokens):

@@ -211,3 +211,19 @@ def test_relu_dropout_matches_masked_reference(p):
     (yr * dy.double()).sum().backward()
     assert rel_l2(y.detach().cpu(), yr) < 1e-6
     assert rel_l2(xd.grad.cpu(), xr.grad) < 1e-6
+
+
+def test_linear_skip_gradient_accumulated_in_gemm():
+    """nn_ops.linear(skip=True): the residual's gradient joins dx inside the addmm."""
+    from e2ep_amd import nn_ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(256, 8, 258, generator=g).transpose(0, 1)  # non-contiguous, like the encoder
+    w = torch.randn(774, 258, generator=g) / 16
+    b = torch.randn(774, generator=g)
+    gy = torch.randn(8, 256, 774, generator=g)
+    gs = torch.randn(8, 256, 258, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    y, xs = nn_ops.linear(xd, w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True), skip=True)
+    ((y * gy.to(DEV)).sum() + (xs * gs.to(DEV)).sum()).backward()
+    ref = gy.double() @ w.double() + gs.double()
+    assert rel_l2(xd.grad.cpu(), ref) < 1e-5
