@@ -170,3 +170,87 @@ int e2ep_se_gate_bwd(const float *x, const float *a, const float *dy, int planes
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Softmax over the channel dim of NCHW (the depth distribution, reference
+// model/bev_model.py:64 `depth.softmax(1)`): thread per pixel, channel loop, pixel-coalesced
+// reads; backward dx = y (dy - sum_c y dy).  PyTorch runs this shape (C = 48, 32 x 32 planes)
+// as a spatial softmax with few workgroups.
+// ------------------------------------------------------------------------------------------
+namespace e2ep {
+
+// C <= SMC_MAX: a thread's channel column is loaded in one batch (all loads in flight) and
+// kept in registers; 64-thread blocks spread the pixels over the whole chip.
+constexpr int SMC_MAX = 64;
+__global__ void __launch_bounds__(64) k_softmax_c_fwd(const float *__restrict__ x, int N, int C,
+                                                      int HW, float *__restrict__ y) {
+  const long long t = (long long)blockIdx.x * 64 + threadIdx.x;
+  if (t >= (long long)N * HW) return;
+  const long long n = t / HW, p = t - n * HW;
+  const float *xs = x + n * C * HW + p;
+  float *ys = y + n * C * HW + p;
+  float v[SMC_MAX];
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c) v[c] = xs[(long long)min(c, C - 1) * HW];  // no branches
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c) v[c] = c < C ? v[c] : -INFINITY;
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c) m = fmaxf(m, v[c]);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c) {
+    v[c] = expf(v[c] - m);  // padded channels: exp(-inf) = 0
+    s += v[c];
+  }
+  const float r = 1.f / s;
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c)
+    if (c < C) ys[(long long)c * HW] = v[c] * r;
+}
+
+__global__ void __launch_bounds__(64) k_softmax_c_bwd(const float *__restrict__ y,
+                                                      const float *__restrict__ dy, int N, int C,
+                                                      int HW, float *__restrict__ dx) {
+  const long long t = (long long)blockIdx.x * 64 + threadIdx.x;
+  if (t >= (long long)N * HW) return;
+  const long long n = t / HW, p = t - n * HW;
+  const long long base = n * C * HW + p;
+  float yv[SMC_MAX], gv[SMC_MAX];
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c) {
+    const float yy = y[base + (long long)min(c, C - 1) * HW];
+    const float gg = dy[base + (long long)min(c, C - 1) * HW];
+    yv[c] = c < C ? yy : 0.f;
+    gv[c] = c < C ? gg : 0.f;
+  }
+  float d = 0.f;
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c) d = __builtin_fmaf(yv[c], gv[c], d);
+#pragma unroll
+  for (int c = 0; c < SMC_MAX; ++c)
+    if (c < C) dx[base + (long long)c * HW] = yv[c] * (gv[c] - d);
+}
+
+}  // namespace e2ep
+
+extern "C" {
+
+int e2ep_softmax_c_fwd(const float *x, int N, int C, int HW, float *y, void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && C <= e2ep::SMC_MAX && HW > 0, E2EP_EINVAL,
+               "e2ep_softmax_c_fwd: bad shape (C <= %d)", e2ep::SMC_MAX);
+  hipLaunchKernelGGL(e2ep::k_softmax_c_fwd, dim3(e2ep::cdiv((long long)N * HW, 64)), dim3(64), 0,
+                     e2ep::as_stream(stream), x, N, C, HW, y);
+  return e2ep::launch_status("e2ep_softmax_c_fwd");
+}
+
+int e2ep_softmax_c_bwd(const float *y, const float *dy, int N, int C, int HW, float *dx,
+                       void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && C <= e2ep::SMC_MAX && HW > 0, E2EP_EINVAL,
+               "e2ep_softmax_c_bwd: bad shape (C <= %d)", e2ep::SMC_MAX);
+  hipLaunchKernelGGL(e2ep::k_softmax_c_bwd, dim3(e2ep::cdiv((long long)N * HW, 64)), dim3(64), 0,
+                     e2ep::as_stream(stream), y, dy, N, C, HW, dx);
+  return e2ep::launch_status("e2ep_softmax_c_bwd");
+}
+
+}  // extern "C"

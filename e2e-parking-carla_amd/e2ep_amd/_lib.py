@@ -66,6 +66,8 @@ SIGNATURES = {
     "e2ep_attn_bwd_workspace": (_sz, [_i, _i, _i]),
     "e2ep_attn_bwd": (_i, [_p] * 6 + [_i] * 11 + [_f, _i, _p, _f, _p, _p, _p, _p, _p, _p]),
     "e2ep_attn_keep_mask": (_i, [_p, _i, _i, _i, _f, _p, _p]),
+    "e2ep_softmax_c_fwd": (_i, [_p, _i, _i, _i, _p, _p]),
+    "e2ep_softmax_c_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_relu_dropout_fwd": (_i, [_p, _i64, _f, _p, _p, _p]),
     "e2ep_relu_dropout_bwd": (_i, [_p, _p, _i64, _f, _p, _p, _p]),
     "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),

@@ -669,3 +669,34 @@ def relu_dropout(x, p=0.0, seed=None):
     if p > 0.0 and seed is None:
         seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=x.device)
     return _ReluDropout.apply(x, float(p), seed)
+
+
+# ------------------------------------------------------------------------------------------
+# softmax over channels (depth distribution)
+# ------------------------------------------------------------------------------------------
+class _SoftmaxC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        N, C = x.shape[:2]
+        HW = x.numel() // (N * C)
+        y = torch.empty_like(x)
+        _lib.call("e2ep_softmax_c_fwd", _lib.ptr(x), N, C, HW, _lib.ptr(y), _lib.stream())
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        N, C = y.shape[:2]
+        HW = y.numel() // (N * C)
+        dx = torch.empty_like(y)
+        _lib.call("e2ep_softmax_c_bwd", _lib.ptr(y), _lib.ptr(dy.contiguous()), N, C, HW,
+                  _lib.ptr(dx), _lib.stream())
+        return dx
+
+
+def softmax_channels(x):
+    """x.softmax(dim=1) for an fp32 NC... HIP tensor, one e2ep launch each way."""
+    _dev(x)
+    return _SoftmaxC.apply(x)

@@ -8,7 +8,7 @@ plan, and the fused outer-product pooling kernel (e2ep_amd.lss)."""
 import torch
 from torch import nn
 
-from e2ep_amd import lss
+from e2ep_amd import lss, nn_ops
 from model.cam_encoder import CamEncoder
 
 
@@ -82,6 +82,8 @@ class BevModel(nn.Module):
         """Camera features (B*N, C, h, w) and depth distribution (B*N, D, h, w)."""
         b, n = images.shape[:2]
         feat, depth = self.cam_encoder(images.reshape(b * n, *images.shape[2:]))
+        if depth.is_cuda and depth.dtype == torch.float32 and depth.shape[1] <= 64:
+            return feat, nn_ops.softmax_channels(depth)  # e2ep kernel (model/bev_model.py:64)
         return feat, depth.softmax(dim=1)
 
     def calc_bev_feature(self, images, intrinsics, extrinsics, extra_channels=0):

@@ -285,6 +285,11 @@ int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o
                   float *dv, void *workspace, void *stream);
 int e2ep_attn_keep_mask(const int32_t *seed, int BH, int Sq, int Sk, float p, uint8_t *out,
                         void *stream);
+/* Softmax over the channel dim of x [N, C, HW] (model/bev_model.py:64 depth.softmax(1)) and
+ * its backward dx = y (dy - sum_c y dy).  C <= 64. */
+int e2ep_softmax_c_fwd(const float *x, int N, int C, int HW, float *y, void *stream);
+int e2ep_softmax_c_bwd(const float *y, const float *dy, int N, int C, int HW, float *dx,
+                       void *stream);
 /* Transformer feed-forward activation y = dropout_p(relu(x)) over n floats (n % 4 == 0,
  * 16-B aligned), and dx = dy * relu'(x) * keep / (1-p).  Keep bit of element c = the
  * attention hash of (*seed, c) (e2ep_attn_keep_mask with BH = Sq = 1, Sk = n shows it). */

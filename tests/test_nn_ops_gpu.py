@@ -336,3 +336,20 @@ def test_add_dropout_layernorm_fused(rows, E, p):
     assert rel_l2(y, y64) < 1e-6
     for got, ref in zip(ts, rs):
         assert rel_l2(got.grad, ref.grad) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(32, 48, 32, 32), (3, 5, 7, 9), (2, 1, 4, 4)])
+def test_softmax_channels_vs_fp64(shape):
+    """Depth softmax over channels (model/bev_model.py:64) vs torch fp64, values and grad."""
+    from e2ep_amd import nn_ops
+    g = _g(sum(shape))
+    x = torch.randn(*shape, generator=g) * 3
+    dy = torch.randn(*shape, generator=g)
+    xd = x.to(DEV).requires_grad_(True)
+    y = nn_ops.softmax_channels(xd)
+    (y * dy.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    y64 = x64.softmax(1)
+    (y64 * dy.double()).sum().backward()
+    assert rel_l2(y.detach().cpu(), y64) < 1e-6
+    assert rel_l2(xd.grad.cpu(), x64.grad) < 1e-5
