@@ -1045,11 +1045,13 @@ size_t e2ep_col_sum_workspace(int rows, int C) {
 int e2ep_col_sum(const float *g, int rows, int C, float *out, void *workspace, void *stream) {
   E2EP_REQUIRE(rows > 0 && C > 0 && workspace, E2EP_EINVAL, "e2ep_col_sum: bad args");
   const int chunks = cdiv(rows, COLSUM_ROWS);
-  float *part = static_cast<float *>(workspace);
+  // one chunk (e.g. the control decoder's 112 token rows): the partial sums are the result
+  float *part = chunks == 1 ? out : static_cast<float *>(workspace);
   hipLaunchKernelGGL(k_col_sum_partial, dim3(cdiv(C, 64), chunks), dim3(256), 0,
                      as_stream(stream), g, rows, C, part);
-  hipLaunchKernelGGL(k_col_sum_final, dim3(cdiv(C, 256)), dim3(256), 0, as_stream(stream), part,
-                     chunks, C, out);
+  if (chunks > 1)
+    hipLaunchKernelGGL(k_col_sum_final, dim3(cdiv(C, 256)), dim3(256), 0, as_stream(stream), part,
+                       chunks, C, out);
   return launch_status("e2ep_col_sum");
 }
 
