@@ -7,15 +7,20 @@ losses, backward, and the Adam(lr 1e-4, wd 1e-4) update (:116-121), fp32, on a s
 B-sample batch (4 x 256x256 cameras) that is resident in HBM before timing.
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
-N>1 is launched by torch.distributed.run (one rank per GPU, RCCL over xGMI): each rank runs
-B samples per step (weak scaling) and the flat gradient buffer is all-reduced (the only
-exchange).  The step is captured into HIP graphs during warm-up (e2ep_amd.train.TrainStep;
---eager disables capture).
+N>1: one rank per GPU, RCCL over xGMI.  Under torch.distributed.run (WORLD_SIZE set) the ranks
+are already there; from a plain command line `--gpus N` re-launches this script under
+torch.distributed.run with N ranks before anything touches the GPU.  Each rank runs B samples
+per step (weak scaling); the gradients are all-reduced in ~25 MB buckets issued during
+backward (the only exchange, captured into the backward graph).  The step is captured into
+HIP graphs during warm-up (e2ep_amd.train.TrainStep; --eager disables capture).
 Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -29,6 +34,10 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "train samples/sec (4-cam frames) at B=8, 1/2/4/8 MI355X; CPU-ref baseline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = the f32 vector rate
+# forward 29.94 GFLOP per 4-cam 256^2 sample (FlopCounterMode), train step
+# = 3 x forward
+STEP_GFLOP_PER_SAMPLE = 3 * 29.94
 
 
 def lss_fwd_bytes(B, N=4, C=64, D=48, hw=1024, XY=40000):
@@ -82,9 +91,29 @@ def device_batch(data, dev):
     return out
 
 
-def cpu_baseline(batch, steps, threads):
+def host_cores():
+    """Threads for the CPU baseline: the CPUs this process may run on (the GPU box's CPU
+    share is its affinity / OMP_NUM_THREADS, not the machine's total), and the CPU model."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n, model
+
+
+def cpu_baseline(batch, steps, warmup, threads):
     """The oracle (CPU restatement of the reference, bit-identical to it in the build
-    container) running the same train step on the host cores."""
+    container) running the same train step on the host cores: `warmup` untimed steps, then
+    the median of `steps` timed steps."""
     from oracle import parking_ref as O
     from e2ep_amd import synthetic
 
@@ -93,12 +122,15 @@ def cpu_baseline(batch, steps, threads):
     m = O.ParkingModelRef(O.Cfg).train()
     opt = O.make_optimizer(m)
     data = synthetic.synthetic_batch(batch, seed=0)
-    O.train_step(m, opt, data)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(warmup):
         O.train_step(m, opt, data)
-    dt = time.perf_counter() - t0
-    return batch * steps / dt, dt
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        O.train_step(m, opt, data)
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    return batch / med, med, ts
 
 
 def load_traffic(batch):
@@ -113,20 +145,40 @@ def load_traffic(batch):
     return float(j["hbm_bytes_per_launch"])
 
 
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def relaunch(n):
+    """`--gpus N` from a plain command line: start N ranks under torch.distributed.run (a
+    child process; nothing here has touched the GPU) and exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="samples per GPU per step")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (median)")
+    ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     # rehearsal of the N>1 path on a one-GPU box: every rank on device 0, gloo all-reduce
     # (E2EP_BENCH_REHEARSAL=1; never used for reported numbers)
     rehearsal = os.environ.get("E2EP_BENCH_REHEARSAL") == "1"
@@ -134,11 +186,14 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = None
     if world > 1:
         if rehearsal:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        backend = dist.get_backend()
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
     from e2ep_amd import _lib, synthetic, timing
     from e2ep_amd.train import TrainStep
@@ -172,50 +227,79 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # per-kernel HIP-event timing: a few eager steps on the same stream after the timed
-    # region (graph replays cannot be bracketed per kernel from the host)
-    timing.reset()
-    timing.enable(True)
-    for _ in range(3):
-        step._fwd_bwd()
-    timing.enable(False)
-    kern = timing.summary()
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     samples = world * args.batch * args.steps
     value = samples / elapsed
+    ms_step = elapsed / args.steps * 1e3
+
+    # per-kernel HIP-event timing: 3 eager forward+backward passes on the same stream after
+    # the timed region (graph replays cannot be bracketed per kernel from the host)
+    n_eager = 3
+    timing.reset()
+    timing.enable(True)
+    for _ in range(n_eager):
+        step._fwd_bwd()
+    timing.enable(False)
+    kern = timing.summary()
+    work = timing.work()
+    gemm = [k for k in ("conv_fwd", "conv_dgrad") if k in kern]
+    g_ms = sum(kern[k][2] for k in gemm)
+    g_flop = sum(work.get(k, 0.0) for k in gemm)
+    g_launch = sum(kern[k][0] for k in gemm)
+    g_tfs = g_flop / (g_ms * 1e-3) / 1e12
+    roofline = {"kernel": "e2ep::k_conv_gemm (implicit-GEMM conv forward + data gradient, "
+                          "v_mfma_f32_32x32x2_f32; the step's largest kernel family)",
+                "bound": "mfma", "achieved": round(g_tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": round(g_tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+                "flop_per_step": g_flop / n_eager, "ms_per_step": round(g_ms / n_eager, 4),
+                "launches_per_step": g_launch // n_eager,
+                "timing": "HIP events around every conv fwd/dgrad launch of 3 eager fwd+bwd "
+                          "passes on the launch stream; FLOPs = 2*N*Cout*P*Q*Cin*R*S per launch"}
+    step_tfs = STEP_GFLOP_PER_SAMPLE * 1e9 * args.batch / (ms_step * 1e-3) / 1e12
+    step_roofline = {"bound": "mfma", "achieved": round(step_tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
+                     "unit": "TFLOP/s", "frac": round(step_tfs / FP32_MFMA_PEAK_TFS, 4),
+                     "flop_per_sample": STEP_GFLOP_PER_SAMPLE * 1e9,
+                     "basis": "3 x 29.94 GFLOP forward per sample (SURVEY.md §8d) x B per GPU "
+                              "/ ms_per_step"}
 
     mean_ms, n_fwd = lss_fwd_kernel_ms(mod.parking_model.bev_model._plan, dev)
     achieved = lss_fwd_bytes(args.batch) / (mean_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.batch)
-    roofline = {"kernel": "e2ep::k_lss_fwd (fused depth x feature outer product + pillar pooling)",
-                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "bytes_per_launch": lss_fwd_bytes(args.batch), "launch_ms": round(mean_ms, 5),
-                "launches": n_fwd, "timing": "HIP events around back-to-back launches on the "
-                                             "launch stream, model's pillar plan"}
+    roofline_lss = {"kernel": "e2ep::k_lss_fwd (fused depth x feature outer product + pillar "
+                              "pooling, the north-star lift-splat kernel)",
+                    "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": load_traffic(args.batch),
+                    "bytes_per_launch": lss_fwd_bytes(args.batch), "launch_ms": round(mean_ms, 5),
+                    "launches": n_fwd, "timing": "HIP events around back-to-back launches on the "
+                                                 "launch stream, model's pillar plan"}
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        v, dt = cpu_baseline(args.batch, args.cpu_steps, threads)
+        threads, cpu_model = host_cores()
+        v, med, ts = cpu_baseline(args.batch, args.cpu_steps, args.cpu_warmup, threads)
         base = {"value": round(v, 4), "unit": "samples/s", "cores": threads, "kind": "port",
-                "sample": f"{args.cpu_steps} timed train steps (after 1 warm-up) of the oracle CPU "
-                          f"restatement at B={args.batch}, 4x256^2, fp32 ({dt:.1f} s)"}
+                "cpu_model": cpu_model,
+                "sample": f"median of {args.cpu_steps} timed train steps (after {args.cpu_warmup} "
+                          f"warm-up) of the oracle CPU restatement at B={args.batch}, 4x256^2, fp32, "
+                          f"{threads} threads; step times "
+                          + ", ".join(f"{t:.2f}" for t in ts) + " s"}
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                "ms_per_step": round(ms_step, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
                 "config": {"workload": "ParkingModel train step (fwd + control/seg/depth losses + bwd "
                                        "+ Adam), 4 cams x 256x256, fp32, random init",
                            "global_batch": world * args.batch, "batch_per_gpu": args.batch,
                            "parallelism": f"dp{world}"},
-                "roofline": roofline, "cpu_baseline": base,
-                "final_loss": round(float(loss), 4)}
+                "world": {"size": world, "backend": backend, "rehearsal": rehearsal},
+                "roofline": roofline, "step_roofline": step_roofline, "roofline_lss": roofline_lss,
+                "cpu_baseline": base, "final_loss": round(float(loss), 4)}
         print(json.dumps(line), flush=True)
         print("kernel timing (launches, mean ms, total ms):",
               {k: (n, round(m, 4), round(t, 3)) for k, (n, m, t) in kern.items()}, file=sys.stderr)

@@ -11,8 +11,10 @@ namespace e2ep {
 
 // torch.optim.Adam evaluates its scalars in double on the host and hands them to fp32
 // kernels: beta**step and lr/bc1 in double, (1 - beta) in double then rounded to fp32.
+// The learning rate is read from device memory (a double written by the host when an LR
+// scheduler changes it), so a captured step follows CosineAnnealingLR under graph replay.
 struct AdamHyper {
-  double lr, beta1, beta2;
+  double beta1, beta2;
   float b1f, b2f, w1, w2, eps, wd, grad_scale;
 };
 
@@ -27,18 +29,21 @@ __global__ void __launch_bounds__(ADAM_THREADS)
     k_adam(const int4 *__restrict__ chunks, const long long *__restrict__ offs,
            const long long *__restrict__ gptrs, const float *__restrict__ gflat,
            float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
-           const float *__restrict__ step, AdamHyper h) {
+           const float *__restrict__ step, const double *__restrict__ lr, AdamHyper h) {
   const int4 c = chunks[blockIdx.x];
   const long long off = offs[c.x] + c.y;
-  const float *g = gflat ? gflat + off : reinterpret_cast<const float *>(gptrs[c.x]);
-  if (g == nullptr) return;  // parameter without a gradient this step: not stepped (as torch)
-  if (!gflat) g += c.y;
+  // a parameter without a gradient this step is not stepped (as torch.optim.Adam); on the
+  // flat (all-reduced) path the table still says which parameters had one, so the result
+  // does not depend on the world size
+  const float *gt = gptrs ? reinterpret_cast<const float *>(gptrs[c.x]) : nullptr;
+  if (gptrs && gt == nullptr) return;
+  const float *g = gflat ? gflat + off : gt + c.y;
   // torch: bias_correction = 1 - beta**step (python double), step_size = lr / bc1,
   // denom = sqrt(v) / sqrt(bc2) + eps, p -= step_size * m / denom
   const double t = (double)step[0];
   const double bc1 = 1.0 - pow(h.beta1, t);
   const double bc2 = 1.0 - pow(h.beta2, t);
-  const float step_size = (float)(h.lr / bc1);
+  const float step_size = (float)(lr[0] / bc1);
   const float bc2s = (float)sqrt(bc2);
   const float w1 = h.w1, w2 = h.w2;
   float *pp = p + off, *mp = m + off, *vp = v + off;
@@ -97,18 +102,17 @@ int e2ep_adam_chunk_elems(void) { return ADAM_THREADS * ADAM_VEC * ADAM_ITERS; }
 
 int e2ep_adam_step(const int *chunks, int n_chunks, const long long *offsets,
                    const long long *grad_ptrs, const float *grad_flat, float *param, float *exp_avg,
-                   float *exp_avg_sq, float *step, double lr, double beta1, double beta2,
+                   float *exp_avg_sq, float *step, const double *lr, double beta1, double beta2,
                    double eps, double weight_decay, float grad_scale, void *stream) {
-  E2EP_REQUIRE(n_chunks > 0 && chunks && offsets && param && exp_avg && exp_avg_sq && step,
+  E2EP_REQUIRE(n_chunks > 0 && chunks && offsets && param && exp_avg && exp_avg_sq && step && lr,
                E2EP_EINVAL, "e2ep_adam_step: null argument");
   E2EP_REQUIRE(grad_ptrs || grad_flat, E2EP_EINVAL, "e2ep_adam_step: no gradients");
-  AdamHyper h{lr,          beta1,         beta2,       (float)beta1, (float)beta2,
-              (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (float)weight_decay,
-              grad_scale};
+  AdamHyper h{beta1, beta2, (float)beta1, (float)beta2, (float)(1.0 - beta1),
+              (float)(1.0 - beta2), (float)eps, (float)weight_decay, grad_scale};
   hipLaunchKernelGGL(k_adam_count, dim3(1), dim3(1), 0, as_stream(stream), step);
   hipLaunchKernelGGL(k_adam, dim3(n_chunks), dim3(ADAM_THREADS), 0, as_stream(stream),
                      reinterpret_cast<const int4 *>(chunks), offsets, grad_ptrs, grad_flat, param,
-                     exp_avg, exp_avg_sq, step, h);
+                     exp_avg, exp_avg_sq, step, lr, h);
   return launch_status("e2ep_adam_step");
 }
 

@@ -14,6 +14,13 @@ def _ws(nbytes, device):
     return torch.empty(nbytes // 4, dtype=torch.float32, device=device) if nbytes else None
 
 
+def conv_flops(dims, in_channels=None):
+    """Algorithmic FLOPs of one conv launch (fwd, or dgrad / wgrad over in_channels):
+    2 * N * Cout * P * Q * Cin * R * S."""
+    N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
+    return 2.0 * N * Cout * P * Q * (in_channels or Cin) * R * S
+
+
 def tap_major(w):
     """[Cout,Cin,R,S] -> [R*S,Cout,Cin] (the kernels' w_layout 1); 1x1 filters unchanged."""
     Cout, Cin, R, S = w.shape
@@ -29,7 +36,7 @@ def conv_fwd(x, w, b, dims, act, y, w_layout=0):
     """Launch the forward conv into y (handles the split-K workspace)."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_fwd_workspace(d), x.device)
-    with timing.region("conv_fwd"):
+    with timing.region("conv_fwd", conv_flops(dims)):
         _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
                   _lib.ptr(y), _lib.ptr(ws), _lib.stream())
     return y
@@ -39,7 +46,7 @@ def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0, res=None):
     """dx = data gradient (+ res, a residual gradient in dx's layout, added in the epilogue)."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_dgrad_workspace(d, m_channels), gy.device)
-    with timing.region("conv_dgrad"):
+    with timing.region("conv_dgrad", conv_flops(dims, m_channels)):
         _lib.call("e2ep_conv_dgrad_acc", _lib.ptr(gy), _lib.ptr(w), d, m_channels, w_layout,
                   _lib.ptr(res), _lib.ptr(dx), _lib.ptr(ws), _lib.stream())
     return dx
@@ -49,7 +56,7 @@ def conv_wgrad(gy, x, dims, dw):
     d = _lib.dims(dims)
     splits = _lib.load().e2ep_conv_wgrad_splits(d)
     ws = torch.empty(splits * dw.numel(), dtype=torch.float32, device=gy.device)
-    with timing.region("conv_wgrad"):
+    with timing.region("conv_wgrad", conv_flops(dims)):
         _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws),
                   _lib.ptr(dw), 0, _lib.stream())
     return dw

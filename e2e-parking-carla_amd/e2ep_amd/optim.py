@@ -11,6 +11,13 @@ autograd hands its result over without an accumulate).  For data parallelism the
 gradients are gathered into a flat buffer of the same layout by one more launch, and
 that buffer is what RCCL all-reduces.
 
+FlatAdam is a torch.optim.Optimizer with one param group, so the reference's
+CosineAnnealingLR (trainer/pl_trainer.py:120) binds to it unchanged.  The learning rate the
+kernel uses lives in a device fp64 scalar: step() (eager) and TrainStep (before each graph
+replay) copy param_groups[0]['lr'] into it when the scheduler has changed it, so a captured
+step follows the schedule.  betas / eps / weight_decay are fixed at construction (the
+reference never changes them).
+
 state_dict() / load_state_dict() use torch.optim.Adam's format, so checkpoints move
 between this optimizer and the reference's.
 """
@@ -21,18 +28,23 @@ from . import _lib
 _ALIGN = 4  # elements (16 bytes)
 
 
-class FlatAdam:
+class FlatAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
-        self.params = list(params)
-        if not self.params:
+        params = list(params)
+        if not params:
             raise ValueError("FlatAdam: empty parameter list")
-        dev = self.params[0].device
+        if isinstance(params[0], dict):
+            raise ValueError("FlatAdam: one parameter group only")
+        dev = params[0].device
         if dev.type != "cuda":
             raise _lib.E2EPError("FlatAdam runs on a HIP device only")
-        for p in self.params:
+        for p in params:
             if p.dtype != torch.float32 or p.device != dev:
                 raise _lib.E2EPError("FlatAdam: parameters must be fp32 on one device")
-        self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps,
+                                      weight_decay=weight_decay))
+        self.params = self.param_groups[0]["params"]
+        self.betas, self.eps, self.weight_decay = tuple(betas), eps, weight_decay
         lib = _lib.load()
         chunk = lib.e2ep_adam_chunk_elems()
         offs, rows, off = [], [], 0
@@ -56,19 +68,48 @@ class FlatAdam:
         self.chunks = torch.tensor(rows, dtype=torch.int32, device=dev).reshape(-1)
         self.n_chunks = len(rows)
         self._offs_host = offs
+        self.spans = [(o, p.numel()) for o, p in zip(offs, self.params)]
         self._gtab = torch.zeros(len(self.params), dtype=torch.int64, device=dev)
         self._gkey = None
+        # row range of each tensor in the chunk table (gradient buckets gather by rows)
+        self.chunk_rows, r = [], 0
+        for p in self.params:
+            n = (p.numel() + chunk - 1) // chunk
+            self.chunk_rows.append((r, r + n))
+            r += n
+        self.lr_dev = torch.full((1,), float(lr), dtype=torch.float64, device=dev)
+        self._lr_written = float(lr)
+
+    # -- learning rate ------------------------------------------------------------------------
+    @property
+    def lr(self):
+        return self.param_groups[0]["lr"]
+
+    @lr.setter
+    def lr(self, v):
+        self.param_groups[0]["lr"] = v
+
+    def sync_lr(self):
+        """Copy param_groups[0]['lr'] (an LR scheduler's output) into the device scalar the
+        Adam kernel reads, if it changed.  Not during capture: the kernel node reads the
+        scalar at replay time, the host writes it between replays."""
+        lr = float(self.param_groups[0]["lr"])
+        if lr != self._lr_written and not torch.cuda.is_current_stream_capturing():
+            self.lr_dev.fill_(lr)
+            self._lr_written = lr
 
     # -- gradients --------------------------------------------------------------------------
     def zero_grad(self, set_to_none=True):
         for p in self.params:
             p.grad = None
 
-    def prepare(self):
+    def prepare(self, params=None):
         """Point the device gradient table at the current .grad tensors (one small H2D copy,
-        only when an address changed).  Call it outside graph capture."""
+        only when an address changed) — of all tensors, or of the index range `params` =
+        (i0, i1) (one gradient bucket).  Call it outside graph capture."""
+        i0, i1 = params if params is not None else (0, len(self.params))
         key = []
-        for p in self.params:
+        for p in self.params[i0:i1]:
             g = p.grad
             if g is None:
                 key.append(0)
@@ -76,31 +117,47 @@ class FlatAdam:
             if g.dtype != torch.float32 or not g.is_contiguous() or g.device != self.flat.device:
                 raise _lib.E2EPError("FlatAdam: gradients must be contiguous fp32 on the device")
             key.append(g.data_ptr())
-        key = tuple(key)
-        if key != self._gkey:
+        old = self._gkey if self._gkey is not None else (None,) * len(self.params)
+        if tuple(key) != tuple(old[i0:i1]):
             if torch.cuda.is_current_stream_capturing():
                 raise _lib.E2EPError("FlatAdam.prepare: gradient addresses changed during capture")
-            self._gtab.copy_(torch.tensor(key, dtype=torch.int64))
-            self._gkey = key
+            self._gtab[i0:i1].copy_(torch.tensor(key, dtype=torch.int64))
+            self._gkey = tuple(old[:i0]) + tuple(key) + tuple(old[i1:])
 
-    def gather_grads(self, out):
-        """Per-tensor gradients -> `out` (flat, parameter layout) for the all-reduce."""
-        _lib.call("e2ep_grad_gather", _lib.ptr(self.chunks), self.n_chunks, _lib.ptr(self.offsets),
-                  _lib.ptr(self._gtab), _lib.ptr(out), _lib.stream())
+    def gather_grads(self, out, params=None):
+        """Per-tensor gradients -> `out` (flat, parameter layout) for the all-reduce;
+        `params` = (i0, i1) restricts it to one bucket of tensors."""
+        if params is None:
+            r0, r1 = 0, self.n_chunks
+        else:
+            r0, r1 = self.chunk_rows[params[0]][0], self.chunk_rows[params[1] - 1][1]
+        if r1 <= r0:
+            return
+        import ctypes
+        _lib.call("e2ep_grad_gather", ctypes.c_void_p(self.chunks.data_ptr() + 16 * r0), r1 - r0,
+                  _lib.ptr(self.offsets), _lib.ptr(self._gtab), _lib.ptr(out), _lib.stream())
 
     # -- update -----------------------------------------------------------------------------
-    def step(self, grad_flat=None, grad_scale=1.0):
+    @torch.no_grad()
+    def step(self, grad_flat=None, grad_scale=1.0, closure=None):
         """One Adam step from the prepared gradient table, or from `grad_flat` (scaled by
-        grad_scale, e.g. 1/world for an all-reduced sum)."""
-        if grad_flat is None and self._gkey is None:
-            raise _lib.E2EPError("FlatAdam.step: call prepare() after backward")
+        grad_scale, e.g. 1/world for an all-reduced sum); tensors whose table entry is null
+        (no gradient) are skipped either way.  torch.optim-style calls (no arguments, or a
+        closure) prepare the table themselves."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if not torch.cuda.is_current_stream_capturing():
+            self.prepare()
+        self.sync_lr()
         b1, b2 = self.betas
         _lib.call("e2ep_adam_step", _lib.ptr(self.chunks), self.n_chunks, _lib.ptr(self.offsets),
-                  None if grad_flat is not None else _lib.ptr(self._gtab),
-                  _lib.ptr(grad_flat) if grad_flat is not None else None,
+                  _lib.ptr(self._gtab), _lib.ptr(grad_flat) if grad_flat is not None else None,
                   _lib.ptr(self.flat), _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq),
-                  _lib.ptr(self.step_count), float(self.lr), float(b1), float(b2), float(self.eps),
-                  float(self.weight_decay), float(grad_scale), _lib.stream())
+                  _lib.ptr(self.step_count), _lib.ptr(self.lr_dev), float(b1), float(b2),
+                  float(self.eps), float(self.weight_decay), float(grad_scale), _lib.stream())
+        return loss
 
     # -- torch.optim.Adam-format state --------------------------------------------------------
     def state_dict(self):
@@ -110,7 +167,7 @@ class FlatAdam:
             state[i] = {"step": self.step_count[0].detach().cpu().clone(),
                         "exp_avg": self.exp_avg[o:o + n].view_as(p).clone(),
                         "exp_avg_sq": self.exp_avg_sq[o:o + n].view_as(p).clone()}
-        group = {"lr": self.lr, "betas": self.betas, "eps": self.eps,
+        group = {"lr": float(self.lr), "betas": self.betas, "eps": self.eps,
                  "weight_decay": self.weight_decay, "amsgrad": False, "maximize": False,
                  "foreach": None, "capturable": False, "differentiable": False, "fused": None,
                  "params": list(range(len(self.params)))}
@@ -118,7 +175,11 @@ class FlatAdam:
 
     def load_state_dict(self, sd):
         g = sd["param_groups"][0]
-        self.lr, self.betas, self.eps, self.weight_decay = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
+        self.betas, self.eps, self.weight_decay = tuple(g["betas"]), g["eps"], g["weight_decay"]
+        pg = self.param_groups[0]
+        pg.update(lr=g["lr"], betas=self.betas, eps=self.eps, weight_decay=self.weight_decay)
+        if "initial_lr" in g:
+            pg["initial_lr"] = g["initial_lr"]
         steps = set()
         with torch.no_grad():
             for i, (p, o) in enumerate(zip(self.params, self._offs_host)):

@@ -11,6 +11,7 @@ import torch
 
 _enabled = False
 _events = defaultdict(list)
+_work = defaultdict(float)
 
 
 def enable(flag=True):
@@ -20,13 +21,17 @@ def enable(flag=True):
 
 def reset():
     _events.clear()
+    _work.clear()
 
 
 @contextmanager
-def region(name):
+def region(name, work=0.0):
+    """Time the launches enqueued inside; `work` = the launch's algorithmic FLOPs (or bytes),
+    summed per region name for roofline figures."""
     if not _enabled:
         yield
         return
+    _work[name] += float(work)
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
     s.record()  # records on torch's current stream == the stream the kernel is enqueued on
@@ -45,3 +50,8 @@ def summary():
         t = [s.elapsed_time(e) for s, e in evs]
         out[k] = (len(t), sum(t) / max(1, len(t)), sum(t))
     return out
+
+
+def work():
+    """{name: total algorithmic work recorded by region(..., work=)} since reset()."""
+    return dict(_work)

@@ -6,61 +6,197 @@ backward and the Adam update — is captured once into HIP graphs and replayed, 
 ~1,500 kernel launches of a step cost a few launches from the host.
 
 Optimizer: e2ep_amd.optim.FlatAdam (one fused launch over a flat parameter buffer; the
-gradients are read where autograd left them).
+gradients are read where autograd left them).  Its learning rate is a device scalar that
+__call__ refreshes from param_groups[0]['lr'] before each replay, so an LR scheduler
+(the reference's CosineAnnealingLR) acts on the captured step.
 
-Data parallelism (one process per GPU, RCCL over xGMI): after backward the gradients are
-gathered into one flat fp32 buffer (one launch), that buffer is all-reduced once per step
-(sum; the 1/world mean is folded into the Adam launch — DistributedDataParallel's averaging,
-without its per-bucket hooks), then the optimizer graph runs.  The all-reduce stays outside
-the graphs.  bev_encoder.layer4 has no gradient (never run, reference
-model/bev_encoder.py:21): callers freeze it so it is not part of the step.
+Data parallelism (one process per GPU, RCCL over xGMI; DistributedDataParallel semantics
+without its module wrapper): the flat fp32 gradient buffer (FlatAdam's layout) is cut into
+buckets of ~25 MB in reverse layout order (the order backward produces gradients).  A
+post-accumulate-grad hook per parameter counts arrivals; when a bucket is complete (and every
+earlier bucket has been issued — the same order on every rank), a side stream waits on an
+event recorded on the compute stream, gathers the bucket's gradients into the flat buffer
+(one launch) and all-reduces that slice asynchronously, so the exchange overlaps the rest of
+backward.  After backward the compute stream waits for every bucket; the 1/world mean is
+folded into the Adam launch.  With RCCL the hooks fire during capture, so the gathers and
+all-reduces are nodes of the backward graph (forked onto the side stream and joined before
+the optimizer).  gloo cannot be captured and does not order itself against HIP streams: with
+gloo and device tensors (the one-GPU rehearsal) the flat buffer is gathered after backward and
+staged explicitly through pinned host memory (copy, host waits on the stream, all-reduce on
+the host, copy back), in eager and graph mode alike.
 
-Graph replay order per step: g_bwd (fwd + losses + bwd) -> [g_gather -> all-reduce] -> g_opt.
-Graphs are captured through e2ep_amd.graphs.capture, which repairs memset nodes (they do
-not replay correctly on this ROCm stack) before instantiation.
+Graph replay order per step: g_bwd (fwd + losses + bwd [+ bucket all-reduces]) ->
+[g_gather -> host-staged all-reduce (gloo)] -> g_opt.  Graphs are captured through
+e2ep_amd.graphs.capture, which repairs memset nodes (they do not replay correctly on this
+ROCm stack) before instantiation.
+
+Graph mode captures the lift-splat pillar plan of the batch's (host) rig: a later batch with
+a different intrinsics/extrinsics rig raises instead of silently training on the captured
+plan (the CARLA rig is constant).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
-from . import graphs
+from . import _lib, graphs
 from .optim import FlatAdam
+
+BUCKET_MB = 25.0  # DistributedDataParallel's default bucket_cap_mb
+
+
+def _rig_key(batch):
+    k, e = batch.get("intrinsics"), batch.get("extrinsics")
+    if not (torch.is_tensor(k) and torch.is_tensor(e)) or k.is_cuda or e.is_cuda:
+        return None  # device rig: the plan is rebuilt inside the step, nothing captured
+    return (tuple(k.shape), tuple(e.shape), k.detach().float().contiguous().numpy().tobytes(),
+            e.detach().float().contiguous().numpy().tobytes())
+
+
+class GradBuckets:
+    """Bucketed, hook-driven gradient all-reduce over the optimizer's flat layout.
+
+    `opt` supplies `spans` ([(flat offset, numel)] per parameter, in layout order),
+    `gather_grads(out, params=(i0, i1))` and `prepare(params=(i0, i1))` (point the device
+    gradient table at the current .grad tensors of that range)."""
+
+    def __init__(self, params, opt, flat, bucket_mb=BUCKET_MB):
+        self.params, self.opt, self.flat = params, opt, flat
+        self.cuda = flat.is_cuda
+        cap = int(bucket_mb * 2 ** 20) // 4
+        spans = opt.spans
+        self.buckets = []  # (i0, i1, lo, hi): parameters [i0, i1), flat [lo, hi)
+        i1 = len(params)
+        while i1 > 0:
+            i0, n = i1, 0
+            while i0 > 0 and (n == 0 or n + spans[i0 - 1][1] <= cap):
+                i0 -= 1
+                n += spans[i0][1]
+            lo = spans[i0][0]
+            hi = flat.numel() if i1 == len(params) else spans[i1][0]  # include alignment pad
+            self.buckets.append((i0, i1, lo, hi))
+            i1 = i0
+        self.of = {}
+        for b, (i0, i1, _, _) in enumerate(self.buckets):
+            for i in range(i0, i1):
+                self.of[i] = b
+        self.comm = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        self.active = False
+        self._handles = [p.register_post_accumulate_grad_hook(self._hook_for(i))
+                         for i, p in enumerate(params)]
+
+    def _hook_for(self, i):
+        def hook(_p):
+            if self.active:
+                self._arrived(i)
+        return hook
+
+    def arm(self):
+        self.pending = [i1 - i0 for (i0, i1, _, _) in self.buckets]
+        self.next = 0
+        self.works = []
+        self.active = True
+
+    def _arrived(self, i):
+        b = self.of[i]
+        self.pending[b] -= 1
+        while self.next < len(self.buckets) and self.pending[self.next] == 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def _launch(self, b):
+        i0, i1, lo, hi = self.buckets[b]
+        if not self.cuda:
+            self.opt.prepare(params=(i0, i1))
+            self.opt.gather_grads(self.flat, params=(i0, i1))
+            self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.comm.wait_event(ev)
+        with torch.cuda.stream(self.comm):
+            if not torch.cuda.is_current_stream_capturing():
+                self.opt.prepare(params=(i0, i1))  # fresh gradient addresses (eager)
+            self.opt.gather_grads(self.flat, params=(i0, i1))
+            self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
+
+    def finish(self):
+        """Issue the buckets whose tensors had no gradient this step (zeros), in order, and
+        make the compute stream wait for every all-reduce."""
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+        for w in self.works:
+            w.wait()
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.comm)
+        self.works = []
+        self.active = False
 
 
 class TrainStep:
     def __init__(self, module, batch, lr=1e-4, weight_decay=1e-4, world=1, graph=True,
-                 warmup=3, optimizer=None):
+                 warmup=3, optimizer=None, bucket_mb=BUCKET_MB, overlap=None, ddp=None):
         self.module = module
         self.batch = batch
         self.world = world
+        # ddp: run the exchange (default: world > 1; ddp=True at world 1 exercises the
+        # collective path on one device, e.g. RCCL capture in tests)
+        self.ddp = world > 1 if ddp is None else bool(ddp)
         self.graph = graph
         self.params = [p for p in module.parameters() if p.requires_grad]
         self.opt = optimizer if optimizer is not None else FlatAdam(
             self.params, lr=lr, weight_decay=weight_decay)
-        self.flat_grad = (torch.zeros(self.opt.numel, dtype=torch.float32,
-                                      device=self.params[0].device) if world > 1 else None)
+        dev = self.params[0].device
+        self.flat_grad = (torch.zeros(self.opt.numel, dtype=torch.float32, device=dev)
+                          if self.ddp else None)
+        self.backend = dist.get_backend() if self.ddp else None
+        if overlap is None:
+            overlap = os.environ.get("E2EP_DDP_OVERLAP", "1") != "0"
+        # hook-driven bucket all-reduce: RCCL (eager or captured) and host tensors (gloo on
+        # CPU); gloo with device tensors is host-staged after backward instead
+        self.overlap = bool(self.ddp and overlap and
+                            (self.backend == "nccl" or not self.flat_grad.is_cuda))
+        self.buckets = (GradBuckets(self.params, self.opt, self.flat_grad, bucket_mb)
+                        if self.overlap else None)
+        self._host = (torch.empty(self.opt.numel, dtype=torch.float32, pin_memory=True)
+                      if self.ddp and not self.overlap and self.flat_grad.is_cuda else None)
         self.loss = None
         self.g_bwd = self.g_gather = self.g_opt = None
-        self._host_sync = world > 1 and dist.get_backend() == "gloo"
+        self._rig = _rig_key(batch)
         if graph:
             self._capture(warmup)
 
     # -- pieces ---------------------------------------------------------------------------
     def _fwd_bwd(self):
         self.opt.zero_grad(set_to_none=True)  # autograd hands its gradient tensors over
+        if self.buckets is not None:
+            self.buckets.arm()
         loss = self.module.training_step(self.batch, 0)
         loss.backward()
+        if self.buckets is not None:
+            self.buckets.finish()
         return loss.detach()
 
     def _gather(self):
-        if self.world > 1:
+        if self.ddp and self.buckets is None:
             self.opt.gather_grads(self.flat_grad)
 
     def _allreduce(self):
-        if self.world > 1:
+        """Non-overlapped exchange (gloo): host-staged for device tensors, with the ordering
+        explicit — the host waits for the compute stream before gloo reads the copy."""
+        if not self.ddp or self.buckets is not None:
+            return
+        if self._host is None:
             dist.all_reduce(self.flat_grad)
+            return
+        self._host.copy_(self.flat_grad, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        dist.all_reduce(self._host)
+        self.flat_grad.copy_(self._host, non_blocking=True)
 
     def _update(self):
-        if self.world > 1:
+        if self.ddp:
             self.opt.step(self.flat_grad, 1.0 / self.world)
         else:
             self.opt.step()
@@ -85,26 +221,30 @@ class TrainStep:
         self.g_bwd, self.loss, self.memsets = graphs.capture(self._fwd_bwd)
         # the captured gradients keep their (graph-pool) addresses on every replay
         self.opt.prepare()
-        if self.world > 1:
+        if self.ddp and self.buckets is None:
             self.g_gather, _, _ = graphs.capture(self._gather, pool=self.g_bwd.pool())
         self.g_opt, _, _ = graphs.capture(self._update, pool=self.g_bwd.pool())
 
     def __call__(self, batch=None):
         """One training step; `batch` (optional) is copied into the captured input buffers."""
         if batch is not None:
+            if self.graph and _rig_key(batch) != self._rig:
+                raise _lib.E2EPError(
+                    "TrainStep(graph=True) captured the lift-splat plan of the first batch's "
+                    "camera rig; this batch has different intrinsics/extrinsics (build a new "
+                    "TrainStep, or pass the rig as device tensors so the plan is rebuilt)")
             for k, v in batch.items():
                 if torch.is_tensor(v) and torch.is_tensor(self.batch.get(k)) and self.batch[k].is_cuda:
                     self.batch[k].copy_(v, non_blocking=True)
+        sync_lr = getattr(self.opt, "sync_lr", None)
+        if sync_lr is not None:
+            sync_lr()
         if not self.graph:
             self.loss = self._eager()
             return self.loss
         self.g_bwd.replay()
-        if self.world > 1:
+        if self.g_gather is not None:
             self.g_gather.replay()
-            if self._host_sync:
-                # gloo's CUDA all-reduce does not order itself after graph replays on this
-                # stack (it hangs); RCCL's does.  Only the gloo rehearsal path pays this.
-                torch.cuda.synchronize()
             self._allreduce()
         self.g_opt.replay()
         return self.loss

@@ -81,7 +81,17 @@ class ParkingTrainingModule(_Base):
         return d["val_loss"]
 
     def configure_optimizers(self):
-        opt = torch.optim.Adam(self.parameters(), lr=self.cfg.learning_rate,
-                               weight_decay=self.cfg.weight_decay)
+        """Adam(lr, weight_decay) + CosineAnnealingLR(T_max=epochs), as the reference
+        (trainer/pl_trainer.py:116-121).  On a HIP device the optimizer is the fused flat Adam
+        (same update; the schedule reaches its captured launches through a device LR scalar);
+        parameters that never receive a gradient (bev_encoder.layer4, reference
+        model/bev_encoder.py:21) are not stepped by either optimizer."""
+        params = [p for p in self.parameters() if p.requires_grad]
+        if params and params[0].is_cuda:
+            from e2ep_amd.optim import FlatAdam
+            opt = FlatAdam(params, lr=self.cfg.learning_rate, weight_decay=self.cfg.weight_decay)
+        else:
+            opt = torch.optim.Adam(params, lr=self.cfg.learning_rate,
+                                   weight_decay=self.cfg.weight_decay)
         sched = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer=opt, T_max=self.cfg.epochs)
         return {"optimizer": opt, "lr_scheduler": sched}

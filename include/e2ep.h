@@ -353,15 +353,19 @@ int e2ep_se_gate_bwd(const float *x, const float *a, const float *dy, int planes
  * offsets[tensor] = element offset of the tensor in the flat
  * param / exp_avg / exp_avg_sq buffers (multiple of 4).  Gradients come from grad_ptrs
  * (device array of per-tensor device addresses; 0 = no gradient, tensor not stepped) or,
- * if grad_flat is non-null, from a flat buffer laid out like the parameters.  `step` is a
- * device fp32 counter incremented by the call (graph-capturable: no host scalars change).
+ * if grad_flat is non-null, from a flat buffer laid out like the parameters (grad_ptrs, when
+ * also given, still marks the tensors without a gradient, which are skipped).  `step` is a
+ * device fp32 counter incremented by the call and `lr` a device fp64 scalar read by it, so a
+ * captured call follows an LR schedule (trainer/pl_trainer.py:120 CosineAnnealingLR) under
+ * graph replay: no host scalar that changes between steps is baked into the launch.
  * ------------------------------------------------------------------------------------- */
 int e2ep_adam_chunk_elems(void);
 int e2ep_adam_step(const int *chunks, int n_chunks, const long long *offsets,
                    const long long *grad_ptrs, const float *grad_flat, float *param, float *exp_avg,
-                   float *exp_avg_sq, float *step, double lr, double beta1, double beta2,
+                   float *exp_avg_sq, float *step, const double *lr, double beta1, double beta2,
                    double eps, double weight_decay, float grad_scale, void *stream);
-/* per-tensor gradients -> flat buffer (zeros for missing gradients), for one all-reduce */
+/* per-tensor gradients -> flat buffer (zeros for missing gradients), for the all-reduce;
+ * a sub-range of the chunk table (chunks + 4*first, n) gathers one gradient bucket */
 int e2ep_grad_gather(const int *chunks, int n_chunks, const long long *offsets,
                      const long long *grad_ptrs, float *grad_flat, void *stream);
 

@@ -1,0 +1,154 @@
+"""Data-parallel and LR-schedule paths of TrainStep on one MI355X.
+
+* The LR a captured step uses is a device scalar (FlatAdam.lr_dev): CosineAnnealingLR
+  (reference trainer/pl_trainer.py:120) changes it between replays exactly as it changes an
+  eager step.
+* RCCL at world 1: the bucketed, hook-driven all-reduce captured INTO the backward graph
+  (side-stream fork/join) gives the same parameters as the step without an exchange.
+* gloo at world 2, both ranks on cuda:0 (the one-GPU rehearsal of the N>1 path): the
+  host-staged flat gradient all-reduce of the real ParkingModel TrainStep with the same batch
+  on both ranks equals the one-process step (mean of two equal gradients), replay for replay.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+class _Small(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(3)
+        self.a = torch.nn.Linear(16, 32)
+        self.b = torch.nn.Linear(32, 4)
+
+    def training_step(self, batch, idx=0):
+        return (self.b(self.a(batch["x"]).relu()) - batch["y"]).pow(2).mean()
+
+
+def _small_batch():
+    g = torch.Generator().manual_seed(1)
+    return {"x": torch.randn(8, 16, generator=g).to(DEV), "y": torch.randn(8, 4, generator=g).to(DEV)}
+
+
+def test_lr_schedule_follows_under_graph_replay():
+    from e2ep_amd.optim import FlatAdam
+    from e2ep_amd.train import TrainStep
+    runs = {}
+    for graph in (False, True):
+        m = _Small().to(DEV)
+        opt = FlatAdam([p for p in m.parameters()], lr=1e-2, weight_decay=1e-4)
+        sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=4)
+        step = TrainStep(m, _small_batch(), graph=graph, warmup=1, optimizer=opt)
+        if not graph:
+            step()  # the graph run's one warm-up step (initial LR)
+        lrs = []
+        for _ in range(4):
+            step()
+            lrs.append(opt.param_groups[0]["lr"])
+            sched.step()
+        runs[graph] = (torch.cat([p.detach().reshape(-1) for p in m.parameters()]), lrs,
+                       float(opt.lr_dev))
+    (pe, lre, _), (pg, lrg, dev_lr) = runs[False], runs[True]
+    assert lre == lrg and lre[0] != lre[2]
+    assert dev_lr == lrg[-1]  # the device scalar the last replay read
+    assert rel_l2(pg, pe) < 1e-6
+    # LR 0 under replay: the captured Adam launch must not move the weights
+    m = _Small().to(DEV)
+    opt = FlatAdam(list(m.parameters()), lr=1e-2)
+    step = TrainStep(m, _small_batch(), graph=True, warmup=1, optimizer=opt)
+    step()
+    opt.param_groups[0]["lr"] = 0.0
+    before = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone()
+    step()
+    after = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    assert torch.equal(before, after)
+    opt.param_groups[0]["lr"] = 1e-2
+    step()
+    assert not torch.equal(after, torch.cat([p.detach().reshape(-1) for p in m.parameters()]))
+
+
+def _port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _parking_module(seed_noise=7):
+    from e2ep_amd import synthetic
+    from trainer.pl_trainer import ParkingTrainingModule
+    from tool.config import default_cfg
+    from weights import make_state
+    mod = ParkingTrainingModule(default_cfg(deterministic=True))
+    mod.parking_model.load_state_dict(make_state(mod.parking_model.state_dict(), 1234))
+    mod = mod.to(DEV).train()
+    for p in mod.parking_model.bev_encoder.layer4.parameters():
+        p.requires_grad_(False)
+    noise = synthetic.target_noise(1, seed=seed_noise).to(DEV)
+    mod.parking_model._noise = lambda b, device, n: noise
+    return mod
+
+
+def _parking_batch():
+    from e2ep_amd import synthetic
+    d = synthetic.synthetic_batch(1, seed=7)
+    return {k: (v if k in ("intrinsics", "extrinsics") else v.to(DEV)) for k, v in d.items()}
+
+
+def _flat_params(mod):
+    return torch.cat([p.detach().reshape(-1) for p in mod.parameters()]).cpu()
+
+
+def test_rccl_bucketed_allreduce_captured_in_backward_graph():
+    """world 1 over RCCL: the exchange is an identity, so the bucketed in-graph all-reduce
+    path must reproduce the plain step bit for bit."""
+    from e2ep_amd.train import TrainStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
+    try:
+        m_ref, m_ddp = _parking_module(), _parking_module()
+        s_ref = TrainStep(m_ref, _parking_batch(), graph=True, warmup=1)
+        s_ddp = TrainStep(m_ddp, _parking_batch(), graph=True, warmup=1, ddp=True, bucket_mb=4.0)
+        assert s_ddp.buckets is not None and len(s_ddp.buckets.buckets) >= 10
+        for _ in range(2):
+            l_ref, l_ddp = float(s_ref()), float(s_ddp())
+            assert l_ref == l_ddp
+        assert torch.equal(_flat_params(m_ref), _flat_params(m_ddp))
+    finally:
+        dist.destroy_process_group()
+
+
+def _gloo_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from e2ep_amd.train import TrainStep
+    m = _parking_module()
+    s = TrainStep(m, _parking_batch(), world=world, graph=True, warmup=1)
+    assert s.buckets is None and s._host is not None
+    losses = [float(s()) for _ in range(2)]
+    out[rank] = (losses, _flat_params(m))
+    dist.destroy_process_group()
+
+
+def test_gloo_two_rank_rehearsal_equals_one_process():
+    from e2ep_amd.train import TrainStep
+    m = _parking_module()
+    s = TrainStep(m, _parking_batch(), graph=True, warmup=1)
+    want_losses = [float(s()) for _ in range(2)]
+    want = _flat_params(m)
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_gloo_worker, args=(2, _port(), out), nprocs=2, join=True)
+        (l0, p0), (l1, p1) = out[0], out[1]
+    assert torch.equal(p0, p1)
+    assert l0 == want_losses and l1 == want_losses
+    assert torch.equal(p0, want)
