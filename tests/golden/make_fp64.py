@@ -6,7 +6,8 @@ Deterministic-train mode (BN batch statistics at B=2) is ill-conditioned: the re
 own fp32 result differs from this fp64 value by ~1e-3 on the segmentation logits and ~2 %
 on some weight gradients (the cumsum-difference pooling noise, SURVEY.md §0 fact 4, is
 amplified by batch-statistic BN).  Parity tests therefore measure both the product and the
-reference against this fp64 value.   Run: python tests/golden/make_fp64.py
+reference against this fp64 value.   Run: python tests/golden/make_fp64.py [b8]
+(b8: the same for the B=8 bench batch, model_train_b8.npz.)
 """
 import os
 import sys
@@ -34,6 +35,54 @@ def oracle_model(dtype):
     return m
 
 
+def sample(t):
+    """make_golden.sample: every k-th element, k = max(1, numel // 16384)."""
+    flat = t.detach().reshape(-1)
+    return flat[::max(1, flat.numel() // 16384)].clone()
+
+
+def main_b8():
+    """fp64 companion of model_train_b8.npz (same batch / noise seeds, same sampling)."""
+    import json
+    torch.set_num_threads(8)
+    m = oracle_model(torch.float64).train()
+    data = synthetic.synthetic_batch(8, seed=11)
+    noise = synthetic.target_noise(8, seed=11)
+    d = {k: (v.double() if v.is_floating_point() and k not in ("intrinsics", "extrinsics") else v)
+         for k, v in data.items()}
+    losses, (pc, ps, pd) = O.train_losses(m, d, noise)
+    losses["train_loss"].backward()
+    with open(os.path.join(HERE, "meta.json")) as f:
+        gkeys = json.load(f)["model_train_b8"]["grad_keys"]
+    params = dict(m.named_parameters())
+    fx = {"loss_control": np.float64(losses["control_loss"].item()),
+          "loss_seg": np.float64(losses["segmentation_loss"].item()),
+          "loss_depth": np.float64(losses["depth_loss"].item()),
+          "pred_control": pc.detach().numpy(),
+          "seg_sample": sample(ps).numpy(), "seg_norm": np.float64(ps.detach().norm()),
+          "depth_sample": sample(pd).numpy(), "depth_norm": np.float64(pd.detach().norm()),
+          "gnorm_all": np.array([float(params[k].grad.norm()) for k in gkeys])}
+    for k in make_grad_probe_keys(params.keys()):
+        fx["gsample::" + k] = sample(params[k].grad).numpy()
+    np.savez_compressed(os.path.join(HERE, "model_train_b8_fp64.npz"), **fx)
+    print("wrote model_train_b8_fp64.npz")
+    # eval-mode gradients (model_evalgrad_b8.npz)
+    m = oracle_model(torch.float64).eval()
+    losses, _ = O.train_losses(m, d, noise)
+    losses["train_loss"].backward()
+    with open(os.path.join(HERE, "meta.json")) as f:
+        gkeys = json.load(f)["model_evalgrad_b8"]["grad_keys"]
+    params = dict(m.named_parameters())
+    fx = {"loss_control": np.float64(losses["control_loss"].item()),
+          "loss_seg": np.float64(losses["segmentation_loss"].item()),
+          "loss_depth": np.float64(losses["depth_loss"].item()),
+          "gnorm_all": np.array([float(params[k].grad.norm()) for k in gkeys])}
+    for k in make_grad_probe_keys(params.keys()):
+        fx["gsample::" + k] = sample(params[k].grad).numpy()
+    np.savez_compressed(os.path.join(HERE, "model_evalgrad_b8_fp64.npz"), **fx)
+    print("wrote model_evalgrad_b8_fp64.npz")
+
+
 def main():
     torch.set_num_threads(8)
     m = oracle_model(torch.float64).train()
@@ -59,4 +108,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "b8":
+        main_b8()
+    else:
+        main()

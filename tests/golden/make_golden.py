@@ -1,6 +1,7 @@
 """Generate the golden vectors under tests/golden/ FROM THE REFERENCE ITSELF.
 
 Run in the build container only (needs /root/reference):  python tests/golden/make_golden.py
+(`python tests/golden/make_golden.py b8` regenerates only the B=8 fixtures.)
 
 The reference has no tests or fixtures of its own, so every golden vector is
 produced here by importing the reference's Python modules unmodified, with:
@@ -67,6 +68,14 @@ def install_shims():
         return orig_to(self, *a, **k)
 
     torch.Tensor.to = to
+    # the product tree mirrors the reference's package names (model, tool, loss, ...) as
+    # regular packages, which would shadow the reference's namespace packages: take it off
+    # the path (e2ep_amd.synthetic is already imported) so `model.*` is the reference's
+    prod = os.path.join(REPO, "e2e-parking-carla_amd")
+    sys.path[:] = [p for p in sys.path if os.path.abspath(p or ".") != prod]
+    for name in list(sys.modules):
+        if name.split(".")[0] in ("model", "tool", "loss", "trainer", "dataset"):
+            del sys.modules[name]
     sys.path.insert(0, REF)
 
 
@@ -98,7 +107,96 @@ def rel(a, b):
     return float((a - b).norm() / max(b.norm(), 1e-30))
 
 
-def main():
+SAMPLE = 16384
+
+
+def sample(t):
+    """A strided subsample of a large output (every k-th element of the flattened tensor,
+    k = max(1, numel // SAMPLE)); tests/test_model_b8_gpu.py recomputes the same indices."""
+    flat = t.detach().reshape(-1)
+    return flat[::max(1, flat.numel() // SAMPLE)].clone()
+
+
+def b8_fixtures(ref, orc, state, cfg, closs, sloss, dloss, meta):
+    """C2 bench workload (B=8, 4 x 256^2): eval forward + predict, and one deterministic-train
+    forward/backward with the three losses.  Full control logits; strided samples + norms of
+    the segmentation / depth outputs; every parameter's gradient norm and strided samples of
+    the probe tensors' gradients."""
+    B = 8
+    data = synthetic.synthetic_batch(B, seed=11)
+    noise = synthetic.target_noise(B, seed=11)
+    ref.load_state_dict(state)
+    orc.load_state_dict(state)
+    ref.eval(), orc.eval()
+    with torch.no_grad(), FixedRand(noise):
+        pc, ps, pd = ref(data)
+        tok, _, _, tgt = ref.predict({**data, "gt_control": data["gt_control"][:, :1]})
+    with torch.no_grad():
+        qc, qs, qd = orc(data, noise)
+    errs = {"control": rel(qc, pc), "seg": rel(qs, ps), "depth": rel(qd, pd)}
+    print("oracle vs reference, eval B=8:", errs)
+    assert max(errs.values()) < 1e-6
+    np.savez_compressed(os.path.join(OUT, "model_eval_b8.npz"), pred_control=pc.numpy(),
+                        seg_sample=sample(ps).numpy(), seg_norm=np.float64(ps.double().norm()),
+                        depth_sample=sample(pd).numpy(), depth_norm=np.float64(pd.double().norm()),
+                        predict_tokens=tok.numpy(), bev_target_sum=tgt.sum((1, 2, 3)).numpy())
+    meta["model_eval_b8"] = {"batch_seed": 11, "noise_seed": 11, "oracle_rel_err": errs,
+                             "sample": SAMPLE}
+
+    deterministic(ref)
+    probe = make_grad_probe_keys(state.keys())
+    # (3c') gradients in eval mode (BN on running statistics): the whole backward without the
+    # batch-statistic BN conditioning of train mode -- a well-conditioned gradient check
+    ref.load_state_dict(state)
+    ref.eval()
+    with FixedRand(noise):
+        pc, ps, pd = ref(data)
+    lc, ls, ld = closs(pc, data), sloss(ps.unsqueeze(1), data["segmentation"]), dloss(pd, data["depth"])
+    (lc + ls + ld).backward()
+    rgrad = dict(ref.named_parameters())
+    gkeys_e = [k for k, v in rgrad.items() if v.grad is not None]
+    fx = {"loss_control": np.float64(lc), "loss_seg": np.float64(ls), "loss_depth": np.float64(ld),
+          "gnorm_all": np.array([float(rgrad[k].grad.double().norm()) for k in gkeys_e])}
+    for k in probe:
+        fx["gsample::" + k] = sample(rgrad[k].grad).numpy()
+    np.savez_compressed(os.path.join(OUT, "model_evalgrad_b8.npz"), **fx)
+    meta["model_evalgrad_b8"] = {"batch_seed": 11, "noise_seed": 11, "probe": probe,
+                                 "grad_keys": gkeys_e, "sample": SAMPLE}
+    ref.zero_grad(set_to_none=True)
+
+    ref.load_state_dict(state)
+    orc.load_state_dict(state)
+    ref.train(), orc.train()
+    with FixedRand(noise):
+        pc, ps, pd = ref(data)
+    lc, ls, ld = closs(pc, data), sloss(ps.unsqueeze(1), data["segmentation"]), dloss(pd, data["depth"])
+    (lc + ls + ld).backward()
+    rgrad = dict(ref.named_parameters())
+    losses_o, _ = O.train_losses(orc, data, noise)
+    losses_o["train_loss"].backward()
+    ograd = dict(orc.named_parameters())
+    lerr = {"control": abs(float(lc) - float(losses_o["control_loss"])),
+            "seg": abs(float(ls) - float(losses_o["segmentation_loss"])),
+            "depth": abs(float(ld) - float(losses_o["depth_loss"]))}
+    gkeys = [k for k, v in rgrad.items() if v.grad is not None]
+    gerr = {k: rel(ograd[k].grad, rgrad[k].grad) for k in gkeys}
+    print("oracle vs reference, train B=8 losses:", lerr, "max grad rel:", max(gerr.values()))
+    assert max(lerr.values()) < 1e-5 and max(gerr.values()) < 1e-5
+    fx = {"loss_control": np.float64(lc), "loss_seg": np.float64(ls), "loss_depth": np.float64(ld),
+          "pred_control": pc.detach().numpy(),
+          "seg_sample": sample(ps).numpy(), "seg_norm": np.float64(ps.detach().double().norm()),
+          "depth_sample": sample(pd).numpy(), "depth_norm": np.float64(pd.detach().double().norm()),
+          "gnorm_all": np.array([float(rgrad[k].grad.double().norm()) for k in gkeys])}
+    for k in probe:
+        fx["gsample::" + k] = sample(rgrad[k].grad).numpy()
+    np.savez_compressed(os.path.join(OUT, "model_train_b8.npz"), **fx)
+    meta["model_train_b8"] = {"batch_seed": 11, "noise_seed": 11, "probe": probe,
+                              "grad_keys": gkeys, "sample": SAMPLE,
+                              "oracle_loss_abs_err": lerr,
+                              "oracle_grad_rel_err_max": max(gerr.values())}
+
+
+def main(only=None):
     install_shims()
     torch.set_num_threads(8)
     import yaml
@@ -114,6 +212,20 @@ def main():
     cfg.device = torch.device("cpu")
     meta = {"generator": "tests/golden/make_golden.py", "reference": REF,
             "torch": torch.__version__, "weights_seed": 1234}
+    if only == "b8":  # regenerate only the B=8 fixtures, keep the others and their meta
+        with open(os.path.join(OUT, "meta.json")) as f:
+            meta = json.load(f)
+        torch.manual_seed(0)
+        ref = ParkingModel(cfg)
+        state = make_state(ref.state_dict(), seed=1234)
+        orc = O.ParkingModelRef(O.Cfg, dropout=False)
+        b8_fixtures(ref, orc, state, cfg, ControlLoss(cfg),
+                    SegmentationLoss(class_weights=torch.Tensor(cfg.seg_vehicle_weights)),
+                    DepthLoss(cfg), meta)
+        with open(os.path.join(OUT, "meta.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+        print("wrote B=8 golden vectors to", OUT)
+        return
 
     # ---------------- (1) geometry / integer pillar index (model/bev_model.py:45-96) ----
     torch.manual_seed(0)
@@ -244,10 +356,13 @@ def main():
     meta["model_train_b2"] = {"batch_seed": 5, "noise_seed": 5, "probe": probe,
                               "oracle_loss_abs_err": lerr, "oracle_grad_rel_err_max": max(gerr.values())}
 
+    # (3c/3d) the C2 bench batch, B=8 (eval and deterministic-train)
+    b8_fixtures(ref, orc, state, cfg, closs, sloss, dloss, meta)
+
     with open(os.path.join(OUT, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print("wrote golden vectors to", OUT)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)
