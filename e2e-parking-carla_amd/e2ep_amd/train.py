@@ -92,10 +92,17 @@ class GradBuckets:
         return hook
 
     def arm(self):
+        """Start a step.  Called on the thread and stream that run forward/backward: the hooks
+        run on autograd's device thread, whose current stream inside a hook need not be the
+        stream the gradient kernels were issued on (under capture it can be a stream outside
+        the capture), so the bucket fork waits on an event of THIS stream."""
         self.pending = [i1 - i0 for (i0, i1, _, _) in self.buckets]
         self.next = 0
         self.works = []
         self.active = True
+        if self.cuda:
+            self.main = torch.cuda.current_stream()
+            self.capturing = torch.cuda.is_current_stream_capturing()
 
     def _arrived(self, i):
         b = self.of[i]
@@ -112,10 +119,15 @@ class GradBuckets:
             self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
             return
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream())
+        ev.record(self.main)
         self.comm.wait_event(ev)
+        here = torch.cuda.current_stream()
+        if not self.capturing and here != self.main:  # eager: also the hook thread's stream
+            ev2 = torch.cuda.Event()
+            ev2.record(here)
+            self.comm.wait_event(ev2)
         with torch.cuda.stream(self.comm):
-            if not torch.cuda.is_current_stream_capturing():
+            if not self.capturing:
                 self.opt.prepare(params=(i0, i1))  # fresh gradient addresses (eager)
             self.opt.gather_grads(self.flat, params=(i0, i1))
             self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
@@ -129,7 +141,7 @@ class GradBuckets:
         for w in self.works:
             w.wait()
         if self.cuda:
-            torch.cuda.current_stream().wait_stream(self.comm)
+            self.main.wait_stream(self.comm)
         self.works = []
         self.active = False
 

@@ -14,7 +14,9 @@ fp64 oracle):
   * eval-mode gradients (BN on running statistics: the full backward, well conditioned —
     the reference's own fp32 error is <= 1.3e-3, median 1.5e-5): losses <= 1e-5 vs ref;
     probe-gradient samples and every parameter's gradient norm held to
-    max(1e-4, 3 x the reference's own error) vs fp64 (BOUND_FACTOR).
+    max(1e-4, 3 x the reference's own error) vs fp64 (BOUND_FACTOR); for the per-tensor
+    gradient norms "the reference's own error" is the larger of its error on that tensor and
+    its median error over all tensors.
   * deterministic-train (BN batch statistics over 32 cameras / 8 BEV samples): the
     reference's own fp32 error reaches 3.4e-2 on camera-encoder gradients and ~1e-3 on the
     segmentation logits (cancellation in the batch-statistic BN backward); the same
@@ -80,11 +82,13 @@ def _norms3(section, gkeys, params, n32, n64):
     floor = 1e-3 * float(np.sqrt(np.mean(n64 ** 2)))
     den = np.maximum(n64, floor)
     e32, e64, eref = np.abs(got - n32) / den, np.abs(got - n64) / den, np.abs(n32 - n64) / den
-    worst = int(np.argmax(e64 - np.maximum(TOL, BOUND_FACTOR * eref)))
+    # per tensor: the reference's own error on that tensor, or (when it happens to land close
+    # to fp64 on one norm) its typical error over all tensors
+    bound = np.maximum(TOL, BOUND_FACTOR * np.maximum(eref, np.median(eref)))
+    worst = int(np.argmax(e64 / bound))
     _record(section, "grad_norms(all %d)" % len(gkeys), vs_ref_max=e32.max(), vs_fp64_max=e64.max(),
             ref_vs_fp64_max=eref.max(), vs_fp64_median=np.median(e64),
-            ref_vs_fp64_median=np.median(eref))
-    bound = np.maximum(TOL, BOUND_FACTOR * eref)
+            ref_vs_fp64_median=np.median(eref), worst_ratio_to_bound=e64[worst] / bound[worst])
     assert (e64 <= bound).all(), (gkeys[worst], e64[worst], eref[worst])
 
 
