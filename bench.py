@@ -10,9 +10,11 @@ B-sample batch (4 x 256x256 cameras) that is resident in HBM bef
 N>1: one rank per GPU, RCCL over xGMI.  Under torch.distributed.run (WORLD_SIZE set) the ranks
 are already there; from a plain command line `--gpus N` re-launches this script under
 torch.distributed.run with N ranks before anything touches the GPU.  Each rank runs B samples
-per step (weak scaling); the gradients are all-reduced in ~25 MB buckets issued during
-backward (the only exchange, captured into the backward graph).  The step is captured into
-HIP graphs during warm-up (e2ep_amd.train.TrainStep; --eager disables capture).
+per step (weak scaling); the flat 78 MB gradient buffer is all-reduced once per step between
+the backward and optimizer graph replays (the only exchange; e2ep_amd.train explains why it
+is not captured).  The step is captured into HIP graphs during warm-up
+(e2ep_amd.train.TrainStep; --eager disables capture and overlaps ~25 MB bucket all-reduces
+with backward instead).
 Rank 0 prints ONE JSON line.
 """
 import argparse

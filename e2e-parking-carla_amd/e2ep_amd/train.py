@@ -11,24 +11,25 @@ __call__ refreshes from param_groups[0]['lr'] before each replay, so an LR sched
 (the reference's CosineAnnealingLR) acts on the captured step.
 
 Data parallelism (one process per GPU, RCCL over xGMI; DistributedDataParallel semantics
-without its module wrapper): the flat fp32 gradient buffer (FlatAdam's layout) is cut into
-buckets of ~25 MB in reverse layout order (the order backward produces gradients).  A
-post-accumulate-grad hook per parameter counts arrivals; when a bucket is complete (and every
-earlier bucket has been issued — the same order on every rank), a side stream waits on an
-event recorded on the compute stream, gathers the bucket's gradients into the flat buffer
-(one launch) and all-reduces that slice asynchronously, so the exchange overlaps the rest of
-backward.  After backward the compute stream waits for every bucket; the 1/world mean is
-folded into the Adam launch.  With RCCL the hooks fire during capture, so the gathers and
-all-reduces are nodes of the backward graph (forked onto the side stream and joined before
-the optimizer).  gloo cannot be captured and does not order itself against HIP streams: with
-gloo and device tensors (the one-GPU rehearsal) the flat buffer is gathered after backward and
-staged explicitly through pinned host memory (copy, host waits on the stream, all-reduce on
-the host, copy back), in eager and graph mode alike.
+without its module wrapper), one flat fp32 gradient buffer in FlatAdam's layout; the
+1/world mean is folded into the Adam launch.
+  * graph mode (the bench): g_bwd (fwd + losses + bwd) -> g_gather (per-tensor gradients ->
+    flat buffer, one launch) -> ONE all-reduce of the 78 MB buffer issued from the host
+    between the replays -> g_opt.  The collective is not captured: on this stack (torch
+    2.10 / RCCL 2.26) a captured ProcessGroupNCCL collective makes the c10d watchdog fault
+    on its capture-time event, and a backward graph with bucket gathers forked onto a side
+    stream replayed wrong camera-encoder gradients (scripts/diag_ddp*.py).
+  * eager mode: DDP-style overlap — the buffer is cut into ~25 MB buckets in reverse layout
+    order; a post-accumulate-grad hook per parameter counts arrivals and, when a bucket is
+    complete (and every earlier one issued: the same order on every rank), a side stream
+    waits on an event of the forward/backward stream, gathers the bucket and all-reduces
+    it asynchronously while backward continues.
+  * gloo with device tensors (the one-GPU rehearsal): gloo does not order itself against
+    HIP streams, so the flat buffer is staged explicitly through pinned host memory (copy,
+    the host waits for the stream, all-reduce on the host, copy back).
 
-Graph replay order per step: g_bwd (fwd + losses + bwd [+ bucket all-reduces]) ->
-[g_gather -> host-staged all-reduce (gloo)] -> g_opt.  Graphs are captured through
-e2ep_amd.graphs.capture, which repairs memset nodes (they do not replay correctly on this
-ROCm stack) before instantiation.
+Graphs are captured through e2ep_amd.graphs.capture, which repairs memset nodes (they do
+not replay correctly on this ROCm stack) before instantiation.
 
 Graph mode captures the lift-splat pillar plan of the batch's (host) rig: a later batch with
 a different intrinsics/extrinsics rig raises instead of silently training on the captured
@@ -165,9 +166,9 @@ class TrainStep:
         self.backend = dist.get_backend() if self.ddp else None
         if overlap is None:
             overlap = os.environ.get("E2EP_DDP_OVERLAP", "1") != "0"
-        # hook-driven bucket all-reduce: RCCL (eager or captured) and host tensors (gloo on
-        # CPU); gloo with device tensors is host-staged after backward instead
-        self.overlap = bool(self.ddp and overlap and
+        # hook-driven bucket all-reduce overlapping backward: eager steps with RCCL, and host
+        # tensors (gloo on CPU); never inside a captured graph (module docstring)
+        self.overlap = bool(self.ddp and overlap and not graph and
                             (self.backend == "nccl" or not self.flat_grad.is_cuda))
         self.buckets = (GradBuckets(self.params, self.opt, self.flat_grad, bucket_mb)
                         if self.overlap else None)

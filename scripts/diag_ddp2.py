@@ -92,7 +92,7 @@ _orig_launch = T.GradBuckets._launch
 
 
 def _spy(self, b):
-    if b in (0, 14, 15, 24) and not getattr(self, "_spied", False):
+    if b in (0,) and not getattr(self, "_spied", False):
         cur = torch.cuda.current_stream()
         print(f"   bucket {b}: hook stream {cur.cuda_stream:#x} main {self.main.cuda_stream:#x} "
               f"capturing(main)={self.capturing} capturing(hook)={torch.cuda.is_current_stream_capturing()}",
@@ -120,9 +120,19 @@ for stub in (True, False):
     print(f"C stub={stub}: max|diff| {d:.3e}, nan count {bad}, n buckets {len(s_ddp.buckets.buckets)}",
           flush=True)
     # which buckets are wrong
-    for b, (i0, i1, lo, hi) in enumerate(s_ddp.buckets.buckets):
-        dd = (gref[lo:hi] - s_ddp.flat_grad[lo:hi]).abs().max().item()
-        if not dd == 0.0:
-            print("   bucket", b, "params", i0, i1, "maxdiff", dd, flush=True)
+    names = [n for n, p in m_ddp.named_parameters() if p.requires_grad]
+    nbad = 0
+    for i, (o, n) in enumerate(s_ddp.opt.spans):
+        a, b = gref[o:o + n], s_ddp.flat_grad[o:o + n]
+        dd = (a - b).abs().max().item()
+        if dd != 0.0:
+            nbad += 1
+            if nbad <= 12 or i < 3:
+                pg = dict(m_ddp.named_parameters())[names[i]].grad
+                print(f"   param {i} {names[i]} n={n} maxdiff {dd:.3e} |ref| {a.abs().max().item():.3e} "
+                      f"|flat| {b.abs().max().item():.3e} ddp.grad==ref {torch.equal(pg.reshape(-1), a)} "
+                      f"flat==ddp.grad {torch.equal(pg.reshape(-1), b)} gtab ok "
+                      f"{int(s_ddp.opt._gtab[i]) == pg.data_ptr()}", flush=True)
+    print("   params wrong:", nbad, "of", len(names), flush=True)
 dist.all_reduce = real
 dist.destroy_process_group()

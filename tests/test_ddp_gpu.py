@@ -3,8 +3,10 @@
 * The LR a captured step uses is a device scalar (FlatAdam.lr_dev): CosineAnnealingLR
   (reference trainer/pl_trainer.py:120) changes it between replays exactly as it changes an
   eager step.
-* RCCL at world 1: the bucketed, hook-driven all-reduce captured INTO the backward graph
-  (side-stream fork/join) gives the same parameters as the step without an exchange.
+* RCCL at world 1 (the exchange is an identity): the graph-mode step (captured gather, host-
+  issued flat all-reduce, captured Adam) and the eager step with the bucketed, hook-driven
+  all-reduce overlapping backward both give the same parameters as the step without an
+  exchange, bit for bit.
 * gloo at world 2, both ranks on cuda:0 (the one-GPU rehearsal of the N>1 path): the
   host-staged flat gradient all-reduce of the real ParkingModel TrainStep with the same batch
   on both ranks equals the one-process step (mean of two equal gradients), replay for replay.
@@ -107,18 +109,20 @@ def _flat_params(mod):
     return torch.cat([p.detach().reshape(-1) for p in mod.parameters()]).cpu()
 
 
-def test_rccl_bucketed_allreduce_captured_in_backward_graph():
-    """world 1 over RCCL: the exchange is an identity, so the bucketed in-graph all-reduce
-    path must reproduce the plain step bit for bit."""
+@pytest.mark.parametrize("graph", [True, False])
+def test_rccl_world1_exchange_is_exact(graph):
     from e2ep_amd.train import TrainStep
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
     try:
         m_ref, m_ddp = _parking_module(), _parking_module()
-        s_ref = TrainStep(m_ref, _parking_batch(), graph=True, warmup=1)
-        s_ddp = TrainStep(m_ddp, _parking_batch(), graph=True, warmup=1, ddp=True, bucket_mb=4.0)
-        assert s_ddp.buckets is not None and len(s_ddp.buckets.buckets) >= 10
-        for _ in range(2):
+        s_ref = TrainStep(m_ref, _parking_batch(), graph=graph, warmup=1)
+        s_ddp = TrainStep(m_ddp, _parking_batch(), graph=graph, warmup=1, ddp=True, bucket_mb=4.0)
+        if graph:
+            assert s_ddp.buckets is None and s_ddp.g_gather is not None
+        else:
+            assert s_ddp.buckets is not None and len(s_ddp.buckets.buckets) >= 10
+        for _ in range(3):
             l_ref, l_ddp = float(s_ref()), float(s_ddp())
             assert l_ref == l_ddp
         assert torch.equal(_flat_params(m_ref), _flat_params(m_ddp))
