@@ -173,7 +173,8 @@ class TrainStep:
         self.buckets = (GradBuckets(self.params, self.opt, self.flat_grad, bucket_mb)
                         if self.overlap else None)
         self._host = (torch.empty(self.opt.numel, dtype=torch.float32, pin_memory=True)
-                      if self.ddp and not self.overlap and self.flat_grad.is_cuda else None)
+                      if self.ddp and self.backend != "nccl" and not self.overlap
+                      and self.flat_grad.is_cuda else None)
         self.loss = None
         self.g_bwd = self.g_gather = self.g_opt = None
         self._rig = _rig_key(batch)

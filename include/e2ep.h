@@ -370,6 +370,45 @@ int e2ep_grad_gather(const int *chunks, int n_chunks, const long long *offsets,
                      const long long *grad_ptrs, float *grad_flat, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Training losses (fp32; fixed-order reductions; every scalar stays on the device):
+ *  - control CE (loss/control_loss.py:15-19): logits [B*T, vocab], targets
+ *    gt[b*gt_stride + gt_offset + t] (int64, the reference's gt_control[:, 1:]), rows whose
+ *    target is `pad` ignored, mean over the rest.  fwd writes loss, lse [B*T] and count
+ *    (non-ignored rows) for bwd; workspace e2ep_control_ce_workspace(B*T) bytes.
+ *  - segmentation CE (loss/seg_loss.py:12-26): logits [images, C, HW], target [images, HW]
+ *    int64, class weights [C]; per-pixel weighted CE, `ignore` pixels contribute 0, plain
+ *    mean over all images*HW pixels; workspace e2ep_seg_ce_workspace(images, HW) bytes.
+ *  - depth BCE (loss/depth_loss.py:18-48): prob [BN, D, H/down, W/down] softmax
+ *    probabilities, gt [BN, H, W] metric depth; label of a cell = one-hot(D+1)[1:] of
+ *    trunc((min non-zero depth of its down x down block - lo) / step) (bins outside [0, D+1)
+ *    -> 0; lo = d_bound[0] - d_bound[2], step = d_bound[2]); BCE (log clamped at -100) over
+ *    the cells with a label, summed / max(1, #such cells).  fwd writes loss, den (the
+ *    normaliser) and cls [BN*h*w] (the class, 0 = background) for bwd; workspace
+ *    e2ep_depth_bce_workspace(BN, H, W, down) bytes.
+ * Backward kernels read the upstream gradient `gloss` (a device scalar) and write the full
+ * input gradient (zeros where the loss does not depend on the input).
+ * ------------------------------------------------------------------------------------- */
+size_t e2ep_control_ce_workspace(int rows);
+int e2ep_control_ce_fwd(const float *logits, const long long *gt, int B, int T, int gt_stride,
+                        int gt_offset, int vocab, int pad, float *loss, float *lse, float *count,
+                        void *workspace, void *stream);
+int e2ep_control_ce_bwd(const float *logits, const long long *gt, const float *lse,
+                        const float *count, const float *gloss, int B, int T, int gt_stride,
+                        int gt_offset, int vocab, int pad, float *dlogits, void *stream);
+size_t e2ep_seg_ce_workspace(int images, int HW);
+int e2ep_seg_ce_fwd(const float *logits, const long long *target, const float *weights, int images,
+                    int C, int HW, int ignore, float *loss, void *workspace, void *stream);
+int e2ep_seg_ce_bwd(const float *logits, const long long *target, const float *weights,
+                    const float *gloss, int images, int C, int HW, int ignore, float *dlogits,
+                    void *stream);
+size_t e2ep_depth_bce_workspace(int BN, int H, int W, int down);
+int e2ep_depth_bce_fwd(const float *prob, const float *gt, int BN, int D, int H, int W, int down,
+                       float lo, float step, float *loss, float *den, int *cls, void *workspace,
+                       void *stream);
+int e2ep_depth_bce_bwd(const float *prob, const int *cls, const float *den, const float *gloss,
+                       int BN, int D, int hw, float *dprob, void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * HIP-graph surgery: replace every memset node of a captured (not yet instantiated)
  * hipGraph_t by an equivalent kernel node.  Memset nodes replay incorrectly after the first
  * launch on this ROCm stack; PyTorch's reductions capture them.  `replaced` (optional)
