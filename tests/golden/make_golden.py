@@ -136,6 +136,19 @@ def b8_fixtures(ref, orc, state, cfg, closs, sloss, dloss, meta):
     errs = {"control": rel(qc, pc), "seg": rel(qs, ps), "depth": rel(qd, pd)}
     print("oracle vs reference, eval B=8:", errs)
     assert max(errs.values()) < 1e-6
+    # validation_step arithmetic (trainer/pl_trainer.py:85-114) on the eval-mode outputs:
+    # the reference's ControlValLoss / SegmentationLoss / DepthLoss modules
+    from loss.control_loss import ControlValLoss
+    with torch.no_grad():
+        acc_steer, reverse = ControlValLoss(cfg)(pc, data)
+        seg_v = sloss(ps.unsqueeze(1), data["segmentation"])
+        dep_v = dloss(pd, data["depth"])
+    val = {"acc_steer_val_loss": acc_steer, "reverse_val_loss": reverse,
+           "segmentation_val_loss": seg_v, "depth_val_loss": dep_v}
+    val["val_loss"] = sum(val.values())
+    np.savez_compressed(os.path.join(OUT, "validation_b8.npz"),
+                        **{k: np.float64(v) for k, v in val.items()})
+    meta["validation_b8"] = {"batch_seed": 11, "noise_seed": 11, "mode": "eval"}
     np.savez_compressed(os.path.join(OUT, "model_eval_b8.npz"), pred_control=pc.numpy(),
                         seg_sample=sample(ps).numpy(), seg_norm=np.float64(ps.double().norm()),
                         depth_sample=sample(pd).numpy(), depth_norm=np.float64(pd.double().norm()),

@@ -178,3 +178,26 @@ def test_b8_deterministic_train_step_matches_reference():
         _check3("train_b8", "grad " + k, sample(params[k].grad), g32["gsample::" + k],
                 g64["gsample::" + k])
     _norms3("train_b8", info["grad_keys"], params, g32["gnorm_all"], g64["gnorm_all"])
+
+
+def test_b8_validation_step_matches_reference():
+    """validation_step (trainer/pl_trainer.py:85-114) in eval mode: ControlValLoss
+    (detokenised acc/steer SmoothL1 + reverse-mass CE, loss/control_loss.py:22-75), the
+    segmentation and depth losses and their sum, each <= 1e-5 relative to the reference."""
+    from trainer.pl_trainer import ParkingTrainingModule
+    from tool.config import default_cfg
+    from weights import make_state
+    g = golden("validation_b8.npz")
+    mod = ParkingTrainingModule(default_cfg(deterministic=True))
+    mod.parking_model.load_state_dict(make_state(mod.parking_model.state_dict(), 1234))
+    mod = mod.to(DEV).eval()
+    data, noise = _batch()
+    with torch.no_grad():
+        val = mod.validation_step(data, 0, noise)
+    logged = mod.logged
+    assert set(logged) == set(g)
+    for k in g:
+        e = abs(float(logged[k]) / float(g[k]) - 1)
+        _record("validation_b8", k, vs_ref=e)
+        assert e < 1e-5, (k, float(logged[k]), float(g[k]))
+    assert float(val) == float(logged["val_loss"])
