@@ -14,6 +14,11 @@ def _ws(nbytes, device):
     return torch.empty(nbytes // 4, dtype=torch.float32, device=device) if nbytes else None
 
 
+def _rname(kind, dims, extra=""):
+    """Timing-region name: per shape when E2EP_TIMING_DETAIL=1 (scripts/conv_breakdown.py)."""
+    return f"{kind}{tuple(dims)}{extra}" if timing.detail() else kind
+
+
 def conv_flops(dims, in_channels=None):
     """Algorithmic FLOPs of one conv launch (fwd, or dgrad / wgrad over in_channels):
     2 * N * Cout * P * Q * Cin * R * S."""
@@ -36,7 +41,7 @@ def conv_fwd(x, w, b, dims, act, y, w_layout=0):
     """Launch the forward conv into y (handles the split-K workspace)."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_fwd_workspace(d), x.device)
-    with timing.region("conv_fwd", conv_flops(dims)):
+    with timing.region(_rname("conv_fwd", dims), conv_flops(dims)):
         _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
                   _lib.ptr(y), _lib.ptr(ws), _lib.stream())
     return y
@@ -46,7 +51,7 @@ def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0, res=None):
     """dx = data gradient (+ res, a residual gradient in dx's layout, added in the epilogue)."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_dgrad_workspace(d, m_channels), gy.device)
-    with timing.region("conv_dgrad", conv_flops(dims, m_channels)):
+    with timing.region(_rname("conv_dgrad", dims, f"gc{m_channels}"), conv_flops(dims, m_channels)):
         _lib.call("e2ep_conv_dgrad_acc", _lib.ptr(gy), _lib.ptr(w), d, m_channels, w_layout,
                   _lib.ptr(res), _lib.ptr(dx), _lib.ptr(ws), _lib.stream())
     return dx
@@ -56,7 +61,7 @@ def conv_wgrad(gy, x, dims, dw):
     d = _lib.dims(dims)
     splits = _lib.load().e2ep_conv_wgrad_splits(d)
     ws = torch.empty(splits * dw.numel(), dtype=torch.float32, device=gy.device)
-    with timing.region("conv_wgrad", conv_flops(dims)):
+    with timing.region(_rname("conv_wgrad", dims), conv_flops(dims)):
         _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws),
                   _lib.ptr(dw), 0, _lib.stream())
     return dw

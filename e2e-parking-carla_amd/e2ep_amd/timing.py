@@ -4,6 +4,7 @@ bench.py enables it for a few eager steps right after its timed (graph-replayed)
 measure the dominant kernel's average launch duration live (the `roofline.achieved`
 figure); it is off by default and then costs one boolean test per launch.  Never enable it
 while a step is being captured into a HIP graph."""
+import os
 from collections import defaultdict
 from contextlib import contextmanager
 
@@ -12,6 +13,11 @@ import torch
 _enabled = False
 _events = defaultdict(list)
 _work = defaultdict(float)
+
+
+def detail():
+    """Per-shape region names (E2EP_TIMING_DETAIL=1), for breakdown scripts only."""
+    return _enabled and os.environ.get("E2EP_TIMING_DETAIL") == "1"
 
 
 def enable(flag=True):
