@@ -47,6 +47,17 @@ struct ConvGeom {
 
 __device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
+// Tap liveness: does any output position o in [0, n_out) read an input o*step + d inside
+// [0, n_in)?  A filter tap that never does only multiplies zero padding (the DeepLab ASPP
+// branches at dilation 24 / 36 on 16x16 maps, reference model/convolutions.py:218-225: 8 of
+// their 9 taps), so the GEMMs skip it: the sums are unchanged (those products are exact
+// zeros) and the weight gradient of such a tap is exactly 0.
+__host__ __device__ __forceinline__ bool axis_live(int d, int n_out, int step, int n_in) {
+  if (n_out <= 0) return false;
+  const int o0 = d >= 0 ? 0 : (-d + step - 1) / step;
+  return o0 < n_out && o0 * step + d < n_in;
+}
+
 // ------------------------------------------------------------------------------------------
 // forward (MODE 0) / data-gradient (MODE 1) implicit GEMM
 // ------------------------------------------------------------------------------------------
@@ -107,10 +118,12 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
         int dx;
         if (MODE == 0) {
           dx = s * g.dw - g.pw;
+          if (!axis_live(dy, g.P, g.sh, g.H) || !axis_live(dx, g.Q, g.sw, g.W)) continue;
         } else {
           const int nx = px + g.pw - s * g.dw;
           if (((nx % g.sw) + g.sw) % g.sw) continue;
           dx = floordiv(nx, g.sw);
+          if (!axis_live(dy, Hc, 1, g.P) || !axis_live(dx, Wc, 1, g.Q)) continue;
         }
         s_tdy[n] = dy;
         s_tdx[n] = dx;
@@ -336,17 +349,29 @@ __global__ void k_conv_reduce(const float *__restrict__ part, int splits, int M,
 // ------------------------------------------------------------------------------------------
 constexpr int WBN = 64;
 
+// live filter taps (axis_live on both axes): the weight-gradient GEMM runs over the columns
+// (ci, live tap) only; the dead taps' gradient is written as 0 by k_reduce_splits
+struct TapList {
+  int n;
+  unsigned long long mask;  // bit tap = live (R*S <= MAXTAPS = 64)
+  int tap[MAXTAPS];
+};
+
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
     const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
-    ConvGeom g, int pix_per_split) {
+    ConvGeom g, int pix_per_split, TapList tl) {
   __shared__ float As[2][BK][BM + PADA];   // As[pixel][co]
   __shared__ float Bs[2][BK][WBN + PADB];  // Bs[pixel][col]
+  __shared__ int s_tap[MAXTAPS];
+  if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
+  __syncthreads();
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
   const int RS = g.R * g.S;
-  const int Kw = g.Cin * RS;
+  const int Kw = g.Cin * RS;       // columns of dW (ci-major, tap-minor)
+  const int Kl = g.Cin * tl.n;     // live columns this GEMM computes: (ci, live tap index)
   const int n0 = blockIdx.x * WBN;
   const int m0 = blockIdx.y * BM;
   const int split = blockIdx.z;
@@ -366,14 +391,14 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + trow + 16 * j;
-    const int cc = col < Kw ? col : 0;
-    const int ci = cc / RS, tap = cc - ci * RS;
+    const int cc = col < Kl ? col : 0;
+    const int ci = cc / tl.n, tap = s_tap[cc - ci * tl.n];
     const int r = tap / g.S, s = tap - r * g.S;
     cdy[j] = r * g.dh - g.ph;
     cdx[j] = s * g.dw - g.pw;
     cconst[j] = ci * HW + cdy[j] * g.W + cdx[j];
     // an out-of-range column gets an impossible row displacement: never in bounds
-    if (col >= Kw) cdy[j] = -(1 << 29);
+    if (col >= Kl) cdy[j] = -(1 << 29);
   }
   const int arow = (m0 + trow) * PQ;  // gout row of this thread's first co
   int p_cur = pbeg + tp;
@@ -443,11 +468,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
     }
   }
   const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
-  const int col = n0 + 32 * wn + li;
+  const int lcol = n0 + 32 * wn + li;
+  const int lci = lcol < Kl ? lcol / tl.n : 0;
+  const int col = lci * RS + s_tap[lcol < Kl ? lcol - lci * tl.n : 0];  // dW column
 #pragma unroll
   for (int rr = 0; rr < 16; ++rr) {
     const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
-    const bool ok = co < g.Cout && col < Kw;
+    const bool ok = co < g.Cout && lcol < Kl;
     bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[rr]);
   }
 }
@@ -588,14 +615,18 @@ __global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gou
 // fixed-order sum of the split slabs (+ optional accumulate into an existing gradient).
 // Block = 64 outputs x 16 split lanes: thread (o, r) sums splits r, r+16, ... with 4
 // independent chains, then the 16 lane sums are added in order through LDS.
+// Entries i whose tap (i % RS) is not live in `mask` are never written by the GEMM: their
+// result is 0 (a weight tap that only ever meets zero padding).
 __global__ void __launch_bounds__(1024) k_reduce_splits(const float *__restrict__ part, int splits,
                                                         int n, float *__restrict__ out,
-                                                        int accumulate) {
+                                                        int accumulate, int RS,
+                                                        unsigned long long mask) {
   __shared__ float red[16][64];
   const int o = threadIdx.x & 63, r = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + o;
+  const bool live = (mask >> (i % RS)) & 1ULL;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (i < n) {
+  if (i < n && live) {
     int k = r;
     for (; k + 48 < splits; k += 64) {
       s0 += part[(size_t)(k + 0) * n + i];
@@ -820,13 +851,36 @@ static bool geom_ok(const ConvGeom &g) {
          4LL * g.N * g.Cin * g.H * g.W < (1LL << 31) && 4LL * g.N * g.Cout * g.P * g.Q < (1LL << 31);
 }
 
-static int valid_taps(int p, int pad, int K, int dil, int st) {
+static int floordiv_h(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+// live taps of one axis (the kernels' tap tables apply the same rules): forward, or data-
+// gradient phase p (stride-phase split, cols = the phase's column count)
+static int live_taps_axis(int mode, int p, int pad, int K, int dil, int st, int n_in, int n_out,
+                          int cols) {
   int n = 0;
   for (int r = 0; r < K; ++r) {
-    const int v = p + pad - r * dil;
-    if (((v % st) + st) % st == 0) ++n;
+    if (mode == 0) {
+      n += axis_live(r * dil - pad, n_out, st, n_in);
+    } else {
+      const int v = p + pad - r * dil;
+      if (((v % st) + st) % st) continue;
+      n += axis_live(floordiv_h(v, st), cols, 1, n_out);
+    }
   }
   return n;
+}
+
+static TapList live_taps(const ConvGeom &g) {
+  TapList t;
+  t.n = 0;
+  t.mask = 0;
+  for (int r = 0; r < g.R; ++r)
+    for (int c = 0; c < g.S; ++c)
+      if (axis_live(r * g.dh - g.ph, g.P, g.sh, g.H) && axis_live(c * g.dw - g.pw, g.Q, g.sw, g.W)) {
+        t.tap[t.n++] = r * g.S + c;
+        t.mask |= 1ULL << (r * g.S + c);
+      }
+  return t;
 }
 
 struct GemmPlan {
@@ -843,7 +897,8 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
   p.nph = mode ? g.sh * g.sw : 1;
   if (mode == 0) {
     p.ncols = (long long)g.N * g.P * g.Q;
-    kmax = g.R * g.S * csteps;
+    kmax = live_taps_axis(0, 0, g.ph, g.R, g.dh, g.sh, g.H, g.P, 0) *
+           live_taps_axis(0, 0, g.pw, g.S, g.dw, g.sw, g.W, g.Q, 0) * csteps;
   } else {
     p.ncols = 0;
     kmax = 0;
@@ -852,7 +907,8 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
       const long long Hp = py < g.H ? (g.H - py + g.sh - 1) / g.sh : 0;
       const long long Wp = px < g.W ? (g.W - px + g.sw - 1) / g.sw : 0;
       p.ncols = std::max(p.ncols, (long long)g.N * Hp * Wp);
-      const int taps = valid_taps(py, g.ph, g.R, g.dh, g.sh) * valid_taps(px, g.pw, g.S, g.dw, g.sw);
+      const int taps = live_taps_axis(1, py, g.ph, g.R, g.dh, g.sh, g.H, g.P, (int)Hp) *
+                       live_taps_axis(1, px, g.pw, g.S, g.dw, g.sw, g.W, g.Q, (int)Wp);
       kmax = std::max(kmax, taps * csteps);
     }
   }
@@ -984,7 +1040,7 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
   if (wgrad1x1_ok(g)) return wgrad1x1_splits(g);
-  const long long base = (long long)cdiv(g.Cin * g.R * g.S, WBN) * cdiv(g.Cout, BM);
+  const long long base = (long long)cdiv(g.Cin * std::max(1, live_taps(g).n), WBN) * cdiv(g.Cout, BM);
   const long long pix = (long long)g.N * g.P * g.Q;
   long long want = (1024 + base - 1) / base;
   long long cap = pix / 256;
@@ -1021,20 +1077,23 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
 #undef W1_LAUNCH
     const int n = g.Cout * g.Cin;
     hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
-                       accumulate);
+                       accumulate, 1, 1ULL);
     return launch_status("e2ep_conv_wgrad");
   }
   const int Ptot = g.N * g.P * g.Q;
   int per = (Ptot + splits - 1) / splits;
   per = (per + BK - 1) / BK * BK;
   const int used = (Ptot + per - 1) / per;
-  dim3 grid(cdiv(g.Cin * g.R * g.S, WBN), cdiv(g.Cout, BM), used);
+  const TapList tl = live_taps(g);
   hipStream_t s = as_stream(stream);
   float *part = static_cast<float *>(workspace);
-  hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per);
+  if (tl.n > 0) {
+    dim3 grid(cdiv(g.Cin * tl.n, WBN), cdiv(g.Cout, BM), used);
+    hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+  }
   const int n = g.Cout * g.Cin * g.R * g.S;
   hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
-                     accumulate);
+                     accumulate, g.R * g.S, tl.mask);
   return launch_status("e2ep_conv_wgrad");
 }
 

@@ -40,6 +40,9 @@ CASES = [
     (3, 24, 16, 16, 24, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),     # direct fwd 1x1 K=24
     (2, 1, 30, 30, 64, 5, 5, 2, (2, 2, 2, 2), 1, False, 0),      # direct K=25, Cout=64, s2
     (2, 3, 21, 23, 17, 3, 3, 1, (2, 2, 2, 2), 2, False, 0),      # direct, dilated, ragged Cout
+    (4, 160, 16, 16, 64, 3, 3, 1, (36, 36, 36, 36), 36, False, 0),  # ASPP dilation 36: 8 dead taps
+    (2, 16, 9, 7, 24, 5, 5, 2, (9, 9, 9, 9), 3, False, 1),       # strided, dead taps both axes
+    (2, 40, 6, 6, 32, 3, 3, 1, (8, 0, 1, 7), 8, True, 0),        # asymmetric pad: dead rows/cols
 ]
 
 
