@@ -157,6 +157,12 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of
  * e2ep_conv_wgrad_workspace bytes) are summed in a fixed order: deterministic. */
+/* Forward / data-gradient GEMM selection (tests, benchmarks): 0 = automatic (default),
+ * 1 = always the first-generation kernel, 2 = the second-generation kernel (k-contiguous LDS
+ * fragments, no padded channel steps) wherever its limits allow.  Returns the previous value;
+ * a value outside 0..2 only queries.  Process-global; not thread-safe against concurrent
+ * launches. */
+int e2ep_conv_gemm_variant(int variant);
 int e2ep_conv_wgrad_splits(const int *dims);
 size_t e2ep_conv_wgrad_workspace(const int *dims, int splits);
 int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,

@@ -43,11 +43,24 @@ CASES = [
     (4, 160, 16, 16, 64, 3, 3, 1, (36, 36, 36, 36), 36, False, 0),  # ASPP dilation 36: 8 dead taps
     (2, 16, 9, 7, 24, 5, 5, 2, (9, 9, 9, 9), 3, False, 1),       # strided, dead taps both axes
     (2, 40, 6, 6, 32, 3, 3, 1, (6, 6, 6, 1), 6, True, 0),        # asymmetric pad: dead rows/cols
+    (2, 65, 64, 64, 64, 7, 7, 2, (3, 3, 3, 3), 1, True, 1),      # stem: 49-row tail, bias+relu
+    (2, 216, 20, 20, 64, 3, 3, 1, (1, 1, 1, 1), 1, False, 0),    # 8-channel remainder x 9 taps
+    (1, 64, 40, 40, 48, 3, 3, 1, (1, 1, 1, 1), 1, False, 0),     # M = 48 (partial 64-row tile)
 ]
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "gemm1", "gemm2"])
+def gemm_variant(request):
+    """Forward / data-gradient GEMM selection (e2ep_conv_gemm_variant): automatic, the first-
+    generation kernel everywhere, the second-generation kernel wherever it applies."""
+    from e2ep_amd import _lib
+    old = _lib.call_raw("e2ep_conv_gemm_variant", request.param)
+    yield request.param
+    _lib.call_raw("e2ep_conv_gemm_variant", old)
+
+
 @pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
-def test_conv_fwd_bwd_vs_fp64(case):
+def test_conv_fwd_bwd_vs_fp64(case, gemm_variant):
     from e2ep_amd import conv
     N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
@@ -101,7 +114,7 @@ SKIP_CASES = [
 
 
 @pytest.mark.parametrize("case", SKIP_CASES, ids=[str(i) for i in range(len(SKIP_CASES))])
-def test_conv_skip_gradient_fused(case):
+def test_conv_skip_gradient_fused(case, gemm_variant):
     from e2ep_amd import conv
     N, Cin, H, W, Cout, R, S, pad, gc = case
     g = torch.Generator().manual_seed(17 + Cin)
