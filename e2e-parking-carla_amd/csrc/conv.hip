@@ -1202,7 +1202,8 @@ static size_t gemm_workspace(const GemmPlan &p, int M) {
 }
 
 // ---- second-generation GEMM plan (k_conv_gemm2) ------------------------------------------
-static int g_gemm_variant = 0;  // 0 auto, 1 always k_conv_gemm, 2 k_conv_gemm2 wherever it applies
+static int g_gemm_variant = 0;  // 0 auto, 1 always k_conv_gemm, 2 k_conv_gemm2 wherever it
+                                // applies, 3 the same with 128-column tiles only
 
 // live taps of the largest phase and the column count (as plan_gemm)
 static void gemm_extent(int mode, const ConvGeom &g, int &taps_max, long long &ncols, int &nph) {
@@ -1225,9 +1226,12 @@ static void gemm_extent(int mode, const ConvGeom &g, int &taps_max, long long &n
   }
 }
 
-// k_conv_gemm2 applies when the tail table fits (remainder channels x taps <= V2_TAIL) and the
-// 64-row tiles do not pad M much (M >= 40).  Auto mode uses it for grids of >= 256 blocks of
-// 128 columns without split-K (large maps); split-K stays on k_conv_gemm.
+// k_conv_gemm2 applies when the tail table fits (remainder channels x taps <= V2_TAIL).
+// Automatic choice (scripts/bench_conv_variants.py, MI355X): spatial filters (R*S > 1) with
+// M >= 40 on large maps — 64 x 256 tiles when their grid fills whole rounds of 2 blocks per CU
+// (>= 95 % of the last round used: the BEV stem 7x7/2 fwd 0.80 -> 0.52 ms), else 64 x 128 tiles
+// when there are >= 1024 of them (the segmentation 3x3 at 200x200); everything else (1x1
+// convs, small maps, split-K grids) stays on k_conv_gemm, which is faster there.
 static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt) {
   if (g_gemm_variant == 1) return false;
   int taps;
@@ -1236,11 +1240,17 @@ static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt
   gemm_extent(mode, g, taps, ncols, nph);
   const int Kc = mode == 0 ? g.Cin : g.Cout;
   if ((Kc % BK) * taps > V2_TAIL || taps == 0) return false;
-  if (g_gemm_variant == 0 && M < 40) return false;
   const long long mblocks = cdiv(M, 64);
   const long long b256 = cdiv(ncols, 256) * mblocks * nph, b128 = cdiv(ncols, 128) * mblocks * nph;
-  if (g_gemm_variant == 0 && b128 < 256) return false;
-  wnt = b256 >= 512 ? 4 : 2;
+  const long long slots = 2LL * 256;  // 64 x 256 tiles resident per round (2 per CU)
+  const bool fill256 = b256 >= slots && 100 * b256 >= 95 * (cdiv(b256, slots) * slots);
+  if (g_gemm_variant == 0) {
+    if (g.R * g.S == 1 || M < 40) return false;
+    if (!fill256 && b128 < 1024) return false;
+    wnt = fill256 ? 4 : 2;
+  } else {
+    wnt = (g_gemm_variant == 2 && b256 >= 512) ? 4 : 2;
+  }
   p.bm = 64;
   p.bnt = 64 * wnt;
   p.nph = nph;
@@ -1332,7 +1342,7 @@ size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
 
 int e2ep_conv_gemm_variant(int variant) {
   const int old = g_gemm_variant;
-  if (variant >= 0 && variant <= 2) g_gemm_variant = variant;
+  if (variant >= 0 && variant <= 3) g_gemm_variant = variant;
   return old;
 }
 

@@ -37,19 +37,22 @@ def main():
         dx = torch.empty(N, Cin, H, W, device="cuda")
         fl = conv.conv_flops(d)
         res = {}
-        for v in (1, 2):
+        for v in (1, 2, 3):
             _lib.call_raw("e2ep_conv_gemm_variant", v)
             tf = timeit(lambda: conv.conv_fwd(x, wt, None, d, 0, y, w_layout=1))
             y1 = y.clone()
             tg = timeit(lambda: conv.conv_dgrad(gy, wt, d, Cin, dx, w_layout=1))
             res[v] = (tf, tg, y1, dx.clone())
         _lib.call_raw("e2ep_conv_gemm_variant", 0)
-        (f1, g1, y1, d1), (f2, g2, y2, d2) = res[1], res[2]
-        ey = float((y1 - y2).norm() / y1.norm())
-        ed = float((d1 - d2).norm() / d1.norm())
-        print(f"{name:8s} fwd {f1 * 1e3:8.1f} -> {f2 * 1e3:8.1f} us ({fl / f1 / 1e9:6.1f} -> {fl / f2 / 1e9:6.1f} TF/s)  "
-              f"dgrad {g1 * 1e3:8.1f} -> {g2 * 1e3:8.1f} us ({fl / g1 / 1e9:6.1f} -> {fl / g2 / 1e9:6.1f} TF/s)  "
-              f"rel diff y {ey:.1e} dx {ed:.1e}", flush=True)
+        y1, d1 = res[1][2], res[1][3]
+        line = f"{name:8s}"
+        for v in (1, 2, 3):
+            f, gg, yv, dv = res[v]
+            ey = float((yv - y1).norm() / y1.norm())
+            ed = float((dv - d1).norm() / d1.norm())
+            line += (f" | v{v} fwd {f * 1e3:7.1f} us {fl / f / 1e9:6.1f} TF/s dgrad {gg * 1e3:7.1f} us "
+                     f"{fl / gg / 1e9:6.1f} TF/s (dy {ey:.0e} ddx {ed:.0e})")
+        print(line, flush=True)
 
 
 if __name__ == "__main__":

@@ -12,6 +12,7 @@ import torch  # noqa: E402
 from e2ep_amd import conv  # noqa: E402
 
 SHAPES = {"stem": (8, 65, 256, 256, 64, 7, 7, 128, 128, 2, 2, 3, 3, 1, 1),
+          "stem64": (8, 64, 256, 256, 64, 7, 7, 128, 128, 2, 2, 3, 3, 1, 1),
           "seg": (8, 64, 200, 200, 64, 3, 3, 200, 200, 1, 1, 1, 1, 1, 1),
           "l1": (8, 64, 64, 64, 64, 3, 3, 64, 64, 1, 1, 1, 1, 1, 1),
           "proj960": (32, 960, 16, 16, 160, 1, 1, 16, 16, 1, 1, 0, 0, 1, 1),
@@ -25,6 +26,9 @@ def main():
     kind = sys.argv[2] if len(sys.argv) > 2 else "all"
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     d = SHAPES[which]
+    if os.environ.get("E2EP_GEMM_VARIANT"):
+        from e2ep_amd import _lib
+        _lib.call_raw("e2ep_conv_gemm_variant", int(os.environ["E2EP_GEMM_VARIANT"]))
     N, Cin, H, W, Cout, R, S, P, Q = d[:9]
     g = torch.Generator(device="cuda").manual_seed(0)
     x = torch.randn(N, Cin, H, W, device="cuda", generator=g)
