@@ -42,16 +42,20 @@ def main():
             tf = timeit(lambda: conv.conv_fwd(x, wt, None, d, 0, y, w_layout=1))
             y1 = y.clone()
             tg = timeit(lambda: conv.conv_dgrad(gy, wt, d, Cin, dx, w_layout=1))
-            res[v] = (tf, tg, y1, dx.clone())
+            dw = torch.empty(Cout, Cin, R, S, device="cuda")
+            tw = timeit(lambda: conv.conv_wgrad(gy, x, d, dw))
+            res[v] = (tf, tg, y1, dx.clone(), tw, dw.clone())
         _lib.call_raw("e2ep_conv_gemm_variant", 0)
-        y1, d1 = res[1][2], res[1][3]
+        y1, d1, w1 = res[1][2], res[1][3], res[1][5]
         line = f"{name:8s}"
         for v in (1, 2, 3):
-            f, gg, yv, dv = res[v]
+            f, gg, yv, dv, tw, wv = res[v]
             ey = float((yv - y1).norm() / y1.norm())
             ed = float((dv - d1).norm() / d1.norm())
-            line += (f" | v{v} fwd {f * 1e3:7.1f} us {fl / f / 1e9:6.1f} TF/s dgrad {gg * 1e3:7.1f} us "
-                     f"{fl / gg / 1e9:6.1f} TF/s (dy {ey:.0e} ddx {ed:.0e})")
+            ew = float((wv - w1).norm() / w1.norm())
+            line += (f" | v{v} fwd {f * 1e3:6.1f} us {fl / f / 1e9:5.1f} TF/s dgrad {gg * 1e3:6.1f} us "
+                     f"{fl / gg / 1e9:5.1f} wgrad {tw * 1e3:6.1f} us {fl / tw / 1e9:5.1f} "
+                     f"(d {ey:.0e} {ed:.0e} {ew:.0e})")
         print(line, flush=True)
 
 

@@ -49,10 +49,11 @@ CASES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["auto", "gemm1", "gemm2"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "gemm1", "gemm2", "gemm2_128"])
 def gemm_variant(request):
-    """Forward / data-gradient GEMM selection (e2ep_conv_gemm_variant): automatic, the first-
-    generation kernel everywhere, the second-generation kernel wherever it applies."""
+    """Conv GEMM selection (e2ep_conv_gemm_variant): automatic, the first-generation kernels
+    everywhere, the second-generation forward / data-gradient / weight-gradient kernels
+    wherever they apply (256- or 128-column tiles)."""
     from e2ep_amd import _lib
     old = _lib.call_raw("e2ep_conv_gemm_variant", request.param)
     yield request.param
