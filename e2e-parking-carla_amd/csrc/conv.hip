@@ -744,127 +744,6 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 
 
 // ------------------------------------------------------------------------------------------
-// bwd-weight, second generation (large spatial filters: the BEV stem, the segmentation 3x3):
-// dW[co][col] = sum_p g[co][p] x[ci(col)][p + tap(col)], col over (ci, live tap), K = output
-// pixels of this split.  Both operands are pixel-contiguous in memory, so the LDS images are
-// k(pixel)-contiguous ([row][16 + 4 pad]) and read as b128 fragments exactly as in
-// k_conv_gemm2 (lane half h of MFMA t takes pixel 8h + t of the step); wave tile 32 x 32*WNT.
-// A: thread = (co row tid/4, 4 consecutive pixels); B: thread = (4 consecutive pixels,
-// columns tid/4 + 64 j): four lanes read 16 consecutive pixels of one column (64-B runs).
-// ------------------------------------------------------------------------------------------
-template <int WNT>
-__global__ void __launch_bounds__(256) k_conv_wgrad2(
-    const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
-    ConvGeom g, int pix_per_split, TapList tl) {
-  constexpr int BN = 64 * WNT;
-  __shared__ __attribute__((aligned(16))) float As[2][64][V2_LDW];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN][V2_LDW];
-  __shared__ int s_tap[MAXTAPS];
-  if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
-  __syncthreads();
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
-  const int RS = g.R * g.S;
-  const int Kw = g.Cin * RS, Kl = g.Cin * tl.n;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * 64, split = blockIdx.z;
-  const int PQ = g.P * g.Q, HW = g.H * g.W;
-  const int Ptot = g.N * PQ;
-  const int pbeg = split * pix_per_split;
-  const int pend = min(Ptot, pbeg + pix_per_split);
-  const int nk = (pend - pbeg + BK - 1) / BK;
-  const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
-
-  const int quad = tid & 3;            // this thread's 4 pixels of every K-step
-  const int arow = m0 + (tid >> 2);    // A: gradient row (co)
-  const bool arow_ok = arow < g.Cout;
-  // B: columns tid/4 + 64 j -> (channel plane offset, tap displacement)
-  int cbase[WNT], cdy[WNT], cdx[WNT];
-#pragma unroll
-  for (int j = 0; j < WNT; ++j) {
-    const int col = n0 + (tid >> 2) + 64 * j;
-    const int cc = col < Kl ? col : 0;
-    const int ci = cc / tl.n, tap = s_tap[cc - ci * tl.n];
-    const int r = tap / g.S, sx = tap - r * g.S;
-    cdy[j] = col < Kl ? r * g.dh - g.ph : -(1 << 29);  // out-of-range column: never in bounds
-    cdx[j] = sx * g.dw - g.pw;
-    cbase[j] = ci * HW;
-  }
-  float ra[4], rb[4 * WNT];
-  auto load_tiles = [&](int kt) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int p = pbeg + kt * BK + 4 * quad + u;
-      const bool pok = p < pend;
-      const int im = pok ? p / PQ : 0;
-      const int od = p - im * PQ;
-      const int oy = od / g.Q, ox = od - oy * g.Q;
-      ra[u] = bload(rg, (pok && arow_ok) ? ((im * g.Cout + arow) * PQ + od) * 4 : OOR);
-      const int yb = oy * g.sh, xb = ox * g.sw;
-      const int xim = im * g.Cin * HW;
-#pragma unroll
-      for (int j = 0; j < WNT; ++j) {
-        const int iy = yb + cdy[j], ix = xb + cdx[j];
-        const bool ok = pok && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-        rb[4 * j + u] = bload(rx, ok ? (xim + cbase[j] + iy * g.W + ix) * 4 : OOR);
-      }
-    }
-  };
-  auto store_tiles = [&](int buf) {
-    *reinterpret_cast<float4 *>(&As[buf][tid >> 2][4 * quad]) = make_float4(ra[0], ra[1], ra[2], ra[3]);
-#pragma unroll
-    for (int j = 0; j < WNT; ++j)
-      *reinterpret_cast<float4 *>(&Bs[buf][(tid >> 2) + 64 * j][4 * quad]) =
-          make_float4(rb[4 * j], rb[4 * j + 1], rb[4 * j + 2], rb[4 * j + 3]);
-  };
-  f32x16 acc[WNT];
-#pragma unroll
-  for (int t = 0; t < WNT; ++t) acc[t] = f32x16{0};
-  const int li = lane & 31, lh = lane >> 5;
-  auto compute = [&](int buf) {
-    const float4 a0 = *reinterpret_cast<const float4 *>(&As[buf][32 * wm + li][8 * lh]);
-    const float4 a1 = *reinterpret_cast<const float4 *>(&As[buf][32 * wm + li][8 * lh + 4]);
-    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-    for (int t = 0; t < WNT; ++t) {
-      const int col = 32 * WNT * wn + 32 * t + li;
-      const float4 b0 = *reinterpret_cast<const float4 *>(&Bs[buf][col][8 * lh]);
-      const float4 b1 = *reinterpret_cast<const float4 *>(&Bs[buf][col][8 * lh + 4]);
-      const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk], b[kk], acc[t], 0, 0, 0);
-    }
-  };
-  if (nk > 0) {
-    load_tiles(0);
-    store_tiles(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      load_tiles(kt + 1);  // past the split: zeros, never stored
-      compute(kt & 1);
-      if (kt + 1 < nk) store_tiles((kt + 1) & 1);
-      __syncthreads();
-    }
-  }
-  // partial slab part[split][co][dW column]
-  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
-#pragma unroll
-  for (int t = 0; t < WNT; ++t) {
-    const int lcol = n0 + 32 * WNT * wn + 32 * t + li;
-    const int lci = lcol < Kl ? lcol / tl.n : 0;
-    const int col = lci * RS + s_tap[lcol < Kl ? lcol - lci * tl.n : 0];
-#pragma unroll
-    for (int rr = 0; rr < 16; ++rr) {
-      const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-      const bool ok = co < g.Cout && lcol < Kl;
-      bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[t][rr]);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // bwd-weight of 1x1 / stride-1 / unpadded convs (the EfficientNet expand / project convs,
 // the BEV heads' 1x1s): dW[co][ci] = sum_q g[co][q] x[ci][q] over all pixels q.  No LDS, no
 // barrier in the main loop: each wave owns a 32 (co) x 32 (ci) tile and a pixel range, and
@@ -1268,17 +1147,6 @@ static TapList live_taps(const ConvGeom &g) {
   return t;
 }
 
-// second-generation weight gradient (k_conv_wgrad2): spatial filters with large pixel counts
-// and >= 40 output channels; 0 = use k_conv_wgrad.  Forced by e2ep_conv_gemm_variant 1 / 2.
-static int g_gemm_variant_wgrad();
-static int wgrad2_wnt(const ConvGeom &g, int nlive) {
-  const int v = g_gemm_variant_wgrad();
-  if (v == 1) return 0;
-  const long long pix = (long long)g.N * g.P * g.Q;
-  if (v == 0 && (g.R * g.S == 1 || g.Cout < 40 || pix < 65536)) return 0;
-  return (long long)g.Cin * nlive >= 256 && v != 3 ? 4 : 2;
-}
-
 struct GemmPlan {
   int bm, bnt, splits, kper, nph;
   long long ncols;  // columns of the largest phase
@@ -1337,7 +1205,6 @@ static size_t gemm_workspace(const GemmPlan &p, int M) {
 // ---- second-generation GEMM plan (k_conv_gemm2) ------------------------------------------
 static int g_gemm_variant = 0;  // 0 auto, 1 always k_conv_gemm, 2 k_conv_gemm2 wherever it
                                 // applies, 3 the same with 128-column tiles only
-static int g_gemm_variant_wgrad() { return g_gemm_variant; }
 
 // live taps of the largest phase and the column count (as plan_gemm)
 static void gemm_extent(int mode, const ConvGeom &g, int &taps_max, long long &ncols, int &nph) {
@@ -1521,15 +1388,6 @@ int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
   if (wgrad1x1_ok(g)) return wgrad1x1_splits(g);
   const int nl = std::max(1, live_taps(g).n);
-  const int wnt = wgrad2_wnt(g, nl);
-  if (wnt) {
-    // second-generation tiles: ~2 blocks per CU over the grid, >= 64 pixel steps per block
-    const long long base = (long long)cdiv(g.Cin * nl, 64 * wnt) * cdiv(g.Cout, 64);
-    const long long pix = (long long)g.N * g.P * g.Q;
-    long long sp = (512 + base - 1) / base;
-    sp = std::min(sp, pix / (64 * BK));
-    return (int)std::max(1LL, std::min(sp, 256LL));
-  }
   const long long base = (long long)cdiv(g.Cin * nl, WBN) * cdiv(g.Cout, BM);
   const long long pix = (long long)g.N * g.P * g.Q;
   long long want = (1024 + base - 1) / base;
@@ -1578,15 +1436,8 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
   hipStream_t s = as_stream(stream);
   float *part = static_cast<float *>(workspace);
   if (tl.n > 0) {
-    const int wnt = wgrad2_wnt(g, tl.n);
-    if (wnt) {
-      dim3 grid(cdiv(g.Cin * tl.n, 64 * wnt), cdiv(g.Cout, 64), used);
-      if (wnt == 4) hipLaunchKernelGGL((k_conv_wgrad2<4>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
-      else hipLaunchKernelGGL((k_conv_wgrad2<2>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
-    } else {
-      dim3 grid(cdiv(g.Cin * tl.n, WBN), cdiv(g.Cout, BM), used);
-      hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
-    }
+    dim3 grid(cdiv(g.Cin * tl.n, WBN), cdiv(g.Cout, BM), used);
+    hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
   }
   const int n = g.Cout * g.Cin * g.R * g.S;
   hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,

@@ -51,9 +51,9 @@ CASES = [
 
 @pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "gemm1", "gemm2", "gemm2_128"])
 def gemm_variant(request):
-    """Conv GEMM selection (e2ep_conv_gemm_variant): automatic, the first-generation kernels
-    everywhere, the second-generation forward / data-gradient / weight-gradient kernels
-    wherever they apply (256- or 128-column tiles)."""
+    """Conv GEMM selection (e2ep_conv_gemm_variant): automatic, the first-generation kernel
+    everywhere, the second-generation forward / data-gradient kernel wherever it applies
+    (256- or 128-column tiles)."""
     from e2ep_amd import _lib
     old = _lib.call_raw("e2ep_conv_gemm_variant", request.param)
     yield request.param
