@@ -33,7 +33,7 @@ class _BnAct(torch.autograd.Function):
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         invstd = torch.empty_like(mean)
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
-        with timing.region("bn_fwd"):
+        with timing.region(timing.name("bn_fwd", x.shape, "_BnAct")):
             _lib.call("e2ep_bn_fwd", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res),
                       _lib.ptr(dc_rand), float(dc_keep), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W,
                       int(train), float(momentum), float(eps), act, _lib.ptr(mean),
@@ -56,7 +56,7 @@ class _BnAct(torch.autograd.Function):
         dres_is_dy = res is not None and nig[3] and ctx.act == 0
         dres = torch.empty_like(x) if (res is not None and nig[3] and not dres_is_dy) else None
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
-        with timing.region("bn_bwd"):
+        with timing.region(timing.name("bn_bwd", x.shape, "_BnAct")):
             _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(mean), _lib.ptr(invstd),
                       _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), _lib.ptr(dc_rand),
                       float(ctx.dc_keep), None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx),
@@ -167,7 +167,7 @@ class _Resize(torch.autograd.Function):
         x = x.contiguous()
         N, C, Hi, Wi = x.shape
         y = torch.empty(N, C, Ho, Wo, dtype=torch.float32, device=x.device)
-        with timing.region("resize_fwd"):
+        with timing.region(timing.name("resize_fwd", x.shape, "_Resize")):
             _lib.call("e2ep_resize_fwd", _lib.ptr(x), N, C, C * Hi * Wi, Hi, Wi, Ho, Wo, sh, sw,
                       _lib.ptr(y), C * Ho * Wo, _lib.stream())
         ctx.meta = (N, C, Hi, Wi, Ho, Wo, sh, sw)
@@ -179,7 +179,7 @@ class _Resize(torch.autograd.Function):
         g = g.contiguous()
         gx = torch.empty(N, C, Hi, Wi, dtype=torch.float32, device=g.device)
         ws = _ws(N * C * Ho * Wi * 4, g.device)
-        with timing.region("resize_bwd"):
+        with timing.region(timing.name("resize_bwd", g.shape, "_Resize")):
             _lib.call("e2ep_resize_bwd", _lib.ptr(g), Ho * Wo, N * C, Hi, Wi, Ho, Wo, sh, sw,
                       _lib.ptr(gx), 0, _lib.ptr(ws), _lib.stream())
         return gx, None, None, None, None
@@ -209,7 +209,7 @@ class _DwConv(torch.autograd.Function):
         N, C, H, W, K, P, Q = dims[:7]
         y = torch.empty(N, C, P, Q, dtype=torch.float32, device=x.device)
         d = _lib.dims(dims)
-        with timing.region("dwconv_fwd"):
+        with timing.region(timing.name("dwconv_fwd", x.shape, "_DwConv")):
             _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, None, None, 0, _lib.ptr(y),
                       _lib.stream())
         ctx.save_for_backward(x, w)
@@ -225,12 +225,12 @@ class _DwConv(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            with timing.region("dwconv_dgrad"):
+            with timing.region(timing.name("dwconv_dgrad", gy.shape, "_DwConv")):
                 _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s)
         if ctx.needs_input_grad[1]:
             dw = torch.empty_like(w)
             ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
-            with timing.region("dwconv_wgrad"):
+            with timing.region(timing.name("dwconv_wgrad", gy.shape, "_DwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
                           _lib.ptr(ws), _lib.ptr(dw), s)
         return dx, dw, None
@@ -252,14 +252,14 @@ class _BnActDwConv(torch.autograd.Function):
         stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
         s = _lib.stream()
-        with timing.region("bn_fwd"):
+        with timing.region(timing.name("bn_fwd", x.shape, "_BnActDwConv")):
             _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
                       _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
                       _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
                       _lib.ptr(stats[3]), _lib.ptr(ws), s)
         y = torch.empty(N, C, P, Q, **f32)
         d = _lib.dims(dims)
-        with timing.region("dwconv_fwd"):
+        with timing.region(timing.name("dwconv_fwd", x.shape, "_BnActDwConv")):
             _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(stats[2]),
                       _lib.ptr(stats[3]), act, _lib.ptr(y), s)
         ctx.save_for_backward(x, gamma, beta, w, stats)
@@ -278,18 +278,18 @@ class _BnActDwConv(torch.autograd.Function):
         if nig[9]:
             dw = torch.empty_like(w)
             ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
-            with timing.region("dwconv_wgrad"):
+            with timing.region(timing.name("dwconv_wgrad", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(stats[2]),
                           _lib.ptr(stats[3]), ctx.act, _lib.ptr(ws), _lib.ptr(dw), s)
         if nig[0] or nig[1] or nig[2]:
             dt = torch.empty_like(x)  # gradient at the activation output
-            with timing.region("dwconv_dgrad"):
+            with timing.region(timing.name("dwconv_dgrad", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s)
             dx = torch.empty_like(x) if nig[0] else None
             dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
             db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
             ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
-            with timing.region("bn_bwd"):
+            with timing.region(timing.name("bn_bwd", x.shape, "_BnActDwConv")):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dt), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx), _lib.ptr(dg),
@@ -387,7 +387,7 @@ class _SeGate(torch.autograd.Function):
         a = a.contiguous()
         N, C, H, W = x.shape
         y = torch.empty_like(x)
-        with timing.region("se_gate_fwd"):
+        with timing.region(timing.name("se_gate_fwd", x.shape, "_SeGate")):
             _lib.call("e2ep_se_gate_fwd", _lib.ptr(x), _lib.ptr(a), N * C, H * W, _lib.ptr(y),
                       _lib.stream())
         ctx.save_for_backward(x, a)
@@ -399,7 +399,7 @@ class _SeGate(torch.autograd.Function):
         N, C, H, W = x.shape
         dx = torch.empty_like(x)
         da = torch.empty_like(a)
-        with timing.region("se_gate_bwd"):
+        with timing.region(timing.name("se_gate_bwd", x.shape, "_SeGate")):
             _lib.call("e2ep_se_gate_bwd", _lib.ptr(x), _lib.ptr(a), _lib.ptr(dy.contiguous()), N * C,
                       H * W, _lib.ptr(dx), _lib.ptr(da), _lib.stream())
         return dx, da
@@ -426,7 +426,7 @@ class _SqueezeExcite(torch.autograd.Function):
         a = torch.empty(N, C, dtype=torch.float32, device=dev)
         y = torch.empty_like(x)
         w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
-        with timing.region("se_fwd"):
+        with timing.region(timing.name("se_fwd", x.shape, "_SqueezeExcite")):
             _lib.call("e2ep_se_fwd", _lib.ptr(x), None, None, _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c),
                       _lib.ptr(b2), N, C, H * W, sq, _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a),
                       _lib.ptr(y), _lib.stream())
@@ -448,7 +448,7 @@ class _SqueezeExcite(torch.autograd.Function):
         dw2 = torch.empty(w2s, dtype=torch.float32, device=dev) if nig[3] else None
         db2 = torch.empty(C, dtype=torch.float32, device=dev) if (hb2 and nig[4]) else None
         ws = torch.empty(2 * N * C + 17 * N * sq, dtype=torch.float32, device=dev)
-        with timing.region("se_bwd"):
+        with timing.region(timing.name("se_bwd", x.shape, "_SqueezeExcite")):
             _lib.call("e2ep_se_bwd", _lib.ptr(x), None, None, _lib.ptr(dy.contiguous()),
                       _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a),
                       N, C, H * W, sq, _lib.ptr(dx), None, _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2),
@@ -472,7 +472,7 @@ class _BnSwishSE(torch.autograd.Function):
         stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
         s = _lib.stream()
-        with timing.region("bn_fwd"):
+        with timing.region(timing.name("bn_fwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
                       _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
                       _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
@@ -480,7 +480,7 @@ class _BnSwishSE(torch.autograd.Function):
         pooled, hpre, a = torch.empty(N, C, **f32), torch.empty(N, sq, **f32), torch.empty(N, C, **f32)
         y = torch.empty_like(x)
         w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
-        with timing.region("se_fwd"):
+        with timing.region(timing.name("se_fwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_se_fwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
                       _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c), _lib.ptr(b2), N, C, H * W, sq,
                       _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), _lib.ptr(y), s)
@@ -506,7 +506,7 @@ class _BnSwishSE(torch.autograd.Function):
         db2 = torch.empty(C, **f32) if (hb2 and nig[11]) else None
         dpooled = torch.empty(N, C, **f32)
         ws = torch.empty(2 * N * C + 17 * N * sq, **f32)
-        with timing.region("se_bwd"):
+        with timing.region(timing.name("se_bwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
                       _lib.ptr(dy), _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled),
                       _lib.ptr(hpre), _lib.ptr(a), N, C, H * W, sq, None, _lib.ptr(dpooled),
@@ -516,7 +516,7 @@ class _BnSwishSE(torch.autograd.Function):
         db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
         if dx is not None or dg is not None or db is not None:
             bws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
-            with timing.region("bn_bwd"):
+            with timing.region(timing.name("bn_bwd", x.shape, "_BnSwishSE")):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           _lib.ptr(a), _lib.ptr(dpooled), N, C, H, W, int(ctx.train), ACT["swish"],
@@ -555,7 +555,7 @@ class _AddDropLN(torch.autograd.Function):
         y = torch.empty_like(a)
         mean = torch.empty(rows, dtype=torch.float32, device=a.device)
         rstd = torch.empty_like(mean)
-        with timing.region("ln_fwd"):
+        with timing.region(timing.name("ln_fwd", a.shape, "_AddDropLN")):
             _lib.call("e2ep_add_drop_ln_fwd", _lib.ptr(a), _lib.ptr(b), _lib.ptr(u), float(p),
                       _lib.ptr(gamma), _lib.ptr(beta), rows, E, float(eps), _lib.ptr(x), _lib.ptr(y),
                       _lib.ptr(mean), _lib.ptr(rstd), _lib.stream())
@@ -572,7 +572,7 @@ class _AddDropLN(torch.autograd.Function):
         dg = torch.empty_like(gamma) if (gamma is not None and nig[2]) else None
         dbeta = torch.empty_like(gamma) if (gamma is not None and nig[3]) else None
         ws = _ws(_lib.load().e2ep_add_drop_ln_bwd_workspace(ctx.rows, ctx.E), x.device)
-        with timing.region("ln_bwd"):
+        with timing.region(timing.name("ln_bwd", x.shape, "_AddDropLN")):
             _lib.call("e2ep_add_drop_ln_bwd", _lib.ptr(dy.contiguous()), _lib.ptr(x), _lib.ptr(mean),
                       _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(u), ctx.p, ctx.rows, ctx.E,
                       _lib.ptr(da), _lib.ptr(db), _lib.ptr(dg), _lib.ptr(dbeta), _lib.ptr(ws),

@@ -20,6 +20,11 @@ def detail():
     return _enabled and os.environ.get("E2EP_TIMING_DETAIL") == "1"
 
 
+def name(kind, shape, tag=""):
+    """Region name: `kind`, or `kind(shape)tag` under E2EP_TIMING_DETAIL=1."""
+    return f"{kind}{tuple(shape)}{tag}" if detail() else kind
+
+
 def enable(flag=True):
     global _enabled
     _enabled = flag
