@@ -361,7 +361,15 @@ __global__ void k_conv_reduce(const float *__restrict__ part, int splits, int M,
 constexpr int V2_LDW = 20;    // LDS row stride in floats (16 k + 4 pad)
 constexpr int V2_TAIL = 256;  // max flattened (remainder channel, tap) rows
 
-template <int MODE, int ACT, int WNT>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// OP: MFMA operand precision — 0 fp32 (v_mfma_f32_32x32x2_f32, exact), 1 bf16 / 2 fp16
+// (v_mfma_f32_32x32x16_{bf16,f16}: the fragments are rounded to nearest-even when read from
+// LDS, products and sums stay fp32; the BASELINE C3 bf16 forward and C5 fp16 inference
+// modes).  A lane's 8 fragment values are exactly the 8 k of its lane half that the 16-deep
+// low-precision MFMA takes, so one MFMA replaces the eight fp32 ones per K-step.
+template <int MODE, int ACT, int WNT, int OP = 0>
 __global__ void __launch_bounds__(256) k_conv_gemm2(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
@@ -540,14 +548,35 @@ __global__ void __launch_bounds__(256) k_conv_gemm2(
     const float4 a0 = *reinterpret_cast<const float4 *>(&As[buf][32 * wm + li][8 * lh]);
     const float4 a1 = *reinterpret_cast<const float4 *>(&As[buf][32 * wm + li][8 * lh + 4]);
     const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    bf16x8 abf;
+    f16x8 ah;
+    if (OP == 1) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) abf[kk] = (__bf16)a[kk];
+    } else if (OP == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) ah[kk] = (_Float16)a[kk];
+    }
 #pragma unroll
     for (int t = 0; t < WNT; ++t) {
       const int col = 32 * WNT * wn + 32 * t + li;
       const float4 b0 = *reinterpret_cast<const float4 *>(&Bs[buf][col][8 * lh]);
       const float4 b1 = *reinterpret_cast<const float4 *>(&Bs[buf][col][8 * lh + 4]);
       const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      if (OP == 0) {
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk], b[kk], acc[t], 0, 0, 0);
+        for (int kk = 0; kk < 8; ++kk) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk], b[kk], acc[t], 0, 0, 0);
+      } else if (OP == 1) {
+        bf16x8 bb;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) bb[kk] = (__bf16)b[kk];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(abf, bb, acc[t], 0, 0, 0);
+      } else {
+        f16x8 bh;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) bh[kk] = (_Float16)b[kk];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[t], 0, 0, 0);
+      }
     }
   };
   if (nk > 0) {
@@ -1203,6 +1232,7 @@ static size_t gemm_workspace(const GemmPlan &p, int M) {
 }
 
 // ---- second-generation GEMM plan (k_conv_gemm2) ------------------------------------------
+static int g_conv_precision = 0;  // GEMM operand precision: 0 fp32, 1 bf16, 2 fp16
 static int g_gemm_variant = 0;  // 0 auto, 1 always k_conv_gemm, 2 k_conv_gemm2 wherever it
                                 // applies, 3 the same with 128-column tiles only
 
@@ -1234,7 +1264,7 @@ static void gemm_extent(int mode, const ConvGeom &g, int &taps_max, long long &n
 // when there are >= 1024 of them (the segmentation 3x3 at 200x200); everything else (1x1
 // convs, small maps, split-K grids) stays on k_conv_gemm, which is faster there.
 static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt) {
-  if (g_gemm_variant == 1) return false;
+  if (g_gemm_variant == 1 && g_conv_precision == 0) return false;
   int taps;
   long long ncols;
   int nph;
@@ -1245,7 +1275,9 @@ static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt
   const long long b256 = cdiv(ncols, 256) * mblocks * nph, b128 = cdiv(ncols, 128) * mblocks * nph;
   const long long slots = 2LL * 256;  // 64 x 256 tiles resident per round (2 per CU)
   const bool fill256 = b256 >= slots && 100 * b256 >= 95 * (cdiv(b256, slots) * slots);
-  if (g_gemm_variant == 0) {
+  if (g_conv_precision != 0) {
+    wnt = b256 >= 512 ? 4 : 2;  // low-precision operands: every GEMM here (k_conv_gemm is fp32)
+  } else if (g_gemm_variant == 0) {
     if (g.R * g.S == 1 || M < 40) return false;
     if (!fill256 && b128 < 1024) return false;
     wnt = fill256 ? 4 : 2;
@@ -1270,9 +1302,18 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     int wnt;
     if (g.wlayout == 1 && plan_gemm2(mode, g, M, p2, wnt)) {
       dim3 grid(cdiv(p2.ncols, p2.bnt), cdiv(M, 64), p2.nph);
-#define G2(MD, AC, W)                                                                          \
-  hipLaunchKernelGGL((k_conv_gemm2<MD, AC, W>), grid, dim3(256), 0, s, w, src, bias, dst, dst_bytes, \
-                     g, M, 1, p2.kper)
+#define G2(MD, AC, W)                                                                         \
+  do {                                                                                        \
+    if (g_conv_precision == 1)                                                                \
+      hipLaunchKernelGGL((k_conv_gemm2<MD, AC, W, 1>), grid, dim3(256), 0, s, w, src, bias, dst, \
+                         dst_bytes, g, M, 1, p2.kper);                                        \
+    else if (g_conv_precision == 2)                                                           \
+      hipLaunchKernelGGL((k_conv_gemm2<MD, AC, W, 2>), grid, dim3(256), 0, s, w, src, bias, dst, \
+                         dst_bytes, g, M, 1, p2.kper);                                        \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_conv_gemm2<MD, AC, W, 0>), grid, dim3(256), 0, s, w, src, bias, dst, \
+                         dst_bytes, g, M, 1, p2.kper);                                        \
+  } while (0)
       if (mode == 0 && act == 0) { if (wnt == 4) G2(0, 0, 4); else G2(0, 0, 2); }
       else if (mode == 0) { if (wnt == 4) G2(0, 1, 4); else G2(0, 1, 2); }
       else { if (wnt == 4) G2(1, 0, 4); else G2(1, 0, 2); }
@@ -1339,6 +1380,12 @@ size_t e2ep_conv_fwd_workspace(const int *dims) {
 size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
   ConvGeom g = make_geom(dims);
   return gemm_workspace(plan_gemm(1, g, m_channels), m_channels);
+}
+
+int e2ep_conv_precision(int precision) {
+  const int old = g_conv_precision;
+  if (precision >= 0 && precision <= 2) g_conv_precision = precision;
+  return old;
 }
 
 int e2ep_conv_gemm_variant(int variant) {

@@ -138,3 +138,47 @@ def test_conv_skip_gradient_fused(case, gemm_variant):
     assert rel_l2(y.detach().cpu(), y64) < 1e-5
     assert rel_l2(xd.grad.cpu(), gx) < 1e-5
     assert rel_l2(wd.grad.cpu(), w64.grad) < 1e-5
+
+
+# low-precision operand modes (e2ep_amd.precision): against fp64 convolutions of the operands
+# ROUNDED to bf16 / fp16 the kernels must agree to fp32-accumulation accuracy (the products
+# are exact); against the unrounded fp64 result the error is the format's rounding (~3e-3
+# bf16, ~4e-4 fp16 relative L2 at these depths) and is bounded loosely.
+LP_CASES = [
+    (2, 65, 64, 64, 64, 7, 7, 2, (3, 3, 3, 3), 1),      # BEV stem (tail rows)
+    (2, 64, 40, 40, 64, 3, 3, 1, (1, 1, 1, 1), 1),      # 3x3 s1
+    (4, 24, 32, 32, 144, 1, 1, 1, (0, 0, 0, 0), 1),     # MBConv expand (1x1)
+    (4, 160, 16, 16, 64, 3, 3, 1, (12, 12, 12, 12), 12),  # ASPP dilated
+    (2, 64, 16, 16, 128, 3, 3, 2, (1, 1, 1, 1), 1),     # stride 2 (dgrad phases)
+]
+
+
+@pytest.mark.parametrize("mode,dt,loose", [("bf16", torch.bfloat16, 1e-2), ("fp16", torch.float16, 2e-3)])
+@pytest.mark.parametrize("case", LP_CASES, ids=[str(i) for i in range(len(LP_CASES))])
+def test_conv_low_precision_operands(case, mode, dt, loose):
+    from e2ep_amd import conv, precision
+    N, Cin, H, W, Cout, R, S, st, pad, dil = case
+    g = torch.Generator().manual_seed(31 + Cin)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    with precision.use(mode):
+        assert precision.get() == mode
+        y = conv.conv2d(xd, wd, None, (st, st), pad, (dil, dil), 0)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy.to(DEV))
+    assert precision.get() == "fp32"
+    r = lambda t: t.to(dt).double()  # noqa: E731
+    y_r = F.conv2d(F.pad(r(x), pad), r(w), None, st, 0, dil)
+    xr = r(x).requires_grad_(True)
+    F.conv2d(F.pad(xr, pad), r(w), None, st, 0, dil).backward(r(gy))
+    y64 = F.conv2d(F.pad(x.double(), pad), w.double(), None, st, 0, dil)
+    assert rel_l2(y, y_r) < 2e-6                  # operands rounded, fp32 accumulation
+    assert rel_l2(xd.grad, xr.grad) < 2e-6        # data gradient: gy and W rounded
+    assert rel_l2(y, y64) < loose                 # vs the exact fp32-operand result
+    # the weight gradient stays fp32 (exact-f32 MFMA) in every mode
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    F.conv2d(F.pad(x64, pad), w64, None, st, 0, dil).backward(gy.double())
+    assert rel_l2(wd.grad, w64.grad) < 2e-6
