@@ -37,6 +37,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "train samples/sec (4-cam frames) at B=8, 1/2/4/8 MI355X; CPU-ref baseline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = the f32 vector rate
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 / fp16
 # forward 29.94 GFLOP per 4-cam 256^2 sample (FlopCounterMode), train step
 # = 3 x forward
 STEP_GFLOP_PER_SAMPLE = 3 * 29.94
@@ -172,6 +173,9 @@ def main():
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
+                    help="conv GEMM operands: fp32 (C2, default) or bf16 (C3: bf16 forward / "
+                         "data-gradient conv operands, fp32 weight gradients and everything else)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -197,12 +201,13 @@ def main():
         backend = dist.get_backend()
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
-    from e2ep_amd import _lib, synthetic, timing
+    from e2ep_amd import _lib, precision, synthetic, timing
     from e2ep_amd.train import TrainStep
     from tool.config import default_cfg
     from trainer.pl_trainer import ParkingTrainingModule
 
     _lib.load()
+    precision.set(args.precision)
     torch.manual_seed(1234)  # identical initial weights on every rank
     mod = ParkingTrainingModule(default_cfg()).to(dev).train()
     # bev_encoder.layer4 is built but never run (reference model/bev_encoder.py:21,23-36):
@@ -253,10 +258,14 @@ def main():
     g_flop = sum(work.get(k, 0.0) for k in gemm)
     g_launch = sum(kern[k][0] for k in gemm)
     g_tfs = g_flop / (g_ms * 1e-3) / 1e12
-    roofline = {"kernel": "e2ep::k_conv_gemm (implicit-GEMM conv forward + data gradient, "
-                          "v_mfma_f32_32x32x2_f32; the step's largest kernel family)",
-                "bound": "mfma", "achieved": round(g_tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
-                "unit": "TFLOP/s", "frac": round(g_tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+    lowp = args.precision != "fp32"
+    g_peak = BF16_MFMA_PEAK_TFS if lowp else FP32_MFMA_PEAK_TFS
+    roofline = {"kernel": ("e2ep::k_conv_gemm2 (implicit-GEMM conv forward + data gradient, "
+                           "v_mfma_f32_32x32x16_bf16)" if lowp else
+                           "e2ep::k_conv_gemm / k_conv_gemm2 (implicit-GEMM conv forward + data "
+                           "gradient, v_mfma_f32_32x32x2_f32)") + "; the step's largest kernel family",
+                "bound": "mfma", "achieved": round(g_tfs, 2), "peak": g_peak,
+                "unit": "TFLOP/s", "frac": round(g_tfs / g_peak, 4), "traffic": None,
                 "flop_per_step": g_flop / n_eager, "ms_per_step": round(g_ms / n_eager, 4),
                 "launches_per_step": g_launch // n_eager,
                 "timing": "HIP events around every conv fwd/dgrad launch of 3 eager fwd+bwd "
@@ -294,9 +303,13 @@ def main():
         line = {"metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "scaling": "weak", "vs_baseline": None,
+                "dtype": "bf16" if lowp else "f32", "data": "synthetic",
                 "config": {"workload": "ParkingModel train step (fwd + control/seg/depth losses + bwd "
-                                       "+ Adam), 4 cams x 256x256, fp32, random init",
+                                       "+ Adam), 4 cams x 256x256, " +
+                                       ("bf16 conv operands in forward / data gradient, fp32 "
+                                        "weight gradients, optimizer and all-reduce (C3)"
+                                        if lowp else "fp32") + ", random init",
                            "global_batch": world * args.batch, "batch_per_gpu": args.batch,
                            "parallelism": f"dp{world}"},
                 "world": {"size": world, "backend": backend, "rehearsal": rehearsal},
