@@ -2,12 +2,12 @@
 B=1 — the call agent/parking_agent.py:385 makes every control step (encoder + 3
 autoregressive ControlPredict passes, reference model/parking_model.py:72-78).
 
-    python scripts/bench_predict.py [--iters 200] [--cpu-iters 5] [--json out.json]
+    python scripts/bench_predict.py [--iters 200] [--cpu-iters 5] [--precision fp16] [--json out.json]
 Reports p50/p90 latency (ms) of (a) eager predict and (b) predict captured once into a HIP
 graph and replayed (static input buffers; the per-call inputs are copied into them on the
 stream, included in the timing), each call synchronised, plus the oracle (CPU restatement of
-the reference) on the host cores.  fp32 throughout: the kernels are fp32 (the fp16 variant
-of this config is not built)."""
+the reference) on the host cores.  --precision fp16 (C5) runs the conv GEMMs on fp16 operands
+(fp32 accumulation; e2ep_amd.precision); the tokens are compared with the fp32 run's."""
 import argparse
 import json
 import os
@@ -29,8 +29,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--cpu-iters", type=int, default=5)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--precision", choices=("fp32", "fp16", "bf16"), default="fp32")
     a = ap.parse_args()
-    from e2ep_amd import _lib, graphs, synthetic
+    from e2ep_amd import _lib, graphs, precision, synthetic
     from model.parking_model import ParkingModel
     from tool.config import default_cfg
 
@@ -44,9 +45,15 @@ def main():
     static = {k: host[k].to(dev) for k in keys}
     static["intrinsics"], static["extrinsics"] = host["intrinsics"], host["extrinsics"]
 
+    noise = synthetic.target_noise(1, seed=0).to(dev)  # fixed target jitter: comparable tokens
+
     def call():
         with torch.no_grad():
-            return m.predict(static)
+            return m.predict(static, noise)
+
+    with torch.no_grad():  # fp32 tokens, for the low-precision comparison
+        ref_tokens = m.predict(static, noise)[0].clone()
+    precision.set(a.precision)
 
     # (a) eager
     for _ in range(5):
@@ -79,6 +86,8 @@ def main():
         torch.cuda.synchronize()
         graph.append(time.perf_counter() - t0)
     same = bool(torch.equal(gout[0], out[0]))
+    same_fp32 = bool(torch.equal(gout[0], ref_tokens))
+    precision.set("fp32")
 
     # (c) the oracle on the host cores
     cpu = []
@@ -92,10 +101,12 @@ def main():
                 t0 = time.perf_counter()
                 ref.predict(host)
                 cpu.append(time.perf_counter() - t0)
-    res = {"config": "C5: ParkingModel.predict, B=1, 4 cams 256x256, fp32", "iters": a.iters,
+    res = {"config": f"C5: ParkingModel.predict, B=1, 4 cams 256x256, conv GEMM operands {a.precision}",
+           "precision": a.precision, "iters": a.iters,
            "eager_p50_ms": round(pct(eager, 50), 3), "eager_p90_ms": round(pct(eager, 90), 3),
            "graph_p50_ms": round(pct(graph, 50), 3), "graph_p90_ms": round(pct(graph, 90), 3),
-           "graph_tokens_equal_eager": same, "graph_memset_nodes_rewritten": nmem,
+           "graph_tokens_equal_eager": same, "tokens_equal_fp32": same_fp32,
+           "tokens": gout[0].cpu().tolist(), "graph_memset_nodes_rewritten": nmem,
            "cpu_oracle_p50_ms": round(pct(cpu, 50), 1) if cpu else None,
            "cpu_threads": torch.get_num_threads() if cpu else None,
            "published_ait_ms_rtx5000": 74.92}

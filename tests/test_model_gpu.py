@@ -97,3 +97,40 @@ def test_bn_counters_batched_like_reference():
     assert len(counts) > 90
     for k, v in counts.items():
         assert v == (0 if k.startswith("bev_encoder.layer4.") else 3), k
+
+
+@pytest.mark.parametrize("mode,tol", [("fp16", 5e-3), ("bf16", 3e-2)])
+def test_low_precision_predict_tokens_match_reference(mode, tol):
+    """C5 (fp16 closed-loop inference) and the C3 forward precision: ParkingModel.predict with
+    the conv GEMMs on fp16 / bf16 operands (e2ep_amd.precision), captured into a HIP graph and
+    replayed, gives the reference's control tokens and target plane exactly; the segmentation
+    and depth outputs stay within the format's rounding of the fp32 reference (rel-L2 `tol`:
+    fp16 keeps 11 mantissa bits, bf16 8)."""
+    from e2ep_amd import graphs, precision, synthetic
+    g = golden("model_eval_b1.npz")
+    m = _model(True).eval()
+    data = synthetic.synthetic_batch(1, seed=3)
+    noise = synthetic.target_noise(1, seed=3).to(DEV)
+    pdata = {k: (v if k in ("intrinsics", "extrinsics") else v.to(DEV)) for k, v in data.items()}
+    pdata["gt_control"] = pdata["gt_control"][:, :1]
+
+    def call():
+        with torch.no_grad():
+            return m.predict(pdata, noise)
+    with precision.use(mode):
+        call()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            call()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graph, out, _ = graphs.capture(call)
+        graph.replay()
+        torch.cuda.synchronize()
+    tok, ps, pd, tgt = out
+    assert np.array_equal(tok.cpu().numpy(), g["predict_tokens"])
+    assert np.array_equal(tgt.cpu().numpy(), g["bev_target"])
+    e_seg, e_dep = rel_l2(ps, g["pred_segmentation"]), rel_l2(pd, g["pred_depth"])
+    print(f"{mode} predict: seg rel-L2 {e_seg:.2e}, depth rel-L2 {e_dep:.2e}")
+    assert e_seg < tol and e_dep < tol
