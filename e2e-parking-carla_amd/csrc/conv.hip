@@ -30,6 +30,8 @@
 namespace e2ep {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BM = 64, BK = 16;
 constexpr int PADA = 4, PADB = 4;
@@ -66,7 +68,10 @@ __host__ __device__ __forceinline__ bool axis_live(int d, int n_out, int step, i
 // MODE 1: rows m = ci, K channels c = co, src = g [N,Cout,P,Q], dst = dx [N,Cin,H,W];
 //         phase z = (py, px), column pixel (u,v) -> (iy, ix) = (py + sh*u, px + sw*v);
 //         tap (r,s) valid for the phase: qy = u + (py + ph - r*dh)/sh (exact), qx likewise.
-template <int MODE, int ACT, int BNT, int BMT, bool AV>
+// OP (0 fp32 / 1 bf16 / 2 fp16) as for k_conv_gemm2 below: for low precision one 16-deep MFMA
+// per K-step takes lane half h's k = 8h .. 8h+7 (eight LDS reads per operand, as the eight
+// fp32 MFMAs would do).
+template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0>
 __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
@@ -247,13 +252,35 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   for (int t = 0; t < NACC; ++t) acc[t] = f32x16{0};
   const int li = lane & 31, lk = lane >> 5;
   auto compute = [&](int buf) {
+    if (OP == 0) {
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float a = As[buf][kk + lk][32 * wm + li];
+      for (int kk = 0; kk < BK; kk += 2) {
+        const float a = As[buf][kk + lk][32 * wm + li];
+#pragma unroll
+        for (int t = 0; t < NACC; ++t) {
+          const float b = Bs[buf][kk + lk][WC * wn + 32 * t + li];
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+        }
+      }
+    } else {
+      bf16x8 abf;
+      f16x8 ah;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = As[buf][8 * lk + j][32 * wm + li];
+        if (OP == 1) abf[j] = (__bf16)a; else ah[j] = (_Float16)a;
+      }
 #pragma unroll
       for (int t = 0; t < NACC; ++t) {
-        const float b = Bs[buf][kk + lk][WC * wn + 32 * t + li];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+        bf16x8 bbf;
+        f16x8 bh;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float b = Bs[buf][8 * lk + j][WC * wn + 32 * t + li];
+          if (OP == 1) bbf[j] = (__bf16)b; else bh[j] = (_Float16)b;
+        }
+        if (OP == 1) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(abf, bbf, acc[t], 0, 0, 0);
+        else acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[t], 0, 0, 0);
       }
     }
   };
@@ -360,9 +387,6 @@ __global__ void k_conv_reduce(const float *__restrict__ part, int splits, int M,
 // ------------------------------------------------------------------------------------------
 constexpr int V2_LDW = 20;    // LDS row stride in floats (16 k + 4 pad)
 constexpr int V2_TAIL = 256;  // max flattened (remainder channel, tap) rows
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // OP: MFMA operand precision — 0 fp32 (v_mfma_f32_32x32x2_f32, exact), 1 bf16 / 2 fp16
 // (v_mfma_f32_32x32x16_{bf16,f16}: the fragments are rounded to nearest-even when read from
@@ -1264,7 +1288,7 @@ static void gemm_extent(int mode, const ConvGeom &g, int &taps_max, long long &n
 // when there are >= 1024 of them (the segmentation 3x3 at 200x200); everything else (1x1
 // convs, small maps, split-K grids) stays on k_conv_gemm, which is faster there.
 static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt) {
-  if (g_gemm_variant == 1 && g_conv_precision == 0) return false;
+  if (g_gemm_variant == 1) return false;
   int taps;
   long long ncols;
   int nph;
@@ -1275,9 +1299,7 @@ static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt
   const long long b256 = cdiv(ncols, 256) * mblocks * nph, b128 = cdiv(ncols, 128) * mblocks * nph;
   const long long slots = 2LL * 256;  // 64 x 256 tiles resident per round (2 per CU)
   const bool fill256 = b256 >= slots && 100 * b256 >= 95 * (cdiv(b256, slots) * slots);
-  if (g_conv_precision != 0) {
-    wnt = b256 >= 512 ? 4 : 2;  // low-precision operands: every GEMM here (k_conv_gemm is fp32)
-  } else if (g_gemm_variant == 0) {
+  if (g_gemm_variant == 0) {
     if (g.R * g.S == 1 || M < 40) return false;
     if (!fill256 && b128 < 1024) return false;
     wnt = fill256 ? 4 : 2;
@@ -1334,9 +1356,18 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     out_bytes = (long long)gemm_workspace(p, M);
   }
   const bool av = mode == 0 && g.wlayout == 1 && (g.Cin & 3) == 0;
-#define GEMM_LAUNCH1(MD, AC, BT, BMT, V)                                                         \
-  hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V>), grid, dim3(256), 0, s, w, src, bias, out, \
-                     out_bytes, g, M, p.splits, p.kper)
+#define GEMM_LAUNCH1(MD, AC, BT, BMT, V)                                                          \
+  do {                                                                                             \
+    if (g_conv_precision == 1)                                                                     \
+      hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 1>), grid, dim3(256), 0, s, w, src, bias, \
+                         out, out_bytes, g, M, p.splits, p.kper);                                  \
+    else if (g_conv_precision == 2)                                                                \
+      hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 2>), grid, dim3(256), 0, s, w, src, bias, \
+                         out, out_bytes, g, M, p.splits, p.kper);                                  \
+    else                                                                                           \
+      hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 0>), grid, dim3(256), 0, s, w, src, bias, \
+                         out, out_bytes, g, M, p.splits, p.kper);                                  \
+  } while (0)
 #define GEMM_LAUNCH(MD, AC, BT, BMT)                                  \
   do {                                                                \
     if (MD == 0 && BMT == 64 && av) GEMM_LAUNCH1(MD, AC, BT, BMT, MD == 0 && BMT == 64); \

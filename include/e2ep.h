@@ -167,8 +167,8 @@ int e2ep_conv_gemm_variant(int variant);
  * MFMA), 1 = bf16, 2 = fp16 (operands rounded to nearest-even, fp32 products and
  * accumulation, fp32 tensors in and out) — BASELINE configs C3 (bf16 forward, fp32
  * gradients: the weight gradients, every other op, the optimizer and the all-reduce stay
- * fp32) and C5 (fp16 inference).  Convs outside the second-generation kernel's limits (the
- * direct tiny-K stem conv, 1x1 convs on 1x1 maps, tail tables over 256 rows) stay fp32.
+ * fp32) and C5 (fp16 inference).  Both GEMM generations take the setting; the direct tiny-K
+ * stem conv and 1x1 convs on 1x1 maps (squeeze-excitation) stay fp32.
  * Returns the previous value; out-of-range values only query.  Process-global. */
 int e2ep_conv_precision(int precision);
 int e2ep_conv_wgrad_splits(const int *dims);
