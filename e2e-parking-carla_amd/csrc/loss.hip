@@ -171,9 +171,13 @@ __device__ __forceinline__ float bce_term(float p, float l) {
   return (l - 1.f) * fmaxf(log1pf(-p), -100.f) - l * fmaxf(logf(p), -100.f);
 }
 
+// T is the ground-truth type: fp32, or fp64 as the reference dataset delivers it
+// (dataset/carla_dataset.py:107-113 returns float64 metres); the bin arithmetic runs in T, as
+// torch does on a T tensor.
+template <typename T>
 __global__ void __launch_bounds__(LOSS_THREADS)
-    k_depth_bce_fwd(const float *__restrict__ prob, const float *__restrict__ gt, int BN, int D,
-                    int H, int W, int down, float lo, float step, int *__restrict__ cls,
+    k_depth_bce_fwd(const float *__restrict__ prob, const T *__restrict__ gt, int BN, int D,
+                    int H, int W, int down, T lo, T step, int *__restrict__ cls,
                     float *__restrict__ part, float *__restrict__ part_fg) {
   __shared__ float red[LOSS_THREADS / 64];
   const int h = H / down, w = W / down;
@@ -183,16 +187,17 @@ __global__ void __launch_bounds__(LOSS_THREADS)
   if (i < cells) {
     const long long bn = i / (h * w);
     const int pix = (int)(i - bn * h * w), ci = pix / w, cj = pix - ci * w;
-    const float *g = gt + (bn * H + (long long)ci * down) * W + (long long)cj * down;
-    float mn = 1e5f;
+    const T *g = gt + (bn * H + (long long)ci * down) * W + (long long)cj * down;
+    T mn = T(1e5);
     for (int r = 0; r < down; ++r)
       for (int c = 0; c < down; ++c) {
-        const float d = g[(long long)r * W + c];
-        mn = fminf(mn, d == 0.f ? 1e5f : d);
+        const T d = g[(long long)r * W + c];
+        const T e = d == T(0) ? T(1e5) : d;
+        mn = e < mn ? e : mn;
       }
     // (d - (d0 - step)) / step, kept in [0, D+1) else 0, truncated: the bin; one-hot[1:]
-    const float b = (mn - lo) / step;
-    const int k = (b < (float)(D + 1) && b >= 0.f) ? (int)b : 0;
+    const T b = (mn - lo) / step;
+    const int k = (b < T(D + 1) && b >= T(0)) ? (int)b : 0;
     cls[i] = k;
     if (k >= 1) {
       fg = 1.f;
@@ -231,6 +236,23 @@ __global__ void __launch_bounds__(LOSS_THREADS)
 }  // namespace e2ep
 
 using namespace e2ep;
+
+template <typename T>
+static int depth_bce_fwd(const char *name, const float *prob, const T *gt, int BN, int D, int H,
+                         int W, int down, T lo, T step, float *loss, float *den, int *cls,
+                         void *workspace, void *stream) {
+  E2EP_REQUIRE(prob && gt && loss && den && cls && workspace, E2EP_EINVAL, "%s: null argument",
+               name);
+  E2EP_REQUIRE(BN > 0 && D > 0 && down > 0 && H % down == 0 && W % down == 0, E2EP_EINVAL,
+               "%s: bad shape H=%d W=%d down=%d", name, H, W, down);
+  const int nb = cdiv((long long)BN * (H / down) * (W / down), LOSS_THREADS);
+  float *part = static_cast<float *>(workspace), *part_fg = part + nb;
+  hipLaunchKernelGGL(k_depth_bce_fwd<T>, dim3(nb), dim3(LOSS_THREADS), 0, as_stream(stream), prob,
+                     gt, BN, D, H, W, down, lo, step, cls, part, part_fg);
+  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(LOSS_THREADS), 0, as_stream(stream), part,
+                     part_fg, nb, 0.f, loss, den);
+  return launch_status(name);
+}
 
 extern "C" {
 
@@ -303,17 +325,15 @@ size_t e2ep_depth_bce_workspace(int BN, int H, int W, int down) {
 int e2ep_depth_bce_fwd(const float *prob, const float *gt, int BN, int D, int H, int W, int down,
                        float lo, float step, float *loss, float *den, int *cls, void *workspace,
                        void *stream) {
-  E2EP_REQUIRE(prob && gt && loss && den && cls && workspace, E2EP_EINVAL,
-               "e2ep_depth_bce_fwd: null argument");
-  E2EP_REQUIRE(BN > 0 && D > 0 && down > 0 && H % down == 0 && W % down == 0, E2EP_EINVAL,
-               "e2ep_depth_bce_fwd: bad shape H=%d W=%d down=%d", H, W, down);
-  const int nb = cdiv((long long)BN * (H / down) * (W / down), LOSS_THREADS);
-  float *part = static_cast<float *>(workspace), *part_fg = part + nb;
-  hipLaunchKernelGGL(k_depth_bce_fwd, dim3(nb), dim3(LOSS_THREADS), 0, as_stream(stream), prob, gt,
-                     BN, D, H, W, down, lo, step, cls, part, part_fg);
-  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(LOSS_THREADS), 0, as_stream(stream), part,
-                     part_fg, nb, 0.f, loss, den);
-  return launch_status("e2ep_depth_bce_fwd");
+  return depth_bce_fwd("e2ep_depth_bce_fwd", prob, gt, BN, D, H, W, down, lo, step, loss, den,
+                       cls, workspace, stream);
+}
+
+int e2ep_depth_bce_fwd_f64(const float *prob, const double *gt, int BN, int D, int H, int W,
+                           int down, double lo, double step, float *loss, float *den, int *cls,
+                           void *workspace, void *stream) {
+  return depth_bce_fwd("e2ep_depth_bce_fwd_f64", prob, gt, BN, D, H, W, down, lo, step, loss, den,
+                       cls, workspace, stream);
 }
 
 int e2ep_depth_bce_bwd(const float *prob, const int *cls, const float *den, const float *gloss,

@@ -115,7 +115,8 @@ class _DepthBCE(torch.autograd.Function):
         den = torch.empty(1, dtype=torch.float32, device=dev)
         cls = torch.empty(BN * h * w, dtype=torch.int32, device=dev)
         ws = _ws(_lib.load().e2ep_depth_bce_workspace(BN, H, W, down), dev)
-        _lib.call("e2ep_depth_bce_fwd", _lib.ptr(prob), _lib.ptr(gt), BN, D, H, W, down, lo, step,
+        fn = "e2ep_depth_bce_fwd_f64" if gt.dtype == torch.float64 else "e2ep_depth_bce_fwd"
+        _lib.call(fn, _lib.ptr(prob), _lib.ptr(gt), BN, D, H, W, down, lo, step,
                   _lib.ptr(loss), _lib.ptr(den), _lib.ptr(cls), _lib.ptr(ws), _lib.stream())
         ctx.save_for_backward(prob, cls, den)
         return loss
@@ -138,6 +139,9 @@ def depth_bce(prob, gt, d_bound, down):
     D = int((d_bound[1] - d_bound[0]) / d_bound[2])
     if prob.shape != (B * N, D, H // down, W // down):
         raise _lib.E2EPError(f"depth_bce: prob {tuple(prob.shape)} vs gt {tuple(gt.shape)}")
-    g = gt.to(device=prob.device, dtype=torch.float32, non_blocking=True).contiguous()
-    lo = float(d_bound[0] - d_bound[2])  # evaluated in Python double, applied in fp32 (as torch)
+    # float64 depth (what the reference dataset yields) keeps float64 bin arithmetic; any other
+    # dtype is promoted/rounded to fp32, as torch computes on a float32 tensor
+    dt = torch.float64 if gt.dtype == torch.float64 else torch.float32
+    g = gt.to(device=prob.device, dtype=dt, non_blocking=True).contiguous()
+    lo = float(d_bound[0] - d_bound[2])  # evaluated in Python double, applied in the gt dtype
     return _DepthBCE.apply(prob, g, int(down), lo, float(d_bound[2]))

@@ -10,10 +10,10 @@ Synthetic batches follow SURVEY.md §8(d): every tensor is drawn from a CPU
 torch.Generator seeded per call, so the same (B, seed) gives the same batch on any host.
 The batch dict has exactly the reference schema (dataset/carla_dataset.py:379-423).
 """
-import math
-
 import numpy as np
 import torch
+
+from .carla_math import Location, Rotation, Transform
 
 # (x, y, z, pitch, yaw) in metres / degrees; order = front, left, right, rear
 # (dataset/carla_dataset.py:209-230, 266-270)
@@ -33,16 +33,8 @@ _CAM2PIXEL = np.array([[0, 1, 0, 0], [0, 0, -1, 0], [1, 0, 0, 0], [0, 0, 0, 1]],
 
 
 def _carla_inverse_matrix(x, y, z, pitch, yaw, roll=0.0):
-    cy, sy = math.cos(math.radians(yaw)), math.sin(math.radians(yaw))
-    cp, sp = math.cos(math.radians(pitch)), math.sin(math.radians(pitch))
-    cr, sr = math.cos(math.radians(roll)), math.sin(math.radians(roll))
-    rot = np.array([[cp * cy, cy * sp * sr - sy * cr, -cy * sp * cr - sy * sr],
-                    [cp * sy, sy * sp * sr + cy * cr, -sy * sp * cr + cy * sr],
-                    [sp, -cp * sr, cp * cr]])
-    inv = np.eye(4)
-    inv[:3, :3] = rot.T
-    inv[:3, 3] = -rot.T @ np.array([x, y, z])
-    return inv
+    t = Transform(Location(x, y, z), Rotation(pitch=pitch, yaw=yaw, roll=roll))
+    return np.array(t.get_inverse_matrix())
 
 
 def rig(n_cams=4, image=256, raw_w=400, raw_h=300, fov=100.0):

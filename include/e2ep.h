@@ -398,7 +398,9 @@ int e2ep_grad_gather(const int *chunks, int n_chunks, const long long *offsets,
  *    -> 0; lo = d_bound[0] - d_bound[2], step = d_bound[2]); BCE (log clamped at -100) over
  *    the cells with a label, summed / max(1, #such cells).  fwd writes loss, den (the
  *    normaliser) and cls [BN*h*w] (the class, 0 = background) for bwd; workspace
- *    e2ep_depth_bce_workspace(BN, H, W, down) bytes.
+ *    e2ep_depth_bce_workspace(BN, H, W, down) bytes.  e2ep_depth_bce_fwd_f64 takes the
+ *    float64 depth the reference dataset produces (dataset/carla_dataset.py:107-113) and
+ *    computes the bins in float64, as torch does on that tensor.
  * Backward kernels read the upstream gradient `gloss` (a device scalar) and write the full
  * input gradient (zeros where the loss does not depend on the input).
  * ------------------------------------------------------------------------------------- */
@@ -419,8 +421,29 @@ size_t e2ep_depth_bce_workspace(int BN, int H, int W, int down);
 int e2ep_depth_bce_fwd(const float *prob, const float *gt, int BN, int D, int H, int W, int down,
                        float lo, float step, float *loss, float *den, int *cls, void *workspace,
                        void *stream);
+int e2ep_depth_bce_fwd_f64(const float *prob, const double *gt, int BN, int D, int H, int W,
+                           int down, double lo, double step, float *loss, float *den, int *cls,
+                           void *workspace, void *stream);
 int e2ep_depth_bce_bwd(const float *prob, const int *cls, const float *den, const float *gloss,
                        int BN, int D, int hw, float *dprob, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Frame decode (dataset/carla_dataset.py:114-131, :494-515, :404-406): the per-step
+ * arithmetic of the reference data path on cached uint8 crops.
+ *  - e2ep_decode_frames: rgb / depth_rgb [*][hw][3] uint8 (either may be NULL); output
+ *    frame f reads source frame src_frame[f] (f when src_frame is NULL: a gather out of a
+ *    resident cache and the decode in one pass) -> image [frames][3][hw] fp32 = (v / 255 - mean_c) / std_c with the ImageNet mean / std
+ *    (torchvision ToTensor + Normalize, each step rounded to fp32), depth [frames][hw] fp64
+ *    metres = 1000 * ((R + 256 G + 65536 B) / (2^24 - 1)).  hw % 4 == 0; inputs 4-byte and
+ *    outputs 16-byte aligned.  Bit-identical to the reference's CPU arithmetic.
+ *  - e2ep_widen_u8_i64: rows x row_len uint8 class ids -> int64, output row r reading
+ *    source row src_row[r] (r when NULL); row_len % 4 == 0, src 4-byte and dst 16-byte
+ *    aligned.
+ * ------------------------------------------------------------------------------------- */
+int e2ep_decode_frames(const void *rgb, const void *depth_rgb, const long long *src_frame,
+                       long long frames, int hw, float *image, double *depth, void *stream);
+int e2ep_widen_u8_i64(const void *src, const long long *src_row, long long rows, int row_len,
+                      long long *dst, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * HIP-graph surgery: replace every memset node of a captured (not yet instantiated)

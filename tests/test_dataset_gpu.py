@@ -1,0 +1,110 @@
+"""The HIP frame decode (csrc/decode.hip) and GpuFrameLoader vs the reference data path.
+
+Bit-exact bar: the decode kernels restate integer / IEEE-rounded arithmetic (uint8 / 255,
+minus mean, over std in fp32; (R + 256 G + 65536 B) / (2^24 - 1) * 1000 in fp64), so every
+output must equal the CPU path's exactly (this repo's dataset/carla_dataset.py, itself pinned
+bit for bit to the reference's by tests/test_dataset_cpu.py)."""
+import numpy as np
+import pytest
+import torch
+
+import carla_fixture
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _cpu_decode(rgb, drgb):
+    from dataset.carla_dataset import depth_from_rgb, normalise_image
+    img = torch.stack([normalise_image(f) for f in rgb.reshape(-1, *rgb.shape[-3:])])
+    dep = torch.from_numpy(np.stack([depth_from_rgb(f) for f in drgb.reshape(-1, *drgb.shape[-3:])]))
+    return img, dep
+
+
+@pytest.mark.parametrize("frames,hw", [(1, 256), (8, 256), (3, 20), (5, 512)])
+def test_decode_frames_bit_exact(frames, hw):
+    from e2ep_amd import decode
+    g = np.random.default_rng(frames * hw)
+    rgb = g.integers(0, 256, (frames, hw, hw, 3), dtype=np.uint8)
+    drgb = g.integers(0, 256, (frames, hw, hw, 3), dtype=np.uint8)
+    drgb[0, 0, 0] = 255      # far plane: exactly 1000 m
+    drgb[-1, -1, -1] = 0     # zero depth
+    img, dep = decode.decode_frames(torch.from_numpy(rgb).to(DEV), torch.from_numpy(drgb).to(DEV))
+    want_img, want_dep = _cpu_decode(rgb, drgb)
+    assert img.dtype == torch.float32 and dep.dtype == torch.float64
+    assert torch.equal(img.cpu(), want_img)
+    assert torch.equal(dep.cpu(), want_dep)
+
+
+def test_decode_gather_and_widen():
+    from e2ep_amd import decode
+    g = np.random.default_rng(1)
+    rgb = torch.from_numpy(g.integers(0, 256, (12, 64, 64, 3), dtype=np.uint8)).to(DEV)
+    src = torch.tensor([11, 0, 5, 5, 3])
+    img, dep = decode.decode_frames(rgb, None, src_frame=src)
+    assert dep is None
+    full, _ = decode.decode_frames(rgb, None)
+    assert torch.equal(img, full[src.to(DEV)])
+    bev = torch.from_numpy(g.integers(0, 3, (6, 200, 200), dtype=np.uint8)).to(DEV)
+    assert torch.equal(decode.widen_rows(bev), bev.long())
+    rows = torch.tensor([5, 2, 2])
+    assert torch.equal(decode.widen_rows(bev, src_row=rows), bev.long()[rows.to(DEV)])
+
+
+def test_decode_rejects_bad_arguments():
+    from e2ep_amd import _lib, decode
+    rgb = torch.zeros(2, 6, 6, 3, dtype=torch.uint8, device=DEV)     # hw = 36 ok
+    with pytest.raises(_lib.E2EPError):
+        decode.decode_frames(rgb, None, src_frame=torch.tensor([2]))  # out of range
+    with pytest.raises(_lib.E2EPError):
+        decode.decode_frames(torch.zeros(2, 5, 5, 3, dtype=torch.uint8, device=DEV))  # hw % 4
+    with pytest.raises(_lib.E2EPError):
+        decode.decode_frames(rgb.float())
+    with pytest.raises(_lib.E2EPError):
+        decode.widen_rows(torch.zeros(3, 5, dtype=torch.uint8, device=DEV))  # row_len % 4
+
+
+@pytest.fixture(scope="module")
+def mini(tmp_path_factory):
+    from dataset.carla_dataset import CarlaDataset
+    from dataset.frame_cache import build_frame_cache
+    d = str(tmp_path_factory.mktemp("carla"))
+    carla_fixture.make_dataset(d, frames=16)
+    cfg = carla_fixture.config(d, batch_size=4)
+    ds = CarlaDataset(d, 1, cfg)
+    cache = build_frame_cache(ds, str(tmp_path_factory.mktemp("fc")))
+    return ds, cache
+
+
+@pytest.mark.parametrize("resident", [False, True])
+def test_gpu_loader_equals_reference_collate(mini, resident):
+    from torch.utils.data import default_collate
+    from dataset.frame_cache import GpuFrameLoader
+    ds, cache = mini
+    loader = GpuFrameLoader(cache, 3, shuffle=True, drop_last=False, seed=5, resident=resident)
+    order = loader.batches()
+    n = 0
+    for idx, batch in zip(order, loader):
+        want = default_collate([ds[int(i)] for i in idx])
+        assert sorted(batch) == sorted(want)
+        for k, v in want.items():
+            on_dev = k not in ("intrinsics", "extrinsics")   # the rig stays on the host
+            assert batch[k].is_cuda == on_dev, k
+            assert batch[k].dtype == v.dtype and batch[k].shape == v.shape, k
+            assert torch.equal(batch[k].cpu(), v), k
+        n += len(idx)
+    assert n == len(ds)
+
+
+def test_gpu_loader_trains_a_step(mini):
+    """A batch from the loader drives the training step (float64 depth into the depth loss)."""
+    from dataset.frame_cache import GpuFrameLoader
+    from trainer.pl_trainer import ParkingTrainingModule
+    ds, cache = mini
+    cfg = ds.cfg
+    batch = next(iter(GpuFrameLoader(cache, 2, shuffle=False)))
+    module = ParkingTrainingModule(cfg).to(DEV)
+    module.train()
+    loss = module.training_step(batch, 0)
+    assert torch.isfinite(loss)
+    loss.backward()

@@ -99,3 +99,26 @@ def test_depth_bce_matches_reference(B, N, H):
     # labels: the reference's own one-hot helper on the same depth map
     lab = losses.depth_onehot(depth, (0.5, 12.5, 0.25), 8)
     assert torch.equal(lab, O.depth_labels(depth))
+
+
+def test_depth_bce_float64_depth_bins_in_float64():
+    """The reference dataset yields float64 metres (dataset/carla_dataset.py:107-113), so the
+    reference bins them in float64: a depth 1e-9 below a bin edge falls in the lower bin, while
+    its fp32 rounding lands on the edge (upper bin).  The fp64 entry point must follow float64."""
+    from e2ep_amd import losses
+    O = _oracle()
+    g = torch.Generator().manual_seed(7)
+    prob = torch.randn(2, 48, 32, 32, generator=g).softmax(1)
+    depth = torch.rand(1, 2, 256, 256, generator=g, dtype=torch.float64) * 15.0
+    depth[0, 0, :8, :8] = 0.75 - 1e-9   # fp64: bin 1; fp32 rounds to 0.75: bin 2
+    depth[0, 1, :8, :8] = 3.0 - 1e-10
+    ref_in = prob.double().requires_grad_()
+    ref = O.depth_loss(ref_in, depth)
+    ref.backward()
+    x = prob.to(DEV).requires_grad_()
+    out = losses.depth_bce(x, depth.to(DEV), (0.5, 12.5, 0.25), 8)
+    out.backward()
+    assert abs(float(out) / float(ref) - 1) < 1e-6
+    assert rel_l2(x.grad, ref_in.grad) < 1e-6
+    out32 = losses.depth_bce(prob.to(DEV), depth.float().to(DEV), (0.5, 12.5, 0.25), 8)
+    assert float(out32) != float(out)   # the fp32 path bins the edge cells differently
