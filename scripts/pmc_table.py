@@ -41,9 +41,16 @@ def main():
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 if c in cs:
                     print(f"   {c + ' / WAVE_CYCLES':40s} {cs[c] / wc:8.3f}")
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "SQ_BUSY_CYCLES" in cs and cs["SQ_BUSY_CYCLES"]:
-            print(f"   {'MFMA busy / SQ busy (x4 SIMD?)':40s} "
-                  f"{cs['SQ_VALU_MFMA_BUSY_CYCLES'] / cs['SQ_BUSY_CYCLES']:8.3f}")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and cs.get("GRBM_GUI_ACTIVE"):
+            # MFMA busy is summed over all 1024 SIMDs (64 cycles per fp32 32x32x2 MFMA, i.e.
+            # 64 FLOP / SIMD / cycle = the 157.3 TF peak at 2.4 GHz); GRBM_GUI_ACTIVE is
+            # summed over the 8 XCDs, so one XCD's active cycles = GRBM / 8.
+            util = cs["SQ_VALU_MFMA_BUSY_CYCLES"] / (cs["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            print(f"   {'MFMA utilisation (busy / (GRBM/8 x 1024))':40s} {util:8.3f}")
+            print(f"   {'MFMA FLOP issued (busy x 64), GFLOP':40s} "
+                  f"{cs['SQ_VALU_MFMA_BUSY_CYCLES'] * 64 / 1e9:8.2f}")
+            print(f"   {'kernel time (GRBM/8 / 2.4 GHz), us':40s} "
+                  f"{cs['GRBM_GUI_ACTIVE'] / 8 / 2.4e3:8.1f}")
         if "FETCH_SIZE" in cs:
             print(f"   {'HBM read (FETCH_SIZE x2, KB->MB)':40s} {2 * cs['FETCH_SIZE'] / 1e3:8.1f}")
         if "WRITE_SIZE" in cs:
