@@ -1,0 +1,361 @@
+// Strided fp32 GEMM on MFMA for the transformer linears (nn.Linear forward and both
+// backward GEMMs of model/feature_fusion.py:13-14,24-29,48-50 and model/control_predict.py:
+// 18-24: d = 258 / 774 / 2048 at 2048 encoder rows and 112 decoder rows).
+//
+//   C[m][n] = sum_k A(m, k) * B(k, n)  (+ bias[n])  (+ Cadd[m][n])  (then ReLU if asked)
+//   A(m, k) = AK ? A[m * lda + k] : A[k * lda + m]
+//   B(k, n) = BKC ? B[n * ldb + k] : B[k * ldb + n]
+//
+// Forward y = x W^T + b is (AK, BKC); dX = dY W is (AK, !BKC); dW = dY^T X is (!AK, !BKC).
+// Design (the k_conv_gemm2 scheme, CDNA4 fp32 MFMA v_mfma_f32_32x32x2_f32):
+//  * block (64 TM) x (64 TN), 4 waves as 2 x 2, wave tile 32 TM x 32 TN (each A fragment
+//    feeds TN MFMAs, each B fragment TM); K-step 32;
+//  * LDS rows are k-contiguous ([row][32 + 4 pad]) whatever the global layout, so a lane's
+//    16 fragment values are four ds_read_b128 (lane half h supplies k = 16h..16h+15 to the 16
+//    MFMAs of a step — the sum over the 32 k is the same, its order fixed);
+//  * global loads are raw buffer loads with out-of-range offsets for the M / N / K edges
+//    (returns 0: no padding copies, K = 258 needs no special case); the next step's tile is
+//    loaded into registers while the current one feeds the MFMAs;
+//  * small grids split K (fixed-order reduction in k_gemm_reduce, so results are
+//    deterministic run to run), large ones write C directly with the fused epilogue.
+#include <algorithm>
+
+#include "common.h"
+
+namespace e2ep {
+
+typedef float g_f32x16 __attribute__((ext_vector_type(16)));
+
+typedef float g_f2 __attribute__((ext_vector_type(2)));
+__device__ g_f2 e2ep_raw_buffer_load_v2f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
+                                           int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.v2f32");
+__device__ __forceinline__ float2 bload2(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  const g_f2 v = e2ep_raw_buffer_load_v2f32(r, byte_off, 0, 0);
+  return make_float2(v[0], v[1]);
+}
+
+// v & (ok ? ~0 : 0) as one v_and_b32 the compiler cannot turn back into a branch
+__device__ __forceinline__ float kmask(float v, bool ok) {
+  const unsigned m = ok ? 0xffffffffu : 0u;
+  unsigned r;
+  asm volatile("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(__builtin_bit_cast(unsigned, v)), "v"(m));
+  return __builtin_bit_cast(float, r);
+}
+constexpr int G_BK = 32;
+constexpr int G_LDW = 36;  // LDS row stride in floats (32 k + 4 pad)
+
+template <bool AK, bool BKC, int TM, int TN>
+__global__ void __launch_bounds__(256)
+    k_gemm(const float *__restrict__ A, int lda, long long a_bytes, int avec,
+           const float *__restrict__ B, int ldb, long long b_bytes, int bvec,
+           const float *__restrict__ bias, const float *__restrict__ Cadd, int ldadd,
+           float *__restrict__ C, int ldc, int M, int N, int K, int kper, int relu) {
+  constexpr int BM = 64 * TM, BN = 64 * TN;
+  __shared__ __attribute__((aligned(16))) float As[2][BM][G_LDW];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][G_LDW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int split = blockIdx.z;
+  const int ksteps = (K + G_BK - 1) / G_BK;
+  const int kbeg = split * kper;
+  const int kend = min(ksteps, kbeg + kper);
+  const int nk = max(0, kend - kbeg);
+  const __amdgpu_buffer_rsrc_t ra_ = rsrc(A, a_bytes), rb_ = rsrc(B, b_bytes);
+
+  // Each operand tile is TM (TN) groups of 64 rows x 32 k; per group a thread loads 8 k of
+  // one row: k-contiguous operands -> (row tid/4, k octet tid%4), float4s when aligned;
+  // m/n-contiguous operands -> (row tid%64, k octet tid/64), lanes coalesced along the row.
+  const int ar = AK ? tid >> 2 : tid & 63, aq = AK ? tid & 3 : tid >> 6;
+  const int br = BKC ? tid >> 2 : tid & 63, bq = BKC ? tid & 3 : tid >> 6;
+
+  float ra[TM][8], rb[TN][8];
+  // Loads are unconditional: the row index is clamped into the matrix (rows past M / N only
+  // feed outputs that are never stored) and k into [0, K); values at k >= K are zeroed with
+  // an integer mask when the registers are written to LDS (after the step's MFMAs, so the
+  // loads stay in flight).  Guarded loads (`ok ? offset : OOR`) let the compiler split the
+  // loop into per-load exec-masked branches, which serialised the loads.
+  auto load_op = [&](auto &regs, const __amdgpu_buffer_rsrc_t &rs, bool kcontig, int vec, int ld,
+                     int row0, int rows, int r, int q, int k0, int i) {
+    const int row = min(row0 + 64 * i + r, rows - 1);
+    const int k = k0 + 8 * q;
+    if (kcontig) {
+      const long long base = (long long)row * ld;
+      if (vec == 2 && k0 + G_BK <= K) {  // uniform: a full, 16-byte aligned step -> 2 float4s
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 v = bload4(rs, (int)((base + k + 4 * h) * 4));
+          regs[i][4 * h] = v.x; regs[i][4 * h + 1] = v.y; regs[i][4 * h + 2] = v.z; regs[i][4 * h + 3] = v.w;
+        }
+      } else if (vec == 1 && k0 + G_BK <= K) {  // 8-byte aligned rows (even ld) -> 4 float2s
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const float2 v = bload2(rs, (int)((base + k + 2 * h) * 4));
+          regs[i][2 * h] = v.x; regs[i][2 * h + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          regs[i][j] = bload(rs, (int)((base + min(k + j, K - 1)) * 4));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        regs[i][j] = bload(rs, (int)(((long long)min(k + j, K - 1) * ld + row) * 4));
+    }
+  };
+  auto load_tiles = [&](int ks_in) {
+    const int k0 = min(ks_in, kend - 1) * G_BK;  // past the range: re-read, never stored
+#pragma unroll
+    for (int i = 0; i < TM; ++i) load_op(ra, ra_, AK, avec, lda, m0, M, ar, aq, k0, i);
+#pragma unroll
+    for (int i = 0; i < TN; ++i) load_op(rb, rb_, BKC, bvec, ldb, n0, N, br, bq, k0, i);
+  };
+  // LDS writes: regs -> k-contiguous rows; the zero mask for k >= K applied here
+  auto store_op = [&](auto &regs, float (*T)[G_LDW], int r, int q, int k0, bool full, int i) {
+    if (!full)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) regs[i][j] = kmask(regs[i][j], k0 + 8 * q + j < K);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      *reinterpret_cast<float4 *>(&T[64 * i + r][8 * q + 4 * h]) =
+          make_float4(regs[i][4 * h], regs[i][4 * h + 1], regs[i][4 * h + 2], regs[i][4 * h + 3]);
+  };
+  auto store_tiles = [&](int buf, int ks) {
+    const int k0 = ks * G_BK;
+    const bool full = k0 + G_BK <= K;  // uniform
+#pragma unroll
+    for (int i = 0; i < TM; ++i) store_op(ra, As[buf], ar, aq, k0, full, i);
+#pragma unroll
+    for (int i = 0; i < TN; ++i) store_op(rb, Bs[buf], br, bq, k0, full, i);
+  };
+
+  // wave (wm, wn) owns rows 32 TM wm + 32 u and columns 32 TN wn + 32 t
+  g_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int u = 0; u < TM; ++u)
+#pragma unroll
+    for (int t = 0; t < TN; ++t) acc[u][t] = g_f32x16{0};
+  const int li = lane & 31, lh = lane >> 5;
+  // lane half h supplies k = 16h .. 16h+15 to the 16 MFMAs of a step
+  auto compute = [&](int buf) {
+    float a[TM][16], b[TN][16];
+#pragma unroll
+    for (int u = 0; u < TM; ++u) {
+      const float *p = &As[buf][32 * TM * wm + 32 * u + li][16 * lh];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4 *>(p + 4 * q);
+        a[u][4 * q] = x.x; a[u][4 * q + 1] = x.y; a[u][4 * q + 2] = x.z; a[u][4 * q + 3] = x.w;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const float *p = &Bs[buf][32 * TN * wn + 32 * t + li][16 * lh];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4 *>(p + 4 * q);
+        b[t][4 * q] = x.x; b[t][4 * q + 1] = x.y; b[t][4 * q + 2] = x.z; b[t][4 * q + 3] = x.w;
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int u = 0; u < TM; ++u)
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+          acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][kk], b[t][kk], acc[u][t], 0, 0, 0);
+  };
+  if (nk > 0) {
+    load_tiles(kbeg);
+    store_tiles(0, kbeg);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      load_tiles(kbeg + kt + 1);  // past the range: re-read, never stored
+      compute(kt & 1);
+      if (kt + 1 < nk) store_tiles((kt + 1) & 1, kbeg + kt + 1);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+  // gridDim.z > 1: raw partial sums into C = workspace[split][M][N] (row stride N).
+  const bool final_ = gridDim.z == 1;
+  float *dst = final_ ? C : C + (long long)split * M * N;
+  const int ldd = final_ ? ldc : N;
+  // edges: buffer stores with out-of-range offsets are dropped; the epilogue's optional
+  // inputs are behind uniform branches, and the 16 Cadd values of a tile are loaded together
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, 4LL * ((long long)(M - 1) * ldd + N));
+  const __amdgpu_buffer_rsrc_t rc = rsrc(Cadd, Cadd ? 4LL * ((long long)(M - 1) * ldadd + N) : 0);
+  const bool add_c = final_ && Cadd != nullptr, add_b = final_ && bias != nullptr;
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    const int n = n0 + 32 * TN * wn + 32 * t + li;
+    const bool nok = n < N;
+    const float bn_ = add_b ? bias[min(n, N - 1)] : 0.f;
+#pragma unroll
+    for (int u = 0; u < TM; ++u) {
+      float cv[16];
+      if (add_c) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + 32 * TM * wm + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          cv[r] = bload(rc, (nok && m < M) ? (int)(((long long)m * ldadd + n) * 4) : OOR);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 32 * TM * wm + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        float v = acc[u][t][r];
+        if (add_b) v += bn_;
+        if (add_c) v += cv[r];
+        if (final_ && relu) v = fmaxf(v, 0.f);
+        bstore(rd, (nok && m < M) ? (int)(((long long)m * ldd + n) * 4) : OOR, v);
+      }
+    }
+  }
+}
+
+// C[m][n] = sum over splits in order (+ bias) (+ Cadd) (ReLU).  V = 4: four consecutive
+// elements per thread with 16-byte loads / stores (dense C and Cadd, M * N % 4 == 0).
+template <int V>
+__global__ void __launch_bounds__(256)
+    k_gemm_reduce(const float *__restrict__ part, int splits, int M, int N,
+                  const float *__restrict__ bias, const float *__restrict__ Cadd, int ldadd,
+                  float *__restrict__ C, int ldc, int relu) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * V;
+  const long long MN = (long long)M * N;
+  if (i >= MN) return;
+  float s[V];
+  if (V == 4) {
+    float4 a = *reinterpret_cast<const float4 *>(part + i);
+    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+    for (int k = 1; k < splits; ++k) {
+      a = *reinterpret_cast<const float4 *>(part + k * MN + i);
+      s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
+    }
+  } else {
+    s[0] = part[i];
+    for (int k = 1; k < splits; ++k) s[0] += part[k * MN + i];
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const long long e = i + v;
+    const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+    if (bias) s[v] += bias[n];
+    if (Cadd) s[v] += Cadd[(long long)m * ldadd + n];
+    if (relu) s[v] = fmaxf(s[v], 0.f);
+    if (V == 1) C[(long long)m * ldc + n] = s[v];
+  }
+  if (V == 4) *reinterpret_cast<float4 *>(C + i) = make_float4(s[0], s[1], s[2], s[3]);
+}
+
+struct GemmLaunch {
+  int tm, tn, splits, kper;
+};
+
+// 64 x 64 tiles (the sweep over 64/128-wide tiles, scripts/bench_gemm.py --sweep: they are
+// the fastest or within 6 % on every transformer shape — more waves per CU hide more load
+// latency); K split toward ~768 workgroups (3 per CU), at most 8 ways and >= 8 K-steps each.
+static int g_force_tm = 0, g_force_tn = 0, g_force_splits = 0;  // 0: automatic
+
+static GemmLaunch gemm_plan(int M, int N, int K) {
+  GemmLaunch p{1, 1, 1, 1};
+  const int ksteps = cdiv(K, G_BK);
+  if (g_force_tm > 0) {  // benchmarking override (e2ep_gemm_force)
+    p.tm = g_force_tm;
+    p.tn = g_force_tn;
+    p.splits = std::max(1, std::min(g_force_splits, ksteps));
+  } else {
+    const long long blocks = (long long)cdiv(M, 64) * cdiv(N, 64);
+    const int cap = std::min(8, std::max(1, ksteps / 8));
+    p.splits = (int)std::min<long long>(cap, std::max(1LL, (long long)cdiv(768, blocks)));
+  }
+  p.kper = cdiv(ksteps, p.splits);
+  p.splits = cdiv(ksteps, p.kper);
+  return p;
+}
+
+}  // namespace e2ep
+
+using namespace e2ep;
+
+extern "C" {
+
+int e2ep_gemm_force(int tm, int tn, int splits) {
+  E2EP_REQUIRE(tm >= 0 && tm <= 2 && tn >= 0 && tn <= 2 && splits >= 0 && (tm == 0) == (tn == 0),
+               E2EP_EINVAL, "e2ep_gemm_force: tm, tn in {1, 2} (0 = automatic)");
+  g_force_tm = tm;
+  g_force_tn = tn;
+  g_force_splits = splits;
+  return 0;
+}
+
+size_t e2ep_gemm_workspace(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const GemmLaunch p = gemm_plan(M, N, K);
+  return p.splits > 1 ? (size_t)p.splits * M * N * sizeof(float) : 0;
+}
+
+int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
+              const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
+              int K, int relu, void *workspace, void *stream) {
+  E2EP_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0, E2EP_EINVAL,
+               "e2ep_gemm: bad arguments M=%d N=%d K=%d", M, N, K);
+  E2EP_REQUIRE(lda >= (a_kcontig ? K : M) && ldb >= (b_kcontig ? K : N) && ldc >= N &&
+                   (!Cadd || ldadd >= N),
+               E2EP_EINVAL, "e2ep_gemm: leading dimension too small");
+  const long long a_bytes = 4LL * (a_kcontig ? (long long)(M - 1) * lda + K : (long long)(K - 1) * lda + M);
+  const long long b_bytes = 4LL * (b_kcontig ? (long long)(N - 1) * ldb + K : (long long)(K - 1) * ldb + N);
+  E2EP_REQUIRE(a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL &&
+                   4LL * ((long long)(M - 1) * std::max(ldc, ldadd) + N) < 0x7fffffffLL,
+               E2EP_ERANGE, "e2ep_gemm: operand larger than 2 GB");
+  const GemmLaunch p = gemm_plan(M, N, K);
+  E2EP_REQUIRE(p.splits == 1 || workspace, E2EP_EINVAL,
+               "e2ep_gemm: workspace of e2ep_gemm_workspace() bytes required");
+  hipStream_t s = as_stream(stream);
+  float *out = p.splits > 1 ? static_cast<float *>(workspace) : C;
+  dim3 grid(cdiv(N, 64 * p.tn), cdiv(M, 64 * p.tm), p.splits);
+  // vector loads along k for k-contiguous operands: 2 = float4 (rows 16-byte aligned), 1 =
+  // float2 (8-byte aligned: the d = 258 rows).  Row-contiguous operands stay on dword loads
+  // (lanes consecutive along the row, 256 B per instruction): a float2 row-pair variant
+  // measured 1.2 - 1.5x slower on the weight-gradient shapes (scripts/bench_gemm.py --sweep).
+  auto vec_of = [](int kc, int ld, const void *ptr) {
+    if (!kc) return 0;
+    if (ld % 4 == 0 && ((uintptr_t)ptr & 15) == 0) return 2;
+    return ld % 2 == 0 && ((uintptr_t)ptr & 7) == 0 ? 1 : 0;
+  };
+  const int avec = vec_of(a_kcontig, lda, A), bvec = vec_of(b_kcontig, ldb, B);
+#define E2EP_GEMM_LAUNCH(AKV, BKV, TMV, TNV)                                                    \
+  hipLaunchKernelGGL((k_gemm<AKV, BKV, TMV, TNV>), grid, dim3(256), 0, s, A, lda, a_bytes, avec, \
+                     B, ldb, b_bytes, bvec, bias, Cadd, ldadd, out, ldc, M, N, K, p.kper, relu)
+#define E2EP_GEMM_T(AKV, BKV)                                            \
+  do {                                                                   \
+    if (p.tm == 2 && p.tn == 2) E2EP_GEMM_LAUNCH(AKV, BKV, 2, 2);        \
+    else if (p.tm == 2) E2EP_GEMM_LAUNCH(AKV, BKV, 2, 1);                \
+    else if (p.tn == 2) E2EP_GEMM_LAUNCH(AKV, BKV, 1, 2);                \
+    else E2EP_GEMM_LAUNCH(AKV, BKV, 1, 1);                               \
+  } while (0)
+  if (a_kcontig && b_kcontig) E2EP_GEMM_T(true, true);
+  else if (a_kcontig) E2EP_GEMM_T(true, false);
+  else if (b_kcontig) E2EP_GEMM_T(false, true);
+  else E2EP_GEMM_T(false, false);
+#undef E2EP_GEMM_T
+#undef E2EP_GEMM_LAUNCH
+  if (p.splits > 1) {
+    const long long MN = (long long)M * N;
+    const bool v4 = MN % 4 == 0 && ldc == N && ((uintptr_t)C & 15) == 0;
+    if (v4)
+      hipLaunchKernelGGL(k_gemm_reduce<4>, dim3(cdiv(MN / 4, 256)), dim3(256), 0, s,
+                         static_cast<const float *>(workspace), p.splits, M, N, bias, Cadd, ldadd,
+                         C, ldc, relu);
+    else
+      hipLaunchKernelGGL(k_gemm_reduce<1>, dim3(cdiv(MN, 256)), dim3(256), 0, s,
+                         static_cast<const float *>(workspace), p.splits, M, N, bias, Cadd, ldadd,
+                         C, ldc, relu);
+  }
+  return launch_status("e2ep_gemm");
+}
+
+}  // extern "C"

@@ -89,6 +89,9 @@ SIGNATURES = {
     "e2ep_depth_bce_workspace": (_sz, [_i, _i, _i, _i]),
     "e2ep_depth_bce_fwd": (_i, [_p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p]),
     "e2ep_depth_bce_fwd_f64": (_i, [_p, _p, _i, _i, _i, _i, _i, _d, _d, _p, _p, _p, _p, _p]),
+    "e2ep_gemm_workspace": (_sz, [_i, _i, _i]),
+    "e2ep_gemm_force": (_i, [_i, _i, _i]),
+    "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_decode_frames": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p]),
     "e2ep_widen_u8_i64": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_depth_bce_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p]),

@@ -589,52 +589,87 @@ def add_drop_layer_norm(a, b, norm, p=0.0):
 
 
 # ------------------------------------------------------------------------------------------
-# nn.Linear with the bias gradient on e2ep_col_sum
+# nn.Linear on e2ep_gemm (forward, input gradient, weight gradient) + e2ep_col_sum (bias grad)
 # ------------------------------------------------------------------------------------------
+def gemm(A, a_kcontig, B, b_kcontig, M, N, K, bias=None, cadd=None, out=None, relu=False,
+         tag="gemm"):
+    """C (M x N, row-major) = A(m,k) B(k,n) (+ bias[n]) (+ cadd) (ReLU) on e2ep_gemm.
+    A is (M x K) when a_kcontig else (K x M), B is (N x K) when b_kcontig else (K x N); both
+    row-major with unit inner stride."""
+    for t, n in ((A, "A"), (B, "B")):
+        if t.dim() != 2 or t.stride(1) != 1 or t.dtype != torch.float32:
+            raise _lib.E2EPError(f"gemm: {n} must be a 2-D fp32 matrix with unit inner stride")
+    want_a = (M, K) if a_kcontig else (K, M)
+    want_b = (N, K) if b_kcontig else (K, N)
+    if tuple(A.shape) != want_a or tuple(B.shape) != want_b:
+        raise _lib.E2EPError(f"gemm: A {tuple(A.shape)} / B {tuple(B.shape)} vs M={M} N={N} K={K}")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=A.device)
+    if cadd is not None and (cadd.shape != (M, N) or cadd.stride(1) != 1):
+        raise _lib.E2EPError("gemm: cadd must be (M, N) with unit inner stride")
+    ws = _ws(_lib.load().e2ep_gemm_workspace(M, N, K), A.device)
+    with timing.region(timing.name("gemm", (M, N, K), tag), 2.0 * M * N * K):
+        _lib.call("e2ep_gemm", _lib.ptr(A), A.stride(0), int(a_kcontig), _lib.ptr(B), B.stride(0),
+                  int(b_kcontig), _lib.ptr(bias), _lib.ptr(cadd),
+                  cadd.stride(0) if cadd is not None else 0, _lib.ptr(out), out.stride(0), M, N, K,
+                  int(relu), _lib.ptr(ws), _lib.stream())
+    return out
+
+
 class _Linear(torch.autograd.Function):
-    """y = x W^T + b.  Forward and the two backward GEMMs stay hipBLASLt (torch.mm); the bias
-    gradient (a column sum over all rows, which torch runs as a 3-8 workgroup reduction for
-    the transformer's 2048 x 258 gradients) is e2ep_col_sum."""
+    """y = x W^T + b (+ ReLU).  All three GEMMs are e2ep_gemm: forward (bias and ReLU in the
+    epilogue), dX = dY W (the residual's gradient added in the epilogue when skip is used),
+    dW = dY^T X; the bias gradient is e2ep_col_sum."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, skip=False):
-        ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
-        y = F.linear(x, weight, bias)
+    def forward(ctx, x, weight, bias, skip=False, relu=False):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if x2.stride(1) != 1 or x2.stride(0) != K:
+            x2 = x2.contiguous()
+        N = weight.shape[0]
+        y = gemm(x2, True, weight, True, x2.shape[0], N, K, bias=bias, relu=relu, tag="linear_fwd")
+        ctx.save_for_backward(x2, weight, y if relu else None)
+        ctx.has_bias, ctx.relu, ctx.xshape = bias is not None, relu, x.shape
+        y = y.view(*x.shape[:-1], N)
         # skip: also hand x back for the layer's residual connection; that gradient is then
-        # accumulated by the input-gradient GEMM itself (addmm), not by an autograd add
+        # accumulated by the input-gradient GEMM's epilogue, not by an autograd add
         return (y, x) if skip else y
 
     @staticmethod
     def backward(ctx, gy, gskip=None):
-        x, weight = ctx.saved_tensors
+        x2, weight, y = ctx.saved_tensors
         nig = ctx.needs_input_grad
-        g2 = gy.reshape(-1, gy.shape[-1])
+        M, K = x2.shape
+        N = weight.shape[0]
+        g2 = gy.reshape(M, N)
+        if g2.stride(1) != 1 or g2.stride(0) != N:
+            g2 = g2.contiguous()
+        if ctx.relu:
+            g2 = g2 * (y > 0)
         dx = dw = db = None
         if nig[0]:
-            if gskip is not None:
-                dx = torch.addmm(gskip.reshape(g2.shape[0], -1), g2, weight).view(x.shape)
-            else:
-                dx = (g2 @ weight).view(x.shape)
+            cadd = gskip.reshape(M, K) if gskip is not None else None
+            if cadd is not None and cadd.stride(1) != 1:
+                cadd = cadd.contiguous()
+            dx = gemm(g2, True, weight, False, M, K, N, cadd=cadd, tag="linear_dgrad").view(ctx.xshape)
         if nig[1]:
-            dw = g2.t() @ x.reshape(-1, x.shape[-1])
+            dw = gemm(g2, False, x2, False, N, K, M, tag="linear_wgrad")
         if ctx.has_bias and nig[2]:
-            g2 = g2.contiguous()
-            rows, C = g2.shape
-            db = torch.empty(C, dtype=torch.float32, device=gy.device)
-            ws = _ws(_lib.load().e2ep_col_sum_workspace(rows, C), gy.device)
-            _lib.call("e2ep_col_sum", _lib.ptr(g2), rows, C, _lib.ptr(db), _lib.ptr(ws), _lib.stream())
-        return dx, dw, db, None
+            db = torch.empty(N, dtype=torch.float32, device=gy.device)
+            ws = _ws(_lib.load().e2ep_col_sum_workspace(M, N), gy.device)
+            _lib.call("e2ep_col_sum", _lib.ptr(g2), M, N, _lib.ptr(db), _lib.ptr(ws), _lib.stream())
+        return dx, dw, db, None, None
 
 
-def linear(x, weight, bias=None, skip=False):
-    """F.linear(x, weight, bias) with an e2ep bias gradient (fp32 HIP tensors); other inputs
-    (CPU, other dtypes) go to F.linear itself.  skip=True returns (y, x_skip): use x_skip for
-    the residual connection around this layer and its gradient joins dx inside the GEMM."""
-    if not x.is_cuda or x.dtype != torch.float32 or (bias is None or not bias.requires_grad):
-        y = F.linear(x, weight, bias)
-        return (y, x) if skip else y
-    return _Linear.apply(x, weight, bias, bool(skip))
+def linear(x, weight, bias=None, skip=False, relu=False):
+    """F.linear(x, weight, bias) (then ReLU when relu) on e2ep_gemm, fp32 HIP tensors.
+    skip=True returns (y, x_skip): use x_skip for the residual connection around this layer
+    and its gradient joins dx inside the GEMM epilogue."""
+    _dev(x, weight, bias)
+    if x.dtype != torch.float32 or weight.dtype != torch.float32 or weight.stride(-1) != 1:
+        raise _lib.E2EPError("linear: fp32 input and a weight with unit inner stride required")
+    return _Linear.apply(x, weight, bias, bool(skip), bool(relu))
 
 
 # ------------------------------------------------------------------------------------------

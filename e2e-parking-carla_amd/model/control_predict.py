@@ -6,7 +6,7 @@ output).  `forward` is the teacher-forced training path, `predict` one autoregre
 import torch
 from torch import nn
 
-from e2ep_amd import transformer
+from e2ep_amd import nn_ops, transformer
 
 
 class ControlPredict(nn.Module):
@@ -46,7 +46,11 @@ class ControlPredict(nn.Module):
         tgt = tgt[:, :-1]
         mask, pad = self.create_mask(tgt)
         emb = self.pos_drop(self.embedding(tgt) + self.pos_embed)
-        return self.output(self.decoder(encoder_out, emb, mask, pad))
+        return self.project(self.decoder(encoder_out, emb, mask, pad))
+
+    def project(self, x):
+        """self.output (vocabulary projection) on e2ep_gemm."""
+        return nn_ops.linear(x, self.output.weight, self.output.bias)
 
     def predict(self, encoder_out, tgt):
         length = tgt.size(1)
@@ -55,5 +59,5 @@ class ControlPredict(nn.Module):
         tgt = torch.cat([tgt, pad], dim=1)
         mask, padm = self.create_mask(tgt)
         emb = self.embedding(tgt) + self.pos_embed
-        logits = self.output(self.decoder(encoder_out, emb, mask, padm))[:, length - 1, :]
+        logits = self.project(self.decoder(encoder_out, emb, mask, padm))[:, length - 1, :]
         return torch.softmax(logits, dim=-1).argmax(dim=-1).view(-1, 1)

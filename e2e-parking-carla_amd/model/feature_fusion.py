@@ -7,7 +7,7 @@ their arithmetic runs through e2ep_amd.transformer."""
 import torch
 from torch import nn
 
-from e2ep_amd import transformer
+from e2ep_amd import nn_ops, transformer
 
 
 class FeatureFusion(nn.Module):
@@ -31,8 +31,16 @@ class FeatureFusion(nn.Module):
                 nn.init.xavier_uniform_(p)
         nn.init.trunc_normal_(self.pos_embed, std=.02)
 
+    def encode_motion(self, ego_motion):
+        """motion_encoder (Linear -> ReLU) x 3 with the ReLU in each GEMM's epilogue."""
+        x = ego_motion
+        for i in (0, 2, 4):
+            lin = self.motion_encoder[i]
+            x = nn_ops.linear(x, lin.weight, lin.bias, relu=True)
+        return x
+
     def forward(self, bev_feature, ego_motion):
-        motion = self.motion_encoder(ego_motion).transpose(1, 2).expand(-1, -1, 2)
+        motion = self.encode_motion(ego_motion).transpose(1, 2).expand(-1, -1, 2)
         tokens = torch.cat([bev_feature.transpose(1, 2), motion], dim=2)
         tokens = self.pos_drop(tokens + self.pos_embed)
         return transformer.encoder(self.tf_encoder, tokens)

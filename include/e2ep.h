@@ -428,6 +428,23 @@ int e2ep_depth_bce_bwd(const float *prob, const int *cls, const float *den, cons
                        int BN, int D, int hw, float *dprob, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Strided fp32 GEMM for the transformer linears (nn.Linear forward and its two backward
+ * GEMMs: model/feature_fusion.py:13-14,24-29,48-50, model/control_predict.py:18-24):
+ *   C[m][n] = sum_k A(m,k) B(k,n) (+ bias[n]) (+ Cadd[m][n]), then ReLU when relu != 0;
+ *   A(m,k) = a_kcontig ? A[m*lda + k] : A[k*lda + m];  B(k,n) = b_kcontig ? B[n*ldb + k]
+ *   : B[k*ldb + n];  C row-major with leading dimension ldc.
+ * v_mfma_f32_32x32x2_f32, fixed summation order (deterministic).  Small grids split K and
+ * need e2ep_gemm_workspace(M, N, K) bytes of workspace (0 when no split).
+ * ------------------------------------------------------------------------------------- */
+size_t e2ep_gemm_workspace(int M, int N, int K);
+/* Benchmarking override of the launch plan: block tile (64 tm) x (64 tn), tm, tn in {1, 2},
+ * and the K split (tm = tn = 0: the automatic plan). */
+int e2ep_gemm_force(int tm, int tn, int splits);
+int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
+              const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
+              int K, int relu, void *workspace, void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Frame decode (dataset/carla_dataset.py:114-131, :494-515, :404-406): the per-step
  * arithmetic of the reference data path on cached uint8 crops.
  *  - e2ep_decode_frames: rgb / depth_rgb [*][hw][3] uint8 (either may be NULL); output

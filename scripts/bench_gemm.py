@@ -1,0 +1,97 @@
+"""e2ep_gemm vs torch (hipBLASLt) on the transformer GEMMs of one C2 step (B = 8).
+
+Each row: (M, N, K, layout, count per step); both sides timed with HIP events over 50
+back-to-back launches on the current stream.  Prints a table and the per-step totals
+(count x time), and writes JSON to --out.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "e2e-parking-carla_amd"))
+
+import torch  # noqa: E402
+
+# (name, M, N, K, a_kcontig, b_kcontig, launches per step); B = 8: 2048 encoder rows, 112
+# decoder rows; 4 layers each
+ROWS = [
+    ("enc in_proj fwd", 2048, 774, 258, 1, 1, 4), ("enc in_proj dgrad", 2048, 258, 774, 1, 0, 4),
+    ("enc in_proj wgrad", 774, 258, 2048, 0, 0, 4),
+    ("enc out fwd", 2048, 258, 258, 1, 1, 4), ("enc out dgrad", 2048, 258, 258, 1, 0, 4),
+    ("enc out wgrad", 258, 258, 2048, 0, 0, 4),
+    ("enc ffn1 fwd", 2048, 2048, 258, 1, 1, 4), ("enc ffn1 dgrad", 2048, 258, 2048, 1, 0, 4),
+    ("enc ffn1 wgrad", 2048, 258, 2048, 0, 0, 4),
+    ("enc ffn2 fwd", 2048, 258, 2048, 1, 1, 4), ("enc ffn2 dgrad", 2048, 2048, 258, 1, 0, 4),
+    ("enc ffn2 wgrad", 258, 2048, 2048, 0, 0, 4),
+    ("dec self in_proj fwd", 112, 774, 258, 1, 1, 4), ("dec cross kv fwd", 2048, 516, 258, 1, 1, 4),
+    ("dec cross kv dgrad", 2048, 258, 516, 1, 0, 4), ("dec cross kv wgrad", 516, 258, 2048, 0, 0, 4),
+    ("dec ffn1 fwd", 112, 2048, 258, 1, 1, 4), ("dec ffn2 fwd", 112, 258, 2048, 1, 1, 4),
+    ("dec ffn1 wgrad", 2048, 258, 112, 0, 0, 4), ("dec ffn2 wgrad", 258, 2048, 112, 0, 0, 4),
+    ("output fwd", 112, 204, 258, 1, 1, 1),
+]
+
+
+def torch_fn(A, ak, B, bk):
+    Am = A if ak else A.t()
+    Bm = B.t() if bk else B
+    return lambda: torch.mm(Am, Bm)
+
+
+def timed(fn, iters=50):
+    for _ in range(5):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--sweep", action="store_true", help="time every (tile, split) plan per shape")
+    args = ap.parse_args()
+    from e2ep_amd import nn_ops
+    rows = []
+    tot_e = tot_t = 0.0
+    print(f"{'gemm':24s} {'M':>5s} {'N':>5s} {'K':>5s}  {'e2ep us':>8s} {'TF/s':>6s}  {'torch us':>8s} {'TF/s':>6s}")
+    for name, M, N, K, ak, bk, cnt in ROWS:
+        A = torch.randn((M, K) if ak else (K, M), device="cuda")
+        B = torch.randn((N, K) if bk else (K, N), device="cuda")
+        out = torch.empty(M, N, device="cuda")
+        te = timed(lambda: nn_ops.gemm(A, ak, B, bk, M, N, K, out=out))
+        tt = timed(torch_fn(A, ak, B, bk))
+        fl = 2.0 * M * N * K
+        rows.append({"name": name, "M": M, "N": N, "K": K, "count": cnt, "e2ep_us": round(te, 2),
+                     "torch_us": round(tt, 2), "e2ep_tflops": round(fl / te / 1e6, 1),
+                     "torch_tflops": round(fl / tt / 1e6, 1)})
+        tot_e += cnt * te
+        tot_t += cnt * tt
+        if args.sweep:
+            from e2ep_amd import _lib
+            best = []
+            for tm, tn in ((1, 1), (1, 2), (2, 1), (2, 2)):
+                for sp in (1, 2, 3, 4, 6, 8):
+                    _lib.call("e2ep_gemm_force", tm, tn, sp)
+                    t = timed(lambda: nn_ops.gemm(A, ak, B, bk, M, N, K, out=out), 20)
+                    best.append((t, tm, tn, sp))
+            _lib.call("e2ep_gemm_force", 0, 0, 0)
+            best.sort()
+            rows[-1]["sweep"] = [[round(t, 1), tm, tn, sp] for t, tm, tn, sp in best[:6]]
+            print("    best:", " ".join(f"{64*tm}x{64*tn}/s{sp}:{t:.1f}" for t, tm, tn, sp in best[:6]), flush=True)
+        print(f"{name:24s} {M:5d} {N:5d} {K:5d}  {te:8.1f} {fl / te / 1e6:6.1f}  {tt:8.1f} {fl / tt / 1e6:6.1f}",
+              flush=True)
+    res = {"rows": rows, "per_step_ms": {"e2ep": round(tot_e / 1e3, 3), "torch": round(tot_t / 1e3, 3)}}
+    print(json.dumps(res["per_step_ms"]))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,106 @@
+"""e2ep_gemm (csrc/gemm.hip) and the nn.Linear built on it (e2ep_amd.nn_ops.linear) vs fp64
+PyTorch: every operand layout the linear uses (forward (A k-contig, B k-contig), input
+gradient (A k-contig, B n-contig), weight gradient (A m-contig, B n-contig)) plus the fourth,
+at the transformer shapes of the C2 step (2048 encoder rows, 112 decoder rows, d = 258, FFN
+2048) and ragged edges (M, N, K not multiples of the tiles; K = 1..3).
+Tolerance: rel-L2 <= 2e-6 against fp64 (fp32 MFMA products are exact, accumulation is
+fp32 over at most 2048 terms); split-K results bitwise identical across launches."""
+import pytest
+import torch
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+SHAPES = [(2048, 774, 258), (2048, 258, 2048), (258, 2048, 2048), (774, 258, 2048),
+          (112, 516, 258), (112, 204, 258), (8, 64, 3), (8, 256, 128), (1, 1, 1), (65, 130, 17),
+          (3, 5, 700), (200, 3, 64)]
+
+
+def _operands(M, N, K, ak, bk, g):
+    A = torch.randn(M, K, generator=g) if ak else torch.randn(K, M, generator=g)
+    B = torch.randn(N, K, generator=g) if bk else torch.randn(K, N, generator=g)
+    Am = A if ak else A.t()
+    Bm = B.t() if bk else B
+    return A, B, Am.double() @ Bm.double()
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
+def test_gemm_layouts_vs_fp64(M, N, K, ak, bk):
+    from e2ep_amd import nn_ops
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K + 11 * ak + 5 * bk)
+    A, B, ref = _operands(M, N, K, ak, bk, g)
+    out = nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K)
+    assert rel_l2(out, ref) < 2e-6
+    again = nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K)
+    assert torch.equal(out, again)
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 258, 258), (112, 204, 258), (37, 70, 2048)])
+def test_gemm_epilogue_bias_add_relu(M, N, K):
+    from e2ep_amd import nn_ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A, B, ref = _operands(M, N, K, True, True, g)
+    bias, cadd = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    out = nn_ops.gemm(A.to(DEV), True, B.to(DEV), True, M, N, K, bias=bias.to(DEV),
+                      cadd=cadd.to(DEV), relu=True)
+    want = (ref + bias.double() + cadd.double()).clamp_min(0)
+    assert rel_l2(out, want) < 2e-6
+    assert float(out.min()) >= 0.0
+
+
+def test_gemm_strided_operands():
+    """Row slices of a bigger matrix (in_proj_weight[E:] for the cross-attention K/V)."""
+    from e2ep_amd import nn_ops
+    g = torch.Generator().manual_seed(3)
+    W = torch.randn(774, 258, generator=g).to(DEV)
+    x = torch.randn(2048, 300, generator=g).to(DEV)[:, :258]     # lda = 300
+    out = nn_ops.gemm(x, True, W[258:], True, 2048, 516, 258)
+    ref = x.double() @ W[258:].double().t()
+    assert rel_l2(out, ref) < 2e-6
+
+
+@pytest.mark.parametrize("shape,relu,skip", [((8, 256, 258), False, True), ((8, 14, 258), False, False),
+                                             ((8, 1, 3), True, False)])
+def test_linear_autograd_vs_fp64(shape, relu, skip):
+    from e2ep_amd import nn_ops
+    g = torch.Generator().manual_seed(len(shape) + shape[-1])
+    K = shape[-1]
+    N = 204 if K == 258 and not skip else 64 if K == 3 else 774
+    x = torch.randn(*shape, generator=g)
+    W = torch.randn(N, K, generator=g) * 0.1
+    b = torch.randn(N, generator=g)
+    gy = torch.randn(*shape[:-1], N, generator=g)
+    gs = torch.randn(*shape, generator=g)
+    xr, Wr, br = (t.double().requires_grad_() for t in (x, W, b))
+    yr = torch.nn.functional.linear(xr, Wr, br)
+    if relu:
+        yr = yr.clamp_min(0)
+    loss_r = (yr * gy.double()).sum() + ((xr * gs.double()).sum() if skip else 0)
+    loss_r.backward()
+    xd, Wd, bd = (t.to(DEV).requires_grad_() for t in (x, W, b))
+    out = nn_ops.linear(xd, Wd, bd, skip=skip, relu=relu)
+    if skip:
+        y, xs = out
+        loss = (y * gy.to(DEV)).sum() + (xs * gs.to(DEV)).sum()
+    else:
+        y = out
+        loss = (y * gy.to(DEV)).sum()
+    loss.backward()
+    assert rel_l2(y, yr) < 2e-6
+    assert rel_l2(xd.grad, xr.grad) < 2e-6
+    assert rel_l2(Wd.grad, Wr.grad) < 2e-6
+    assert rel_l2(bd.grad, br.grad) < 2e-6
+
+
+def test_gemm_rejects_bad_shapes():
+    from e2ep_amd import _lib, nn_ops
+    A = torch.randn(4, 5, device=DEV)
+    with pytest.raises(_lib.E2EPError):
+        nn_ops.gemm(A, True, torch.randn(3, 6, device=DEV), True, 4, 3, 5)
+    with pytest.raises(_lib.E2EPError):
+        nn_ops.gemm(A.t(), True, torch.randn(3, 5, device=DEV), True, 5, 3, 4)
+    with pytest.raises(_lib.E2EPError):
+        nn_ops.linear(torch.randn(2, 5), torch.randn(3, 5), None)
