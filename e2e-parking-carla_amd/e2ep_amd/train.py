@@ -18,7 +18,7 @@ without its module wrapper), one flat fp32 gradient buffer in FlatAdam's layout;
     between the replays -> g_opt.  The collective is not captured: on this stack (torch
     2.10 / RCCL 2.26) a captured ProcessGroupNCCL collective makes the c10d watchdog fault
     on its capture-time event, and a backward graph with bucket gathers forked onto a side
-    stream replayed wrong camera-encoder gradients (scripts/diag_ddp*.py).
+    stream replayed wrong camera-encoder gradients (profiles/r02/ddp_diag/).
   * eager mode: DDP-style overlap — the buffer is cut into ~25 MB buckets in reverse layout
     order; a post-accumulate-grad hook per parameter counts arrivals and, when a bucket is
     complete (and every earlier one issued: the same order on every rank), a side stream

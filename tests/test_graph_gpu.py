@@ -2,7 +2,7 @@
 
 Without the repair, a hipMemsetAsync captured into a graph leaves garbage from the second
 replay on, and PyTorch's captured reductions (bias gradients of broadcast adds) go wrong
-(scripts/diag_memset3.py, scripts/diag_mha_graph3.py)."""
+(one-off diagnostics, git history at cb07871^)."""
 import ctypes
 
 import pytest
