@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "gemm.h"
 
 namespace e2ep {
 
@@ -44,18 +45,21 @@ __device__ __forceinline__ float kmask(float v, bool ok) {
 constexpr int G_BK = 32;
 constexpr int G_LDW = 36;  // LDS row stride in floats (32 k + 4 pad)
 
-template <bool AK, bool BKC, int TM, int TN>
+template <bool AK, bool BKC, int WM, int TM, int TN>
 __global__ void __launch_bounds__(256)
     k_gemm(const float *__restrict__ A, int lda, long long a_bytes, int avec,
            const float *__restrict__ B, int ldb, long long b_bytes, int bvec,
-           const float *__restrict__ bias, const float *__restrict__ Cadd, int ldadd,
-           float *__restrict__ C, int ldc, int M, int N, int K, int kper, int relu) {
-  constexpr int BM = 64 * TM, BN = 64 * TN;
+           const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
+           int ldadd, float *__restrict__ C, long long c_bytes, int ldc, GemmCols cols, int M,
+           int N, int K, int kper, int relu) {
+  constexpr int WN = 4 / WM;                      // waves along N
+  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+  constexpr int GA = BM / 32, GB = BN / 32;       // 32-row load groups per operand tile
   __shared__ __attribute__((aligned(16))) float As[2][BM][G_LDW];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN][G_LDW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % WM, wn = wave / WM;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int split = blockIdx.z;
   const int ksteps = (K + G_BK - 1) / G_BK;
@@ -64,71 +68,90 @@ __global__ void __launch_bounds__(256)
   const int nk = max(0, kend - kbeg);
   const __amdgpu_buffer_rsrc_t ra_ = rsrc(A, a_bytes), rb_ = rsrc(B, b_bytes);
 
-  // Each operand tile is TM (TN) groups of 64 rows x 32 k; per group a thread loads 8 k of
-  // one row: k-contiguous operands -> (row tid/4, k octet tid%4), float4s when aligned;
-  // m/n-contiguous operands -> (row tid%64, k octet tid/64), lanes coalesced along the row.
-  const int ar = AK ? tid >> 2 : tid & 63, aq = AK ? tid & 3 : tid >> 6;
-  const int br = BKC ? tid >> 2 : tid & 63, bq = BKC ? tid & 3 : tid >> 6;
+  // An operand tile is groups of 32 rows x 32 k; per group a thread loads 4 values:
+  // k-contiguous -> (row tid/8, k quad tid%8), one float4 / two float2 when aligned;
+  // row-contiguous -> (row tid%32, k quad tid/32), lanes coalesced along the row.
+  const int ar = AK ? tid >> 3 : tid & 31, aq = AK ? tid & 7 : tid >> 5;
+  const int br = BKC ? tid >> 3 : tid & 31, bq = BKC ? tid & 7 : tid >> 5;
 
-  float ra[TM][8], rb[TN][8];
+  // column-batched B: this thread's load column is fixed, so its image offset is too
+  long long bcol_off[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int n = min(n0 + 32 * i + br, N - 1);
+    bcol_off[i] = cols.hw ? (long long)(n / cols.hw) * cols.b_img + n % cols.hw : n;
+  }
+
+  // One step of register lookahead: the next K-step's loads are issued before this step's
+  // MFMAs and written to the other LDS buffer after them.  (Deeper register pipelines, 2 and
+  // 3 steps, measured 4-5 % slower: the extra registers cost a wave per SIMD.)
+  float ra[GA][4], rb[GB][4];
   // Loads are unconditional: the row index is clamped into the matrix (rows past M / N only
   // feed outputs that are never stored) and k into [0, K); values at k >= K are zeroed with
   // an integer mask when the registers are written to LDS (after the step's MFMAs, so the
   // loads stay in flight).  Guarded loads (`ok ? offset : OOR`) let the compiler split the
   // loop into per-load exec-masked branches, which serialised the loads.
-  auto load_op = [&](auto &regs, const __amdgpu_buffer_rsrc_t &rs, bool kcontig, int vec, int ld,
-                     int row0, int rows, int r, int q, int k0, int i) {
-    const int row = min(row0 + 64 * i + r, rows - 1);
-    const int k = k0 + 8 * q;
-    if (kcontig) {
-      const long long base = (long long)row * ld;
-      if (vec == 2 && k0 + G_BK <= K) {  // uniform: a full, 16-byte aligned step -> 2 float4s
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float4 v = bload4(rs, (int)((base + k + 4 * h) * 4));
-          regs[i][4 * h] = v.x; regs[i][4 * h + 1] = v.y; regs[i][4 * h + 2] = v.z; regs[i][4 * h + 3] = v.w;
-        }
-      } else if (vec == 1 && k0 + G_BK <= K) {  // 8-byte aligned rows (even ld) -> 4 float2s
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const float2 v = bload2(rs, (int)((base + k + 2 * h) * 4));
-          regs[i][2 * h] = v.x; regs[i][2 * h + 1] = v.y;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          regs[i][j] = bload(rs, (int)((base + min(k + j, K - 1)) * 4));
-      }
+  auto load_k = [&](float *regs, const __amdgpu_buffer_rsrc_t &rs, int vec, long long base,
+                    int k, bool full) {  // 4 k-contiguous values at base + k
+    if (vec == 2 && full) {
+      const float4 v = bload4(rs, (int)((base + k) * 4));
+      regs[0] = v.x; regs[1] = v.y; regs[2] = v.z; regs[3] = v.w;
+    } else if (vec == 1 && full) {
+      const float2 v0 = bload2(rs, (int)((base + k) * 4)), v1 = bload2(rs, (int)((base + k + 2) * 4));
+      regs[0] = v0.x; regs[1] = v0.y; regs[2] = v1.x; regs[3] = v1.y;
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        regs[i][j] = bload(rs, (int)(((long long)min(k + j, K - 1) * ld + row) * 4));
+      for (int j = 0; j < 4; ++j) regs[j] = bload(rs, (int)((base + min(k + j, K - 1)) * 4));
     }
   };
-  auto load_tiles = [&](int ks_in) {
+  auto load_tiles = [&](float (&xa)[GA][4], float (&xb)[GB][4], int ks_in) {
     const int k0 = min(ks_in, kend - 1) * G_BK;  // past the range: re-read, never stored
+    const bool full = k0 + G_BK <= K;             // uniform
 #pragma unroll
-    for (int i = 0; i < TM; ++i) load_op(ra, ra_, AK, avec, lda, m0, M, ar, aq, k0, i);
+    for (int i = 0; i < GA; ++i) {
+      const int row = min(m0 + 32 * i + ar, M - 1);
+      const int k = k0 + 4 * aq;
+      if (AK) {
+        load_k(xa[i], ra_, avec, (long long)row * lda, k, full);
+      } else {
 #pragma unroll
-    for (int i = 0; i < TN; ++i) load_op(rb, rb_, BKC, bvec, ldb, n0, N, br, bq, k0, i);
+        for (int j = 0; j < 4; ++j)
+          xa[i][j] = bload(ra_, (int)(((long long)min(k + j, K - 1) * lda + row) * 4));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int k = k0 + 4 * bq;
+      if (BKC) {
+        const int row = min(n0 + 32 * i + br, N - 1);
+        load_k(xb[i], rb_, bvec, (long long)row * ldb, k, full);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          xb[i][j] = bload(rb_, (int)(((long long)min(k + j, K - 1) * ldb + bcol_off[i]) * 4));
+      }
+    }
   };
   // LDS writes: regs -> k-contiguous rows; the zero mask for k >= K applied here
-  auto store_op = [&](auto &regs, float (*T)[G_LDW], int r, int q, int k0, bool full, int i) {
-    if (!full)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) regs[i][j] = kmask(regs[i][j], k0 + 8 * q + j < K);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      *reinterpret_cast<float4 *>(&T[64 * i + r][8 * q + 4 * h]) =
-          make_float4(regs[i][4 * h], regs[i][4 * h + 1], regs[i][4 * h + 2], regs[i][4 * h + 3]);
-  };
-  auto store_tiles = [&](int buf, int ks) {
+  auto store_tiles = [&](float (&xa)[GA][4], float (&xb)[GB][4], int buf, int ks) {
     const int k0 = ks * G_BK;
     const bool full = k0 + G_BK <= K;  // uniform
 #pragma unroll
-    for (int i = 0; i < TM; ++i) store_op(ra, As[buf], ar, aq, k0, full, i);
+    for (int i = 0; i < GA; ++i) {
+      if (!full)
 #pragma unroll
-    for (int i = 0; i < TN; ++i) store_op(rb, Bs[buf], br, bq, k0, full, i);
+        for (int j = 0; j < 4; ++j) xa[i][j] = kmask(xa[i][j], k0 + 4 * aq + j < K);
+      *reinterpret_cast<float4 *>(&As[buf][32 * i + ar][4 * aq]) =
+          make_float4(xa[i][0], xa[i][1], xa[i][2], xa[i][3]);
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      if (!full)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xb[i][j] = kmask(xb[i][j], k0 + 4 * bq + j < K);
+      *reinterpret_cast<float4 *>(&Bs[buf][32 * i + br][4 * bq]) =
+          make_float4(xb[i][0], xb[i][1], xb[i][2], xb[i][3]);
+    }
   };
 
   // wave (wm, wn) owns rows 32 TM wm + 32 u and columns 32 TN wn + 32 t
@@ -168,32 +191,35 @@ __global__ void __launch_bounds__(256)
           acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][kk], b[t][kk], acc[u][t], 0, 0, 0);
   };
   if (nk > 0) {
-    load_tiles(kbeg);
-    store_tiles(0, kbeg);
+    load_tiles(ra, rb, kbeg);
+    store_tiles(ra, rb, 0, kbeg);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-      load_tiles(kbeg + kt + 1);  // past the range: re-read, never stored
+      load_tiles(ra, rb, kbeg + kt + 1);  // past the range: re-read, never stored
       compute(kt & 1);
-      if (kt + 1 < nk) store_tiles((kt + 1) & 1, kbeg + kt + 1);
+      if (kt + 1 < nk) store_tiles(ra, rb, (kt + 1) & 1, kbeg + kt + 1);
       __syncthreads();
     }
   }
 
   // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-  // gridDim.z > 1: raw partial sums into C = workspace[split][M][N] (row stride N).
+  // gridDim.z > 1: raw partial sums into C = workspace[split][M][N] (dense, unbatched).
   const bool final_ = gridDim.z == 1;
   float *dst = final_ ? C : C + (long long)split * M * N;
   const int ldd = final_ ? ldc : N;
+  const bool batched = final_ && cols.hw > 0;
   // edges: buffer stores with out-of-range offsets are dropped; the epilogue's optional
   // inputs are behind uniform branches, and the 16 Cadd values of a tile are loaded together
-  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, 4LL * ((long long)(M - 1) * ldd + N));
-  const __amdgpu_buffer_rsrc_t rc = rsrc(Cadd, Cadd ? 4LL * ((long long)(M - 1) * ldadd + N) : 0);
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, final_ ? c_bytes : 4LL * M * N);
+  const __amdgpu_buffer_rsrc_t rc =
+      rsrc(Cadd, Cadd ? (batched ? c_bytes : 4LL * ((long long)(M - 1) * ldadd + N)) : 0);
   const bool add_c = final_ && Cadd != nullptr, add_b = final_ && bias != nullptr;
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
     const int n = n0 + 32 * TN * wn + 32 * t + li;
     const bool nok = n < N;
-    const float bn_ = add_b ? bias[min(n, N - 1)] : 0.f;
+    const long long cbase = batched ? (long long)(n / cols.hw) * cols.c_img + n % cols.hw : n;
+    const float bn_ = (add_b && !bias_rows) ? bias[min(n, N - 1)] : 0.f;
 #pragma unroll
     for (int u = 0; u < TM; ++u) {
       float cv[16];
@@ -201,29 +227,31 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + 32 * TM * wm + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          cv[r] = bload(rc, (nok && m < M) ? (int)(((long long)m * ldadd + n) * 4) : OOR);
+          const long long off = batched ? cbase + (long long)m * ldd : (long long)m * ldadd + n;
+          cv[r] = bload(rc, (nok && m < M) ? (int)(off * 4) : OOR);
         }
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + 32 * TM * wm + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * lh;
         float v = acc[u][t][r];
-        if (add_b) v += bn_;
+        if (add_b) v += bias_rows ? bias[min(m, M - 1)] : bn_;
         if (add_c) v += cv[r];
         if (final_ && relu) v = fmaxf(v, 0.f);
-        bstore(rd, (nok && m < M) ? (int)(((long long)m * ldd + n) * 4) : OOR, v);
+        bstore(rd, (nok && m < M) ? (int)((cbase + (long long)m * ldd) * 4) : OOR, v);
       }
     }
   }
 }
 
 // C[m][n] = sum over splits in order (+ bias) (+ Cadd) (ReLU).  V = 4: four consecutive
-// elements per thread with 16-byte loads / stores (dense C and Cadd, M * N % 4 == 0).
+// elements per thread with 16-byte loads / stores (plain dense C, column bias, M*N % 4 == 0);
+// V = 1 handles column-batched C (Cadd in C's layout) and row bias.
 template <int V>
 __global__ void __launch_bounds__(256)
     k_gemm_reduce(const float *__restrict__ part, int splits, int M, int N,
-                  const float *__restrict__ bias, const float *__restrict__ Cadd, int ldadd,
-                  float *__restrict__ C, int ldc, int relu) {
+                  const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
+                  int ldadd, float *__restrict__ C, int ldc, GemmCols cols, int relu) {
   const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * V;
   const long long MN = (long long)M * N;
   if (i >= MN) return;
@@ -243,38 +271,103 @@ __global__ void __launch_bounds__(256)
   for (int v = 0; v < V; ++v) {
     const long long e = i + v;
     const int m = (int)(e / N), n = (int)(e - (long long)m * N);
-    if (bias) s[v] += bias[n];
-    if (Cadd) s[v] += Cadd[(long long)m * ldadd + n];
+    const long long off = cols.hw ? (long long)(n / cols.hw) * cols.c_img + n % cols.hw +
+                                        (long long)m * ldc
+                                  : (long long)m * ldc + n;
+    if (bias) s[v] += bias[bias_rows ? m : n];
+    if (Cadd) s[v] += Cadd[cols.hw ? off : (long long)m * ldadd + n];
     if (relu) s[v] = fmaxf(s[v], 0.f);
-    if (V == 1) C[(long long)m * ldc + n] = s[v];
+    if (V == 1) C[off] = s[v];
   }
   if (V == 4) *reinterpret_cast<float4 *>(C + i) = make_float4(s[0], s[1], s[2], s[3]);
 }
 
 struct GemmLaunch {
-  int tm, tn, splits, kper;
+  int wm, tm, tn, splits, kper;
 };
 
-// 64 x 64 tiles (the sweep over 64/128-wide tiles, scripts/bench_gemm.py --sweep: they are
-// the fastest or within 6 % on every transformer shape — more waves per CU hide more load
-// latency); K split toward ~768 workgroups (3 per CU), at most 8 ways and >= 8 K-steps each.
+// Tiles (scripts/bench_gemm.py --sweep / --conv): 64 x 64 (2 x 2 waves), or 32 x 128 (1 x 4
+// waves) when M is not a multiple of 64 and 32-row tiles pad it less (M = 32, 112, 144, 160,
+// 336 ...); K split toward ~768 workgroups (3 per CU), at most 8 ways and >= 8 K-steps each.
 static int g_force_tm = 0, g_force_tn = 0, g_force_splits = 0;  // 0: automatic
 
 static GemmLaunch gemm_plan(int M, int N, int K) {
-  GemmLaunch p{1, 1, 1, 1};
+  GemmLaunch p{2, 1, 1, 1, 1};
   const int ksteps = cdiv(K, G_BK);
-  if (g_force_tm > 0) {  // benchmarking override (e2ep_gemm_force)
-    p.tm = g_force_tm;
-    p.tn = g_force_tn;
+  if (g_force_tm > 0) {  // benchmarking override (e2ep_gemm_force): tm = 1 -> 64 x 64,
+    p.wm = g_force_tm == 1 ? 2 : 1;  // tm = 2 -> 32 x 128
     p.splits = std::max(1, std::min(g_force_splits, ksteps));
   } else {
-    const long long blocks = (long long)cdiv(M, 64) * cdiv(N, 64);
+    if (cdiv(M, 32) * 32 < cdiv(M, 64) * 64) p.wm = 1;
+    const int bm = 32 * p.wm, bn = 32 * (4 / p.wm);
+    const long long blocks = (long long)cdiv(M, bm) * cdiv(N, bn);
     const int cap = std::min(8, std::max(1, ksteps / 8));
     p.splits = (int)std::min<long long>(cap, std::max(1LL, (long long)cdiv(768, blocks)));
   }
   p.kper = cdiv(ksteps, p.splits);
   p.splits = cdiv(ksteps, p.kper);
   return p;
+}
+
+size_t gemm_ws(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const GemmLaunch p = gemm_plan(M, N, K);
+  return p.splits > 1 ? (size_t)p.splits * M * N * sizeof(float) : 0;
+}
+
+// vector loads along k for k-contiguous operands: 2 = float4 (rows 16-byte aligned), 1 =
+// float2 (8-byte aligned: the d = 258 rows).  Row-contiguous operands stay on dword loads
+// (lanes consecutive along the row): a float2 row-pair variant measured 1.2 - 1.5x slower on
+// the weight-gradient shapes.
+static int vec_of(bool kc, int ld, const void *ptr) {
+  if (!kc) return 0;
+  if (ld % 4 == 0 && ((uintptr_t)ptr & 15) == 0) return 2;
+  return ld % 2 == 0 && ((uintptr_t)ptr & 7) == 0 ? 1 : 0;
+}
+
+int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B, int ldb,
+             bool bk, long long b_bytes, const float *bias, bool bias_rows, const float *Cadd,
+             int ldadd, float *C, long long c_bytes, int ldc, GemmCols cols, int M, int N, int K,
+             int relu, void *workspace, hipStream_t s) {
+  const GemmLaunch p = gemm_plan(M, N, K);
+  if (p.splits > 1 && !workspace) {
+    set_error("gemm: workspace of e2ep_gemm_workspace() bytes required");
+    return E2EP_EINVAL;
+  }
+  float *out = p.splits > 1 ? static_cast<float *>(workspace) : C;
+  const int bm = 32 * p.wm, bn = 32 * (4 / p.wm);
+  dim3 grid(cdiv(N, bn), cdiv(M, bm), p.splits);
+  const int avec = vec_of(ak, lda, A), bvec = vec_of(bk, ldb, B);
+  const int br = bias_rows ? 1 : 0;
+#define E2EP_GEMM_LAUNCH(AKV, BKV, WMV)                                                          \
+  hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, 1, 1>), grid, dim3(256), 0, s, A, lda, a_bytes, avec, \
+                     B, ldb, b_bytes, bvec, bias, br, Cadd, ldadd, out, c_bytes, ldc, cols, M, N, \
+                     K, p.kper, relu)
+#define E2EP_GEMM_T(AKV, BKV)                    \
+  do {                                           \
+    if (p.wm == 1) E2EP_GEMM_LAUNCH(AKV, BKV, 1); \
+    else E2EP_GEMM_LAUNCH(AKV, BKV, 2);           \
+  } while (0)
+  if (ak && bk) E2EP_GEMM_T(true, true);
+  else if (ak) E2EP_GEMM_T(true, false);
+  else if (bk) E2EP_GEMM_T(false, true);
+  else E2EP_GEMM_T(false, false);
+#undef E2EP_GEMM_T
+#undef E2EP_GEMM_LAUNCH
+  if (p.splits > 1) {
+    const long long MN = (long long)M * N;
+    const bool v4 = MN % 4 == 0 && ldc == N && cols.hw == 0 && !bias_rows &&
+                    (!Cadd || ldadd == N) && ((uintptr_t)C & 15) == 0;
+    if (v4)
+      hipLaunchKernelGGL(k_gemm_reduce<4>, dim3(cdiv(MN / 4, 256)), dim3(256), 0, s,
+                         static_cast<const float *>(workspace), p.splits, M, N, bias, br, Cadd,
+                         ldadd, C, ldc, cols, relu);
+    else
+      hipLaunchKernelGGL(k_gemm_reduce<1>, dim3(cdiv(MN, 256)), dim3(256), 0, s,
+                         static_cast<const float *>(workspace), p.splits, M, N, bias, br, Cadd,
+                         ldadd, C, ldc, cols, relu);
+  }
+  return 0;
 }
 
 }  // namespace e2ep
@@ -285,18 +378,14 @@ extern "C" {
 
 int e2ep_gemm_force(int tm, int tn, int splits) {
   E2EP_REQUIRE(tm >= 0 && tm <= 2 && tn >= 0 && tn <= 2 && splits >= 0 && (tm == 0) == (tn == 0),
-               E2EP_EINVAL, "e2ep_gemm_force: tm, tn in {1, 2} (0 = automatic)");
+               E2EP_EINVAL, "e2ep_gemm_force: tm in {1 (64 x 64), 2 (32 x 128)} (0 = automatic)");
   g_force_tm = tm;
   g_force_tn = tn;
   g_force_splits = splits;
   return 0;
 }
 
-size_t e2ep_gemm_workspace(int M, int N, int K) {
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
-  const GemmLaunch p = gemm_plan(M, N, K);
-  return p.splits > 1 ? (size_t)p.splits * M * N * sizeof(float) : 0;
-}
+size_t e2ep_gemm_workspace(int M, int N, int K) { return gemm_ws(M, N, K); }
 
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
@@ -308,53 +397,14 @@ int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, i
                E2EP_EINVAL, "e2ep_gemm: leading dimension too small");
   const long long a_bytes = 4LL * (a_kcontig ? (long long)(M - 1) * lda + K : (long long)(K - 1) * lda + M);
   const long long b_bytes = 4LL * (b_kcontig ? (long long)(N - 1) * ldb + K : (long long)(K - 1) * ldb + N);
-  E2EP_REQUIRE(a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL &&
-                   4LL * ((long long)(M - 1) * std::max(ldc, ldadd) + N) < 0x7fffffffLL,
+  const long long c_bytes = 4LL * ((long long)(M - 1) * ldc + N);
+  E2EP_REQUIRE(a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL && c_bytes < 0x7fffffffLL &&
+                   (!Cadd || 4LL * ((long long)(M - 1) * ldadd + N) < 0x7fffffffLL),
                E2EP_ERANGE, "e2ep_gemm: operand larger than 2 GB");
-  const GemmLaunch p = gemm_plan(M, N, K);
-  E2EP_REQUIRE(p.splits == 1 || workspace, E2EP_EINVAL,
-               "e2ep_gemm: workspace of e2ep_gemm_workspace() bytes required");
-  hipStream_t s = as_stream(stream);
-  float *out = p.splits > 1 ? static_cast<float *>(workspace) : C;
-  dim3 grid(cdiv(N, 64 * p.tn), cdiv(M, 64 * p.tm), p.splits);
-  // vector loads along k for k-contiguous operands: 2 = float4 (rows 16-byte aligned), 1 =
-  // float2 (8-byte aligned: the d = 258 rows).  Row-contiguous operands stay on dword loads
-  // (lanes consecutive along the row, 256 B per instruction): a float2 row-pair variant
-  // measured 1.2 - 1.5x slower on the weight-gradient shapes (scripts/bench_gemm.py --sweep).
-  auto vec_of = [](int kc, int ld, const void *ptr) {
-    if (!kc) return 0;
-    if (ld % 4 == 0 && ((uintptr_t)ptr & 15) == 0) return 2;
-    return ld % 2 == 0 && ((uintptr_t)ptr & 7) == 0 ? 1 : 0;
-  };
-  const int avec = vec_of(a_kcontig, lda, A), bvec = vec_of(b_kcontig, ldb, B);
-#define E2EP_GEMM_LAUNCH(AKV, BKV, TMV, TNV)                                                    \
-  hipLaunchKernelGGL((k_gemm<AKV, BKV, TMV, TNV>), grid, dim3(256), 0, s, A, lda, a_bytes, avec, \
-                     B, ldb, b_bytes, bvec, bias, Cadd, ldadd, out, ldc, M, N, K, p.kper, relu)
-#define E2EP_GEMM_T(AKV, BKV)                                            \
-  do {                                                                   \
-    if (p.tm == 2 && p.tn == 2) E2EP_GEMM_LAUNCH(AKV, BKV, 2, 2);        \
-    else if (p.tm == 2) E2EP_GEMM_LAUNCH(AKV, BKV, 2, 1);                \
-    else if (p.tn == 2) E2EP_GEMM_LAUNCH(AKV, BKV, 1, 2);                \
-    else E2EP_GEMM_LAUNCH(AKV, BKV, 1, 1);                               \
-  } while (0)
-  if (a_kcontig && b_kcontig) E2EP_GEMM_T(true, true);
-  else if (a_kcontig) E2EP_GEMM_T(true, false);
-  else if (b_kcontig) E2EP_GEMM_T(false, true);
-  else E2EP_GEMM_T(false, false);
-#undef E2EP_GEMM_T
-#undef E2EP_GEMM_LAUNCH
-  if (p.splits > 1) {
-    const long long MN = (long long)M * N;
-    const bool v4 = MN % 4 == 0 && ldc == N && ((uintptr_t)C & 15) == 0;
-    if (v4)
-      hipLaunchKernelGGL(k_gemm_reduce<4>, dim3(cdiv(MN / 4, 256)), dim3(256), 0, s,
-                         static_cast<const float *>(workspace), p.splits, M, N, bias, Cadd, ldadd,
-                         C, ldc, relu);
-    else
-      hipLaunchKernelGGL(k_gemm_reduce<1>, dim3(cdiv(MN, 256)), dim3(256), 0, s,
-                         static_cast<const float *>(workspace), p.splits, M, N, bias, Cadd, ldadd,
-                         C, ldc, relu);
-  }
+  const int rc = gemm_run(A, lda, a_kcontig, a_bytes, B, ldb, b_kcontig, b_bytes, bias, false,
+                          Cadd, ldadd, C, c_bytes, ldc, GemmCols{0, 0, 0}, M, N, K, relu,
+                          workspace, as_stream(stream));
+  if (rc) return rc;
   return launch_status("e2ep_gemm");
 }
 

@@ -32,6 +32,19 @@ ROWS = [
     ("output fwd", 112, 204, 258, 1, 1, 1),
 ]
 
+# 1x1 convs of the C2 step as single-image GEMMs (N*H*W columns), --conv: (name, M, N, K,
+# a_kcontig, b_kcontig, current conv kernel us from profiles/r02 conv breakdown)
+CONV_ROWS = [
+    ("960>160 fwd", 160, 8192, 960, 1, 0, 52.4), ("960>160 dgrad", 960, 8192, 160, 0, 0, 38.2),
+    ("960>160 wgrad", 160, 960, 8192, 1, 1, 53.6),
+    ("160>960 fwd", 960, 8192, 160, 1, 0, 42.1), ("160>960 dgrad", 160, 8192, 960, 0, 0, 51.9),
+    ("160>960 wgrad", 960, 160, 8192, 1, 1, 53.3),
+    ("672>112 fwd", 112, 8192, 672, 1, 0, 36.5), ("112>672 dgrad", 112, 8192, 672, 0, 0, 30.7),
+    ("32>192 fwd", 192, 131072, 32, 1, 0, 36.7), ("192>32 wgrad", 32, 192, 131072, 1, 1, 52.2),
+    ("24>144 fwd", 144, 524288, 24, 1, 0, 125.1), ("24>144 wgrad", 144, 24, 524288, 1, 1, 133.1),
+    ("56>336 fwd", 336, 32768, 56, 1, 0, 34.0), ("336>56 dgrad", 336, 32768, 56, 0, 0, 30.1),
+]
+
 
 def torch_fn(A, ak, B, bk):
     Am = A if ak else A.t()
@@ -55,7 +68,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--sweep", action="store_true", help="time every (tile, split) plan per shape")
+    ap.add_argument("--conv", action="store_true", help="1x1-conv-shaped GEMMs vs the conv kernels")
     args = ap.parse_args()
+    if args.conv:
+        from e2ep_amd import nn_ops
+        for name, M, N, K, ak, bk, conv_us in CONV_ROWS:
+            A = torch.randn((M, K) if ak else (K, M), device="cuda")
+            B = torch.randn((N, K) if bk else (K, N), device="cuda")
+            out = torch.empty(M, N, device="cuda")
+            te = timed(lambda: nn_ops.gemm(A, ak, B, bk, M, N, K, out=out))
+            tt = timed(torch_fn(A, ak, B, bk))
+            fl = 2.0 * M * N * K
+            print(f"{name:16s} {M:6d} {N:7d} {K:7d}  e2ep {te:7.1f} us {fl / te / 1e6:6.1f} TF/s  "
+                  f"torch {tt:7.1f}  conv kernel {conv_us:7.1f}", flush=True)
+        return
     from e2ep_amd import nn_ops
     rows = []
     tot_e = tot_t = 0.0
