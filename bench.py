@@ -85,6 +85,62 @@ def lss_fwd_kernel_ms(plan, dev, C=64, iters=50):
     return s.elapsed_time(e) / iters, iters
 
 
+def lss_c4(dev, iters=50):
+    """C4 (BASELINE configs[3]): the lift-splat pair at 6 cams x 512^2, B = 4 per GPU, 200 x 200
+    BEV — the HBM-bound voxel pooling stressed at hi-res.  Mean durations of e2ep_lss_fwd /
+    e2ep_lss_bwd over `iters` back-to-back launches (HIP events on the launch stream) on the
+    hi-res rig's own pillar plan, and the algorithmic GB/s (lss_fwd_bytes / lss_bwd_bytes)."""
+    from e2ep_amd import _lib, synthetic
+    from model.bev_model import BevModel
+    from tool.config import default_cfg
+
+    cfg = default_cfg()
+    cfg.final_dim = (512, 512)
+    bm = BevModel(cfg).to(dev)
+    B = 4
+    K, E = synthetic.rig(6, 512, 512, 512)
+    K = K.unsqueeze(0).expand(B, *K.shape).contiguous()
+    E = E.unsqueeze(0).expand(B, *E.shape).contiguous()
+    plan = bm.plan(K, E, dev)
+    N, D, hw, XY, C = plan.N, plan.D, plan.h * plan.w, plan.XYZ, 64
+    g = torch.Generator(device="cpu").manual_seed(0)
+    prob = torch.rand(B * N, D, hw, generator=g).softmax(1).to(dev)
+    featT = torch.randn(B * N, hw, C, generator=g).to(dev)
+    bev = torch.empty(B, C, XY, device=dev)
+    gT = torch.randn(B, XY, C, generator=g).to(dev)
+    gp, gf = torch.empty_like(prob), torch.empty(B * N, C, hw, device=dev)
+
+    def fwd():
+        _lib.call("e2ep_lss_fwd", _lib.ptr(prob), _lib.ptr(featT), _lib.ptr(plan.offsets),
+                  _lib.ptr(plan.order), _lib.ptr(plan.tiles), B, N, D, hw, C, XY, _lib.ptr(bev),
+                  C * XY, _lib.stream())
+
+    def bwd():
+        _lib.call("e2ep_lss_bwd", _lib.ptr(gT), _lib.ptr(prob), _lib.ptr(featT),
+                  _lib.ptr(plan.pillar), B, N, D, hw, C, XY, _lib.ptr(gp), _lib.ptr(gf),
+                  _lib.stream())
+
+    out = {"config": "C4: 6 cams x 512^2, B=4, 200x200 BEV, C=64, D=48", "unit": "GB/s",
+           "peak": HBM_PEAK_GBS}
+    for name, fn, nb in (("fwd", fwd, lss_fwd_bytes(B, N, C, D, hw, XY)),
+                         ("bwd", bwd, lss_bwd_bytes(B, N, C, D, hw, XY))):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        gbs = nb / (ms * 1e-3) / 1e9
+        out[name] = {"launch_ms": round(ms, 5), "bytes_per_launch": nb, "achieved": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    del bm
+    return out
+
+
 def device_batch(data, dev):
     out = {}
     for k, v in data.items():
@@ -288,6 +344,8 @@ def main():
                     "launches": n_fwd, "timing": "HIP events around back-to-back launches on the "
                                                  "launch stream, model's pillar plan"}
 
+    c4 = lss_c4(dev) if rank == 0 else None
+
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads, cpu_model = host_cores()
@@ -314,7 +372,7 @@ def main():
                            "parallelism": f"dp{world}"},
                 "world": {"size": world, "backend": backend, "rehearsal": rehearsal},
                 "roofline": roofline, "step_roofline": step_roofline, "roofline_lss": roofline_lss,
-                "cpu_baseline": base, "final_loss": round(float(loss), 4)}
+                "lss_c4": c4, "cpu_baseline": base, "final_loss": round(float(loss), 4)}
         print(json.dumps(line), flush=True)
         print("kernel timing (launches, mean ms, total ms):",
               {k: (n, round(m, 4), round(t, 3)) for k, (n, m, t) in kern.items()}, file=sys.stderr)

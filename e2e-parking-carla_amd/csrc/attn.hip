@@ -28,6 +28,7 @@
 // seed is read from device memory (drawn by the caller each call, graph-capturable), so the
 // backward regenerates the same mask without storing it.
 #include "common.h"
+#include "dropout.h"
 
 namespace e2ep {
 
@@ -41,22 +42,6 @@ constexpr int FWD_KG = E2EP_ATT_KG;  // keys per online-softmax rescale in the f
 
 // 2^x on the hardware v_exp_f32 (arguments here are <= 0 or -inf; tiny results flush to 0)
 __device__ __forceinline__ float att_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-__device__ __forceinline__ uint32_t att_mix(uint32_t x) {  // 32-bit integer finaliser
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-// dropout keep test for counter c: uniform 24-bit value >= p
-__device__ __forceinline__ bool att_keep(uint32_t seedmix, uint32_t c, float p) {
-  return (float)(att_mix(c ^ seedmix) >> 8) * (1.0f / 16777216.0f) >= p;
-}
-__device__ __forceinline__ uint32_t att_seedmix(const int *seed) {
-  return seed ? att_mix((uint32_t)seed[0] * 0x9e3779b9u + 0x632be5abu) : 0u;
-}
 
 template <int DHP>
 __device__ __forceinline__ float dot_lds(const float (&r)[DHP], const float *row) {

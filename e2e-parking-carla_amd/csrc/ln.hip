@@ -2,12 +2,15 @@
 // feature fusion encoder and the control decoder (torch.nn.TransformerEncoderLayer /
 // TransformerDecoderLayer, reference model/feature_fusion.py:13-14,48-50 and
 // model/control_predict.py:19-20,39-47):  y = LayerNorm(a + dropout(b))  with
-// dropout(b) = b * [u >= p] / (1 - p)  (u: uniform draws, one per element; p = 0: identity).
+// dropout(b) = b * [u >= p] / (1 - p)  (u: uniform draws, one per element; p = 0: identity),
+// or, without u, the counter hash of dropout.h keyed by a per-call device seed (element index
+// row * E + c as the counter) — no uniform tensor is drawn, written or read.
 // Forward: one wave per row (E = d_model columns, lanes stride the row).  Backward: one wave
 // per row for the input gradients (da = dx, db = dx * mask / (1 - p)); gamma / beta gradients
 // as per-block column partials over fixed row ranges, summed in block order by a second
 // kernel — deterministic.
 #include "common.h"
+#include "dropout.h"
 
 namespace e2ep {
 
@@ -15,12 +18,14 @@ constexpr int LN_MAXV = 8;  // up to 512 columns per row (8 per lane)
 
 __global__ void __launch_bounds__(256) k_add_drop_ln_fwd(
     const float *__restrict__ a, const float *__restrict__ b, const float *__restrict__ u,
-    float p, float scale, const float *__restrict__ gamma, const float *__restrict__ beta,
-    int rows, int E, float eps, float *__restrict__ x, float *__restrict__ y,
-    float *__restrict__ mean, float *__restrict__ rstd) {
+    const int *__restrict__ seed, float p, float scale, const float *__restrict__ gamma,
+    const float *__restrict__ beta, int rows, int E, float eps, float *__restrict__ x,
+    float *__restrict__ y, float *__restrict__ mean, float *__restrict__ rstd) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const size_t base = (size_t)row * E;
+  const bool hashed = !u && seed && p > 0.f;
+  const uint32_t sm_ = hashed ? att_seedmix(seed) : 0u;
   float v[LN_MAXV];
   float s = 0.f;
 #pragma unroll
@@ -30,6 +35,7 @@ __global__ void __launch_bounds__(256) k_add_drop_ln_fwd(
     if (c < E) {
       float bv = b ? b[base + c] : 0.f;
       if (u) bv = u[base + c] >= p ? bv * scale : 0.f;
+      else if (hashed) bv = att_keep(sm_, (uint32_t)(base + c), p) ? bv * scale : 0.f;
       v[j] = a[base + c] + bv;
       s += v[j];
     }
@@ -66,8 +72,10 @@ constexpr int LN_ROWS_PER_WAVE = 1;
 __global__ void __launch_bounds__(256) k_add_drop_ln_bwd(
     const float *__restrict__ dy, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ rstd, const float *__restrict__ gamma, const float *__restrict__ u,
-    float p, float scale, int rows, int E, float *__restrict__ da, float *__restrict__ db,
-    float *__restrict__ part) {
+    const int *__restrict__ seed, float p, float scale, int rows, int E, float *__restrict__ da,
+    float *__restrict__ db, float *__restrict__ part) {
+  const bool hashed = !u && seed && p > 0.f;
+  const uint32_t sm_ = hashed ? att_seedmix(seed) : 0u;
   __shared__ float sg[4][LN_MAXV * 64], sb[4][LN_MAXV * 64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float pg[LN_MAXV], pb[LN_MAXV];
@@ -102,7 +110,10 @@ __global__ void __launch_bounds__(256) k_add_drop_ln_bwd(
       if (c < E) {
         const float dx = rs * (gy[j] - c1 - xh[j] * c2);
         if (da) da[base + c] = dx;
-        if (db) db[base + c] = u ? (u[base + c] >= p ? dx * scale : 0.f) : dx;
+        if (db)
+          db[base + c] = u        ? (u[base + c] >= p ? dx * scale : 0.f)
+                         : hashed ? (att_keep(sm_, (uint32_t)(base + c), p) ? dx * scale : 0.f)
+                                  : dx;
       }
     }
   }
@@ -149,38 +160,72 @@ using namespace e2ep;
 
 extern "C" {
 
-int e2ep_add_drop_ln_fwd(const float *a, const float *b, const float *u, float p,
-                         const float *gamma, const float *beta, int rows, int E, float eps,
-                         float *x, float *y, float *mean, float *rstd, void *stream) {
+static int add_drop_ln_fwd(const float *a, const float *b, const float *u, const int *seed,
+                           float p, const float *gamma, const float *beta, int rows, int E,
+                           float eps, float *x, float *y, float *mean, float *rstd,
+                           hipStream_t stream) {
   E2EP_REQUIRE(rows > 0 && E > 0, E2EP_EINVAL, "e2ep_add_drop_ln_fwd: bad shape");
   E2EP_REQUIRE(E <= 64 * LN_MAXV, E2EP_ERANGE, "e2ep_add_drop_ln_fwd: E %d > %d", E, 64 * LN_MAXV);
   E2EP_REQUIRE(p >= 0.f && p < 1.f, E2EP_EINVAL, "e2ep_add_drop_ln_fwd: p must be in [0, 1)");
+  E2EP_REQUIRE((long long)rows * E < 0xffffffffLL, E2EP_ERANGE, "e2ep_add_drop_ln_fwd: too large");
   const float scale = 1.f / (1.f - p);
-  hipLaunchKernelGGL(k_add_drop_ln_fwd, dim3(cdiv(rows, 4)), dim3(256), 0, as_stream(stream), a, b,
-                     u, p, scale, gamma, beta, rows, E, eps, x, y, mean, rstd);
+  hipLaunchKernelGGL(k_add_drop_ln_fwd, dim3(cdiv(rows, 4)), dim3(256), 0, stream, a, b, u, seed,
+                     p, scale, gamma, beta, rows, E, eps, x, y, mean, rstd);
   return launch_status("e2ep_add_drop_ln_fwd");
+}
+
+int e2ep_add_drop_ln_fwd(const float *a, const float *b, const float *u, float p,
+                         const float *gamma, const float *beta, int rows, int E, float eps,
+                         float *x, float *y, float *mean, float *rstd, void *stream) {
+  return add_drop_ln_fwd(a, b, u, nullptr, p, gamma, beta, rows, E, eps, x, y, mean, rstd,
+                         as_stream(stream));
+}
+
+int e2ep_add_drop_ln_fwd_seeded(const float *a, const float *b, const int *seed, float p,
+                                const float *gamma, const float *beta, int rows, int E, float eps,
+                                float *x, float *y, float *mean, float *rstd, void *stream) {
+  E2EP_REQUIRE(seed || p == 0.f, E2EP_EINVAL, "e2ep_add_drop_ln_fwd_seeded: seed required for p > 0");
+  return add_drop_ln_fwd(a, b, nullptr, seed, p, gamma, beta, rows, E, eps, x, y, mean, rstd,
+                         as_stream(stream));
 }
 
 size_t e2ep_add_drop_ln_bwd_workspace(int rows, int E) {
   return (size_t)2 * cdiv(rows, 4 * LN_ROWS_PER_WAVE) * E * sizeof(float);
 }
 
-int e2ep_add_drop_ln_bwd(const float *dy, const float *x, const float *mean, const float *rstd,
-                         const float *gamma, const float *u, float p, int rows, int E,
-                         float *da, float *db, float *dgamma, float *dbeta, void *workspace,
-                         void *stream) {
+static int add_drop_ln_bwd(const float *dy, const float *x, const float *mean, const float *rstd,
+                           const float *gamma, const float *u, const int *seed, float p, int rows,
+                           int E, float *da, float *db, float *dgamma, float *dbeta,
+                           void *workspace, hipStream_t stream) {
   E2EP_REQUIRE(rows > 0 && E > 0, E2EP_EINVAL, "e2ep_add_drop_ln_bwd: bad shape");
   E2EP_REQUIRE(E <= 64 * LN_MAXV, E2EP_ERANGE, "e2ep_add_drop_ln_bwd: E %d > %d", E, 64 * LN_MAXV);
   const float scale = 1.f / (1.f - p);
   const int nblk = cdiv(rows, 4 * LN_ROWS_PER_WAVE);
   float *part = (dgamma || dbeta) ? static_cast<float *>(workspace) : nullptr;
-  E2EP_REQUIRE(!part || workspace, E2EP_EINVAL, "e2ep_add_drop_ln_bwd: workspace needed");
-  hipLaunchKernelGGL(k_add_drop_ln_bwd, dim3(nblk), dim3(256), 0, as_stream(stream), dy, x, mean, rstd,
-                     gamma, u, p, scale, rows, E, da, db, part);
+  E2EP_REQUIRE(!(dgamma || dbeta) || workspace, E2EP_EINVAL, "e2ep_add_drop_ln_bwd: workspace needed");
+  hipLaunchKernelGGL(k_add_drop_ln_bwd, dim3(nblk), dim3(256), 0, stream, dy, x, mean, rstd,
+                     gamma, u, seed, p, scale, rows, E, da, db, part);
   if (part)
-    hipLaunchKernelGGL(k_ln_param_grads, dim3(cdiv(E, 64), 2), dim3(1024), 0, as_stream(stream),
-                       part, nblk, E, dgamma, dbeta);
+    hipLaunchKernelGGL(k_ln_param_grads, dim3(cdiv(E, 64), 2), dim3(1024), 0, stream, part, nblk,
+                       E, dgamma, dbeta);
   return launch_status("e2ep_add_drop_ln_bwd");
+}
+
+int e2ep_add_drop_ln_bwd(const float *dy, const float *x, const float *mean, const float *rstd,
+                         const float *gamma, const float *u, float p, int rows, int E,
+                         float *da, float *db, float *dgamma, float *dbeta, void *workspace,
+                         void *stream) {
+  return add_drop_ln_bwd(dy, x, mean, rstd, gamma, u, nullptr, p, rows, E, da, db, dgamma, dbeta,
+                         workspace, as_stream(stream));
+}
+
+int e2ep_add_drop_ln_bwd_seeded(const float *dy, const float *x, const float *mean,
+                                const float *rstd, const float *gamma, const int *seed, float p,
+                                int rows, int E, float *da, float *db, float *dgamma,
+                                float *dbeta, void *workspace, void *stream) {
+  E2EP_REQUIRE(seed || p == 0.f, E2EP_EINVAL, "e2ep_add_drop_ln_bwd_seeded: seed required for p > 0");
+  return add_drop_ln_bwd(dy, x, mean, rstd, gamma, nullptr, seed, p, rows, E, da, db, dgamma,
+                         dbeta, workspace, as_stream(stream));
 }
 
 }  // extern "C"

@@ -460,9 +460,16 @@ __global__ void __launch_bounds__(256) k_lss_bwd(
   __shared__ float s_gp[64][BWD_PIX + 1];
   __shared__ float s_gf[64][BWD_PIX + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bn = blockIdx.y;  // b*N + n
+  // XCD-contiguous work order: workgroups are dealt round-robin to the 8 XCDs, so block L runs
+  // on XCD L % 8; give XCD x the contiguous work range [x G/8, (x+1) G/8) — at B = 8 one
+  // sample's 4 cameras, so an XCD's L2 holds the gT rows of one sample (a camera's rays
+  // touch ~1/4 of its 10 MB) instead of every XCD streaming all eight samples' rows.
+  const int chunks = (HW + BWD_PIX - 1) / BWD_PIX;
+  const int G = gridDim.x, L = blockIdx.x;
+  const int w = (G % 8 == 0) ? (L % 8) * (G / 8) + L / 8 : L;
+  const int bn = w / chunks;  // b*N + n
   const int b = bn / N;
-  const int pix0 = blockIdx.x * BWD_PIX;
+  const int pix0 = (w - bn * chunks) * BWD_PIX;
   const bool lane_ok = lane < C;
   const __amdgpu_buffer_rsrc_t rg = rsrc(gT, 4LL * B * XYZ * C);
   const int rowbase = b * XYZ;
@@ -746,7 +753,7 @@ int e2ep_lss_bwd(const float *gT, const float *prob, const float *featT, const i
   E2EP_REQUIRE(B > 0 && N > 0 && D > 0 && hw > 0 && C > 0 && XYZ > 0, E2EP_EINVAL,
                "e2ep_lss_bwd: bad shape");
   E2EP_REQUIRE(C <= 64 && D <= 64, E2EP_ERANGE, "e2ep_lss_bwd: needs C<=64, D<=64 (got %d,%d)", C, D);
-  dim3 grid(cdiv(hw, BWD_PIX), B * N);
+  dim3 grid(cdiv(hw, BWD_PIX) * B * N);  // 1-D: the kernel maps blocks to XCD-contiguous work
   E2EP_REQUIRE(4LL * B * XYZ * C < 0x7fffffffLL, E2EP_ERANGE,
                "e2ep_lss_bwd: gT over 2 GiB (32-bit buffer offsets)");
   hipLaunchKernelGGL(k_lss_bwd, grid, dim3(256), 0, as_stream(stream), gT, prob, featT, pillar, B,

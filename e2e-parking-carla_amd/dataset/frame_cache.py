@@ -286,8 +286,11 @@ class GpuFrameLoader:
             slots.append({k: torch.empty((width,) + a.shape[1:],
                                          dtype=_tdtype(a)).pin_memory()
                           for k, a in self.cache.arrays.items()})
-        done = [None] * len(slots)      # event: the slot's last H2D copy has finished
-        free, ready = queue.Queue(), queue.Queue(maxsize=self.prefetch)
+        # The producer thread only gathers rows on the host (numpy), never calls HIP: a slot
+        # comes back to it through `free` after the main thread has seen the slot's H2D copy
+        # complete, so no thread but the caller's touches the device (a HIP call from a helper
+        # thread would break a graph capture running on the main thread).
+        free, ready = queue.Queue(), queue.Queue()
         for s in range(len(slots)):
             free.put(s)
         stop = threading.Event()
@@ -298,8 +301,6 @@ class GpuFrameLoader:
                     s = free.get()
                     if stop.is_set():
                         return
-                    if done[s] is not None:
-                        done[s].synchronize()
                     self.cache.gather(idx.numpy(),
                                       out={k: v.numpy() for k, v in slots[s].items()})
                     ready.put((s, len(idx)))
@@ -311,6 +312,7 @@ class GpuFrameLoader:
         th.start()
         copy = torch.cuda.Stream(self.device)
         main = torch.cuda.current_stream(self.device)
+        inflight = []  # (slot, event of its H2D copy), oldest first
         try:
             while True:
                 item = ready.get()
@@ -319,7 +321,6 @@ class GpuFrameLoader:
                 if isinstance(item, BaseException):
                     raise item
                 s, B = item
-                copy.wait_stream(main)  # the previous batch's buffers may be reused by torch
                 with torch.cuda.stream(copy):
                     host = slots[s]
                     d = {k: v[:B].to(self.device, non_blocking=True) for k, v in host.items()}
@@ -328,8 +329,12 @@ class GpuFrameLoader:
                 main.wait_event(ev)
                 for t in d.values():
                     t.record_stream(main)
-                done[s] = ev
-                free.put(s)
+                inflight.append((s, ev))
+                # hand back the slots whose copies are done (keep at most one in flight)
+                while len(inflight) > 1 or (inflight and inflight[0][1].query()):
+                    s0, e0 = inflight.pop(0)
+                    e0.synchronize()
+                    free.put(s0)
                 labels = {k: d[k] for k in LABEL_FIELDS}
                 yield self._assemble(d["rgb"], d["depth_rgb"], d["bev"], labels, B)
         finally:

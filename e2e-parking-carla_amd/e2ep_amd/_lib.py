@@ -63,6 +63,8 @@ SIGNATURES = {
     "e2ep_avgpool_bwd": (_i, [_p, _i, _i, _p, _p]),
     "e2ep_add_drop_ln_fwd": (_i, [_p, _p, _p, _f, _p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
     "e2ep_add_drop_ln_bwd_workspace": (_sz, [_i, _i]),
+    "e2ep_add_drop_ln_fwd_seeded": (_i, [_p, _p, _p, _f, _p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
+    "e2ep_add_drop_ln_bwd_seeded": (_i, [_p, _p, _p, _p, _p, _p, _f, _i, _i, _p, _p, _p, _p, _p, _p]),
     "e2ep_add_drop_ln_bwd": (_i, [_p, _p, _p, _p, _p, _p, _f, _i, _i, _p, _p, _p, _p, _p, _p]),
     "e2ep_attn_fwd": (_i, [_p, _p, _p] + [_i] * 11 + [_f, _i, _p, _f, _p, _p, _p, _p]),
     "e2ep_attn_bwd_workspace": (_sz, [_i, _i, _i]),

@@ -17,7 +17,7 @@ import math
 
 import torch
 
-from . import _lib, nn_ops, timing
+from . import _lib, nn_ops, rng, timing
 
 MAX_SEQ = 256
 MAX_HEAD_DIM = 64
@@ -77,7 +77,7 @@ def attention(qb, kvb, H, causal=False, key_pad=None, p=0.0, seed=None):
     """Functional entry: see _Attn.  key_pad: bool (B, Sk) or None; seed: int32 (1,) device
     tensor, drawn here when p > 0 and none is given."""
     if p > 0.0 and seed is None:
-        seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=qb.device)
+        seed = rng.seed(qb.device)
     qb = qb.contiguous()
     kvb = None if kvb is None else kvb.contiguous()
     if key_pad is not None:

@@ -4,7 +4,7 @@ each backward is the matching e2ep gradient kernel (no PyTorch arithmetic)."""
 import torch
 import torch.nn.functional as F
 
-from . import _lib, timing
+from . import _lib, rng, timing
 
 ACT = {None: 0, "none": 0, "relu": 1, "swish": 2}
 
@@ -546,7 +546,7 @@ def squeeze_excite(x, w1, b1, w2, b2):
 # ------------------------------------------------------------------------------------------
 class _AddDropLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b, gamma, beta, u, p, eps):
+    def forward(ctx, a, b, gamma, beta, u, seed, p, eps):
         a = a.contiguous()
         b = b.contiguous()
         E = a.shape[-1]
@@ -555,17 +555,19 @@ class _AddDropLN(torch.autograd.Function):
         y = torch.empty_like(a)
         mean = torch.empty(rows, dtype=torch.float32, device=a.device)
         rstd = torch.empty_like(mean)
+        # mask from `u` (explicit uniforms) or, without u, from the counter hash keyed by seed
+        fn, mask = ("e2ep_add_drop_ln_fwd", u) if seed is None else ("e2ep_add_drop_ln_fwd_seeded", seed)
         with timing.region(timing.name("ln_fwd", a.shape, "_AddDropLN")):
-            _lib.call("e2ep_add_drop_ln_fwd", _lib.ptr(a), _lib.ptr(b), _lib.ptr(u), float(p),
+            _lib.call(fn, _lib.ptr(a), _lib.ptr(b), _lib.ptr(mask), float(p),
                       _lib.ptr(gamma), _lib.ptr(beta), rows, E, float(eps), _lib.ptr(x), _lib.ptr(y),
                       _lib.ptr(mean), _lib.ptr(rstd), _lib.stream())
-        ctx.save_for_backward(x, mean, rstd, gamma, u)
-        ctx.p, ctx.rows, ctx.E = float(p), rows, E
+        ctx.save_for_backward(x, mean, rstd, gamma, mask)
+        ctx.p, ctx.rows, ctx.E, ctx.seeded = float(p), rows, E, seed is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, mean, rstd, gamma, u = ctx.saved_tensors
+        x, mean, rstd, gamma, mask = ctx.saved_tensors
         nig = ctx.needs_input_grad
         da = torch.empty_like(x) if nig[0] else None
         db = torch.empty_like(x) if nig[1] else None
@@ -573,19 +575,24 @@ class _AddDropLN(torch.autograd.Function):
         dbeta = torch.empty_like(gamma) if (gamma is not None and nig[3]) else None
         ws = _ws(_lib.load().e2ep_add_drop_ln_bwd_workspace(ctx.rows, ctx.E), x.device)
         with timing.region(timing.name("ln_bwd", x.shape, "_AddDropLN")):
-            _lib.call("e2ep_add_drop_ln_bwd", _lib.ptr(dy.contiguous()), _lib.ptr(x), _lib.ptr(mean),
-                      _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(u), ctx.p, ctx.rows, ctx.E,
+            _lib.call("e2ep_add_drop_ln_bwd_seeded" if ctx.seeded else "e2ep_add_drop_ln_bwd",
+                      _lib.ptr(dy.contiguous()), _lib.ptr(x), _lib.ptr(mean),
+                      _lib.ptr(rstd), _lib.ptr(gamma), _lib.ptr(mask), ctx.p, ctx.rows, ctx.E,
                       _lib.ptr(da), _lib.ptr(db), _lib.ptr(dg), _lib.ptr(dbeta), _lib.ptr(ws),
                       _lib.stream())
-        return da, db, dg, dbeta, None, None, None
+        return da, db, dg, dbeta, None, None, None, None
 
 
-def add_drop_layer_norm(a, b, norm, p=0.0):
+def add_drop_layer_norm(a, b, norm, p=0.0, u=None, seed=None):
     """norm(a + dropout_p(b)) for an nn.LayerNorm `norm` over the last dim, one fused op.
-    p > 0 draws the dropout mask with torch.rand_like (graph-capturable)."""
+    The dropout mask is [u >= p] when uniforms `u` are given, else the counter hash keyed by a
+    device seed (e2ep_amd.rng: this step's pool; graph-capturable, nothing drawn per element)."""
     _dev(a, b)
-    u = torch.rand_like(b) if p > 0.0 else None
-    return _AddDropLN.apply(a, b, norm.weight, norm.bias, u, p, norm.eps)
+    if p > 0.0 and u is None and seed is None:
+        seed = rng.seed(a.device)
+    if p == 0.0:
+        u = seed = None
+    return _AddDropLN.apply(a, b, norm.weight, norm.bias, u, seed, p, norm.eps)
 
 
 # ------------------------------------------------------------------------------------------
@@ -702,7 +709,7 @@ def relu_dropout(x, p=0.0, seed=None):
     _dev(x)
     x = x.contiguous()
     if p > 0.0 and seed is None:
-        seed = torch.randint(0, 2 ** 31 - 1, (1,), dtype=torch.int32, device=x.device)
+        seed = rng.seed(x.device)
     return _ReluDropout.apply(x, float(p), seed)
 
 

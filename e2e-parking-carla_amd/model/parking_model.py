@@ -10,7 +10,7 @@ reproducible runs; by default it is drawn on the device exactly like the referen
 import torch
 from torch import nn
 
-from e2ep_amd import lss, nn_ops
+from e2ep_amd import lss, nn_ops, rng
 from model.bev_encoder import BevEncoder
 from model.bev_model import BevModel
 from model.control_predict import ControlPredict
@@ -70,6 +70,8 @@ class ParkingModel(nn.Module):
         return fuse_feature, pred_segmentation, pred_depth, bev_target
 
     def forward(self, data, noise=None):
+        if self.training:  # one launch draws every dropout seed of this step (e2ep_amd.rng)
+            rng.begin_step(data["image"].device)
         fuse_feature, pred_segmentation, pred_depth, _ = self.encoder(data, noise)
         gt = data["gt_control"].to(fuse_feature.device, non_blocking=True)
         pred_control = self.control_predict(fuse_feature, gt)

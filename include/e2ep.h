@@ -261,8 +261,18 @@ int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, cons
  *   y = (x - mean) * rstd * gamma + beta,  rstd = 1 / sqrt(biased var + eps)
  * x (nullable), mean, rstd [rows] are saved for the backward, which returns da = dL/dx,
  * db = da * [u >= p] / (1 - p) and gamma / beta gradients (fixed-order column sums;
- * workspace e2ep_add_drop_ln_bwd_workspace bytes).
+ * workspace e2ep_add_drop_ln_bwd_workspace bytes).  The _seeded variants draw the mask from
+ * the counter hash shared with the attention / feed-forward dropout (keep element
+ * row * E + c iff hash(seed, row * E + c) >= p), keyed by the device int32 *seed: no uniform
+ * tensor is read.
  * ------------------------------------------------------------------------------------- */
+int e2ep_add_drop_ln_fwd_seeded(const float *a, const float *b, const int *seed, float p,
+                                const float *gamma, const float *beta, int rows, int E, float eps,
+                                float *x, float *y, float *mean, float *rstd, void *stream);
+int e2ep_add_drop_ln_bwd_seeded(const float *dy, const float *x, const float *mean,
+                                const float *rstd, const float *gamma, const int *seed, float p,
+                                int rows, int E, float *da, float *db, float *dgamma,
+                                float *dbeta, void *workspace, void *stream);
 int e2ep_add_drop_ln_fwd(const float *a, const float *b, const float *u, float p,
                          const float *gamma, const float *beta, int rows, int E, float eps,
                          float *x, float *y, float *mean, float *rstd, void *stream);

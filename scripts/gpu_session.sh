@@ -23,5 +23,6 @@ PYTEST_ARGS=${PYTEST_ARGS:-tests}
 [[ $STEPS == *bench* ]]  && run bench 600 python bench.py --steps 20 --warmup 5
 [[ $STEPS == *rehearse* ]] && E2EP_BENCH_REHEARSAL=1 run rehearsal_2rank 600 python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline
 [[ $STEPS == *prof* ]]   && run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 --no-cpu-baseline
+[[ $STEPS == *c4prof* ]] && run c4prof 600 rocprofv3 --kernel-trace --stats -d $OUT/c4prof -o run --output-format csv -- python scripts/bench_lss.py --cams 6 --image 512 --batch 4
 [[ $STEPS == *pmc* ]]    && run pmc_lss 600 bash scripts/pmc_lss.sh
 exit 0

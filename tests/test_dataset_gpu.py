@@ -84,7 +84,9 @@ def test_gpu_loader_equals_reference_collate(mini, resident):
     loader = GpuFrameLoader(cache, 3, shuffle=True, drop_last=False, seed=5, resident=resident)
     order = loader.batches()
     n = 0
-    for idx, batch in zip(order, loader):
+    it = iter(loader)
+    for idx in order:
+        batch = next(it)
         want = default_collate([ds[int(i)] for i in idx])
         assert sorted(batch) == sorted(want)
         for k, v in want.items():
@@ -94,6 +96,7 @@ def test_gpu_loader_equals_reference_collate(mini, resident):
             assert torch.equal(batch[k].cpu(), v), k
         n += len(idx)
     assert n == len(ds)
+    assert next(it, None) is None  # exhausted: the producer thread has finished
 
 
 def test_gpu_loader_trains_a_step(mini):
@@ -102,7 +105,9 @@ def test_gpu_loader_trains_a_step(mini):
     from trainer.pl_trainer import ParkingTrainingModule
     ds, cache = mini
     cfg = ds.cfg
-    batch = next(iter(GpuFrameLoader(cache, 2, shuffle=False)))
+    it = iter(GpuFrameLoader(cache, 2, shuffle=False))
+    batch = next(it)
+    it.close()  # stop the host gather thread now, not at garbage collection
     module = ParkingTrainingModule(cfg).to(DEV)
     module.train()
     loss = module.training_step(batch, 0)

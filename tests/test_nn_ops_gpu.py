@@ -327,7 +327,8 @@ def test_add_dropout_layernorm_fused(rows, E, p):
     beta = 0.1 * torch.randn(E, generator=g)
     dy = torch.randn(rows, E, generator=g)
     ts = [t.to(DEV).requires_grad_(True) for t in (a, b, gamma, beta)]
-    y = nn_ops._AddDropLN.apply(ts[0], ts[1], ts[2], ts[3], u.to(DEV) if p > 0 else None, p, 1e-5)
+    y = nn_ops._AddDropLN.apply(ts[0], ts[1], ts[2], ts[3], u.to(DEV) if p > 0 else None, None, p,
+                                1e-5)
     y.backward(dy.to(DEV))
     rs = [t.double().requires_grad_(True) for t in (a, b, gamma, beta)]
     mask = (u >= p).double() / (1 - p) if p > 0 else torch.ones_like(u).double()
@@ -336,6 +337,48 @@ def test_add_dropout_layernorm_fused(rows, E, p):
     assert rel_l2(y, y64) < 1e-6
     for got, ref in zip(ts, rs):
         assert rel_l2(got.grad, ref.grad) < 1e-5
+
+
+@pytest.mark.parametrize("rows,E,p", [(2048, 258, 0.1), (112, 258, 0.1), (7, 33, 0.5)])
+def test_add_dropout_layernorm_seeded(rows, E, p):
+    """The seeded LayerNorm dropout (no uniform tensor) keeps element row*E + c exactly when the
+    shared counter hash does: the mask comes from e2ep_attn_keep_mask over one (rows x E)
+    'head', and values / all gradients match fp64 torch with that mask."""
+    from e2ep_amd import _lib, nn_ops
+    g = _g(rows * 3 + E)
+    a = torch.randn(rows, E, generator=g)
+    b = torch.randn(rows, E, generator=g)
+    gamma = 1 + 0.2 * torch.randn(E, generator=g)
+    beta = 0.1 * torch.randn(E, generator=g)
+    dy = torch.randn(rows, E, generator=g)
+    seed = torch.tensor([12345 + rows], dtype=torch.int32, device=DEV)
+    keep = torch.empty(rows, E, dtype=torch.uint8, device=DEV)
+    _lib.call("e2ep_attn_keep_mask", _lib.ptr(seed), 1, rows, E, p, _lib.ptr(keep), _lib.stream())
+    keep = keep.cpu().double()
+    assert abs(float(keep.mean()) - (1 - p)) < 0.05
+    ts = [t.to(DEV).requires_grad_(True) for t in (a, b, gamma, beta)]
+    norm = torch.nn.LayerNorm(E).to(DEV)
+    norm.weight, norm.bias = torch.nn.Parameter(ts[2]), torch.nn.Parameter(ts[3])
+    y = nn_ops.add_drop_layer_norm(ts[0], ts[1], norm, p, seed=seed)
+    y.backward(dy.to(DEV))
+    rs = [t.double().requires_grad_(True) for t in (a, b, gamma, beta)]
+    y64 = F.layer_norm(rs[0] + rs[1] * keep / (1 - p), (E,), rs[2], rs[3], 1e-5)
+    y64.backward(dy.double())
+    assert rel_l2(y, y64) < 1e-6
+    for got, ref in zip((ts[0], ts[1], norm.weight, norm.bias), rs):
+        assert rel_l2(got.grad, ref.grad) < 1e-5
+    y2 = nn_ops.add_drop_layer_norm(ts[0].detach(), ts[1].detach(), norm, p, seed=seed)
+    assert torch.equal(y2, y.detach())
+
+
+def test_dropout_seed_pool_hands_out_distinct_seeds():
+    from e2ep_amd import rng
+    rng.begin_step(DEV)
+    seeds = [rng.seed(DEV) for _ in range(40)]
+    vals = torch.cat(seeds).cpu().tolist()
+    assert len(set(vals)) == 40 and all(s.numel() == 1 and s.dtype == torch.int32 for s in seeds)
+    rng.begin_step(DEV)
+    assert torch.cat([rng.seed(DEV) for _ in range(40)]).cpu().tolist() != vals
 
 
 @pytest.mark.parametrize("shape", [(32, 48, 32, 32), (3, 5, 7, 9), (2, 1, 4, 4)])
