@@ -1259,7 +1259,8 @@ static size_t gemm_workspace(const GemmPlan &p, int M) {
 // ---- second-generation GEMM plan (k_conv_gemm2) ------------------------------------------
 static int g_conv_precision = 0;  // GEMM operand precision: 0 fp32, 1 bf16, 2 fp16
 static int g_gemm_variant = 0;  // 0 auto, 1 always k_conv_gemm, 2 k_conv_gemm2 wherever it
-                                // applies, 3 the same with 128-column tiles only
+                                // applies, 3 the same with 128-column tiles only, 4 auto with
+                                // the 1x1 forward / data gradient on the batched k_gemm
 
 // live taps of the largest phase and the column count (as plan_gemm)
 static void gemm_extent(int mode, const ConvGeom &g, int &taps_max, long long &ncols, int &nph) {
@@ -1300,7 +1301,7 @@ static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt
   const long long b256 = cdiv(ncols, 256) * mblocks * nph, b128 = cdiv(ncols, 128) * mblocks * nph;
   const long long slots = 2LL * 256;  // 64 x 256 tiles resident per round (2 per CU)
   const bool fill256 = b256 >= slots && 100 * b256 >= 95 * (cdiv(b256, slots) * slots);
-  if (g_gemm_variant == 0) {
+  if (g_gemm_variant == 0 || g_gemm_variant == 4) {
     if (g.R * g.S == 1 || M < 40) return false;
     if (!fill256 && b128 < 1024) return false;
     wnt = fill256 ? 4 : 2;
@@ -1317,15 +1318,16 @@ static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt
   return true;
 }
 
-// 1x1 / stride-1 / unpadded convolutions forward and data gradient run as a column-batched
-// GEMM on k_gemm (gemm.hip): columns = (image, pixel), the weight as the A operand (k-
-// contiguous in the forward, row-contiguous in the data gradient), bias per output channel
-// (row) and the skip gradient in dx's layout.  Measured on the EfficientNet 1x1 shapes at
-// 16x16 .. 64x64 maps: 15-35 % faster than k_conv_gemm (scripts/bench_gemm.py --conv).  fp32
-// only (the bf16 / fp16 operand modes stay on k_conv_gemm / k_conv_gemm2).
+// Variant 4: 1x1 / stride-1 / unpadded convolutions forward and data gradient as a column-
+// batched GEMM on k_gemm (gemm.hip): columns = (image, pixel), the weight as the A operand
+// (k-contiguous in the forward, row-contiguous in the data gradient), bias per output channel
+// (row), the skip gradient in dx's layout.  In isolation 15-35 % faster than k_conv_gemm on
+// the EfficientNet 1x1 shapes (scripts/bench_gemm.py --conv), but 0.33 ms/step SLOWER inside
+// the replayed train step (rocprofv3 kernel stats, profiles/r02/session4), so it is opt-in.
+// fp32 only.
 static bool conv1x1_gemm_ok(int mode, const ConvGeom &g) {
   (void)mode;
-  return g_gemm_variant == 0 && g_conv_precision == 0 && g.R == 1 && g.S == 1 && g.sh == 1 &&
+  return g_gemm_variant == 4 && g_conv_precision == 0 && g.R == 1 && g.S == 1 && g.sh == 1 &&
          g.sw == 1 && g.ph == 0 && g.pw == 0 && (g.H * g.W) % 32 == 0 &&
          4LL * g.N * std::max(g.Cin, g.Cout) * g.H * g.W < 0x7fffffffLL;
 }
@@ -1461,7 +1463,7 @@ int e2ep_conv_precision(int precision) {
 
 int e2ep_conv_gemm_variant(int variant) {
   const int old = g_gemm_variant;
-  if (variant >= 0 && variant <= 3) g_gemm_variant = variant;
+  if (variant >= 0 && variant <= 4) g_gemm_variant = variant;
   return old;
 }
 

@@ -159,8 +159,9 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
  * e2ep_conv_wgrad_workspace bytes) are summed in a fixed order: deterministic. */
 /* Forward / data-gradient GEMM selection (tests, benchmarks): 0 = automatic (default),
  * 1 = always the first-generation kernel, 2 = the second-generation kernel (k-contiguous LDS
- * fragments, no padded channel steps) wherever its limits allow.  Returns the previous value;
- * a value outside 0..2 only queries.  Process-global; not thread-safe against concurrent
+ * fragments, no padded channel steps) wherever its limits allow, 3 = the same with 128-column
+ * tiles only, 4 = automatic but the 1x1 forward / data gradient on the column-batched GEMM of
+ * e2ep_gemm.  Returns the previous value; a value outside 0..4 only queries.  Process-global; not thread-safe against concurrent
  * launches. */
 int e2ep_conv_gemm_variant(int variant);
 /* Operand precision of the forward / data-gradient conv GEMMs: 0 = fp32 (default; exact-f32

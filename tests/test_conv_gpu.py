@@ -49,11 +49,11 @@ CASES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "gemm1", "gemm2", "gemm2_128"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "gemm1", "gemm2", "gemm2_128", "gemm1x1"])
 def gemm_variant(request):
     """Conv GEMM selection (e2ep_conv_gemm_variant): automatic, the first-generation kernel
     everywhere, the second-generation forward / data-gradient kernel wherever it applies
-    (256- or 128-column tiles)."""
+    (256- or 128-column tiles), automatic with the 1x1 convs on the column-batched k_gemm."""
     from e2ep_amd import _lib
     old = _lib.call_raw("e2ep_conv_gemm_variant", request.param)
     yield request.param
