@@ -141,6 +141,23 @@ def lss_c4(dev, iters=50):
     return out
 
 
+def plan_rebuild_ms(bm, K, E, dev, iters=20):
+    """Cost of NOT memoising the lift-splat plan: rig algebra + pillar index + counting sort +
+    tile schedule from device-resident K / E (the agent's path, where K / E arrive on the GPU
+    and the plan is rebuilt every predict).  HIP events around `iters` rebuilds."""
+    Kd, Ed = K.to(dev), E.to(dev)
+    for _ in range(3):
+        bm.plan(Kd, Ed, dev)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        bm.plan(Kd, Ed, dev)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
 def device_batch(data, dev):
     out = {}
     for k, v in data.items():
@@ -342,7 +359,12 @@ def main():
                     "traffic": load_traffic(args.batch),
                     "bytes_per_launch": lss_fwd_bytes(args.batch), "launch_ms": round(mean_ms, 5),
                     "launches": n_fwd, "timing": "HIP events around back-to-back launches on the "
-                                                 "launch stream, model's pillar plan"}
+                                                 "launch stream, model's pillar plan",
+                    "plan_rebuild_ms": round(plan_rebuild_ms(
+                        mod.parking_model.bev_model, data["intrinsics"], data["extrinsics"], dev), 4),
+                    "plan_note": "the train step reuses the pillar plan memoised on the host K/E "
+                                 "bytes (constant rig); plan_rebuild_ms is the per-step cost if "
+                                 "it were rebuilt (device K/E, the agent path)"}
 
     c4 = lss_c4(dev) if rank == 0 else None
 
