@@ -164,6 +164,66 @@ __global__ void __launch_bounds__(256) k_resize_bwd_2d(const float *__restrict__
   gx[idx] = accumulate ? gx[idx] + s : s;
 }
 
+// Single-pass backward writing the source gradient pillar-major, gxT[n][i * Wi + j][c]
+// (channels last) — the layout the lift-splat backward gathers rows of (k_lss_bwd reads one
+// 256-B channel row per pillar), so the BEV gradient needs no transpose.  Block = one source
+// row i x 32 source columns x 64 channels of one image: thread (column tid % 32, channel
+// group tid / 32) sums the 4 x 4 taps of 8 channels from the NCHW gradient (lanes along the
+// gradient rows), the 32 x 64 tile is transposed through LDS and stored as 32 contiguous
+// 256-B rows.  Same per-element arithmetic (and order) as k_resize_bwd_2d.
+constexpr int RBC_C = 64;
+__global__ void __launch_bounds__(256) k_resize_bwd_2d_cl(const float *__restrict__ g,
+                                                          long long g_pstride, int C, int Ho,
+                                                          int Wo, int Hi, int Wi, float sh,
+                                                          float sw, float *__restrict__ gxT) {
+  __shared__ int s_ow[RB_TW];
+  __shared__ float s_ww[RB_TW][RB_T], s_wh[RB_T];
+  __shared__ int s_oh;
+  __shared__ float tile[RB_TW][RBC_C + 1];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.y, j0 = blockIdx.x * RB_TW;
+  const int cchunks = (C + RBC_C - 1) / RBC_C;
+  const int n = blockIdx.z / cchunks, c0 = (blockIdx.z - n * cchunks) * RBC_C;
+  if (tid == 0) {
+    float w[RB_T];
+    s_oh = axis_taps(i, sh, Hi, Ho, w);
+#pragma unroll
+    for (int k = 0; k < RB_T; ++k) s_wh[k] = w[k];
+  } else if (tid >= 64 && tid < 64 + RB_TW) {
+    float w[RB_T];
+    const int c = tid - 64;
+    s_ow[c] = axis_taps(min(j0 + c, Wi - 1), sw, Wi, Wo, w);
+#pragma unroll
+    for (int k = 0; k < RB_T; ++k) s_ww[c][k] = w[k];
+  }
+  __syncthreads();
+  const int jj = tid % RB_TW, cg = tid / RB_TW;
+  const int ow = s_ow[jj], oh = s_oh;
+#pragma unroll
+  for (int q = 0; q < RBC_C / 8; ++q) {
+    const int cl = cg + 8 * q, c = c0 + cl;
+    float s = 0.f;
+    if (c < C) {
+      const float *gp = g + ((long long)n * C + c) * g_pstride;
+#pragma unroll
+      for (int a = 0; a < RB_T; ++a) {
+        const float *gr = gp + (long long)min(oh + a, Ho - 1) * Wo;
+        float t = 0.f;
+#pragma unroll
+        for (int b = 0; b < RB_T; ++b) t += s_ww[jj][b] * gr[min(ow + b, Wo - 1)];
+        s += s_wh[a] * t;
+      }
+    }
+    tile[jj][cl] = s;
+  }
+  __syncthreads();
+  for (int e = tid; e < RB_TW * RBC_C; e += 256) {
+    const int r = e / RBC_C, cl = e - r * RBC_C;
+    const int j = j0 + r, c = c0 + cl;
+    if (j < Wi && c < C) gxT[((long long)n * Hi * Wi + (long long)i * Wi + j) * C + c] = tile[r][cl];
+  }
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -178,6 +238,16 @@ int e2ep_resize_fwd(const float *x, int N, int C, long long x_nstride, int Hi, i
   hipLaunchKernelGGL(k_resize_fwd, dim3(cdiv(Ho * Wo, 256), N * C), dim3(256), 0, as_stream(stream),
                      x, C, x_nstride, Hi, Wi, Ho, Wo, scale_h, scale_w, y, y_nstride);
   return launch_status("e2ep_resize_fwd");
+}
+
+int e2ep_resize_bwd_cl(const float *g, long long g_pstride, int N, int C, int Hi, int Wi, int Ho,
+                       int Wo, float scale_h, float scale_w, float *gxT, void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && Hi <= 65535 &&
+                   (long long)N * cdiv(C, RBC_C) <= 65535 && scale_h >= 0.5f && scale_w >= 0.5f,
+               E2EP_EINVAL, "e2ep_resize_bwd_cl: bad shape or scale < 0.5");
+  hipLaunchKernelGGL(k_resize_bwd_2d_cl, dim3(cdiv(Wi, RB_TW), Hi, N * cdiv(C, RBC_C)), dim3(256),
+                     0, as_stream(stream), g, g_pstride, C, Ho, Wo, Hi, Wi, scale_h, scale_w, gxT);
+  return launch_status("e2ep_resize_bwd_cl");
 }
 
 size_t e2ep_resize_bwd_workspace(int planes, int Ho, int Wi) {

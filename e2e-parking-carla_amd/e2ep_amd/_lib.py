@@ -53,6 +53,7 @@ SIGNATURES = {
     "e2ep_resize_fwd": (_i, [_p, _i, _i, _i64, _i, _i, _i, _i, _f, _f, _p, _i64, _p]),
     "e2ep_resize_bwd_workspace": (_sz, [_i, _i, _i]),
     "e2ep_resize_bwd": (_i, [_p, _i64, _i, _i, _i, _i, _i, _f, _f, _p, _i, _p, _p]),
+    "e2ep_resize_bwd_cl": (_i, [_p, _i64, _i, _i, _i, _i, _i, _i, _f, _f, _p, _p]),
     "e2ep_dwconv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p]),
     "e2ep_dwconv_dgrad": (_i, [_p, _p, _p, _p, _p]),
     "e2ep_dwconv_wgrad_workspace": (_sz, [_p]),

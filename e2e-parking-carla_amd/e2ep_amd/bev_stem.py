@@ -4,8 +4,9 @@ the target-point plane, then conv7x7/2 (65->64) — reference model/bev_encoder.
 Forward writes the two resizes straight into one (B, 65, 256, 256) buffer (no torch.cat of
 the target channel, reference model/parking_model.py:45).  Backward computes the data
 gradient for the 64 feature channels only (the target plane is a constant), resizes it
-back to 200x200 with the deterministic gather, and the weight gradient with the split-K
-kernel."""
+back to 200x200 with the deterministic gather straight into a channels-last (pillar-major)
+tensor — the lift-splat backward reads it without a transpose — and the weight gradient
+with the split-K kernel."""
 import torch
 
 from . import _lib, conv, timing
@@ -48,11 +49,13 @@ class _BevStem(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dres = conv.conv_dgrad(gy, wt, dims, C,
                                    torch.empty(B, C, H, W, dtype=torch.float32, device=gy.device), w_layout=1)
-            dbev = torch.empty(B, C, X, Y, dtype=torch.float32, device=gy.device)
-            ws = torch.empty(B * C * H * Y, dtype=torch.float32, device=gy.device)
+            # channels-last (pillar-major [B][X*Y][C]): the layout the lift-splat backward
+            # gathers rows of, so it needs no transpose of the BEV gradient
+            dbev = torch.empty(B, C, X, Y, dtype=torch.float32, device=gy.device,
+                               memory_format=torch.channels_last)
             with timing.region("resize_bwd"):
-                _lib.call("e2ep_resize_bwd", _lib.ptr(dres), H * W, B * C, X, Y, H, W, sh, sw,
-                          _lib.ptr(dbev), 0, _lib.ptr(ws), s)
+                _lib.call("e2ep_resize_bwd_cl", _lib.ptr(dres), H * W, B, C, X, Y, H, W, sh, sw,
+                          _lib.ptr(dbev), s)
         if ctx.needs_input_grad[2]:
             dw = conv.conv_wgrad(gy, x, dims, torch.empty_like(w))
         return dbev, None, dw, None

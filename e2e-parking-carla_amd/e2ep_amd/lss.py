@@ -125,8 +125,11 @@ class _LiftSplat(torch.autograd.Function):
         prob, featT = ctx.saved_tensors
         p, C = ctx.plan, ctx.C
         hw = p.h * p.w
-        gout = gout.contiguous()
-        gT = transpose(gout, C, p.XYZ, p.B, in_bstride=gout.shape[1] * p.XYZ)  # (B, XYZ, C)
+        if gout.shape[1] == C and gout.is_contiguous(memory_format=torch.channels_last):
+            gT = gout  # pillar-major already (the BEV stem's resize backward writes it so)
+        else:
+            gout = gout.contiguous()
+            gT = transpose(gout, C, p.XYZ, p.B, in_bstride=gout.shape[1] * p.XYZ)  # (B, XYZ, C)
         gp = torch.empty_like(prob)
         gf = torch.empty(p.B * p.N, C, p.h, p.w, dtype=torch.float32, device=gout.device)
         with timing.region("lss_bwd"):

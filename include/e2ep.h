@@ -338,6 +338,12 @@ size_t e2ep_resize_bwd_workspace(int planes, int Ho, int Wi);
 int e2ep_resize_bwd(const float *g, long long g_pstride, int planes, int Hi, int Wi, int Ho,
                     int Wo, float scale_h, float scale_w, float *gx, int accumulate,
                     void *workspace, void *stream);
+/* Backward for scale_h, scale_w >= 0.5 (up to 2x upsampling) written channels-last:
+ * gxT[n][i * Wi + j][c] from the NCHW gradient g (plane (n, c) at g + (n*C + c)*g_pstride).
+ * The BEV encoder stem's 200 -> 256 resize (model/bev_encoder.py:24) hands the lift-splat
+ * backward (tool/geometry.py:307-317, e2ep_lss_bwd) its pillar-major BEV gradient directly. */
+int e2ep_resize_bwd_cl(const float *g, long long g_pstride, int N, int C, int Hi, int Wi, int Ho,
+                       int Wo, float scale_h, float scale_w, float *gxT, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Depthwise conv (EfficientNet MBConv _depthwise_conv; k 3 or 5, stride 1 or 2, static
@@ -448,9 +454,9 @@ int e2ep_depth_bce_bwd(const float *prob, const int *cls, const float *den, cons
  * need e2ep_gemm_workspace(M, N, K) bytes of workspace (0 when no split).
  * ------------------------------------------------------------------------------------- */
 size_t e2ep_gemm_workspace(int M, int N, int K);
-/* Benchmarking override of the launch plan: block tile (64 tm) x (64 tn), tm, tn in {1, 2},
- * and the K split (tm = tn = 0: the automatic plan). */
-int e2ep_gemm_force(int tm, int tn, int splits);
+/* Benchmarking override of the launch plan: block tile 1 = 64x64, 2 = 32x128, 3 = 128x128,
+ * 4 = 64x128, 5 = 128x64, 6 = 64x256 (0 = the automatic plan), and the K split. */
+int e2ep_gemm_force(int tile, int splits, int unused);
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
               int K, int relu, void *workspace, void *stream);

@@ -53,15 +53,44 @@ def torch_fn(A, ak, B, bk):
 
 
 def timed(fn, iters=50):
-    for _ in range(5):
-        fn()
+    """GPU time per launch (us): `iters` launches captured into one HIP graph, replayed
+    between two events — no host dispatch gaps (eager back-to-back launches of these small
+    GEMMs are host-bound at ~12 us)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(iters):
-        fn()
+    g.replay()
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+TILES = {1: "64x64", 2: "32x128", 3: "128x128", 4: "64x128", 5: "128x64", 6: "64x256"}
+
+
+def sweep(fn):
+    """Every (tile, split) plan for one shape: best six as [[us, tile, splits] ...]."""
+    from e2ep_amd import _lib
+    best = []
+    for tile in TILES:
+        for sp in (1, 2, 3, 4, 6, 8):
+            _lib.call("e2ep_gemm_force", tile, sp, 0)
+            best.append((timed(fn, 20), tile, sp))
+    _lib.call("e2ep_gemm_force", 0, 0, 0)
+    best.sort()
+    print("    best:", " ".join(f"{TILES[t]}/s{sp}:{us:.1f}" for us, t, sp in best[:6]), flush=True)
+    return [[round(us, 1), t, sp] for us, t, sp in best[:6]]
 
 
 def main():
@@ -81,6 +110,8 @@ def main():
             fl = 2.0 * M * N * K
             print(f"{name:16s} {M:6d} {N:7d} {K:7d}  e2ep {te:7.1f} us {fl / te / 1e6:6.1f} TF/s  "
                   f"torch {tt:7.1f}  conv kernel {conv_us:7.1f}", flush=True)
+            if args.sweep:
+                sweep(lambda: nn_ops.gemm(A, ak, B, bk, M, N, K, out=out))
         return
     from e2ep_amd import nn_ops
     rows = []
@@ -99,17 +130,7 @@ def main():
         tot_e += cnt * te
         tot_t += cnt * tt
         if args.sweep:
-            from e2ep_amd import _lib
-            best = []
-            for tm, tn in ((1, 1), (1, 2), (2, 1), (2, 2)):
-                for sp in (1, 2, 3, 4, 6, 8):
-                    _lib.call("e2ep_gemm_force", tm, tn, sp)
-                    t = timed(lambda: nn_ops.gemm(A, ak, B, bk, M, N, K, out=out), 20)
-                    best.append((t, tm, tn, sp))
-            _lib.call("e2ep_gemm_force", 0, 0, 0)
-            best.sort()
-            rows[-1]["sweep"] = [[round(t, 1), tm, tn, sp] for t, tm, tn, sp in best[:6]]
-            print("    best:", " ".join(f"{64*tm}x{64*tn}/s{sp}:{t:.1f}" for t, tm, tn, sp in best[:6]), flush=True)
+            rows[-1]["sweep"] = sweep(lambda: nn_ops.gemm(A, ak, B, bk, M, N, K, out=out))
         print(f"{name:24s} {M:5d} {N:5d} {K:5d}  {te:8.1f} {fl / te / 1e6:6.1f}  {tt:8.1f} {fl / tt / 1e6:6.1f}",
               flush=True)
     res = {"rows": rows, "per_step_ms": {"e2ep": round(tot_e / 1e3, 3), "torch": round(tot_t / 1e3, 3)}}

@@ -38,6 +38,29 @@ def test_gemm_layouts_vs_fp64(M, N, K, ak, bk):
     assert torch.equal(out, again)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
+def test_gemm_every_tile_and_split(tile, ak, bk):
+    """Each block tile (e2ep_gemm_force) with and without a K split, ragged M / N / K, plus
+    the bias + residual + ReLU epilogue (written directly, or by the split reduction)."""
+    from e2ep_amd import _lib, nn_ops
+    M, N, K = 197, 301, 333
+    g = torch.Generator().manual_seed(tile * 10 + 2 * ak + bk)
+    A, B, ref = _operands(M, N, K, ak, bk, g)
+    bias, cadd = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    want = (ref + bias.double() + cadd.double()).clamp_min(0)
+    try:
+        for splits in (1, 3):
+            _lib.call("e2ep_gemm_force", tile, splits, 0)
+            out = nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K)
+            assert rel_l2(out, ref) < 2e-6, (tile, splits)
+            out = nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K, bias=bias.to(DEV),
+                              cadd=cadd.to(DEV), relu=True)
+            assert rel_l2(out, want) < 2e-6, (tile, splits)
+    finally:
+        _lib.call("e2ep_gemm_force", 0, 0, 0)
+
+
 @pytest.mark.parametrize("M,N,K", [(2048, 258, 258), (112, 204, 258), (37, 70, 2048)])
 def test_gemm_epilogue_bias_add_relu(M, N, K):
     from e2ep_amd import nn_ops

@@ -241,6 +241,46 @@ def test_bev_stem_resize_conv_fused():
     assert rel_l2(wd.grad, w64.grad) < 2e-5
 
 
+@pytest.mark.parametrize("N,C,Hi,Wi,Ho,Wo", [(2, 64, 200, 200, 256, 256), (3, 70, 37, 45, 50, 61),
+                                             (1, 5, 9, 33, 9, 40)])
+def test_resize_bwd_channels_last_equals_nchw(N, C, Hi, Wi, Ho, Wo):
+    """e2ep_resize_bwd_cl (pillar-major output for the lift-splat backward) is bit-equal to the
+    NCHW gather backward, transposed to channels-last."""
+    from e2ep_amd import _lib
+    g = torch.randn(N, C, Ho, Wo, generator=_g(C + Wi)).to(DEV)
+    sh, sw = Hi / Ho, Wi / Wo
+    ref = torch.empty(N, C, Hi, Wi, device=DEV)
+    ws = torch.empty(N * C * Ho * Wi, device=DEV)
+    _lib.call("e2ep_resize_bwd", _lib.ptr(g), Ho * Wo, N * C, Hi, Wi, Ho, Wo, sh, sw,
+              _lib.ptr(ref), 0, _lib.ptr(ws), _lib.stream())
+    out = torch.empty(N, C, Hi, Wi, device=DEV, memory_format=torch.channels_last)
+    _lib.call("e2ep_resize_bwd_cl", _lib.ptr(g), Ho * Wo, N, C, Hi, Wi, Ho, Wo, sh, sw,
+              _lib.ptr(out), _lib.stream())
+    assert torch.equal(out, ref)
+
+
+def test_lift_splat_bwd_takes_channels_last_gradient():
+    """The lift-splat backward fed a channels-last BEV gradient (no transpose) returns exactly
+    the gradients it returns for the same gradient in NCHW."""
+    from e2ep_amd import lss, synthetic
+    from model.bev_model import BevModel
+    from tool.config import default_cfg
+    bm = BevModel(default_cfg()).to(DEV)
+    K, E = synthetic.rig(4, 256)
+    plan = bm.plan(K.unsqueeze(0).expand(2, *K.shape).contiguous(),
+                   E.unsqueeze(0).expand(2, *E.shape).contiguous(), DEV)
+    gen = _g(5)
+    prob = torch.rand(8, plan.D, plan.h, plan.w, generator=gen).softmax(1).to(DEV)
+    feat = torch.randn(8, 64, plan.h, plan.w, generator=gen).to(DEV)
+    gbev = torch.randn(2, 64, plan.X, plan.Y, generator=gen).to(DEV)
+    grads = []
+    for gb in (gbev.contiguous(), gbev.contiguous(memory_format=torch.channels_last)):
+        p, f = prob.clone().requires_grad_(True), feat.clone().requires_grad_(True)
+        lss.lift_splat(p, f, plan).backward(gb)
+        grads.append((p.grad, f.grad))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
 @pytest.mark.parametrize("shape", [(8, 96, 16, 16, 6), (4, 40, 9, 7, 10), (32, 672, 16, 16, 28),
                                    (32, 1632, 8, 8, 68), (5, 300, 3, 3, 75), (2, 4096, 2, 2, 256)])
 def test_squeeze_excite_fused(shape):
