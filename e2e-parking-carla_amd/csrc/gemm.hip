@@ -16,14 +16,12 @@
 //  * global loads are raw buffer loads with out-of-range offsets for the M / N / K edges
 //    (returns 0: no padding copies, K = 258 needs no special case); the next step's tile is
 //    loaded into registers while the current one feeds the MFMAs;
-//  * small grids split K (the last block of a tile sums the slabs in split order, splitk.h,
-//    so results are deterministic run to run), large ones write C directly with the fused
-//    epilogue.
+//  * small grids split K (fixed-order reduction in k_gemm_reduce, so results are
+//    deterministic run to run), large ones write C directly with the fused epilogue.
 #include <algorithm>
 
 #include "common.h"
 #include "gemm.h"
-#include "splitk.h"
 
 namespace e2ep {
 
@@ -46,7 +44,6 @@ __device__ __forceinline__ float kmask(float v, bool ok) {
 }
 constexpr int G_BK = 32;
 constexpr int G_LDW = 36;  // LDS row stride in floats (32 k + 4 pad)
-constexpr int G_MAXSPLIT = 8;  // K splits at most (gemm_plan)
 
 template <bool AK, bool BKC, int WM, int TM, int TN>
 __global__ void __launch_bounds__(256)
@@ -54,7 +51,7 @@ __global__ void __launch_bounds__(256)
            const float *__restrict__ B, int ldb, long long b_bytes, int bvec,
            const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
            int ldadd, float *__restrict__ C, long long c_bytes, int ldc, GemmCols cols, int M,
-           int N, int K, int kper, int relu, float *__restrict__ part, unsigned *counters) {
+           int N, int K, int kper, int relu) {
   constexpr int WN = 4 / WM;                      // waves along N
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
   constexpr int GA = BM / 32, GB = BN / 32;       // 32-row load groups per operand tile
@@ -199,23 +196,16 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       load_tiles(ra, rb, kbeg + kt + 1);  // past the range: re-read, never stored
-      // keep the next step's loads ahead of this step's MFMAs (left alone, the scheduler
-      // sinks the B loads below the MFMAs and their latency is exposed every K-step)
-      __builtin_amdgcn_sched_barrier(0);
       compute(kt & 1);
-      __builtin_amdgcn_sched_barrier(0);
-      // unconditional (after the last step it fills the idle buffer with a re-read tile):
-      // a conditional store lets the compiler sink the loads into its branch, after the MFMAs
-      store_tiles(ra, rb, (kt + 1) & 1, min(kbeg + kt + 1, kend - 1));
+      if (kt + 1 < nk) store_tiles(ra, rb, (kt + 1) & 1, kbeg + kt + 1);
       __syncthreads();
     }
   }
 
   // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-  // gridDim.z > 1: raw partial sums into part[split][M][N] (dense, unbatched); the tile's
-  // last-arriving block then sums the slabs and applies the epilogue (splitk.h).
+  // gridDim.z > 1: raw partial sums into C = workspace[split][M][N] (dense, unbatched).
   const bool final_ = gridDim.z == 1;
-  float *dst = final_ ? C : part + (long long)split * M * N;
+  float *dst = final_ ? C : C + (long long)split * M * N;
   const int ldd = final_ ? ldc : N;
   const bool batched = final_ && cols.hw > 0;
   // edges: buffer stores with out-of-range offsets are dropped; the epilogue's optional
@@ -248,53 +238,48 @@ __global__ void __launch_bounds__(256)
         if (add_b) v += bias_rows ? bias[min(m, M - 1)] : bn_;
         if (add_c) v += cv[r];
         if (final_ && relu) v = fmaxf(v, 0.f);
-        const int o = (nok && m < M) ? (int)((cbase + (long long)m * ldd) * 4) : OOR;
-        if (final_) bstore(rd, o, v);
-        else store_sys(rd, o, v);
+        bstore(rd, (nok && m < M) ? (int)((cbase + (long long)m * ldd) * 4) : OOR, v);
       }
     }
   }
-  if (final_ || !splitk_last(counters + blockIdx.y * gridDim.x + blockIdx.x, gridDim.z)) return;
-  // last block of the tile: C = sum over splits in order (+ bias) (+ Cadd) (ReLU).  The
-  // slabs are read 16 elements per thread at a time with every split's loads issued before
-  // any is summed (one memory latency per chunk, not one per split).
-  constexpr int EPT = BM * BN / 256, CH = EPT < 16 ? EPT : 16;
+}
+
+// C[m][n] = sum over splits in order (+ bias) (+ Cadd) (ReLU).  V = 4: four consecutive
+// elements per thread with 16-byte loads / stores (plain dense C, column bias, M*N % 4 == 0);
+// V = 1 handles column-batched C (Cadd in C's layout) and row bias.
+template <int V>
+__global__ void __launch_bounds__(256)
+    k_gemm_reduce(const float *__restrict__ part, int splits, int M, int N,
+                  const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
+                  int ldadd, float *__restrict__ C, int ldc, GemmCols cols, int relu) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * V;
   const long long MN = (long long)M * N;
-  const int S = gridDim.z;
-  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * S * MN);
-  const bool bc = cols.hw > 0;
-  for (int jc = 0; jc < EPT; jc += CH) {
-    int off[CH];
-    float x[G_MAXSPLIT][CH];
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      const int e = tid + 256 * (jc + j);
-      const int m = m0 + e / BN, n = n0 + e % BN;
-      off[j] = (m < M && n < N) ? (int)(((long long)m * N + n) * 4) : OOR;
+  if (i >= MN) return;
+  float s[V];
+  if (V == 4) {
+    float4 a = *reinterpret_cast<const float4 *>(part + i);
+    s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
+    for (int k = 1; k < splits; ++k) {
+      a = *reinterpret_cast<const float4 *>(part + k * MN + i);
+      s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
     }
-#pragma unroll
-    for (int k = 0; k < G_MAXSPLIT; ++k)
-#pragma unroll
-      for (int j = 0; j < CH; ++j)
-        x[k][j] = load_sys(rp, (k < S && off[j] != OOR) ? off[j] + (int)(4LL * k * MN) : OOR);
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      float v = x[0][j];
-#pragma unroll
-      for (int k = 1; k < G_MAXSPLIT; ++k)
-        if (k < S) v += x[k][j];
-      const int e = tid + 256 * (jc + j);
-      const int m = m0 + e / BN, n = n0 + e % BN;
-      if (m >= M || n >= N) continue;
-      const long long o = bc ? (long long)(n / cols.hw) * cols.c_img + n % cols.hw +
-                                   (long long)m * ldc
-                             : (long long)m * ldc + n;
-      if (bias) v += bias[bias_rows ? m : n];
-      if (Cadd) v += Cadd[bc ? o : (long long)m * ldadd + n];
-      if (relu) v = fmaxf(v, 0.f);
-      C[o] = v;
-    }
+  } else {
+    s[0] = part[i];
+    for (int k = 1; k < splits; ++k) s[0] += part[k * MN + i];
   }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const long long e = i + v;
+    const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+    const long long off = cols.hw ? (long long)(n / cols.hw) * cols.c_img + n % cols.hw +
+                                        (long long)m * ldc
+                                  : (long long)m * ldc + n;
+    if (bias) s[v] += bias[bias_rows ? m : n];
+    if (Cadd) s[v] += Cadd[cols.hw ? off : (long long)m * ldadd + n];
+    if (relu) s[v] = fmaxf(s[v], 0.f);
+    if (V == 1) C[off] = s[v];
+  }
+  if (V == 4) *reinterpret_cast<float4 *>(C + i) = make_float4(s[0], s[1], s[2], s[3]);
 }
 
 struct GemmLaunch {
@@ -305,6 +290,8 @@ struct GemmLaunch {
 //   1: 64 x 64 (2 x 2 waves, 32 x 32)     2: 32 x 128 (1 x 4, 32 x 32)
 //   3: 128 x 128 (2 x 2, 64 x 64)         4: 64 x 128 (2 x 2, 32 x 64)
 //   5: 128 x 64 (2 x 2, 64 x 32)          6: 64 x 256 (1 x 4, 64 x 64)
+// (the larger tiles measured no faster on the C2 shapes, scripts/bench_gemm.py --sweep:
+// profiles/r02/gemm_sweep_tiles.json; they stay selectable for other shapes)
 struct GemmTile {
   int bm, bn;
 };
@@ -323,21 +310,18 @@ static GemmTile tile_dims(int tile) {
 // a multiple of 64 and 32-row tiles pad it less (M = 32, 112, 144, 160, 336 ...); K split
 // toward ~768 workgroups (3 per CU), at most 8 ways and >= 8 K-steps each.
 static int g_force_tile = 0, g_force_splits = 0;  // 0: automatic
-E2EP_TILE_POOL(g_gemm_tiles);
-static unsigned *g_gemm_pool = nullptr;
-static unsigned g_gemm_next = 0;
 
 static GemmLaunch gemm_plan(int M, int N, int K) {
   GemmLaunch p{1, 1, 1};
   const int ksteps = cdiv(K, G_BK);
   if (g_force_tile > 0) {  // benchmarking override (e2ep_gemm_force)
     p.tile = g_force_tile;
-    p.splits = std::max(1, std::min({g_force_splits, ksteps, G_MAXSPLIT}));
+    p.splits = std::max(1, std::min(g_force_splits, ksteps));
   } else {
     if (cdiv(M, 32) * 32 < cdiv(M, 64) * 64) p.tile = 2;
     const GemmTile t = tile_dims(p.tile);
     const long long blocks = (long long)cdiv(M, t.bm) * cdiv(N, t.bn);
-    const int cap = std::min(G_MAXSPLIT, std::max(1, ksteps / 8));
+    const int cap = std::min(8, std::max(1, ksteps / 8));
     p.splits = (int)std::min<long long>(cap, std::max(1LL, (long long)cdiv(768, blocks)));
   }
   p.kper = cdiv(ksteps, p.splits);
@@ -370,25 +354,15 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
     set_error("gemm: workspace of e2ep_gemm_workspace() bytes required");
     return E2EP_EINVAL;
   }
-  float *part = p.splits > 1 ? static_cast<float *>(workspace) : nullptr;
+  float *out = p.splits > 1 ? static_cast<float *>(workspace) : C;
   const GemmTile td = tile_dims(p.tile);
   dim3 grid(cdiv(N, td.bn), cdiv(M, td.bm), p.splits);
   const int avec = vec_of(ak, lda, A), bvec = vec_of(bk, ldb, B);
   const int br = bias_rows ? 1 : 0;
-  unsigned *counters = nullptr;
-  if (p.splits > 1) {
-    const unsigned tiles = grid.x * grid.y;
-    if (tiles > TILE_POOL || 4LL * p.splits * M * N >= 0x7fffffffLL ||
-        !pool_ptr(HIP_SYMBOL(g_gemm_tiles), g_gemm_pool)) {
-      set_error("gemm: split-K tile counters unavailable (%u tiles)", tiles);
-      return E2EP_EINVAL;
-    }
-    counters = g_gemm_pool + tile_range(g_gemm_next, tiles);
-  }
 #define E2EP_GEMM_LAUNCH(AKV, BKV, WMV, TMV, TNV)                                               \
   hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, TMV, TNV>), grid, dim3(256), 0, s, A, lda, a_bytes, \
-                     avec, B, ldb, b_bytes, bvec, bias, br, Cadd, ldadd, C, c_bytes, ldc, cols, \
-                     M, N, K, p.kper, relu, part, counters)
+                     avec, B, ldb, b_bytes, bvec, bias, br, Cadd, ldadd, out, c_bytes, ldc, cols, \
+                     M, N, K, p.kper, relu)
 #define E2EP_GEMM_T(AKV, BKV)                                     \
   do {                                                            \
     switch (p.tile) {                                             \
@@ -406,6 +380,19 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
   else E2EP_GEMM_T(false, false);
 #undef E2EP_GEMM_T
 #undef E2EP_GEMM_LAUNCH
+  if (p.splits > 1) {
+    const long long MN = (long long)M * N;
+    const bool v4 = MN % 4 == 0 && ldc == N && cols.hw == 0 && !bias_rows &&
+                    (!Cadd || ldadd == N) && ((uintptr_t)C & 15) == 0;
+    if (v4)
+      hipLaunchKernelGGL(k_gemm_reduce<4>, dim3(cdiv(MN / 4, 256)), dim3(256), 0, s,
+                         static_cast<const float *>(workspace), p.splits, M, N, bias, br, Cadd,
+                         ldadd, C, ldc, cols, relu);
+    else
+      hipLaunchKernelGGL(k_gemm_reduce<1>, dim3(cdiv(MN, 256)), dim3(256), 0, s,
+                         static_cast<const float *>(workspace), p.splits, M, N, bias, br, Cadd,
+                         ldadd, C, ldc, cols, relu);
+  }
   return 0;
 }
 
