@@ -39,6 +39,11 @@ constexpr float LOG2E = 1.4426950408889634f;
 #define E2EP_ATT_KG 4
 #endif
 constexpr int FWD_KG = E2EP_ATT_KG;  // keys per online-softmax rescale in the forward
+#ifndef E2EP_ATT_LONG_LANES
+#define E2EP_ATT_LONG_LANES 1
+#endif
+// lanes per query (forward, dq) / per key (dk, dv) for sequences longer than 16 (encoder)
+constexpr int ATT_LONG_LANES = E2EP_ATT_LONG_LANES;
 
 // 2^x on the hardware v_exp_f32 (arguments here are <= 0 or -inf; tiny results flush to 0)
 __device__ __forceinline__ float att_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -508,9 +513,9 @@ int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, 
   hipLaunchKernelGGL((k_attn_fwd<DHP, LPQ>), dim3(cdiv(Sq, 64 / LPQ), B * H), blk, 0, st, q, k, v, \
                      key_pad, seed, a, o, lse)
   if (dh <= 44) {
-    if (Sq <= 16) E2EP_ATT_FWD(44, 4); else E2EP_ATT_FWD(44, 1);
+    if (Sq <= 16) E2EP_ATT_FWD(44, 4); else E2EP_ATT_FWD(44, ATT_LONG_LANES);
   } else {
-    if (Sq <= 16) E2EP_ATT_FWD(64, 4); else E2EP_ATT_FWD(64, 1);
+    if (Sq <= 16) E2EP_ATT_FWD(64, 4); else E2EP_ATT_FWD(64, ATT_LONG_LANES);
   }
 #undef E2EP_ATT_FWD
   return launch_status("e2ep_attn_fwd");
@@ -536,11 +541,11 @@ int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o
   hipLaunchKernelGGL((k_attn_bwd_kv<DHP, LPK>), dim3(cdiv(Sk, 64 / LPK), B * H), blk, 0, s, q, k, \
                      v, dout, lse, D, key_pad, seed, a, dk, dv)
   if (dh <= 44) {
-    if (Sq <= 16) E2EP_ATT_BQ(44, 4); else E2EP_ATT_BQ(44, 1);
-    if (Sk <= 16) E2EP_ATT_BKV(44, 4); else E2EP_ATT_BKV(44, 1);
+    if (Sq <= 16) E2EP_ATT_BQ(44, 4); else E2EP_ATT_BQ(44, ATT_LONG_LANES);
+    if (Sk <= 16) E2EP_ATT_BKV(44, 4); else E2EP_ATT_BKV(44, ATT_LONG_LANES);
   } else {
-    if (Sq <= 16) E2EP_ATT_BQ(64, 4); else E2EP_ATT_BQ(64, 1);
-    if (Sk <= 16) E2EP_ATT_BKV(64, 4); else E2EP_ATT_BKV(64, 1);
+    if (Sq <= 16) E2EP_ATT_BQ(64, 4); else E2EP_ATT_BQ(64, ATT_LONG_LANES);
+    if (Sk <= 16) E2EP_ATT_BKV(64, 4); else E2EP_ATT_BKV(64, ATT_LONG_LANES);
   }
 #undef E2EP_ATT_BQ
 #undef E2EP_ATT_BKV

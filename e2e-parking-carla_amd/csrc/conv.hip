@@ -674,6 +674,7 @@ struct TapList {
   int tap[MAXTAPS];
 };
 
+template <int OP>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
     const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
     ConvGeom g, int pix_per_split, TapList tl) {
@@ -758,12 +759,24 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   f32x16 acc = {0};
   const int nk = (pend - pbeg + BK - 1) / BK;
   const int li = lane & 31, lk = lane >> 5;
+  // OP 1 (bf16 mode, BASELINE C3): one 32x32x16 bf16 MFMA per 16-pixel K-step, lane half h
+  // taking pixels 8h .. 8h+7 (eight LDS reads per operand, as the eight fp32 MFMAs do)
   auto compute = [&](int buf) {
+    if (OP == 0) {
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float a = As[buf][kk + lk][32 * wm + li];
-      const float b = Bs[buf][kk + lk][32 * wn + li];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      for (int kk = 0; kk < BK; kk += 2) {
+        const float a = As[buf][kk + lk][32 * wm + li];
+        const float b = Bs[buf][kk + lk][32 * wn + li];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      }
+    } else {
+      bf16x8 a, b;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] = (__bf16)As[buf][8 * lk + j][32 * wm + li];
+        b[j] = (__bf16)Bs[buf][8 * lk + j][32 * wn + li];
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
     }
   };
   // unconditional loads (past the range they read zeros): exact s_waitcnt, see k_conv_gemm
@@ -851,7 +864,7 @@ static int wgrad1x1_splits(const ConvGeom &g) {
   return wgrad1x1_splits_for(g, to, tc);
 }
 
-template <int TI, int TJ>
+template <int TI, int TJ, int OP>
 __global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gout,
                                                    const float *__restrict__ x,
                                                    float *__restrict__ part, ConvGeom g,
@@ -894,18 +907,37 @@ __global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gou
         b[u][j] = bload4(rx, (ok && ci < g.Cin) ? (((n * g.Cin + ci) * PQ) + p) * 4 : OOR);
       }
     }
+    if (OP == 0) {
 #pragma unroll
-    for (int u = 0; u < W1_GROUPS; ++u)
+      for (int u = 0; u < W1_GROUPS; ++u)
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-          f32x16 &c = acc[i * TJ + j];
-          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].x, b[u][j].x, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].y, b[u][j].y, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].z, b[u][j].z, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].w, b[u][j].w, c, 0, 0, 0);
-        }
+          for (int j = 0; j < TJ; ++j) {
+            f32x16 &c = acc[i * TJ + j];
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].x, b[u][j].x, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].y, b[u][j].y, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].z, b[u][j].z, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][i].w, b[u][j].w, c, 0, 0, 0);
+          }
+    } else {
+      // bf16 mode: groups u, u+1 (16 pixels) feed one 32x32x16 MFMA; lane half h holds
+      // pixels 4h..4h+3 of each group, identically for both operands
+#pragma unroll
+      for (int u = 0; u < W1_GROUPS; u += 2)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            const bf16x8 av = {(__bf16)a[u][i].x, (__bf16)a[u][i].y, (__bf16)a[u][i].z,
+                               (__bf16)a[u][i].w, (__bf16)a[u + 1][i].x, (__bf16)a[u + 1][i].y,
+                               (__bf16)a[u + 1][i].z, (__bf16)a[u + 1][i].w};
+            const bf16x8 bv = {(__bf16)b[u][j].x, (__bf16)b[u][j].y, (__bf16)b[u][j].z,
+                               (__bf16)b[u][j].w, (__bf16)b[u + 1][j].x, (__bf16)b[u + 1][j].y,
+                               (__bf16)b[u + 1][j].z, (__bf16)b[u + 1][j].w};
+            acc[i * TJ + j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[i * TJ + j], 0, 0, 0);
+          }
+    }
   }
   // the four waves' tiles are summed in wave order through one LDS tile
   for (int w = 0; w < 4; ++w) {
@@ -1536,8 +1568,15 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
     int to, tc;
     wgrad1x1_tiles(g, to, tc);
     const dim3 grid(cdiv(g.Cout, to) * cdiv(g.Cin, tc), used);
-#define W1_LAUNCH(TI, TJ) \
-  hipLaunchKernelGGL((k_wgrad_1x1<TI, TJ>), grid, dim3(256), 0, s, gout, x, part, g, used, gps)
+#define W1_LAUNCH(TI, TJ)                                                                      \
+  do {                                                                                         \
+    if (g_conv_precision == 1)                                                                 \
+      hipLaunchKernelGGL((k_wgrad_1x1<TI, TJ, 1>), grid, dim3(256), 0, s, gout, x, part, g, used, \
+                         gps);                                                                 \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_wgrad_1x1<TI, TJ, 0>), grid, dim3(256), 0, s, gout, x, part, g, used, \
+                         gps);                                                                 \
+  } while (0)
     if (to == 64 && tc == 64) W1_LAUNCH(2, 2);
     else if (to == 64) W1_LAUNCH(2, 1);
     else if (tc == 64) W1_LAUNCH(1, 2);
@@ -1557,7 +1596,10 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
   float *part = static_cast<float *>(workspace);
   if (tl.n > 0) {
     dim3 grid(cdiv(g.Cin * tl.n, WBN), cdiv(g.Cout, BM), used);
-    hipLaunchKernelGGL(k_conv_wgrad, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+    if (g_conv_precision == 1)  // bf16 operands (C3), fp32 accumulate / gradient
+      hipLaunchKernelGGL(k_conv_wgrad<1>, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+    else
+      hipLaunchKernelGGL(k_conv_wgrad<0>, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
   }
   const int n = g.Cout * g.Cin * g.R * g.S;
   hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,

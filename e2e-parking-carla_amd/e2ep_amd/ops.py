@@ -2,9 +2,9 @@
 
 Model modules call these functions instead of torch.nn.functional; every one of them runs
 an e2ep HIP kernel from libe2ep_hip.so (include/e2ep.h) — there is no PyTorch or CPU
-fallback, and a missing library raises.  What still runs as PyTorch/hipBLASLt work is
-listed in DESIGN.md §4: the transformer layers' linear GEMMs (hipBLASLt), the token
-embedding, and small elementwise glue (concat, a few autograd accumulation adds).
+fallback, and a missing library raises.  What still runs as PyTorch work is listed in
+DESIGN.md §4: the token embedding and small elementwise glue (concat, a few autograd
+accumulation adds); every GEMM, including the transformer linears, is an e2ep kernel.
 """
 from . import conv as _conv
 from . import nn_ops

@@ -164,11 +164,12 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
  * e2ep_gemm.  Returns the previous value; a value outside 0..4 only queries.  Process-global; not thread-safe against concurrent
  * launches. */
 int e2ep_conv_gemm_variant(int variant);
-/* Operand precision of the forward / data-gradient conv GEMMs: 0 = fp32 (default; exact-f32
- * MFMA), 1 = bf16, 2 = fp16 (operands rounded to nearest-even, fp32 products and
- * accumulation, fp32 tensors in and out) — BASELINE configs C3 (bf16 forward, fp32
- * gradients: the weight gradients, every other op, the optimizer and the all-reduce stay
- * fp32) and C5 (fp16 inference).  Both GEMM generations take the setting; the direct tiny-K
+/* Operand precision of the conv GEMMs: 0 = fp32 (default; exact-f32 MFMA), 1 = bf16, 2 = fp16
+ * (operands rounded to nearest-even, fp32 products and accumulation, fp32 tensors in and
+ * out) — BASELINE configs C3 (bf16 forward / fp32 gradients, AMP-style: bf16 operands in the
+ * forward, data-gradient and weight-gradient GEMMs, gradients accumulated and stored fp32;
+ * every other op, the optimizer and the all-reduce stay fp32) and C5 (fp16 inference: forward
+ * and data-gradient GEMMs only).  Both GEMM generations take the setting; the direct tiny-K
  * stem conv and 1x1 convs on 1x1 maps (squeeze-excitation) stay fp32.
  * Returns the previous value; out-of-range values only query.  Process-global. */
 int e2ep_conv_precision(int precision);

@@ -150,6 +150,7 @@ LP_CASES = [
     (4, 24, 32, 32, 144, 1, 1, 1, (0, 0, 0, 0), 1),     # MBConv expand (1x1)
     (4, 160, 16, 16, 64, 3, 3, 1, (12, 12, 12, 12), 12),  # ASPP dilated
     (2, 64, 16, 16, 128, 3, 3, 2, (1, 1, 1, 1), 1),     # stride 2 (dgrad phases)
+    (8, 32, 128, 128, 48, 1, 1, 1, (0, 0, 0, 0), 1),    # 1x1, LDS-free weight gradient
 ]
 
 
@@ -177,8 +178,15 @@ def test_conv_low_precision_operands(case, mode, dt, loose):
     assert rel_l2(y, y_r) < 2e-6                  # operands rounded, fp32 accumulation
     assert rel_l2(xd.grad, xr.grad) < 2e-6        # data gradient: gy and W rounded
     assert rel_l2(y, y64) < loose                 # vs the exact fp32-operand result
-    # the weight gradient stays fp32 (exact-f32 MFMA) in every mode
-    x64 = x.double().requires_grad_(True)
-    w64 = w.double().requires_grad_(True)
-    F.conv2d(F.pad(x64, pad), w64, None, st, 0, dil).backward(gy.double())
-    assert rel_l2(wd.grad, w64.grad) < 2e-6
+    if mode == "bf16":
+        # C3 (bf16 forward / fp32 gradients, AMP-style): the weight-gradient GEMM takes bf16
+        # operands too (x and gy rounded), accumulates and stores fp32
+        wr = r(w).requires_grad_(True)
+        F.conv2d(F.pad(r(x), pad), wr, None, st, 0, dil).backward(r(gy))
+        assert rel_l2(wd.grad, wr.grad) < 5e-6
+    else:
+        # fp16 (inference mode C5): the weight gradient stays fp32 (exact-f32 MFMA)
+        x64 = x.double().requires_grad_(True)
+        w64 = w.double().requires_grad_(True)
+        F.conv2d(F.pad(x64, pad), w64, None, st, 0, dil).backward(gy.double())
+        assert rel_l2(wd.grad, w64.grad) < 2e-6
