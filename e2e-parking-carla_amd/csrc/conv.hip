@@ -674,12 +674,14 @@ struct TapList {
   int tap[MAXTAPS];
 };
 
-template <int OP>
+template <int OP, int KB>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
     const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
     ConvGeom g, int pix_per_split, TapList tl) {
-  __shared__ float As[2][BK][BM + PADA];   // As[pixel][co]
-  __shared__ float Bs[2][BK][WBN + PADB];  // Bs[pixel][col]
+  constexpr int TPR = 256 / KB;  // co / col rows per load pass
+  constexpr int NJ = 64 / TPR;   // loads per thread per operand per K-step
+  __shared__ float As[2][KB][BM + PADA];   // As[pixel][co]
+  __shared__ float Bs[2][KB][WBN + PADB];  // Bs[pixel][col]
   __shared__ int s_tap[MAXTAPS];
   if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
   __syncthreads();
@@ -699,16 +701,16 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   const int pend = min(Ptot, pbeg + pix_per_split);
   const int HW = g.H * g.W;
 
-  // thread -> pixel = tid & 15 (same pixel for its A and B loads), co / col rows = tid >> 4.
+  // thread -> pixel = tid % KB (same pixel for its A and B loads), co / col rows = tid / KB.
   // Guards are branch-free: an invalid element gets an offset >= the buffer size (reads 0);
   // per-column constants (channel plane + tap displacement) are folded once.
-  const int tp = tid & 15, trow = tid >> 4;
+  const int tp = tid % KB, trow = tid / KB;
   const int nrg = (int)min(4LL * g.N * g.Cout * PQ, 0x7fffffffLL);
   const int nrx = (int)min(4LL * g.N * g.Cin * HW, 0x7fffffffLL);
-  int cconst[4], cdy[4], cdx[4];
+  int cconst[NJ], cdy[NJ], cdx[NJ];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + trow + 16 * j;
+  for (int j = 0; j < NJ; ++j) {
+    const int col = n0 + trow + TPR * j;
     const int cc = col < Kl ? col : 0;
     const int ci = cc / tl.n, tap = s_tap[cc - ci * tl.n];
     const int r = tap / g.S, s = tap - r * g.S;
@@ -724,59 +726,62 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 
   const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
   const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
-  float ra0[4], rb0[4], ra1[4], rb1[4];  // two register sets: loads run two K-steps ahead
-  auto load_tiles = [&](float(&ra)[4], float(&rb)[4]) {
+  float ra0[NJ], rb0[NJ], ra1[NJ], rb1[NJ];  // two register sets: loads run two K-steps ahead
+  auto load_tiles = [&](float(&ra)[NJ], float(&rb)[NJ]) {
     const bool pok = p_cur < pend;
     const int oy = od / g.Q, ox = od - oy * g.Q;
     const int abase = pok ? (im * g.Cout * PQ + od + arow) * 4 : nrg;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int co = m0 + trow + 16 * j;
-      ra[j] = bload(rg, co < g.Cout ? abase + j * 16 * PQ * 4 : OOR);
+    for (int j = 0; j < NJ; ++j) {
+      const int co = m0 + trow + TPR * j;
+      ra[j] = bload(rg, co < g.Cout ? abase + j * TPR * PQ * 4 : OOR);
     }
     const int yb = oy * g.sh, xb0 = ox * g.sw;
     const int pbase = im * g.Cin * HW + yb * g.W + xb0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const bool ok = pok && (unsigned)(yb + cdy[j]) < (unsigned)g.H &&
                       (unsigned)(xb0 + cdx[j]) < (unsigned)g.W;
       rb[j] = bload(rx, ok ? (pbase + cconst[j]) * 4 : nrx);
     }
-    p_cur += BK;
-    od += BK;
+    p_cur += KB;
+    od += KB;
     while (od >= PQ) {
       od -= PQ;
       ++im;
     }
   };
-  auto store_tiles = [&](int buf, const float(&ra)[4], const float(&rb)[4]) {
+  auto store_tiles = [&](int buf, const float(&ra)[NJ], const float(&rb)[NJ]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) As[buf][tp][trow + 16 * j] = ra[j];
+    for (int j = 0; j < NJ; ++j) As[buf][tp][trow + TPR * j] = ra[j];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) Bs[buf][tp][trow + 16 * j] = rb[j];
+    for (int j = 0; j < NJ; ++j) Bs[buf][tp][trow + TPR * j] = rb[j];
   };
 
   f32x16 acc = {0};
-  const int nk = (pend - pbeg + BK - 1) / BK;
+  const int nk = (pend - pbeg + KB - 1) / KB;
   const int li = lane & 31, lk = lane >> 5;
-  // OP 1 (bf16 mode, BASELINE C3): one 32x32x16 bf16 MFMA per 16-pixel K-step, lane half h
-  // taking pixels 8h .. 8h+7 (eight LDS reads per operand, as the eight fp32 MFMAs do)
+  // OP 1 (bf16 mode, BASELINE C3): one 32x32x16 bf16 MFMA per 16 pixels, lane half h taking
+  // pixels 8h .. 8h+7 of them (eight LDS reads per operand, as the eight fp32 MFMAs do)
   auto compute = [&](int buf) {
     if (OP == 0) {
 #pragma unroll
-      for (int kk = 0; kk < BK; kk += 2) {
+      for (int kk = 0; kk < KB; kk += 2) {
         const float a = As[buf][kk + lk][32 * wm + li];
         const float b = Bs[buf][kk + lk][32 * wn + li];
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
       }
     } else {
-      bf16x8 a, b;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        a[j] = (__bf16)As[buf][8 * lk + j][32 * wm + li];
-        b[j] = (__bf16)Bs[buf][8 * lk + j][32 * wn + li];
+      for (int kb = 0; kb < KB; kb += 16) {
+        bf16x8 a, b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[j] = (__bf16)As[buf][kb + 8 * lk + j][32 * wm + li];
+          b[j] = (__bf16)Bs[buf][kb + 8 * lk + j][32 * wn + li];
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
       }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
     }
   };
   // unconditional loads (past the range they read zeros): exact s_waitcnt, see k_conv_gemm
@@ -1290,6 +1295,7 @@ static size_t gemm_workspace(const GemmPlan &p, int M) {
 
 // ---- second-generation GEMM plan (k_conv_gemm2) ------------------------------------------
 static int g_conv_precision = 0;  // GEMM operand precision: 0 fp32, 1 bf16, 2 fp16
+static int g_wgrad_kb = 16;       // k_conv_wgrad pixels per K-step (e2ep_conv_wgrad_kstep)
 static int g_gemm_variant = 0;  // 0 auto, 1 always k_conv_gemm, 2 k_conv_gemm2 wherever it
                                 // applies, 3 the same with 128-column tiles only, 4 auto with
                                 // the 1x1 forward / data gradient on the batched k_gemm
@@ -1493,6 +1499,12 @@ int e2ep_conv_precision(int precision) {
   return old;
 }
 
+int e2ep_conv_wgrad_kstep(int pixels) {
+  const int old = g_wgrad_kb;
+  if (pixels == 16 || pixels == 32) g_wgrad_kb = pixels;
+  return old;
+}
+
 int e2ep_conv_gemm_variant(int variant) {
   const int old = g_gemm_variant;
   if (variant >= 0 && variant <= 4) g_gemm_variant = variant;
@@ -1588,18 +1600,24 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
     return launch_status("e2ep_conv_wgrad");
   }
   const int Ptot = g.N * g.P * g.Q;
+  const int kb = g_wgrad_kb;
   int per = (Ptot + splits - 1) / splits;
-  per = (per + BK - 1) / BK * BK;
+  per = (per + kb - 1) / kb * kb;
   const int used = (Ptot + per - 1) / per;
   const TapList tl = live_taps(g);
   hipStream_t s = as_stream(stream);
   float *part = static_cast<float *>(workspace);
   if (tl.n > 0) {
     dim3 grid(cdiv(g.Cin * tl.n, WBN), cdiv(g.Cout, BM), used);
-    if (g_conv_precision == 1)  // bf16 operands (C3), fp32 accumulate / gradient
-      hipLaunchKernelGGL(k_conv_wgrad<1>, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
-    else
-      hipLaunchKernelGGL(k_conv_wgrad<0>, grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+#define WG_LAUNCH(OPV, KBV) \
+  hipLaunchKernelGGL((k_conv_wgrad<OPV, KBV>), grid, dim3(256), 0, s, gout, x, part, g, per, tl)
+    // bf16 operands in C3 (fp32 accumulate / gradient); pixel K-step 16 or 32
+    if (g_conv_precision == 1) {
+      if (kb == 32) WG_LAUNCH(1, 32); else WG_LAUNCH(1, 16);
+    } else {
+      if (kb == 32) WG_LAUNCH(0, 32); else WG_LAUNCH(0, 16);
+    }
+#undef WG_LAUNCH
   }
   const int n = g.Cout * g.Cin * g.R * g.S;
   hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,

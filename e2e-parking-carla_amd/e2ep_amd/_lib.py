@@ -37,6 +37,7 @@ SIGNATURES = {
     "e2ep_conv_dgrad_acc": (_i, [_p, _p, _p, _i, _i, _p, _p, _p, _p]),
     "e2ep_conv_gemm_variant": (_i, [_i]),
     "e2ep_conv_precision": (_i, [_i]),
+    "e2ep_conv_wgrad_kstep": (_i, [_i]),
     "e2ep_conv_wgrad_splits": (_i, [_p]),
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),
     "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _p, _i, _p]),

@@ -173,6 +173,9 @@ int e2ep_conv_gemm_variant(int variant);
  * stem conv and 1x1 convs on 1x1 maps (squeeze-excitation) stay fp32.
  * Returns the previous value; out-of-range values only query.  Process-global. */
 int e2ep_conv_precision(int precision);
+/* Pixels per K-step of the tiled weight-gradient kernel (benchmarking): 16 (default) or 32;
+ * returns the previous value, other values only query.  Process-global. */
+int e2ep_conv_wgrad_kstep(int pixels);
 int e2ep_conv_wgrad_splits(const int *dims);
 size_t e2ep_conv_wgrad_workspace(const int *dims, int splits);
 int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,

@@ -89,6 +89,27 @@ def test_conv_fwd_bwd_vs_fp64(case, gemm_variant):
         assert rel_l2(bd.grad, b64.grad) < 2e-6
 
 
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_conv_wgrad_kstep32_vs_fp64(case):
+    """The tiled weight-gradient kernel with 32-pixel K-steps (e2ep_conv_wgrad_kstep)."""
+    from e2ep_amd import _lib, conv
+    N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5
+    wd = w.to(DEV).requires_grad_(True)
+    old = _lib.call_raw("e2ep_conv_wgrad_kstep", 32)
+    try:
+        y = conv.conv2d(x.to(DEV), wd, None, (st, st), pad, (dil, dil), 0)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy.to(DEV))
+    finally:
+        _lib.call_raw("e2ep_conv_wgrad_kstep", old)
+    w64 = w.double().requires_grad_(True)
+    F.conv2d(F.pad(x.double(), pad), w64, None, st, 0, dil).backward(gy.double())
+    assert rel_l2(wd.grad, w64.grad) < 2e-6
+
+
 def test_conv_wgrad_deterministic():
     from e2ep_amd import conv
     g = torch.Generator().manual_seed(0)
