@@ -274,7 +274,7 @@ def main():
         backend = dist.get_backend()
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
-    from e2ep_amd import _lib, precision, synthetic, timing
+    from e2ep_amd import _lib, conv, precision, synthetic, timing
     from e2ep_amd.train import TrainStep
     from tool.config import default_cfg
     from trainer.pl_trainer import ParkingTrainingModule
@@ -321,9 +321,13 @@ def main():
     n_eager = 3
     timing.reset()
     timing.enable(True)
+    # serial weight gradients here: a kernel's events then time that kernel alone, not its
+    # overlap with a side-stream weight gradient (the timed step above runs them forked)
+    prev_overlap = conv.set_wgrad_overlap(False)
     for _ in range(n_eager):
         step._fwd_bwd()
     timing.enable(False)
+    conv.set_wgrad_overlap(prev_overlap)
     kern = timing.summary()
     work = timing.work()
     gemm = [k for k in ("conv_fwd", "conv_dgrad") if k in kern]

@@ -17,7 +17,7 @@ struct GemmCols {
 int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B, int ldb,
              bool bk, long long b_bytes, const float *bias, bool bias_rows, const float *Cadd,
              int ldadd, float *C, long long c_bytes, int ldc, GemmCols cols, int M, int N, int K,
-             int relu, void *workspace, hipStream_t s);
+             int relu, void *workspace, hipStream_t s, float *rs = nullptr);
 size_t gemm_ws(int M, int N, int K);
 
 }  // namespace e2ep

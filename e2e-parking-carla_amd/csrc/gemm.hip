@@ -51,7 +51,10 @@ __global__ void __launch_bounds__(256)
            const float *__restrict__ B, int ldb, long long b_bytes, int bvec,
            const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
            int ldadd, float *__restrict__ C, long long c_bytes, int ldc, GemmCols cols, int M,
-           int N, int K, int kper, int relu) {
+           int N, int K, int kper, int relu, float *__restrict__ rs) {
+  // rs != null (only !AK, !BKC, unbatched): B gets a logical column N of ones, so column N of
+  // the product is the row sum of A over k — rs[m] = sum_k A(m, k), the bias gradient of a
+  // linear layer taken by its weight-gradient GEMM (no separate column-sum launches)
   constexpr int WN = 4 / WM;                      // waves along N
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
   constexpr int GA = BM / 32, GB = BN / 32;       // 32-row load groups per operand tile
@@ -76,10 +79,12 @@ __global__ void __launch_bounds__(256)
 
   // column-batched B: this thread's load column is fixed, so its image offset is too
   long long bcol_off[GB];
+  bool bone[GB];
 #pragma unroll
   for (int i = 0; i < GB; ++i) {
     const int n = min(n0 + 32 * i + br, N - 1);
     bcol_off[i] = cols.hw ? (long long)(n / cols.hw) * cols.b_img + n % cols.hw : n;
+    bone[i] = !BKC && rs && n0 + 32 * i + br == N;
   }
 
   // One step of register lookahead: the next K-step's loads are issued before this step's
@@ -127,8 +132,10 @@ __global__ void __launch_bounds__(256)
         load_k(xb[i], rb_, bvec, (long long)row * ldb, k, full);
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          xb[i][j] = bload(rb_, (int)(((long long)min(k + j, K - 1) * ldb + bcol_off[i]) * 4));
+        for (int j = 0; j < 4; ++j) {
+          const float v = bload(rb_, (int)(((long long)min(k + j, K - 1) * ldb + bcol_off[i]) * 4));
+          xb[i][j] = bone[i] ? 1.f : v;
+        }
       }
     }
   };
@@ -205,19 +212,22 @@ __global__ void __launch_bounds__(256)
   // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
   // gridDim.z > 1: raw partial sums into C = workspace[split][M][N] (dense, unbatched).
   const bool final_ = gridDim.z == 1;
-  float *dst = final_ ? C : C + (long long)split * M * N;
-  const int ldd = final_ ? ldc : N;
+  const int Nw = rs ? N + 1 : N;  // split-K partials carry the row-sum column
+  float *dst = final_ ? C : C + (long long)split * M * Nw;
+  const int ldd = final_ ? ldc : Nw;
   const bool batched = final_ && cols.hw > 0;
   // edges: buffer stores with out-of-range offsets are dropped; the epilogue's optional
   // inputs are behind uniform branches, and the 16 Cadd values of a tile are loaded together
-  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, final_ ? c_bytes : 4LL * M * N);
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, final_ ? c_bytes : 4LL * M * Nw);
+  const __amdgpu_buffer_rsrc_t rrs = rsrc(rs, rs && final_ ? 4LL * M : 0);
   const __amdgpu_buffer_rsrc_t rc =
       rsrc(Cadd, Cadd ? (batched ? c_bytes : 4LL * ((long long)(M - 1) * ldadd + N)) : 0);
   const bool add_c = final_ && Cadd != nullptr, add_b = final_ && bias != nullptr;
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
     const int n = n0 + 32 * TN * wn + 32 * t + li;
-    const bool nok = n < N;
+    const bool nok = n < N || (rs && !final_ && n == N);  // partial row-sum column
+    const bool rsc = rs && final_ && n == N;
     const long long cbase = batched ? (long long)(n / cols.hw) * cols.c_img + n % cols.hw : n;
     const float bn_ = (add_b && !bias_rows) ? bias[min(n, N - 1)] : 0.f;
 #pragma unroll
@@ -239,6 +249,7 @@ __global__ void __launch_bounds__(256)
         if (add_c) v += cv[r];
         if (final_ && relu) v = fmaxf(v, 0.f);
         bstore(rd, (nok && m < M) ? (int)((cbase + (long long)m * ldd) * 4) : OOR, v);
+        if (rs) bstore(rrs, (rsc && m < M) ? m * 4 : OOR, v);
       }
     }
   }
@@ -251,9 +262,12 @@ template <int V>
 __global__ void __launch_bounds__(256)
     k_gemm_reduce(const float *__restrict__ part, int splits, int M, int N,
                   const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
-                  int ldadd, float *__restrict__ C, int ldc, GemmCols cols, int relu) {
+                  int ldadd, float *__restrict__ C, int ldc, GemmCols cols, int relu,
+                  float *__restrict__ rs) {
+  // rs: the partials are M x (N + 1), column N = row sums of A (V = 1 only)
+  const int Nw = rs ? N + 1 : N;
   const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * V;
-  const long long MN = (long long)M * N;
+  const long long MN = (long long)M * Nw;
   if (i >= MN) return;
   float s[V];
   if (V == 4) {
@@ -270,7 +284,11 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     const long long e = i + v;
-    const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+    const int m = (int)(e / Nw), n = (int)(e - (long long)m * Nw);
+    if (V == 1 && rs && n == N) {
+      rs[m] = s[v];
+      return;
+    }
     const long long off = cols.hw ? (long long)(n / cols.hw) * cols.c_img + n % cols.hw +
                                         (long long)m * ldc
                                   : (long long)m * ldc + n;
@@ -348,21 +366,26 @@ static int vec_of(bool kc, int ld, const void *ptr) {
 int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B, int ldb,
              bool bk, long long b_bytes, const float *bias, bool bias_rows, const float *Cadd,
              int ldadd, float *C, long long c_bytes, int ldc, GemmCols cols, int M, int N, int K,
-             int relu, void *workspace, hipStream_t s) {
-  const GemmLaunch p = gemm_plan(M, N, K);
+             int relu, void *workspace, hipStream_t s, float *rs) {
+  if (rs && (ak || bk || cols.hw)) {
+    set_error("gemm: the row sum of A needs a k-major A, a row-contiguous B, unbatched C");
+    return E2EP_EINVAL;
+  }
+  const int Nx = rs ? N + 1 : N;  // logical columns including the ones column
+  const GemmLaunch p = gemm_plan(M, Nx, K);
   if (p.splits > 1 && !workspace) {
     set_error("gemm: workspace of e2ep_gemm_workspace() bytes required");
     return E2EP_EINVAL;
   }
   float *out = p.splits > 1 ? static_cast<float *>(workspace) : C;
   const GemmTile td = tile_dims(p.tile);
-  dim3 grid(cdiv(N, td.bn), cdiv(M, td.bm), p.splits);
+  dim3 grid(cdiv(Nx, td.bn), cdiv(M, td.bm), p.splits);
   const int avec = vec_of(ak, lda, A), bvec = vec_of(bk, ldb, B);
   const int br = bias_rows ? 1 : 0;
 #define E2EP_GEMM_LAUNCH(AKV, BKV, WMV, TMV, TNV)                                               \
   hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, TMV, TNV>), grid, dim3(256), 0, s, A, lda, a_bytes, \
                      avec, B, ldb, b_bytes, bvec, bias, br, Cadd, ldadd, out, c_bytes, ldc, cols, \
-                     M, N, K, p.kper, relu)
+                     M, N, K, p.kper, relu, rs)
 #define E2EP_GEMM_T(AKV, BKV)                                     \
   do {                                                            \
     switch (p.tile) {                                             \
@@ -381,17 +404,17 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
 #undef E2EP_GEMM_T
 #undef E2EP_GEMM_LAUNCH
   if (p.splits > 1) {
-    const long long MN = (long long)M * N;
-    const bool v4 = MN % 4 == 0 && ldc == N && cols.hw == 0 && !bias_rows &&
+    const long long MN = (long long)M * Nx;
+    const bool v4 = !rs && MN % 4 == 0 && ldc == N && cols.hw == 0 && !bias_rows &&
                     (!Cadd || ldadd == N) && ((uintptr_t)C & 15) == 0;
     if (v4)
       hipLaunchKernelGGL(k_gemm_reduce<4>, dim3(cdiv(MN / 4, 256)), dim3(256), 0, s,
                          static_cast<const float *>(workspace), p.splits, M, N, bias, br, Cadd,
-                         ldadd, C, ldc, cols, relu);
+                         ldadd, C, ldc, cols, relu, nullptr);
     else
       hipLaunchKernelGGL(k_gemm_reduce<1>, dim3(cdiv(MN, 256)), dim3(256), 0, s,
                          static_cast<const float *>(workspace), p.splits, M, N, bias, br, Cadd,
-                         ldadd, C, ldc, cols, relu);
+                         ldadd, C, ldc, cols, relu, rs);
   }
   return 0;
 }
@@ -412,6 +435,7 @@ int e2ep_gemm_force(int tile, int splits, int unused) {
 }
 
 size_t e2ep_gemm_workspace(int M, int N, int K) { return gemm_ws(M, N, K); }
+size_t e2ep_gemm_rowsum_workspace(int M, int N, int K) { return gemm_ws(M, N + 1, K); }
 
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
@@ -429,9 +453,28 @@ int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, i
                E2EP_ERANGE, "e2ep_gemm: operand larger than 2 GB");
   const int rc = gemm_run(A, lda, a_kcontig, a_bytes, B, ldb, b_kcontig, b_bytes, bias, false,
                           Cadd, ldadd, C, c_bytes, ldc, GemmCols{0, 0, 0}, M, N, K, relu,
-                          workspace, as_stream(stream));
+                          workspace, as_stream(stream), nullptr);
   if (rc) return rc;
   return launch_status("e2ep_gemm");
+}
+
+int e2ep_gemm_rowsum(const float *A, int lda, const float *B, int ldb, float *C, int ldc,
+                     float *rowsum, int M, int N, int K, void *workspace, void *stream) {
+  E2EP_REQUIRE(A && B && C && rowsum && M > 0 && N > 0 && K > 0, E2EP_EINVAL,
+               "e2ep_gemm_rowsum: bad arguments M=%d N=%d K=%d", M, N, K);
+  E2EP_REQUIRE(lda >= M && ldb >= N && ldc >= N, E2EP_EINVAL,
+               "e2ep_gemm_rowsum: leading dimension too small");
+  const long long a_bytes = 4LL * ((long long)(K - 1) * lda + M);
+  const long long b_bytes = 4LL * ((long long)(K - 1) * ldb + N);
+  const long long c_bytes = 4LL * ((long long)(M - 1) * ldc + N);
+  E2EP_REQUIRE(a_bytes < 0x7fffffffLL && b_bytes < 0x7fffffffLL && c_bytes < 0x7fffffffLL &&
+                   4LL * M * (N + 1) * 8 < 0x7fffffffLL,
+               E2EP_ERANGE, "e2ep_gemm_rowsum: operand larger than 2 GB");
+  const int rc = gemm_run(A, lda, false, a_bytes, B, ldb, false, b_bytes, nullptr, false, nullptr,
+                          0, C, c_bytes, ldc, GemmCols{0, 0, 0}, M, N, K, 0, workspace,
+                          as_stream(stream), rowsum);
+  if (rc) return rc;
+  return launch_status("e2ep_gemm_rowsum");
 }
 
 }  // extern "C"

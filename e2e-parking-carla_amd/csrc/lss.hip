@@ -543,6 +543,32 @@ __global__ void __launch_bounds__(256) k_transpose(const float *__restrict__ in,
   }
 }
 
+// many small transposes in one launch (the conv weights' tap-major copies, conv.py
+// TapMajorBatch): entry e = {src, dst, rows, cols, first tile, column tiles} as int64;
+// block = one 64 x 64 tile of one entry (found by a scan of the n <= 256 tile offsets)
+__global__ void __launch_bounds__(256) k_transpose_multi(const long long *__restrict__ tab, int n) {
+  __shared__ float tile[64][65];
+  const int bid = blockIdx.x;
+  int e = 0;
+  while (e + 1 < n && tab[(e + 1) * 6 + 4] <= bid) ++e;
+  const long long *t = tab + e * 6;
+  const float *src = reinterpret_cast<const float *>(t[0]);
+  float *dst = reinterpret_cast<float *>(t[1]);
+  const int rows = (int)t[2], cols = (int)t[3], ct = (int)t[5];
+  const int loc = bid - (int)t[4];
+  const int r0 = (loc / ct) * 64, c0 = (loc % ct) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int gr = r0 + r, gc = c0 + tx;
+    if (gr < rows && gc < cols) tile[r][tx] = src[(long long)gr * cols + gc];
+  }
+  __syncthreads();
+  for (int c = ty; c < 64; c += 4) {
+    const int gc = c0 + c, gr = r0 + tx;
+    if (gr < rows && gc < cols) dst[(long long)gc * rows + gr] = tile[tx][c];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // target channel: block per sample, zero the plane and set the 8x8 square
 // ------------------------------------------------------------------------------------------
@@ -769,6 +795,13 @@ int e2ep_transpose(const float *in, long long in_bstride, int batch, int rows, i
   hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, as_stream(stream), in, in_bstride, rows, cols,
                      out);
   return launch_status("e2ep_transpose");
+}
+
+int e2ep_transpose_multi(const long long *table, int n, int tiles, void *stream) {
+  E2EP_REQUIRE(table && n > 0 && n <= 256 && tiles > 0, E2EP_EINVAL,
+               "e2ep_transpose_multi: bad table (n %d, tiles %d)", n, tiles);
+  hipLaunchKernelGGL(k_transpose_multi, dim3(tiles), dim3(256), 0, as_stream(stream), table, n);
+  return launch_status("e2ep_transpose_multi");
 }
 
 int e2ep_target_bev(const float *target_point, const float *noise, int B, int X, int Y, float res_x,

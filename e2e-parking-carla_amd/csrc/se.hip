@@ -12,6 +12,8 @@
 namespace e2ep {
 
 constexpr int SE_MAXC = 4096, SE_MAXSQ = 256;
+// float4 loads in flight per lane in the per-plane reductions (squeeze, da)
+constexpr int SE_U = 4;
 
 __device__ __forceinline__ float sigm(float v) { return 1.f / (1.f + expf(-v)); }
 
@@ -38,9 +40,19 @@ __device__ __forceinline__ float plane_sum(const float *__restrict__ p, int HW, 
   float s = 0.f;
   if ((HW & 3) == 0) {
     const int HW4 = HW >> 2;
-    for (int i = lane; i < HW4; i += 64) {
-      const float4 v = se_in4(reinterpret_cast<const float4 *>(p)[i], sc, sh, t);
-      s += (v.x + v.y) + (v.z + v.w);
+    const float4 *p4 = reinterpret_cast<const float4 *>(p);
+    // SE_U loads in flight per lane (clamped, unconditional); the lane still sums i, i + 64,
+    // ... in ascending order
+    for (int i0 = lane; i0 < HW4; i0 += 64 * SE_U) {
+      float4 v[SE_U];
+#pragma unroll
+      for (int u = 0; u < SE_U; ++u) v[u] = p4[min(i0 + u * 64, HW4 - 1)];
+#pragma unroll
+      for (int u = 0; u < SE_U; ++u) {
+        if (i0 + u * 64 >= HW4) break;
+        const float4 w = se_in4(v[u], sc, sh, t);
+        s += (w.x + w.y) + (w.z + w.w);
+      }
     }
   } else {
     for (int i = lane; i < HW; i += 64) s += se_in(p[i], sc, sh, t);
@@ -147,10 +159,22 @@ __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn
   const float *xp = x + (size_t)pl * HW, *gp = dy + (size_t)pl * HW;
   float acc = 0.f;
   if ((HW & 3) == 0) {
-    for (int i = lane; i < (HW >> 2); i += 64) {
-      const float4 u = se_in4(reinterpret_cast<const float4 *>(xp)[i], sc, sh, t);
-      const float4 g = reinterpret_cast<const float4 *>(gp)[i];
-      acc += (u.x * g.x + u.y * g.y) + (u.z * g.z + u.w * g.w);
+    const int HW4 = HW >> 2;
+    const float4 *x4 = reinterpret_cast<const float4 *>(xp), *g4 = reinterpret_cast<const float4 *>(gp);
+    for (int i0 = lane; i0 < HW4; i0 += 64 * SE_U) {
+      float4 xv[SE_U], gv[SE_U];
+#pragma unroll
+      for (int u = 0; u < SE_U; ++u) {
+        const int i = min(i0 + u * 64, HW4 - 1);
+        xv[u] = x4[i];
+        gv[u] = g4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < SE_U; ++u) {
+        if (i0 + u * 64 >= HW4) break;
+        const float4 w = se_in4(xv[u], sc, sh, t), g = gv[u];
+        acc += (w.x * g.x + w.y * g.y) + (w.z * g.z + w.w * g.w);
+      }
     }
   } else {
     for (int i = lane; i < HW; i += 64) acc += se_in(xp[i], sc, sh, t) * gp[i];

@@ -29,6 +29,7 @@ SIGNATURES = {
     "e2ep_lss_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i64, _p]),
     "e2ep_lss_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "e2ep_transpose": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
+    "e2ep_transpose_multi": (_i, [_p, _i, _i, _p]),
     "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
     "e2ep_conv_fwd_workspace": (_sz, [_p]),
     "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _p]),
@@ -95,7 +96,10 @@ SIGNATURES = {
     "e2ep_depth_bce_fwd_f64": (_i, [_p, _p, _i, _i, _i, _i, _i, _d, _d, _p, _p, _p, _p, _p]),
     "e2ep_gemm_workspace": (_sz, [_i, _i, _i]),
     "e2ep_gemm_force": (_i, [_i, _i, _i]),
+    "e2ep_bn_small": (_i, [_i]),
     "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
+    "e2ep_gemm_rowsum_workspace": (_sz, [_i, _i, _i]),
+    "e2ep_gemm_rowsum": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _p, _p]),
     "e2ep_decode_frames": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p]),
     "e2ep_widen_u8_i64": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_depth_bce_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p]),

@@ -46,6 +46,14 @@ class _BevStem(torch.autograd.Function):
         s = _lib.stream()
         d = _lib.dims(dims)
         dbev = dw = None
+        fork = None
+        if ctx.needs_input_grad[2]:  # weight gradient on the side stream (conv._Fork)
+            dw = torch.empty_like(w)
+            ws = torch.empty(_lib.load().e2ep_conv_wgrad_splits(d) * dw.numel(), dtype=torch.float32,
+                             device=gy.device)
+            fork = conv._Fork(gy.device, on=ctx.needs_input_grad[0])
+            with fork:
+                conv.conv_wgrad(gy, x, dims, dw, ws)
         if ctx.needs_input_grad[0]:
             dres = conv.conv_dgrad(gy, wt, dims, C,
                                    torch.empty(B, C, H, W, dtype=torch.float32, device=gy.device), w_layout=1)
@@ -56,8 +64,8 @@ class _BevStem(torch.autograd.Function):
             with timing.region("resize_bwd"):
                 _lib.call("e2ep_resize_bwd_cl", _lib.ptr(dres), H * W, B, C, X, Y, H, W, sh, sw,
                           _lib.ptr(dbev), s)
-        if ctx.needs_input_grad[2]:
-            dw = conv.conv_wgrad(gy, x, dims, torch.empty_like(w))
+        if fork is not None:
+            fork.join()
         return dbev, None, dw, None
 
 

@@ -5,6 +5,8 @@ e2ep_conv_dgrad (stride-phase split) / e2ep_conv_wgrad (split pixel reduction) /
 e2ep_bias_grad.  1x1 convs on 1x1 maps run on e2ep_skinny_gemm.  groups must be 1
 (depthwise convs use e2ep_amd.nn_ops).  `grad_channels` limits the input gradient to the
 first channels (the BEV encoder's target-point channel is a constant: no gradient)."""
+import os
+
 import torch
 
 from . import _lib, timing
@@ -26,11 +28,91 @@ def conv_flops(dims, in_channels=None):
     return 2.0 * N * Cout * P * Q * (in_channels or Cin) * R * S
 
 
+class TapMajorBatch:
+    """Every spatial conv weight's tap-major copy in one launch per forward.
+
+    The first forward inside the scope transposes per weight (one launch each) and records
+    the weights in call order; later forwards transpose all recorded weights with a single
+    e2ep_transpose_multi launch at scope entry into persistent buffers (stable addresses, so
+    a HIP-graph capture of the step replays it) and tap_major() hands out views.  A weight
+    that was not recorded, or whose storage moved (re-flattened parameters), falls back to
+    its own launch; a moved weight re-records on the next forward."""
+
+    def __init__(self):
+        self.recorded = None   # weights in call order
+        self._log = None
+        self._views = {}       # id(weight) -> tap-major view, valid while active
+        self._key = None
+        self._table = None
+        self._buf = None
+        self._tiles = 0
+        self.active = False
+
+    def _build(self, ws):
+        dev = ws[0].device
+        sizes = [w.numel() for w in ws]
+        self._buf = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
+        rows, off, tile0 = [], 0, 0
+        views = []
+        for w, n in zip(ws, sizes):
+            Cout, Cin, R, S = w.shape
+            v = self._buf[off:off + n].view(R * S, Cout, Cin)
+            r, c = Cout * Cin, R * S
+            ct = (c + 63) // 64
+            rows.append([w.data_ptr(), v.data_ptr(), r, c, tile0, ct])
+            tile0 += ((r + 63) // 64) * ct
+            off += n
+            views.append(v)
+        self._table = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self._tiles = tile0
+        self._key = [(w.data_ptr(), tuple(w.shape)) for w in ws]
+        self._vlist = views
+
+    def __enter__(self):
+        ws = self.recorded
+        if ws is None:
+            self._log = []
+        elif [(w.data_ptr(), tuple(w.shape)) for w in ws] != self._key:
+            self.recorded, self._log = None, []  # storage moved: record again
+        else:
+            _lib.call("e2ep_transpose_multi", _lib.ptr(self._table), len(ws), self._tiles,
+                      _lib.stream())
+            self._views = {id(w): v for w, v in zip(ws, self._vlist)}
+        self.active = True
+        _TAP_BATCH.append(self)
+        return self
+
+    def __exit__(self, *exc):
+        _TAP_BATCH.pop()
+        self.active = False
+        self._views = {}
+        if self.recorded is None and self._log is not None and not exc[0]:
+            log = [w for w in self._log if w.dtype == torch.float32 and w.is_contiguous()]
+            if 0 < len(log) <= 256:
+                self.recorded = log
+                self._build(log)
+        self._log = None
+        return False
+
+    def lookup(self, w):
+        v = self._views.get(id(w))
+        if v is None and self._log is not None and all(w is not o for o in self._log):
+            self._log.append(w)
+        return v
+
+
+_TAP_BATCH = []  # active TapMajorBatch scopes (innermost last)
+
+
 def tap_major(w):
     """[Cout,Cin,R,S] -> [R*S,Cout,Cin] (the kernels' w_layout 1); 1x1 filters unchanged."""
     Cout, Cin, R, S = w.shape
     if R * S == 1:
         return w.contiguous()
+    if _TAP_BATCH:
+        v = _TAP_BATCH[-1].lookup(w)
+        if v is not None:
+            return v
     out = torch.empty(R * S, Cout, Cin, dtype=torch.float32, device=w.device)
     _lib.call("e2ep_transpose", _lib.ptr(w.contiguous()), Cout * Cin * R * S, 1, Cout * Cin, R * S,
               _lib.ptr(out), _lib.stream())
@@ -57,14 +139,68 @@ def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0, res=None):
     return dx
 
 
-def conv_wgrad(gy, x, dims, dw):
+def conv_wgrad(gy, x, dims, dw, ws=None):
     d = _lib.dims(dims)
     splits = _lib.load().e2ep_conv_wgrad_splits(d)
-    ws = torch.empty(splits * dw.numel(), dtype=torch.float32, device=gy.device)
+    if ws is None:
+        ws = torch.empty(splits * dw.numel(), dtype=torch.float32, device=gy.device)
     with timing.region(_rname("conv_wgrad", dims), conv_flops(dims)):
         _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws),
                   _lib.ptr(dw), 0, _lib.stream())
     return dw
+
+
+# Weight gradients on a side stream.  A conv's weight gradient (and bias gradient) does not
+# feed the rest of the backward, so it is launched on a second stream forked from the current
+# one and runs concurrently with the data gradient; the current stream joins the side stream
+# before the backward returns.  Every tensor the side stream touches is allocated on the
+# current stream and still referenced at the join, so the caching allocator cannot hand its
+# memory out while the side stream uses it.  Under HIP-graph capture the fork / join become
+# parallel graph branches.  Small convs (16x16 / 32x32 maps) fill a fraction of the chip, so
+# their two GEMMs overlap instead of running back to back.
+_SIDE = {}
+_OVERLAP = [os.environ.get("E2EP_WGRAD_OVERLAP", "1") != "0"]
+
+
+def set_wgrad_overlap(on):
+    """Enable / disable the side-stream weight gradients (returns the previous setting)."""
+    prev = _OVERLAP[0]
+    _OVERLAP[0] = bool(on)
+    return prev
+
+
+def side_stream(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _SIDE.get(idx)
+    if st is None:
+        st = _SIDE[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
+class _Fork:
+    """with _Fork(dev) as side: ...launches on `side`...  — forks from the current stream on
+    entry (side waits for it); join() makes the current stream wait for the side stream."""
+
+    def __init__(self, device, on=True):
+        self.on = on and _OVERLAP[0]
+        self.main = torch.cuda.current_stream(device)
+        self.side = side_stream(device) if self.on else self.main
+
+    def __enter__(self):
+        if self.on:
+            self.side.wait_stream(self.main)
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self._ctx.__exit__(*exc)
+        return False
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
 
 
 class _Conv2d(torch.autograd.Function):
@@ -95,6 +231,23 @@ class _Conv2d(torch.autograd.Function):
             _lib.call("e2ep_act_bwd", _lib.ptr(y), _lib.ptr(gy), gy.numel(), 1, _lib.ptr(gm), s)
             gy = gm
         dx = dw = db = None
+        # weight / bias gradients on the side stream, concurrent with the data gradient
+        want_w, want_b = ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2]
+        fork = None
+        if want_w or want_b:
+            if want_w:  # allocated on the current stream (see _Fork)
+                dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
+                ws = torch.empty(_lib.load().e2ep_conv_wgrad_splits(_lib.dims(dims)) * dw.numel(),
+                                 dtype=torch.float32, device=x.device)
+            if want_b:
+                db = torch.empty(Cout, dtype=torch.float32, device=x.device)
+            fork = _Fork(x.device, on=ctx.needs_input_grad[0])
+            with fork:
+                if want_w:
+                    conv_wgrad(gy, x, dims, dw, ws)
+                if want_b:
+                    _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db),
+                              _lib.stream())
         if ctx.needs_input_grad[0]:
             gc = ctx.gc or Cin
             res = gskip.contiguous() if (gskip is not None and gc == Cin) else None
@@ -108,11 +261,8 @@ class _Conv2d(torch.autograd.Function):
             else:
                 dx = torch.zeros_like(x)
                 dx[:, :gc] = dxg
-        if ctx.needs_input_grad[1]:
-            dw = conv_wgrad(gy, x, dims, torch.empty(ctx.wshape, dtype=torch.float32, device=x.device))
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = torch.empty(Cout, dtype=torch.float32, device=x.device)
-            _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db), s)
+        if fork is not None:
+            fork.join()
         if dx is None and gskip is not None and ctx.needs_input_grad[0]:
             dx = gskip
         return dx, dw, db, None, None, None, None

@@ -4,7 +4,7 @@ each backward is the matching e2ep gradient kernel (no PyTorch arithmetic)."""
 import torch
 import torch.nn.functional as F
 
-from . import _lib, rng, timing
+from . import _lib, conv, rng, timing
 
 ACT = {None: 0, "none": 0, "relu": 1, "swish": 2}
 
@@ -223,16 +223,20 @@ class _DwConv(torch.autograd.Function):
         d = _lib.dims(ctx.dims)
         s = _lib.stream()
         dx = dw = None
+        fork = None
+        if ctx.needs_input_grad[1]:  # weight gradient on the side stream (conv._Fork)
+            dw = torch.empty_like(w)
+            ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
+            fork = conv._Fork(x.device, on=ctx.needs_input_grad[0])
+            with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_DwConv")):
+                _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
+                          _lib.ptr(ws), _lib.ptr(dw), _lib.stream())
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             with timing.region(timing.name("dwconv_dgrad", gy.shape, "_DwConv")):
                 _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s)
-        if ctx.needs_input_grad[1]:
-            dw = torch.empty_like(w)
-            ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
-            with timing.region(timing.name("dwconv_wgrad", gy.shape, "_DwConv")):
-                _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
-                          _lib.ptr(ws), _lib.ptr(dw), s)
+        if fork is not None:
+            fork.join()
         return dx, dw, None
 
 
@@ -275,12 +279,14 @@ class _BnActDwConv(torch.autograd.Function):
         s = _lib.stream()
         nig = ctx.needs_input_grad
         dw = dx = dg = db = None
-        if nig[9]:
+        fork = None
+        if nig[9]:  # weight gradient on the side stream (conv._Fork)
             dw = torch.empty_like(w)
-            ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
-            with timing.region(timing.name("dwconv_wgrad", gy.shape, "_BnActDwConv")):
+            wsw = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
+            fork = conv._Fork(x.device, on=nig[0] or nig[1] or nig[2])
+            with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(stats[2]),
-                          _lib.ptr(stats[3]), ctx.act, _lib.ptr(ws), _lib.ptr(dw), s)
+                          _lib.ptr(stats[3]), ctx.act, _lib.ptr(wsw), _lib.ptr(dw), _lib.stream())
         if nig[0] or nig[1] or nig[2]:
             dt = torch.empty_like(x)  # gradient at the activation output
             with timing.region(timing.name("dwconv_dgrad", gy.shape, "_BnActDwConv")):
@@ -294,6 +300,8 @@ class _BnActDwConv(torch.autograd.Function):
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx), _lib.ptr(dg),
                           _lib.ptr(db), None, _lib.ptr(ws), s)
+        if fork is not None:
+            fork.join()
         return dx, dg, db, None, None, None, None, None, None, dw, None
 
 
@@ -599,7 +607,7 @@ def add_drop_layer_norm(a, b, norm, p=0.0, u=None, seed=None):
 # nn.Linear on e2ep_gemm (forward, input gradient, weight gradient) + e2ep_col_sum (bias grad)
 # ------------------------------------------------------------------------------------------
 def gemm(A, a_kcontig, B, b_kcontig, M, N, K, bias=None, cadd=None, out=None, relu=False,
-         tag="gemm"):
+         tag="gemm", ws=None):
     """C (M x N, row-major) = A(m,k) B(k,n) (+ bias[n]) (+ cadd) (ReLU) on e2ep_gemm.
     A is (M x K) when a_kcontig else (K x M), B is (N x K) when b_kcontig else (K x N); both
     row-major with unit inner stride."""
@@ -614,7 +622,8 @@ def gemm(A, a_kcontig, B, b_kcontig, M, N, K, bias=None, cadd=None, out=None, re
         out = torch.empty(M, N, dtype=torch.float32, device=A.device)
     if cadd is not None and (cadd.shape != (M, N) or cadd.stride(1) != 1):
         raise _lib.E2EPError("gemm: cadd must be (M, N) with unit inner stride")
-    ws = _ws(_lib.load().e2ep_gemm_workspace(M, N, K), A.device)
+    if ws is None:
+        ws = _ws(_lib.load().e2ep_gemm_workspace(M, N, K), A.device)
     with timing.region(timing.name("gemm", (M, N, K), tag), 2.0 * M * N * K):
         _lib.call("e2ep_gemm", _lib.ptr(A), A.stride(0), int(a_kcontig), _lib.ptr(B), B.stride(0),
                   int(b_kcontig), _lib.ptr(bias), _lib.ptr(cadd),
@@ -626,7 +635,8 @@ def gemm(A, a_kcontig, B, b_kcontig, M, N, K, bias=None, cadd=None, out=None, re
 class _Linear(torch.autograd.Function):
     """y = x W^T + b (+ ReLU).  All three GEMMs are e2ep_gemm: forward (bias and ReLU in the
     epilogue), dX = dY W (the residual's gradient added in the epilogue when skip is used),
-    dW = dY^T X; the bias gradient is e2ep_col_sum."""
+    dW = dY^T X with the bias gradient as the same launch's row sum (e2ep_gemm_rowsum); without
+    a weight gradient the bias gradient is e2ep_col_sum."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, skip=False, relu=False):
@@ -655,17 +665,37 @@ class _Linear(torch.autograd.Function):
         if ctx.relu:
             g2 = g2 * (y > 0)
         dx = dw = db = None
+        # weight / bias gradients on the side stream, concurrent with the input gradient
+        # (conv._Fork: every buffer allocated here, on the current stream, before the fork)
+        want_b = ctx.has_bias and nig[2]
+        fork = None
+        if nig[1] or want_b:
+            if nig[1]:
+                dw = torch.empty(N, K, dtype=torch.float32, device=gy.device)
+                wsw = _ws(_lib.load().e2ep_gemm_rowsum_workspace(N, K, M) if want_b
+                          else _lib.load().e2ep_gemm_workspace(N, K, M), gy.device)
+            if want_b:
+                db = torch.empty(N, dtype=torch.float32, device=gy.device)
+                wsb = None if nig[1] else _ws(_lib.load().e2ep_col_sum_workspace(M, N), gy.device)
+            fork = conv._Fork(gy.device, on=nig[0])
+            with fork:
+                if nig[1] and want_b:  # dW and db in one launch
+                    with timing.region(timing.name("gemm", (N, K, M), "linear_wgrad"), 2.0 * N * K * M):
+                        _lib.call("e2ep_gemm_rowsum", _lib.ptr(g2), g2.stride(0), _lib.ptr(x2),
+                                  x2.stride(0), _lib.ptr(dw), K, _lib.ptr(db), N, K, M, _lib.ptr(wsw),
+                                  _lib.stream())
+                elif nig[1]:
+                    gemm(g2, False, x2, False, N, K, M, out=dw, ws=wsw, tag="linear_wgrad")
+                else:
+                    _lib.call("e2ep_col_sum", _lib.ptr(g2), M, N, _lib.ptr(db), _lib.ptr(wsb),
+                              _lib.stream())
         if nig[0]:
             cadd = gskip.reshape(M, K) if gskip is not None else None
             if cadd is not None and cadd.stride(1) != 1:
                 cadd = cadd.contiguous()
             dx = gemm(g2, True, weight, False, M, K, N, cadd=cadd, tag="linear_dgrad").view(ctx.xshape)
-        if nig[1]:
-            dw = gemm(g2, False, x2, False, N, K, M, tag="linear_wgrad")
-        if ctx.has_bias and nig[2]:
-            db = torch.empty(N, dtype=torch.float32, device=gy.device)
-            ws = _ws(_lib.load().e2ep_col_sum_workspace(M, N), gy.device)
-            _lib.call("e2ep_col_sum", _lib.ptr(g2), M, N, _lib.ptr(db), _lib.ptr(ws), _lib.stream())
+        if fork is not None:
+            fork.join()
         return dx, dw, db, None, None
 
 

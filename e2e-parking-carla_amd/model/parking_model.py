@@ -10,7 +10,7 @@ reproducible runs; by default it is drawn on the device exactly like the referen
 import torch
 from torch import nn
 
-from e2ep_amd import lss, nn_ops, rng
+from e2ep_amd import conv, lss, nn_ops, rng
 from model.bev_encoder import BevEncoder
 from model.bev_model import BevModel
 from model.control_predict import ControlPredict
@@ -43,12 +43,16 @@ class ParkingModel(nn.Module):
         return out, out[:, c:].detach().clone()
 
     def encoder(self, data, noise=None):
-        if self.training:  # all BN num_batches_tracked updates in one launch
-            if getattr(self, "_bn_counters", None) is None:
-                self._bn_counters = nn_ops.BnCounters()
-            with self._bn_counters:
-                return self._encoder(data, noise)
-        return self._encoder(data, noise)
+        # every spatial conv weight's tap-major copy in one launch (e2ep_amd.conv.TapMajorBatch)
+        if getattr(self, "_tap_batch", None) is None:
+            self._tap_batch = conv.TapMajorBatch()
+        with self._tap_batch:
+            if self.training:  # all BN num_batches_tracked updates in one launch
+                if getattr(self, "_bn_counters", None) is None:
+                    self._bn_counters = nn_ops.BnCounters()
+                with self._bn_counters:
+                    return self._encoder(data, noise)
+            return self._encoder(data, noise)
 
     def _encoder(self, data, noise=None):
         dev = self.bev_model.frustum.device

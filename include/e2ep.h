@@ -110,6 +110,13 @@ int e2ep_lss_bwd(const float *gT, const float *prob, const float *featT, const i
  * out batch stride rows*cols.  Used to produce featT / gT above. */
 int e2ep_transpose(const float *in, long long in_bstride, int batch, int rows, int cols,
                    float *out, void *stream);
+/* Many transposes in one launch: `table` (device, n <= 256 entries of 6 int64) holds per
+ * entry {src, dst, rows, cols, first tile, ceil(cols / 64)}, tiles counted in 64 x 64 blocks
+ * in entry order; dst = src^T (rows x cols -> cols x rows).  Replaces the per-conv weight
+ * transposes of one forward (every R x S > 1 conv weight [Cout,Cin,R,S] -> [R*S,Cout,Cin],
+ * the kernels' w_layout 1; reference convs: model/cam_encoder.py, model/bev_encoder.py,
+ * model/convolutions.py, model/segmentation_head.py) with a single launch. */
+int e2ep_transpose_multi(const long long *table, int n, int tiles, void *stream);
 
 /* Target-point channel (replaces ParkingModel.add_target_bev, model/parking_model.py:28-46).
  *   target_point [B,3] (x m, y m, yaw);  noise [B,2] uniform [0,1) (the rand_like draw)
@@ -461,9 +468,24 @@ size_t e2ep_gemm_workspace(int M, int N, int K);
 /* Benchmarking override of the launch plan: block tile 1 = 64x64, 2 = 32x128, 3 = 128x128,
  * 4 = 64x128, 5 = 128x64, 6 = 64x256 (0 = the automatic plan), and the K split. */
 int e2ep_gemm_force(int tile, int splits, int unused);
+
+/* BatchNorm single-launch switch: on = 1 (default) lets e2ep_bn_fwd / e2ep_bn_stats /
+ * e2ep_bn_bwd run channels of N*H*W <= 32768 (H*W % 4 == 0, training statistics) as one
+ * block-per-channel launch that keeps the channel in registers; 0 forces the split
+ * statistics + apply kernels for every shape; < 0 only queries.  Returns the previous value. */
+int e2ep_bn_small(int on);
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
               int K, int relu, void *workspace, void *stream);
+/* Weight gradient of a linear layer together with its bias gradient (replaces the
+ * nn.Linear backward's grad_weight = dY^T X and grad_bias = dY.sum(0), model/feature_fusion.py
+ * :13-14,24-29, model/control_predict.py:18-24): C = A(m,k) B(k,n) with A(m,k) = A[k*lda + m]
+ * and B(k,n) = B[k*ldb + n] (the a_kcontig = b_kcontig = 0 case of e2ep_gemm), and
+ * rowsum[m] = sum_k A(m,k) taken by the same launch as a column of ones appended to B.
+ * Workspace: e2ep_gemm_rowsum_workspace(M, N, K) bytes (0 when no K split). */
+size_t e2ep_gemm_rowsum_workspace(int M, int N, int K);
+int e2ep_gemm_rowsum(const float *A, int lda, const float *B, int ldb, float *C, int ldc,
+                     float *rowsum, int M, int N, int K, void *workspace, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Frame decode (dataset/carla_dataset.py:114-131, :494-515, :404-406): the per-step

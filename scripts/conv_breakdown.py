@@ -13,7 +13,8 @@ import torch  # noqa: E402
 
 
 def main():
-    from e2ep_amd import synthetic, timing
+    from e2ep_amd import conv, synthetic, timing
+    conv.set_wgrad_overlap(False)  # time each weight-gradient launch alone
     from e2ep_amd.train import TrainStep
     from tool.config import default_cfg
     from trainer.pl_trainer import ParkingTrainingModule

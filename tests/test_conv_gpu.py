@@ -211,3 +211,65 @@ def test_conv_low_precision_operands(case, mode, dt, loose):
         w64 = w.double().requires_grad_(True)
         F.conv2d(F.pad(x64, pad), w64, None, st, 0, dil).backward(gy.double())
         assert rel_l2(wd.grad, w64.grad) < 2e-6
+
+
+def test_tap_major_batch_one_launch_matches_per_weight():
+    """TapMajorBatch: the first scope records the spatial weights (per-weight transposes), the
+    second transposes all of them in one e2ep_transpose_multi launch; 1x1 weights pass
+    through; a weight whose storage moved makes the next scope record again."""
+    from e2ep_amd import conv
+    torch.manual_seed(0)
+    ws = [torch.randn(64, 65, 7, 7, device=DEV), torch.randn(48, 3, 3, 3, device=DEV),
+          torch.randn(130, 70, 5, 5, device=DEV), torch.randn(32, 16, 1, 1, device=DEV)]
+    ref = [w.permute(2, 3, 0, 1).reshape(w.shape[2] * w.shape[3], w.shape[0], w.shape[1]) for w in ws]
+    tb = conv.TapMajorBatch()
+    for it in range(3):
+        with tb:
+            outs = [conv.tap_major(w) for w in ws]
+            assert (tb.recorded is not None) == (it > 0)
+            torch.cuda.synchronize()
+            for o, r in zip(outs[:3], ref[:3]):
+                assert torch.equal(o, r)
+            assert torch.equal(outs[3], ws[3])
+    assert len(tb.recorded) == 3  # the 1x1 weight never enters the batch
+    ws[2].data = ws[2].data.clone()  # same tensor object, storage moved (re-flattened)
+    ref[2] = ref[2] * 1
+    with tb:
+        o = conv.tap_major(ws[2])
+        torch.cuda.synchronize()
+        assert torch.equal(o, ref[2])
+    assert len(tb.recorded) == 1 and tb.recorded[0] is ws[2]
+
+
+def test_side_stream_weight_gradient_equals_serial():
+    """conv / linear / BEV-stem backward with the weight gradients forked to the side stream
+    (conv._Fork) give bitwise the same gradients as the serial order (graph replay of the
+    forked step: test_train_step_gpu / test_graph_gpu, graph == eager)."""
+    from e2ep_amd import conv, nn_ops
+    torch.manual_seed(3)
+    x = torch.randn(8, 48, 32, 32, device=DEV, requires_grad=True)
+    w = torch.randn(64, 48, 3, 3, device=DEV, requires_grad=True)
+    b = torch.randn(64, device=DEV, requires_grad=True)
+    lx = torch.randn(300, 258, device=DEV, requires_grad=True)
+    lw = torch.randn(774, 258, device=DEV, requires_grad=True)
+    lb = torch.randn(774, device=DEV, requires_grad=True)
+    gy = torch.randn(8, 64, 32, 32, device=DEV)
+    gl = torch.randn(300, 774, device=DEV)
+
+    def run():
+        for t in (x, w, b, lx, lw, lb):
+            t.grad = None
+        y = conv.conv2d(x, w, b, pad=(1, 1, 1, 1), act=1)
+        yl = nn_ops.linear(lx, lw, lb)
+        torch.autograd.backward([y, yl], [gy, gl])
+        return [t.grad.clone() for t in (x, w, b, lx, lw, lb)]
+
+    prev = conv.set_wgrad_overlap(False)
+    try:
+        serial = run()
+        conv.set_wgrad_overlap(True)
+        for _ in range(3):
+            got = run()
+            assert all(torch.equal(a, c) for a, c in zip(got, serial))
+    finally:
+        conv.set_wgrad_overlap(prev)

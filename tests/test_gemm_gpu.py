@@ -127,3 +127,71 @@ def test_gemm_rejects_bad_shapes():
         nn_ops.gemm(A.t(), True, torch.randn(3, 5, device=DEV), True, 5, 3, 4)
     with pytest.raises(_lib.E2EPError):
         nn_ops.linear(torch.randn(2, 5), torch.randn(3, 5), None)
+
+
+def _rowsum_gemm(g2, x2):
+    """dW = g2^T x2 and db = g2.sum(0) through the one-launch e2ep_gemm_rowsum."""
+    from e2ep_amd import _lib
+    rows, N = g2.shape
+    K = x2.shape[1]
+    dw = torch.empty(N, K, dtype=torch.float32, device=DEV)
+    db = torch.empty(N, dtype=torch.float32, device=DEV)
+    nb = _lib.load().e2ep_gemm_rowsum_workspace(N, K, rows)
+    ws = torch.empty(max(1, nb // 4), dtype=torch.float32, device=DEV)
+    _lib.call("e2ep_gemm_rowsum", _lib.ptr(g2), g2.stride(0), _lib.ptr(x2), x2.stride(0),
+              _lib.ptr(dw), K, _lib.ptr(db), N, K, rows, _lib.ptr(ws), _lib.stream())
+    return dw, db
+
+
+@pytest.mark.parametrize("rows,N,K", [(2048, 774, 258), (2048, 258, 2048), (2048, 2048, 258),
+                                      (112, 258, 258), (112, 204, 258), (24, 64, 15),
+                                      (37, 70, 100), (5, 3, 32), (300, 33, 64)])
+def test_gemm_rowsum_weight_and_bias_gradient(rows, N, K):
+    """Linear backward's dW = dY^T X with db = dY.sum(0) taken by the same launch (a ones column
+    appended to X): both vs fp64, for widths where the ones column lands in a partial tile
+    (K % 32 != 0) and where it needs a tile of its own (K % 64 == 0), with and without K split."""
+    g = torch.Generator().manual_seed(rows + 3 * N + K)
+    g2, x2 = torch.randn(rows, N, generator=g), torch.randn(rows, K, generator=g)
+    dw, db = _rowsum_gemm(g2.to(DEV), x2.to(DEV))
+    assert rel_l2(dw, g2.double().t() @ x2.double()) < 2e-6
+    assert rel_l2(db, g2.double().sum(0)) < 2e-6
+    dw2, db2 = _rowsum_gemm(g2.to(DEV), x2.to(DEV))
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+def test_gemm_rowsum_every_tile_and_split(tile):
+    from e2ep_amd import _lib
+    rows, N, K = 333, 197, 256
+    g = torch.Generator().manual_seed(tile)
+    g2, x2 = torch.randn(rows, N, generator=g), torch.randn(rows, K, generator=g)
+    try:
+        for splits in (1, 3):
+            _lib.call("e2ep_gemm_force", tile, splits, 0)
+            dw, db = _rowsum_gemm(g2.to(DEV), x2.to(DEV))
+            assert rel_l2(dw, g2.double().t() @ x2.double()) < 2e-6, (tile, splits)
+            assert rel_l2(db, g2.double().sum(0)) < 2e-6, (tile, splits)
+    finally:
+        _lib.call("e2ep_gemm_force", 0, 0, 0)
+
+
+def test_linear_bias_gradient_from_rowsum_launch():
+    """nn_ops.linear backward: weight and bias gradients (one e2ep_gemm_rowsum launch) and the
+    bias-only case (e2ep_col_sum) against fp64 autograd."""
+    from e2ep_amd import nn_ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(4, 50, 258, generator=g)
+    w = torch.randn(774, 258, generator=g) / 16
+    b = torch.randn(774, generator=g)
+    dy = torch.randn(4, 50, 774, generator=g)
+    xd, wd, bd = (t.to(DEV).requires_grad_(True) for t in (x, w, b))
+    nn_ops.linear(xd, wd, bd).backward(dy.to(DEV))
+    x64, w64, b64 = (t.double().requires_grad_(True) for t in (x, w, b))
+    torch.nn.functional.linear(x64, w64, b64).backward(dy.double())
+    assert rel_l2(wd.grad, w64.grad) < 2e-6
+    assert rel_l2(bd.grad, b64.grad) < 2e-6
+    assert rel_l2(xd.grad, x64.grad) < 2e-6
+    wf = w.to(DEV)  # frozen weight: bias gradient alone
+    bd.grad = None
+    nn_ops.linear(xd.detach(), wf, bd).backward(dy.to(DEV))
+    assert rel_l2(bd.grad, b64.grad) < 2e-6

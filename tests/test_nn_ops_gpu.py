@@ -15,12 +15,23 @@ def _g(seed):
     return torch.Generator().manual_seed(seed)
 
 
+@pytest.fixture(params=[1, 0], ids=["bn_one_launch", "bn_split"])
+def bn_path(request):
+    """Run a BN test through the single-launch block-per-channel kernels (channels of
+    N*H*W <= 32768) and again with every shape forced onto the split stats + apply kernels."""
+    from e2ep_amd import _lib
+    prev = _lib.call_raw("e2ep_bn_small", request.param)
+    yield request.param
+    _lib.call_raw("e2ep_bn_small", prev)
+
+
 @pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("act", [None, "relu", "swish"])
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("shape", [(4, 24, 32, 32), (3, 7, 5, 9), (32, 6, 1, 1),
-                                   (4, 160, 8, 8), (16, 128, 32, 32)])
-def test_bn_act(train, act, res, shape):
+                                   (4, 160, 8, 8), (16, 128, 32, 32), (8, 16, 64, 64),
+                                   (3, 12, 44, 36), (2, 8, 136, 128)])
+def test_bn_act(train, act, res, shape, bn_path):
     from e2ep_amd import nn_ops
     g = _g(sum(shape) + 3 * train)
     x = torch.randn(*shape, generator=g) * 2 + 0.5
@@ -60,7 +71,7 @@ def test_bn_act(train, act, res, shape):
 
 
 @pytest.mark.parametrize("shape", [(8, 24, 16, 16), (6, 10, 5, 7), (16, 136, 8, 8)])
-def test_bn_drop_connect_fused(shape):
+def test_bn_drop_connect_fused(shape, bn_path):
     """MBConv tail in training: bn2 -> efficientnet-pytorch drop_connect (x / keep *
     floor(keep + u)) -> + inputs, fused into the BN kernels; vs fp64 torch."""
     from e2ep_amd import nn_ops
@@ -152,7 +163,7 @@ def test_depthwise(case):
                                   (2, 40, 32, 32, 5, 2, (1, 2, 1, 2), False),
                                   (3, 8, 13, 11, 3, 2, (0, 1, 0, 1), True),
                                   (2, 6, 64, 48, 5, 2, (2, 2, 2, 2), True)])
-def test_bn_swish_depthwise_fused(case):
+def test_bn_swish_depthwise_fused(case, bn_path):
     """MBConv _bn0 -> swish -> _depthwise_conv with the BN + swish applied inside the
     depthwise input load (e2ep_bn_stats + dwconv in_scale/in_shift), train and eval, vs fp64
     torch: output, x / gamma / beta / weight gradients and running statistics."""
@@ -312,7 +323,7 @@ def test_squeeze_excite_fused(shape):
 @pytest.mark.parametrize("case", [(8, 96, 16, 16, 6, True), (4, 40, 9, 7, 10, True),
                                   (32, 672, 16, 16, 28, True), (5, 300, 3, 3, 75, False),
                                   (2, 144, 64, 64, 6, True)])
-def test_bn_swish_se_fused(case):
+def test_bn_swish_se_fused(case, bn_path):
     """MBConv _bn1 -> swish -> SE with the BN + swish applied on load by the SE kernels
     (e2ep_bn_stats + se x_scale/x_shift; backward through e2ep_bn_bwd gate_logit /
     gate_dpooled), train and eval, vs fp64 torch: output, every gradient, running stats."""
