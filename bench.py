@@ -6,7 +6,10 @@ encoder -> fusion -> seg/depth heads -> control decoder), the control + segmenta
 losses, backward, and the Adam(lr 1e-4, wd 1e-4) update (:116-121), fp32, on a synthetic
 B-sample batch (4 x 256x256 cameras) that is resident in HBM before timing.
 
-    python bench.py [--gpus N --steps K --warmup W --batch B]
+    python bench.py [--gpus N --steps K --warmup W --batch B] [--precision bf16] [--workload c4]
+--precision bf16 is BASELINE configs[2] (C3); --workload c4 is configs[3] (6 cams x 512^2, B=4
+per GPU; its own metric name, no lift-splat / step roofline entries).  The default is the
+metric's configuration, configs[1] (C2).
 N>1: one rank per GPU, RCCL over xGMI.  Under torch.distributed.run (WORLD_SIZE set) the ranks
 are already there; from a plain command line `--gpus N` re-launches this script under
 torch.distributed.run with N ranks before anything touches the GPU.  Each rank runs B samples
@@ -35,6 +38,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "train samples/sec (4-cam frames) at B=8, 1/2/4/8 MI355X; CPU-ref baseline"
+METRIC_C4 = "train samples/sec (6-cam 512x512 frames, C4) at B=4 per MI355X; CPU-ref baseline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = the f32 vector rate
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 / fp16
@@ -186,18 +190,21 @@ def host_cores():
     return n, model
 
 
-def cpu_baseline(batch, steps, warmup, threads):
+def cpu_baseline(batch, steps, warmup, threads, hires=False):
     """The oracle (CPU restatement of the reference, bit-identical to it in the build
     container) running the same train step on the host cores: `warmup` untimed steps, then
-    the median of `steps` timed steps."""
+    the median of `steps` timed steps.  hires: the C4 rig (6 x 512^2)."""
     from oracle import parking_ref as O
     from e2ep_amd import synthetic
 
+    class CfgC4(O.Cfg):
+        final_dim = [512, 512]
+
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    m = O.ParkingModelRef(O.Cfg).train()
+    m = O.ParkingModelRef(CfgC4 if hires else O.Cfg).train()
     opt = O.make_optimizer(m)
-    data = synthetic.synthetic_batch(batch, seed=0)
+    data = synthetic.synthetic_batch(batch, seed=0, hires=hires)
     for _ in range(warmup):
         O.train_step(m, opt, data)
     ts = []
@@ -241,7 +248,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8, help="samples per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="samples per GPU per step (default 8; 4 for --workload c4)")
+    ap.add_argument("--workload", choices=("c2", "c4"), default="c2",
+                    help="c2: 4 cams x 256^2 (BASELINE configs[1], the metric's config); c4: the "
+                         "hi-res rig, 6 cams x 512^2, B=4 per GPU (configs[3])")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (median)")
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -250,6 +261,9 @@ def main():
                     help="conv GEMM operands: fp32 (C2, default) or bf16 (C3: bf16 forward / "
                          "data-gradient conv operands, fp32 weight gradients and everything else)")
     args = ap.parse_args()
+    hires = args.workload == "c4"
+    if args.batch is None:
+        args.batch = 4 if hires else 8
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch(args.gpus))
@@ -282,12 +296,13 @@ def main():
     _lib.load()
     precision.set(args.precision)
     torch.manual_seed(1234)  # identical initial weights on every rank
-    mod = ParkingTrainingModule(default_cfg()).to(dev).train()
+    cfg = default_cfg(final_dim=[512, 512], image_crop=512) if hires else default_cfg()
+    mod = ParkingTrainingModule(cfg).to(dev).train()
     # bev_encoder.layer4 is built but never run (reference model/bev_encoder.py:21,23-36):
     # it never has a gradient, so it is kept out of the reducer and the optimizer step.
     for p in mod.parking_model.bev_encoder.layer4.parameters():
         p.requires_grad_(False)
-    data = device_batch(synthetic.synthetic_batch(args.batch, seed=rank), dev)
+    data = device_batch(synthetic.synthetic_batch(args.batch, seed=rank, hires=hires), dev)
     if world > 1:  # identical initial weights on every rank (DDP's init broadcast)
         for t in list(mod.parameters()) + list(mod.buffers()):
             dist.broadcast(t.data, 0)
@@ -348,7 +363,7 @@ def main():
                 "timing": "HIP events around every conv fwd/dgrad launch of 3 eager fwd+bwd "
                           "passes on the launch stream; FLOPs = 2*N*Cout*P*Q*Cin*R*S per launch"}
     step_tfs = STEP_GFLOP_PER_SAMPLE * 1e9 * args.batch / (ms_step * 1e-3) / 1e12
-    step_roofline = {"bound": "mfma", "achieved": round(step_tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
+    step_roofline = None if hires else {"bound": "mfma", "achieved": round(step_tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": round(step_tfs / FP32_MFMA_PEAK_TFS, 4),
                      "flop_per_sample": STEP_GFLOP_PER_SAMPLE * 1e9,
                      "basis": "3 x 29.94 GFLOP forward per sample (SURVEY.md §8d) x B per GPU "
@@ -356,7 +371,7 @@ def main():
 
     mean_ms, n_fwd = lss_fwd_kernel_ms(mod.parking_model.bev_model._plan, dev)
     achieved = lss_fwd_bytes(args.batch) / (mean_ms * 1e-3) / 1e9
-    roofline_lss = {"kernel": "e2ep::k_lss_fwd (fused depth x feature outer product + pillar "
+    roofline_lss = None if hires else {"kernel": "e2ep::k_lss_fwd (fused depth x feature outer product + pillar "
                               "pooling, the north-star lift-splat kernel)",
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -375,22 +390,26 @@ def main():
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads, cpu_model = host_cores()
-        v, med, ts = cpu_baseline(args.batch, args.cpu_steps, args.cpu_warmup, threads)
+        # C4 CPU steps take ~4x a C2 one: a bounded sample of B=1 steps (samples/s is per sample)
+        cb = 1 if hires else args.batch
+        cs, cw = (3, 1) if hires else (args.cpu_steps, args.cpu_warmup)
+        v, med, ts = cpu_baseline(cb, cs, cw, threads, hires)
         base = {"value": round(v, 4), "unit": "samples/s", "cores": threads, "kind": "port",
                 "cpu_model": cpu_model,
-                "sample": f"median of {args.cpu_steps} timed train steps (after {args.cpu_warmup} "
-                          f"warm-up) of the oracle CPU restatement at B={args.batch}, 4x256^2, fp32, "
+                "sample": f"median of {cs} timed train steps (after {cw} warm-up) of the oracle CPU "
+                          f"restatement at B={cb}, {'6x512^2' if hires else '4x256^2'}, fp32, "
                           f"{threads} threads; step times "
                           + ", ".join(f"{t:.2f}" for t in ts) + " s"}
 
     if rank == 0:
-        line = {"metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world,
+        line = {"metric": METRIC_C4 if hires else METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms_step, 3), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None,
                 "dtype": "bf16" if lowp else "f32", "data": "synthetic",
                 "config": {"workload": "ParkingModel train step (fwd + control/seg/depth losses + bwd "
-                                       "+ Adam), 4 cams x 256x256, " +
+                                       "+ Adam), " + ("6 cams x 512x512 (C4), " if hires else
+                                                      "4 cams x 256x256, ") +
                                        ("bf16 conv operands in forward / data gradient, fp32 "
                                         "weight gradients, optimizer and all-reduce (C3)"
                                         if lowp else "fp32") + ", random init",

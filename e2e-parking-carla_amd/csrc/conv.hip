@@ -1298,7 +1298,8 @@ static int g_conv_precision = 0;  // GEMM operand precision: 0 fp32, 1 bf16, 2 f
 static int g_wgrad_kb = 16;       // k_conv_wgrad pixels per K-step (e2ep_conv_wgrad_kstep)
 static int g_gemm_variant = 0;  // 0 auto, 1 always k_conv_gemm, 2 k_conv_gemm2 wherever it
                                 // applies, 3 the same with 128-column tiles only, 4 auto with
-                                // the 1x1 forward / data gradient on the batched k_gemm
+                                // the 1x1 forward / data gradient on the batched k_gemm, 5 the
+                                // same for maps of <= 1024 pixels only
 
 // live taps of the largest phase and the column count (as plan_gemm)
 static void gemm_extent(int mode, const ConvGeom &g, int &taps_max, long long &ncols, int &nph) {
@@ -1339,7 +1340,7 @@ static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt
   const long long b256 = cdiv(ncols, 256) * mblocks * nph, b128 = cdiv(ncols, 128) * mblocks * nph;
   const long long slots = 2LL * 256;  // 64 x 256 tiles resident per round (2 per CU)
   const bool fill256 = b256 >= slots && 100 * b256 >= 95 * (cdiv(b256, slots) * slots);
-  if (g_gemm_variant == 0 || g_gemm_variant == 4) {
+  if (g_gemm_variant == 0 || g_gemm_variant >= 4) {
     if (g.R * g.S == 1 || M < 40) return false;
     if (!fill256 && b128 < 1024) return false;
     wnt = fill256 ? 4 : 2;
@@ -1365,7 +1366,8 @@ static bool plan_gemm2(int mode, const ConvGeom &g, int M, GemmPlan &p, int &wnt
 // fp32 only.
 static bool conv1x1_gemm_ok(int mode, const ConvGeom &g) {
   (void)mode;
-  return g_gemm_variant == 4 && g_conv_precision == 0 && g.R == 1 && g.S == 1 && g.sh == 1 &&
+  return (g_gemm_variant == 4 || (g_gemm_variant == 5 && g.H * g.W <= 1024)) &&
+         g_conv_precision == 0 && g.R == 1 && g.S == 1 && g.sh == 1 &&
          g.sw == 1 && g.ph == 0 && g.pw == 0 && (g.H * g.W) % 32 == 0 &&
          4LL * g.N * std::max(g.Cin, g.Cout) * g.H * g.W < 0x7fffffffLL;
 }
@@ -1507,7 +1509,7 @@ int e2ep_conv_wgrad_kstep(int pixels) {
 
 int e2ep_conv_gemm_variant(int variant) {
   const int old = g_gemm_variant;
-  if (variant >= 0 && variant <= 4) g_gemm_variant = variant;
+  if (variant >= 0 && variant <= 5) g_gemm_variant = variant;
   return old;
 }
 

@@ -130,6 +130,8 @@ def load():
                          f"`make -C e2e-parking-carla_amd/csrc` or __graft_entry__.build().")
         raise _ERR
     _LIB = lib
+    if os.environ.get("E2EP_CONV_VARIANT"):  # A/B timing of the conv GEMM kernel choice
+        lib.e2ep_conv_gemm_variant(int(os.environ["E2EP_CONV_VARIANT"]))
     return lib
 
 

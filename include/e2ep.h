@@ -168,7 +168,8 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
  * 1 = always the first-generation kernel, 2 = the second-generation kernel (k-contiguous LDS
  * fragments, no padded channel steps) wherever its limits allow, 3 = the same with 128-column
  * tiles only, 4 = automatic but the 1x1 forward / data gradient on the column-batched GEMM of
- * e2ep_gemm.  Returns the previous value; a value outside 0..4 only queries.  Process-global; not thread-safe against concurrent
+ * e2ep_gemm, 5 = the same for maps of at most 1024 pixels only.  Returns the previous value;
+ * a value outside 0..5 only queries.  Process-global; not thread-safe against concurrent
  * launches. */
 int e2ep_conv_gemm_variant(int variant);
 /* Operand precision of the conv GEMMs: 0 = fp32 (default; exact-f32 MFMA), 1 = bf16, 2 = fp16

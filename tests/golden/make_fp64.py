@@ -6,8 +6,8 @@ Deterministic-train mode (BN batch statistics at B=2) is ill-conditioned: the re
 own fp32 result differs from this fp64 value by ~1e-3 on the segmentation logits and ~2 %
 on some weight gradients (the cumsum-difference pooling noise, SURVEY.md §0 fact 4, is
 amplified by batch-statistic BN).  Parity tests therefore measure both the product and the
-reference against this fp64 value.   Run: python tests/golden/make_fp64.py [b8]
-(b8: the same for the B=8 bench batch, model_train_b8.npz.)
+reference against this fp64 value.   Run: python tests/golden/make_fp64.py [b8|c4]
+(b8: the same for the B=8 bench batch, model_train_b8.npz; c4: model_train_c4.npz.)
 """
 import os
 import sys
@@ -24,9 +24,9 @@ from e2ep_amd import synthetic  # noqa: E402
 from weights import make_grad_probe_keys, make_state  # noqa: E402
 
 
-def oracle_model(dtype):
+def oracle_model(dtype, cfg=O.Cfg):
     torch.manual_seed(0)
-    m = O.ParkingModelRef(O.Cfg, dropout=False)
+    m = O.ParkingModelRef(cfg, dropout=False)
     m.load_state_dict(make_state(m.state_dict(), 1234))
     keep = {k: v.detach().clone() for k, v in m.bev_model.named_parameters(recurse=False)}
     m = m.to(dtype)
@@ -107,8 +107,42 @@ def main():
     print("wrote model_train_b2_fp64.npz")
 
 
+def main_c4():
+    """fp64 companion of model_train_c4.npz (C4: 6 cameras at 512x512, B=1)."""
+    torch.set_num_threads(8)
+
+    class CfgC4(O.Cfg):
+        final_dim = [512, 512]
+
+    import json
+    with open(os.path.join(HERE, "meta.json")) as f:
+        meta = json.load(f)
+    data = synthetic.synthetic_batch(1, seed=13, hires=True)
+    noise = synthetic.target_noise(1, seed=13)
+    d = {k: (v.double() if v.is_floating_point() and k not in ("intrinsics", "extrinsics") else v)
+         for k, v in data.items()}
+    for mode, name in (("train", "model_train_c4"), ("eval", "model_evalgrad_c4")):
+        m = oracle_model(torch.float64, CfgC4)
+        m.train(mode == "train")
+        losses, (pc, ps, pd) = O.train_losses(m, d, noise)
+        losses["train_loss"].backward()
+        params = dict(m.named_parameters())
+        fx = {"loss_control": np.float64(losses["control_loss"].item()),
+              "loss_seg": np.float64(losses["segmentation_loss"].item()),
+              "loss_depth": np.float64(losses["depth_loss"].item()),
+              "gnorm_all": np.array([float(params[k].grad.norm()) for k in meta[name]["grad_keys"]])}
+        if mode == "train":
+            fx.update(pred_control=pc.detach().numpy(),
+                      seg_slice=ps.detach()[:, :, 90:110, 90:110].numpy(),
+                      depth_slice=pd.detach()[:, :, 10:14].numpy())
+        np.savez_compressed(os.path.join(HERE, name + "_fp64.npz"), **fx)
+        print("wrote", name + "_fp64.npz")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "b8":
         main_b8()
+    elif len(sys.argv) > 1 and sys.argv[1] == "c4":
+        main_c4()
     else:
         main()

@@ -1,7 +1,8 @@
 """Generate the golden vectors under tests/golden/ FROM THE REFERENCE ITSELF.
 
 Run in the build container only (needs /root/reference):  python tests/golden/make_golden.py
-(`python tests/golden/make_golden.py b8` regenerates only the B=8 fixtures.)
+(`python tests/golden/make_golden.py b8` regenerates only the B=8 fixtures, `... c4` adds the
+C4 6-camera 512x512 fixtures.)
 
 The reference has no tests or fixtures of its own, so every golden vector is
 produced here by importing the reference's Python modules unmodified, with:
@@ -209,6 +210,77 @@ def b8_fixtures(ref, orc, state, cfg, closs, sloss, dloss, meta):
                               "oracle_grad_rel_err_max": max(gerr.values())}
 
 
+def c4_fixtures(cfg, meta):
+    """BASELINE configs[3] (C4: 6 cameras at 512x512, B=1) through the full reference model:
+    eval forward + predict, and one deterministic-train forward/backward (losses, output
+    slices, probed gradient norms).  The oracle must reproduce the reference first."""
+    from model.parking_model import ParkingModel
+    from loss.control_loss import ControlLoss
+    from loss.seg_loss import SegmentationLoss
+    from loss.depth_loss import DepthLoss
+    cfg.final_dim = [512, 512]
+    cfg.image_crop = 512
+    torch.manual_seed(0)
+    ref = ParkingModel(cfg)
+    state = make_state(ref.state_dict(), seed=1234)
+    ref.load_state_dict(state)
+
+    class CfgC4(O.Cfg):
+        final_dim = [512, 512]
+
+    orc = O.ParkingModelRef(CfgC4, dropout=False)
+    orc.load_state_dict(state)
+    data = synthetic.synthetic_batch(1, seed=13, hires=True)
+    noise = synthetic.target_noise(1, seed=13)
+    ref.eval(), orc.eval()
+    with torch.no_grad(), FixedRand(noise):
+        pc, ps, pd = ref(data)
+        tok, _, _, tgt = ref.predict({**data, "gt_control": data["gt_control"][:, :1]})
+    with torch.no_grad():
+        qc, qs, qd = orc(data, noise)
+    errs = {"control": rel(qc, pc), "seg": rel(qs, ps), "depth": rel(qd, pd)}
+    print("C4 oracle vs reference, eval:", errs)
+    assert max(errs.values()) < 1e-6
+    np.savez_compressed(os.path.join(OUT, "model_eval_c4.npz"), pred_control=pc.numpy(),
+                        pred_segmentation=ps.numpy(), pred_depth=pd.numpy(), predict_tokens=tok.numpy(),
+                        bev_target=tgt.numpy())
+    meta["model_eval_c4"] = {"batch_seed": 13, "noise_seed": 13, "hires": True, "oracle_rel_err": errs}
+
+    deterministic(ref)
+    closs, dloss = ControlLoss(cfg), DepthLoss(cfg)
+    sloss = SegmentationLoss(class_weights=torch.Tensor(cfg.seg_vehicle_weights))
+    # eval-mode gradients (BN on running statistics): the well-conditioned full backward
+    ref.load_state_dict(state)
+    ref.eval()
+    with FixedRand(noise):
+        pc, ps, pd = ref(data)
+    lc, ls, ld = closs(pc, data), sloss(ps.unsqueeze(1), data["segmentation"]), dloss(pd, data["depth"])
+    (lc + ls + ld).backward()
+    rgrad = dict(ref.named_parameters())
+    gkeys_e = [k for k, v in rgrad.items() if v.grad is not None]
+    np.savez_compressed(os.path.join(OUT, "model_evalgrad_c4.npz"),
+                        loss_control=np.float64(lc), loss_seg=np.float64(ls), loss_depth=np.float64(ld),
+                        gnorm_all=np.array([float(rgrad[k].grad.double().norm()) for k in gkeys_e]))
+    meta["model_evalgrad_c4"] = {"batch_seed": 13, "noise_seed": 13, "hires": True, "grad_keys": gkeys_e}
+    ref.zero_grad(set_to_none=True)
+    # deterministic train (BN batch statistics over 6 cameras)
+    ref.load_state_dict(state)
+    ref.train()
+    with FixedRand(noise):
+        pc, ps, pd = ref(data)
+    lc, ls, ld = closs(pc, data), sloss(ps.unsqueeze(1), data["segmentation"]), dloss(pd, data["depth"])
+    (lc + ls + ld).backward()
+    rgrad = dict(ref.named_parameters())
+    gkeys = [k for k, v in rgrad.items() if v.grad is not None]
+    fx = {"loss_control": np.float64(lc), "loss_seg": np.float64(ls), "loss_depth": np.float64(ld),
+          "pred_control": pc.detach().numpy(),
+          "seg_slice": ps.detach()[:, :, 90:110, 90:110].numpy(),
+          "depth_slice": pd.detach()[:, :, 10:14].numpy(),
+          "gnorm_all": np.array([float(rgrad[k].grad.double().norm()) for k in gkeys])}
+    np.savez_compressed(os.path.join(OUT, "model_train_c4.npz"), **fx)
+    meta["model_train_c4"] = {"batch_seed": 13, "noise_seed": 13, "hires": True, "grad_keys": gkeys}
+
+
 def main(only=None):
     install_shims()
     torch.set_num_threads(8)
@@ -225,6 +297,14 @@ def main(only=None):
     cfg.device = torch.device("cpu")
     meta = {"generator": "tests/golden/make_golden.py", "reference": REF,
             "torch": torch.__version__, "weights_seed": 1234}
+    if only == "c4":  # add the C4 fixtures, keep the others and their meta
+        with open(os.path.join(OUT, "meta.json")) as f:
+            meta = json.load(f)
+        c4_fixtures(cfg, meta)
+        with open(os.path.join(OUT, "meta.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+        print("wrote C4 golden vectors to", OUT)
+        return
     if only == "b8":  # regenerate only the B=8 fixtures, keep the others and their meta
         with open(os.path.join(OUT, "meta.json")) as f:
             meta = json.load(f)

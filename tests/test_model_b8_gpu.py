@@ -89,6 +89,9 @@ def _norms3(section, gkeys, params, n32, n64):
     _record(section, "grad_norms(all %d)" % len(gkeys), vs_ref_max=e32.max(), vs_fp64_max=e64.max(),
             ref_vs_fp64_max=eref.max(), vs_fp64_median=np.median(e64),
             ref_vs_fp64_median=np.median(eref), worst_ratio_to_bound=e64[worst] / bound[worst])
+    top = len(gkeys) if os.environ.get("E2EP_PARITY_ALL") == "1" else 8
+    for i in np.argsort(-(e64 / bound))[:top]:  # the tensors closest to (or past) their bound
+        _record(section + "_worst", gkeys[i], vs_fp64=e64[i], ref_vs_fp64=eref[i], bound=bound[i])
     assert (e64 <= bound).all(), (gkeys[worst], e64[worst], eref[worst])
 
 
