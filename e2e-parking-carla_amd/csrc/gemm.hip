@@ -300,6 +300,70 @@ __global__ void __launch_bounds__(256)
   if (V == 4) *reinterpret_cast<float4 *>(C + i) = make_float4(s[0], s[1], s[2], s[3]);
 }
 
+// Skinny GEMM for the forward layout with few rows (M <= g_skinny_rows, at most SK_ROWS: the
+// control decoder's 14 token rows in C5 predict): C[m][n] = sum_k A[m*lda + k]
+// B[n*ldb + k] (+ bias[n]) (+ Cadd) (ReLU).  One block per (output column n, chunk of
+// SK_MAXM rows); lanes stride k (float2 when lda, ldb are even and the bases 8-byte aligned),
+// each lane keeps SK_MAXM partial dot products; fixed-order wave, then block, reductions.  The
+// MFMA tiles (32 x 128 at the least) left those launches a chain of K-steps on a dozen blocks
+// (15 us for a 14 x 2048 x 258 product).
+constexpr int SK_MAXM = 16, SK_ROWS = 128;
+template <int V>
+__global__ void __launch_bounds__(256) k_gemm_skinny(
+    const float *__restrict__ A, int lda, const float *__restrict__ B, int ldb,
+    const float *__restrict__ bias, const float *__restrict__ Cadd, int ldadd,
+    float *__restrict__ C, int ldc, int M, int N, int K, int relu) {
+  __shared__ float red[4][SK_MAXM];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = blockIdx.x;
+  const int m0 = blockIdx.y * SK_MAXM;
+  A += (size_t)m0 * lda;
+  C += (size_t)m0 * ldc;
+  if (Cadd) Cadd += (size_t)m0 * ldadd;
+  M = min(M - m0, SK_MAXM);
+  float acc[SK_MAXM];
+#pragma unroll
+  for (int m = 0; m < SK_MAXM; ++m) acc[m] = 0.f;
+  const float *brow = B + (size_t)n * ldb;
+  for (int k = (wave * 64 + lane) * V; k < K; k += 256 * V) {
+    if (V == 2 && k + 1 < K) {
+      const float2 b = *reinterpret_cast<const float2 *>(brow + k);
+      float2 a[SK_MAXM];
+#pragma unroll
+      for (int m = 0; m < SK_MAXM; ++m)
+        a[m] = *reinterpret_cast<const float2 *>(A + (size_t)min(m, M - 1) * lda + k);
+#pragma unroll
+      for (int m = 0; m < SK_MAXM; ++m) {
+        acc[m] = fmaf(a[m].x, b.x, acc[m]);
+        acc[m] = fmaf(a[m].y, b.y, acc[m]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if (k + j >= K) break;
+        const float b = brow[k + j];
+#pragma unroll
+        for (int m = 0; m < SK_MAXM; ++m)
+          acc[m] = fmaf(A[(size_t)min(m, M - 1) * lda + k + j], b, acc[m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < SK_MAXM; ++m) {
+    const float v = wave_sum(acc[m]);
+    if (lane == 0) red[wave][m] = v;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < M) {
+    const int m = threadIdx.x;
+    float v = (red[0][m] + red[1][m]) + (red[2][m] + red[3][m]);
+    if (bias) v += bias[n];
+    if (Cadd) v += Cadd[(size_t)m * ldadd + n];
+    if (relu) v = fmaxf(v, 0.f);
+    C[(size_t)m * ldc + n] = v;
+  }
+}
+
 struct GemmLaunch {
   int tile, splits, kper;
 };
@@ -328,6 +392,10 @@ static GemmTile tile_dims(int tile) {
 // a multiple of 64 and 32-row tiles pad it less (M = 32, 112, 144, 160, 336 ...); K split
 // toward ~768 workgroups (3 per CU), at most 8 ways and >= 8 K-steps each.
 static int g_force_tile = 0, g_force_splits = 0;  // 0: automatic
+// e2ep_gemm_skinny: few-row forward products up to this M.  16 (the decoder at B = 1): C5
+// predict fp16 4.84 -> 4.28 ms p50; the C2 step's 112-row decoder measured slower on it (25.66
+// vs 25.39 ms/step, profiles/r02/session6/skinny_ab.txt), so it stays on the MFMA tiles.
+static int g_skinny_rows = 16;
 
 static GemmLaunch gemm_plan(int M, int N, int K) {
   GemmLaunch p{1, 1, 1};
@@ -363,6 +431,10 @@ static int vec_of(bool kc, int ld, const void *ptr) {
   return ld % 2 == 0 && ((uintptr_t)ptr & 7) == 0 ? 1 : 0;
 }
 
+static bool skinny_ok(bool ak, bool bk, bool bias_rows, GemmCols cols, int M, float *rs) {
+  return ak && bk && !bias_rows && cols.hw == 0 && !rs && M <= g_skinny_rows && g_force_tile == 0;
+}
+
 int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B, int ldb,
              bool bk, long long b_bytes, const float *bias, bool bias_rows, const float *Cadd,
              int ldadd, float *C, long long c_bytes, int ldc, GemmCols cols, int M, int N, int K,
@@ -370,6 +442,17 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
   if (rs && (ak || bk || cols.hw)) {
     set_error("gemm: the row sum of A needs a k-major A, a row-contiguous B, unbatched C");
     return E2EP_EINVAL;
+  }
+  if (skinny_ok(ak, bk, bias_rows, cols, M, rs)) {
+    const bool v2 = lda % 2 == 0 && ldb % 2 == 0 && ((uintptr_t)A & 7) == 0 && ((uintptr_t)B & 7) == 0;
+    const dim3 grid(N, cdiv(M, SK_MAXM));
+    if (v2)
+      hipLaunchKernelGGL(k_gemm_skinny<2>, grid, dim3(256), 0, s, A, lda, B, ldb, bias, Cadd, ldadd,
+                         C, ldc, M, N, K, relu);
+    else
+      hipLaunchKernelGGL(k_gemm_skinny<1>, grid, dim3(256), 0, s, A, lda, B, ldb, bias, Cadd, ldadd,
+                         C, ldc, M, N, K, relu);
+    return 0;
   }
   const int Nx = rs ? N + 1 : N;  // logical columns including the ones column
   const GemmLaunch p = gemm_plan(M, Nx, K);
@@ -435,6 +518,12 @@ int e2ep_gemm_force(int tile, int splits, int unused) {
 }
 
 size_t e2ep_gemm_workspace(int M, int N, int K) { return gemm_ws(M, N, K); }
+
+int e2ep_gemm_skinny(int max_rows) {
+  const int prev = g_skinny_rows;
+  if (max_rows >= 0) g_skinny_rows = std::min(max_rows, SK_ROWS);
+  return prev;
+}
 size_t e2ep_gemm_rowsum_workspace(int M, int N, int K) { return gemm_ws(M, N + 1, K); }
 
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,

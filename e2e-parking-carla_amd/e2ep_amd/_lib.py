@@ -96,6 +96,7 @@ SIGNATURES = {
     "e2ep_depth_bce_fwd_f64": (_i, [_p, _p, _i, _i, _i, _i, _i, _d, _d, _p, _p, _p, _p, _p]),
     "e2ep_gemm_workspace": (_sz, [_i, _i, _i]),
     "e2ep_gemm_force": (_i, [_i, _i, _i]),
+    "e2ep_gemm_skinny": (_i, [_i]),
     "e2ep_bn_small": (_i, [_i]),
     "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_gemm_rowsum_workspace": (_sz, [_i, _i, _i]),
@@ -132,6 +133,8 @@ def load():
     _LIB = lib
     if os.environ.get("E2EP_CONV_VARIANT"):  # A/B timing of the conv GEMM kernel choice
         lib.e2ep_conv_gemm_variant(int(os.environ["E2EP_CONV_VARIANT"]))
+    if os.environ.get("E2EP_GEMM_SKINNY"):  # A/B timing of the few-row GEMM path
+        lib.e2ep_gemm_skinny(int(os.environ["E2EP_GEMM_SKINNY"]))
     return lib
 
 

@@ -469,6 +469,11 @@ size_t e2ep_gemm_workspace(int M, int N, int K);
 /* Benchmarking override of the launch plan: block tile 1 = 64x64, 2 = 32x128, 3 = 128x128,
  * 4 = 64x128, 5 = 128x64, 6 = 64x256 (0 = the automatic plan), and the K split. */
 int e2ep_gemm_force(int tile, int splits, int unused);
+/* Few-row forward products (a_kcontig and b_kcontig, M <= max_rows, at most 128; default 16)
+ * run on a block-per-output-column dot-product kernel instead of the MFMA tiles (the control
+ * decoder's 14 rows at B = 1, C5 predict); 0 disables it, < 0 only queries.  Returns the
+ * previous limit. */
+int e2ep_gemm_skinny(int max_rows);
 
 /* BatchNorm single-launch switch: on = 1 (default) lets e2ep_bn_fwd / e2ep_bn_stats /
  * e2ep_bn_bwd run channels of N*H*W <= 32768 (H*W % 4 == 0, training statistics) as one

@@ -2,7 +2,7 @@
 PyTorch: every operand layout the linear uses (forward (A k-contig, B k-contig), input
 gradient (A k-contig, B n-contig), weight gradient (A m-contig, B n-contig)) plus the fourth,
 at the transformer shapes of the C2 step (2048 encoder rows, 112 decoder rows, d = 258, FFN
-2048) and ragged edges (M, N, K not multiples of the tiles; K = 1..3).
+2048), the C5 decoder's 14 rows (the skinny wave-per-column kernel for M <= 16) and ragged edges (M, N, K not multiples of the tiles; K = 1..3).
 Tolerance: rel-L2 <= 2e-6 against fp64 (fp32 MFMA products are exact, accumulation is
 fp32 over at most 2048 terms); split-K results bitwise identical across launches."""
 import pytest
@@ -15,7 +15,7 @@ DEV = "cuda"
 
 SHAPES = [(2048, 774, 258), (2048, 258, 2048), (258, 2048, 2048), (774, 258, 2048),
           (112, 516, 258), (112, 204, 258), (8, 64, 3), (8, 256, 128), (1, 1, 1), (65, 130, 17),
-          (3, 5, 700), (200, 3, 64)]
+          (3, 5, 700), (200, 3, 64), (14, 2048, 258), (16, 258, 2048), (14, 205, 258)]
 
 
 def _operands(M, N, K, ak, bk, g):
@@ -61,7 +61,8 @@ def test_gemm_every_tile_and_split(tile, ak, bk):
         _lib.call("e2ep_gemm_force", 0, 0, 0)
 
 
-@pytest.mark.parametrize("M,N,K", [(2048, 258, 258), (112, 204, 258), (37, 70, 2048)])
+@pytest.mark.parametrize("M,N,K", [(2048, 258, 258), (112, 204, 258), (37, 70, 2048),
+                                   (14, 2048, 258), (15, 258, 2048), (7, 33, 17)])
 def test_gemm_epilogue_bias_add_relu(M, N, K):
     from e2ep_amd import nn_ops
     g = torch.Generator().manual_seed(M + N + K)
