@@ -392,6 +392,10 @@ static GemmTile tile_dims(int tile) {
 // a multiple of 64 and 32-row tiles pad it less (M = 32, 112, 144, 160, 336 ...); K split
 // toward ~768 workgroups (3 per CU), at most 8 ways and >= 8 K-steps each.
 static int g_force_tile = 0, g_force_splits = 0;  // 0: automatic
+// K-steps per split for grids under 64 blocks (e2ep_gemm_split_min).  8, 4 and 2 measured
+// the same C2 step within noise (25.52 / 25.49 / 25.44 ms, profiles/r02/session6/
+// gemm_split_min_ab.txt): the default stays 8.
+static int g_split_min_small = 8;
 // e2ep_gemm_skinny: few-row forward products up to this M.  16 (the decoder at B = 1): C5
 // predict fp16 4.84 -> 4.28 ms p50; the C2 step's 112-row decoder measured slower on it (25.66
 // vs 25.39 ms/step, profiles/r02/session6/skinny_ab.txt), so it stays on the MFMA tiles.
@@ -407,7 +411,11 @@ static GemmLaunch gemm_plan(int M, int N, int K) {
     if (cdiv(M, 32) * 32 < cdiv(M, 64) * 64) p.tile = 2;
     const GemmTile t = tile_dims(p.tile);
     const long long blocks = (long long)cdiv(M, t.bm) * cdiv(N, t.bn);
-    const int cap = std::min(8, std::max(1, ksteps / 8));
+    // tiny grids (the decoder's 112-row products: a dozen blocks) are a chain of K-steps, so
+    // they may split down to g_split_min_small steps per split (e2ep_gemm_split_min)
+    const long long nb = (long long)cdiv(M, t.bm) * cdiv(N, t.bn);
+    const int smin = nb < 64 ? g_split_min_small : 8;
+    const int cap = std::min(nb < 64 ? 16 : 8, std::max(1, ksteps / smin));
     p.splits = (int)std::min<long long>(cap, std::max(1LL, (long long)cdiv(768, blocks)));
   }
   p.kper = cdiv(ksteps, p.splits);
@@ -518,6 +526,12 @@ int e2ep_gemm_force(int tile, int splits, int unused) {
 }
 
 size_t e2ep_gemm_workspace(int M, int N, int K) { return gemm_ws(M, N, K); }
+
+int e2ep_gemm_split_min(int ksteps) {
+  const int prev = g_split_min_small;
+  if (ksteps > 0) g_split_min_small = ksteps;
+  return prev;
+}
 
 int e2ep_gemm_skinny(int max_rows) {
   const int prev = g_skinny_rows;

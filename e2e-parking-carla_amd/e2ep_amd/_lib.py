@@ -97,6 +97,7 @@ SIGNATURES = {
     "e2ep_gemm_workspace": (_sz, [_i, _i, _i]),
     "e2ep_gemm_force": (_i, [_i, _i, _i]),
     "e2ep_gemm_skinny": (_i, [_i]),
+    "e2ep_gemm_split_min": (_i, [_i]),
     "e2ep_bn_small": (_i, [_i]),
     "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_gemm_rowsum_workspace": (_sz, [_i, _i, _i]),
@@ -135,6 +136,8 @@ def load():
         lib.e2ep_conv_gemm_variant(int(os.environ["E2EP_CONV_VARIANT"]))
     if os.environ.get("E2EP_GEMM_SKINNY"):  # A/B timing of the few-row GEMM path
         lib.e2ep_gemm_skinny(int(os.environ["E2EP_GEMM_SKINNY"]))
+    if os.environ.get("E2EP_GEMM_SPLIT_MIN"):  # A/B timing of small-grid K splits
+        lib.e2ep_gemm_split_min(int(os.environ["E2EP_GEMM_SPLIT_MIN"]))
     return lib
 
 

@@ -474,6 +474,9 @@ int e2ep_gemm_force(int tile, int splits, int unused);
  * decoder's 14 rows at B = 1, C5 predict); 0 disables it, < 0 only queries.  Returns the
  * previous limit. */
 int e2ep_gemm_skinny(int max_rows);
+/* Minimum K-steps (32 deep) per K split for grids under 64 blocks (default 8); <= 0 queries.
+ * Returns the previous value. */
+int e2ep_gemm_split_min(int ksteps);
 
 /* BatchNorm single-launch switch: on = 1 (default) lets e2ep_bn_fwd / e2ep_bn_stats /
  * e2ep_bn_bwd run channels of N*H*W <= 32768 (H*W % 4 == 0, training statistics) as one
