@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(ATT_WAVES * 64) k_attn_bwd_q(
     axpy_lds<DHP>(acc, pj * (dp - Di), sK + j * DHP);
   }
   if (LPQ > 1) lane_sum<LPQ, DHP>(acc);
-  if (w == 0 && sub == 0 && i < a.Sq) Dbuf[(long long)bh * a.Sq + i] = Di;
+  if (Dbuf && w == 0 && sub == 0 && i < a.Sq) Dbuf[(long long)bh * a.Sq + i] = Di;
   __syncthreads();
   constexpr int MS = DHP * 64;
   float *mrg = sm;  // [w][DHP][64], column = query within the block
@@ -497,6 +497,25 @@ static int relu_drop_check(const void *x, long long n, float p, const int32_t *s
 
 using namespace e2ep;
 
+// D_i = dO_i . O_i per (batch*head, query), the same fma chain as k_attn_bwd_q computes for
+// its own rows, so k_attn_bwd_kv can start without waiting for k_attn_bwd_q
+template <int DHP>
+__global__ void __launch_bounds__(256) k_attn_bwd_d(const float *__restrict__ o,
+                                                    const float *__restrict__ dout, AttnDims a,
+                                                    float *__restrict__ Dbuf) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= a.B * a.H * a.Sq) return;
+  const int bh = t / a.Sq, i = t - bh * a.Sq, b = bh / a.H, h = bh - b * a.H;
+  const long long orow = (long long)b * a.o_sb + h * a.dh + (long long)i * a.o_ss;
+  float dor[DHP], orr[DHP];
+  load_row<DHP>(dor, dout + orow, a.dh, 1.f);
+  load_row<DHP>(orr, o + orow, a.dh, 1.f);
+  float Di = 0.f;
+#pragma unroll
+  for (int d = 0; d < DHP; ++d) Di = __builtin_fmaf(dor[d], orr[d], Di);
+  Dbuf[t] = Di;
+}
+
 extern "C" {
 
 int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, int Sq, int Sk,
@@ -523,33 +542,60 @@ int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, 
 
 size_t e2ep_attn_bwd_workspace(int B, int H, int Sq) { return (size_t)B * H * Sq * sizeof(float); }
 
-int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o, const float *dout,
-                  const float *lse, int B, int H, int Sq, int Sk, int dh, int q_ss, int q_sb,
-                  int kv_ss, int kv_sb, int o_ss, int o_sb, float scale, int causal,
-                  const uint8_t *key_pad, float p, const int32_t *seed, float *dq, float *dk,
-                  float *dv, void *workspace, void *stream) {
+int e2ep_attn_bwd_part(const float *q, const float *k, const float *v, const float *o,
+                       const float *dout, const float *lse, int B, int H, int Sq, int Sk, int dh,
+                       int q_ss, int q_sb, int kv_ss, int kv_sb, int o_ss, int o_sb, float scale,
+                       int causal, const uint8_t *key_pad, float p, const int32_t *seed, float *dq,
+                       float *dk, float *dv, void *workspace, int part, void *stream) {
+  E2EP_REQUIRE(part >= 0 && part <= 3, E2EP_EINVAL, "e2ep_attn_bwd_part: part must be 0..3");
   const AttnDims a = make_dims(B, H, Sq, Sk, dh, q_ss, q_sb, kv_ss, kv_sb, o_ss, o_sb, scale, causal, p);
   if (int rc = attn_check(a, "e2ep_attn_bwd")) return rc;
   E2EP_REQUIRE(p == 0.f || seed, E2EP_EINVAL, "e2ep_attn_bwd: dropout needs a seed");
   float *D = static_cast<float *>(workspace);
   hipStream_t s = as_stream(stream);
   const dim3 blk(ATT_WAVES * 64);
-#define E2EP_ATT_BQ(DHP, LPQ)                                                                    \
+#define E2EP_ATT_BQ(DHP, LPQ, DB)                                                                \
   hipLaunchKernelGGL((k_attn_bwd_q<DHP, LPQ>), dim3(cdiv(Sq, 64 / LPQ), B * H), blk, 0, s, q, k, v, \
-                     o, dout, lse, key_pad, seed, a, dq, D)
+                     o, dout, lse, key_pad, seed, a, dq, DB)
 #define E2EP_ATT_BKV(DHP, LPK)                                                                   \
   hipLaunchKernelGGL((k_attn_bwd_kv<DHP, LPK>), dim3(cdiv(Sk, 64 / LPK), B * H), blk, 0, s, q, k, \
                      v, dout, lse, D, key_pad, seed, a, dk, dv)
-  if (dh <= 44) {
-    if (Sq <= 16) E2EP_ATT_BQ(44, 4); else E2EP_ATT_BQ(44, ATT_LONG_LANES);
-    if (Sk <= 16) E2EP_ATT_BKV(44, 4); else E2EP_ATT_BKV(44, ATT_LONG_LANES);
-  } else {
-    if (Sq <= 16) E2EP_ATT_BQ(64, 4); else E2EP_ATT_BQ(64, ATT_LONG_LANES);
-    if (Sk <= 16) E2EP_ATT_BKV(64, 4); else E2EP_ATT_BKV(64, ATT_LONG_LANES);
+  // part 0: everything in order; 1: D only; 2: dq only (D already in the workspace); 3: dk, dv
+  // only (likewise) — parts 2 and 3 are independent and may run on two streams
+  if (part == 1) {
+    if (dh <= 44)
+      hipLaunchKernelGGL(k_attn_bwd_d<44>, dim3(cdiv(B * H * Sq, 256)), dim3(256), 0, s, o, dout, a, D);
+    else
+      hipLaunchKernelGGL(k_attn_bwd_d<64>, dim3(cdiv(B * H * Sq, 256)), dim3(256), 0, s, o, dout, a, D);
+    return launch_status("e2ep_attn_bwd");
+  }
+  float *Dq = part == 2 ? nullptr : D;  // dq pass alone: D is read by the other pass, not rewritten
+  if (part != 3) {
+    if (dh <= 44) {
+      if (Sq <= 16) E2EP_ATT_BQ(44, 4, Dq); else E2EP_ATT_BQ(44, ATT_LONG_LANES, Dq);
+    } else {
+      if (Sq <= 16) E2EP_ATT_BQ(64, 4, Dq); else E2EP_ATT_BQ(64, ATT_LONG_LANES, Dq);
+    }
+  }
+  if (part != 2) {
+    if (dh <= 44) {
+      if (Sk <= 16) E2EP_ATT_BKV(44, 4); else E2EP_ATT_BKV(44, ATT_LONG_LANES);
+    } else {
+      if (Sk <= 16) E2EP_ATT_BKV(64, 4); else E2EP_ATT_BKV(64, ATT_LONG_LANES);
+    }
   }
 #undef E2EP_ATT_BQ
 #undef E2EP_ATT_BKV
   return launch_status("e2ep_attn_bwd");
+}
+
+int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o, const float *dout,
+                  const float *lse, int B, int H, int Sq, int Sk, int dh, int q_ss, int q_sb,
+                  int kv_ss, int kv_sb, int o_ss, int o_sb, float scale, int causal,
+                  const uint8_t *key_pad, float p, const int32_t *seed, float *dq, float *dk,
+                  float *dv, void *workspace, void *stream) {
+  return e2ep_attn_bwd_part(q, k, v, o, dout, lse, B, H, Sq, Sk, dh, q_ss, q_sb, kv_ss, kv_sb, o_ss,
+                            o_sb, scale, causal, key_pad, p, seed, dq, dk, dv, workspace, 0, stream);
 }
 
 int e2ep_attn_keep_mask(const int32_t *seed, int BH, int Sq, int Sk, float p, uint8_t *out,

@@ -72,6 +72,7 @@ SIGNATURES = {
     "e2ep_attn_fwd": (_i, [_p, _p, _p] + [_i] * 11 + [_f, _i, _p, _f, _p, _p, _p, _p]),
     "e2ep_attn_bwd_workspace": (_sz, [_i, _i, _i]),
     "e2ep_attn_bwd": (_i, [_p] * 6 + [_i] * 11 + [_f, _i, _p, _f, _p, _p, _p, _p, _p, _p]),
+    "e2ep_attn_bwd_part": (_i, [_p] * 6 + [_i] * 11 + [_f, _i, _p, _f, _p, _p, _p, _p, _p, _i, _p]),
     "e2ep_attn_keep_mask": (_i, [_p, _i, _i, _i, _f, _p, _p]),
     "e2ep_softmax_c_fwd": (_i, [_p, _i, _i, _i, _p, _p]),
     "e2ep_softmax_c_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),

@@ -14,10 +14,17 @@ agent/parking_agent.py:71-80,266-268), a float attn_mask not declared causal, bi
 add_zero_attn, separate projection weights, or shapes outside the kernel's range.
 """
 import math
+import os
 
 import torch
 
-from . import _lib, nn_ops, rng, timing
+from . import _lib, conv, nn_ops, rng, timing
+
+# E2EP_ATTN_SPLIT=1: D first, then dq on the current stream and dk/dv on the side stream.  Off
+# by default: the C2 step measured 0.18 ms slower with it (25.58 vs 25.40 ms/step,
+# profiles/r02/session6/attn_split_ab.txt) — the two passes contend for the same CUs and the
+# extra D launch is on the critical path.
+_SPLIT_BWD = os.environ.get("E2EP_ATTN_SPLIT", "0") == "1"
 
 MAX_SEQ = 256
 MAX_HEAD_DIM = 64
@@ -65,11 +72,21 @@ class _Attn(torch.autograd.Function):
         dkptr = dkvt.data_ptr() + 4 * k_off
         ws = torch.empty(_lib.call_raw("e2ep_attn_bwd_workspace", B, H, Sq) // 4,
                          dtype=torch.float32, device=qb.device)
+        args = (_lib.ptr(qb), kptr, kptr + 4 * E, _lib.ptr(o), _lib.ptr(do), _lib.ptr(lse), *dims,
+                1.0 / math.sqrt(dims[4]), int(causal), _lib.ptr(key_pad), p, _lib.ptr(seed),
+                _lib.ptr(dqb), dkptr, dkptr + 4 * E, _lib.ptr(ws))
         with timing.region("attn_bwd"):
-            _lib.call("e2ep_attn_bwd", _lib.ptr(qb), kptr, kptr + 4 * E, _lib.ptr(o), _lib.ptr(do),
-                      _lib.ptr(lse), *dims, 1.0 / math.sqrt(dims[4]), int(causal),
-                      _lib.ptr(key_pad), p, _lib.ptr(seed), _lib.ptr(dqb), dkptr, dkptr + 4 * E,
-                      _lib.ptr(ws), _lib.stream())
+            if not (conv.wgrad_overlap() and _SPLIT_BWD):  # serial (A/B, per-kernel timing)
+                _lib.call("e2ep_attn_bwd_part", *args, 0, _lib.stream())
+            else:
+                # D first, then dq here and dk/dv on the side stream concurrently (conv._Fork:
+                # every buffer is allocated above, on the current stream)
+                _lib.call("e2ep_attn_bwd_part", *args, 1, _lib.stream())
+                fork = conv._Fork(qb.device)
+                with fork:
+                    _lib.call("e2ep_attn_bwd_part", *args, 3, _lib.stream())
+                _lib.call("e2ep_attn_bwd_part", *args, 2, _lib.stream())
+                fork.join()
         return dqb, dkvb, None, None, None, None, None
 
 

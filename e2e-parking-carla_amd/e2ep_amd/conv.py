@@ -169,6 +169,10 @@ def set_wgrad_overlap(on):
     return prev
 
 
+def wgrad_overlap():
+    return _OVERLAP[0]
+
+
 def side_stream(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _SIDE.get(idx)

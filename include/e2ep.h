@@ -320,6 +320,14 @@ int e2ep_attn_bwd(const float *q, const float *k, const float *v, const float *o
                   int kv_ss, int kv_sb, int o_ss, int o_sb, float scale, int causal,
                   const uint8_t *key_pad, float p, const int32_t *seed, float *dq, float *dk,
                   float *dv, void *workspace, void *stream);
+/* The same backward in parts (part 0 = all of it, as e2ep_attn_bwd): 1 writes D = rowsum(dO * O)
+ * into the workspace; after it, 2 (dq) and 3 (dk, dv) are independent and may run concurrently
+ * on two streams (e2ep_amd.attention forks them). */
+int e2ep_attn_bwd_part(const float *q, const float *k, const float *v, const float *o,
+                       const float *dout, const float *lse, int B, int H, int Sq, int Sk, int dh,
+                       int q_ss, int q_sb, int kv_ss, int kv_sb, int o_ss, int o_sb, float scale,
+                       int causal, const uint8_t *key_pad, float p, const int32_t *seed, float *dq,
+                       float *dk, float *dv, void *workspace, int part, void *stream);
 int e2ep_attn_keep_mask(const int32_t *seed, int BH, int Sq, int Sk, float p, uint8_t *out,
                         void *stream);
 /* Softmax over the channel dim of x [N, C, HW] (model/bev_model.py:64 depth.softmax(1)) and

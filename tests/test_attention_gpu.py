@@ -227,3 +227,33 @@ def test_linear_skip_gradient_accumulated_in_gemm():
     ((y * gy.to(DEV)).sum() + (xs * gs.to(DEV)).sum()).backward()
     ref = gy.double() @ w.double() + gs.double()
     assert rel_l2(xd.grad.cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("packed,causal,p", [(True, False, 0.1), (False, False, 0.0), (True, True, 0.1)])
+def test_split_backward_equals_serial(packed, causal, p):
+    """Backward as D, then dq and dk/dv forked onto two streams (E2EP_ATTN_SPLIT=1) gives bitwise the
+    serial e2ep_attn_bwd result, for self-attention (packed QKV: dq and dk/dv written into
+    one tensor by the two streams) and cross-attention, with dropout and a causal mask."""
+    from e2ep_amd import attention, conv
+    attention._SPLIT_BWD, split0 = True, attention._SPLIT_BWD
+    torch.manual_seed(5)
+    S, Sk, B, dh = 14, 256, 4, 43
+    qb = torch.randn(S, B, (3 if packed else 1) * H * dh, device=DEV, requires_grad=True)
+    kvb = None if packed else torch.randn(Sk, B, 2 * H * dh, device=DEV, requires_grad=True)
+    seed = torch.tensor([1234], dtype=torch.int32, device=DEV)
+    g = torch.randn(S, B, H * dh, device=DEV)
+    res = []
+    for on in (False, True):
+        prev = conv.set_wgrad_overlap(on)
+        try:
+            for t in (qb, kvb):
+                if t is not None:
+                    t.grad = None
+            o = attention.attention(qb, kvb, H, causal and packed, None, p, seed)
+            o.backward(g)
+            res.append([t.grad.clone() for t in (qb, kvb) if t is not None])
+        finally:
+            conv.set_wgrad_overlap(prev)
+    attention._SPLIT_BWD = split0
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
