@@ -257,3 +257,23 @@ def test_split_backward_equals_serial(packed, causal, p):
     attention._SPLIT_BWD = split0
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_fully_masked_row_fused_zero_module_nan():
+    """Documented difference: a query whose keys are all padding gives 0 from the
+    fused path (output = the out-projection bias) where torch's MultiheadAttention (the
+    fallback / reference path) gives NaN on its math path; rows with any live key agree.  The
+    reference's decoder never builds such a row."""
+    from e2ep_amd import attention
+    m = _module(3).to(DEV).train()  # training-mode math path in torch (no fast path)
+    x = torch.randn(12, 2, E, device=DEV)
+    kpm = torch.zeros(2, 12, dtype=torch.bool, device=DEV)
+    kpm[1] = True
+    with torch.no_grad():
+        fused = attention.mha(m, x, x, x, key_padding_mask=kpm)
+        ref = m(x, x, x, key_padding_mask=kpm, need_weights=False)[0]
+    # torch's math path gives NaN; an SDPA backend may give the attention-free row instead
+    assert torch.isnan(ref[:, 1]).all() or rel_l2(ref[:, 1], fused[:, 1]) < 1e-5
+    attn_part = fused[:, 1] - m.out_proj.bias  # all-masked rows: attention output 0
+    assert torch.isfinite(fused).all() and attn_part.abs().max() < 1e-6
+    assert rel_l2(fused[:, 0], ref[:, 0]) < 1e-5
