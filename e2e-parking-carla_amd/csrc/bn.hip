@@ -10,6 +10,8 @@
 // and combined in a fixed order: biased variance for normalisation, unbiased for the
 // running-variance update (PyTorch semantics), deterministic run to run.
 // Backward recomputes the pre-activation from x (no saved activation tensor).
+#include <algorithm>
+
 #include "common.h"
 
 namespace e2ep {
@@ -361,16 +363,22 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(
 }
 
 // ------------------------------------------------------------------------------------------
-// Single-launch BatchNorm for channels of at most BNS_T * 4 * BNS_R elements (N * H * W; the
-// 16x16 / 32x32 EfficientNet stages and the BEV encoder's deeper layers, 77 of the 97 BN
-// layers of a step): one 1024-thread block per channel holds the channel in registers from
+// Single-launch BatchNorm for channels of at most BNS_T * 4 * BNS_R = 8192 elements (N * H * W:
+// the 16x16 EfficientNet stages and the BEV encoder's deepest layers): one 256-thread block per
+// channel holds the channel in registers from
 // the statistics to the normalisation, so forward is one launch and one read of x (instead of
 // stats + apply / finalize), backward one launch and one read of x, dy (instead of reduce +
 // apply).  Same fp64 statistics and element arithmetic as the split kernels above; the
 // summation is in a fixed order (thread t takes vectors t, t + 1024, ...), so deterministic.
 // ------------------------------------------------------------------------------------------
-constexpr int BNS_T = 1024, BNS_R = 8;
+constexpr int BNS_T = 256, BNS_R = 8;
 static int g_bn_small = 1;  // e2ep_bn_small(0) routes every shape to the split kernels (tests, A/B)
+// largest channel (in float4 vectors) the single-launch kernels take, forward / backward
+// (e2ep_bn_small_limits, A/B timing; at most BNS_R * BNS_T).  In the replayed C2 step, blocks
+// of 1024 threads for channels up to 32768 elements measured 0.25 ms/step slower than the
+// split kernels there (25.45 vs 25.19 ms, profiles/r02/session6/wgrad_target_bn_limits_ab.txt),
+// so only the 256-thread shapes take the single launch.
+static int g_bns_fwd_max = BNS_R * BNS_T, g_bns_bwd_max = BNS_R * BNS_T;
 static bool bn_small_enabled() { return g_bn_small != 0; }
 
 template <int T>
@@ -521,12 +529,10 @@ __global__ void __launch_bounds__(T) k_bn_bwd_small(
   }
 }
 
-// launch shape of the single-launch kernels (R = 0: the channel is too large): 256-thread
-// blocks up to 2048 vectors per channel (all of a step's blocks resident at once; 1024-thread
-// blocks measured 16.8 us for the 16x16 stages against 11 us of the split pair), 1024
-// threads above
+// vectors per thread of the single-launch kernels (R = 0: the channel is too large); 256-thread
+// blocks, every block of a step resident at once
 static int bns_r(int totv, int &threads) {
-  threads = totv <= 8 * 256 ? 256 : BNS_T;
+  threads = BNS_T;
   const int per = cdiv(totv, threads);
   if (per <= 1) return 1;
   if (per <= 2) return 2;
@@ -536,15 +542,11 @@ static int bns_r(int totv, int &threads) {
 }
 #define BNS_LAUNCH(KERNEL, R, TH, ...)                                                            \
   do {                                                                                            \
-    if (TH == 256) {                                                                              \
-      if (R == 1) hipLaunchKernelGGL((KERNEL<256, 1>), dim3(C), dim3(256), 0, s, __VA_ARGS__);    \
-      else if (R == 2) hipLaunchKernelGGL((KERNEL<256, 2>), dim3(C), dim3(256), 0, s, __VA_ARGS__); \
-      else if (R == 4) hipLaunchKernelGGL((KERNEL<256, 4>), dim3(C), dim3(256), 0, s, __VA_ARGS__); \
-      else hipLaunchKernelGGL((KERNEL<256, 8>), dim3(C), dim3(256), 0, s, __VA_ARGS__);           \
-    } else {                                                                                      \
-      if (R == 4) hipLaunchKernelGGL((KERNEL<BNS_T, 4>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
-      else hipLaunchKernelGGL((KERNEL<BNS_T, 8>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);       \
-    }                                                                                             \
+    (void)(TH);                                                                                   \
+    if (R == 1) hipLaunchKernelGGL((KERNEL<BNS_T, 1>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);  \
+    else if (R == 2) hipLaunchKernelGGL((KERNEL<BNS_T, 2>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
+    else if (R == 4) hipLaunchKernelGGL((KERNEL<BNS_T, 4>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<BNS_T, 8>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);         \
   } while (0)
 
 // elementwise activation forward/backward (for activations not fused into a BN)
@@ -600,7 +602,7 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
   const int totv = N * HWv;
   const bool small_ok = bn_small_enabled();
   int th = 0;
-  const int R = (train && v4 && small_ok) ? bns_r(totv, th) : 0;
+  const int R = (train && v4 && small_ok && totv <= g_bns_fwd_max) ? bns_r(totv, th) : 0;
   if (R) {
     BNS_LAUNCH(k_bn_fwd_small, R, th, x, per_c, eps, momentum, running_mean, running_var, mean, invstd,
                gamma, beta, res, dc_rand, dc_keep, N, C, HWv, act, y, nullptr, nullptr);
@@ -647,7 +649,7 @@ int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *
   const int totv = N * HWv;
   const bool small_ok = bn_small_enabled();
   int th = 0;
-  const int R = (train && v4 && small_ok) ? bns_r(totv, th) : 0;
+  const int R = (train && v4 && small_ok && totv <= g_bns_fwd_max) ? bns_r(totv, th) : 0;
   if (R) {
     BNS_LAUNCH(k_bn_fwd_small, R, th, x, per_c, eps, momentum, running_mean, running_var, mean, invstd,
                gamma, beta, nullptr, nullptr, 1.f, N, C, HWv, 0, nullptr, scale, shift);
@@ -689,7 +691,7 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
   const int totv = N * HWv;
   const bool small_ok = bn_small_enabled();
   int th = 0;
-  const int R = (v4 && small_ok) ? bns_r(totv, th) : 0;
+  const int R = (v4 && small_ok && totv <= g_bns_bwd_max) ? bns_r(totv, th) : 0;
   if (R) {
     BNS_LAUNCH(k_bn_bwd_small, R, th, x, dy, mean, invstd, gamma, beta, res, dc_rand, dc_keep, gt, per_c,
                N, C, HWv, act, train, dx, dres, dgamma, dbeta);
@@ -719,6 +721,12 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(256), 0, s, part, sp, dgamma, dbeta);
   }
   return launch_status("e2ep_bn_bwd");
+}
+
+int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec) {
+  if (fwd_max_vec >= 0) g_bns_fwd_max = std::min(fwd_max_vec, BNS_R * BNS_T);
+  if (bwd_max_vec >= 0) g_bns_bwd_max = std::min(bwd_max_vec, BNS_R * BNS_T);
+  return 0;
 }
 
 int e2ep_bn_small(int on) {

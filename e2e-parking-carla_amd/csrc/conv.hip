@@ -1244,6 +1244,10 @@ struct GemmPlan {
 };
 
 // Deterministic launch plan shared by the workspace query and the launch.
+// split-K plan of the forward / data-gradient GEMMs (e2ep_conv_split_params, A/B timing)
+static int g_split_target = 1024, g_split_thresh = 512;
+static int g_wgrad_target = 1024;  // workgroups the spatial weight-gradient split aims at
+
 static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
   GemmPlan p;
   const int Kc = mode == 0 ? g.Cin : g.Cout;
@@ -1277,7 +1281,7 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
   p.splits = 1;
   // split K when the grid cannot fill the chip twice over (measured best: aim at ~1024
   // workgroups below 512, scripts/bench_conv.py)
-  const int target = 1024, thresh = 512;
+  const int target = g_split_target, thresh = g_split_thresh;
   if (blocks < thresh && p.nph == 1) {
     int s = (int)((target + blocks - 1) / blocks);
     s = std::min(s, std::max(1, kmax / 4));
@@ -1507,6 +1511,13 @@ int e2ep_conv_wgrad_kstep(int pixels) {
   return old;
 }
 
+int e2ep_conv_split_params(int target, int thresh, int wgrad_target) {
+  if (target > 0) g_split_target = target;
+  if (thresh >= 0) g_split_thresh = thresh;
+  if (wgrad_target > 0) g_wgrad_target = wgrad_target;
+  return 0;
+}
+
 int e2ep_conv_gemm_variant(int variant) {
   const int old = g_gemm_variant;
   if (variant >= 0 && variant <= 5) g_gemm_variant = variant;
@@ -1556,7 +1567,7 @@ int e2ep_conv_wgrad_splits(const int *dims) {
   const int nl = std::max(1, live_taps(g).n);
   const long long base = (long long)cdiv(g.Cin * nl, WBN) * cdiv(g.Cout, BM);
   const long long pix = (long long)g.N * g.P * g.Q;
-  long long want = (1024 + base - 1) / base;
+  long long want = (g_wgrad_target + base - 1) / base;
   long long cap = pix / 256;
   long long s = want < cap ? want : cap;
   if (s < 1) s = 1;

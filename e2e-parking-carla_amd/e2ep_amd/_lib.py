@@ -37,6 +37,7 @@ SIGNATURES = {
     "e2ep_conv_dgrad": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),
     "e2ep_conv_dgrad_acc": (_i, [_p, _p, _p, _i, _i, _p, _p, _p, _p]),
     "e2ep_conv_gemm_variant": (_i, [_i]),
+    "e2ep_conv_split_params": (_i, [_i, _i, _i]),
     "e2ep_conv_precision": (_i, [_i]),
     "e2ep_conv_wgrad_kstep": (_i, [_i]),
     "e2ep_conv_wgrad_splits": (_i, [_p]),
@@ -100,6 +101,7 @@ SIGNATURES = {
     "e2ep_gemm_skinny": (_i, [_i]),
     "e2ep_gemm_split_min": (_i, [_i]),
     "e2ep_bn_small": (_i, [_i]),
+    "e2ep_bn_small_limits": (_i, [_i, _i]),
     "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_gemm_rowsum_workspace": (_sz, [_i, _i, _i]),
     "e2ep_gemm_rowsum": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _p, _p]),
@@ -137,6 +139,12 @@ def load():
         lib.e2ep_conv_gemm_variant(int(os.environ["E2EP_CONV_VARIANT"]))
     if os.environ.get("E2EP_GEMM_SKINNY"):  # A/B timing of the few-row GEMM path
         lib.e2ep_gemm_skinny(int(os.environ["E2EP_GEMM_SKINNY"]))
+    if os.environ.get("E2EP_CONV_SPLIT"):  # "target,thresh[,wgrad_target]" for A/B timing
+        v = [int(x) for x in os.environ["E2EP_CONV_SPLIT"].split(",")] + [0]
+        lib.e2ep_conv_split_params(v[0], v[1], v[2])
+    if os.environ.get("E2EP_BN_SMALL_LIMITS"):  # "fwd_max_vec,bwd_max_vec" for A/B timing
+        f, b = (int(x) for x in os.environ["E2EP_BN_SMALL_LIMITS"].split(","))
+        lib.e2ep_bn_small_limits(f, b)
     if os.environ.get("E2EP_GEMM_SPLIT_MIN"):  # A/B timing of small-grid K splits
         lib.e2ep_gemm_split_min(int(os.environ["E2EP_GEMM_SPLIT_MIN"]))
     return lib

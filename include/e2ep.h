@@ -172,6 +172,11 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
  * a value outside 0..5 only queries.  Process-global; not thread-safe against concurrent
  * launches. */
 int e2ep_conv_gemm_variant(int variant);
+/* Split-K plans: forward / data-gradient conv GEMM grids under `thresh` workgroups are split
+ * toward `target` (defaults 1024 / 512; thresh 0 = never split); the spatial weight gradient
+ * (e2ep_conv_wgrad_splits) aims at `wgrad_target` workgroups (default 1024).  Values <= 0
+ * (thresh < 0) keep the current setting.  For A/B timing. */
+int e2ep_conv_split_params(int target, int thresh, int wgrad_target);
 /* Operand precision of the conv GEMMs: 0 = fp32 (default; exact-f32 MFMA), 1 = bf16, 2 = fp16
  * (operands rounded to nearest-even, fp32 products and accumulation, fp32 tensors in and
  * out) — BASELINE configs C3 (bf16 forward / fp32 gradients, AMP-style: bf16 operands in the
@@ -487,10 +492,13 @@ int e2ep_gemm_skinny(int max_rows);
 int e2ep_gemm_split_min(int ksteps);
 
 /* BatchNorm single-launch switch: on = 1 (default) lets e2ep_bn_fwd / e2ep_bn_stats /
- * e2ep_bn_bwd run channels of N*H*W <= 32768 (H*W % 4 == 0, training statistics) as one
+ * e2ep_bn_bwd run channels of N*H*W <= 8192 (H*W % 4 == 0, training statistics) as one
  * block-per-channel launch that keeps the channel in registers; 0 forces the split
  * statistics + apply kernels for every shape; < 0 only queries.  Returns the previous value. */
 int e2ep_bn_small(int on);
+/* Largest channel, in float4 vectors (N*H*W / 4), the single-launch BN kernels take in the
+ * forward / backward (default and maximum 2048 each; < 0 keeps the setting).  For A/B timing. */
+int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
               int K, int relu, void *workspace, void *stream);

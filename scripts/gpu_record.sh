@@ -1,9 +1,9 @@
 #!/bin/bash
-# Session-6 GPU batch 16 (record of HEAD): full GPU suite, smoke(), the default bench line
-# (C2 + CPU baseline), C3 bf16 line, rocprofv3 kernel trace of the replayed C2 step.
+# Record of HEAD on one MI355X: full GPU suite, smoke(), default bench line, C3,
+# rocprofv3 kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-O=gpurun_out/s6p
+O=${1:-gpurun_out/record}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -n "FAIL\|Error" $O/pytest_gpu.log | head; exit 1; }
 tail -1 $O/pytest_gpu.log

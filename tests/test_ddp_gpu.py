@@ -127,6 +127,7 @@ def test_rccl_world1_exchange_is_exact(graph):
             assert l_ref == l_ddp
         assert torch.equal(_flat_params(m_ref), _flat_params(m_ddp))
     finally:
+        torch.cuda.synchronize()  # no queued work on any stream when the communicator goes
         dist.destroy_process_group()
 
 
