@@ -3,6 +3,7 @@
 #include <stdio.h>
 
 #include "e2ep.h"
+#include "tune.h"
 
 namespace e2ep {
 static thread_local char g_err[512] = "";
@@ -12,9 +13,20 @@ void set_error(const char *fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+// launch-plan tunables (tune.h TUNE_*), e2ep_tune.  Defaults from in-step A/B on the replayed
+// C2 step (profiles/r02/session6/tune_ab_round*.txt): split-BN target 2048 (was 1024),
+// depthwise weight-gradient target 1024 (was 2048), 1x1 weight-gradient target 1024 (was
+// 2048) together -0.23 ms/step; the rest keep their values (no gain measured).
+int g_tune[TUNE_N] = {2048, 4096, 1024, 1024, 768, 1024};
 }  // namespace e2ep
 
 extern "C" {
 int e2ep_abi_version(void) { return 1; }
+int e2ep_tune(int key, int value) {
+  if (key < 0 || key >= e2ep::TUNE_N) return -1;
+  const int prev = e2ep::g_tune[key];
+  if (value > 0) e2ep::g_tune[key] = value;
+  return prev;
+}
 const char *e2ep_last_error(void) { return e2ep::g_err; }
 }

@@ -561,9 +561,9 @@ __global__ void k_act_bwd(const float *__restrict__ x, const float *__restrict__
 }
 
 static int bn_splits(long long per_channel, int C) {
-  // enough workgroups to fill the chip (~1024) with >= 4096 elements each
-  long long want = (1024 + C - 1) / C;
-  long long cap = per_channel / 4096;
+  // enough workgroups to fill the chip (e2ep_tune key 0) with >= key-1 elements each
+  long long want = (g_tune[TUNE_BN_SPLIT_TARGET] + C - 1) / C;
+  long long cap = per_channel / g_tune[TUNE_BN_SPLIT_MIN];
   long long s = want < cap ? want : cap;
   if (s < 1) s = 1;
   if (s > 256) s = 256;
@@ -571,7 +571,7 @@ static int bn_splits(long long per_channel, int C) {
 }
 
 // vectors per apply workgroup (4 per thread)
-constexpr int APPLY_PER = 1024;
+#define APPLY_PER (g_tune[TUNE_BN_APPLY_PER])
 
 }  // namespace e2ep
 

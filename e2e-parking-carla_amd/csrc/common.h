@@ -5,6 +5,7 @@
 #include <stdio.h>
 
 #include "e2ep.h"
+#include "tune.h"
 
 namespace e2ep {
 

@@ -842,7 +842,7 @@ static bool wgrad1x1_ok(const ConvGeom &g) {
 static int wgrad1x1_splits_for(const ConvGeom &g, int to, int tc) {
   const long long tiles = (long long)cdiv(g.Cout, to) * cdiv(g.Cin, tc);
   const long long pix = (long long)g.N * g.P * g.Q;
-  long long want = (2048 + tiles - 1) / tiles;   // ~2048 workgroups
+  long long want = (g_tune[TUNE_WGRAD1X1_TARGET] + tiles - 1) / tiles;   // e2ep_tune key 3 / 5
   long long cap = pix / 2048;                    // >= 16 loop iterations per wave
   long long s = want < cap ? want : cap;
   if (s < 1) s = 1;

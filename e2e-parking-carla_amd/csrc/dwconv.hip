@@ -495,7 +495,7 @@ static int dw_wgrad_splits(const DwGeom &g) {
   if (dw_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     const int cunits = g.N * d.units_per_plane;
-    int want = (2048 + g.C - 1) / g.C;           // ~2048 workgroups
+    int want = (g_tune[TUNE_DW_WGRAD_TARGET] + g.C - 1) / g.C;  // e2ep_tune key 3 / 5
     int cap = (cunits + 7) / 8;                   // >= 8 units (2 per wave) each
     int s = want < cap ? want : cap;
     return s < 1 ? 1 : (s > 128 ? 128 : s);

@@ -416,7 +416,7 @@ static GemmLaunch gemm_plan(int M, int N, int K) {
     const long long nb = (long long)cdiv(M, t.bm) * cdiv(N, t.bn);
     const int smin = nb < 64 ? g_split_min_small : 8;
     const int cap = std::min(nb < 64 ? 16 : 8, std::max(1, ksteps / smin));
-    p.splits = (int)std::min<long long>(cap, std::max(1LL, (long long)cdiv(768, blocks)));
+    p.splits = (int)std::min<long long>(cap, std::max(1LL, (long long)cdiv(g_tune[TUNE_GEMM_SPLIT_TARGET], blocks)));
   }
   p.kper = cdiv(ksteps, p.splits);
   p.splits = cdiv(ksteps, p.kper);

@@ -1,0 +1,15 @@
+// Launch-plan tunables shared by the kernel files (set through e2ep_tune, read at launch).
+#pragma once
+
+namespace e2ep {
+enum Tune {
+  TUNE_BN_SPLIT_TARGET = 0,   // workgroups the split BN statistics / reduction aim at
+  TUNE_BN_SPLIT_MIN = 1,      // minimum elements per split-BN workgroup
+  TUNE_BN_APPLY_PER = 2,      // float4 vectors per BN apply workgroup
+  TUNE_DW_WGRAD_TARGET = 3,   // workgroups the depthwise weight gradient aims at
+  TUNE_GEMM_SPLIT_TARGET = 4, // workgroups a K-split e2ep_gemm aims at
+  TUNE_WGRAD1X1_TARGET = 5,   // workgroups the 1x1 weight gradient aims at
+  TUNE_N = 6
+};
+extern int g_tune[TUNE_N];
+}  // namespace e2ep

@@ -102,6 +102,7 @@ SIGNATURES = {
     "e2ep_gemm_split_min": (_i, [_i]),
     "e2ep_bn_small": (_i, [_i]),
     "e2ep_bn_small_limits": (_i, [_i, _i]),
+    "e2ep_tune": (_i, [_i, _i]),
     "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_gemm_rowsum_workspace": (_sz, [_i, _i, _i]),
     "e2ep_gemm_rowsum": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _p, _p]),
@@ -145,6 +146,10 @@ def load():
     if os.environ.get("E2EP_BN_SMALL_LIMITS"):  # "fwd_max_vec,bwd_max_vec" for A/B timing
         f, b = (int(x) for x in os.environ["E2EP_BN_SMALL_LIMITS"].split(","))
         lib.e2ep_bn_small_limits(f, b)
+    if os.environ.get("E2EP_TUNE"):  # "key=value,..." launch-plan tunables for A/B timing
+        for kv in os.environ["E2EP_TUNE"].split(","):
+            k, v = kv.split("=")
+            lib.e2ep_tune(int(k), int(v))
     if os.environ.get("E2EP_GEMM_SPLIT_MIN"):  # A/B timing of small-grid K splits
         lib.e2ep_gemm_split_min(int(os.environ["E2EP_GEMM_SPLIT_MIN"]))
     return lib
