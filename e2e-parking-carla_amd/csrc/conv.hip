@@ -1276,7 +1276,7 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
   p.bm = 5LL * cdiv(M, 32) * 32 <= 4LL * cdiv(M, 64) * 64 ? 32 : 64;
   const long long mblocks = cdiv(M, p.bm);
   const int wide_n = p.bm == 64 ? 128 : 256;
-  p.bnt = cdiv(p.ncols, wide_n) * mblocks * p.nph >= 512 ? wide_n : wide_n / 2;
+  p.bnt = cdiv(p.ncols, wide_n) * mblocks * p.nph >= g_tune[TUNE_CONV_WIDE_MIN] ? wide_n : wide_n / 2;
   const long long blocks = cdiv(p.ncols, p.bnt) * mblocks * p.nph;
   p.splits = 1;
   // split K when the grid cannot fill the chip twice over (measured best: aim at ~1024

@@ -9,7 +9,8 @@ enum Tune {
   TUNE_DW_WGRAD_TARGET = 3,   // workgroups the depthwise weight gradient aims at
   TUNE_GEMM_SPLIT_TARGET = 4, // workgroups a K-split e2ep_gemm aims at
   TUNE_WGRAD1X1_TARGET = 5,   // workgroups the 1x1 weight gradient aims at
-  TUNE_N = 6
+  TUNE_CONV_WIDE_MIN = 6,     // conv fwd / dgrad grids of at least this many wide tiles use them
+  TUNE_N = 7
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

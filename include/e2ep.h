@@ -503,7 +503,9 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * value, -1 for an unknown key), defaults in parentheses: 0 split-BN target workgroups (2048),
  * 1 minimum elements per split-BN workgroup (4096), 2 float4 vectors per BN apply workgroup
  * (1024), 3 depthwise weight-gradient target workgroups (1024), 4 K-split e2ep_gemm target
- * workgroups (768), 5 1x1 weight-gradient target workgroups (1024).  For A/B timing. */
+ * workgroups (768), 5 1x1 weight-gradient target workgroups (1024), 6 conv forward /
+ * data-gradient grids of at least this many wide (128 / 256-column) tiles use them (512).
+ * For A/B timing. */
 int e2ep_tune(int key, int value);
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
