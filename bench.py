@@ -243,6 +243,202 @@ def relaunch(n):
     return subprocess.call(cmd)
 
 
+def train_step_rate(dev, world, rank, batch, steps, warmup, hires=False, eager=False):
+    """Time `steps` replays of the captured TrainStep (fwd + 3 losses + bwd + Adam) after
+    `warmup` untimed ones, bracketed by a barrier + device synchronisation on both sides, the
+    elapsed time taken as the max over ranks.  Returns samples/s over all ranks, ms/step, the
+    last loss and the live module / step (for the per-kernel passes)."""
+    from e2ep_amd import synthetic
+    from e2ep_amd.train import TrainStep
+    from tool.config import default_cfg
+    from trainer.pl_trainer import ParkingTrainingModule
+
+    torch.manual_seed(1234)  # identical initial weights on every rank
+    cfg = default_cfg(final_dim=[512, 512], image_crop=512) if hires else default_cfg()
+    mod = ParkingTrainingModule(cfg).to(dev).train()
+    # bev_encoder.layer4 is built but never run (reference model/bev_encoder.py:21,23-36):
+    # it never has a gradient, so it is kept out of the reducer and the optimizer step.
+    for p in mod.parking_model.bev_encoder.layer4.parameters():
+        p.requires_grad_(False)
+    data = device_batch(synthetic.synthetic_batch(batch, seed=rank, hires=hires), dev)
+    if world > 1:  # identical initial weights on every rank (DDP's init broadcast)
+        for t in list(mod.parameters()) + list(mod.buffers()):
+            dist.broadcast(t.data, 0)
+    # warm-up steps (the first ones also capture the step into HIP graphs)
+    step = TrainStep(mod, data, lr=mod.cfg.learning_rate, weight_decay=mod.cfg.weight_decay,
+                     world=world, graph=not eager, warmup=max(1, warmup))
+    if eager:
+        for _ in range(warmup):
+            step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return {"value": world * batch * steps / elapsed, "ms_per_step": elapsed / steps * 1e3,
+            "loss": loss, "module": mod, "step": step}
+
+
+def conv_roofline(step, lowp, n_eager=3):
+    """The headline roofline entry: the conv GEMM family (forward + data gradient), its FLOPs
+    (2*N*Cout*P*Q*Cin*R*S per launch) over its summed HIP-event time in `n_eager` eager
+    forward+backward passes on the launch stream after the timed region (graph replays cannot
+    be bracketed per kernel from the host).  Returns (entry, per-region kernel summary)."""
+    from e2ep_amd import conv, timing
+    timing.reset()
+    timing.enable(True)
+    # serial weight gradients here: a kernel's events then time that kernel alone, not its
+    # overlap with a side-stream weight gradient (the timed step runs them forked)
+    prev_overlap = conv.set_wgrad_overlap(False)
+    for _ in range(n_eager):
+        step._fwd_bwd()
+    timing.enable(False)
+    conv.set_wgrad_overlap(prev_overlap)
+    kern = timing.summary()
+    work = timing.work()
+    gemm = [k for k in ("conv_fwd", "conv_dgrad") if k in kern]
+    g_ms = sum(kern[k][2] for k in gemm)
+    g_flop = sum(work.get(k, 0.0) for k in gemm)
+    g_launch = sum(kern[k][0] for k in gemm)
+    g_tfs = g_flop / (g_ms * 1e-3) / 1e12
+    g_peak = BF16_MFMA_PEAK_TFS if lowp else FP32_MFMA_PEAK_TFS
+    entry = {"kernel": ("e2ep::k_conv_gemm / k_conv_gemm2 (implicit-GEMM conv forward + data "
+                        "gradient, v_mfma_f32_32x32x16_bf16)" if lowp else
+                        "e2ep::k_conv_gemm / k_conv_gemm2 (implicit-GEMM conv forward + data "
+                        "gradient, v_mfma_f32_32x32x2_f32)") + "; the step's largest kernel family",
+             "bound": "mfma", "achieved": round(g_tfs, 2), "peak": g_peak,
+             "unit": "TFLOP/s", "frac": round(g_tfs / g_peak, 4), "traffic": None,
+             "flop_per_step": g_flop / n_eager, "ms_per_step": round(g_ms / n_eager, 4),
+             "launches_per_step": g_launch // n_eager,
+             "timing": f"HIP events around every conv fwd/dgrad launch of {n_eager} eager fwd+bwd "
+                       "passes on the launch stream; FLOPs = 2*N*Cout*P*Q*Cin*R*S per launch"}
+    return entry, kern
+
+
+def _release():
+    """Return the memory of models / captured steps the caller has dropped (graph pools
+    included) before the next configuration is built."""
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def secondary_c3(dev, steps, warmup):
+    """BASELINE configs[2] per GPU (C3): the same B=8 train step with bf16 operands in every
+    conv GEMM (forward, data gradient, weight gradient), fp32 accumulation, fp32 tensors in
+    HBM, fp32 master weights / Adam / all-reduce; samples/s and its conv-family roofline
+    against the bf16 dense peak."""
+    from e2ep_amd import precision
+    prev = precision.set("bf16")
+    try:
+        r = train_step_rate(dev, 1, 0, 8, steps, warmup)
+        roof, _ = conv_roofline(r["step"], True)
+    finally:
+        precision.set(prev)
+    out = {"config": "C3 per GPU: B=8, 4 cams x 256^2, bf16 operands in the conv GEMMs (forward, "
+                     "data gradient, weight gradient), fp32 accumulate / storage / optimizer",
+           "value": round(r["value"], 3), "unit": "samples/s", "ms_per_step": round(r["ms_per_step"], 3),
+           "steps": steps, "roofline": roof}
+    del r
+    _release()
+    return out
+
+
+def secondary_c4(dev, steps, warmup):
+    """BASELINE configs[3] (C4): the full train step at 6 cams x 512^2, B=4 per GPU, fp32."""
+    r = train_step_rate(dev, 1, 0, 4, steps, warmup, hires=True)
+    out = {"config": "C4: train step, 6 cams x 512x512, 200x200 BEV, B=4, fp32",
+           "value": round(r["value"], 3), "unit": "samples/s",
+           "ms_per_step": round(r["ms_per_step"], 3), "steps": steps}
+    del r
+    _release()
+    return out
+
+
+def secondary_c5(dev, iters=200, cpu_iters=5, cpu_threads=None):
+    """BASELINE configs[4] (C5): closed-loop inference — ParkingModel.predict at B=1 (encoder +
+    3 autoregressive decoder passes, reference model/parking_model.py:72-78, called every
+    control step at agent/parking_agent.py:385) with fp16 conv operands, captured once into a
+    HIP graph; per call the inputs are copied into the captured buffers, the graph replayed
+    and the device synchronised; p50 / p90 over `iters` calls.  The oracle's predict on the host
+    cores beside it (p50 of `cpu_iters` calls)."""
+    import numpy as np
+    from e2ep_amd import graphs, precision, synthetic
+    from model.parking_model import ParkingModel
+    from tool.config import default_cfg
+
+    torch.manual_seed(0)
+    m = ParkingModel(default_cfg()).to(dev).eval()
+    host = synthetic.synthetic_batch(1, seed=0)
+    host["gt_control"] = host["gt_control"][:, :1]  # BOS: the agent's first token
+    keys = ("image", "target_point", "ego_motion", "gt_control")
+    static = {k: host[k].to(dev) for k in keys}
+    static["intrinsics"], static["extrinsics"] = host["intrinsics"], host["extrinsics"]
+    noise = synthetic.target_noise(1, seed=0).to(dev)
+
+    def call():
+        with torch.no_grad():
+            return m.predict(static, noise)
+
+    with torch.no_grad():
+        tok32 = call()[0].clone()
+    prev = precision.set("fp16")
+    try:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                call()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g, gout, _ = graphs.capture(call)
+        ts = []
+        for _ in range(iters + 10):
+            t0 = time.perf_counter()
+            for k in keys:
+                static[k].copy_(host[k], non_blocking=True)
+            g.replay()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        ts = np.asarray(ts[10:]) * 1e3
+        same = bool(torch.equal(gout[0], tok32))
+    finally:
+        precision.set(prev)
+    out = {"config": "C5: ParkingModel.predict, B=1, 4 cams x 256^2, fp16 conv operands, HIP graph",
+           "p50_ms": round(float(np.percentile(ts, 50)), 3),
+           "p90_ms": round(float(np.percentile(ts, 90)), 3), "calls": iters,
+           "tokens_equal_fp32": same, "published_ait_ms_rtx5000": 74.92}
+    del g, gout, m, static
+    _release()
+    if cpu_iters > 0:
+        from oracle import parking_ref as O
+        if cpu_threads:
+            torch.set_num_threads(cpu_threads)
+        ref = O.ParkingModelRef(O.Cfg).eval()
+        cts = []
+        with torch.no_grad():
+            ref.predict(host)
+            for _ in range(cpu_iters):
+                t0 = time.perf_counter()
+                ref.predict(host)
+                cts.append(time.perf_counter() - t0)
+        out["cpu_baseline"] = {"p50_ms": round(float(np.percentile(np.asarray(cts) * 1e3, 50)), 1),
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"p50 of {cpu_iters} oracle predict calls at B=1 fp32"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,9 +453,12 @@ def main():
     ap.add_argument("--cpu-warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the C3 / C4 / C5 sub-records of the default (C2, N=1) line")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
-                    help="conv GEMM operands: fp32 (C2, default) or bf16 (C3: bf16 forward / "
-                         "data-gradient conv operands, fp32 weight gradients and everything else)")
+                    help="conv GEMM operands: fp32 (C2, default) or bf16 (C3: bf16 operands in "
+                         "the forward, data-gradient and weight-gradient conv GEMMs, fp32 "
+                         "accumulation, storage, optimizer and everything else)")
     args = ap.parse_args()
     hires = args.workload == "c4"
     if args.batch is None:
@@ -288,80 +487,19 @@ def main():
         backend = dist.get_backend()
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
-    from e2ep_amd import _lib, conv, precision, synthetic, timing
-    from e2ep_amd.train import TrainStep
-    from tool.config import default_cfg
-    from trainer.pl_trainer import ParkingTrainingModule
+    from e2ep_amd import _lib, conv, precision, timing
 
     _lib.load()
     precision.set(args.precision)
-    torch.manual_seed(1234)  # identical initial weights on every rank
-    cfg = default_cfg(final_dim=[512, 512], image_crop=512) if hires else default_cfg()
-    mod = ParkingTrainingModule(cfg).to(dev).train()
-    # bev_encoder.layer4 is built but never run (reference model/bev_encoder.py:21,23-36):
-    # it never has a gradient, so it is kept out of the reducer and the optimizer step.
-    for p in mod.parking_model.bev_encoder.layer4.parameters():
-        p.requires_grad_(False)
-    data = device_batch(synthetic.synthetic_batch(args.batch, seed=rank, hires=hires), dev)
-    if world > 1:  # identical initial weights on every rank (DDP's init broadcast)
-        for t in list(mod.parameters()) + list(mod.buffers()):
-            dist.broadcast(t.data, 0)
-    # warm-up steps (the first ones also capture the step into HIP graphs)
-    step = TrainStep(mod, data, lr=mod.cfg.learning_rate, weight_decay=mod.cfg.weight_decay,
-                     world=world, graph=not args.eager, warmup=max(1, args.warmup))
-    if args.eager:
-        for _ in range(args.warmup):
-            step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    samples = world * args.batch * args.steps
-    value = samples / elapsed
-    ms_step = elapsed / args.steps * 1e3
+    r = train_step_rate(dev, world, rank, args.batch, args.steps, args.warmup, hires,
+                        eager=args.eager)
+    mod, step, loss = r["module"], r["step"], r["loss"]
+    value, ms_step = r["value"], r["ms_per_step"]
+    final_loss = round(float(loss), 4)
+    data = step.batch
 
-    # per-kernel HIP-event timing: 3 eager forward+backward passes on the same stream after
-    # the timed region (graph replays cannot be bracketed per kernel from the host)
-    n_eager = 3
-    timing.reset()
-    timing.enable(True)
-    # serial weight gradients here: a kernel's events then time that kernel alone, not its
-    # overlap with a side-stream weight gradient (the timed step above runs them forked)
-    prev_overlap = conv.set_wgrad_overlap(False)
-    for _ in range(n_eager):
-        step._fwd_bwd()
-    timing.enable(False)
-    conv.set_wgrad_overlap(prev_overlap)
-    kern = timing.summary()
-    work = timing.work()
-    gemm = [k for k in ("conv_fwd", "conv_dgrad") if k in kern]
-    g_ms = sum(kern[k][2] for k in gemm)
-    g_flop = sum(work.get(k, 0.0) for k in gemm)
-    g_launch = sum(kern[k][0] for k in gemm)
-    g_tfs = g_flop / (g_ms * 1e-3) / 1e12
     lowp = args.precision != "fp32"
-    g_peak = BF16_MFMA_PEAK_TFS if lowp else FP32_MFMA_PEAK_TFS
-    roofline = {"kernel": ("e2ep::k_conv_gemm2 (implicit-GEMM conv forward + data gradient, "
-                           "v_mfma_f32_32x32x16_bf16)" if lowp else
-                           "e2ep::k_conv_gemm / k_conv_gemm2 (implicit-GEMM conv forward + data "
-                           "gradient, v_mfma_f32_32x32x2_f32)") + "; the step's largest kernel family",
-                "bound": "mfma", "achieved": round(g_tfs, 2), "peak": g_peak,
-                "unit": "TFLOP/s", "frac": round(g_tfs / g_peak, 4), "traffic": None,
-                "flop_per_step": g_flop / n_eager, "ms_per_step": round(g_ms / n_eager, 4),
-                "launches_per_step": g_launch // n_eager,
-                "timing": "HIP events around every conv fwd/dgrad launch of 3 eager fwd+bwd "
-                          "passes on the launch stream; FLOPs = 2*N*Cout*P*Q*Cin*R*S per launch"}
+    roofline, kern = conv_roofline(step, lowp)
     step_tfs = STEP_GFLOP_PER_SAMPLE * 1e9 * args.batch / (ms_step * 1e-3) / 1e12
     step_roofline = None if hires else {"bound": "mfma", "achieved": round(step_tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": round(step_tfs / FP32_MFMA_PEAK_TFS, 4),
@@ -401,6 +539,21 @@ def main():
                           f"{threads} threads; step times "
                           + ", ".join(f"{t:.2f}" for t in ts) + " s"}
 
+    secondary = None
+    if (rank == 0 and world == 1 and not hires and not lowp and not args.eager
+            and not args.no_secondary):
+        # the other BASELINE configs on this GPU, each on a fresh model (the C2 graphs freed)
+        mod = step = r = data = loss = None
+        _release()
+        secondary = {}
+        threads = host_cores()[0]
+        for name, fn in (("c3", lambda: secondary_c3(dev, args.steps, args.warmup)),
+                         ("c4", lambda: secondary_c4(dev, max(5, args.steps // 2), 3)),
+                         ("c5", lambda: secondary_c5(dev, cpu_iters=0 if args.no_cpu_baseline
+                                                     else 5, cpu_threads=threads))):
+            secondary[name] = fn()
+            print(f"[bench] {name}: {secondary[name]}", file=sys.stderr, flush=True)
+
     if rank == 0:
         line = {"metric": METRIC_C4 if hires else METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup,
@@ -410,14 +563,16 @@ def main():
                 "config": {"workload": "ParkingModel train step (fwd + control/seg/depth losses + bwd "
                                        "+ Adam), " + ("6 cams x 512x512 (C4), " if hires else
                                                       "4 cams x 256x256, ") +
-                                       ("bf16 conv operands in forward / data gradient, fp32 "
-                                        "weight gradients, optimizer and all-reduce (C3)"
+                                       ("bf16 operands in the conv GEMMs (forward, data gradient, "
+                                        "weight gradient), fp32 accumulate and storage, fp32 "
+                                        "optimizer and all-reduce (C3)"
                                         if lowp else "fp32") + ", random init",
                            "global_batch": world * args.batch, "batch_per_gpu": args.batch,
                            "parallelism": f"dp{world}"},
                 "world": {"size": world, "backend": backend, "rehearsal": rehearsal},
                 "roofline": roofline, "step_roofline": step_roofline, "roofline_lss": roofline_lss,
-                "lss_c4": c4, "cpu_baseline": base, "final_loss": round(float(loss), 4)}
+                "lss_c4": c4, "cpu_baseline": base, "final_loss": final_loss,
+                "secondary": secondary}
         print(json.dumps(line), flush=True)
         print("kernel timing (launches, mean ms, total ms):",
               {k: (n, round(m, 4), round(t, 3)) for k, (n, m, t) in kern.items()}, file=sys.stderr)

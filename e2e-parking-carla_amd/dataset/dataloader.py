@@ -51,15 +51,24 @@ class ParkingDataModule(_Base):
                           pin_memory=True, worker_init_fn=seed_worker, drop_last=True)
 
     def _cached_loader(self, dataset, split, shuffle):
-        from dataset.frame_cache import FrameCache, GpuFrameLoader, build_frame_cache
+        """Under DDP every rank runs setup(): rank 0 alone (re)builds the cache when it is
+        missing or was built from another dataset / config (frame_cache.cache_matches), the
+        others wait at a barrier and then open it read-only — and refuse a cache that still
+        does not match rather than train on stale frames."""
+        from dataset.frame_cache import FrameCache, GpuFrameLoader, build_frame_cache, cache_matches
         path = os.path.join(self.cfg.frame_cache, split)
-        if os.path.exists(os.path.join(path, "meta.json")):
-            cache = FrameCache(path)
-        else:
-            cache = build_frame_cache(dataset, path,
-                                      workers=getattr(self.cfg, "num_workers", None) or 8)
-        rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
-        world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+        dist = torch.distributed
+        ddp = dist.is_available() and dist.is_initialized()
+        rank = dist.get_rank() if ddp else 0
+        world = dist.get_world_size() if ddp else 1
+        if rank == 0 and not cache_matches(path, dataset):
+            build_frame_cache(dataset, path, workers=getattr(self.cfg, "num_workers", None) or 8)
+        if ddp:
+            dist.barrier()
+        if not cache_matches(path, dataset):
+            raise RuntimeError(f"frame cache {path} does not match the {split} dataset "
+                               "(built from another dataset or config)")
+        cache = FrameCache(path)
         return GpuFrameLoader(cache, self.cfg.batch_size, shuffle=shuffle, drop_last=True,
                               seed=42, resident=bool(getattr(self.cfg, "frame_cache_resident",
                                                              False)),

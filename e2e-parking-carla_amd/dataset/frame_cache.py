@@ -86,6 +86,9 @@ def build_frame_cache(dataset, out_dir, workers=0, chunk=32):
     workers > 1 forks that many decoder processes (build before touching the GPU)."""
     global _BUILD
     os.makedirs(out_dir, exist_ok=True)
+    meta_path = os.path.join(out_dir, "meta.json")
+    if os.path.exists(meta_path):  # a cache being rebuilt is not a cache until meta.json is back
+        os.remove(meta_path)
     n = len(dataset)
     crop = dataset.image_crop
     tokens = dataset.control.shape[1] if n else 3 * dataset.cfg.future_frame_nums + 3
@@ -124,10 +127,40 @@ def build_frame_cache(dataset, out_dir, workers=0, chunk=32):
             _fill(dataset, out_dir, lo, hi)
     meta = {"version": VERSION, "samples": n, "image_crop": crop, "bev": BEV,
             "intrinsics": dataset.intrinsic.tolist(), "extrinsics": dataset.extrinsic.tolist(),
+            "fingerprint": dataset_fingerprint(dataset),
             "fields": {f: [np.dtype(dt).str, list(shape)] for f, (dt, shape) in layout.items()}}
-    with open(os.path.join(out_dir, "meta.json"), "w") as f:
+    # meta.json last and atomically: its presence means every array above is complete
+    tmp = meta_path + f".tmp{os.getpid()}"
+    with open(tmp, "w") as f:
         json.dump(meta, f)
+    os.replace(tmp, meta_path)
     return FrameCache(out_dir)
+
+
+def dataset_fingerprint(dataset):
+    """SHA-256 over what identifies a CarlaDataset's samples without decoding any frame: the
+    sample count, crop, rig and the per-sample label rows (which encode the task / frame
+    ordering).  A cache whose fingerprint differs belongs to another dataset or config."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(repr((len(dataset), int(dataset.image_crop))).encode())
+    for a in (dataset.intrinsic, dataset.extrinsic, dataset.target_point, dataset.control,
+              dataset.velocity, dataset.throttle_brake, dataset.steer, dataset.reverse):
+        a = np.ascontiguousarray(np.asarray(a))
+        h.update(a.dtype.str.encode() + repr(a.shape).encode() + a.tobytes())
+    return h.hexdigest()
+
+
+def cache_matches(path, dataset):
+    """True when `path` holds a complete cache (meta.json present) built from `dataset`."""
+    meta_path = os.path.join(path, "meta.json")
+    if not os.path.exists(meta_path):
+        return False
+    with open(meta_path) as f:
+        meta = json.load(f)
+    return (meta.get("version") == VERSION and meta.get("samples") == len(dataset)
+            and meta.get("image_crop") == dataset.image_crop
+            and meta.get("fingerprint") == dataset_fingerprint(dataset))
 
 
 class FrameCache(torch.utils.data.Dataset):

@@ -39,10 +39,14 @@ def rig_transforms(intrinsics, extrinsics, device):
 
 
 def rig_transforms_host(intrinsics, extrinsics):
-    """The reference's own fp32 CPU algebra (torch.inverse + matmul), for comparisons: its last
-    ulp depends on the host CPU's LAPACK kernels.  Returns CPU tensors."""
-    K = intrinsics.detach().float().cpu()
-    E = extrinsics.detach().float().cpu()
+    """The reference's own fp32 CPU algebra, op for op (model/bev_model.py:46-53:
+    torch.inverse(E), R = inv[..., :3, :3], t = inv[..., :3, 3], R.matmul(torch.inverse(K))) on
+    the dense (B,N,·,·) batch the data loader collates.  Used for host-resident rigs (the
+    dataloader / agent path, memoised), so the pillar index is the reference's bit for bit on
+    the same host: its last ulp comes from the host CPU's LAPACK kernels, which the fp64 device
+    algebra (rig_transforms) cannot reproduce.  Returns CPU tensors."""
+    K = intrinsics.detach().float().cpu().contiguous()
+    E = extrinsics.detach().float().cpu().contiguous()
     inv_e = torch.inverse(E)
     combine = inv_e[..., :3, :3].matmul(torch.inverse(K))
     return combine.contiguous(), inv_e[..., :3, 3].contiguous()

@@ -70,6 +70,7 @@ class FlatAdam(torch.optim.Optimizer):
         self._offs_host = offs
         self.spans = [(o, p.numel()) for o, p in zip(offs, self.params)]
         self._gtab = torch.zeros(len(self.params), dtype=torch.int64, device=dev)
+        self._has_bool = torch.zeros(len(self.params), dtype=torch.bool, device=dev)
         self._gkey = None
         # row range of each tensor in the chunk table (gradient buckets gather by rows)
         self.chunk_rows, r = [], 0
@@ -139,11 +140,21 @@ class FlatAdam(torch.optim.Optimizer):
 
     # -- update -----------------------------------------------------------------------------
     @torch.no_grad()
-    def step(self, grad_flat=None, grad_scale=1.0, closure=None):
+    def has_grad(self, out):
+        """out[i] = 1 if parameter i has a gradient this step (from the prepared table), else 0
+        (int64, capturable).  Data-parallel callers all-reduce it with MAX and pass it to
+        step(grad_flat, ..., has_grad=out): every replica then steps the same parameters."""
+        torch.ne(self._gtab, 0, out=self._has_bool)
+        out.copy_(self._has_bool)
+        return out
+
+    def step(self, grad_flat=None, grad_scale=1.0, closure=None, has_grad=None):
         """One Adam step from the prepared gradient table, or from `grad_flat` (scaled by
         grad_scale, e.g. 1/world for an all-reduced sum); tensors whose table entry is null
-        (no gradient) are skipped either way.  torch.optim-style calls (no arguments, or a
-        closure) prepare the table themselves."""
+        (no gradient) are skipped either way.  With `grad_flat`, `has_grad` (int64 per
+        parameter, non-zero = step it; see has_grad()) replaces this rank's own table, so a
+        parameter that had a gradient on any rank is stepped on every rank, as under DDP.
+        torch.optim-style calls (no arguments, or a closure) prepare the table themselves."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -153,7 +164,9 @@ class FlatAdam(torch.optim.Optimizer):
         self.sync_lr()
         b1, b2 = self.betas
         _lib.call("e2ep_adam_step", _lib.ptr(self.chunks), self.n_chunks, _lib.ptr(self.offsets),
-                  _lib.ptr(self._gtab), _lib.ptr(grad_flat) if grad_flat is not None else None,
+                  _lib.ptr(has_grad if (has_grad is not None and grad_flat is not None)
+                           else self._gtab),
+                  _lib.ptr(grad_flat) if grad_flat is not None else None,
                   _lib.ptr(self.flat), _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq),
                   _lib.ptr(self.step_count), _lib.ptr(self.lr_dev), float(b1), float(b2),
                   float(self.eps), float(self.weight_decay), float(grad_scale), _lib.stream())

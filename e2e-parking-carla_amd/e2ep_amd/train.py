@@ -82,6 +82,7 @@ class GradBuckets:
             for i in range(i0, i1):
                 self.of[i] = b
         self.comm = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        self.has = torch.zeros(len(params), dtype=torch.int64, device=flat.device)
         self.active = False
         self._handles = [p.register_post_accumulate_grad_hook(self._hook_for(i))
                          for i, p in enumerate(params)]
@@ -143,6 +144,9 @@ class GradBuckets:
             w.wait()
         if self.cuda:
             self.main.wait_stream(self.comm)
+        self.opt.prepare()
+        self.opt.has_grad(self.has)
+        dist.all_reduce(self.has, op=dist.ReduceOp.MAX)
         self.works = []
         self.active = False
 
@@ -163,6 +167,11 @@ class TrainStep:
         dev = self.params[0].device
         self.flat_grad = (torch.zeros(self.opt.numel, dtype=torch.float32, device=dev)
                           if self.ddp else None)
+        # which parameters had a gradient on ANY rank (all-reduced MAX with the gradients):
+        # every replica steps the same set, as under DDP (a rank-local mask lets
+        # replicas drift when a branch is rank-dependent)
+        self.has_grad = (torch.zeros(len(self.params), dtype=torch.int64, device=dev)
+                         if self.ddp else None)
         self.backend = dist.get_backend() if self.ddp else None
         if overlap is None:
             overlap = os.environ.get("E2EP_DDP_OVERLAP", "1") != "0"
@@ -172,6 +181,8 @@ class TrainStep:
                             (self.backend == "nccl" or not self.flat_grad.is_cuda))
         self.buckets = (GradBuckets(self.params, self.opt, self.flat_grad, bucket_mb)
                         if self.overlap else None)
+        if self.buckets is not None:
+            self.has_grad = self.buckets.has
         self._host = (torch.empty(self.opt.numel, dtype=torch.float32, pin_memory=True)
                       if self.ddp and self.backend != "nccl" and not self.overlap
                       and self.flat_grad.is_cuda else None)
@@ -195,6 +206,7 @@ class TrainStep:
     def _gather(self):
         if self.ddp and self.buckets is None:
             self.opt.gather_grads(self.flat_grad)
+            self.opt.has_grad(self.has_grad)
 
     def _allreduce(self):
         """Non-overlapped exchange (gloo): host-staged for device tensors, with the ordering
@@ -203,15 +215,19 @@ class TrainStep:
             return
         if self._host is None:
             dist.all_reduce(self.flat_grad)
+            dist.all_reduce(self.has_grad, op=dist.ReduceOp.MAX)
             return
         self._host.copy_(self.flat_grad, non_blocking=True)
+        has = self.has_grad.cpu()  # synchronises the stream too
         torch.cuda.current_stream().synchronize()
         dist.all_reduce(self._host)
+        dist.all_reduce(has, op=dist.ReduceOp.MAX)
         self.flat_grad.copy_(self._host, non_blocking=True)
+        self.has_grad.copy_(has, non_blocking=True)
 
     def _update(self):
         if self.ddp:
-            self.opt.step(self.flat_grad, 1.0 / self.world)
+            self.opt.step(self.flat_grad, 1.0 / self.world, has_grad=self.has_grad)
         else:
             self.opt.step()
 

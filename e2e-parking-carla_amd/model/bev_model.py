@@ -59,8 +59,10 @@ class BevModel(nn.Module):
 
     def plan(self, intrinsics, extrinsics, device):
         """Pillar plan for this batch's rig.  The plan is a pure function of (frustum, K, E);
-        when K and E are host tensors (the dataloader / agent case) it is memoised on their
-        bytes, since the CARLA rig is constant.  E2EP_PLAN_CACHE=0
+        when K and E are host tensors (the dataloader / agent case) the rig algebra is the
+        reference's own fp32 CPU ops (lss.rig_transforms_host) and the plan is memoised on their
+        bytes, since the CARLA rig is constant; device K and E go through
+        the fp64 device algebra (lss.rig_transforms) with no host synchronisation.  E2EP_PLAN_CACHE=0
         rebuilds it every call (6 kernel launches, no host synchronisation)."""
         if self._host_consts is None:
             self._host_consts = self._consts()
@@ -72,7 +74,10 @@ class BevModel(nn.Module):
                    extrinsics.detach().float().contiguous().numpy().tobytes())
             if key == self._plan_key and self._plan is not None:
                 return self._plan
-        combine, trans = lss.rig_transforms(intrinsics, extrinsics, device)
+        if intrinsics.is_cuda or extrinsics.is_cuda:  # device rig: fp64 algebra on the GPU
+            combine, trans = lss.rig_transforms(intrinsics, extrinsics, device)
+        else:  # host rig: the reference's fp32 CPU ops, so the pillar index is bit-exact
+            combine, trans = lss.rig_transforms_host(intrinsics, extrinsics)
         plan = lss.build_plan(self.frustum, combine, trans, lo, res, dims, device)
         if key is not None:
             self._plan_key, self._plan = key, plan

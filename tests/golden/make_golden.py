@@ -2,7 +2,7 @@
 
 Run in the build container only (needs /root/reference):  python tests/golden/make_golden.py
 (`python tests/golden/make_golden.py b8` regenerates only the B=8 fixtures, `... c4` adds the
-C4 6-camera 512x512 fixtures.)
+C4 6-camera 512x512 fixtures, `... b8bf16` the C3 bf16-autocast comparator.)
 
 The reference has no tests or fixtures of its own, so every golden vector is
 produced here by importing the reference's Python modules unmodified, with:
@@ -210,6 +210,63 @@ def b8_fixtures(ref, orc, state, cfg, closs, sloss, dloss, meta):
                               "oracle_grad_rel_err_max": max(gerr.values())}
 
 
+def b8_bf16amp_fixtures(ref, state, closs, sloss, dloss, meta):
+    """C3 comparator: the reference's own deterministic-train step at the B=8 bench batch run
+    the way a bf16 mixed-precision trainer runs its convolutional modules (camera encoder, BEV
+    encoder, segmentation head — the layers the product's C3 mode runs on bf16 operands) —
+    their forward under torch.autocast(bfloat16) (the CPU autocast; its bf16 op list covers
+    conv / linear / matmul like the GPU one), activations between their layers in bf16, fp32
+    parameters and gradients; the transformer, lift-splat and losses stay fp32 as in the
+    product.  Its error against the fp64 oracle is the bf16 error budget the
+    product's C3 mode is held to (tests/test_train_step_b8_gpu.py)."""
+    data = synthetic.synthetic_batch(8, seed=11)
+    noise = synthetic.target_noise(8, seed=11)
+    deterministic(ref)
+    ref.load_state_dict(state)
+    ref.train()
+    ref.zero_grad(set_to_none=True)
+    # the convolutional modules run under autocast; their outputs return to fp32 at the module
+    # boundary (the reference's lift-splat index_put and everything after it require fp32: the
+    # whole model under autocast raises in model/bev_model.py:103)
+    conv_mods = (ref.bev_model.cam_encoder, ref.bev_encoder, ref.segmentation_head)
+    saved = [m.forward for m in conv_mods]
+
+    def amp(fwd):
+        def run(*a, **k):
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                out = fwd(*a, **k)
+            if isinstance(out, tuple):
+                return tuple(o.float() for o in out)
+            return out.float()
+        return run
+
+    for m in conv_mods:
+        m.forward = amp(m.forward)
+    try:
+        with FixedRand(noise):
+            pc, ps, pd = ref(data)
+    finally:
+        for m, f in zip(conv_mods, saved):
+            m.forward = f
+    lc, ls, ld = closs(pc, data), sloss(ps.unsqueeze(1), data["segmentation"]), dloss(pd, data["depth"])
+    (lc + ls + ld).backward()
+    rgrad = dict(ref.named_parameters())
+    gkeys = meta["model_train_b8"]["grad_keys"]
+    assert [k for k, v in rgrad.items() if v.grad is not None] == gkeys
+    fx = {"loss_control": np.float64(lc.float()), "loss_seg": np.float64(ls.float()),
+          "loss_depth": np.float64(ld.float()),
+          "pred_control": pc.detach().float().numpy(),
+          "seg_sample": sample(ps.float()).numpy(), "depth_sample": sample(pd.float()).numpy(),
+          "gnorm_all": np.array([float(rgrad[k].grad.double().norm()) for k in gkeys])}
+    for k in meta["model_train_b8"]["probe"]:
+        fx["gsample::" + k] = sample(rgrad[k].grad).numpy()
+    np.savez_compressed(os.path.join(OUT, "model_train_b8_bf16amp.npz"), **fx)
+    meta["model_train_b8_bf16amp"] = {"batch_seed": 11, "noise_seed": 11,
+                                      "autocast": "cpu bfloat16: cam_encoder, bev_encoder, segmentation_head forward",
+                                      "grad_keys": "model_train_b8"}
+    ref.zero_grad(set_to_none=True)
+
+
 def c4_fixtures(cfg, meta):
     """BASELINE configs[3] (C4: 6 cameras at 512x512, B=1) through the full reference model:
     eval forward + predict, and one deterministic-train forward/backward (losses, output
@@ -304,6 +361,19 @@ def main(only=None):
         with open(os.path.join(OUT, "meta.json"), "w") as f:
             json.dump(meta, f, indent=1)
         print("wrote C4 golden vectors to", OUT)
+        return
+    if only == "b8bf16":  # add the C3 (bf16 autocast) comparator, keep everything else
+        with open(os.path.join(OUT, "meta.json")) as f:
+            meta = json.load(f)
+        torch.manual_seed(0)
+        ref = ParkingModel(cfg)
+        state = make_state(ref.state_dict(), seed=1234)
+        b8_bf16amp_fixtures(ref, state, ControlLoss(cfg),
+                            SegmentationLoss(class_weights=torch.Tensor(cfg.seg_vehicle_weights)),
+                            DepthLoss(cfg), meta)
+        with open(os.path.join(OUT, "meta.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+        print("wrote the B=8 bf16-autocast comparator to", OUT)
         return
     if only == "b8":  # regenerate only the B=8 fixtures, keep the others and their meta
         with open(os.path.join(OUT, "meta.json")) as f:

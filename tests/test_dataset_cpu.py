@@ -154,6 +154,24 @@ def test_frame_cache_holds_the_reference_inputs(root, cfg, tmp_path):
     assert np.array_equal(g["rgb"][0], again.arrays["rgb"][3])
 
 
+def test_frame_cache_reuse_is_validated(root, cfg, tmp_path):
+    """A cache directory is reused only when it is complete (meta.json, written last and
+    atomically) and was built from the same dataset (fingerprint of count, crop, rig and label
+    rows); another split or changed labels do not match, and a rebuild invalidates first."""
+    from dataset.carla_dataset import CarlaDataset
+    from dataset.frame_cache import build_frame_cache, cache_matches
+    path = str(tmp_path / "fc")
+    ds = CarlaDataset(root, 1, cfg)
+    assert not cache_matches(path, ds)
+    build_frame_cache(ds, path, chunk=4)
+    assert cache_matches(path, ds)
+    assert not any(f.startswith("meta.json.tmp") for f in os.listdir(path))
+    assert not cache_matches(path, CarlaDataset(root, 0, cfg))
+    changed = CarlaDataset(root, 1, cfg)
+    changed.target_point = changed.target_point + 1.0
+    assert not cache_matches(path, changed)
+
+
 def test_frame_cache_empty_split(tmp_path, cfg):
     from dataset.carla_dataset import CarlaDataset
     from dataset.frame_cache import FrameCache, build_frame_cache

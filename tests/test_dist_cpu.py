@@ -37,6 +37,10 @@ class _HostSGD:
         for i in range(i0, i1):
             self.had_grad[i] = self.params[i].grad is not None
 
+    def has_grad(self, out):
+        out.copy_(torch.tensor([p.grad is not None for p in self.params], dtype=out.dtype))
+        return out
+
     def gather_grads(self, out, params=None):
         i0, i1 = params if params is not None else (0, len(self.params))
         for i in range(i0, i1):
@@ -45,10 +49,11 @@ class _HostSGD:
             out[o:o + n] = 0.0 if g is None else g.reshape(-1)
 
     @torch.no_grad()
-    def step(self, grad_flat=None, grad_scale=1.0):
+    def step(self, grad_flat=None, grad_scale=1.0, has_grad=None):
         self.prepare()
         for i, p in enumerate(self.params):
-            if not self.had_grad[i]:
+            stepped = self.had_grad[i] if has_grad is None or grad_flat is None else bool(has_grad[i])
+            if not stepped:
                 continue  # no gradient: not stepped (FlatAdam's null table entry)
             o, n = self.spans[i]
             g = p.grad if grad_flat is None else grad_flat[o:o + n].view_as(p)
@@ -65,11 +70,16 @@ class _Tiny(torch.nn.Module):
         self.frozen = torch.nn.Linear(2, 2)  # no grad, like bev_encoder.layer4
         for p in self.frozen.parameters():
             p.requires_grad_(False)
+        self.branch = torch.nn.Linear(4, 1)  # used only where self.use_branch (rank-dependent)
         self.unused = torch.nn.Linear(3, 3)  # trainable but never run: no gradient
+        self.use_branch = False
 
     def training_step(self, batch, idx=0):
         h = self.conv(batch["x"]).relu().mean((2, 3))
-        return torch.nn.functional.mse_loss(self.head(self.mid(h).relu() + h), batch["y"])
+        loss = torch.nn.functional.mse_loss(self.head(self.mid(h).relu() + h), batch["y"])
+        if self.use_branch:
+            loss = loss + 0.1 * self.branch(h).square().mean()
+        return loss
 
 
 def _data():
@@ -77,13 +87,14 @@ def _data():
     return {"x": torch.randn(4, 3, 8, 8, generator=g), "y": torch.randn(4, 2, generator=g)}
 
 
-def _worker(rank, world, port, out, overlap):
+def _worker(rank, world, port, out, overlap, branch_rank=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from e2ep_amd.train import TrainStep
     d = _data()
     half = {k: v[rank * 2:(rank + 1) * 2] for k, v in d.items()}
     m = _Tiny()
+    m.use_branch = rank == branch_rank
     params = [p for p in m.parameters() if p.requires_grad]
     # 64-byte buckets: one bucket per tensor or two, so several all-reduces run per step
     s = TrainStep(m, half, world=world, graph=False, optimizer=_HostSGD(params, 1e-2),
@@ -122,3 +133,20 @@ def test_two_rank_step_equals_full_batch_step(overlap):
     n_unused = sum(p.numel() for p in ref.unused.parameters())
     assert torch.equal(got0[-n_unused:], torch.cat([p.detach().reshape(-1)
                                                     for p in _Tiny().unused.parameters()]))
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_rank_dependent_branch_steps_every_replica(overlap):
+    """A parameter that gets a gradient on one rank only (a rank-dependent branch) is stepped
+    on every rank with the averaged gradient, as under DDP: the replicas stay identical
+    (the gradient-presence mask is all-reduced with the gradients)."""
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_worker, args=(2, _port(), out, overlap, 1), nprocs=2, join=True)
+        got0, got1 = out[0], out[1]
+    assert torch.equal(got0, got1)
+    init = _Tiny()
+    nb = sum(p.numel() for p in init.branch.parameters())
+    nu = sum(p.numel() for p in init.unused.parameters())
+    start = torch.cat([p.detach().reshape(-1) for p in init.branch.parameters()])
+    assert not torch.equal(got0[-(nu + nb):-nu], start)  # moved on rank 0 too

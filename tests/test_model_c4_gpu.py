@@ -11,20 +11,24 @@ evalgrad_c4, train_c4) and stdout.
 Bounds.  Eval forward: <= 1e-4 vs the fp32 reference (the north-star contract); tokens and
 target plane identical.  Losses and train-mode outputs: within max(1e-4, 3 x the reference's
 own fp32 error) of the fp64 oracle.  Gradient norms (all 530 parameters, eval mode and
-deterministic train): C4's gradients are ill-conditioned through the control path — the
-reference's own fp32 error vs fp64 has median 2.3e-4 / max 3.8e-3 in eval mode (10 x the C2
-figures) and 3.8e-3 / 3.8e-2 in train mode — and the product's rounding lands on other tensors
-than the reference's (scripts/diag_evalgrad_run.py, per loss term: the product is closer to
-fp64 than the reference on the segmentation and depth paths, 2 x further on the control
-path).  The gradient norms are therefore bounded as a set: max error <= 3 x the reference's
-max, median <= 5 x the reference's median (tests/test_model_b8_gpu.py keeps the per-tensor
-rule at the bench config, where the product is within 8e-5 of fp64 everywhere)."""
+deterministic train): the per-tensor rule of the bench config (tests/test_model_b8_gpu.py
+_norms3: each tensor within max(1e-4, 3 x the reference's own error on it, or its median
+error if larger) of fp64).
+
+History: round 2 held C4's gradients only as a set, because the product was further from
+fp64 than the reference there.  The cause was the pillar index: the device rig algebra (fp64
+Gauss-Jordan) flipped 6 of the 1.18 M frustum points to a neighbouring cell against the
+reference's fp32 LAPACK combine, and the fp64 oracle keeps the reference's fp32 geometry, so
+those points moved BEV features the train-mode BN statistics then spread everywhere.  Host
+rigs now go through the reference's own fp32 CPU algebra (bit-exact pillar table,
+tests/test_lss_gpu.py::test_host_rig_pillar_index_bit_exact_end_to_end) and the product is
+10-400 x closer to fp64 than the reference on every C4 output (profiles/r03/parity_c4.json)."""
 import numpy as np
 import pytest
 import torch
 
 from helpers import golden, meta, rel_l2
-from test_model_b8_gpu import BOUND_FACTOR, TOL, _check3, _record
+from test_model_b8_gpu import BOUND_FACTOR, TOL, _check3, _norms3, _record
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -51,19 +55,6 @@ def _scalar(section, name, got, ref32, ref64):
     e32, e64, eref = r(got, ref32), r(got, ref64), r(ref32, ref64)
     _record(section, name, vs_ref=e32, vs_fp64=e64, ref_vs_fp64=eref)
     assert e64 <= max(TOL, BOUND_FACTOR * eref), (section, name, e64, eref)
-
-
-def _norm_set(section, gkeys, params, n32, n64):
-    got = np.array([float(params[k].grad.double().norm()) for k in gkeys])
-    den = np.maximum(n64, 1e-3 * float(np.sqrt(np.mean(n64 ** 2))))
-    e64, eref = np.abs(got - n64) / den, np.abs(n32 - n64) / den
-    _record(section, "grad_norms(all %d)" % len(gkeys), vs_fp64_max=e64.max(),
-            ref_vs_fp64_max=eref.max(), vs_fp64_median=np.median(e64),
-            ref_vs_fp64_median=np.median(eref))
-    for i in np.argsort(-e64)[:8]:
-        _record(section + "_worst", gkeys[i], vs_fp64=e64[i], ref_vs_fp64=eref[i])
-    assert e64.max() <= 3.0 * eref.max(), (section, e64.max(), eref.max())
-    assert np.median(e64) <= 5.0 * np.median(eref), (section, np.median(e64), np.median(eref))
 
 
 def _cfg():
@@ -115,7 +106,7 @@ def test_c4_eval_mode_gradients_match_reference():
     for k, gk in (("control_loss", "loss_control"), ("segmentation_loss", "loss_seg"),
                   ("depth_loss", "loss_depth")):
         chk(_scalar, "evalgrad_c4", gk, losses[k].detach(), g32[gk], g64[gk])
-    chk(_norm_set, "evalgrad_c4", meta()["model_evalgrad_c4"]["grad_keys"],
+    chk(_norms3, "evalgrad_c4", meta()["model_evalgrad_c4"]["grad_keys"],
         dict(mod.parking_model.named_parameters()), g32["gnorm_all"], g64["gnorm_all"])
     chk.done()
 
@@ -137,6 +128,6 @@ def test_c4_deterministic_train_step_matches_reference():
     chk(_check3, "train_c4", "pred_control", pc, g32["pred_control"], g64["pred_control"])
     chk(_check3, "train_c4", "seg_slice", ps[:, :, 90:110, 90:110], g32["seg_slice"], g64["seg_slice"])
     chk(_check3, "train_c4", "depth_slice", pd[:, :, 10:14], g32["depth_slice"], g64["depth_slice"])
-    chk(_norm_set, "train_c4", meta()["model_train_c4"]["grad_keys"],
+    chk(_norms3, "train_c4", meta()["model_train_c4"]["grad_keys"],
         dict(mod.parking_model.named_parameters()), g32["gnorm_all"], g64["gnorm_all"])
     chk.done()
