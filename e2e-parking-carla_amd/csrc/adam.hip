@@ -29,7 +29,8 @@ __global__ void __launch_bounds__(ADAM_THREADS)
     k_adam(const int4 *__restrict__ chunks, const long long *__restrict__ offs,
            const long long *__restrict__ gptrs, const float *__restrict__ gflat,
            float *__restrict__ p, float *__restrict__ m, float *__restrict__ v,
-           const float *__restrict__ step, const double *__restrict__ lr, AdamHyper h) {
+           const float *__restrict__ step, const double *__restrict__ lr, AdamHyper h,
+           int *__restrict__ stepped) {
   const int4 c = chunks[blockIdx.x];
   const long long off = offs[c.x] + c.y;
   // a parameter without a gradient this step is not stepped (as torch.optim.Adam); on the
@@ -37,6 +38,8 @@ __global__ void __launch_bounds__(ADAM_THREADS)
   // does not depend on the world size
   const float *gt = gptrs ? reinterpret_cast<const float *>(gptrs[c.x]) : nullptr;
   if (gptrs && gt == nullptr) return;
+  // per-tensor "stepped at least once" flag (torch.optim.Adam keeps state only for those)
+  if (stepped && c.y == 0 && threadIdx.x == 0) stepped[c.x] = 1;
   const float *g = gflat ? gflat + off : gt + c.y;
   // torch: bias_correction = 1 - beta**step (python double), step_size = lr / bc1,
   // denom = sqrt(v) / sqrt(bc2) + eps, p -= step_size * m / denom
@@ -103,7 +106,8 @@ int e2ep_adam_chunk_elems(void) { return ADAM_THREADS * ADAM_VEC * ADAM_ITERS; }
 int e2ep_adam_step(const int *chunks, int n_chunks, const long long *offsets,
                    const long long *grad_ptrs, const float *grad_flat, float *param, float *exp_avg,
                    float *exp_avg_sq, float *step, const double *lr, double beta1, double beta2,
-                   double eps, double weight_decay, float grad_scale, void *stream) {
+                   double eps, double weight_decay, float grad_scale, int *stepped,
+                   void *stream) {
   E2EP_REQUIRE(n_chunks > 0 && chunks && offsets && param && exp_avg && exp_avg_sq && step && lr,
                E2EP_EINVAL, "e2ep_adam_step: null argument");
   E2EP_REQUIRE(grad_ptrs || grad_flat, E2EP_EINVAL, "e2ep_adam_step: no gradients");
@@ -112,7 +116,7 @@ int e2ep_adam_step(const int *chunks, int n_chunks, const long long *offsets,
   hipLaunchKernelGGL(k_adam_count, dim3(1), dim3(1), 0, as_stream(stream), step);
   hipLaunchKernelGGL(k_adam, dim3(n_chunks), dim3(ADAM_THREADS), 0, as_stream(stream),
                      reinterpret_cast<const int4 *>(chunks), offsets, grad_ptrs, grad_flat, param,
-                     exp_avg, exp_avg_sq, step, lr, h);
+                     exp_avg, exp_avg_sq, step, lr, h, stepped);
   return launch_status("e2ep_adam_step");
 }
 

@@ -7,18 +7,28 @@ kernel nodes by e2ep_graph_replace_memsets, and only then instantiated."""
 import ctypes
 
 import torch
+import torch.distributed as dist
 
 from . import _lib
+
+
+def capture_mode():
+    """'thread_local' while a process group exists, else 'global'.
+
+    With a process group the c10d watchdog thread polls its RCCL work events during a
+    capture; under the global mode those calls race with (and invalidate) the capture — in
+    round 2 an abort inside destroy_process_group after the world-1 RCCL test.
+    Without one, the global mode is kept: it makes any unsafe HIP call from another thread
+    (autograd's device thread runs the captured backward) fail the capture loudly instead of
+    being captured or skipped silently."""
+    return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
 
 
 def capture(fn, pool=None):
     """Capture fn() into a repaired, instantiated graph.  Returns (graph, fn's result,
     number of memset nodes rewritten)."""
     g = torch.cuda.CUDAGraph(keep_graph=True)
-    # thread-local capture: other threads' HIP calls during the capture (the c10d watchdog
-    # polling its RCCL work events when a process group exists) must neither invalidate the
-    # capture nor be refused by it
-    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+    with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_mode()):
         out = fn()
     n = ctypes.c_int(0)
     _lib.call("e2ep_graph_replace_memsets", ctypes.c_void_p(g.raw_cuda_graph()), ctypes.byref(n))

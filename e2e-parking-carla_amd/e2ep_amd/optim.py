@@ -64,6 +64,10 @@ class FlatAdam(torch.optim.Optimizer):
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
         self.step_count = torch.zeros(1, dtype=torch.float32, device=dev)
+        # 1 for every tensor stepped at least once (written by the Adam kernel): state_dict
+        # holds state for those only, as torch.optim.Adam does (a tensor that never had a
+        # gradient, e.g. bev_encoder.layer4, has no state there)
+        self.stepped = torch.zeros(len(self.params), dtype=torch.int32, device=dev)
         self.offsets = torch.tensor(offs, dtype=torch.int64, device=dev)
         self.chunks = torch.tensor(rows, dtype=torch.int32, device=dev).reshape(-1)
         self.n_chunks = len(rows)
@@ -169,13 +173,17 @@ class FlatAdam(torch.optim.Optimizer):
                   _lib.ptr(grad_flat) if grad_flat is not None else None,
                   _lib.ptr(self.flat), _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq),
                   _lib.ptr(self.step_count), _lib.ptr(self.lr_dev), float(b1), float(b2),
-                  float(self.eps), float(self.weight_decay), float(grad_scale), _lib.stream())
+                  float(self.eps), float(self.weight_decay), float(grad_scale),
+                  _lib.ptr(self.stepped), _lib.stream())
         return loss
 
     # -- torch.optim.Adam-format state --------------------------------------------------------
     def state_dict(self):
         state = {}
+        stepped = self.stepped.cpu().tolist()
         for i, (p, o) in enumerate(zip(self.params, self._offs_host)):
+            if not stepped[i]:
+                continue
             n = p.numel()
             state[i] = {"step": self.step_count[0].detach().cpu().clone(),
                         "exp_avg": self.exp_avg[o:o + n].view_as(p).clone(),
@@ -195,10 +203,12 @@ class FlatAdam(torch.optim.Optimizer):
             pg["initial_lr"] = g["initial_lr"]
         steps = set()
         with torch.no_grad():
+            self.stepped.zero_()
             for i, (p, o) in enumerate(zip(self.params, self._offs_host)):
                 s = sd["state"].get(i)
                 if s is None:
                     continue
+                self.stepped[i] = 1
                 n = p.numel()
                 self.exp_avg[o:o + n].copy_(s["exp_avg"].reshape(-1))
                 self.exp_avg_sq[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))

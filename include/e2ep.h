@@ -414,12 +414,15 @@ int e2ep_se_gate_bwd(const float *x, const float *a, const float *dy, int planes
  * device fp32 counter incremented by the call and `lr` a device fp64 scalar read by it, so a
  * captured call follows an LR schedule (trainer/pl_trainer.py:120 CosineAnnealingLR) under
  * graph replay: no host scalar that changes between steps is baked into the launch.
+ * `stepped` (optional, int32 per tensor) is set to 1 for every tensor the call steps, so the
+ * caller can write torch.optim.Adam-format state for exactly the stepped tensors.
  * ------------------------------------------------------------------------------------- */
 int e2ep_adam_chunk_elems(void);
 int e2ep_adam_step(const int *chunks, int n_chunks, const long long *offsets,
                    const long long *grad_ptrs, const float *grad_flat, float *param, float *exp_avg,
                    float *exp_avg_sq, float *step, const double *lr, double beta1, double beta2,
-                   double eps, double weight_decay, float grad_scale, void *stream);
+                   double eps, double weight_decay, float grad_scale, int *stepped,
+                   void *stream);
 /* per-tensor gradients -> flat buffer (zeros for missing gradients), for the all-reduce;
  * a sub-range of the chunk table (chunks + 4*first, n) gathers one gradient bucket */
 int e2ep_grad_gather(const int *chunks, int n_chunks, const long long *offsets,
@@ -505,7 +508,14 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * (1024), 3 depthwise weight-gradient target workgroups (1024), 4 K-split e2ep_gemm target
  * workgroups (768), 5 1x1 weight-gradient target workgroups (1024), 6 conv forward /
  * data-gradient grids of at least this many wide (128 / 256-column) tiles use them (512).
- * For A/B timing. */
+ * For A/B timing.
+ * Contract for every plan override and tunable above (e2ep_conv_split_params,
+ * e2ep_gemm_force, e2ep_gemm_split_min, e2ep_bn_small*, e2ep_tune): a launch recomputes its
+ * plan from these process-wide settings, and the *_workspace() queries size the workspace
+ * from the same plan, so set them before a caller queries workspace sizes (in practice:
+ * before the first step is run or captured) and never change them between a caller's
+ * workspace query and its launch; a larger split count than the workspace was sized for
+ * would write past it. */
 int e2ep_tune(int key, int value);
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,

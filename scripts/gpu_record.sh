@@ -13,7 +13,7 @@ timeout -k 10 300 python bench.py > $O/bench_c2.log 2>&1 || exit 1
 echo "c2: $(grep -o '"value": [0-9.]*' $O/bench_c2.log | head -1) $(grep -o '"ms_per_step": [0-9.]*' $O/bench_c2.log | head -1)"
 timeout -k 10 200 python bench.py --no-cpu-baseline --precision bf16 > $O/bench_c3_bf16.log 2>&1 || exit 1
 echo "c3: $(grep -o '"value": [0-9.]*' $O/bench_c3_bf16.log | head -1)"
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 10 --no-cpu-baseline > $O/prof.log 2>&1 || exit 1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 10 --no-cpu-baseline --no-secondary > $O/prof.log 2>&1 || exit 1
 db=$(find $O/prof -name "*.db" | tail -n 1); python scripts/step_kernels.py "$db" 10 --top 80 > $O/step_kernels.txt 2>&1 || true
 head -3 $O/step_kernels.txt
 echo done

@@ -11,7 +11,7 @@ tail -1 $O/pytest.log
 for i in $(seq 1 $REP); do
   for t in ${TUNES:-0=1024 0=2048 1=8192 2=2048 3=1024 4=1536 5=1024}; do
     log=$O/bench_${t//[=,]/_}_$i.log
-    E2EP_TUNE=$t timeout -k 10 200 python bench.py --no-cpu-baseline > $log 2>&1 || exit 1
+    E2EP_TUNE=$t timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary > $log 2>&1 || exit 1
     echo "tune $t run $i: $(grep -o '"ms_per_step": [0-9.]*' $log | head -1)"
   done
 done

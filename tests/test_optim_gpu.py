@@ -62,6 +62,14 @@ def test_flat_adam_views_and_missing_grad():
     opt.step()
     assert torch.equal(ps[2].detach(), before[2])  # no gradient: not stepped (as torch)
     assert not torch.equal(ps[0].detach(), before[0])
+    # torch.optim.Adam keeps no state for a tensor that was never stepped
+    ref = _params(1)
+    topt = torch.optim.Adam(ref, lr=1e-2)
+    for p, g in zip(ref, _grads(0, skip=2)):
+        p.grad = g
+    topt.step()
+    assert sorted(opt.state_dict()["state"]) == sorted(topt.state_dict()["state"]) == [
+        i for i in range(len(SHAPES)) if i != 2]
 
 
 def test_flat_adam_gathered_grads_equal_table_grads():
