@@ -197,7 +197,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   const int nrx = (int)min(4LL * g.N * Kc * HWs, 0x7fffffffLL);
 
   // global -> register loads run two K-steps ahead of the MFMAs (two register sets), LDS
-  // is double buffered: one barrier per K-step, ~2 steps of MFMA work to cover a load
+  // is double buffered: one barrier per K-step, ~2 steps of MFMA work to cover a load.  (A
+  // third register set, loads three steps ahead, measured 5-40 % slower per shape in round 3.)
   float ra0[NA], rb0[BPER], ra1[NA], rb1[BPER];
   // Every call issues the same loads (steps past the range read zeros), so the loop has no
   // branches around loads and the s_waitcnt before each LDS store waits only for the step
@@ -293,12 +294,15 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     for (int kt = 0; kt < nk; kt += 2) {
       // buffer 0 holds step kt, registers 1 hold step kt+1
       load_tiles(kbeg + kt + 2, ra0, rb0);
+      // the loads stay at the top of the step (hipcc otherwise sinks them behind the MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
       compute(0);
       store_tiles(1, ra1, rb1);
       __syncthreads();
       if (kt + 1 >= nk) break;
       // buffer 1 holds step kt+1, registers 0 hold step kt+2
       load_tiles(kbeg + kt + 3, ra1, rb1);
+      __builtin_amdgcn_sched_barrier(0);
       compute(1);
       store_tiles(0, ra0, rb0);
       __syncthreads();
@@ -610,6 +614,7 @@ __global__ void __launch_bounds__(256) k_conv_gemm2(
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       load_tiles(kbeg + kt + 1);  // past the range: reads zeros, never stored
+      __builtin_amdgcn_sched_barrier(0);  // loads first, then the step's MFMAs
       compute(kt & 1);
       if (kt + 1 < nk) store_tiles((kt + 1) & 1);
       __syncthreads();
@@ -792,11 +797,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
     __syncthreads();
     for (int kt = 0; kt < nk; kt += 2) {
       load_tiles(ra0, rb0);
+      __builtin_amdgcn_sched_barrier(0);  // loads first, then the step's MFMAs
       compute(0);
       store_tiles(1, ra1, rb1);
       __syncthreads();
       if (kt + 1 >= nk) break;
       load_tiles(ra1, rb1);
+      __builtin_amdgcn_sched_barrier(0);
       compute(1);
       store_tiles(0, ra0, rb0);
       __syncthreads();
@@ -1274,9 +1281,19 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
   // 32-row tiles when 64-row tiles would pad M by more than 25 % (M = 24, 32, 96; measured:
   // for smaller savings the wider tile's better reuse wins, scripts/bench_conv.py)
   p.bm = 5LL * cdiv(M, 32) * 32 <= 4LL * cdiv(M, 64) * 64 ? 32 : 64;
-  const long long mblocks = cdiv(M, p.bm);
+  const long long mblocks0 = cdiv(M, p.bm);
   const int wide_n = p.bm == 64 ? 128 : 256;
-  p.bnt = cdiv(p.ncols, wide_n) * mblocks * p.nph >= g_tune[TUNE_CONV_WIDE_MIN] ? wide_n : wide_n / 2;
+  p.bnt = cdiv(p.ncols, wide_n) * mblocks0 * p.nph >= g_tune[TUNE_CONV_WIDE_MIN] ? wide_n : wide_n / 2;
+  // benchmarking override of the tile (e2ep_tune key 7 = bm * 1000 + bnt; 1 = automatic)
+  const int ft = g_tune[TUNE_CONV_FORCE_TILE];
+  if (ft > 1) {
+    const int fbm = ft / 1000, fbn = ft % 1000;
+    if ((fbm == 64 && (fbn == 64 || fbn == 128)) || (fbm == 32 && (fbn == 128 || fbn == 256))) {
+      p.bm = fbm;
+      p.bnt = fbn;
+    }
+  }
+  const long long mblocks = cdiv(M, p.bm);
   const long long blocks = cdiv(p.ncols, p.bnt) * mblocks * p.nph;
   p.splits = 1;
   // split K when the grid cannot fill the chip twice over (measured best: aim at ~1024
@@ -1288,6 +1305,9 @@ static GemmPlan plan_gemm(int mode, const ConvGeom &g, int M) {
     s = std::min(s, 32);
     p.splits = std::max(1, s);
   }
+  // benchmarking override of the K split (e2ep_tune key 8 = splits + 1; 1 = automatic)
+  if (g_tune[TUNE_CONV_FORCE_SPLITS] > 1 && p.nph == 1)
+    p.splits = std::min(g_tune[TUNE_CONV_FORCE_SPLITS] - 1, std::max(1, kmax));
   p.kper = cdiv(std::max(kmax, 1), p.splits);
   if (p.splits > 1) p.splits = cdiv(kmax, p.kper);
   return p;

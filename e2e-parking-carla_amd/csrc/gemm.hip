@@ -19,6 +19,7 @@
 //  * small grids split K (fixed-order reduction in k_gemm_reduce, so results are
 //    deterministic run to run), large ones write C directly with the fused epilogue.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "gemm.h"
@@ -45,10 +46,10 @@ __device__ __forceinline__ float kmask(float v, bool ok) {
 constexpr int G_BK = 32;
 constexpr int G_LDW = 36;  // LDS row stride in floats (32 k + 4 pad)
 
-template <bool AK, bool BKC, int WM, int TM, int TN>
+template <bool AK, bool BKC, int WM, int TM, int TN, int AVEC, int BVEC>
 __global__ void __launch_bounds__(256)
-    k_gemm(const float *__restrict__ A, int lda, long long a_bytes, int avec,
-           const float *__restrict__ B, int ldb, long long b_bytes, int bvec,
+    k_gemm(const float *__restrict__ A, int lda, long long a_bytes,
+           const float *__restrict__ B, int ldb, long long b_bytes,
            const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
            int ldadd, float *__restrict__ C, long long c_bytes, int ldc, GemmCols cols, int M,
            int N, int K, int kper, int relu, float *__restrict__ rs) {
@@ -91,17 +92,20 @@ __global__ void __launch_bounds__(256)
   // MFMAs and written to the other LDS buffer after them.  (Deeper register pipelines, 2 and
   // 3 steps, measured 4-5 % slower: the extra registers cost a wave per SIMD.)
   float ra[GA][4], rb[GB][4];
-  // Loads are unconditional: the row index is clamped into the matrix (rows past M / N only
-  // feed outputs that are never stored) and k into [0, K); values at k >= K are zeroed with
-  // an integer mask when the registers are written to LDS (after the step's MFMAs, so the
-  // loads stay in flight).  Guarded loads (`ok ? offset : OOR`) let the compiler split the
-  // loop into per-load exec-masked branches, which serialised the loads.
-  auto load_k = [&](float *regs, const __amdgpu_buffer_rsrc_t &rs, int vec, long long base,
-                    int k, bool full) {  // 4 k-contiguous values at base + k
-    if (vec == 2 && full) {
+  // Loads are unconditional and branch-free: the row index is clamped into the matrix (rows
+  // past M / N only feed outputs that are never stored) and k into the buffer; values at
+  // k >= K are zeroed with an integer mask when the registers are written to LDS (after the
+  // step's MFMAs, so the loads stay in flight).  The vector width is a template parameter: a
+  // run-time width / K-tail switch made hipcc branch around every load group and wait
+  // vmcnt(0) before the next one, serialising each K-step's loads (round 3, from the ISA).
+  // A vector load at the K tail may read past the row (masked) or the buffer (reads 0).
+  auto load_k = [&](float *regs, const __amdgpu_buffer_rsrc_t &rs, auto vec_c, long long base,
+                    int k) {  // 4 k-contiguous values at base + k
+    constexpr int vec = decltype(vec_c)::value;
+    if constexpr (vec == 2) {
       const float4 v = bload4(rs, (int)((base + k) * 4));
       regs[0] = v.x; regs[1] = v.y; regs[2] = v.z; regs[3] = v.w;
-    } else if (vec == 1 && full) {
+    } else if constexpr (vec == 1) {
       const float2 v0 = bload2(rs, (int)((base + k) * 4)), v1 = bload2(rs, (int)((base + k + 2) * 4));
       regs[0] = v0.x; regs[1] = v0.y; regs[2] = v1.x; regs[3] = v1.y;
     } else {
@@ -111,13 +115,12 @@ __global__ void __launch_bounds__(256)
   };
   auto load_tiles = [&](float (&xa)[GA][4], float (&xb)[GB][4], int ks_in) {
     const int k0 = min(ks_in, kend - 1) * G_BK;  // past the range: re-read, never stored
-    const bool full = k0 + G_BK <= K;             // uniform
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int row = min(m0 + 32 * i + ar, M - 1);
       const int k = k0 + 4 * aq;
       if (AK) {
-        load_k(xa[i], ra_, avec, (long long)row * lda, k, full);
+        load_k(xa[i], ra_, std::integral_constant<int, AVEC>{}, (long long)row * lda, k);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -129,7 +132,7 @@ __global__ void __launch_bounds__(256)
       const int k = k0 + 4 * bq;
       if (BKC) {
         const int row = min(n0 + 32 * i + br, N - 1);
-        load_k(xb[i], rb_, bvec, (long long)row * ldb, k, full);
+        load_k(xb[i], rb_, std::integral_constant<int, BVEC>{}, (long long)row * ldb, k);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -203,6 +206,9 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       load_tiles(ra, rb, kbeg + kt + 1);  // past the range: re-read, never stored
+      // keep the loads at the top of the step: hipcc otherwise sinks them behind half the
+      // MFMAs, leaving half a step to cover their latency before the LDS write waits on them
+      __builtin_amdgcn_sched_barrier(0);
       compute(kt & 1);
       if (kt + 1 < nk) store_tiles(ra, rb, (kt + 1) & 1, kbeg + kt + 1);
       __syncthreads();
@@ -473,25 +479,42 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
   dim3 grid(cdiv(Nx, td.bn), cdiv(M, td.bm), p.splits);
   const int avec = vec_of(ak, lda, A), bvec = vec_of(bk, ldb, B);
   const int br = bias_rows ? 1 : 0;
-#define E2EP_GEMM_LAUNCH(AKV, BKV, WMV, TMV, TNV)                                               \
-  hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, TMV, TNV>), grid, dim3(256), 0, s, A, lda, a_bytes, \
-                     avec, B, ldb, b_bytes, bvec, bias, br, Cadd, ldadd, out, c_bytes, ldc, cols, \
-                     M, N, K, p.kper, relu, rs)
-#define E2EP_GEMM_T(AKV, BKV)                                     \
-  do {                                                            \
-    switch (p.tile) {                                             \
-      case 2: E2EP_GEMM_LAUNCH(AKV, BKV, 1, 1, 1); break;          \
-      case 3: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 2, 2); break;          \
-      case 4: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 1, 2); break;          \
-      case 5: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 2, 1); break;          \
-      case 6: E2EP_GEMM_LAUNCH(AKV, BKV, 1, 2, 2); break;          \
-      default: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 1, 1); break;         \
-    }                                                             \
+#define E2EP_GEMM_LAUNCH(AKV, BKV, WMV, TMV, TNV, AVV, BVV)                                     \
+  hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, TMV, TNV, AVV, BVV>), grid, dim3(256), 0, s, A, lda,  \
+                     a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, out, c_bytes, ldc, cols, M, \
+                     N, K, p.kper, relu, rs)
+#define E2EP_GEMM_T(AKV, BKV, AVV, BVV)                                     \
+  do {                                                                      \
+    switch (p.tile) {                                                       \
+      case 2: E2EP_GEMM_LAUNCH(AKV, BKV, 1, 1, 1, AVV, BVV); break;          \
+      case 3: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 2, 2, AVV, BVV); break;          \
+      case 4: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 1, 2, AVV, BVV); break;          \
+      case 5: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 2, 1, AVV, BVV); break;          \
+      case 6: E2EP_GEMM_LAUNCH(AKV, BKV, 1, 2, 2, AVV, BVV); break;          \
+      default: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 1, 1, AVV, BVV); break;         \
+    }                                                                       \
   } while (0)
-  if (ak && bk) E2EP_GEMM_T(true, true);
-  else if (ak) E2EP_GEMM_T(true, false);
-  else if (bk) E2EP_GEMM_T(false, true);
-  else E2EP_GEMM_T(false, false);
+  // vector widths along k of the k-contiguous operands (template: no run-time switch)
+#define E2EP_GEMM_BV(AKV, BKV, AVV)                 \
+  do {                                              \
+    if (bvec == 2) E2EP_GEMM_T(AKV, BKV, AVV, 2);    \
+    else if (bvec == 1) E2EP_GEMM_T(AKV, BKV, AVV, 1); \
+    else E2EP_GEMM_T(AKV, BKV, AVV, 0);              \
+  } while (0)
+  if (ak && bk) {
+    if (avec == 2) E2EP_GEMM_BV(true, true, 2);
+    else if (avec == 1) E2EP_GEMM_BV(true, true, 1);
+    else E2EP_GEMM_BV(true, true, 0);
+  } else if (ak) {
+    if (avec == 2) E2EP_GEMM_T(true, false, 2, 0);
+    else if (avec == 1) E2EP_GEMM_T(true, false, 1, 0);
+    else E2EP_GEMM_T(true, false, 0, 0);
+  } else if (bk) {
+    E2EP_GEMM_BV(false, true, 0);
+  } else {
+    E2EP_GEMM_T(false, false, 0, 0);
+  }
+#undef E2EP_GEMM_BV
 #undef E2EP_GEMM_T
 #undef E2EP_GEMM_LAUNCH
   if (p.splits > 1) {

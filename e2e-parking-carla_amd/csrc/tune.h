@@ -10,7 +10,9 @@ enum Tune {
   TUNE_GEMM_SPLIT_TARGET = 4, // workgroups a K-split e2ep_gemm aims at
   TUNE_WGRAD1X1_TARGET = 5,   // workgroups the 1x1 weight gradient aims at
   TUNE_CONV_WIDE_MIN = 6,     // conv fwd / dgrad grids of at least this many wide tiles use them
-  TUNE_N = 7
+  TUNE_CONV_FORCE_TILE = 7,   // benchmarking: k_conv_gemm tile bm * 1000 + bnt (1 = automatic)
+  TUNE_CONV_FORCE_SPLITS = 8, // benchmarking: k_conv_gemm K splits + 1 (1 = automatic)
+  TUNE_N = 9
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

@@ -90,7 +90,8 @@ int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
 
 /* Diagnostics only: when dev_buf != NULL every later e2ep_lss_fwd launch (C % 4 == 0 path)
  * records per block {start, end (s_memrealtime, 100 MHz), XCC/HW id, points} as 4 int64 at
- * dev_buf[4*block]; NULL turns it off.  Used by scripts/trace_lss_fwd.py. */
+ * dev_buf[4*block]; NULL turns it off (the round-2 per-block trace; the reading script is in
+ * git history, commit a6dfde2). */
 int e2ep_debug_fwd_trace(void *dev_buf);
 
 /* Backward of e2ep_lss_fwd (replaces VoxelsSumming.backward, tool/geometry.py:307-317, and
@@ -507,7 +508,9 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * 1 minimum elements per split-BN workgroup (4096), 2 float4 vectors per BN apply workgroup
  * (1024), 3 depthwise weight-gradient target workgroups (1024), 4 K-split e2ep_gemm target
  * workgroups (768), 5 1x1 weight-gradient target workgroups (1024), 6 conv forward /
- * data-gradient grids of at least this many wide (128 / 256-column) tiles use them (512).
+ * data-gradient grids of at least this many wide (128 / 256-column) tiles use them (512),
+ * 7 k_conv_gemm block tile forced to bm * 1000 + bnt (64064, 64128, 32128, 32256; 1 =
+ * automatic), 8 k_conv_gemm K splits forced to value - 1 (1 = automatic).
  * For A/B timing.
  * Contract for every plan override and tunable above (e2ep_conv_split_params,
  * e2ep_gemm_force, e2ep_gemm_split_min, e2ep_bn_small*, e2ep_tune): a launch recomputes its

@@ -1,8 +1,10 @@
 """Per-shape timing of the e2ep implicit-GEMM conv kernels (fwd / dgrad / wgrad separately,
 back-to-back launches between HIP events) on the conv shapes of one ParkingModel train step.
 
-    python scripts/bench_conv.py [--record] [--top 30]
---record runs the model once to (re)write scripts/conv_shapes.json."""
+    python scripts/bench_conv.py [--record] [--top 30] [--ab "6=512;6=1024"]
+--record runs the model once to (re)write scripts/conv_shapes.json; --ab times every shape
+under each ';'-separated e2ep_tune setting ("key=value,key=value"), interleaved in one
+process, and prints the per-setting totals and per-shape times side by side."""
 import argparse
 import json
 import os
@@ -61,7 +63,10 @@ def main():
     ap.add_argument("--record", action="store_true")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--ab", default=None)
     a = ap.parse_args()
+    if a.ab:
+        return ab(a)
     from e2ep_amd import _lib, conv
     shapes = record(a.batch) if a.record or not os.path.exists(SHAPES) else json.load(open(SHAPES))
     rows = []
@@ -96,6 +101,58 @@ def main():
     for tot_ms, n, d, tf, td, tw, fl in rows[:a.top]:
         desc = f"{d[0]},{d[1]},{d[2]},{d[3]}->{d[4]},{d[5]}x{d[6]}/{d[9]}"
         print(f"{desc:>34} {n:2d} | {tf:6.3f} {td:6.3f} {tw:6.3f} | {fl / tf / 1e9:5.1f} {fl / td / 1e9:5.1f} {fl / tw / 1e9:5.1f}")
+
+
+def _apply(setting):
+    from e2ep_amd import _lib
+    lib = _lib.load()
+    for kv in filter(None, setting.split(",")):
+        k, v = kv.split("=")
+        if k == "v":  # conv GEMM kernel variant (e2ep_conv_gemm_variant)
+            lib.e2ep_conv_gemm_variant(int(v))
+        else:
+            lib.e2ep_tune(int(k), int(v))
+
+
+def ab(a):
+    """Interleaved A/B of e2ep_tune settings per shape (fwd / dgrad / wgrad)."""
+    from e2ep_amd import conv
+    settings = a.ab.split(";")
+    shapes = json.load(open(SHAPES))
+    tot = {st: [0.0, 0.0, 0.0] for st in settings}
+    rows = []
+    for sh in shapes:
+        d = sh["dims"]
+        N, Cin, H, W, Cout, R, S, P, Q = d[:9]
+        x = torch.randn(N, Cin, H, W, device="cuda")
+        w = torch.randn(Cout, Cin, R, S, device="cuda")
+        gy = torch.randn(N, Cout, P, Q, device="cuda")
+        y = torch.empty_like(gy)
+        gc = sh["grad_channels"] or Cin
+        dx = torch.empty(N, gc, H, W, device="cuda")
+        dw = torch.empty_like(w)
+        wt = conv.tap_major(w)
+        res = {}
+        for rep in range(3):
+            for st in settings:
+                _apply(st)
+                t = (timeit(lambda: conv.conv_fwd(x, wt, None, d, sh["act"], y, w_layout=1)),
+                     timeit(lambda: conv.conv_dgrad(gy, wt, d, gc, dx, w_layout=1)),
+                     timeit(lambda: conv.conv_wgrad(gy, x, d, dw)))
+                res[st] = t if st not in res else tuple(min(u, v) for u, v in zip(res[st], t))
+        n = sh["count"]
+        for st in settings:
+            for i in range(3):
+                tot[st][i] += n * res[st][i]
+        rows.append((n, d, res))
+    _apply(settings[0])
+    for st in settings:
+        f, dg, wg = tot[st]
+        print(f"[{st}] fwd {f:.3f} dgrad {dg:.3f} wgrad {wg:.3f} = {f + dg + wg:.3f} ms/step")
+    for n, d, res in sorted(rows, key=lambda r: -r[0] * sum(r[2][settings[0]])):
+        desc = f"{d[0]},{d[1]},{d[2]},{d[3]}->{d[4]},{d[5]}x{d[6]}/{d[9]}"
+        print(f"{desc:>34} {n:2d} | " + " | ".join(
+            " ".join(f"{1e3 * v:6.1f}" for v in res[st]) for st in settings))
 
 
 if __name__ == "__main__":
