@@ -494,6 +494,14 @@ def main():
     r = train_step_rate(dev, world, rank, args.batch, args.steps, args.warmup, hires,
                         eager=args.eager)
     mod, step, loss = r["module"], r["step"], r["loss"]
+    grad_exchange = None
+    if world > 1:
+        if getattr(step, "segmented", False):
+            b1, b2 = step.seg_buckets
+            grad_exchange = (f"backward in 2 captured segments; {len(b1)} stage-1 buckets "
+                             f"all-reduced (RCCL) during the stage-2 backward, {len(b2)} after it")
+        else:
+            grad_exchange = "one flat all-reduce between the backward and optimizer graphs"
     value, ms_step = r["value"], r["ms_per_step"]
     final_loss = round(float(loss), 4)
     data = step.batch
@@ -569,7 +577,8 @@ def main():
                                         if lowp else "fp32") + ", random init",
                            "global_batch": world * args.batch, "batch_per_gpu": args.batch,
                            "parallelism": f"dp{world}"},
-                "world": {"size": world, "backend": backend, "rehearsal": rehearsal},
+                "world": {"size": world, "backend": backend, "rehearsal": rehearsal,
+                          "grad_exchange": grad_exchange},
                 "roofline": roofline, "step_roofline": step_roofline, "roofline_lss": roofline_lss,
                 "lss_c4": c4, "cpu_baseline": base, "final_loss": final_loss,
                 "secondary": secondary}

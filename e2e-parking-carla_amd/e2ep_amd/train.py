@@ -13,12 +13,19 @@ __call__ refreshes from param_groups[0]['lr'] before each replay, so an LR sched
 Data parallelism (one process per GPU, RCCL over xGMI; DistributedDataParallel semantics
 without its module wrapper), one flat fp32 gradient buffer in FlatAdam's layout; the
 1/world mean is folded into the Adam launch.
-  * graph mode (the bench): g_bwd (fwd + losses + bwd) -> g_gather (per-tensor gradients ->
-    flat buffer, one launch) -> ONE all-reduce of the 78 MB buffer issued from the host
-    between the replays -> g_opt.  The collective is not captured: on this stack (torch
-    2.10 / RCCL 2.26) a captured ProcessGroupNCCL collective makes the c10d watchdog fault
-    on its capture-time event, and a backward graph with bucket gathers forked onto a side
-    stream replayed wrong camera-encoder gradients (profiles/r02/ddp_diag/).
+  * graph mode with RCCL (the bench at N > 1): the backward runs in two segments
+    (e2ep_amd.segments; the model cuts its forward below the BEV encoder): g_s1 (fwd + losses
+    + stage-1 backward: heads, transformer, BEV encoder) -> g_s1g (their gradients -> the flat
+    buffer) -> the host issues the stage-1 buckets' all-reduces (~25 MB each, reverse layout
+    order) on a communication stream -> g_s2 (stage 2: lift-splat + camera encoder backward,
+    concurrent with those all-reduces) -> g_s2g -> the stage-2 bucket(s) -> the compute stream
+    waits for every bucket -> g_opt.  No collective is captured: on this stack (torch 2.10 /
+    RCCL 2.26) a captured ProcessGroupNCCL collective made the c10d watchdog fault on its
+    capture-time event, and a backward graph with bucket gathers forked onto a side stream
+    replayed wrong camera-encoder gradients (profiles/r02/ddp_diag/); here every
+    collective is an ordinary host-issued RCCL call between graph replays.
+  * graph mode without cut points (or gloo): g_bwd (fwd + losses + bwd) -> g_gather -> ONE
+    all-reduce of the flat buffer issued from the host between the replays -> g_opt.
   * eager mode: DDP-style overlap — the buffer is cut into ~25 MB buckets in reverse layout
     order; a post-accumulate-grad hook per parameter counts arrivals and, when a bucket is
     complete (and every earlier one issued: the same order on every rank), a side stream
@@ -40,7 +47,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import _lib, graphs
+from . import _lib, graphs, segments
 from .optim import FlatAdam
 
 BUCKET_MB = 25.0  # DistributedDataParallel's default bucket_cap_mb
@@ -177,6 +184,7 @@ class TrainStep:
             overlap = os.environ.get("E2EP_DDP_OVERLAP", "1") != "0"
         # hook-driven bucket all-reduce overlapping backward: eager steps with RCCL, and host
         # tensors (gloo on CPU); never inside a captured graph (module docstring)
+        self._bucket_mb = bucket_mb
         self.overlap = bool(self.ddp and overlap and not graph and
                             (self.backend == "nccl" or not self.flat_grad.is_cuda))
         self.buckets = (GradBuckets(self.params, self.opt, self.flat_grad, bucket_mb)
@@ -188,6 +196,10 @@ class TrainStep:
                       and self.flat_grad.is_cuda else None)
         self.loss = None
         self.g_bwd = self.g_gather = self.g_opt = None
+        # segmented backward (graph mode, RCCL): stage graphs, their gathers, bucket ranges
+        self.segmented = bool(self.ddp and graph and self.backend == "nccl")
+        self.g_s1 = self.g_s1g = self.g_s2 = self.g_s2g = None
+        self.seg_buckets = None  # ([stage-1 (lo, hi)], [stage-2 (lo, hi)]) of the flat buffer
         self._rig = _rig_key(batch)
         if graph:
             self._capture(warmup)
@@ -239,6 +251,91 @@ class TrainStep:
         self._update()
         return loss
 
+    # -- segmented backward (graph mode with RCCL) ----------------------------------------
+    def _stage1(self):
+        self.opt.zero_grad(set_to_none=True)
+        with segments.record() as rec:
+            loss = self.module.training_step(self.batch, 0)
+        self._pairs = rec.pairs
+        loss.backward()
+        return loss.detach()
+
+    def _stage2(self):
+        segments.backward_rest(self._pairs)
+
+    def _buckets_of(self, i0, i1, bucket_mb):
+        """Flat ranges of ~bucket_mb over parameters [i0, i1), last parameters first (the
+        order their gradients complete in, as DistributedDataParallel buckets them)."""
+        cap = int(bucket_mb * 2 ** 20) // 4
+        spans, out = self.opt.spans, []
+        end = self.opt.numel if i1 == len(self.params) else spans[i1][0]
+        j1 = i1
+        while j1 > i0:
+            j0, n = j1, 0
+            while j0 > i0 and (n == 0 or n + spans[j0 - 1][1] <= cap):
+                j0 -= 1
+                n += spans[j0][1]
+            lo = spans[j0][0]
+            out.append((lo, end))
+            end, j1 = lo, j0
+        return out
+
+    def _capture_segmented(self, bucket_mb):
+        """Capture g_s1 / g_s1g / g_s2 / g_s2g; False (nothing kept) when the module declares
+        no cut point or its stage-1 gradients are not a suffix of the flat layout."""
+        segments.ensure_anchor(self.params[0].device)
+        g1, loss, _ = graphs.capture(self._stage1)
+        if not self._pairs:
+            return False
+        has1 = [p.grad is not None for p in self.params]
+        if not any(has1):
+            return False
+        i1 = has1.index(True)
+        if not all(has1[i1:]):
+            return False
+        self.opt.prepare(params=(i1, len(self.params)))
+        g1g, _, _ = graphs.capture(lambda: self.opt.gather_grads(self.flat_grad,
+                                                                 params=(i1, len(self.params))),
+                                   pool=g1.pool())
+        g2, _, _ = graphs.capture(self._stage2, pool=g1.pool())
+        self.opt.prepare()
+        if i1 > 0:
+            g2g, _, _ = graphs.capture(lambda: self.opt.gather_grads(self.flat_grad, params=(0, i1)),
+                                       pool=g1.pool())
+        else:
+            g2g = None
+        self.g_s1, self.g_s1g, self.g_s2, self.g_s2g, self.loss = g1, g1g, g2, g2g, loss
+        self.seg_buckets = (self._buckets_of(i1, len(self.params), bucket_mb),
+                            self._buckets_of(0, i1, bucket_mb))
+        self.comm = torch.cuda.Stream(device=self.flat_grad.device)
+        # which tensors have a gradient is fixed by the captured graphs: all-reduced once (MAX)
+        self.opt.has_grad(self.has_grad)
+        dist.all_reduce(self.has_grad, op=dist.ReduceOp.MAX)
+        return True
+
+    def _replay_segmented(self):
+        main = torch.cuda.current_stream()
+        works = []
+
+        def issue(ranges):
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                for lo, hi in ranges:
+                    works.append(dist.all_reduce(self.flat_grad[lo:hi], async_op=True))
+
+        self.g_s1.replay()
+        self.g_s1g.replay()
+        issue(self.seg_buckets[0])  # overlaps the stage-2 backward below
+        self.g_s2.replay()
+        if self.g_s2g is not None:
+            self.g_s2g.replay()
+        issue(self.seg_buckets[1])
+        for w in works:
+            w.wait()  # the compute stream waits for every bucket
+        self.g_opt.replay()
+
     # -- capture --------------------------------------------------------------------------
     def _capture(self, warmup):
         s = torch.cuda.Stream()
@@ -248,6 +345,13 @@ class TrainStep:
                 self._eager()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        if self.segmented:
+            self.segmented = self._capture_segmented(self._bucket_mb)
+            if self.segmented:
+                self.g_opt, _, _ = graphs.capture(self._update, pool=self.g_s1.pool())
+                return
+            self.opt.zero_grad(set_to_none=True)
+            self._pairs = None
         self.g_bwd, self.loss, self.memsets = graphs.capture(self._fwd_bwd)
         # the captured gradients keep their (graph-pool) addresses on every replay
         self.opt.prepare()
@@ -271,6 +375,9 @@ class TrainStep:
             sync_lr()
         if not self.graph:
             self.loss = self._eager()
+            return self.loss
+        if self.segmented:
+            self._replay_segmented()
             return self.loss
         self.g_bwd.replay()
         if self.g_gather is not None:

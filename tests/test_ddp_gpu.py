@@ -3,10 +3,11 @@
 * The LR a captured step uses is a device scalar (FlatAdam.lr_dev): CosineAnnealingLR
   (reference trainer/pl_trainer.py:120) changes it between replays exactly as it changes an
   eager step.
-* RCCL at world 1 (the exchange is an identity): the graph-mode step (captured gather, host-
-  issued flat all-reduce, captured Adam) and the eager step with the bucketed, hook-driven
-  all-reduce overlapping backward both give the same parameters as the step without an
-  exchange, bit for bit.
+* RCCL at world 1 (the exchange is an identity): the graph-mode step (backward in two
+  captured segments, the stage-1 buckets' all-reduces issued between the segment replays so
+  they overlap the stage-2 backward, captured Adam) and the eager step with the bucketed,
+  hook-driven all-reduce overlapping backward both give the same parameters as the step
+  without an exchange, bit for bit.
 * gloo at world 2, both ranks on cuda:0 (the one-GPU rehearsal of the N>1 path): the
   host-staged flat gradient all-reduce of the real ParkingModel TrainStep with the same batch
   on both ranks equals the one-process step (mean of two equal gradients), replay for replay.
@@ -119,7 +120,13 @@ def test_rccl_world1_exchange_is_exact(graph):
         s_ref = TrainStep(m_ref, _parking_batch(), graph=graph, warmup=1)
         s_ddp = TrainStep(m_ddp, _parking_batch(), graph=graph, warmup=1, ddp=True, bucket_mb=4.0)
         if graph:
-            assert s_ddp.buckets is None and s_ddp.g_gather is not None
+            # segmented backward: >= 4 buckets, most of them issued before stage 2 runs
+            assert s_ddp.buckets is None and s_ddp.segmented and s_ddp.g_bwd is None
+            b1, b2 = s_ddp.seg_buckets
+            assert len(b1) + len(b2) >= 4 and len(b1) >= 3 and len(b2) >= 1
+            spans = sorted(b1 + b2)
+            assert spans[0][0] == 0 and spans[-1][1] == s_ddp.flat_grad.numel()
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))  # a partition
         else:
             assert s_ddp.buckets is not None and len(s_ddp.buckets.buckets) >= 10
         for _ in range(3):
