@@ -297,6 +297,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       // the loads stay at the top of the step (hipcc otherwise sinks them behind the MFMAs)
       __builtin_amdgcn_sched_barrier(0);
       compute(0);
+      __builtin_amdgcn_sched_barrier(0);  // the LDS write after all of the step's MFMAs
       store_tiles(1, ra1, rb1);
       __syncthreads();
       if (kt + 1 >= nk) break;
@@ -304,6 +305,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       load_tiles(kbeg + kt + 3, ra1, rb1);
       __builtin_amdgcn_sched_barrier(0);
       compute(1);
+      __builtin_amdgcn_sched_barrier(0);
       store_tiles(0, ra0, rb0);
       __syncthreads();
     }
@@ -613,10 +615,14 @@ __global__ void __launch_bounds__(256) k_conv_gemm2(
     store_tiles(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-      load_tiles(kbeg + kt + 1);  // past the range: reads zeros, never stored
+      load_tiles(kbeg + kt + 1);  // past the range: reads zeros
       __builtin_amdgcn_sched_barrier(0);  // loads first, then the step's MFMAs
       compute(kt & 1);
-      if (kt + 1 < nk) store_tiles((kt + 1) & 1);
+      // all of the step's MFMAs before the LDS write (hipcc otherwise hoists the write, and
+      // its wait on the loads, into the middle of them); unconditional (the last step's zeros
+      // land in the idle buffer): a conditional store lets hipcc sink the loads into its branch
+      __builtin_amdgcn_sched_barrier(0);
+      store_tiles((kt + 1) & 1);
       __syncthreads();
     }
   }
@@ -805,6 +811,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
       load_tiles(ra1, rb1);
       __builtin_amdgcn_sched_barrier(0);
       compute(1);
+      __builtin_amdgcn_sched_barrier(0);
       store_tiles(0, ra0, rb0);
       __syncthreads();
     }
@@ -821,6 +828,153 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// bwd-weight, second generation (round 3).  The same GEMM as k_conv_wgrad (M = Cout, N =
+// (ci, live tap), K = pixels split over blocks into fixed-order slabs), for maps whose pixel
+// count per image is a multiple of the 32-pixel K-step (every hot-path map), so a K-step never
+// straddles two images:
+//  * the step's image and first pixel are wave-uniform.  (k_conv_wgrad advances a per-lane
+//    pixel index through the images with a divergent loop, and hipcc drains the in-flight
+//    loads around it: the ISA showed vmcnt(7..1) waits before every step's loads.)
+//  * LDS rows are k-contiguous ([row][32 + 4 pad]); a lane's 16 MFMA operands per step are
+//    four ds_read_b128 per operand (lane half h supplies k = 16h .. 16h+15), as in k_gemm.
+//  * A = g rows load as float4 along the pixels; B = the im2col x columns load one pixel per
+//    lane, lanes on consecutive pixels (coalesced along the image rows).
+//  * the next step's loads are issued at the top of the step (one step of lookahead).
+// OP 1 (bf16, BASELINE C3): two 32x32x16 bf16 MFMAs per step on the same operand registers.
+// ------------------------------------------------------------------------------------------
+constexpr int W2K = 32, W2LD = 36;
+
+template <int OP>
+__global__ void __launch_bounds__(256) k_conv_wgrad2(
+    const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
+    ConvGeom g, int pix_per_split, TapList tl) {
+  __shared__ __attribute__((aligned(16))) float As[2][64][W2LD];  // As[co][pixel]
+  __shared__ __attribute__((aligned(16))) float Bs[2][64][W2LD];  // Bs[column][pixel]
+  __shared__ int s_tap[MAXTAPS];
+  if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
+  __syncthreads();
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int RS = g.R * g.S;
+  const int Kw = g.Cin * RS;    // columns of dW (ci-major, tap-minor)
+  const int Kl = g.Cin * tl.n;  // live columns (ci, live tap index)
+  const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const int split = blockIdx.z;
+  const int PQ = g.P * g.Q;
+  const int Ptot = g.N * PQ;
+  const int pbeg = split * pix_per_split;  // a multiple of W2K
+  const int pend = min(Ptot, pbeg + pix_per_split);
+  const int nk = max(0, (pend - pbeg) / W2K);  // Ptot % W2K == 0: whole steps only
+  const int HW = g.H * g.W;
+
+  // A: thread = (co row tid/8 and +32, pixel quad tid%8)
+  const int ar = tid >> 3, aq = tid & 7;
+  // B: thread = (pixel tid%32, column group tid/32): columns bcg + 8 j
+  const int bp = tid & 31, bcg = tid >> 5;
+  int cconst[8], cdy[8], cdx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = n0 + bcg + 8 * j;
+    const int cc = col < Kl ? col : 0;
+    const int ci = cc / tl.n, tap = s_tap[cc - ci * tl.n];
+    const int r = tap / g.S, sx = tap - r * g.S;
+    cdy[j] = r * g.dh - g.ph;
+    cdx[j] = sx * g.dw - g.pw;
+    cconst[j] = ci * HW + cdy[j] * g.W + cdx[j];
+    if (col >= Kl) cdy[j] = -(1 << 29);  // never in bounds
+  }
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
+  const int nrx = (int)min(4LL * g.N * g.Cin * HW, 0x7fffffffLL);
+
+  float4 ra[2];
+  float rb[8];
+  auto load_tiles = [&](int ks) {
+    const int p0 = pbeg + min(ks, nk - 1) * W2K;  // past the range: re-read, never stored
+    const int im = p0 / PQ, od0 = p0 - im * PQ;   // wave-uniform
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = m0 + ar + 32 * i;
+      ra[i] = bload4(rg, co < g.Cout ? ((im * g.Cout + co) * PQ + od0 + 4 * aq) * 4 : OOR);
+    }
+    const int od = od0 + bp;
+    const int oy = od / g.Q, ox = od - oy * g.Q;
+    const int yb = oy * g.sh, xb = ox * g.sw;
+    const int pbase = im * g.Cin * HW + yb * g.W + xb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = (unsigned)(yb + cdy[j]) < (unsigned)g.H && (unsigned)(xb + cdx[j]) < (unsigned)g.W;
+      rb[j] = bload(rx, ok ? (pbase + cconst[j]) * 4 : nrx);
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<float4 *>(&As[buf][ar + 32 * i][4 * aq]) = ra[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Bs[buf][bcg + 8 * j][bp] = rb[j];
+  };
+
+  f32x16 acc = {0};
+  const int li = lane & 31, lh = lane >> 5;
+  auto compute = [&](int buf) {
+    float a[16], b[16];
+    const float *pa = &As[buf][32 * wm + li][16 * lh];
+    const float *pb = &Bs[buf][32 * wn + li][16 * lh];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 u = *reinterpret_cast<const float4 *>(pa + 4 * q);
+      const float4 v = *reinterpret_cast<const float4 *>(pb + 4 * q);
+      a[4 * q] = u.x; a[4 * q + 1] = u.y; a[4 * q + 2] = u.z; a[4 * q + 3] = u.w;
+      b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+    }
+    if (OP == 0) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk], b[kk], acc, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        bf16x8 av, bv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          av[j] = (__bf16)a[8 * blk + j];
+          bv[j] = (__bf16)b[8 * blk + j];
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+      }
+    }
+  };
+  if (nk > 0) {
+    load_tiles(0);
+    store_tiles(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      load_tiles(kt + 1);
+      __builtin_amdgcn_sched_barrier(0);  // loads first, then the step's MFMAs
+      compute(kt & 1);
+      // all of the step's MFMAs before the LDS write (hipcc otherwise hoists the write, and its
+      // wait on the loads, into the middle of them); unconditional (the last step's copy lands
+      // in the idle buffer and is never read): a conditional store lets hipcc sink the B loads
+      // into its branch, behind the MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      store_tiles((kt + 1) & 1);
+      __syncthreads();
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
+  const int lcol = n0 + 32 * wn + li;
+  const int lci = lcol < Kl ? lcol / tl.n : 0;
+  const int col = lci * RS + s_tap[lcol < Kl ? lcol - lci * tl.n : 0];  // dW column
+#pragma unroll
+  for (int rr = 0; rr < 16; ++rr) {
+    const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+    const bool ok = co < g.Cout && lcol < Kl;
+    bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[rr]);
+  }
+}
 
 // ------------------------------------------------------------------------------------------
 // bwd-weight of 1x1 / stride-1 / unpadded convs (the EfficientNet expand / project convs,
@@ -1006,6 +1160,52 @@ __global__ void __launch_bounds__(1024) k_reduce_splits(const float *__restrict_
     for (int j = 0; j < 16; ++j) s += red[j][o];
     out[i] = accumulate ? out[i] + s : s;
   }
+}
+
+// The same reduction, four consecutive outputs per thread (n % 4 == 0): float4 loads of every
+// slab in split order, summed in that order.  The 16-lane tree above runs ~1.4 loads per
+// thread and left the launch latency-bound (15 us for the 13.5 MB of slabs of a 16x16 1x1
+// conv's weight gradient, ~1 TB/s); here each thread keeps all its slab loads in flight.
+__global__ void __launch_bounds__(256) k_reduce_splits4(const float *__restrict__ part, int splits,
+                                                         int n, float *__restrict__ out,
+                                                         int accumulate, int RS,
+                                                         unsigned long long mask) {
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 acc = *reinterpret_cast<const float4 *>(part + i);
+#pragma unroll 8
+  for (int k = 1; k < splits; ++k) {
+    const float4 v = *reinterpret_cast<const float4 *>(part + (size_t)k * n + i);
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  float r[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (!((mask >> ((i + e) % RS)) & 1ULL)) r[e] = 0.f;  // dead tap: never written by the GEMM
+  float4 o = make_float4(r[0], r[1], r[2], r[3]);
+  if (accumulate) {
+    const float4 a = *reinterpret_cast<const float4 *>(out + i);
+    o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+  }
+  *reinterpret_cast<float4 *>(out + i) = o;
+}
+
+// fixed-order split-K reduction of the weight-gradient slabs: the float4 kernel when it has
+// enough threads to fill the chip (>= 32768: one per 4 outputs) and few slabs each; the split-
+// lane kernel otherwise (small weights with hundreds of slabs, e.g. the 1x1 weight gradients
+// of the 128x128 maps: one float4 thread per 4 outputs serialises those, 27 -> 39 us)
+static void reduce_splits(const float *part, int splits, int n, float *out, int accumulate, int RS,
+                          unsigned long long mask, hipStream_t s) {
+  if (n % 4 == 0 && n >= 131072 && splits <= 64 && (reinterpret_cast<uintptr_t>(part) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) & 15) == 0)
+    hipLaunchKernelGGL(k_reduce_splits4, dim3(cdiv(n / 4, 256)), dim3(256), 0, s, part, splits, n,
+                       out, accumulate, RS, mask);
+  else
+    hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, splits, n, out,
+                       accumulate, RS, mask);
 }
 
 // per-channel bias gradient: db[c] = sum over (n, p) of g[n, c, p]  (one block per channel)
@@ -1628,19 +1828,27 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
     else W1_LAUNCH(1, 1);
 #undef W1_LAUNCH
     const int n = g.Cout * g.Cin;
-    hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
-                       accumulate, 1, 1ULL);
+    reduce_splits(part, used, n, dw, accumulate, 1, 1ULL, s);
     return launch_status("e2ep_conv_wgrad");
   }
   const int Ptot = g.N * g.P * g.Q;
-  const int kb = g_wgrad_kb;
+  // second generation when the K-step never straddles images (e2ep_tune key 9: 1 = always
+  // the first generation, for A/B timing)
+  const bool v2 = (g.P * g.Q) % W2K == 0 && g_tune[TUNE_WGRAD_GEN] != 1;
+  const int kb = v2 ? W2K : g_wgrad_kb;
   int per = (Ptot + splits - 1) / splits;
   per = (per + kb - 1) / kb * kb;
   const int used = (Ptot + per - 1) / per;
   const TapList tl = live_taps(g);
   hipStream_t s = as_stream(stream);
   float *part = static_cast<float *>(workspace);
-  if (tl.n > 0) {
+  if (tl.n > 0 && v2) {
+    dim3 grid(cdiv(g.Cin * tl.n, 64), cdiv(g.Cout, 64), used);
+    if (g_conv_precision == 1)
+      hipLaunchKernelGGL((k_conv_wgrad2<1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+    else
+      hipLaunchKernelGGL((k_conv_wgrad2<0>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+  } else if (tl.n > 0) {
     dim3 grid(cdiv(g.Cin * tl.n, WBN), cdiv(g.Cout, BM), used);
 #define WG_LAUNCH(OPV, KBV) \
   hipLaunchKernelGGL((k_conv_wgrad<OPV, KBV>), grid, dim3(256), 0, s, gout, x, part, g, per, tl)
@@ -1653,8 +1861,7 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
 #undef WG_LAUNCH
   }
   const int n = g.Cout * g.Cin * g.R * g.S;
-  hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, used, n, dw,
-                     accumulate, g.R * g.S, tl.mask);
+  reduce_splits(part, used, n, dw, accumulate, g.R * g.S, tl.mask, s);
   return launch_status("e2ep_conv_wgrad");
 }
 

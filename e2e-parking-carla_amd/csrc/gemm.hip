@@ -210,7 +210,12 @@ __global__ void __launch_bounds__(256)
       // MFMAs, leaving half a step to cover their latency before the LDS write waits on them
       __builtin_amdgcn_sched_barrier(0);
       compute(kt & 1);
-      if (kt + 1 < nk) store_tiles(ra, rb, (kt + 1) & 1, kbeg + kt + 1);
+      // all of the step's MFMAs before the LDS write (hipcc otherwise hoists the write, and its
+      // wait on the loads, into the middle of them); unconditional: the last step's copy lands
+      // in the idle buffer and is never read (a conditional store lets hipcc sink loads into
+      // its branch, behind the MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
+      store_tiles(ra, rb, (kt + 1) & 1, min(kbeg + kt + 1, kend - 1));
       __syncthreads();
     }
   }

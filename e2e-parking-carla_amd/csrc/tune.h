@@ -12,7 +12,8 @@ enum Tune {
   TUNE_CONV_WIDE_MIN = 6,     // conv fwd / dgrad grids of at least this many wide tiles use them
   TUNE_CONV_FORCE_TILE = 7,   // benchmarking: k_conv_gemm tile bm * 1000 + bnt (1 = automatic)
   TUNE_CONV_FORCE_SPLITS = 8, // benchmarking: k_conv_gemm K splits + 1 (1 = automatic)
-  TUNE_N = 9
+  TUNE_WGRAD_GEN = 9,         // spatial weight-gradient kernel: 2 = k_conv_wgrad2 where it applies, 1 = k_conv_wgrad
+  TUNE_N = 10
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep
