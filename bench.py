@@ -336,9 +336,9 @@ def _release():
 
 def secondary_c3(dev, steps, warmup):
     """BASELINE configs[2] per GPU (C3): the same B=8 train step with bf16 operands in every
-    conv GEMM (forward, data gradient, weight gradient), fp32 accumulation, fp32 tensors in
-    HBM, fp32 master weights / Adam / all-reduce; samples/s and its conv-family roofline
-    against the bf16 dense peak."""
+    conv GEMM and transformer linear (forward, data gradient, weight gradient), fp32
+    accumulation, fp32 tensors in HBM, fp32 master weights / Adam / all-reduce; samples/s and
+    its conv-family roofline against the bf16 dense peak."""
     from e2ep_amd import precision
     prev = precision.set("bf16")
     try:
@@ -346,7 +346,8 @@ def secondary_c3(dev, steps, warmup):
         roof, _ = conv_roofline(r["step"], True)
     finally:
         precision.set(prev)
-    out = {"config": "C3 per GPU: B=8, 4 cams x 256^2, bf16 operands in the conv GEMMs (forward, "
+    out = {"config": "C3 per GPU: B=8, 4 cams x 256^2, bf16 operands in the conv GEMMs and the "
+                     "transformer linears (forward, "
                      "data gradient, weight gradient), fp32 accumulate / storage / optimizer",
            "value": round(r["value"], 3), "unit": "samples/s", "ms_per_step": round(r["ms_per_step"], 3),
            "steps": steps, "roofline": roof}
@@ -456,9 +457,9 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the C3 / C4 / C5 sub-records of the default (C2, N=1) line")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
-                    help="conv GEMM operands: fp32 (C2, default) or bf16 (C3: bf16 operands in "
-                         "the forward, data-gradient and weight-gradient conv GEMMs, fp32 "
-                         "accumulation, storage, optimizer and everything else)")
+                    help="GEMM operands: fp32 (C2, default) or bf16 (C3: bf16 operands in the "
+                         "forward, data-gradient and weight-gradient conv GEMMs and transformer "
+                         "linears, fp32 accumulation, storage, optimizer and everything else)")
     args = ap.parse_args()
     hires = args.workload == "c4"
     if args.batch is None:
@@ -571,9 +572,9 @@ def main():
                 "config": {"workload": "ParkingModel train step (fwd + control/seg/depth losses + bwd "
                                        "+ Adam), " + ("6 cams x 512x512 (C4), " if hires else
                                                       "4 cams x 256x256, ") +
-                                       ("bf16 operands in the conv GEMMs (forward, data gradient, "
-                                        "weight gradient), fp32 accumulate and storage, fp32 "
-                                        "optimizer and all-reduce (C3)"
+                                       ("bf16 operands in the conv GEMMs and transformer linears "
+                                        "(forward, data gradient, weight gradient), fp32 "
+                                        "accumulate and storage, fp32 optimizer and all-reduce (C3)"
                                         if lowp else "fp32") + ", random init",
                            "global_batch": world * args.batch, "batch_per_gpu": args.batch,
                            "parallelism": f"dp{world}"},

@@ -183,32 +183,108 @@ __device__ __forceinline__ void dw_wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// stage input rows [iy0, iy0 + IR) of plane `src` (H x W) into this wave's LDS buffer
+// stage input rows [iy0, iy0 + IR) of plane `src` (H x W) into this wave's LDS buffer.  The
+// loads are branch-free buffer loads (rows outside the plane read 0 through an out-of-range
+// offset) issued before any is used: a guarded `if (row ok) v = load` made hipcc branch
+// around each load and wait for it, one round trip per float4 (1.2-3 TB/s, round 3).
+constexpr int DW_MAXV = 6;  // float4 per lane the unrolled staging covers (host-checked)
+// the input transform resolved for one channel (read once per wave, not per staged row)
+struct DwT {
+  float sc, sh;
+  int act;
+  bool on;
+};
+__device__ __forceinline__ DwT dw_t(DwIn tf, int c) {
+  const bool on = tf.sc != nullptr;
+  return DwT{on ? tf.sc[c] : 1.f, on ? tf.sh[c] : 0.f, tf.act, on};
+}
+// transform of one staged float4; `in` = inside the plane (padding stays zero).  The act
+// branches are wave-uniform; the padding test is a per-lane select, not a branch
+__device__ __forceinline__ float4 dw_tf4(float4 v, const DwT &t, bool in) {
+  if (!t.on) return v;
+  float z[4] = {v.x * t.sc + t.sh, v.y * t.sc + t.sh, v.z * t.sc + t.sh, v.w * t.sc + t.sh};
+  if (t.act == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[i] = z[i] / (1.f + expf(-z[i]));
+  } else if (t.act == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[i] = fmaxf(z[i], 0.f);
+  }
+  return make_float4(in ? z[0] : 0.f, in ? z[1] : 0.f, in ? z[2] : 0.f, in ? z[3] : 0.f);
+}
+// buffer descriptor of a wave-uniform plane: the base pointer and size go through
+// readfirstlane so the descriptor lives in SGPRs (a VGPR descriptor makes hipcc wrap every
+// buffer load in a waterfall loop)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_u(const float *p, long long bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes >= 0x7fffffff ? 0x7fffffff : bytes));
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(((unsigned long long)hi << 32) | lo), (short)0, nb, 0x00020000);
+}
 __device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, int W, int iy0,
                                          int IR, int WP, float *lds, int lane,
                                          DwIn tf = DwIn{nullptr, nullptr, 0}, int c = 0) {
   const int W4 = W >> 2;
-  const bool t = tf.sc != nullptr;
-  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
-  for (int e = lane; e < IR * W4; e += 64) {
+  const DwT t = dw_t(tf, c);
+  const __amdgpu_buffer_rsrc_t rs = rsrc_u(src, 4LL * H * W);
+  float4 v[DW_MAXV];
+  bool in[DW_MAXV];
+#pragma unroll
+  for (int i = 0; i < DW_MAXV; ++i) {
+    const int e = lane + 64 * i;
     const int r = e / W4, j = e - r * W4;
     const int iy = iy0 + r;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)iy < (unsigned)H) {
-      v = *reinterpret_cast<const float4 *>(src + (size_t)iy * W + 4 * j);
-      if (t) {
-        v.x = dw_in(v.x, sc, sh, tf.act);
-        v.y = dw_in(v.y, sc, sh, tf.act);
-        v.z = dw_in(v.z, sc, sh, tf.act);
-        v.w = dw_in(v.w, sc, sh, tf.act);
-      }
-    }
-    *reinterpret_cast<float4 *>(lds + r * WP + DW_PADL + 4 * j) = v;
+    in[i] = e < IR * W4 && (unsigned)iy < (unsigned)H;
+    v[i] = bload4(rs, in[i] ? (iy * W + 4 * j) * 4 : OOR);
+  }
+#pragma unroll
+  for (int i = 0; i < DW_MAXV; ++i) {
+    const int e = lane + 64 * i;
+    if (e >= IR * W4) break;
+    const int r = e / W4, j = e - r * W4;
+    // padding rows stay zero (the padding lives in the normalised space)
+    *reinterpret_cast<float4 *>(lds + r * WP + DW_PADL + 4 * j) = dw_tf4(v[i], t, in[i]);
   }
   // halo columns
   for (int e = lane; e < IR * 2 * DW_PADL; e += 64) {
     const int r = e / (2 * DW_PADL), j = e - r * (2 * DW_PADL);
     lds[r * WP + (j < DW_PADL ? j : W + j)] = 0.f;
+  }
+}
+
+// The same staging split in two for software pipelining: dw_fetch issues a unit's row loads
+// into registers (at most DW_MAXV float4 per lane), dw_put writes them (normalised) and the
+// halo zeros into LDS once they have landed.
+__device__ __forceinline__ void dw_fetch(const float *__restrict__ src, int H, int W, int iy0,
+                                         int IR, int lane, float4 (&r)[DW_MAXV], bool active) {
+  const int W4 = W >> 2;
+  const __amdgpu_buffer_rsrc_t rs = rsrc_u(src, 4LL * H * W);
+#pragma unroll
+  for (int i = 0; i < DW_MAXV; ++i) {
+    const int e = lane + 64 * i;
+    const int rr = e / W4, j = e - rr * W4;
+    const int iy = iy0 + rr;
+    const bool ok = active && e < IR * W4 && (unsigned)iy < (unsigned)H;
+    r[i] = bload4(rs, ok ? (iy * W + 4 * j) * 4 : OOR);  // branch-free (see dw_stage)
+  }
+}
+__device__ __forceinline__ void dw_put(const float4 (&r)[DW_MAXV], int H, int W, int iy0, int IR,
+                                       int WP, float *lds, int lane, const DwT &t) {
+  const int W4 = W >> 2;
+#pragma unroll
+  for (int i = 0; i < DW_MAXV; ++i) {
+    const int e = lane + 64 * i;
+    if (e >= IR * W4) break;
+    const int rr = e / W4, j = e - rr * W4;
+    // padding rows stay zero
+    *reinterpret_cast<float4 *>(lds + rr * WP + DW_PADL + 4 * j) =
+        dw_tf4(r[i], t, (unsigned)(iy0 + rr) < (unsigned)H);
+  }
+  for (int e = lane; e < IR * 2 * DW_PADL; e += 64) {
+    const int rr = e / (2 * DW_PADL), j = e - rr * (2 * DW_PADL);
+    lds[rr * WP + (j < DW_PADL ? j : W + j)] = 0.f;
   }
 }
 
@@ -218,7 +294,8 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
                                                       DwStrip d, int units, float *__restrict__ y,
                                                       DwIn tf) {
   extern __shared__ float dw_lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
   const int unit = blockIdx.x * 4 + wave;
   float *lds = dw_lds + wave * d.IR * d.WP;
   const bool active = unit < units;  // wave-uniform
@@ -266,7 +343,8 @@ __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restri
                                                            int units_per_plane, int units,
                                                            float *__restrict__ dx) {
   extern __shared__ float dw_lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
   const int unit = blockIdx.x * 4 + wave;
   float *lds = dw_lds + wave * GR * WPg;
   const bool active = unit < units;
@@ -312,7 +390,8 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
                                                         DwStrip d, int splits,
                                                         float *__restrict__ part, DwIn tf) {
   extern __shared__ float dw_lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
   const int c = blockIdx.x, sp = blockIdx.y;
   float *lds = dw_lds + wave * d.IR * d.WP;
   const int cunits = g.N * d.units_per_plane;  // units of this channel
@@ -324,22 +403,44 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
   float acc[K * K];
 #pragma unroll
   for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
-  // every wave runs the same number of rounds (barriers), idle slots stage nothing
+  // Software-pipelined over the wave's units (u0 + wave, u0 + wave + 4, ...): the next unit's
+  // input rows and gy row are loaded into registers before the current unit's FMAs, so the
+  // load latency overlaps compute (the wave used to stage, wait, compute, one unit at a time:
+  // 1.2-2.1 TB/s).  Up to DW_MAXV float4 per lane per unit (host-checked).
+  auto unit_of = [&](int un, int &n, int &oy0) {
+    n = un / d.units_per_plane;
+    oy0 = (un - n * d.units_per_plane) * d.RO;
+  };
+  float4 rx[DW_MAXV];
+  float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+  const __amdgpu_buffer_rsrc_t rgy = rsrc(gy, 4LL * g.N * g.C * g.P * g.Q);
+  int n = 0, oy0 = 0;
+  bool active = beg + wave < end;
+  if (active) unit_of(beg + wave, n, oy0);
+  auto fetch = [&](bool act, int nn, int yy0) {
+    dw_fetch(x + ((size_t)nn * g.C + c) * g.H * g.W, g.H, g.W, yy0 * ST - g.pt, d.IR, lane, rx, act);
+    const int oy = yy0 + ro;
+    const bool ok = act && ro < d.RO && oy < g.P;
+    gq = bload4(rgy, ok ? ((nn * g.C + c) * g.P + oy) * g.Q * 4 + ox0 * 4 : OOR);
+  };
+  const DwT tfc = dw_t(tf, c);  // the block's channel: read once
+  fetch(active, n, oy0);
   for (int u0 = beg; u0 < end; u0 += 4) {
-    const int un = u0 + wave;
-    const bool active = un < end;
-    int n = 0, oy0 = 0;
-    if (active) {
-      n = un / d.units_per_plane;
-      oy0 = (un - n * d.units_per_plane) * d.RO;
-      dw_stage(x + ((size_t)n * g.C + c) * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds,
-               lane, tf, c);
-    }
+    dw_put(rx, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane, tfc);
+    const float gv[4] = {gq.x, gq.y, gq.z, gq.w};
+    const bool cur_active = active;
+    const int cur_oy0 = oy0;
+    // next unit of this wave: its loads fly while this unit computes
+    const bool nxt = u0 + 4 + wave < end;
+    int nn = 0, noy0 = 0;
+    if (nxt) unit_of(u0 + 4 + wave, nn, noy0);
+    fetch(nxt, nn, noy0);
+    active = nxt;
+    n = nn;
+    oy0 = noy0;
     dw_wave_sync();
-    const int oy = oy0 + ro;
-    if (active && ro < d.RO && oy < g.P) {
-      const float4 gv4 = *reinterpret_cast<const float4 *>(gy + (((size_t)n * g.C + c) * g.P + oy) * g.Q + ox0);
-      const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
+    const int oy = cur_oy0 + ro;
+    if (cur_active && ro < d.RO && oy < g.P) {
       const float *base = lds + (ro * ST) * d.WP + DW_PADL + ox0 * ST - g.pl;
 #pragma unroll
       for (int a = 0; a < K; ++a) {
@@ -404,8 +505,11 @@ using namespace e2ep;
 extern "C" {
 
 static bool dw_strip_ok(const DwGeom &g) {
-  return g.Q % 4 == 0 && g.Q <= 256 && g.W % 4 == 0 && (g.K == 3 || g.K == 5) &&
-         (g.st == 1 || g.st == 2);
+  if (!(g.Q % 4 == 0 && g.Q <= 256 && g.W % 4 == 0 && (g.K == 3 || g.K == 5) &&
+        (g.st == 1 || g.st == 2)))
+    return false;
+  const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
+  return d.IR * (g.W / 4) <= 64 * DW_MAXV;  // the unrolled staging's reach
 }
 
 #define DW_STRIP_DISPATCH(KERNEL, FLIPARG, GRID, SHMEM, ...)                                    \
@@ -467,10 +571,12 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
       return launch_status("e2ep_dwconv_dgrad");
     }
   }
+  const int RO2 = g.W % 4 == 0 && g.W <= 256 ? 64 / (g.W / 4) : 0;
+  const int GR2 = ((RO2 - 1 + g.pt) >> 1) - ((g.pt - (g.K - 1)) >> 1) + 2;
   if (g.st == 2 && g.W % 4 == 0 && g.W <= 256 && g.Q % 4 == 0 && (g.K == 3 || g.K == 5) &&
-      g.pl <= 2 && g.pt <= 2) {
-    const int RO = 64 / (g.W / 4);
-    const int GR = ((RO - 1 + g.pt) >> 1) - ((g.pt - (g.K - 1)) >> 1) + 2;
+      g.pl <= 2 && g.pt <= 2 && GR2 * (g.Q / 4) <= 64 * DW_MAXV) {
+    const int RO = RO2;
+    const int GR = GR2;
     const int WPg = g.Q + 2 * DW_PADL;
     const int upp = (g.H + RO - 1) / RO, units = g.N * g.C * upp;
     const size_t shm = 4 * GR * WPg * sizeof(float);
@@ -491,8 +597,15 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
   return launch_status("e2ep_dwconv_dgrad");
 }
 
+// the pipelined weight-gradient strip kernel holds a unit's input rows in registers
+static bool dw_wgrad_strip_ok(const DwGeom &g) {
+  if (!dw_strip_ok(g)) return false;
+  const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
+  return d.IR * (g.W / 4) <= 64 * DW_MAXV;
+}
+
 static int dw_wgrad_splits(const DwGeom &g) {
-  if (dw_strip_ok(g)) {
+  if (dw_wgrad_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     const int cunits = g.N * d.units_per_plane;
     int want = (g_tune[TUNE_DW_WGRAD_TARGET] + g.C - 1) / g.C;  // e2ep_tune key 3 / 5
@@ -518,7 +631,7 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
                "e2ep_dwconv_wgrad: bad geometry");
   const int sp = dw_wgrad_splits(g);
   float *part = static_cast<float *>(workspace);
-  if (dw_strip_ok(g)) {
+  if (dw_wgrad_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     DW_STRIP_DISPATCH(k_dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
                       sp, part, tf);

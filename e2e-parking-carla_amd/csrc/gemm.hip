@@ -27,6 +27,7 @@
 namespace e2ep {
 
 typedef float g_f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 g_bf16x8 __attribute__((ext_vector_type(8)));
 
 typedef float g_f2 __attribute__((ext_vector_type(2)));
 __device__ g_f2 e2ep_raw_buffer_load_v2f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
@@ -46,7 +47,10 @@ __device__ __forceinline__ float kmask(float v, bool ok) {
 constexpr int G_BK = 32;
 constexpr int G_LDW = 36;  // LDS row stride in floats (32 k + 4 pad)
 
-template <bool AK, bool BKC, int WM, int TM, int TN, int AVEC, int BVEC>
+// OP: MFMA operand precision, 0 = fp32 (v_mfma_f32_32x32x2_f32, exact), 1 = bf16 (BASELINE
+// C3: the fragments are rounded to bf16 when read from LDS, two v_mfma_f32_32x32x16_bf16 per
+// 32-deep step, products and sums fp32; HBM tensors stay fp32)
+template <bool AK, bool BKC, int WM, int TM, int TN, int AVEC, int BVEC, int OP = 0>
 __global__ void __launch_bounds__(256)
     k_gemm(const float *__restrict__ A, int lda, long long a_bytes,
            const float *__restrict__ B, int ldb, long long b_bytes,
@@ -192,13 +196,34 @@ __global__ void __launch_bounds__(256)
         b[t][4 * q] = x.x; b[t][4 * q + 1] = x.y; b[t][4 * q + 2] = x.z; b[t][4 * q + 3] = x.w;
       }
     }
+    if (OP == 0) {
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk)
+      for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
-      for (int u = 0; u < TM; ++u)
+        for (int u = 0; u < TM; ++u)
 #pragma unroll
-        for (int t = 0; t < TN; ++t)
-          acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][kk], b[t][kk], acc[u][t], 0, 0, 0);
+          for (int t = 0; t < TN; ++t)
+            acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][kk], b[t][kk], acc[u][t], 0, 0, 0);
+    } else {
+      // lane half h supplies k = 16h + 8 blk + j to MFMA blk (element j): one consistent
+      // permutation of the step's 32 k for both operands
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+        g_bf16x8 ab[TM], bb[TN];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int u = 0; u < TM; ++u) ab[u][j] = (__bf16)a[u][8 * blk + j];
+#pragma unroll
+          for (int t = 0; t < TN; ++t) bb[t][j] = (__bf16)b[t][8 * blk + j];
+        }
+#pragma unroll
+        for (int u = 0; u < TM; ++u)
+#pragma unroll
+          for (int t = 0; t < TN; ++t)
+            acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab[u], bb[t], acc[u][t], 0, 0, 0);
+      }
+    }
   };
   if (nk > 0) {
     load_tiles(ra, rb, kbeg);
@@ -411,6 +436,8 @@ static int g_split_min_small = 8;
 // predict fp16 4.84 -> 4.28 ms p50; the C2 step's 112-row decoder measured slower on it (25.66
 // vs 25.39 ms/step, profiles/r02/session6/skinny_ab.txt), so it stays on the MFMA tiles.
 static int g_skinny_rows = 16;
+// operand precision of k_gemm (e2ep_gemm_precision): 0 fp32, 1 bf16 (C3)
+static int g_gemm_precision = 0;
 
 static GemmLaunch gemm_plan(int M, int N, int K) {
   GemmLaunch p{1, 1, 1};
@@ -474,7 +501,8 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
     return 0;
   }
   const int Nx = rs ? N + 1 : N;  // logical columns including the ones column
-  const GemmLaunch p = gemm_plan(M, Nx, K);
+  GemmLaunch p = gemm_plan(M, Nx, K);
+  if (g_gemm_precision == 1 && p.tile != 1 && p.tile != 2) p.tile = 1;  // bf16: tiles 1 / 2 only
   if (p.splits > 1 && !workspace) {
     set_error("gemm: workspace of e2ep_gemm_workspace() bytes required");
     return E2EP_EINVAL;
@@ -490,6 +518,17 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
                      N, K, p.kper, relu, rs)
 #define E2EP_GEMM_T(AKV, BKV, AVV, BVV)                                     \
   do {                                                                      \
+    if (g_gemm_precision == 1) { /* bf16: the automatic tiles */            \
+      if (p.tile == 2)                                                      \
+        hipLaunchKernelGGL((k_gemm<AKV, BKV, 1, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, A, \
+                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, out, c_bytes, \
+                           ldc, cols, M, N, K, p.kper, relu, rs);           \
+      else                                                                  \
+        hipLaunchKernelGGL((k_gemm<AKV, BKV, 2, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, A, \
+                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, out, c_bytes, \
+                           ldc, cols, M, N, K, p.kper, relu, rs);           \
+      break;                                                                \
+    }                                                                       \
     switch (p.tile) {                                                       \
       case 2: E2EP_GEMM_LAUNCH(AKV, BKV, 1, 1, 1, AVV, BVV); break;          \
       case 3: E2EP_GEMM_LAUNCH(AKV, BKV, 2, 2, 2, AVV, BVV); break;          \
@@ -558,6 +597,12 @@ size_t e2ep_gemm_workspace(int M, int N, int K) { return gemm_ws(M, N, K); }
 int e2ep_gemm_split_min(int ksteps) {
   const int prev = g_split_min_small;
   if (ksteps > 0) g_split_min_small = ksteps;
+  return prev;
+}
+
+int e2ep_gemm_precision(int precision) {
+  const int prev = g_gemm_precision;
+  if (precision == 0 || precision == 1) g_gemm_precision = precision;
   return prev;
 }
 

@@ -39,6 +39,7 @@ SIGNATURES = {
     "e2ep_conv_gemm_variant": (_i, [_i]),
     "e2ep_conv_split_params": (_i, [_i, _i, _i]),
     "e2ep_conv_precision": (_i, [_i]),
+    "e2ep_gemm_precision": (_i, [_i]),
     "e2ep_conv_wgrad_kstep": (_i, [_i]),
     "e2ep_conv_wgrad_splits": (_i, [_p]),
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),

@@ -491,6 +491,11 @@ int e2ep_gemm_force(int tile, int splits, int unused);
  * decoder's 14 rows at B = 1, C5 predict); 0 disables it, < 0 only queries.  Returns the
  * previous limit. */
 int e2ep_gemm_skinny(int max_rows);
+/* Operand precision of e2ep_gemm / e2ep_gemm_rowsum: 0 = fp32 (default, exact-f32 MFMA), 1 =
+ * bf16 operands rounded as they enter the matrix cores (v_mfma_f32_32x32x16_bf16), fp32
+ * products, sums and tensors (BASELINE C3); < 0 only queries.  Returns the previous value.
+ * The few-row path (e2ep_gemm_skinny) stays fp32. */
+int e2ep_gemm_precision(int precision);
 /* Minimum K-steps (32 deep) per K split for grids under 64 blocks (default 8); <= 0 queries.
  * Returns the previous value. */
 int e2ep_gemm_split_min(int ksteps);

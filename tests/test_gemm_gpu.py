@@ -196,3 +196,25 @@ def test_linear_bias_gradient_from_rowsum_launch():
     bd.grad = None
     nn_ops.linear(xd.detach(), wf, bd).backward(dy.to(DEV))
     assert rel_l2(bd.grad, b64.grad) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 774, 258), (258, 2048, 2048), (112, 516, 258),
+                                   (65, 130, 17), (2048, 258, 2048)])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False)])
+def test_gemm_bf16_operands_vs_rounded_fp64(M, N, K, ak, bk):
+    """C3 (e2ep_gemm_precision 1): bf16 operands, fp32 products and sums — against fp64 of the
+    bf16-rounded operands (rel-L2 2e-6: only the fp32 accumulation differs), and the rounding
+    really happens (the unrounded fp64 product is ~1e-3 away)."""
+    from e2ep_amd import nn_ops, precision
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K + ak + 2 * bk)
+    A, B, ref = _operands(M, N, K, ak, bk, g)
+    Ar, Br = A.bfloat16().double(), B.bfloat16().double()
+    want = (Ar if ak else Ar.t()) @ (Br.t() if bk else Br)
+    with precision.use("bf16"):
+        out = nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K)
+        again = nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K)
+    assert rel_l2(out, want) < 2e-6
+    assert torch.equal(out, again)
+    if K >= 64:
+        assert rel_l2(out, ref) > 1e-4
+    assert rel_l2(nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K), ref) < 2e-6  # fp32 again
