@@ -268,7 +268,63 @@ struct BnBwdElem {
     dz = dyv * act_bwd(dc_scale(dc_rand, keep, n, zb) + rv, act);
     dzb = dc_rand ? __fdiv_rn(__fmul_rn(dz, floorf(__fadd_rn(keep, dc_rand[n]))), keep) : dz;
   }
+  // the same with the sample's drop-connect factor floor(keep + u[n]) loaded beforehand
+  __device__ __forceinline__ void with_factor(float xv, float dyv, float rv, float dcf, float &xh,
+                                              float &dz, float &dzb) const {
+    xh = (xv - mu) * is;
+    const float zb = xh * g + b;
+    const float zs = dc_rand ? __fmul_rn(__fdiv_rn(zb, keep), dcf) : zb;
+    dz = dyv * act_bwd(zs + rv, act);
+    dzb = dc_rand ? __fdiv_rn(__fmul_rn(dz, dcf), keep) : dz;
+  }
 };
+
+// per-vector sample factors of the single-launch kernels, loaded before the channel data:
+// a per-element `dc_rand[n]` / gate read inside the element loop made hipcc wait vmcnt(0)
+// (the counters are in order) behind every x / dy load, one round trip per vector (the
+// single-launch backward ran at 1.7 TB/s, round 3)
+template <int T, int R>
+__device__ __forceinline__ void bns_factors(int tot, int HWv, int C, int c, const float *dc_rand,
+                                            float keep, const BnGate *gt, float (&dcf)[R],
+                                            float (&gs)[R], float (&gd)[R]) {
+  int n[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    n[u] = min((int)threadIdx.x + u * T, tot - 1) / HWv;
+    dcf[u] = 1.f;
+    gs[u] = 1.f;
+    gd[u] = 0.f;
+  }
+  // raw loads only (uniform branches); bns_factors_finish does the arithmetic once the
+  // caller has issued its channel loads too, so every load of the block is in flight at once
+  if (dc_rand) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) dcf[u] = dc_rand[n[u]];
+  }
+  if (gt && gt->on()) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      gs[u] = gt->logit[n[u] * C + c];
+      gd[u] = gt->dpooled[n[u] * C + c];
+    }
+  }
+}
+template <int R>
+__device__ __forceinline__ void bns_factors_finish(const float *dc_rand, float keep,
+                                                   const BnGate *gt, float (&dcf)[R],
+                                                   float (&gs)[R], float (&gd)[R]) {
+  if (dc_rand) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) dcf[u] = floorf(__fadd_rn(keep, dcf[u]));
+  }
+  if (gt && gt->on()) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      gs[u] = 1.f / (1.f + expf(-gs[u]));  // = BnGate::coef
+      gd[u] = gd[u] * gt->inv_hw;
+    }
+  }
+}
 
 // backward reduction: per channel sums of dzb and dzb * xhat (fp64); grid (C, splits)
 template <int VEC>
@@ -416,6 +472,8 @@ __global__ void __launch_bounds__(T) k_bn_fwd_small(
     const float *__restrict__ res, const float *__restrict__ dc_rand, float dc_keep, int N, int C,
     int HWv, int act, float *__restrict__ y, float *__restrict__ scale, float *__restrict__ shift) {
   const int c = blockIdx.x, tot = N * HWv;
+  float dcf[R], gs[R], gd[R];
+  if (y) bns_factors<T, R>(tot, HWv, C, c, dc_rand, dc_keep, nullptr, dcf, gs, gd);
   float4 v[R];
 #pragma unroll
   for (int u = 0; u < R; ++u) v[u] = Vec<4>::ld(x + bns_off(min((int)threadIdx.x + u * T, tot - 1), HWv, C, c));
@@ -451,17 +509,22 @@ __global__ void __launch_bounds__(T) k_bn_fwd_small(
     }
   }
   if (!y) return;
+  float4 rr[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u)
+    rr[u] = res ? Vec<4>::ld(res + bns_off(min((int)threadIdx.x + u * T, tot - 1), HWv, C, c))
+                : Vec<4>::zero();
+  bns_factors_finish<R>(dc_rand, dc_keep, nullptr, dcf, gs, gd);
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const int t = threadIdx.x + u * T;
     if (t >= tot) break;
-    const int n = t / HWv;
     const size_t off = bns_off(t, HWv, C, c);
-    const float4 r = res ? Vec<4>::ld(res + off) : Vec<4>::zero();
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float z = dc_scale(dc_rand, dc_keep, n, Vec<4>::get(v[u], i) * sc + sh);
-      Vec<4>::set(v[u], i, act_fwd(z + Vec<4>::get(r, i), act));
+      const float zb = Vec<4>::get(v[u], i) * sc + sh;
+      const float z = dc_rand ? __fmul_rn(__fdiv_rn(zb, dc_keep), dcf[u]) : zb;  // = dc_scale
+      Vec<4>::set(v[u], i, act_fwd(z + Vec<4>::get(rr[u], i), act));
     }
     Vec<4>::st(y + off, v[u]);
   }
@@ -478,25 +541,29 @@ __global__ void __launch_bounds__(T) k_bn_bwd_small(
   const int c = blockIdx.x, tot = N * HWv;
   const BnBwdElem<4> el{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f,
                         dc_rand, dc_keep, act};
-  float4 xv[R], dv[R];
+  float dcf[R], gs[R], gd[R];
+  bns_factors<T, R>(tot, HWv, C, c, dc_rand, dc_keep, &gt, dcf, gs, gd);
+  float4 xv[R], dv[R], rv[R];
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const size_t off = bns_off(min((int)threadIdx.x + u * T, tot - 1), HWv, C, c);
     xv[u] = Vec<4>::ld(x + off);
     dv[u] = Vec<4>::ld(dy + off);
+    rv[u] = res ? Vec<4>::ld(res + off) : Vec<4>::zero();
   }
+  bns_factors_finish<R>(dc_rand, dc_keep, &gt, dcf, gs, gd);
   double s = 0.0, q = 0.0;
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const int t = threadIdx.x + u * T;
     if (t >= tot) break;
-    const int n = t / HWv;
-    dv[u] = gate_dy<4>(dv[u], gt, n, C, c);
-    const float4 rv = res ? Vec<4>::ld(res + bns_off(t, HWv, C, c)) : Vec<4>::zero();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Vec<4>::set(dv[u], i, Vec<4>::get(dv[u], i) * gs[u] + gd[u]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float xh, dz, dzb;
-      el(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i), Vec<4>::get(rv, i), n, xh, dz, dzb);
+      el.with_factor(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i), Vec<4>::get(rv[u], i), dcf[u],
+                     xh, dz, dzb);
       s += dzb;
       q += (double)dzb * xh;
     }
@@ -513,14 +580,13 @@ __global__ void __launch_bounds__(T) k_bn_bwd_small(
   for (int u = 0; u < R; ++u) {
     const int t = threadIdx.x + u * T;
     if (t >= tot) break;
-    const int n = t / HWv;
     const size_t off = bns_off(t, HWv, C, c);
-    const float4 rv = res ? Vec<4>::ld(res + off) : Vec<4>::zero();
     float4 ox, orr;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float xh, dz, dzb;
-      el(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i), Vec<4>::get(rv, i), n, xh, dz, dzb);
+      el.with_factor(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i), Vec<4>::get(rv[u], i), dcf[u],
+                     xh, dz, dzb);
       Vec<4>::set(orr, i, dz);
       Vec<4>::set(ox, i, gis * (train ? dzb - (ms + xh * mq) : dzb));
     }

@@ -40,6 +40,10 @@ SIGNATURES = {
     "e2ep_conv_split_params": (_i, [_i, _i, _i]),
     "e2ep_conv_precision": (_i, [_i]),
     "e2ep_gemm_precision": (_i, [_i]),
+    "e2ep_fusion_tokens_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _f, _p, _p, _p]),
+    "e2ep_fusion_tokens_bwd": (_i, [_p, _i, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
+    "e2ep_embed_tokens_fwd": (_i, [_p, _i, _p, _i, _p, _i, _i, _i, _f, _p, _p, _p]),
+    "e2ep_embed_tokens_bwd": (_i, [_p, _p, _i, _i, _i, _i, _i, _f, _p, _p, _p, _p]),
     "e2ep_conv_wgrad_kstep": (_i, [_i]),
     "e2ep_conv_wgrad_splits": (_i, [_p]),
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),

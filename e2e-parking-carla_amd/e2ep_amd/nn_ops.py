@@ -744,6 +744,81 @@ def relu_dropout(x, p=0.0, seed=None):
 
 
 # ------------------------------------------------------------------------------------------
+# transformer token assembly + positional embedding + pos_drop (csrc/tokens.hip)
+# ------------------------------------------------------------------------------------------
+class _FusionTokens(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, bev, motion, pos, p, seed):
+        B, C, S = bev.shape
+        E = pos.shape[-1]
+        out = torch.empty((B, S, E), dtype=torch.float32, device=bev.device)
+        _lib.call("e2ep_fusion_tokens_fwd", _lib.ptr(bev), _lib.ptr(motion), _lib.ptr(pos), B, C, S,
+                  E, float(p), _lib.ptr(seed), _lib.ptr(out), _lib.stream())
+        ctx.save_for_backward(seed)
+        ctx.meta = (B, C, S, E, float(p), tuple(motion.shape))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (seed,) = ctx.saved_tensors
+        B, C, S, E, p, mshape = ctx.meta
+        g = g.contiguous()
+        dbev = torch.empty((B, C, S), dtype=torch.float32, device=g.device)
+        dmotion = torch.empty(mshape, dtype=torch.float32, device=g.device)
+        dpos = torch.empty((1, S, E), dtype=torch.float32, device=g.device)
+        _lib.call("e2ep_fusion_tokens_bwd", _lib.ptr(g), B, C, S, E, p, _lib.ptr(seed),
+                  _lib.ptr(dbev), _lib.ptr(dmotion), _lib.ptr(dpos), _lib.stream())
+        return dbev, dmotion, dpos, None, None
+
+
+def fusion_tokens(bev, motion, pos, p=0.0, seed=None):
+    """drop(cat([bev.transpose(1, 2), motion.transpose(1, 2).expand(-1, -1, E - C)], 2) + pos)
+    in one launch each way (reference model/feature_fusion.py:41-46): bev (B, C, S), motion
+    (B, 1, S), pos (1, S, E) fp32 HIP tensors."""
+    _dev(bev, motion, pos)
+    bev, motion, pos = bev.contiguous(), motion.contiguous(), pos.contiguous()
+    if p > 0.0 and seed is None:
+        seed = rng.seed(bev.device)
+    return _FusionTokens.apply(bev, motion, pos, float(p), seed)
+
+
+class _EmbedTokens(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tok, table, pos, p, seed):
+        B, T = tok.shape
+        V, E = table.shape
+        out = torch.empty((B, T, E), dtype=torch.float32, device=table.device)
+        _lib.call("e2ep_embed_tokens_fwd", _lib.ptr(tok), tok.stride(0), _lib.ptr(table), V,
+                  _lib.ptr(pos), B, T, E, float(p), _lib.ptr(seed), _lib.ptr(out), _lib.stream())
+        ctx.save_for_backward(tok, seed)
+        ctx.meta = (B, T, V, E, float(p))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        tok, seed = ctx.saved_tensors
+        B, T, V, E, p = ctx.meta
+        g = g.contiguous()
+        dtable = torch.empty((V, E), dtype=torch.float32, device=g.device)
+        dpos = torch.empty((1, T, E), dtype=torch.float32, device=g.device)
+        _lib.call("e2ep_embed_tokens_bwd", _lib.ptr(g), _lib.ptr(tok), tok.stride(0), V, B, T, E, p,
+                  _lib.ptr(seed), _lib.ptr(dtable), _lib.ptr(dpos), _lib.stream())
+        return None, dtable, dpos, None, None
+
+
+def embed_tokens(tok, table, pos, p=0.0, seed=None):
+    """drop(embedding(tok) + pos) in one launch each way (reference model/control_predict.py:
+    53-54): tok (B, T) int64 (row stride free, unit column stride), table (V, E), pos (1, T, E)."""
+    _dev(table, pos)
+    if tok.dtype != torch.int64 or tok.dim() != 2 or tok.stride(1) != 1 or tok.device != table.device:
+        raise _lib.E2EPError("embed_tokens: tok must be a (B, T) int64 device tensor with unit column stride")
+    pos = pos.contiguous()
+    if p > 0.0 and seed is None:
+        seed = rng.seed(table.device)
+    return _EmbedTokens.apply(tok, table, pos, float(p), seed)
+
+
+# ------------------------------------------------------------------------------------------
 # softmax over channels (depth distribution)
 # ------------------------------------------------------------------------------------------
 class _SoftmaxC(torch.autograd.Function):

@@ -45,7 +45,9 @@ class ControlPredict(nn.Module):
     def forward(self, encoder_out, tgt):
         tgt = tgt[:, :-1]
         mask, pad = self.create_mask(tgt)
-        emb = self.pos_drop(self.embedding(tgt) + self.pos_embed)
+        # embedding + pos_embed -> pos_drop as one kernel each way
+        p = self.pos_drop.p if self.training else 0.0
+        emb = nn_ops.embed_tokens(tgt, self.embedding.weight, self.pos_embed, p)
         return self.project(self.decoder(encoder_out, emb, mask, pad))
 
     def project(self, x):
@@ -58,6 +60,6 @@ class ControlPredict(nn.Module):
                          dtype=torch.long, device=tgt.device)
         tgt = torch.cat([tgt, pad], dim=1)
         mask, padm = self.create_mask(tgt)
-        emb = self.embedding(tgt) + self.pos_embed
+        emb = nn_ops.embed_tokens(tgt, self.embedding.weight, self.pos_embed)
         logits = self.project(self.decoder(encoder_out, emb, mask, padm))[:, length - 1, :]
         return torch.softmax(logits, dim=-1).argmax(dim=-1).view(-1, 1)

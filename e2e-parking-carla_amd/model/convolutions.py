@@ -4,7 +4,7 @@ DeepLabHead — the only reachable classes of that file).  Forwards run on e2ep_
 import torch
 from torch import nn
 
-from e2ep_amd import ops
+from e2ep_amd import nn_ops, ops
 
 
 def _conv_bn(cin, cout, k, pad=0, dil=1):
@@ -47,7 +47,13 @@ class ASPP(nn.Module):
     def forward(self, x):
         branches = [_run_conv_bn_relu(self.convs[0], x)] + [m(x) for m in self.convs[1:]]
         y = _run_conv_bn_relu(self.project, torch.cat(branches, 1))
-        return self.project[3](y)
+        # Dropout(0.5) after the project BN-ReLU (reference model/convolutions.py:264): y >= 0,
+        # so dropout(y) = dropout(relu(y)) runs on the fused ReLU-dropout kernel, one launch
+        # each way (its backward's relu mask only drops entries whose BN-ReLU gradient is 0)
+        p = self.project[3].p if self.training else 0.0
+        if p > 0.0:
+            y = nn_ops.relu_dropout(y, p)
+        return y
 
 
 class DeepLabHead(nn.Sequential):

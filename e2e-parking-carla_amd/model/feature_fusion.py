@@ -40,7 +40,9 @@ class FeatureFusion(nn.Module):
         return x
 
     def forward(self, bev_feature, ego_motion):
-        motion = self.encode_motion(ego_motion).transpose(1, 2).expand(-1, -1, 2)
-        tokens = torch.cat([bev_feature.transpose(1, 2), motion], dim=2)
-        tokens = self.pos_drop(tokens + self.pos_embed)
+        # cat([bev^T, motion^T expanded]) + pos_embed -> pos_drop as one kernel each way
+        # (reference model/feature_fusion.py:41-46)
+        motion = self.encode_motion(ego_motion)  # (B, 1, S)
+        p = self.pos_drop.p if self.training else 0.0
+        tokens = nn_ops.fusion_tokens(bev_feature, motion, self.pos_embed, p)
         return transformer.encoder(self.tf_encoder, tokens)

@@ -403,6 +403,33 @@ int e2ep_se_gate_bwd(const float *x, const float *a, const float *dy, int planes
                      float *dx, float *da, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Transformer token assembly with the positional embedding and pos_drop, fwd and bwd
+ * (dropout: keep bit = counter hash of the device seed and the output element index, scale
+ * 1 / (1 - p); p = 0 is the identity and needs no seed):
+ *  - fusion encoder (replaces model/feature_fusion.py:41-46: transpose, expand, torch.cat,
+ *    + pos_embed, pos_drop): tokens [B][S][E] = drop(x + pos[S][E]) with x = bev[b][e][s]
+ *    (bev [B][C][S], the BEV encoder output) for e < C and motion[b][s] (motion [B][S]) for
+ *    C <= e < E.  bwd: dbev [B][C][S], dmotion [B][S] (sum over the E - C broadcast channels,
+ *    which must lie in one 32-channel tile), dpos [S][E] (sum over b in order).
+ *  - control decoder (replaces model/control_predict.py:53-54: embedding + pos_embed +
+ *    pos_drop): out [B][T][E] = drop(table[tok[b*tok_stride + t]] + pos[T][E]) (int64 tokens,
+ *    clamped into [0, V)); bwd: dtable [V][E] (every row written: sum over the (b, t) whose
+ *    token is v, in (b, t) order), dpos [T][E] (sum over b in order).  No atomics.
+ * ------------------------------------------------------------------------------------- */
+int e2ep_fusion_tokens_fwd(const float *bev, const float *motion, const float *pos, int B, int C,
+                           int S, int E, float p, const int32_t *seed, float *tokens,
+                           void *stream);
+int e2ep_fusion_tokens_bwd(const float *dtokens, int B, int C, int S, int E, float p,
+                           const int32_t *seed, float *dbev, float *dmotion, float *dpos,
+                           void *stream);
+int e2ep_embed_tokens_fwd(const int64_t *tok, int tok_stride, const float *table, int V,
+                          const float *pos, int B, int T, int E, float p, const int32_t *seed,
+                          float *out, void *stream);
+int e2ep_embed_tokens_bwd(const float *dout, const int64_t *tok, int tok_stride, int V, int B,
+                          int T, int E, float p, const int32_t *seed, float *dtable, float *dpos,
+                          void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Optimizer: fused Adam over one flat parameter buffer (replaces torch.optim.Adam configured
  * at trainer/pl_trainer.py:116-121; torch Adam semantics: L2 weight decay added to the
  * gradient, bias-corrected step, no amsgrad).
