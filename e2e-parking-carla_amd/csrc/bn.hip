@@ -552,20 +552,21 @@ __global__ void __launch_bounds__(T) k_bn_bwd_small(
     rv[u] = res ? Vec<4>::ld(res + off) : Vec<4>::zero();
   }
   bns_factors_finish<R>(dc_rand, dc_keep, &gt, dcf, gs, gd);
+  // one pass of the element math (act derivative: an exp and a divide for swish) whose results
+  // stay in registers for the apply below (the block holds one channel: registers are free)
+  float xh[R][4], dz[R][4], dzb[R][4];
   double s = 0.0, q = 0.0;
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const int t = threadIdx.x + u * T;
-    if (t >= tot) break;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Vec<4>::set(dv[u], i, Vec<4>::get(dv[u], i) * gs[u] + gd[u]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float xh, dz, dzb;
-      el.with_factor(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i), Vec<4>::get(rv[u], i), dcf[u],
-                     xh, dz, dzb);
-      s += dzb;
-      q += (double)dzb * xh;
+      el.with_factor(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i) * gs[u] + gd[u],
+                     Vec<4>::get(rv[u], i), dcf[u], xh[u][i], dz[u][i], dzb[u][i]);
+      if (t < tot) {
+        s += dzb[u][i];
+        q += (double)dzb[u][i] * xh[u][i];
+      }
     }
   }
   block_sum2_t<T>(s, q);
@@ -584,11 +585,8 @@ __global__ void __launch_bounds__(T) k_bn_bwd_small(
     float4 ox, orr;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float xh, dz, dzb;
-      el.with_factor(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i), Vec<4>::get(rv[u], i), dcf[u],
-                     xh, dz, dzb);
-      Vec<4>::set(orr, i, dz);
-      Vec<4>::set(ox, i, gis * (train ? dzb - (ms + xh * mq) : dzb));
+      Vec<4>::set(orr, i, dz[u][i]);
+      Vec<4>::set(ox, i, gis * (train ? dzb[u][i] - (ms + xh[u][i] * mq) : dzb[u][i]));
     }
     if (dres) Vec<4>::st(dres + off, orr);
     if (dx) Vec<4>::st(dx + off, ox);

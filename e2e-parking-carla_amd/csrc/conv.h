@@ -1,0 +1,57 @@
+// Internal interface shared by the convolution kernel files (conv.hip, conv_lp.hip).
+#pragma once
+#include "common.h"
+
+namespace e2ep {
+
+constexpr int MAXTAPS = 64;  // live filter taps per phase (R * S <= 64)
+
+struct ConvGeom {
+  int N;            // images
+  int Cin, H, W;    // input
+  int Cout, R, S;   // filter
+  int P, Q;         // output spatial
+  int sh, sw, ph, pw, dh, dw;
+  int wlayout;      // 0: [Cout][Cin][R*S] (PyTorch), 1: [R*S][Cout][Cin] (tap-major)
+};
+
+__host__ __device__ __forceinline__ int floordiv(int a, int b) {
+  return a >= 0 ? a / b : -((-a + b - 1) / b);
+}
+
+// Tap liveness: does any output position o in [0, n_out) read an input o*step + d inside
+// [0, n_in)?  A filter tap that never does only multiplies zero padding (the DeepLab ASPP
+// branches at dilation 24 / 36 on 16x16 maps, reference model/convolutions.py:218-225: 8 of
+// their 9 taps), so the GEMMs skip it: the sums are unchanged (those products are exact
+// zeros) and the weight gradient of such a tap is exactly 0.
+__host__ __device__ __forceinline__ bool axis_live(int d, int n_out, int step, int n_in) {
+  if (n_out <= 0) return false;
+  const int o0 = d >= 0 ? 0 : (-d + step - 1) / step;
+  return o0 < n_out && o0 * step + d < n_in;
+}
+
+// live filter taps (axis_live on both axes): the weight-gradient GEMMs run over the columns
+// (ci, live tap) only; the dead taps' gradient is written as 0 by the split reduction
+struct TapList {
+  int n;
+  unsigned long long mask;  // bit tap = live (R*S <= MAXTAPS = 64)
+  int tap[MAXTAPS];
+};
+
+// Low-precision (bf16 / fp16 operand) implicit-GEMM forward (mode 0) / data gradient (mode 1),
+// conv_lp.hip.  lp_workspace() bytes of split-K workspace (0: none); lp_launch() returns an
+// E2EP status.  Tap-major weights ([R*S][Cout][Cin]) or 1x1 filters only.
+bool lp_ok(int mode, const ConvGeom &g, int M);
+size_t lp_workspace(int mode, const ConvGeom &g, int M);
+int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
+              float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
+              hipStream_t s);
+
+// bf16 weight gradient (C3), conv_lp.hip: partial slabs part[split][Cout][Cin*R*S] for the
+// fixed-order split reduction of conv.hip; lp_wgrad_launch returns the slabs written.
+bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl);
+int lp_wgrad_splits(const ConvGeom &g, const TapList &tl);
+int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
+                    int splits, float *part, hipStream_t s);
+
+}  // namespace e2ep

@@ -26,6 +26,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "conv.h"
 #include "gemm.h"
 
 namespace e2ep {
@@ -37,30 +38,6 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr int BM = 64, BK = 16;
 constexpr int PADA = 4, PADB = 4;
 constexpr int MAXPH = 4;
-constexpr int MAXTAPS = 64;
-
-struct ConvGeom {
-  int N;            // images
-  int Cin, H, W;    // input
-  int Cout, R, S;   // filter
-  int P, Q;         // output spatial
-  int sh, sw, ph, pw, dh, dw;
-  int wlayout;      // 0: [Cout][Cin][R*S] (PyTorch), 1: [R*S][Cout][Cin] (tap-major)
-};
-
-__device__ __forceinline__ int floordiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
-
-// Tap liveness: does any output position o in [0, n_out) read an input o*step + d inside
-// [0, n_in)?  A filter tap that never does only multiplies zero padding (the DeepLab ASPP
-// branches at dilation 24 / 36 on 16x16 maps, reference model/convolutions.py:218-225: 8 of
-// their 9 taps), so the GEMMs skip it: the sums are unchanged (those products are exact
-// zeros) and the weight gradient of such a tap is exactly 0.
-__host__ __device__ __forceinline__ bool axis_live(int d, int n_out, int step, int n_in) {
-  if (n_out <= 0) return false;
-  const int o0 = d >= 0 ? 0 : (-d + step - 1) / step;
-  return o0 < n_out && o0 * step + d < n_in;
-}
-
 // ------------------------------------------------------------------------------------------
 // forward (MODE 0) / data-gradient (MODE 1) implicit GEMM
 // ------------------------------------------------------------------------------------------
@@ -676,14 +653,6 @@ __global__ void __launch_bounds__(256) k_conv_gemm2(
 // reduced in fixed order.
 // ------------------------------------------------------------------------------------------
 constexpr int WBN = 64;
-
-// live filter taps (axis_live on both axes): the weight-gradient GEMM runs over the columns
-// (ci, live tap) only; the dead taps' gradient is written as 0 by k_reduce_splits
-struct TapList {
-  int n;
-  unsigned long long mask;  // bit tap = live (R*S <= MAXTAPS = 64)
-  int tap[MAXTAPS];
-};
 
 template <int OP, int KB>
 __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
@@ -1413,7 +1382,6 @@ static bool geom_ok(const ConvGeom &g) {
          4LL * g.N * g.Cin * g.H * g.W < (1LL << 31) && 4LL * g.N * g.Cout * g.P * g.Q < (1LL << 31);
 }
 
-static int floordiv_h(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
 // live taps of one axis (the kernels' tap tables apply the same rules): forward, or data-
 // gradient phase p (stride-phase split, cols = the phase's column count)
@@ -1426,7 +1394,7 @@ static int live_taps_axis(int mode, int p, int pad, int K, int dil, int st, int 
     } else {
       const int v = p + pad - r * dil;
       if (((v % st) + st) % st) continue;
-      n += axis_live(floordiv_h(v, st), cols, 1, n_out);
+      n += axis_live(floordiv(v, st), cols, 1, n_out);
     }
   }
   return n;
@@ -1621,6 +1589,8 @@ static int conv1x1_gemm(int mode, int act, const float *w, const float *src, con
 static int launch_gemm(int mode, int act, const float *w, const float *src, const float *bias,
                        float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
                        hipStream_t s) {
+  if (g_conv_precision != 0 && lp_ok(mode, g, M))  // bf16 / fp16 operands: conv_lp.hip
+    return lp_launch(mode, act, g_conv_precision, w, src, bias, dst, dst_bytes, g, M, workspace, s);
   if (conv1x1_gemm_ok(mode, g))
     return conv1x1_gemm(mode, act, w, src, bias, dst, dst_bytes, g, M, workspace, s);
   {
@@ -1709,12 +1679,22 @@ extern "C" {
 size_t e2ep_conv_fwd_workspace(const int *dims) {
   ConvGeom g = make_geom(dims);
   if (direct_ok(g)) return 0;
+  if (g_conv_precision != 0) {  // the launch's w_layout is not known here: cover both paths
+    g.wlayout = 1;
+    if (lp_ok(0, g, g.Cout))
+      return std::max(lp_workspace(0, g, g.Cout), gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout));
+  }
   if (conv1x1_gemm_ok(0, g)) return conv1x1_ws(0, g, g.Cout);
   return gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout);
 }
 
 size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
   ConvGeom g = make_geom(dims);
+  if (g_conv_precision != 0) {
+    g.wlayout = 1;
+    if (lp_ok(1, g, m_channels))
+      return std::max(lp_workspace(1, g, m_channels), gemm_workspace(plan_gemm(1, g, m_channels), m_channels));
+  }
   if (conv1x1_gemm_ok(1, g)) return conv1x1_ws(1, g, m_channels);
   return gemm_workspace(plan_gemm(1, g, m_channels), m_channels);
 }
@@ -1783,6 +1763,10 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
 
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
+  if (g_conv_precision == 1) {  // C3: bf16 weight gradient on k_wgrad_lp (conv_lp.hip)
+    const TapList tl = live_taps(g);
+    if (lp_wgrad_ok(g, tl)) return lp_wgrad_splits(g, tl);
+  }
   if (wgrad1x1_ok(g)) return wgrad1x1_splits(g);
   const int nl = std::max(1, live_taps(g).n);
   const long long base = (long long)cdiv(g.Cin * nl, WBN) * cdiv(g.Cout, BM);
@@ -1804,6 +1788,16 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
                     void *workspace, float *dw, int accumulate, void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g) && splits > 0, E2EP_EINVAL, "e2ep_conv_wgrad: bad geometry");
+  if (g_conv_precision == 1) {
+    const TapList tl = live_taps(g);
+    if (lp_wgrad_ok(g, tl)) {
+      hipStream_t s = as_stream(stream);
+      float *part = static_cast<float *>(workspace);
+      const int used = lp_wgrad_launch(gout, x, g, tl, splits, part, s);
+      reduce_splits(part, used, g.Cout * g.Cin * g.R * g.S, dw, accumulate, g.R * g.S, tl.mask, s);
+      return launch_status("e2ep_conv_wgrad");
+    }
+  }
   if (wgrad1x1_ok(g)) {
     const int groups = g.N * g.P * g.Q / 8;
     const int gps = cdiv(groups, splits);

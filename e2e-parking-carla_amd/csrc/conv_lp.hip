@@ -1,0 +1,702 @@
+// Low-precision implicit-GEMM convolution (forward / data gradient) for gfx950: the BASELINE
+// C3 bf16 training mode and the C5 fp16 inference mode (operands rounded to nearest-even as
+// they are staged, fp32 accumulate, fp32 tensors in HBM).
+//
+// k_conv_gemm / k_conv_gemm2 (conv.hip) were shaped for the exact-f32 MFMA
+// (v_mfma_f32_32x32x2_f32, 64 cycles per 4096 FLOP): a 16-deep K-step feeds eight of them per
+// accumulator.  Run with bf16 operands the same step is ONE v_mfma_f32_32x32x16_bf16 (32
+// cycles for 32768 FLOP), so those kernels spend their time on per-step load issue, the fp32
+// LDS round trip, per-fragment conversions and barriers (C3 conv family at 0.027 of the bf16
+// peak, profiles/r02/bench_c3_bf16.json).  This kernel is built for the 16-bit MFMA instead:
+//  * operands are converted ONCE, when written to LDS (packed 8 x 16-bit per ds_write_b128),
+//    and the LDS images hold 16-bit values: half the LDS bytes, no conversion per fragment;
+//  * a K-step is 32 deep (two 16-deep MFMAs per accumulator per barrier) and the block tile is
+//    up to 128 x 256 (wave tiles up to 64 x 128: each A fragment feeds WN MFMAs, each B
+//    fragment WM), so L2 -> LDS operand bytes per FLOP drop 2 - 4x against 64 x 64 tiles;
+//  * LDS rows are k-contiguous, 32 values + 8 pad (80 B): the b128 fragment reads (a lane's 8
+//    consecutive k of one row) and the b128 stores are bank-conflict free;
+//  * K order as k_conv_gemm2: (live tap, 32-channel chunk) steps, then the remainder channels
+//    flattened over the taps 32 (channel, tap) pairs per step (no zero-padded channel steps:
+//    the BEV stem's 65 channels take 2 chunk steps per tap + 2 tail steps, not 3 per tap);
+//  * the data gradient is split by input-pixel phase, as in conv.hip;
+//  * one register set of lookahead: the next step's global loads are issued at the top of the
+//    step, its LDS store follows all of the step's MFMAs (sched_barrier fences, as conv.hip).
+// Small grids split K into fixed-order partial slabs (k_conv_lp_reduce): deterministic.
+#include <algorithm>
+
+#include "conv.h"
+
+namespace e2ep {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int LK = 32;   // K per step
+constexpr int LLD = 40;  // LDS row stride in 16-bit elements (32 k + 8 pad = 80 B)
+
+template <int OP> struct LpType;
+template <> struct LpType<1> { typedef __bf16 T; typedef bf16x8 T8; };
+template <> struct LpType<2> { typedef _Float16 T; typedef f16x8 T8; };
+
+template <int OP>
+__device__ __forceinline__ typename LpType<OP>::T8 cvt8(const float *v) {
+  f32x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = v[j];
+  return __builtin_convertvector(f, typename LpType<OP>::T8);
+}
+
+template <int OP>
+__device__ __forceinline__ f32x16 mfma16(typename LpType<OP>::T8 a, typename LpType<OP>::T8 b,
+                                         f32x16 c) {
+  if constexpr (OP == 1) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// MODE 0 (forward): rows m = co, K = (tap, ci), src = x [N,Cin,H,W], dst = y [N,Cout,P,Q].
+// MODE 1 (data gradient): rows m = ci, K = (tap, co), src = g [N,Cout,P,Q], dst = dx
+//   [N,M,H,W]; phase z = (py, px) (blockIdx.z / splits) as in k_conv_gemm.
+// Block tile (64 WM) x (64 WN), 2 x 2 waves of (32 WM) x (32 WN).
+template <int MODE, int ACT, int WM, int WN, int OP>
+__global__ void __launch_bounds__(256) k_conv_lp(
+    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
+    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
+  typedef typename LpType<OP>::T T;
+  typedef typename LpType<OP>::T8 T8;
+  constexpr int BMT = 64 * WM, BNT = 64 * WN;
+  constexpr int KGB = 256 / BNT;  // B k-groups (4, 2, 1)
+  constexpr int RPB = LK / KGB;   // B k rows per thread (8, 16, 32)
+  constexpr int KGA = 256 / BMT;  // A k-groups (4, 2)
+  constexpr int RPA = LK / KGA;   // A k per thread (8, 16)
+  __shared__ __attribute__((aligned(16))) T As[2][BMT][LLD];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LLD];
+  __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
+  __shared__ int s_ntaps;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.y * BMT, n0 = blockIdx.x * BNT;
+  const int split = blockIdx.z % splits, z = blockIdx.z / splits;
+
+  int py = 0, px = 0, Hc, Wc;
+  if (MODE == 0) {
+    Hc = g.P; Wc = g.Q;
+  } else {
+    py = z / g.sw; px = z % g.sw;
+    Hc = py < g.H ? (g.H - py + g.sh - 1) / g.sh : 0;
+    Wc = px < g.W ? (g.W - px + g.sw - 1) / g.sw : 0;
+  }
+  const int HWc = Hc * Wc;
+  const int Ntot = g.N * HWc;
+  if (n0 >= Ntot) return;
+
+  // live tap table of this phase (the same rules as k_conv_gemm)
+  if (tid == 0) {
+    int n = 0;
+    for (int r = 0; r < g.R; ++r) {
+      int dy;
+      if (MODE == 0) {
+        dy = r * g.dh - g.ph;
+      } else {
+        const int ny = py + g.ph - r * g.dh;
+        if (((ny % g.sh) + g.sh) % g.sh) continue;
+        dy = floordiv(ny, g.sh);
+      }
+      for (int s = 0; s < g.S; ++s) {
+        int dx;
+        if (MODE == 0) {
+          dx = s * g.dw - g.pw;
+          if (!axis_live(dy, g.P, g.sh, g.H) || !axis_live(dx, g.Q, g.sw, g.W)) continue;
+        } else {
+          const int nx = px + g.pw - s * g.dw;
+          if (((nx % g.sw) + g.sw) % g.sw) continue;
+          dx = floordiv(nx, g.sw);
+          if (!axis_live(dy, Hc, 1, g.P) || !axis_live(dx, Wc, 1, g.Q)) continue;
+        }
+        s_tdy[n] = dy;
+        s_tdx[n] = dx;
+        s_trs[n] = r * g.S + s;
+        ++n;
+      }
+    }
+    s_ntaps = n;
+  }
+  __syncthreads();
+  const int ntaps = s_ntaps;
+  const int Kc = MODE == 0 ? g.Cin : g.Cout;  // channels summed per tap
+  const int cfull = Kc / LK, crem = Kc - cfull * LK;
+  const int ntail = crem * ntaps;             // flattened (remainder channel, tap) rows
+  const int kmain = ntaps * cfull;
+  const int ksteps_all = kmain + (ntail + LK - 1) / LK;
+  const int kbeg = split * kper;
+  const int kend = min(ksteps_all, kbeg + kper);
+  const int nk = max(0, kend - kbeg);
+
+  const int Hs = MODE == 0 ? g.H : g.P, Ws = MODE == 0 ? g.W : g.Q;  // src spatial
+  const int HWs = Hs * Ws;
+  const int RS = g.R * g.S;
+  const __amdgpu_buffer_rsrc_t rw = rsrc(w, 4LL * g.Cout * g.Cin * RS);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(src, 4LL * g.N * Kc * HWs);
+  const int nrw = (int)min(4LL * g.Cout * g.Cin * RS, 0x7fffffffLL);
+  const int nrx = (int)min(4LL * g.N * Kc * HWs, 0x7fffffffLL);
+  const int tapstride = g.Cout * g.Cin;  // tap-major weights [RS][Cout][Cin]
+
+  // B: this thread's column (fixed) and k group (rows kg*RPB .. +RPB-1 of each step)
+  const int bn = tid % BNT, kg = tid / BNT;
+  const int ncol = n0 + bn;
+  const bool col_ok = ncol < Ntot;
+  int img = 0, cp = 0;
+  if (col_ok) {
+    img = ncol / HWc;
+    cp = ncol - img * HWc;
+  }
+  const int cy = cp / Wc, cx = cp - cy * Wc;
+  const int ybase = MODE == 0 ? cy * g.sh : cy;
+  const int xbase = MODE == 0 ? cx * g.sw : cx;
+  const int simg = img * Kc * HWs;
+  // A: MODE 0 thread = (row tid/KGA, k group tid%KGA): RPA channels contiguous in memory
+  // (float4 loads when Cin % 4 == 0); MODE 1 thread = (row tid%BMT, k group tid/BMT): rows
+  // contiguous in memory (lanes coalesce along ci), one load per k
+  const int am = MODE == 0 ? tid / KGA : tid % BMT;
+  const int akg = MODE == 0 ? tid % KGA : tid / BMT;
+  const bool arow_ok = m0 + am < M;
+  const bool avec = MODE == 0 && (g.Cin & 3) == 0;
+
+  float ra[RPA], rb[RPB];
+  const int klast = kend - 1;
+  auto load_tiles = [&](int ks_in) {
+    const bool live = ks_in <= klast;
+    const int ks = min(ks_in, klast);
+    if (ks < kmain) {  // one tap, 32 channels
+      const int tap = ks / cfull;
+      const int c0 = (ks - tap * cfull) * LK;
+      const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * tapstride;
+      if (MODE == 0) {
+        const int base = (live && arow_ok) ? (rs + (m0 + am) * g.Cin + c0 + akg * RPA) * 4 : nrw;
+        if (avec) {
+#pragma unroll
+          for (int q = 0; q < RPA / 4; ++q) {
+            const float4 v = bload4(rw, base + 16 * q);
+            ra[4 * q] = v.x; ra[4 * q + 1] = v.y; ra[4 * q + 2] = v.z; ra[4 * q + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < RPA; ++j) ra[j] = bload(rw, base + 4 * j);
+        }
+      } else {
+        // A[m = ci][k = co] = w[rs][co][ci]
+        const int base = (live && arow_ok) ? (rs + (c0 + akg * RPA) * g.Cin + m0 + am) * 4 : nrw;
+#pragma unroll
+        for (int j = 0; j < RPA; ++j) ra[j] = bload(rw, base + j * g.Cin * 4);
+      }
+      const int iy = ybase + dy, ix = xbase + dx;
+      const bool pix_ok = live && col_ok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
+      const int bbase = pix_ok ? (simg + (c0 + kg * RPB) * HWs + iy * Ws + ix) * 4 : nrx;
+#pragma unroll
+      for (int r = 0; r < RPB; ++r) rb[r] = bload(rx, bbase + r * HWs * 4);
+    } else {  // tail step: 32 flattened (remainder channel, tap) rows
+      // a thread's rows are consecutive flattened indices: decode the first (one division),
+      // then step the (channel, tap) pair
+      const int t0 = (ks - kmain) * LK;
+      {
+        const int i0 = t0 + akg * RPA;
+        int cq = i0 / ntaps, t = i0 - cq * ntaps;
+#pragma unroll
+        for (int j = 0; j < RPA; ++j) {
+          const bool ok = live && arow_ok && i0 + j < ntail;
+          const int c = cfull * LK + cq, rs = s_trs[ok ? t : 0] * tapstride;
+          ra[j] = bload(rw, ok ? (MODE == 0 ? rs + (m0 + am) * g.Cin + c : rs + c * g.Cin + m0 + am) * 4 : OOR);
+          const bool wrap = ++t == ntaps;
+          t = wrap ? 0 : t;
+          cq += wrap ? 1 : 0;
+        }
+      }
+      {
+        const int i0 = t0 + kg * RPB;
+        int cq = i0 / ntaps, t = i0 - cq * ntaps;
+#pragma unroll
+        for (int r = 0; r < RPB; ++r) {
+          const bool in = i0 + r < ntail;
+          const int tt = in ? t : 0;
+          const int iy = ybase + s_tdy[tt], ix = xbase + s_tdx[tt];
+          const bool ok = live && col_ok && in && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
+          rb[r] = bload(rx, ok ? (simg + (cfull * LK + cq) * HWs + iy * Ws + ix) * 4 : OOR);
+          const bool wrap = ++t == ntaps;
+          t = wrap ? 0 : t;
+          cq += wrap ? 1 : 0;
+        }
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < RPA / 8; ++q)
+      *reinterpret_cast<T8 *>(&As[buf][am][akg * RPA + 8 * q]) = cvt8<OP>(ra + 8 * q);
+#pragma unroll
+    for (int q = 0; q < RPB / 8; ++q)
+      *reinterpret_cast<T8 *>(&Bs[buf][bn][kg * RPB + 8 * q]) = cvt8<OP>(rb + 8 * q);
+  };
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{0};
+  const int li = lane & 31, lh = lane >> 5;
+  // lane half h supplies k = 8h .. 8h+7 of each 16-deep MFMA (one b128 read per fragment)
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int kk = 0; kk < LK / 16; ++kk) {
+      T8 a[WM], b[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+        a[i] = *reinterpret_cast<const T8 *>(&As[buf][32 * (WM * wm + i) + li][16 * kk + 8 * lh]);
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        b[j] = *reinterpret_cast<const T8 *>(&Bs[buf][32 * (WN * wn + j) + li][16 * kk + 8 * lh]);
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[i][j] = mfma16<OP>(a[i], b[j], acc[i][j]);
+    }
+  };
+  if (nk > 0) {
+    load_tiles(kbeg);
+    store_tiles(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      load_tiles(kbeg + kt + 1);          // past the range: re-reads, stored to the idle buffer
+      __builtin_amdgcn_sched_barrier(0);  // loads first, then the step's MFMAs
+      compute(kt & 1);
+      __builtin_amdgcn_sched_barrier(0);  // the LDS write after all of the step's MFMAs
+      store_tiles((kt + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // splits == 1: final values (bias, act; MODE 1: + residual gradient) into dst;
+  // splits > 1:  raw partial sums into dst = part[split][m][n] (k_conv_lp_reduce).
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, dst_bytes);
+  const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes : 0);
+  const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
+  const int HWd = Hd * Wd;
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int n = n0 + 32 * (WN * wn + j) + li;
+    const bool nok = n < Ntot;
+    int dbase, mstride;
+    if (splits == 1) {
+      const int im = n / HWc;
+      const int p = n - im * HWc;
+      int dp = p;
+      if (MODE == 1) {
+        const int u = p / Wc, v = p - u * Wc;
+        dp = (py + g.sh * u) * Wd + (px + g.sw * v);
+      }
+      dbase = im * M * HWd + dp;
+      mstride = HWd;
+    } else {
+      dbase = split * M * Ntot + n;
+      mstride = Ntot;
+    }
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 32 * (WM * wm + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        float v = acc[i][j][r];
+        const int off = (nok && m < M) ? (dbase + m * mstride) * 4 : OOR;
+        if (splits == 1) {
+          if (MODE == 0) {
+            if (bias) v += bias[min(m, M - 1)];
+            if (ACT == 1) v = fmaxf(v, 0.f);
+          } else if (bias) {
+            v += bload(rres, off);
+          }
+        }
+        bstore(rd, off, v);
+      }
+    }
+  }
+}
+
+// split-K reduction (fixed order) + bias / relu / residual epilogue:
+// out[img][m][p] = act(sum_s part[s][m][img*HW + p] + bias[m]) (+ res[img][m][p])
+__global__ void __launch_bounds__(256) k_conv_lp_reduce(
+    const float *__restrict__ part, int splits, int M, int HW, int Ntot,
+    const float *__restrict__ bias, int act, const float *__restrict__ res,
+    float *__restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= Ntot) return;
+  const int m = blockIdx.y;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[((size_t)k * M + m) * Ntot + n];
+  if (bias) s += bias[m];
+  if (act == 1) s = fmaxf(s, 0.f);
+  const int im = n / HW, p = n - im * HW;
+  const size_t o = ((size_t)im * M + m) * HW + p;
+  if (res) s += res[o];
+  out[o] = s;
+}
+
+// ---- launch plan ---------------------------------------------------------------------------
+struct LpPlan {
+  int wm, wn, splits, kper, nph;
+  long long ncols;  // columns of the largest phase
+};
+
+static LpPlan lp_plan(int mode, const ConvGeom &g, int M) {
+  LpPlan p;
+  const int Kc = mode == 0 ? g.Cin : g.Cout;
+  const int cfull = Kc / LK, crem = Kc - cfull * LK;
+  p.nph = mode ? g.sh * g.sw : 1;
+  p.ncols = 0;
+  int kmax = 0;
+  for (int z = 0; z < p.nph; ++z) {
+    int taps = 0;
+    long long cols;
+    if (mode == 0) {
+      cols = (long long)g.N * g.P * g.Q;
+      int ty = 0, tx = 0;
+      for (int r = 0; r < g.R; ++r) ty += axis_live(r * g.dh - g.ph, g.P, g.sh, g.H);
+      for (int s = 0; s < g.S; ++s) tx += axis_live(s * g.dw - g.pw, g.Q, g.sw, g.W);
+      taps = ty * tx;
+    } else {
+      const int py = z / g.sw, px = z % g.sw;
+      const int Hp = py < g.H ? (g.H - py + g.sh - 1) / g.sh : 0;
+      const int Wp = px < g.W ? (g.W - px + g.sw - 1) / g.sw : 0;
+      cols = (long long)g.N * Hp * Wp;
+      int ty = 0, tx = 0;
+      for (int r = 0; r < g.R; ++r) {
+        const int v = py + g.ph - r * g.dh;
+        if (((v % g.sh) + g.sh) % g.sh == 0) ty += axis_live(floordiv(v, g.sh), Hp, 1, g.P);
+      }
+      for (int s = 0; s < g.S; ++s) {
+        const int v = px + g.pw - s * g.dw;
+        if (((v % g.sw) + g.sw) % g.sw == 0) tx += axis_live(floordiv(v, g.sw), Wp, 1, g.Q);
+      }
+      taps = ty * tx;
+    }
+    p.ncols = std::max(p.ncols, cols);
+    kmax = std::max(kmax, taps * cfull + cdiv((long long)crem * taps, LK));
+  }
+  // rows: 128-row tiles when they pad M by at most 25 % (M = 112, 336, 672, 960 ...)
+  const bool tall = cdiv(M, 128) * 128LL * 4 <= 5LL * M;
+  p.wm = tall ? 2 : 1;
+  const long long mb = cdiv(M, 64 * p.wm);
+  // columns: the widest tile that still gives >= 2 workgroups per CU
+  p.wn = 1;
+  for (int wn = 4; wn >= 1; wn >>= 1) {
+    if (p.wm == 2 && wn == 4) continue;  // 128 x 256 is not instantiated
+    if (cdiv(p.ncols, 64 * wn) * mb * p.nph >= 512 || wn == 1) {
+      p.wn = wn;
+      break;
+    }
+  }
+  const int ft = g_tune[TUNE_LP_FORCE_TILE];  // benchmarking override: wm * 10 + wn
+  if (ft > 1) {
+    const int fwm = ft / 10, fwn = ft % 10;
+    if ((fwm == 1 || fwm == 2) && (fwn == 1 || fwn == 2 || fwn == 4) && !(fwm == 2 && fwn == 4)) {
+      p.wm = fwm;
+      p.wn = fwn;
+    }
+  }
+  const long long blocks = cdiv(p.ncols, 64 * p.wn) * cdiv(M, 64 * p.wm) * p.nph;
+  p.splits = 1;
+  if (blocks < 512 && p.nph == 1) {  // K split toward ~1024 workgroups, >= 4 steps each
+    int s = (int)((1024 + blocks - 1) / blocks);
+    s = std::min(s, std::max(1, kmax / 4));
+    p.splits = std::max(1, std::min(s, 32));
+  }
+  p.kper = cdiv(std::max(kmax, 1), p.splits);
+  if (p.splits > 1) p.splits = cdiv(kmax, p.kper);
+  return p;
+}
+
+// Shapes left on k_conv_gemm (conv.hip), measured faster there (scripts/bench_conv.py --ab,
+// profiles/r03/lp_ab.txt): M < 40 (it has 32-row tiles) and single-step K (Kc <= 32 on a 1x1:
+// the 128x128-map expand / project convs, a streaming pass whose smaller tiles keep more
+// workgroups in flight per CU).
+bool lp_ok(int mode, const ConvGeom &g, int M) {
+  if (g_tune[TUNE_LP] == 1 || !(g.wlayout == 1 || g.R * g.S == 1)) return false;
+  if (g_tune[TUNE_LP_FORCE_TILE] > 1) return true;  // benchmarking / tests: every shape
+  const LpPlan p = lp_plan(mode, g, M);
+  const int Kc = mode == 0 ? g.Cin : g.Cout;
+  return M >= 40 && (g.R * g.S > 1 || Kc > LK) && p.kper >= 1;
+}
+
+size_t lp_workspace(int mode, const ConvGeom &g, int M) {
+  const LpPlan p = lp_plan(mode, g, M);
+  return p.splits > 1 ? (size_t)p.splits * M * p.ncols * sizeof(float) : 0;
+}
+
+template <int MODE, int ACT, int OP>
+static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, const float *src,
+                     const float *bias, float *out, long long out_bytes, const ConvGeom &g, int M) {
+#define LP_L(WMV, WNV)                                                                          \
+  hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP>), grid, dim3(256), 0, s, w, src, bias, \
+                     out, out_bytes, g, M, p.splits, p.kper)
+  if (p.wm == 2) {
+    if (p.wn == 2) LP_L(2, 2);
+    else LP_L(2, 1);
+  } else {
+    if (p.wn == 4) LP_L(1, 4);
+    else if (p.wn == 2) LP_L(1, 2);
+    else LP_L(1, 1);
+  }
+#undef LP_L
+}
+
+int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
+              float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
+              hipStream_t s) {
+  const LpPlan p = lp_plan(mode, g, M);
+  const dim3 grid(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
+  float *out = dst;
+  long long out_bytes = dst_bytes;
+  if (p.splits > 1) {
+    if (!workspace) {
+      set_error("conv (low precision): split-K plan needs a workspace (query the *_workspace entry point)");
+      return E2EP_EINVAL;
+    }
+    out = static_cast<float *>(workspace);
+    out_bytes = (long long)p.splits * M * p.ncols * 4;
+  }
+  const float *kb = p.splits > 1 ? nullptr : bias;  // bias / residual go to the reduction
+  if (mode == 0 && act == 0) {
+    if (op == 1) lp_tiles<0, 0, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M);
+    else lp_tiles<0, 0, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M);
+  } else if (mode == 0) {
+    if (op == 1) lp_tiles<0, 1, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M);
+    else lp_tiles<0, 1, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M);
+  } else {
+    if (op == 1) lp_tiles<1, 0, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M);
+    else lp_tiles<1, 0, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M);
+  }
+  if (p.splits > 1) {
+    const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
+    hipLaunchKernelGGL(k_conv_lp_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
+                       static_cast<const float *>(workspace), p.splits, M, HW, (int)p.ncols,
+                       mode == 0 ? bias : nullptr, act, mode == 1 ? bias : nullptr, dst);
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 weight gradient (BASELINE C3: bf16 operands, fp32 accumulate and gradient).
+//   dW[co][ci*RS + tap] = sum_(n,p) g[n,co,p] x[n,ci,p+tap]: M = Cout, N = (ci, live tap)
+//   columns, K = pixels, split over blocks into fixed-order partial slabs (k_reduce_splits).
+// k_conv_wgrad2 (conv.hip) with bf16 operands runs two 16-deep MFMAs per 64 x 64 tile and
+// 32-pixel step, converting every fragment from fp32 LDS rows.  Here, as in k_conv_lp, the
+// operands are converted once into 16-bit LDS rows (32 pixels + 8 pad), tiles are up to
+// 128 x 128 (wave tiles up to 64 x 64: 8 MFMAs per wave per step), and:
+//  * A = g rows: a thread owns 8 consecutive pixels of a row (two float4 loads, one b128
+//    LDS write);
+//  * B = im2col x columns: a thread owns a pixel PAIR of BNT/16 columns (lanes on consecutive
+//    pairs: coalesced along the image rows), packed to bf16x2 per column (one b32 write);
+//  * a step never straddles two images (P*Q % 32 == 0, every hot-path map), so its image and
+//    first pixel are block-uniform.
+// ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int WM, int WN>
+__global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout,
+                                                  const float *__restrict__ x,
+                                                  float *__restrict__ part, ConvGeom g,
+                                                  int pix_per_split, TapList tl) {
+  constexpr int BMT = 64 * WM, BNT = 64 * WN;
+  constexpr int NBC = BNT / 16;  // B columns per thread
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][BMT][LLD];  // As[co][pixel]
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BNT][LLD];  // Bs[column][pixel]
+  __shared__ int s_tap[MAXTAPS];
+  if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
+  __syncthreads();
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int RS = g.R * g.S;
+  const int Kw = g.Cin * RS;    // columns of dW (ci-major, tap-minor)
+  const int Kl = g.Cin * tl.n;  // live columns (ci, live tap index)
+  const int n0 = blockIdx.x * BNT, m0 = blockIdx.y * BMT;
+  const int split = blockIdx.z;
+  const int PQ = g.P * g.Q;
+  const int Ptot = g.N * PQ;
+  const int pbeg = split * pix_per_split;  // a multiple of LK
+  const int pend = min(Ptot, pbeg + pix_per_split);
+  const int nk = max(0, (pend - pbeg) / LK);
+  const int HW = g.H * g.W;
+
+  // A: thread = (co row tid/4 (+64 i), pixel octet tid%4)
+  const int ar = tid >> 2, ao = tid & 3;
+  // B: thread = (pixel pair tid%16, column group tid/16): columns bcg + 16 j
+  const int bq = tid & 15, bcg = tid >> 4;
+  int cconst[NBC], cdy[NBC], cdx[NBC];
+#pragma unroll
+  for (int j = 0; j < NBC; ++j) {
+    const int col = n0 + bcg + 16 * j;
+    const int cc = col < Kl ? col : 0;
+    const int ci = cc / tl.n, tap = s_tap[cc - ci * tl.n];
+    const int r = tap / g.S, sx = tap - r * g.S;
+    cdy[j] = r * g.dh - g.ph;
+    cdx[j] = sx * g.dw - g.pw;
+    cconst[j] = ci * HW + cdy[j] * g.W + cdx[j];
+    if (col >= Kl) cdy[j] = -(1 << 29);  // never in bounds
+  }
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
+  const int nrx = (int)min(4LL * g.N * g.Cin * HW, 0x7fffffffLL);
+
+  float4 ra[WM][2];
+  float rb[NBC][2];
+  auto load_tiles = [&](int ks) {
+    const int p0 = pbeg + min(ks, nk - 1) * LK;  // past the range: re-read, never stored
+    const int im = p0 / PQ, od0 = p0 - im * PQ;   // block-uniform
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      const int co = m0 + ar + 64 * i;
+      const int base = co < g.Cout ? ((im * g.Cout + co) * PQ + od0 + 8 * ao) * 4 : OOR;
+      ra[i][0] = bload4(rg, base);
+      ra[i][1] = bload4(rg, base + 16);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int od = od0 + 2 * bq + e;
+      const int oy = od / g.Q, ox = od - oy * g.Q;
+      const int yb = oy * g.sh, xb = ox * g.sw;
+      const int pbase = im * g.Cin * HW + yb * g.W + xb;
+#pragma unroll
+      for (int j = 0; j < NBC; ++j) {
+        const bool ok = (unsigned)(yb + cdy[j]) < (unsigned)g.H && (unsigned)(xb + cdx[j]) < (unsigned)g.W;
+        rb[j][e] = bload(rx, ok ? (pbase + cconst[j]) * 4 : nrx);
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      const float v[8] = {ra[i][0].x, ra[i][0].y, ra[i][0].z, ra[i][0].w,
+                          ra[i][1].x, ra[i][1].y, ra[i][1].z, ra[i][1].w};
+      *reinterpret_cast<bf16x8 *>(&As[buf][ar + 64 * i][8 * ao]) = cvt8<1>(v);
+    }
+#pragma unroll
+    for (int j = 0; j < NBC; ++j) {
+      const f32x2 f = {rb[j][0], rb[j][1]};
+      *reinterpret_cast<bf16x2 *>(&Bs[buf][bcg + 16 * j][2 * bq]) = __builtin_convertvector(f, bf16x2);
+    }
+  };
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{0};
+  const int li = lane & 31, lh = lane >> 5;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int kk = 0; kk < LK / 16; ++kk) {
+      bf16x8 a[WM], b[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+        a[i] = *reinterpret_cast<const bf16x8 *>(&As[buf][32 * (WM * wm + i) + li][16 * kk + 8 * lh]);
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        b[j] = *reinterpret_cast<const bf16x8 *>(&Bs[buf][32 * (WN * wn + j) + li][16 * kk + 8 * lh]);
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if (nk > 0) {
+    load_tiles(0);
+    store_tiles(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      load_tiles(kt + 1);
+      __builtin_amdgcn_sched_barrier(0);  // loads first, then the step's MFMAs
+      compute(kt & 1);
+      __builtin_amdgcn_sched_barrier(0);  // the LDS write after all of the step's MFMAs
+      store_tiles((kt + 1) & 1);
+      __syncthreads();
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int lcol = n0 + 32 * (WN * wn + j) + li;
+    const int lci = lcol < Kl ? lcol / tl.n : 0;
+    const int col = lci * RS + s_tap[lcol < Kl ? lcol - lci * tl.n : 0];  // dW column
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int co = m0 + 32 * (WM * wm + i) + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+        const bool ok = co < g.Cout && lcol < Kl;
+        bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[i][j][rr]);
+      }
+    }
+  }
+}
+
+static void lp_wgrad_tile(const ConvGeom &g, const TapList &tl, int &wm, int &wn) {
+  const int Kl = g.Cin * tl.n;
+  wm = cdiv(g.Cout, 128) * 128LL * 4 <= 5LL * g.Cout ? 2 : 1;
+  wn = cdiv(Kl, 128) * 128LL * 4 <= 5LL * Kl ? 2 : 1;
+  // few pixels (slabs of >= 8 steps): smaller tiles until the grid has >= 256 workgroups
+  const long long cap = std::max(1LL, (long long)g.N * g.P * g.Q / (8 * LK));
+  while (wm * wn > 1 && (long long)cdiv(Kl, 64 * wn) * cdiv(g.Cout, 64 * wm) * std::min(cap, 256LL) < 256) {
+    if (wm >= wn) wm = 1;
+    else wn = 1;
+  }
+  const int ft = g_tune[TUNE_LP_WGRAD_TILE];  // benchmarking override: wm * 10 + wn
+  if (ft > 1 && (ft / 10 == 1 || ft / 10 == 2) && (ft % 10 == 1 || ft % 10 == 2)) {
+    wm = ft / 10;
+    wn = ft % 10;
+  }
+}
+
+// Few (Cout, column) pairs over many pixels (the 128x128 maps' 24 / 48-channel 1x1s, the
+// segmentation classifier) stay on k_wgrad_1x1 / k_conv_wgrad2, measured faster there.
+bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl) {
+  if (g_tune[TUNE_LP_WGRAD] == 1 || tl.n <= 0 || (g.P * g.Q) % LK != 0) return false;
+  return g_tune[TUNE_LP_WGRAD_TILE] > 1 || (long long)g.Cout * g.Cin * tl.n >= 2048;
+}
+
+int lp_wgrad_splits(const ConvGeom &g, const TapList &tl) {
+  int wm, wn;
+  lp_wgrad_tile(g, tl, wm, wn);
+  const long long tiles = (long long)cdiv(g.Cin * tl.n, 64 * wn) * cdiv(g.Cout, 64 * wm);
+  const long long pix = (long long)g.N * g.P * g.Q;
+  long long s = (1024 + tiles - 1) / tiles;  // toward ~1024 workgroups
+  s = std::min(s, std::max(1LL, pix / (8 * LK)));  // >= 8 steps per slab
+  return (int)std::max(1LL, std::min(s, 256LL));
+}
+
+int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
+                    int splits, float *part, hipStream_t s) {
+  int wm, wn;
+  lp_wgrad_tile(g, tl, wm, wn);
+  const int Ptot = g.N * g.P * g.Q;
+  int per = (Ptot + splits - 1) / splits;
+  per = (per + LK - 1) / LK * LK;
+  const int used = (Ptot + per - 1) / per;
+  const dim3 grid(cdiv(g.Cin * tl.n, 64 * wn), cdiv(g.Cout, 64 * wm), used);
+  if (wm == 2 && wn == 2)
+    hipLaunchKernelGGL((k_wgrad_lp<2, 2>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+  else if (wm == 2)
+    hipLaunchKernelGGL((k_wgrad_lp<2, 1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+  else if (wn == 2)
+    hipLaunchKernelGGL((k_wgrad_lp<1, 2>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+  else
+    hipLaunchKernelGGL((k_wgrad_lp<1, 1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+  return used;
+}
+
+}  // namespace e2ep

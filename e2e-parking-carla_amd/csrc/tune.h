@@ -13,7 +13,11 @@ enum Tune {
   TUNE_CONV_FORCE_TILE = 7,   // benchmarking: k_conv_gemm tile bm * 1000 + bnt (1 = automatic)
   TUNE_CONV_FORCE_SPLITS = 8, // benchmarking: k_conv_gemm K splits + 1 (1 = automatic)
   TUNE_WGRAD_GEN = 9,         // spatial weight-gradient kernel: 2 = k_conv_wgrad2 where it applies, 1 = k_conv_wgrad
-  TUNE_N = 10
+  TUNE_LP_FORCE_TILE = 10,    // benchmarking: k_conv_lp wave tile wm * 10 + wn (1 = automatic)
+  TUNE_LP = 11,               // low-precision conv forward / data gradient: 2 = k_conv_lp, 1 = k_conv_gemm(2)
+  TUNE_LP_WGRAD = 12,         // bf16 weight gradient: 2 = k_wgrad_lp, 1 = k_conv_wgrad2 / k_wgrad_1x1
+  TUNE_LP_WGRAD_TILE = 13,    // benchmarking: k_wgrad_lp wave tile wm * 10 + wn (1 = automatic)
+  TUNE_N = 14
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

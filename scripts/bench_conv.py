@@ -1,7 +1,7 @@
 """Per-shape timing of the e2ep implicit-GEMM conv kernels (fwd / dgrad / wgrad separately,
 back-to-back launches between HIP events) on the conv shapes of one ParkingModel train step.
 
-    python scripts/bench_conv.py [--record] [--top 30] [--ab "6=512;6=1024"]
+    python scripts/bench_conv.py [--record] [--top 30] [--ab "6=512;6=1024"] [--precision bf16]
 --record runs the model once to (re)write scripts/conv_shapes.json; --ab times every shape
 under each ';'-separated e2ep_tune setting ("key=value,key=value"), interleaved in one
 process, and prints the per-setting totals and per-shape times side by side."""
@@ -64,7 +64,10 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--ab", default=None)
+    ap.add_argument("--precision", choices=("fp32", "bf16", "fp16"), default="fp32")
     a = ap.parse_args()
+    from e2ep_amd import precision
+    precision.set(a.precision)
     if a.ab:
         return ab(a)
     from e2ep_amd import _lib, conv

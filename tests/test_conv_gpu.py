@@ -273,3 +273,89 @@ def test_side_stream_weight_gradient_equals_serial():
             assert all(torch.equal(a, c) for a, c in zip(got, serial))
     finally:
         conv.set_wgrad_overlap(prev)
+
+
+# k_conv_lp (csrc/conv_lp.hip): the bf16 / fp16 forward and data-gradient kernel, every conv
+# geometry of CASES, every block tile (e2ep_tune key 10 = wm * 10 + wn; 1 = automatic), against
+# fp64 convolutions of the rounded operands (bias, ReLU and the skip gradient in fp32).
+LP_TILES = [1, 11, 12, 14, 21, 22]
+
+
+@pytest.mark.parametrize("tile", LP_TILES, ids=[f"t{t}" for t in LP_TILES])
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_conv_lp_kernel_all_geometries(case, tile):
+    from e2ep_amd import _lib, conv, precision
+    N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
+    mode, dt = ("fp16", torch.float16) if tile == 12 else ("bf16", torch.bfloat16)
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5
+    b = torch.randn(Cout, generator=g) if has_b else None
+    if H * W == 1 and R * S == 1:
+        pytest.skip("1x1 convs on 1x1 maps run on the fp32 skinny GEMM in every mode")
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    old_t = _lib.call_raw("e2ep_tune", 10, tile)
+    old_lp = _lib.call_raw("e2ep_tune", 11, 2)
+    old_wt = _lib.call_raw("e2ep_tune", 13, tile if tile in (11, 12, 21, 22) else 1)
+    old_wlp = _lib.call_raw("e2ep_tune", 12, 2)
+    try:
+        with precision.use(mode):
+            y = conv.conv2d(xd, wd, b.to(DEV) if has_b else None, (st, st), pad, (dil, dil), act)
+            gy = torch.randn(y.shape, generator=g)
+            y.backward(gy.to(DEV))
+    finally:
+        for k, v in ((10, old_t), (11, old_lp), (13, old_wt), (12, old_wlp)):
+            _lib.call_raw("e2ep_tune", k, v)
+    r = lambda t: t.to(dt).double()  # noqa: E731
+    xr = r(x).requires_grad_(True)
+    y_r = F.conv2d(F.pad(xr, pad), r(w), b.double() if has_b else None, st, 0, dil)
+    if act:
+        y_r = torch.relu(y_r)
+    # the data gradient takes the gradient through the product's own ReLU mask, rounded
+    gy_in = gy.double() * (y.detach().cpu() > 0) if act else gy.double()
+    F.conv2d(F.pad(xr, pad), r(w), None, st, 0, dil).backward(r(gy_in.float()))
+    if Cin * R * S <= 32 and R * S > 1 and Cout <= 64:
+        # the direct forward kernel (k_conv_direct, the EfficientNet stem) is fp32 in every mode
+        y64 = F.conv2d(F.pad(x.double(), pad), w.double(), b.double() if has_b else None, st, 0, dil)
+        assert rel_l2(y, torch.relu(y64) if act else y64) < 2e-6
+    else:
+        assert rel_l2(y, y_r) < 2e-6
+    assert rel_l2(xd.grad, xr.grad) < 2e-6
+    # weight gradient: bf16 operands (x and the gradient at the conv output) in C3 (k_wgrad_lp,
+    # key 13 = its tile), fp32 in the fp16 inference mode
+    if mode == "bf16":
+        wr = r(w).requires_grad_(True)
+        F.conv2d(F.pad(r(x), pad), wr, None, st, 0, dil).backward(r(gy_in.float()))
+        assert rel_l2(wd.grad, wr.grad) < 5e-6
+    else:
+        w64 = w.double().requires_grad_(True)
+        F.conv2d(F.pad(x.double(), pad), w64, None, st, 0, dil).backward(gy_in)
+        assert rel_l2(wd.grad, w64.grad) < 2e-6
+
+
+@pytest.mark.parametrize("case", SKIP_CASES, ids=[str(i) for i in range(len(SKIP_CASES))])
+def test_conv_lp_skip_gradient_fused(case):
+    """k_conv_lp data gradient with the skip gradient added in its epilogue / reduction."""
+    from e2ep_amd import conv, precision
+    N, Cin, H, W, Cout, R, S, pad, gc = case
+    g = torch.Generator().manual_seed(17 + Cin)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    with precision.use("bf16"):
+        y, xs = conv.conv2d(xd, wd, None, (1, 1), pad, (1, 1), 0, grad_channels=gc, skip=True)
+        gy = torch.randn(y.shape, generator=g)
+        gs = torch.randn(x.shape, generator=g)
+        ((y * gy.to(DEV)).sum() + (xs * gs.to(DEV)).sum()).backward()
+    r = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    xr = r(x).requires_grad_(True)
+    y_r = F.conv2d(F.pad(xr, pad), r(w))
+    (y_r * r(gy)).sum().backward()
+    gx = xr.grad.clone()
+    if gc is not None:
+        gx[:, gc:] = 0
+    gx += gs.double()
+    assert rel_l2(y.detach().cpu(), y_r) < 2e-6
+    assert rel_l2(xd.grad.cpu(), gx) < 2e-6
