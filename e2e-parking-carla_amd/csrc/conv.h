@@ -38,20 +38,23 @@ struct TapList {
   int tap[MAXTAPS];
 };
 
-// Low-precision (bf16 / fp16 operand) implicit-GEMM forward (mode 0) / data gradient (mode 1),
-// conv_lp.hip.  lp_workspace() bytes of split-K workspace (0: none); lp_launch() returns an
+// Implicit-GEMM forward (mode 0) / data gradient (mode 1) with 32-deep K-steps and up to
+// 128-row tiles, conv_lp.hip: bf16 / fp16 operands (op 1 / 2), and fp32 (op 0) where
+// TUNE_LP32 selects it.  lp_workspace() bytes of split-K workspace (0: none); lp_launch() returns an
 // E2EP status.  Tap-major weights ([R*S][Cout][Cin]) or 1x1 filters only.
-bool lp_ok(int mode, const ConvGeom &g, int M);
-size_t lp_workspace(int mode, const ConvGeom &g, int M);
+bool lp_ok(int mode, const ConvGeom &g, int M, int op);
+size_t lp_workspace(int mode, const ConvGeom &g, int M, int op);
 int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
               float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
               hipStream_t s);
 
-// bf16 weight gradient (C3), conv_lp.hip: partial slabs part[split][Cout][Cin*R*S] for the
-// fixed-order split reduction of conv.hip; lp_wgrad_launch returns the slabs written.
+// Weight gradient with 32-pixel K-steps and up to 128 x 128 tiles, conv_lp.hip: bf16 operands
+// (op 1, C3) or fp32 (op 0, where TUNE_LP32W selects it).  Partial slabs
+// part[split][Cout][Cin*R*S] for the fixed-order split reduction of conv.hip;
+// lp_wgrad_launch returns the slabs written.
 bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl);
 int lp_wgrad_splits(const ConvGeom &g, const TapList &tl);
 int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
-                    int splits, float *part, hipStream_t s);
+                    int splits, float *part, hipStream_t s, int op);
 
 }  // namespace e2ep

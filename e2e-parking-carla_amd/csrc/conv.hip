@@ -1586,10 +1586,17 @@ static int conv1x1_gemm(int mode, int act, const float *w, const float *src, con
                   workspace, s);
 }
 
+// weight-gradient kernel family: k_wgrad_lp for C3 (bf16 operands; fp16 inference keeps the fp32
+// weight gradient) unless e2ep_tune key 12 = 1, and for fp32 when key 15 = 2
+static bool lp_wgrad_selected() {
+  if (g_conv_precision == 1) return g_tune[TUNE_LP_WGRAD] != 1;
+  return g_tune[TUNE_LP32W] == 2;
+}
+
 static int launch_gemm(int mode, int act, const float *w, const float *src, const float *bias,
                        float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
                        hipStream_t s) {
-  if (g_conv_precision != 0 && lp_ok(mode, g, M))  // bf16 / fp16 operands: conv_lp.hip
+  if (g_conv_precision != 0 && lp_ok(mode, g, M, g_conv_precision))
     return lp_launch(mode, act, g_conv_precision, w, src, bias, dst, dst_bytes, g, M, workspace, s);
   if (conv1x1_gemm_ok(mode, g))
     return conv1x1_gemm(mode, act, w, src, bias, dst, dst_bytes, g, M, workspace, s);
@@ -1617,6 +1624,8 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
       return 0;
     }
   }
+  if (g_conv_precision == 0 && g_tune[TUNE_LP32] == 2 && lp_ok(mode, g, M, 0))
+    return lp_launch(mode, act, 0, w, src, bias, dst, dst_bytes, g, M, workspace, s);
   const GemmPlan p = plan_gemm(mode, g, M);
   dim3 grid(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
   float *out = dst;
@@ -1679,10 +1688,11 @@ extern "C" {
 size_t e2ep_conv_fwd_workspace(const int *dims) {
   ConvGeom g = make_geom(dims);
   if (direct_ok(g)) return 0;
-  if (g_conv_precision != 0) {  // the launch's w_layout is not known here: cover both paths
+  if (g_conv_precision != 0 || g_tune[TUNE_LP32] == 2) {  // w_layout unknown here: cover all
     g.wlayout = 1;
-    if (lp_ok(0, g, g.Cout))
-      return std::max(lp_workspace(0, g, g.Cout), gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout));
+    if (lp_ok(0, g, g.Cout, g_conv_precision))
+      return std::max(lp_workspace(0, g, g.Cout, g_conv_precision),
+                      gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout));
   }
   if (conv1x1_gemm_ok(0, g)) return conv1x1_ws(0, g, g.Cout);
   return gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout);
@@ -1690,10 +1700,11 @@ size_t e2ep_conv_fwd_workspace(const int *dims) {
 
 size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
   ConvGeom g = make_geom(dims);
-  if (g_conv_precision != 0) {
+  if (g_conv_precision != 0 || g_tune[TUNE_LP32] == 2) {
     g.wlayout = 1;
-    if (lp_ok(1, g, m_channels))
-      return std::max(lp_workspace(1, g, m_channels), gemm_workspace(plan_gemm(1, g, m_channels), m_channels));
+    if (lp_ok(1, g, m_channels, g_conv_precision))
+      return std::max(lp_workspace(1, g, m_channels, g_conv_precision),
+                      gemm_workspace(plan_gemm(1, g, m_channels), m_channels));
   }
   if (conv1x1_gemm_ok(1, g)) return conv1x1_ws(1, g, m_channels);
   return gemm_workspace(plan_gemm(1, g, m_channels), m_channels);
@@ -1763,7 +1774,7 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
 
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
-  if (g_conv_precision == 1) {  // C3: bf16 weight gradient on k_wgrad_lp (conv_lp.hip)
+  if (lp_wgrad_selected()) {  // k_wgrad_lp (conv_lp.hip): C3 bf16, or fp32 when selected
     const TapList tl = live_taps(g);
     if (lp_wgrad_ok(g, tl)) return lp_wgrad_splits(g, tl);
   }
@@ -1788,12 +1799,12 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
                     void *workspace, float *dw, int accumulate, void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g) && splits > 0, E2EP_EINVAL, "e2ep_conv_wgrad: bad geometry");
-  if (g_conv_precision == 1) {
+  if (lp_wgrad_selected()) {
     const TapList tl = live_taps(g);
     if (lp_wgrad_ok(g, tl)) {
       hipStream_t s = as_stream(stream);
       float *part = static_cast<float *>(workspace);
-      const int used = lp_wgrad_launch(gout, x, g, tl, splits, part, s);
+      const int used = lp_wgrad_launch(gout, x, g, tl, splits, part, s, g_conv_precision == 1 ? 1 : 0);
       reduce_splits(part, used, g.Cout * g.Cin * g.R * g.S, dw, accumulate, g.R * g.S, tl.mask, s);
       return launch_status("e2ep_conv_wgrad");
     }

@@ -35,13 +35,18 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int LK = 32;   // K per step
 constexpr int LLD = 40;  // LDS row stride in 16-bit elements (32 k + 8 pad = 80 B)
+// fp32 operands (OP 0): 32 k + 4 pad = 144 B rows (b128 reads and writes conflict-free)
+constexpr int lld_of(int op) { return op == 0 ? 36 : LLD; }
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int OP> struct LpType;
+template <> struct LpType<0> { typedef float T; typedef f32x4 T8; };
 template <> struct LpType<1> { typedef __bf16 T; typedef bf16x8 T8; };
 template <> struct LpType<2> { typedef _Float16 T; typedef f16x8 T8; };
 
 template <int OP>
 __device__ __forceinline__ typename LpType<OP>::T8 cvt8(const float *v) {
+  static_assert(OP != 0, "fp32 rows are stored as float4");
   f32x8 f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = v[j];
@@ -70,8 +75,10 @@ __global__ void __launch_bounds__(256) k_conv_lp(
   constexpr int RPB = LK / KGB;   // B k rows per thread (8, 16, 32)
   constexpr int KGA = 256 / BMT;  // A k-groups (4, 2)
   constexpr int RPA = LK / KGA;   // A k per thread (8, 16)
-  __shared__ __attribute__((aligned(16))) T As[2][BMT][LLD];
-  __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LLD];
+  constexpr int LD = lld_of(OP);
+  static_assert(OP != 0 || WN <= 2, "fp32: 64 x 256 tiles would leave one block per CU");
+  __shared__ __attribute__((aligned(16))) T As[2][BMT][LD];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LD];
   __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
   __shared__ int s_ntaps;
 
@@ -232,12 +239,23 @@ __global__ void __launch_bounds__(256) k_conv_lp(
     }
   };
   auto store_tiles = [&](int buf) {
+    if constexpr (OP == 0) {
 #pragma unroll
-    for (int q = 0; q < RPA / 8; ++q)
-      *reinterpret_cast<T8 *>(&As[buf][am][akg * RPA + 8 * q]) = cvt8<OP>(ra + 8 * q);
+      for (int q = 0; q < RPA / 4; ++q)
+        *reinterpret_cast<f32x4 *>(&As[buf][am][akg * RPA + 4 * q]) =
+            f32x4{ra[4 * q], ra[4 * q + 1], ra[4 * q + 2], ra[4 * q + 3]};
 #pragma unroll
-    for (int q = 0; q < RPB / 8; ++q)
-      *reinterpret_cast<T8 *>(&Bs[buf][bn][kg * RPB + 8 * q]) = cvt8<OP>(rb + 8 * q);
+      for (int q = 0; q < RPB / 4; ++q)
+        *reinterpret_cast<f32x4 *>(&Bs[buf][bn][kg * RPB + 4 * q]) =
+            f32x4{rb[4 * q], rb[4 * q + 1], rb[4 * q + 2], rb[4 * q + 3]};
+    } else {
+#pragma unroll
+      for (int q = 0; q < RPA / 8; ++q)
+        *reinterpret_cast<T8 *>(&As[buf][am][akg * RPA + 8 * q]) = cvt8<OP>(ra + 8 * q);
+#pragma unroll
+      for (int q = 0; q < RPB / 8; ++q)
+        *reinterpret_cast<T8 *>(&Bs[buf][bn][kg * RPB + 8 * q]) = cvt8<OP>(rb + 8 * q);
+    }
   };
 
   f32x16 acc[WM][WN];
@@ -246,8 +264,36 @@ __global__ void __launch_bounds__(256) k_conv_lp(
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{0};
   const int li = lane & 31, lh = lane >> 5;
-  // lane half h supplies k = 8h .. 8h+7 of each 16-deep MFMA (one b128 read per fragment)
+  // 16-bit: lane half h supplies k = 8h .. 8h+7 of each 16-deep MFMA (one b128 read per
+  // fragment).  fp32 (v_mfma_f32_32x32x2_f32, exact): MFMA i of the step takes k = i from lane
+  // half 0 and k = 16 + i from lane half 1, so a lane's 16 operands per row are one 64-B run
+  // (four b128 reads); the 32 k are summed in that fixed order.
   auto compute = [&](int buf) {
+    if constexpr (OP == 0) {
+      float a[WM][16], b[WN][16];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(&As[buf][32 * (WM * wm + i) + li][16 * lh + 4 * q]);
+          a[i][4 * q] = v[0]; a[i][4 * q + 1] = v[1]; a[i][4 * q + 2] = v[2]; a[i][4 * q + 3] = v[3];
+        }
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(&Bs[buf][32 * (WN * wn + j) + li][16 * lh + 4 * q]);
+          b[j][4 * q] = v[0]; b[j][4 * q + 1] = v[1]; b[j][4 * q + 2] = v[2]; b[j][4 * q + 3] = v[3];
+        }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < LK / 16; ++kk) {
       T8 a[WM], b[WN];
@@ -349,7 +395,7 @@ struct LpPlan {
   long long ncols;  // columns of the largest phase
 };
 
-static LpPlan lp_plan(int mode, const ConvGeom &g, int M) {
+static LpPlan lp_plan(int mode, const ConvGeom &g, int M, int op) {
   LpPlan p;
   const int Kc = mode == 0 ? g.Cin : g.Cout;
   const int cfull = Kc / LK, crem = Kc - cfull * LK;
@@ -391,16 +437,19 @@ static LpPlan lp_plan(int mode, const ConvGeom &g, int M) {
   // columns: the widest tile that still gives >= 2 workgroups per CU
   p.wn = 1;
   for (int wn = 4; wn >= 1; wn >>= 1) {
-    if (p.wm == 2 && wn == 4) continue;  // 128 x 256 is not instantiated
+    if ((p.wm == 2 || op == 0) && wn == 4) continue;  // not instantiated
     if (cdiv(p.ncols, 64 * wn) * mb * p.nph >= 512 || wn == 1) {
       p.wn = wn;
       break;
     }
   }
+  // fp32: 64 x 64 tiles (the larger fp32 tiles measured 1.3 - 2x slower: profiles/r03/lp/
+  // conv_ab_fp32.txt)
+  if (op == 0) p.wm = p.wn = 1;
   const int ft = g_tune[TUNE_LP_FORCE_TILE];  // benchmarking override: wm * 10 + wn
   if (ft > 1) {
     const int fwm = ft / 10, fwn = ft % 10;
-    if ((fwm == 1 || fwm == 2) && (fwn == 1 || fwn == 2 || fwn == 4) && !(fwm == 2 && fwn == 4)) {
+    if ((fwm == 1 || fwm == 2) && (fwn == 1 || fwn == 2 || fwn == 4) && !((fwm == 2 || op == 0) && fwn == 4)) {
       p.wm = fwm;
       p.wn = fwn;
     }
@@ -421,16 +470,19 @@ static LpPlan lp_plan(int mode, const ConvGeom &g, int M) {
 // profiles/r03/lp_ab.txt): M < 40 (it has 32-row tiles) and single-step K (Kc <= 32 on a 1x1:
 // the 128x128-map expand / project convs, a streaming pass whose smaller tiles keep more
 // workgroups in flight per CU).
-bool lp_ok(int mode, const ConvGeom &g, int M) {
+bool lp_ok(int mode, const ConvGeom &g, int M, int op) {
   if (g_tune[TUNE_LP] == 1 || !(g.wlayout == 1 || g.R * g.S == 1)) return false;
   if (g_tune[TUNE_LP_FORCE_TILE] > 1) return true;  // benchmarking / tests: every shape
-  const LpPlan p = lp_plan(mode, g, M);
   const int Kc = mode == 0 ? g.Cin : g.Cout;
-  return M >= 40 && (g.R * g.S > 1 || Kc > LK) && p.kper >= 1;
+  // fp32 (e2ep_tune key 14): spatial filters with >= 64 rows and >= 64 channels per tap on
+  // maps below k_conv_gemm2's range (3x3 layers of the BEV encoder / heads: -4..-6 us per launch
+  // against k_conv_gemm; the 1x1s measured slower, profiles/r03/lp/conv_ab_fp32.txt)
+  if (op == 0) return g.R * g.S > 1 && M >= 64 && Kc >= 64;
+  return M >= 40 && (g.R * g.S > 1 || Kc > LK);
 }
 
-size_t lp_workspace(int mode, const ConvGeom &g, int M) {
-  const LpPlan p = lp_plan(mode, g, M);
+size_t lp_workspace(int mode, const ConvGeom &g, int M, int op) {
+  const LpPlan p = lp_plan(mode, g, M, op);
   return p.splits > 1 ? (size_t)p.splits * M * p.ncols * sizeof(float) : 0;
 }
 
@@ -444,8 +496,13 @@ static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, 
     if (p.wn == 2) LP_L(2, 2);
     else LP_L(2, 1);
   } else {
-    if (p.wn == 4) LP_L(1, 4);
-    else if (p.wn == 2) LP_L(1, 2);
+    if constexpr (OP != 0) {
+      if (p.wn == 4) {
+        LP_L(1, 4);
+        return;
+      }
+    }
+    if (p.wn == 2) LP_L(1, 2);
     else LP_L(1, 1);
   }
 #undef LP_L
@@ -454,7 +511,7 @@ static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, 
 int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
               float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
               hipStream_t s) {
-  const LpPlan p = lp_plan(mode, g, M);
+  const LpPlan p = lp_plan(mode, g, M, op);
   const dim3 grid(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
   float *out = dst;
   long long out_bytes = dst_bytes;
@@ -467,16 +524,16 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
     out_bytes = (long long)p.splits * M * p.ncols * 4;
   }
   const float *kb = p.splits > 1 ? nullptr : bias;  // bias / residual go to the reduction
-  if (mode == 0 && act == 0) {
-    if (op == 1) lp_tiles<0, 0, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M);
-    else lp_tiles<0, 0, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M);
-  } else if (mode == 0) {
-    if (op == 1) lp_tiles<0, 1, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M);
-    else lp_tiles<0, 1, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M);
-  } else {
-    if (op == 1) lp_tiles<1, 0, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M);
-    else lp_tiles<1, 0, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M);
-  }
+#define LP_OPS(MD, AC)                                                     \
+  do {                                                                     \
+    if (op == 1) lp_tiles<MD, AC, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M); \
+    else if (op == 2) lp_tiles<MD, AC, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M); \
+    else lp_tiles<MD, AC, 0>(p, grid, s, w, src, kb, out, out_bytes, g, M); \
+  } while (0)
+  if (mode == 0 && act == 0) LP_OPS(0, 0);
+  else if (mode == 0) LP_OPS(0, 1);
+  else LP_OPS(1, 0);
+#undef LP_OPS
   if (p.splits > 1) {
     const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
     hipLaunchKernelGGL(k_conv_lp_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
@@ -504,15 +561,18 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <int WM, int WN>
+// OP 0: the same GEMM on the exact-f32 MFMA with fp32 LDS rows (k_conv_lp's fp32 K order).
+template <int WM, int WN, int OP>
 __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout,
                                                   const float *__restrict__ x,
                                                   float *__restrict__ part, ConvGeom g,
                                                   int pix_per_split, TapList tl) {
+  typedef typename LpType<OP == 0 ? 0 : 1>::T T;
+  constexpr int LD = lld_of(OP);
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
   constexpr int NBC = BNT / 16;  // B columns per thread
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][BMT][LLD];  // As[co][pixel]
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BNT][LLD];  // Bs[column][pixel]
+  __shared__ __attribute__((aligned(16))) T As[2][BMT][LD];  // As[co][pixel]
+  __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LD];  // Bs[column][pixel]
   __shared__ int s_tap[MAXTAPS];
   if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
   __syncthreads();
@@ -580,14 +640,22 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   auto store_tiles = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
-      const float v[8] = {ra[i][0].x, ra[i][0].y, ra[i][0].z, ra[i][0].w,
-                          ra[i][1].x, ra[i][1].y, ra[i][1].z, ra[i][1].w};
-      *reinterpret_cast<bf16x8 *>(&As[buf][ar + 64 * i][8 * ao]) = cvt8<1>(v);
+      if constexpr (OP == 0) {
+        *reinterpret_cast<float4 *>(&As[buf][ar + 64 * i][8 * ao]) = ra[i][0];
+        *reinterpret_cast<float4 *>(&As[buf][ar + 64 * i][8 * ao + 4]) = ra[i][1];
+      } else {
+        const float v[8] = {ra[i][0].x, ra[i][0].y, ra[i][0].z, ra[i][0].w,
+                            ra[i][1].x, ra[i][1].y, ra[i][1].z, ra[i][1].w};
+        *reinterpret_cast<bf16x8 *>(&As[buf][ar + 64 * i][8 * ao]) = cvt8<1>(v);
+      }
     }
 #pragma unroll
     for (int j = 0; j < NBC; ++j) {
       const f32x2 f = {rb[j][0], rb[j][1]};
-      *reinterpret_cast<bf16x2 *>(&Bs[buf][bcg + 16 * j][2 * bq]) = __builtin_convertvector(f, bf16x2);
+      if constexpr (OP == 0)
+        *reinterpret_cast<f32x2 *>(&Bs[buf][bcg + 16 * j][2 * bq]) = f;
+      else
+        *reinterpret_cast<bf16x2 *>(&Bs[buf][bcg + 16 * j][2 * bq]) = __builtin_convertvector(f, bf16x2);
     }
   };
 
@@ -598,6 +666,31 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{0};
   const int li = lane & 31, lh = lane >> 5;
   auto compute = [&](int buf) {
+    if constexpr (OP == 0) {  // MFMA i: k = i (lane half 0) and 16 + i (lane half 1)
+      float a[WM][16], b[WN][16];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(&As[buf][32 * (WM * wm + i) + li][16 * lh + 4 * q]);
+          a[i][4 * q] = v[0]; a[i][4 * q + 1] = v[1]; a[i][4 * q + 2] = v[2]; a[i][4 * q + 3] = v[3];
+        }
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = *reinterpret_cast<const f32x4 *>(&Bs[buf][32 * (WN * wn + j) + li][16 * lh + 4 * q]);
+          b[j][4 * q] = v[0]; b[j][4 * q + 1] = v[1]; b[j][4 * q + 2] = v[2]; b[j][4 * q + 3] = v[3];
+        }
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < LK / 16; ++kk) {
       bf16x8 a[WM], b[WN];
@@ -665,7 +758,7 @@ static void lp_wgrad_tile(const ConvGeom &g, const TapList &tl, int &wm, int &wn
 // Few (Cout, column) pairs over many pixels (the 128x128 maps' 24 / 48-channel 1x1s, the
 // segmentation classifier) stay on k_wgrad_1x1 / k_conv_wgrad2, measured faster there.
 bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl) {
-  if (g_tune[TUNE_LP_WGRAD] == 1 || tl.n <= 0 || (g.P * g.Q) % LK != 0) return false;
+  if (tl.n <= 0 || (g.P * g.Q) % LK != 0) return false;
   return g_tune[TUNE_LP_WGRAD_TILE] > 1 || (long long)g.Cout * g.Cin * tl.n >= 2048;
 }
 
@@ -680,7 +773,7 @@ int lp_wgrad_splits(const ConvGeom &g, const TapList &tl) {
 }
 
 int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
-                    int splits, float *part, hipStream_t s) {
+                    int splits, float *part, hipStream_t s, int op) {
   int wm, wn;
   lp_wgrad_tile(g, tl, wm, wn);
   const int Ptot = g.N * g.P * g.Q;
@@ -688,14 +781,18 @@ int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const 
   per = (per + LK - 1) / LK * LK;
   const int used = (Ptot + per - 1) / per;
   const dim3 grid(cdiv(g.Cin * tl.n, 64 * wn), cdiv(g.Cout, 64 * wm), used);
-  if (wm == 2 && wn == 2)
-    hipLaunchKernelGGL((k_wgrad_lp<2, 2>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
-  else if (wm == 2)
-    hipLaunchKernelGGL((k_wgrad_lp<2, 1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
-  else if (wn == 2)
-    hipLaunchKernelGGL((k_wgrad_lp<1, 2>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
-  else
-    hipLaunchKernelGGL((k_wgrad_lp<1, 1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
+#define WL(WMV, WNV)                                                                             \
+  do {                                                                                           \
+    if (op == 1)                                                                                 \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
+    else                                                                                         \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 0>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
+  } while (0)
+  if (wm == 2 && wn == 2) WL(2, 2);
+  else if (wm == 2) WL(2, 1);
+  else if (wn == 2) WL(1, 2);
+  else WL(1, 1);
+#undef WL
   return used;
 }
 

@@ -17,7 +17,9 @@ enum Tune {
   TUNE_LP = 11,               // low-precision conv forward / data gradient: 2 = k_conv_lp, 1 = k_conv_gemm(2)
   TUNE_LP_WGRAD = 12,         // bf16 weight gradient: 2 = k_wgrad_lp, 1 = k_conv_wgrad2 / k_wgrad_1x1
   TUNE_LP_WGRAD_TILE = 13,    // benchmarking: k_wgrad_lp wave tile wm * 10 + wn (1 = automatic)
-  TUNE_N = 14
+  TUNE_LP32 = 14,             // fp32 conv forward / data gradient: 2 = k_conv_lp<OP 0> where lp_ok, 1 = conv.hip kernels
+  TUNE_LP32W = 15,            // fp32 weight gradient: 2 = k_wgrad_lp<OP 0> where lp_wgrad_ok, 1 = conv.hip kernels
+  TUNE_N = 16
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

@@ -359,3 +359,38 @@ def test_conv_lp_skip_gradient_fused(case):
     gx += gs.double()
     assert rel_l2(y.detach().cpu(), y_r) < 2e-6
     assert rel_l2(xd.grad.cpu(), gx) < 2e-6
+
+
+@pytest.mark.parametrize("tile", [1, 11, 12, 21, 22], ids=["t1", "t11", "t12", "t21", "t22"])
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_conv_lp_fp32_all_geometries(case, tile):
+    """k_conv_lp / k_wgrad_lp with exact-f32 MFMA operands (e2ep_tune keys 14 / 15 = 2), every
+    tile (keys 10 / 13), vs fp64: forward, data and weight gradients."""
+    from e2ep_amd import _lib, conv
+    N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
+    if H * W == 1 and R * S == 1:
+        pytest.skip("1x1 convs on 1x1 maps run on the skinny GEMM")
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5
+    b = torch.randn(Cout, generator=g) if has_b else None
+    xd = x.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    keys = ((14, 2), (15, 2), (10, tile), (13, tile))
+    old = [_lib.call_raw("e2ep_tune", k, v) for k, v in keys]
+    try:
+        y = conv.conv2d(xd, wd, b.to(DEV) if has_b else None, (st, st), pad, (dil, dil), act)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy.to(DEV))
+    finally:
+        for (k, _), v in zip(keys, old):
+            _lib.call_raw("e2ep_tune", k, v)
+    x64 = x.double().requires_grad_(True)
+    w64 = w.double().requires_grad_(True)
+    y64 = F.conv2d(F.pad(x64, pad), w64, b.double() if has_b else None, st, 0, dil)
+    if act:
+        y64 = torch.relu(y64)
+    y64.backward(gy.double())
+    assert rel_l2(y, y64) < 2e-6
+    assert rel_l2(xd.grad, x64.grad) < 2e-6
+    assert rel_l2(wd.grad, w64.grad) < 2e-6
