@@ -53,7 +53,7 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
 // part[split][Cout][Cin*R*S] for the fixed-order split reduction of conv.hip;
 // lp_wgrad_launch returns the slabs written.
 bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl);
-int lp_wgrad_splits(const ConvGeom &g, const TapList &tl);
+int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op);
 int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
                     int splits, float *part, hipStream_t s, int op);
 

@@ -1776,7 +1776,7 @@ int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
   if (lp_wgrad_selected()) {  // k_wgrad_lp (conv_lp.hip): C3 bf16, or fp32 when selected
     const TapList tl = live_taps(g);
-    if (lp_wgrad_ok(g, tl)) return lp_wgrad_splits(g, tl);
+    if (lp_wgrad_ok(g, tl)) return lp_wgrad_splits(g, tl, g_conv_precision == 1 ? 1 : 0);
   }
   if (wgrad1x1_ok(g)) return wgrad1x1_splits(g);
   const int nl = std::max(1, live_taps(g).n);

@@ -28,15 +28,18 @@
 
 namespace e2ep {
 
+constexpr int MAXPH_LP = 4;  // stride phases of the data gradient (sh * sw <= 4, conv.hip)
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int LK = 32;   // K per step
-constexpr int LLD = 40;  // LDS row stride in 16-bit elements (32 k + 8 pad = 80 B)
-// fp32 operands (OP 0): 32 k + 4 pad = 144 B rows (b128 reads and writes conflict-free)
-constexpr int lld_of(int op) { return op == 0 ? 36 : LLD; }
+constexpr int LK = 32;   // default K per step (k_conv_lp: channels of one tap; k_wgrad_lp: pixels)
+// LDS row stride in elements: 16-bit rows of lk k + 8 pad (32 k: 80 B, 64 k: 144 B), fp32
+// rows of 32 k + 4 pad (144 B); 20- and 36-dword strides keep the b128 reads and writes
+// bank-conflict free
+constexpr int lld_of(int op, int lk) { return op == 0 ? lk + 4 : lk + 8; }
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int OP> struct LpType;
@@ -64,7 +67,7 @@ __device__ __forceinline__ f32x16 mfma16(typename LpType<OP>::T8 a, typename LpT
 // MODE 1 (data gradient): rows m = ci, K = (tap, co), src = g [N,Cout,P,Q], dst = dx
 //   [N,M,H,W]; phase z = (py, px) (blockIdx.z / splits) as in k_conv_gemm.
 // Block tile (64 WM) x (64 WN), 2 x 2 waves of (32 WM) x (32 WN).
-template <int MODE, int ACT, int WM, int WN, int OP>
+template <int MODE, int ACT, int WM, int WN, int OP, int LKS>
 __global__ void __launch_bounds__(256) k_conv_lp(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
@@ -72,11 +75,12 @@ __global__ void __launch_bounds__(256) k_conv_lp(
   typedef typename LpType<OP>::T8 T8;
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
   constexpr int KGB = 256 / BNT;  // B k-groups (4, 2, 1)
-  constexpr int RPB = LK / KGB;   // B k rows per thread (8, 16, 32)
+  constexpr int RPB = LKS / KGB;   // B k rows per thread (8, 16, 32)
   constexpr int KGA = 256 / BMT;  // A k-groups (4, 2)
-  constexpr int RPA = LK / KGA;   // A k per thread (8, 16)
-  constexpr int LD = lld_of(OP);
-  static_assert(OP != 0 || WN <= 2, "fp32: 64 x 256 tiles would leave one block per CU");
+  constexpr int RPA = LKS / KGA;   // A k per thread (8, 16)
+  constexpr int LD = lld_of(OP, LKS);
+  static_assert(OP != 0 || (WN <= 2 && LKS == 32), "fp32: 32-deep steps, tiles up to 128 x 128");
+  static_assert(LKS == 32 || LKS == 64, "K step 32 or 64");
   __shared__ __attribute__((aligned(16))) T As[2][BMT][LD];
   __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LD];
   __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
@@ -134,10 +138,10 @@ __global__ void __launch_bounds__(256) k_conv_lp(
   __syncthreads();
   const int ntaps = s_ntaps;
   const int Kc = MODE == 0 ? g.Cin : g.Cout;  // channels summed per tap
-  const int cfull = Kc / LK, crem = Kc - cfull * LK;
+  const int cfull = Kc / LKS, crem = Kc - cfull * LKS;
   const int ntail = crem * ntaps;             // flattened (remainder channel, tap) rows
   const int kmain = ntaps * cfull;
-  const int ksteps_all = kmain + (ntail + LK - 1) / LK;
+  const int ksteps_all = kmain + (ntail + LKS - 1) / LKS;
   const int kbeg = split * kper;
   const int kend = min(ksteps_all, kbeg + kper);
   const int nk = max(0, kend - kbeg);
@@ -179,7 +183,7 @@ __global__ void __launch_bounds__(256) k_conv_lp(
     const int ks = min(ks_in, klast);
     if (ks < kmain) {  // one tap, 32 channels
       const int tap = ks / cfull;
-      const int c0 = (ks - tap * cfull) * LK;
+      const int c0 = (ks - tap * cfull) * LKS;
       const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * tapstride;
       if (MODE == 0) {
         const int base = (live && arow_ok) ? (rs + (m0 + am) * g.Cin + c0 + akg * RPA) * 4 : nrw;
@@ -207,14 +211,14 @@ __global__ void __launch_bounds__(256) k_conv_lp(
     } else {  // tail step: 32 flattened (remainder channel, tap) rows
       // a thread's rows are consecutive flattened indices: decode the first (one division),
       // then step the (channel, tap) pair
-      const int t0 = (ks - kmain) * LK;
+      const int t0 = (ks - kmain) * LKS;
       {
         const int i0 = t0 + akg * RPA;
         int cq = i0 / ntaps, t = i0 - cq * ntaps;
 #pragma unroll
         for (int j = 0; j < RPA; ++j) {
           const bool ok = live && arow_ok && i0 + j < ntail;
-          const int c = cfull * LK + cq, rs = s_trs[ok ? t : 0] * tapstride;
+          const int c = cfull * LKS + cq, rs = s_trs[ok ? t : 0] * tapstride;
           ra[j] = bload(rw, ok ? (MODE == 0 ? rs + (m0 + am) * g.Cin + c : rs + c * g.Cin + m0 + am) * 4 : OOR);
           const bool wrap = ++t == ntaps;
           t = wrap ? 0 : t;
@@ -230,7 +234,7 @@ __global__ void __launch_bounds__(256) k_conv_lp(
           const int tt = in ? t : 0;
           const int iy = ybase + s_tdy[tt], ix = xbase + s_tdx[tt];
           const bool ok = live && col_ok && in && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
-          rb[r] = bload(rx, ok ? (simg + (cfull * LK + cq) * HWs + iy * Ws + ix) * 4 : OOR);
+          rb[r] = bload(rx, ok ? (simg + (cfull * LKS + cq) * HWs + iy * Ws + ix) * 4 : OOR);
           const bool wrap = ++t == ntaps;
           t = wrap ? 0 : t;
           cq += wrap ? 1 : 0;
@@ -295,7 +299,7 @@ __global__ void __launch_bounds__(256) k_conv_lp(
       return;
     }
 #pragma unroll
-    for (int kk = 0; kk < LK / 16; ++kk) {
+    for (int kk = 0; kk < LKS / 16; ++kk) {
       T8 a[WM], b[WN];
 #pragma unroll
       for (int i = 0; i < WM; ++i)
@@ -391,17 +395,16 @@ __global__ void __launch_bounds__(256) k_conv_lp_reduce(
 
 // ---- launch plan ---------------------------------------------------------------------------
 struct LpPlan {
-  int wm, wn, splits, kper, nph;
+  int wm, wn, lk, splits, kper, nph;
   long long ncols;  // columns of the largest phase
 };
 
 static LpPlan lp_plan(int mode, const ConvGeom &g, int M, int op) {
   LpPlan p;
   const int Kc = mode == 0 ? g.Cin : g.Cout;
-  const int cfull = Kc / LK, crem = Kc - cfull * LK;
   p.nph = mode ? g.sh * g.sw : 1;
   p.ncols = 0;
-  int kmax = 0;
+  int taps_ph[MAXPH_LP];
   for (int z = 0; z < p.nph; ++z) {
     int taps = 0;
     long long cols;
@@ -428,7 +431,7 @@ static LpPlan lp_plan(int mode, const ConvGeom &g, int M, int op) {
       taps = ty * tx;
     }
     p.ncols = std::max(p.ncols, cols);
-    kmax = std::max(kmax, taps * cfull + cdiv((long long)crem * taps, LK));
+    taps_ph[z] = taps;
   }
   // rows: 128-row tiles when they pad M by at most 25 % (M = 112, 336, 672, 960 ...)
   const bool tall = cdiv(M, 128) * 128LL * 4 <= 5LL * M;
@@ -454,6 +457,16 @@ static LpPlan lp_plan(int mode, const ConvGeom &g, int M, int op) {
       p.wn = fwn;
     }
   }
+  // K-step depth: 32 (64-deep steps for the 16-bit operands, half the barriers and twice the
+  // loads in flight per step, measured equal: 6.80 vs 6.79 ms for the bf16 conv set,
+  // profiles/r03/lp/conv_ab_bf16_lk.txt; e2ep_tune key 16 forces 32 / 64 for A/B)
+  p.lk = 32;
+  if (op != 0 && (g_tune[TUNE_LP_LK] == 32 || (g_tune[TUNE_LP_LK] == 64 && p.wn <= 2)))
+    p.lk = g_tune[TUNE_LP_LK];
+  const int cfull = Kc / p.lk, crem = Kc - cfull * p.lk;
+  int kmax = 0;
+  for (int z = 0; z < p.nph; ++z)
+    kmax = std::max(kmax, taps_ph[z] * cfull + cdiv((long long)crem * taps_ph[z], p.lk));
   const long long blocks = cdiv(p.ncols, 64 * p.wn) * cdiv(M, 64 * p.wm) * p.nph;
   p.splits = 1;
   if (blocks < 512 && p.nph == 1) {  // K split toward ~1024 workgroups, >= 4 steps each
@@ -489,9 +502,15 @@ size_t lp_workspace(int mode, const ConvGeom &g, int M, int op) {
 template <int MODE, int ACT, int OP>
 static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, const float *src,
                      const float *bias, float *out, long long out_bytes, const ConvGeom &g, int M) {
-#define LP_L(WMV, WNV)                                                                          \
-  hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP>), grid, dim3(256), 0, s, w, src, bias, \
-                     out, out_bytes, g, M, p.splits, p.kper)
+#define LP_L(WMV, WNV)                                                                              \
+  do {                                                                                              \
+    if (OP != 0 && WNV <= 2 && p.lk == 64)                                                          \
+      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32>),     \
+                         grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits, p.kper); \
+    else                                                                                            \
+      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32>), grid, dim3(256), 0, s, w, src,   \
+                         bias, out, out_bytes, g, M, p.splits, p.kper);                             \
+  } while (0)
   if (p.wm == 2) {
     if (p.wn == 2) LP_L(2, 2);
     else LP_L(2, 1);
@@ -562,15 +581,20 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // OP 0: the same GEMM on the exact-f32 MFMA with fp32 LDS rows (k_conv_lp's fp32 K order).
-template <int WM, int WN, int OP>
+template <int WM, int WN, int OP, int LKS>
 __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout,
                                                   const float *__restrict__ x,
                                                   float *__restrict__ part, ConvGeom g,
                                                   int pix_per_split, TapList tl) {
   typedef typename LpType<OP == 0 ? 0 : 1>::T T;
-  constexpr int LD = lld_of(OP);
+  constexpr int LD = lld_of(OP, LKS);
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
-  constexpr int NBC = BNT / 16;  // B columns per thread
+  static_assert(OP != 0 || LKS == 32, "fp32: 32-pixel steps");
+  constexpr int OPR = LKS / 8;             // A pixel octets per row
+  constexpr int NA8 = BMT * OPR / 256;     // A octets per thread
+  constexpr int PP = LKS / 2;              // B pixel pairs per step
+  constexpr int CG = 256 / PP;             // B column groups
+  constexpr int NBC = BNT / CG;            // B columns per thread
   __shared__ __attribute__((aligned(16))) T As[2][BMT][LD];  // As[co][pixel]
   __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LD];  // Bs[column][pixel]
   __shared__ int s_tap[MAXTAPS];
@@ -587,19 +611,18 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   const int split = blockIdx.z;
   const int PQ = g.P * g.Q;
   const int Ptot = g.N * PQ;
-  const int pbeg = split * pix_per_split;  // a multiple of LK
+  const int pbeg = split * pix_per_split;  // a multiple of LKS
   const int pend = min(Ptot, pbeg + pix_per_split);
-  const int nk = max(0, (pend - pbeg) / LK);
+  const int nk = max(0, (pend - pbeg) / LKS);
   const int HW = g.H * g.W;
 
-  // A: thread = (co row tid/4 (+64 i), pixel octet tid%4)
-  const int ar = tid >> 2, ao = tid & 3;
-  // B: thread = (pixel pair tid%16, column group tid/16): columns bcg + 16 j
-  const int bq = tid & 15, bcg = tid >> 4;
+  // A: octet o = tid + 256 i -> (co row o / OPR, pixel octet o % OPR)
+  // B: thread = (pixel pair tid % PP, column group tid / PP): columns bcg + CG j
+  const int bq = tid % PP, bcg = tid / PP;
   int cconst[NBC], cdy[NBC], cdx[NBC];
 #pragma unroll
   for (int j = 0; j < NBC; ++j) {
-    const int col = n0 + bcg + 16 * j;
+    const int col = n0 + bcg + CG * j;
     const int cc = col < Kl ? col : 0;
     const int ci = cc / tl.n, tap = s_tap[cc - ci * tl.n];
     const int r = tap / g.S, sx = tap - r * g.S;
@@ -612,14 +635,15 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
   const int nrx = (int)min(4LL * g.N * g.Cin * HW, 0x7fffffffLL);
 
-  float4 ra[WM][2];
+  float4 ra[NA8][2];
   float rb[NBC][2];
   auto load_tiles = [&](int ks) {
-    const int p0 = pbeg + min(ks, nk - 1) * LK;  // past the range: re-read, never stored
-    const int im = p0 / PQ, od0 = p0 - im * PQ;   // block-uniform
+    const int p0 = pbeg + min(ks, nk - 1) * LKS;  // past the range: re-read, never stored
+    const int im = p0 / PQ, od0 = p0 - im * PQ;    // block-uniform
 #pragma unroll
-    for (int i = 0; i < WM; ++i) {
-      const int co = m0 + ar + 64 * i;
+    for (int i = 0; i < NA8; ++i) {
+      const int o = tid + 256 * i, ar = o / OPR, ao = o % OPR;
+      const int co = m0 + ar;
       const int base = co < g.Cout ? ((im * g.Cout + co) * PQ + od0 + 8 * ao) * 4 : OOR;
       ra[i][0] = bload4(rg, base);
       ra[i][1] = bload4(rg, base + 16);
@@ -639,23 +663,24 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   };
   auto store_tiles = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < WM; ++i) {
+    for (int i = 0; i < NA8; ++i) {
+      const int o = tid + 256 * i, ar = o / OPR, ao = o % OPR;
       if constexpr (OP == 0) {
-        *reinterpret_cast<float4 *>(&As[buf][ar + 64 * i][8 * ao]) = ra[i][0];
-        *reinterpret_cast<float4 *>(&As[buf][ar + 64 * i][8 * ao + 4]) = ra[i][1];
+        *reinterpret_cast<float4 *>(&As[buf][ar][8 * ao]) = ra[i][0];
+        *reinterpret_cast<float4 *>(&As[buf][ar][8 * ao + 4]) = ra[i][1];
       } else {
         const float v[8] = {ra[i][0].x, ra[i][0].y, ra[i][0].z, ra[i][0].w,
                             ra[i][1].x, ra[i][1].y, ra[i][1].z, ra[i][1].w};
-        *reinterpret_cast<bf16x8 *>(&As[buf][ar + 64 * i][8 * ao]) = cvt8<1>(v);
+        *reinterpret_cast<bf16x8 *>(&As[buf][ar][8 * ao]) = cvt8<1>(v);
       }
     }
 #pragma unroll
     for (int j = 0; j < NBC; ++j) {
       const f32x2 f = {rb[j][0], rb[j][1]};
       if constexpr (OP == 0)
-        *reinterpret_cast<f32x2 *>(&Bs[buf][bcg + 16 * j][2 * bq]) = f;
+        *reinterpret_cast<f32x2 *>(&Bs[buf][bcg + CG * j][2 * bq]) = f;
       else
-        *reinterpret_cast<bf16x2 *>(&Bs[buf][bcg + 16 * j][2 * bq]) = __builtin_convertvector(f, bf16x2);
+        *reinterpret_cast<bf16x2 *>(&Bs[buf][bcg + CG * j][2 * bq]) = __builtin_convertvector(f, bf16x2);
     }
   };
 
@@ -692,7 +717,7 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
       return;
     }
 #pragma unroll
-    for (int kk = 0; kk < LK / 16; ++kk) {
+    for (int kk = 0; kk < LKS / 16; ++kk) {
       bf16x8 a[WM], b[WN];
 #pragma unroll
       for (int i = 0; i < WM; ++i)
@@ -738,12 +763,21 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   }
 }
 
+// pixels per K-step of k_wgrad_lp: 32 (bf16 64-pixel steps measured equal, 128 slower: register
+// pressure; e2ep_tune key 17 forces 32 / 64 / 128 for A/B), fp32 32
+static int lp_wgrad_lk(const ConvGeom &g, int op) {
+  const int pq = g.P * g.Q, f = g_tune[TUNE_LPW_LK];
+  if (op == 0) return 32;
+  if ((f == 32 || f == 64 || f == 128) && pq % f == 0) return f;
+  return 32;
+}
+
 static void lp_wgrad_tile(const ConvGeom &g, const TapList &tl, int &wm, int &wn) {
   const int Kl = g.Cin * tl.n;
   wm = cdiv(g.Cout, 128) * 128LL * 4 <= 5LL * g.Cout ? 2 : 1;
   wn = cdiv(Kl, 128) * 128LL * 4 <= 5LL * Kl ? 2 : 1;
   // few pixels (slabs of >= 8 steps): smaller tiles until the grid has >= 256 workgroups
-  const long long cap = std::max(1LL, (long long)g.N * g.P * g.Q / (8 * LK));
+  const long long cap = std::max(1LL, (long long)g.N * g.P * g.Q / 256);
   while (wm * wn > 1 && (long long)cdiv(Kl, 64 * wn) * cdiv(g.Cout, 64 * wm) * std::min(cap, 256LL) < 256) {
     if (wm >= wn) wm = 1;
     else wn = 1;
@@ -762,13 +796,14 @@ bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl) {
   return g_tune[TUNE_LP_WGRAD_TILE] > 1 || (long long)g.Cout * g.Cin * tl.n >= 2048;
 }
 
-int lp_wgrad_splits(const ConvGeom &g, const TapList &tl) {
+int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op) {
   int wm, wn;
   lp_wgrad_tile(g, tl, wm, wn);
+  const int lk = lp_wgrad_lk(g, op);
   const long long tiles = (long long)cdiv(g.Cin * tl.n, 64 * wn) * cdiv(g.Cout, 64 * wm);
   const long long pix = (long long)g.N * g.P * g.Q;
   long long s = (1024 + tiles - 1) / tiles;  // toward ~1024 workgroups
-  s = std::min(s, std::max(1LL, pix / (8 * LK)));  // >= 8 steps per slab
+  s = std::min(s, std::max(1LL, pix / (std::max(256, 4 * lk))));  // >= 256 pixels per slab
   return (int)std::max(1LL, std::min(s, 256LL));
 }
 
@@ -776,17 +811,22 @@ int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const 
                     int splits, float *part, hipStream_t s, int op) {
   int wm, wn;
   lp_wgrad_tile(g, tl, wm, wn);
+  const int lk = lp_wgrad_lk(g, op);
   const int Ptot = g.N * g.P * g.Q;
   int per = (Ptot + splits - 1) / splits;
-  per = (per + LK - 1) / LK * LK;
+  per = (per + lk - 1) / lk * lk;
   const int used = (Ptot + per - 1) / per;
   const dim3 grid(cdiv(g.Cin * tl.n, 64 * wn), cdiv(g.Cout, 64 * wm), used);
 #define WL(WMV, WNV)                                                                             \
   do {                                                                                           \
-    if (op == 1)                                                                                 \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
+    if (op != 1)                                                                                 \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 0, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
+    else if (lk == 128)                                                                          \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 128>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
+    else if (lk == 64)                                                                           \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
     else                                                                                         \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 0>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
   } while (0)
   if (wm == 2 && wn == 2) WL(2, 2);
   else if (wm == 2) WL(2, 1);

@@ -19,7 +19,9 @@ enum Tune {
   TUNE_LP_WGRAD_TILE = 13,    // benchmarking: k_wgrad_lp wave tile wm * 10 + wn (1 = automatic)
   TUNE_LP32 = 14,             // fp32 conv forward / data gradient: 2 = k_conv_lp<OP 0> where lp_ok, 1 = conv.hip kernels
   TUNE_LP32W = 15,            // fp32 weight gradient: 2 = k_wgrad_lp<OP 0> where lp_wgrad_ok, 1 = conv.hip kernels
-  TUNE_N = 16
+  TUNE_LP_LK = 16,            // k_conv_lp K step (16-bit operands): 32 / 64 forced, 1 = automatic
+  TUNE_LPW_LK = 17,           // k_wgrad_lp pixels per step (bf16): 32 / 64 / 128 forced, 1 = automatic
+  TUNE_N = 18
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

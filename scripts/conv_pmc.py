@@ -1,7 +1,8 @@
 """Diagnostics: run one conv shape's forward / data-gradient / weight-gradient kernels
 repeatedly (for rocprofv3 --pmc passes and kernel-trace timing).
 
-    python scripts/conv_pmc.py <shape> [fwd|dgrad|wgrad|all] [reps]"""
+    python scripts/conv_pmc.py <shape> [fwd|dgrad|wgrad|all] [reps]
+(E2EP_PRECISION=bf16 for the C3 kernels)"""
 import os
 import sys
 
@@ -18,7 +19,8 @@ SHAPES = {"stem": (8, 65, 256, 256, 64, 7, 7, 128, 128, 2, 2, 3, 3, 1, 1),
           "proj960": (32, 960, 16, 16, 160, 1, 1, 16, 16, 1, 1, 0, 0, 1, 1),
           "exp160": (32, 160, 16, 16, 960, 1, 1, 16, 16, 1, 1, 0, 0, 1, 1),
           "bev256": (8, 256, 16, 16, 256, 3, 3, 16, 16, 1, 1, 1, 1, 1, 1),
-          "up216": (32, 216, 32, 32, 64, 3, 3, 32, 32, 1, 1, 1, 1, 1, 1)}
+          "up216": (32, 216, 32, 32, 64, 3, 3, 32, 32, 1, 1, 1, 1, 1, 1),
+          "exp112": (32, 112, 16, 16, 672, 1, 1, 16, 16, 1, 1, 0, 0, 1, 1)}
 
 
 def main():
@@ -26,6 +28,9 @@ def main():
     kind = sys.argv[2] if len(sys.argv) > 2 else "all"
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     d = SHAPES[which]
+    if os.environ.get("E2EP_PRECISION"):  # fp32 (default) / bf16 / fp16 operands
+        from e2ep_amd import precision
+        precision.set(os.environ["E2EP_PRECISION"])
     if os.environ.get("E2EP_GEMM_VARIANT"):
         from e2ep_amd import _lib
         _lib.call_raw("e2ep_conv_gemm_variant", int(os.environ["E2EP_GEMM_VARIANT"]))

@@ -281,9 +281,12 @@ def test_side_stream_weight_gradient_equals_serial():
 LP_TILES = [1, 11, 12, 14, 21, 22]
 
 
+@pytest.mark.parametrize("lk", [1, 32, 128], ids=["lkauto", "lk32", "lkw128"])
 @pytest.mark.parametrize("tile", LP_TILES, ids=[f"t{t}" for t in LP_TILES])
 @pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
-def test_conv_lp_kernel_all_geometries(case, tile):
+def test_conv_lp_kernel_all_geometries(case, tile, lk):
+    """lk: K-step depth (e2ep_tune key 16 for k_conv_lp: automatic = 64 channels for 16-bit
+    operands, or 32; key 17 for k_wgrad_lp: automatic = 64 pixels, 32 or 128)."""
     from e2ep_amd import _lib, conv, precision
     N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
     mode, dt = ("fp16", torch.float16) if tile == 12 else ("bf16", torch.bfloat16)
@@ -299,13 +302,15 @@ def test_conv_lp_kernel_all_geometries(case, tile):
     old_lp = _lib.call_raw("e2ep_tune", 11, 2)
     old_wt = _lib.call_raw("e2ep_tune", 13, tile if tile in (11, 12, 21, 22) else 1)
     old_wlp = _lib.call_raw("e2ep_tune", 12, 2)
+    old_lk = _lib.call_raw("e2ep_tune", 16, 32 if lk == 32 else 1)
+    old_wlk = _lib.call_raw("e2ep_tune", 17, lk)
     try:
         with precision.use(mode):
             y = conv.conv2d(xd, wd, b.to(DEV) if has_b else None, (st, st), pad, (dil, dil), act)
             gy = torch.randn(y.shape, generator=g)
             y.backward(gy.to(DEV))
     finally:
-        for k, v in ((10, old_t), (11, old_lp), (13, old_wt), (12, old_wlp)):
+        for k, v in ((10, old_t), (11, old_lp), (13, old_wt), (12, old_wlp), (16, old_lk), (17, old_wlk)):
             _lib.call_raw("e2ep_tune", k, v)
     r = lambda t: t.to(dt).double()  # noqa: E731
     xr = r(x).requires_grad_(True)
