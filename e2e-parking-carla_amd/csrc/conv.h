@@ -13,7 +13,28 @@ struct ConvGeom {
   int P, Q;         // output spatial
   int sh, sw, ph, pw, dh, dw;
   int wlayout;      // 0: [Cout][Cin][R*S] (PyTorch), 1: [R*S][Cout][Cin] (tap-major)
+  int korder;       // forward / data-gradient K order: 0 tap-outer, 1 channel-chunk-outer
+  int xcd;          // conv_lp.hip kernels: 1 = XCD-contiguous block order (xcd_block)
 };
+
+// XCD-contiguous logical block index: hardware block i runs on XCD i % 8 (a placement used for
+// speed only, never for correctness); logical = the i-th block of that XCD's contiguous share
+// of the grid, so neighbouring tiles (shared input rows, shared gradient rows) meet in one XCD's
+// L2.  A bijection for any grid size.
+__device__ __forceinline__ void xcd_block(bool on, int &bx, int &by, int &bz) {
+  bx = blockIdx.x;
+  by = blockIdx.y;
+  bz = blockIdx.z;
+  if (!on) return;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int total = gx * gy * gridDim.z;
+  const int i = bx + gx * (by + gy * bz);
+  const int q = total >> 3, r = total & 7, x = i & 7, j = i >> 3;
+  const int L = x * q + min(x, r) + j;
+  bx = L % gx;
+  by = (L / gx) % gy;
+  bz = L / (gx * gy);
+}
 
 __host__ __device__ __forceinline__ int floordiv(int a, int b) {
   return a >= 0 ? a / b : -((-a + b - 1) / b);

@@ -184,8 +184,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   auto load_tiles = [&](int ks_in, float(&ra)[NA], float(&rb)[BPER]) {
     const bool live = ks_in <= klast;                 // uniform
     const int ks = min(ks_in, klast);
-    const int tap = ks / csteps;                      // uniform
-    const int c0 = (ks - tap * csteps) * BK;
+    const int tap = g.korder ? ks % ntaps : ks / csteps;  // uniform
+    const int c0 = (g.korder ? ks / ntaps : ks - tap * csteps) * BK;
     const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * a_tstride;
     if (MODE == 0) {
       const int c = c0 + ac;
@@ -494,8 +494,8 @@ __global__ void __launch_bounds__(256) k_conv_gemm2(
     const bool live = ks_in <= klast;
     const int ks = min(ks_in, klast);
     if (ks < kmain) {                                  // full step: one tap, 16 channels
-      const int tap = ks / cfull;
-      const int c0 = (ks - tap * cfull) * BK;
+      const int tap = g.korder ? ks % ntaps : ks / cfull;
+      const int c0 = (g.korder ? ks / ntaps : ks - tap * cfull) * BK;
       const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * tapstride;
       if (MODE == 0) {
         const int c = c0 + 4 * akq;
@@ -1372,6 +1372,8 @@ static ConvGeom make_geom(const int *d) {
   g.Cout = d[4]; g.R = d[5]; g.S = d[6]; g.P = d[7]; g.Q = d[8];
   g.sh = d[9]; g.sw = d[10]; g.ph = d[11]; g.pw = d[12]; g.dh = d[13]; g.dw = d[14];
   g.wlayout = 0;
+  g.korder = 0;  // set by korder_of() at launch
+  g.xcd = g_tune[TUNE_XCD] == 2;
   return g;
 }
 
@@ -1593,9 +1595,24 @@ static bool lp_wgrad_selected() {
   return g_tune[TUNE_LP32W] == 2;
 }
 
+// K order of the forward / data-gradient GEMMs (e2ep_tune key 18; 1 = automatic): channel
+// chunk outer and taps inner for 16-bit operands (a block reads the same input rows for every
+// tap of a chunk while they are cache resident: bf16 BEV stem forward 416 -> 287 us, data
+// gradient 230 -> 160 us, profiles/r03/lp/korder_ab_bf16.txt), tap outer for fp32 (MFMA-bound
+// there: the channel-outer order measured 1 % slower); 2 forces channel outer, 3 tap outer
+static int korder_of() {
+  const int t = g_tune[TUNE_KORDER];
+  if (t == 2) return 1;
+  if (t == 3) return 0;
+  return g_conv_precision != 0 ? 1 : 0;
+}
+
 static int launch_gemm(int mode, int act, const float *w, const float *src, const float *bias,
-                       float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
+                       float *dst, long long dst_bytes, const ConvGeom &g0, int M, void *workspace,
                        hipStream_t s) {
+  ConvGeom g = g0;
+  g.korder = korder_of();
+  g.xcd = g_tune[TUNE_XCD] == 2;
   if (g_conv_precision != 0 && lp_ok(mode, g, M, g_conv_precision))
     return lp_launch(mode, act, g_conv_precision, w, src, bias, dst, dst_bytes, g, M, workspace, s);
   if (conv1x1_gemm_ok(mode, g))

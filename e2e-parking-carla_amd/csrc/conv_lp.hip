@@ -89,8 +89,10 @@ __global__ void __launch_bounds__(256) k_conv_lp(
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.y * BMT, n0 = blockIdx.x * BNT;
-  const int split = blockIdx.z % splits, z = blockIdx.z / splits;
+  int bx, by, bz;
+  xcd_block(g.xcd != 0, bx, by, bz);
+  const int m0 = by * BMT, n0 = bx * BNT;
+  const int split = bz % splits, z = bz / splits;
 
   int py = 0, px = 0, Hc, Wc;
   if (MODE == 0) {
@@ -182,8 +184,8 @@ __global__ void __launch_bounds__(256) k_conv_lp(
     const bool live = ks_in <= klast;
     const int ks = min(ks_in, klast);
     if (ks < kmain) {  // one tap, 32 channels
-      const int tap = ks / cfull;
-      const int c0 = (ks - tap * cfull) * LKS;
+      const int tap = g.korder ? ks % ntaps : ks / cfull;
+      const int c0 = (g.korder ? ks / ntaps : ks - tap * cfull) * LKS;
       const int dy = s_tdy[tap], dx = s_tdx[tap], rs = s_trs[tap] * tapstride;
       if (MODE == 0) {
         const int base = (live && arow_ok) ? (rs + (m0 + am) * g.Cin + c0 + akg * RPA) * 4 : nrw;
@@ -607,8 +609,10 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   const int RS = g.R * g.S;
   const int Kw = g.Cin * RS;    // columns of dW (ci-major, tap-minor)
   const int Kl = g.Cin * tl.n;  // live columns (ci, live tap index)
-  const int n0 = blockIdx.x * BNT, m0 = blockIdx.y * BMT;
-  const int split = blockIdx.z;
+  int bx, by, bz;
+  xcd_block(g.xcd != 0, bx, by, bz);
+  const int n0 = bx * BNT, m0 = by * BMT;
+  const int split = bz;
   const int PQ = g.P * g.Q;
   const int Ptot = g.N * PQ;
   const int pbeg = split * pix_per_split;  // a multiple of LKS

@@ -12,7 +12,7 @@ mkdir -p "$O"
 for i in $(seq 1 "$REP"); do
   for v in "$@"; do
     log="$O/bench_${VAR}_${v//,/_}_$i.log"
-    env "$VAR=$v" timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary > "$log" 2>&1 || exit 1
+    env "$VAR=$v" timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary $BENCH_ARGS > "$log" 2>&1 || exit 1
     echo "$VAR=$v run $i: $(grep -o '"ms_per_step": [0-9.]*' "$log" | head -1)"
   done
 done
