@@ -30,9 +30,12 @@ class ControlPredict(nn.Module):
     def create_mask(self, tgt):
         """Causal float mask (0 on/below the diagonal, -inf above) + PAD key mask."""
         L = tgt.shape[1]
-        causal = torch.full((L, L), float("-inf"), device=tgt.device).triu(1)
-        self._causal_mask = causal
-        return causal, tgt == self.pad_idx
+        # built once per (length, device): the fused attention takes causality as a flag, so
+        # the tensor only identifies the mask (two kernel launches per step saved)
+        if getattr(self, "_causal_key", None) != (L, tgt.device):
+            self._causal_mask = torch.full((L, L), float("-inf"), device=tgt.device).triu(1)
+            self._causal_key = (L, tgt.device)
+        return self._causal_mask, tgt == self.pad_idx
 
     def decoder(self, encoder_out, tgt_embedding, tgt_mask, tgt_padding_mask):
         # A mask made by create_mask is known to be causal: saying so skips torch's
