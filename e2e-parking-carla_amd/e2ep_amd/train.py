@@ -185,7 +185,10 @@ class TrainStep:
         # hook-driven bucket all-reduce overlapping backward: eager steps with RCCL, and host
         # tensors (gloo on CPU); never inside a captured graph (module docstring)
         self._bucket_mb = bucket_mb
-        self.overlap = bool(self.ddp and overlap and not graph and
+        # overlap="captured" (diagnostics only, scripts/diag_capture_hooks.py): the hook-driven
+        # buckets inside the captured backward, the round-2 design that replayed wrong gradients
+        captured_hooks = overlap == "captured"
+        self.overlap = bool(self.ddp and overlap and (not graph or captured_hooks) and
                             (self.backend == "nccl" or not self.flat_grad.is_cuda))
         self.buckets = (GradBuckets(self.params, self.opt, self.flat_grad, bucket_mb)
                         if self.overlap else None)
@@ -197,7 +200,7 @@ class TrainStep:
         self.loss = None
         self.g_bwd = self.g_gather = self.g_opt = None
         # segmented backward (graph mode, RCCL): stage graphs, their gathers, bucket ranges
-        self.segmented = bool(self.ddp and graph and self.backend == "nccl")
+        self.segmented = bool(self.ddp and graph and self.backend == "nccl" and not captured_hooks)
         self.g_s1 = self.g_s1g = self.g_s2 = self.g_s2g = None
         self.seg_buckets = None  # ([stage-1 (lo, hi)], [stage-2 (lo, hi)]) of the flat buffer
         self._rig = _rig_key(batch)
