@@ -39,11 +39,13 @@ constexpr float LOG2E = 1.4426950408889634f;
 #define E2EP_ATT_KG 4
 #endif
 constexpr int FWD_KG = E2EP_ATT_KG;  // keys per online-softmax rescale in the forward
-#ifndef E2EP_ATT_LONG_LANES
-#define E2EP_ATT_LONG_LANES 1
-#endif
-// lanes per query (forward, dq) / per key (dk, dv) for sequences longer than 16 (encoder)
-constexpr int ATT_LONG_LANES = E2EP_ATT_LONG_LANES;
+// lanes per query (forward, dq) / per key (dk, dv) for sequences longer than 16 (the encoder's
+// 256): e2ep_tune key 20 (1 = automatic = 1, or 2 / 4 for A/B; more lanes per query = smaller
+// query tiles, more workgroups)
+static int att_lanes() {
+  const int t = g_tune[TUNE_ATT_LANES];
+  return t == 2 || t == 4 ? t : 1;
+}
 
 // 2^x on the hardware v_exp_f32 (arguments here are <= 0 or -inf; tiny results flush to 0)
 __device__ __forceinline__ float att_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -532,9 +534,9 @@ int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, 
   hipLaunchKernelGGL((k_attn_fwd<DHP, LPQ>), dim3(cdiv(Sq, 64 / LPQ), B * H), blk, 0, st, q, k, v, \
                      key_pad, seed, a, o, lse)
   if (dh <= 44) {
-    if (Sq <= 16) E2EP_ATT_FWD(44, 4); else E2EP_ATT_FWD(44, ATT_LONG_LANES);
+    if (Sq <= 16 || att_lanes() == 4) E2EP_ATT_FWD(44, 4); else if (att_lanes() == 2) E2EP_ATT_FWD(44, 2); else E2EP_ATT_FWD(44, 1);
   } else {
-    if (Sq <= 16) E2EP_ATT_FWD(64, 4); else E2EP_ATT_FWD(64, ATT_LONG_LANES);
+    if (Sq <= 16 || att_lanes() == 4) E2EP_ATT_FWD(64, 4); else if (att_lanes() == 2) E2EP_ATT_FWD(64, 2); else E2EP_ATT_FWD(64, 1);
   }
 #undef E2EP_ATT_FWD
   return launch_status("e2ep_attn_fwd");
@@ -572,16 +574,16 @@ int e2ep_attn_bwd_part(const float *q, const float *k, const float *v, const flo
   float *Dq = part == 2 ? nullptr : D;  // dq pass alone: D is read by the other pass, not rewritten
   if (part != 3) {
     if (dh <= 44) {
-      if (Sq <= 16) E2EP_ATT_BQ(44, 4, Dq); else E2EP_ATT_BQ(44, ATT_LONG_LANES, Dq);
+      if (Sq <= 16 || att_lanes() == 4) E2EP_ATT_BQ(44, 4, Dq); else if (att_lanes() == 2) E2EP_ATT_BQ(44, 2, Dq); else E2EP_ATT_BQ(44, 1, Dq);
     } else {
-      if (Sq <= 16) E2EP_ATT_BQ(64, 4, Dq); else E2EP_ATT_BQ(64, ATT_LONG_LANES, Dq);
+      if (Sq <= 16 || att_lanes() == 4) E2EP_ATT_BQ(64, 4, Dq); else if (att_lanes() == 2) E2EP_ATT_BQ(64, 2, Dq); else E2EP_ATT_BQ(64, 1, Dq);
     }
   }
   if (part != 2) {
     if (dh <= 44) {
-      if (Sk <= 16) E2EP_ATT_BKV(44, 4); else E2EP_ATT_BKV(44, ATT_LONG_LANES);
+      if (Sk <= 16 || att_lanes() == 4) E2EP_ATT_BKV(44, 4); else if (att_lanes() == 2) E2EP_ATT_BKV(44, 2); else E2EP_ATT_BKV(44, 1);
     } else {
-      if (Sk <= 16) E2EP_ATT_BKV(64, 4); else E2EP_ATT_BKV(64, ATT_LONG_LANES);
+      if (Sk <= 16 || att_lanes() == 4) E2EP_ATT_BKV(64, 4); else if (att_lanes() == 2) E2EP_ATT_BKV(64, 2); else E2EP_ATT_BKV(64, 1);
     }
   }
 #undef E2EP_ATT_BQ

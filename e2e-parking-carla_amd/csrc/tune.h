@@ -23,7 +23,8 @@ enum Tune {
   TUNE_LPW_LK = 17,           // k_wgrad_lp pixels per step (bf16): 32 / 64 / 128 forced, 1 = automatic
   TUNE_KORDER = 18,           // conv forward / data-gradient K order: 1 = automatic, 2 = channel chunk outer, 3 = tap outer
   TUNE_XCD = 19,              // conv_lp.hip kernels: 2 = XCD-contiguous block order, 1 = hardware order
-  TUNE_N = 20
+  TUNE_ATT_LANES = 20,        // attention lanes per query / key for long sequences: 1 (automatic), 2, 4
+  TUNE_N = 21
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

@@ -542,7 +542,18 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * workgroups (768), 5 1x1 weight-gradient target workgroups (1024), 6 conv forward /
  * data-gradient grids of at least this many wide (128 / 256-column) tiles use them (512),
  * 7 k_conv_gemm block tile forced to bm * 1000 + bnt (64064, 64128, 32128, 32256; 1 =
- * automatic), 8 k_conv_gemm K splits forced to value - 1 (1 = automatic).
+ * automatic), 8 k_conv_gemm K splits forced to value - 1 (1 = automatic), 9 spatial
+ * weight-gradient kernel (2 = k_conv_wgrad2 where it applies, 1 = k_conv_wgrad), 10 k_conv_lp
+ * wave tile forced to wm * 10 + wn (1 = automatic), 11 16-bit conv forward / data gradient on
+ * k_conv_lp (2) or the fp32-era kernels with rounded operands (1), 12 bf16 weight gradient on
+ * k_wgrad_lp (2) or k_conv_wgrad2 / k_wgrad_1x1 (1), 13 k_wgrad_lp tile forced (wm * 10 + wn;
+ * 1 = automatic), 14 fp32 3x3 layers on the fp32 k_conv_lp tile (2) or not (1), 15 fp32 weight
+ * gradient on k_wgrad_lp (2) or not (1, default), 16 k_conv_lp K step (32 / 64; 1 = automatic
+ * = 32), 17 k_wgrad_lp pixels per step (32 / 64 / 128; 1 = automatic = 32), 18 forward /
+ * data-gradient K order (1 = automatic: channel chunk outer for 16-bit operands, tap outer for
+ * fp32; 2 channel outer; 3 tap outer), 19 XCD-contiguous block order of the conv_lp.hip
+ * kernels (2 = on, 1 = off, default), 20 attention lanes per query / key for sequences longer
+ * than 16 (1 = automatic, 2, 4).
  * For A/B timing.
  * Contract for every plan override and tunable above (e2ep_conv_split_params,
  * e2ep_gemm_force, e2ep_gemm_split_min, e2ep_bn_small*, e2ep_tune): a launch recomputes its
