@@ -27,6 +27,7 @@
 // Dropout: keep(b*h, i, j) = hash(seed, (bh*Sq + i)*Sk + j) >= p, scaled by 1/(1-p); the
 // seed is read from device memory (drawn by the caller each call, graph-capturable), so the
 // backward regenerates the same mask without storing it.
+#include "attn.h"
 #include "common.h"
 #include "dropout.h"
 
@@ -75,12 +76,6 @@ __device__ __forceinline__ void axpy_lds(float (&acc)[DHP], float a, const float
   }
 }
 
-struct AttnDims {
-  int B, H, Sq, Sk, dh;
-  int q_ss, q_sb, kv_ss, kv_sb, o_ss, o_sb;  // element strides (sequence, batch)
-  float scale, p;
-  int causal;
-};
 
 // stage rows [0, n) of a head's (S, B, E)-strided matrix into LDS as [n][DHP] (zero padded).
 // Loads go out STAGE_BATCH per thread before any LDS store (branch-free buffer loads; out of
@@ -528,6 +523,10 @@ int e2ep_attn_fwd(const float *q, const float *k, const float *v, int B, int H, 
   if (int rc = attn_check(a, "e2ep_attn_fwd")) return rc;
   E2EP_REQUIRE(p == 0.f || seed, E2EP_EINVAL, "e2ep_attn_fwd: dropout needs a seed");
   hipStream_t st = as_stream(stream);
+  if (attn_mf_ok(a, key_pad)) {  // the fusion encoder's 256-token self-attention (attn_mf.hip)
+    attn_mf_fwd(q, k, v, seed, a, o, lse, st);
+    return launch_status("e2ep_attn_fwd");
+  }
   const dim3 blk(ATT_WAVES * 64);
   // short query sequences (the control decoder's 14 tokens): 4 lanes per query
 #define E2EP_ATT_FWD(DHP, LPQ)                                                                   \
@@ -572,6 +571,11 @@ int e2ep_attn_bwd_part(const float *q, const float *k, const float *v, const flo
     return launch_status("e2ep_attn_bwd");
   }
   float *Dq = part == 2 ? nullptr : D;  // dq pass alone: D is read by the other pass, not rewritten
+  if (attn_mf_ok(a, key_pad)) {  // matrix-core dq (+ D) (attn_mf.hip); dk / dv below or there
+    if (attn_mf_bwd(q, k, v, o, dout, lse, seed, a, dq, dk, dv, D, part, s) || part == 2)
+      return launch_status("e2ep_attn_bwd");
+    part = 3;  // dk / dv on the vector-FMA kernel (faster at this shape), reading D
+  }
   if (part != 3) {
     if (dh <= 44) {
       if (Sq <= 16 || att_lanes() == 4) E2EP_ATT_BQ(44, 4, Dq); else if (att_lanes() == 2) E2EP_ATT_BQ(44, 2, Dq); else E2EP_ATT_BQ(44, 1, Dq);

@@ -24,7 +24,8 @@ enum Tune {
   TUNE_KORDER = 18,           // conv forward / data-gradient K order: 1 = automatic, 2 = channel chunk outer, 3 = tap outer
   TUNE_XCD = 19,              // conv_lp.hip kernels: 2 = XCD-contiguous block order, 1 = hardware order
   TUNE_ATT_LANES = 20,        // attention lanes per query / key for long sequences: 1 (automatic), 2, 4
-  TUNE_N = 21
+  TUNE_ATT_MF = 21,           // attention on the matrix-core kernels where they apply: 2 = on, 1 = off
+  TUNE_N = 22
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

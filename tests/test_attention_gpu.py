@@ -277,3 +277,48 @@ def test_fully_masked_row_fused_zero_module_nan():
     attn_part = fused[:, 1] - m.out_proj.bias  # all-masked rows: attention output 0
     assert torch.isfinite(fused).all() and attn_part.abs().max() < 1e-6
     assert rel_l2(fused[:, 0], ref[:, 0]) < 1e-5
+
+
+@pytest.mark.parametrize("Sq,Sk", [(256, 256), (128, 256), (256, 128), (128, 128)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_matrix_core_matches_reference(Sq, Sk, p):
+    """The matrix-core kernels (csrc/attn_mf.hip: unmasked, Sq / Sk in {128, 256}, the fusion
+    encoder's shape) vs the fp64 restatement with the kernel's own keep mask, and vs the
+    vector-FMA kernels (e2ep_tune key 21 = 1) on the same inputs and mask."""
+    from e2ep_amd import _lib, attention
+    g = torch.Generator().manual_seed(13 + Sq + Sk)
+    B, dh = 4, 43
+    Ed = H * dh
+    qb = torch.randn(Sq, B, Ed, generator=g)
+    kvb = torch.randn(Sk, B, 2 * Ed, generator=g)
+    do = torch.randn(Sq, B, Ed, generator=g)
+    seed = torch.tensor([777], dtype=torch.int32, device=DEV)
+    keep = torch.empty(B * H, Sq, Sk, dtype=torch.uint8, device=DEV)
+    _lib.call("e2ep_attn_keep_mask", _lib.ptr(seed), B * H, Sq, Sk, p if p > 0 else 0.0,
+              _lib.ptr(keep), _lib.stream())
+    keep = keep.cpu().double() if p > 0 else torch.ones(B * H, Sq, Sk, dtype=torch.float64)
+    outs = {}
+    for mf in (3, 2, 1):  # all three passes / forward + dq / none on the matrix cores
+        old = _lib.call_raw("e2ep_tune", 21, mf)
+        try:
+            qd = qb.to(DEV).requires_grad_(True)
+            kvd = kvb.to(DEV).requires_grad_(True)
+            o = attention.attention(qd, kvd, H, False, None, p, seed if p > 0 else None)
+            (o * do.to(DEV)).sum().backward()
+        finally:
+            _lib.call_raw("e2ep_tune", 21, old)
+        outs[mf] = (o.detach().cpu(), qd.grad.cpu(), kvd.grad.cpu())
+
+    def heads(t):
+        S = t.shape[0]
+        return t.reshape(S, B, H, dh).permute(1, 2, 0, 3).reshape(B * H, S, dh)
+    qr = qb.double().requires_grad_(True)
+    kvr = kvb.double().requires_grad_(True)
+    orr = _ref_core(heads(qr), heads(kvr[..., :Ed]), heads(kvr[..., Ed:]), keep, p, False, None)
+    orr = orr.reshape(B, H, Sq, dh).permute(2, 0, 1, 3).reshape(Sq, B, Ed)
+    (orr * do.double()).sum().backward()
+    for mf in (3, 2):
+        for got, ref in zip(outs[mf], (orr.detach(), qr.grad, kvr.grad)):
+            assert rel_l2(got, ref) < 1e-5
+        for a, b in zip(outs[mf], outs[1]):  # both kernel families, same mask
+            assert rel_l2(a, b) < 1e-5
