@@ -312,10 +312,12 @@ def conv_roofline(step, lowp, n_eager=3):
     g_launch = sum(kern[k][0] for k in gemm)
     g_tfs = g_flop / (g_ms * 1e-3) / 1e12
     g_peak = BF16_MFMA_PEAK_TFS if lowp else FP32_MFMA_PEAK_TFS
-    entry = {"kernel": ("e2ep::k_conv_gemm / k_conv_gemm2 (implicit-GEMM conv forward + data "
-                        "gradient, v_mfma_f32_32x32x16_bf16)" if lowp else
-                        "e2ep::k_conv_gemm / k_conv_gemm2 (implicit-GEMM conv forward + data "
-                        "gradient, v_mfma_f32_32x32x2_f32)") + "; the step's largest kernel family",
+    entry = {"kernel": ("e2ep::k_conv_lp (+ k_conv_gemm for M < 40 / single-step K; implicit-GEMM "
+                        "conv forward + data gradient, v_mfma_f32_32x32x16_bf16, 16-bit LDS rows)"
+                        if lowp else
+                        "e2ep::k_conv_gemm / k_conv_gemm2 / k_conv_lp<fp32> (implicit-GEMM conv "
+                        "forward + data gradient, v_mfma_f32_32x32x2_f32)") +
+                       "; the step's largest kernel family",
              "bound": "mfma", "achieved": round(g_tfs, 2), "peak": g_peak,
              "unit": "TFLOP/s", "frac": round(g_tfs / g_peak, 4), "traffic": None,
              "flop_per_step": g_flop / n_eager, "ms_per_step": round(g_ms / n_eager, 4),

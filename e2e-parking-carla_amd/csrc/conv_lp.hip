@@ -806,7 +806,8 @@ int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op) {
   const int lk = lp_wgrad_lk(g, op);
   const long long tiles = (long long)cdiv(g.Cin * tl.n, 64 * wn) * cdiv(g.Cout, 64 * wm);
   const long long pix = (long long)g.N * g.P * g.Q;
-  long long s = (1024 + tiles - 1) / tiles;  // toward ~1024 workgroups
+  const long long target = g_tune[TUNE_LPW_TARGET];  // workgroups aimed at (e2ep_tune key 22)
+  long long s = (target + tiles - 1) / tiles;
   s = std::min(s, std::max(1LL, pix / (std::max(256, 4 * lk))));  // >= 256 pixels per slab
   return (int)std::max(1LL, std::min(s, 256LL));
 }

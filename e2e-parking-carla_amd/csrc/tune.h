@@ -25,7 +25,8 @@ enum Tune {
   TUNE_XCD = 19,              // conv_lp.hip kernels: 2 = XCD-contiguous block order, 1 = hardware order
   TUNE_ATT_LANES = 20,        // attention lanes per query / key for long sequences: 1 (automatic), 2, 4
   TUNE_ATT_MF = 21,           // attention on the matrix-core kernels where they apply: 2 = on, 1 = off
-  TUNE_N = 22
+  TUNE_LPW_TARGET = 22,       // workgroups the k_wgrad_lp K split aims at
+  TUNE_N = 23
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep
