@@ -288,48 +288,90 @@ __device__ __forceinline__ void dw_put(const float4 (&r)[DW_MAXV], int H, int W,
   }
 }
 
-template <int K, int ST, bool FLIP>
+// One lane's LDS window row v[0 .. NV) starting at `base`.  OFF >= 0: base sits OFF floats past a
+// 16-B boundary (OFF = -pl mod 4: the staged rows start 16-B aligned, every lane's first
+// output column is a multiple of 4), and the row is read as ceil((OFF + NV) / 4) ds_read_b128
+// from that boundary: 4 lane groups of 16 consecutive 16-B words, conflict-free, where the
+// scalar reads (OFF = -1, e2ep_tune key 23 = 1) land lanes 8 apart on one bank (4-way) at
+// 1 or 2 floats per instruction.  The words read past the window stay inside the staged row
+// (its right halo), since the row pitch is a multiple of 4.
+template <int NV, int OFF>
+__device__ __forceinline__ void dw_row(const float *base, float (&v)[NV]) {
+  if constexpr (OFF < 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = base[j];
+  } else {
+    constexpr int NF = (OFF + NV + 3) / 4;
+    const float4 *p = reinterpret_cast<const float4 *>(base - OFF);
+    float f[4 * NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const float4 t = p[i];
+      f[4 * i] = t.x;
+      f[4 * i + 1] = t.y;
+      f[4 * i + 2] = t.z;
+      f[4 * i + 3] = t.w;
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = f[OFF + j];
+  }
+}
+
+template <int K, int ST, bool FLIP, int OFF>
 __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
                                                       const float *__restrict__ w, DwGeom g,
                                                       DwStrip d, int units, float *__restrict__ y,
                                                       DwIn tf) {
+  // Grid-stride over units, software-pipelined like k_dw_wgrad_strip: the wave's next unit's
+  // input rows are loaded into registers before the current unit's FMAs (one unit per wave
+  // with stage / wait / compute in series ran at 1.7-3.5 TB/s).  The grid is capped at
+  // e2ep_tune key 24 blocks, so each wave walks several units.
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
-  const int unit = blockIdx.x * 4 + wave;
   float *lds = dw_lds + wave * d.IR * d.WP;
-  const bool active = unit < units;  // wave-uniform
-  int nc = 0, oy0 = 0;
-  if (active) {
-    nc = unit / d.units_per_plane;
-    oy0 = (unit - nc * d.units_per_plane) * d.RO;
-    dw_stage(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane, tf,
-             nc % g.C);
-  }
-  dw_wave_sync();
-  if (!active) return;
-  const int c = nc % g.C;
-  float wr[K * K];
-#pragma unroll
-  for (int t = 0; t < K * K; ++t) wr[t] = w[c * K * K + (FLIP ? K * K - 1 - t : t)];
   const int QL = g.Q >> 2;  // lanes per output row
   const int ro = lane / QL, ox0 = 4 * (lane - ro * QL);
-  const int oy = oy0 + ro;
-  if (ro >= d.RO || oy >= g.P) return;
   constexpr int NV = 3 * ST + K;
-  float o[4] = {0.f, 0.f, 0.f, 0.f};
-  const float *base = lds + (ro * ST) * d.WP + DW_PADL + ox0 * ST - g.pl;
+  const int step = gridDim.x * 4;
+  int u = blockIdx.x * 4 + wave;  // wave-uniform
+  int nc = 0, oy0 = 0;
+  auto unit_of = [&](int un) {
+    nc = un / d.units_per_plane;
+    oy0 = (un - nc * d.units_per_plane) * d.RO;
+  };
+  float4 rx[DW_MAXV];
+  if (u < units) unit_of(u);
+  dw_fetch(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, lane, rx, u < units);
+  for (; u < units; u += step) {
+    const int c = nc % g.C;
+    dw_put(rx, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane, dw_t(tf, c));
+    const int cur_nc = nc, cur_oy0 = oy0;
+    const bool nxt = u + step < units;
+    if (nxt) unit_of(u + step);
+    dw_fetch(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, lane, rx, nxt);
+    float wr[K * K];
 #pragma unroll
-  for (int a = 0; a < K; ++a) {
-    float v[NV];
+    for (int t = 0; t < K * K; ++t) wr[t] = w[c * K * K + (FLIP ? K * K - 1 - t : t)];
+    dw_wave_sync();
+    const int oy = cur_oy0 + ro;
+    if (ro < d.RO && oy < g.P) {
+      float o[4] = {0.f, 0.f, 0.f, 0.f};
+      const float *base = lds + (ro * ST) * d.WP + DW_PADL + ox0 * ST - g.pl;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) v[j] = base[a * d.WP + j];
+      for (int a = 0; a < K; ++a) {
+        float v[NV];
+        dw_row<NV, OFF>(base + a * d.WP, v);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int b = 0; b < K; ++b) o[u] = __builtin_fmaf(wr[a * K + b], v[u * ST + b], o[u]);
+          for (int b = 0; b < K; ++b) o[q] = __builtin_fmaf(wr[a * K + b], v[q * ST + b], o[q]);
+      }
+      *reinterpret_cast<float4 *>(y + ((size_t)cur_nc * g.P + oy) * g.Q + ox0) =
+          make_float4(o[0], o[1], o[2], o[3]);
+    }
+    dw_wave_sync();  // LDS reuse
   }
-  *reinterpret_cast<float4 *>(y + ((size_t)nc * g.P + oy) * g.Q + ox0) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // stride-2 data gradient over strip units: a wave owns RO = 64/(W/4) rows of dx of one plane,
@@ -384,7 +426,7 @@ __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restri
 // weight gradient partials over strip units: grid (C, splits); the block's waves walk the
 // channel's units (n, strip) of its slice; per lane K*K register accumulators, fixed-order
 // wave + block reduction.
-template <int K, int ST>
+template <int K, int ST, int OFF>
 __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
                                                         const float *__restrict__ x, DwGeom g,
                                                         DwStrip d, int splits,
@@ -445,8 +487,7 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
 #pragma unroll
       for (int a = 0; a < K; ++a) {
         float v[NV];
-#pragma unroll
-        for (int j = 0; j < NV; ++j) v[j] = base[a * d.WP + j];
+        dw_row<NV, OFF>(base + a * d.WP, v);
 #pragma unroll
         for (int b = 0; b < K; ++b)
 #pragma unroll
@@ -502,6 +543,37 @@ using namespace e2ep;
     }                                                                                         \
   } while (0)
 
+// the strip kernels' LDS row-read variant: dw_row's OFF for left pad pl, or -1 (scalar reads)
+// grid of the forward strip kernel: one unit per wave up to e2ep_tune key 24 blocks
+static int dw_fwd_blocks(int units) { return std::min(cdiv(units, 4), g_tune[TUNE_DW_FWD_BLOCKS]); }
+static int dw_off(int pl) { return g_tune[TUNE_DW_VEC] == 1 ? -1 : ((-pl) & 3); }
+
+// launch a strip kernel with the row-read variant `off` as its compile-time OFF
+template <int K, int ST, bool FLIP>
+static void dw_fwd_strip(int off, dim3 grid, size_t shm, hipStream_t st, const float *x,
+                         const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf) {
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, x, w, g, d, units, y, tf); };
+  switch (off) {
+    case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0>); break;
+    case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1>); break;
+    case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2>); break;
+    case 3: go(k_dw_fwd_strip<K, ST, FLIP, 3>); break;
+    default: go(k_dw_fwd_strip<K, ST, FLIP, -1>);
+  }
+}
+template <int K, int ST>
+static void dw_wgrad_strip(int off, dim3 grid, size_t shm, hipStream_t st, const float *gy,
+                           const float *x, DwGeom g, DwStrip d, int splits, float *part, DwIn tf) {
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, gy, x, g, d, splits, part, tf); };
+  switch (off) {
+    case 0: go(k_dw_wgrad_strip<K, ST, 0>); break;
+    case 1: go(k_dw_wgrad_strip<K, ST, 1>); break;
+    case 2: go(k_dw_wgrad_strip<K, ST, 2>); break;
+    case 3: go(k_dw_wgrad_strip<K, ST, 3>); break;
+    default: go(k_dw_wgrad_strip<K, ST, -1>);
+  }
+}
+
 extern "C" {
 
 static bool dw_strip_ok(const DwGeom &g) {
@@ -512,16 +584,17 @@ static bool dw_strip_ok(const DwGeom &g) {
   return d.IR * (g.W / 4) <= 64 * DW_MAXV;  // the unrolled staging's reach
 }
 
-#define DW_STRIP_DISPATCH(KERNEL, FLIPARG, GRID, SHMEM, ...)                                    \
+#define DW_STRIP_DISPATCH(LAUNCHER, FLIPARG, GRID, SHMEM, ...)                                   \
   do {                                                                                         \
+    const int off = dw_off(g.pl);                                                              \
     if (g.K == 3 && g.st == 1)                                                                 \
-      hipLaunchKernelGGL((KERNEL<3, 1 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+      LAUNCHER<3, 1 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
     else if (g.K == 3 && g.st == 2)                                                            \
-      hipLaunchKernelGGL((KERNEL<3, 2 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+      LAUNCHER<3, 2 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
     else if (g.K == 5 && g.st == 1)                                                            \
-      hipLaunchKernelGGL((KERNEL<5, 1 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+      LAUNCHER<5, 1 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
     else                                                                                       \
-      hipLaunchKernelGGL((KERNEL<5, 2 FLIPARG>), GRID, dim3(256), SHMEM, as_stream(stream), __VA_ARGS__); \
+      LAUNCHER<5, 2 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
   } while (0)
 #define DW_NOFLIP , false
 #define DW_NONE
@@ -538,8 +611,8 @@ int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float
   if (dw_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     const int units = g.N * g.C * d.units_per_plane;
-    DW_STRIP_DISPATCH(k_dw_fwd_strip, DW_NOFLIP, dim3(cdiv(units, 4)), 4 * d.IR * d.WP * 4, x, w, g,
-                      d, units, y, tf);
+    DW_STRIP_DISPATCH(dw_fwd_strip, DW_NOFLIP, dim3(dw_fwd_blocks(units)), 4 * d.IR * d.WP * 4, x,
+                      w, g, d, units, y, tf);
     return launch_status("e2ep_dwconv_fwd");
   }
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_fwd: N*C > 65535");
@@ -560,14 +633,14 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
     if (dw_strip_ok(t) && t.pt >= 0 && t.pl >= 0 && t.pl <= DW_PADL) {
       const DwStrip d = dw_strip(t.K, 1, t.W, t.P, t.Q);
       const int units = t.N * t.C * d.units_per_plane;
+      const size_t shm = 4 * d.IR * d.WP * 4;
+      const DwIn none{nullptr, nullptr, 0};
       if (t.K == 3)
-        hipLaunchKernelGGL((k_dw_fwd_strip<3, 1, true>), dim3(cdiv(units, 4)), dim3(256),
-                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx,
-                           DwIn{nullptr, nullptr, 0});
+        dw_fwd_strip<3, 1, true>(dw_off(t.pl), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
+                                 w, t, d, units, dx, none);
       else
-        hipLaunchKernelGGL((k_dw_fwd_strip<5, 1, true>), dim3(cdiv(units, 4)), dim3(256),
-                           4 * d.IR * d.WP * 4, as_stream(stream), gy, w, t, d, units, dx,
-                           DwIn{nullptr, nullptr, 0});
+        dw_fwd_strip<5, 1, true>(dw_off(t.pl), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
+                                 w, t, d, units, dx, none);
       return launch_status("e2ep_dwconv_dgrad");
     }
   }
@@ -633,7 +706,7 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
   float *part = static_cast<float *>(workspace);
   if (dw_wgrad_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
-    DW_STRIP_DISPATCH(k_dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
+    DW_STRIP_DISPATCH(dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
                       sp, part, tf);
   } else {
     DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part, in_scale, in_shift, in_act);

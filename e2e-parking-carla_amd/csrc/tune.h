@@ -26,7 +26,9 @@ enum Tune {
   TUNE_ATT_LANES = 20,        // attention lanes per query / key for long sequences: 1 (automatic), 2, 4
   TUNE_ATT_MF = 21,           // attention on the matrix-core kernels where they apply: 2 = on, 1 = off
   TUNE_LPW_TARGET = 22,       // workgroups the k_wgrad_lp K split aims at
-  TUNE_N = 23
+  TUNE_DW_VEC = 23,           // depthwise strip kernels' LDS rows: 2 = ds_read_b128 windows, 1 = scalar reads
+  TUNE_DW_FWD_BLOCKS = 24,    // depthwise forward / stride-1 data-gradient strip kernel: grid cap (blocks)
+  TUNE_N = 25
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

@@ -15,6 +15,20 @@ def _g(seed):
     return torch.Generator().manual_seed(seed)
 
 
+@pytest.fixture(params=[0, 3], ids=["dw_grid_default", "dw_grid_3"])
+def dw_grid(request):
+    """Depthwise forward grid cap (e2ep_tune key 24): default, and 3 blocks so each wave walks
+    many units of the grid-stride loop (with the fused BN input transform changing channel
+    from unit to unit)."""
+    from e2ep_amd import _lib
+    if not request.param:
+        yield 0
+        return
+    prev = _lib.load().e2ep_tune(24, request.param)
+    yield request.param
+    _lib.load().e2ep_tune(24, prev)
+
+
 @pytest.fixture(params=[1, 0], ids=["bn_one_launch", "bn_split"])
 def bn_path(request):
     """Run a BN test through the single-launch block-per-channel kernels (channels of
@@ -136,9 +150,28 @@ def test_resize(case):
                                   (2, 8, 128, 128, 3, 2, (0, 1, 0, 1)), (2, 32, 64, 64, 3, 1, (1, 1, 1, 1)),
                                   (2, 40, 32, 32, 5, 1, (2, 2, 2, 2)), (3, 16, 16, 16, 3, 1, (1, 1, 1, 1)),
                                   (2, 12, 24, 20, 5, 1, (2, 2, 2, 2)), (2, 16, 32, 32, 5, 2, (1, 2, 1, 2)),
-                                  (2, 8, 20, 24, 3, 2, (0, 1, 0, 1)), (2, 6, 64, 48, 5, 2, (2, 2, 2, 2))])
-def test_depthwise(case):
-    from e2ep_amd import ops
+                                  (2, 8, 20, 24, 3, 2, (0, 1, 0, 1)), (2, 6, 64, 48, 5, 2, (2, 2, 2, 2)),
+                                  (2, 16, 32, 32, 5, 1, (3, 1, 3, 1))])
+@pytest.mark.parametrize("variant", [(2, 0), (1, 3)])
+def test_depthwise(case, variant):
+    """variant = (e2ep_tune key 23, key 24): the strip kernels' LDS window reads (2 = 16-B
+    vector reads from the aligned boundary OFF = -pad_left mod 4 floats back, 1 = scalar
+    reads) and the forward grid cap (0 = default; 3 blocks = every wave walks many units of
+    the software-pipelined grid-stride loop)."""
+    from e2ep_amd import _lib, ops
+    lib = _lib.load()
+    rows, blocks = variant
+    prev = lib.e2ep_tune(23, rows)
+    prevb = lib.e2ep_tune(24, blocks) if blocks else None
+    try:
+        _depthwise_case(ops, case)
+    finally:
+        lib.e2ep_tune(23, prev)
+        if blocks:
+            lib.e2ep_tune(24, prevb)
+
+
+def _depthwise_case(ops, case):
     N, C, H, W, K, s, pad = case
     g = _g(C + H)
     x = torch.randn(N, C, H, W, generator=g)
@@ -163,7 +196,7 @@ def test_depthwise(case):
                                   (2, 40, 32, 32, 5, 2, (1, 2, 1, 2), False),
                                   (3, 8, 13, 11, 3, 2, (0, 1, 0, 1), True),
                                   (2, 6, 64, 48, 5, 2, (2, 2, 2, 2), True)])
-def test_bn_swish_depthwise_fused(case, bn_path):
+def test_bn_swish_depthwise_fused(case, bn_path, dw_grid):
     """MBConv _bn0 -> swish -> _depthwise_conv with the BN + swish applied inside the
     depthwise input load (e2ep_bn_stats + dwconv in_scale/in_shift), train and eval, vs fp64
     torch: output, x / gamma / beta / weight gradients and running statistics."""
