@@ -556,7 +556,8 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * than 16 (1 = automatic, 2, 4), 21 attention on the matrix-core kernels of attn_mf.hip where
  * they apply (2 = forward and dq, default; 3 = also dk / dv; 1 = off), 22 k_wgrad_lp K-split
  * target workgroups (1024), 23 depthwise strip kernels' LDS window reads (2 = 16-B vector
- * reads, default; 1 = scalar reads).
+ * reads, default; 1 = scalar reads), 24 depthwise forward / stride-1 data-gradient grid cap in
+ * blocks (2048; each wave walks units beyond it in a software-pipelined loop).
  * For A/B timing.
  * Contract for every plan override and tunable above (e2ep_conv_split_params,
  * e2ep_gemm_force, e2ep_gemm_split_min, e2ep_bn_small*, e2ep_tune): a launch recomputes its
