@@ -141,12 +141,9 @@ def mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, is_causal
             out = mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
                       need_weights=False)[0]
             return (out, query) if skip else out
-        # split (one SplitBackward -> one cat of the two weight gradients) rather than two
-        # slices (each: zero-fill + copy, then an add)
-        Wq, Wkv = W.split([E, 2 * E])
-        bq, bkv = (None, None) if bias is None else bias.split([E, 2 * E])
-        q, qs = nn_ops.linear(query, Wq, bq, skip=True)
-        kv = nn_ops.linear(key, Wkv, bkv)
+        # one Function over the whole in_proj_weight: its backward writes the q and kv row
+        # blocks of dW / db in place (a weight split would concatenate them: 2 cat launches)
+        q, kv, qs = nn_ops.in_proj_qkv(query, key, W, bias, E)
         o = attention(q, kv, H, is_causal, key_padding_mask, p)
     out = nn_ops.linear(o, mod.out_proj.weight, mod.out_proj.bias)
     return (out, qs) if skip else out

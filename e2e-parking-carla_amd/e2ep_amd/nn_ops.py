@@ -1,6 +1,8 @@
 """Autograd ops over the e2ep BN / resize / depthwise / pooling / SE kernels (csrc/bn.hip,
 resize.hip, dwconv.hip, pool.hip).  Each forward enqueues on torch's current HIP stream;
 each backward is the matching e2ep gradient kernel (no PyTorch arithmetic)."""
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
@@ -84,7 +86,13 @@ class BnCounters:
         if self.recorded is None:
             self._log = []
         else:
-            torch._foreach_add_([bn.num_batches_tracked for bn in self.recorded], 1)
+            ctrs = [bn.num_batches_tracked for bn in self.recorded]
+            key = tuple(c.data_ptr() for c in ctrs)
+            if getattr(self, "_table_key", None) == key:
+                # one e2ep launch over the device table of the counters' addresses
+                _lib.call("e2ep_add_i64_multi", _lib.ptr(self._table), len(ctrs), 1, _lib.stream())
+            else:
+                torch._foreach_add_(ctrs, 1)
             self.batched = True
         _COUNTERS.append(self)
         return self
@@ -93,6 +101,15 @@ class BnCounters:
         _COUNTERS.pop()
         if self.recorded is None and self._log is not None and not exc[0]:
             self.recorded = self._log
+            ctrs = [bn.num_batches_tracked for bn in self.recorded]
+            # the device table of counter addresses for later forwards (the buffers live as
+            # long as the modules), built here, outside any graph capture: the first forward
+            # runs eagerly
+            if (ctrs and all(c.is_cuda and c.dtype == torch.int64 for c in ctrs)
+                    and not torch.cuda.is_current_stream_capturing()):
+                self._table = torch.tensor([c.data_ptr() for c in ctrs], dtype=torch.int64,
+                                           device=ctrs[0].device)
+                self._table_key = tuple(c.data_ptr() for c in ctrs)
         self._log = None
         self.batched = False
         return False
@@ -550,6 +567,74 @@ def squeeze_excite(x, w1, b1, w2, b2):
 
 
 # ------------------------------------------------------------------------------------------
+# channel concatenation, loss sum, PAD mask (csrc/small.hip)
+# ------------------------------------------------------------------------------------------
+class _CatChannels(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        xs = [x.contiguous() for x in xs]
+        N, _, H, W = xs[0].shape
+        chans = [x.shape[1] for x in xs]
+        y = torch.empty(N, sum(chans), H, W, dtype=torch.float32, device=xs[0].device)
+        n = len(xs)
+        _lib.call("e2ep_cat_channels", (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs]),
+                  (ctypes.c_int * n)(*chans), n, N, H * W, _lib.ptr(y), _lib.stream())
+        ctx.chans = chans
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        N, _, H, W = g.shape
+        outs = [torch.empty(N, c, H, W, dtype=torch.float32, device=g.device) for c in ctx.chans]
+        n = len(outs)
+        _lib.call("e2ep_split_channels", _lib.ptr(g), (ctypes.c_int * n)(*ctx.chans), n, N, H * W,
+                  (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs]), _lib.stream())
+        return tuple(outs)
+
+
+def cat_channels(xs):
+    """torch.cat(xs, 1) of NCHW fp32 device tensors as one e2ep launch, and its backward as
+    one launch writing every piece's gradient contiguous (no slice copies downstream).  Falls
+    back to torch.cat outside the kernel's range (more than 8 pieces, H*W % 4 != 0)."""
+    _dev(*xs)
+    if (len(xs) > 8 or any(x.dim() != 4 or x.dtype != torch.float32 for x in xs)
+            or (xs[0].shape[2] * xs[0].shape[3]) % 4):
+        return torch.cat(xs, 1)
+    return _CatChannels.apply(*xs)
+
+
+class _Sum3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, c):
+        out = torch.empty((), dtype=torch.float32, device=a.device)
+        _lib.call("e2ep_sum3", _lib.ptr(a), _lib.ptr(b), _lib.ptr(c), _lib.ptr(out), _lib.stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g, g
+
+
+def sum3(a, b, c):
+    """(a + b) + c of three fp32 device scalars in one launch (the step's total loss)."""
+    _dev(a, b, c)
+    return _Sum3.apply(a, b, c)
+
+
+def eq_mask(tok, value):
+    """tok == value for a (B, T) int64 device tensor with unit column stride, as a bool mask
+    (one launch)."""
+    if tok.dtype != torch.int64 or tok.dim() != 2 or tok.stride(1) != 1 or not tok.is_cuda:
+        raise _lib.E2EPError("eq_mask: (B, T) int64 device tensor with unit column stride")
+    B, T = tok.shape
+    m = torch.empty(B, T, dtype=torch.bool, device=tok.device)
+    _lib.call("e2ep_eq_mask_i64", _lib.ptr(tok), tok.stride(0), B, T, int(value), _lib.ptr(m),
+              _lib.stream())
+    return m
+
+
+# ------------------------------------------------------------------------------------------
 # residual add + dropout + LayerNorm (post-norm transformer layers)
 # ------------------------------------------------------------------------------------------
 class _AddDropLN(torch.autograd.Function):
@@ -662,41 +747,105 @@ class _Linear(torch.autograd.Function):
         g2 = gy.reshape(M, N)
         if g2.stride(1) != 1 or g2.stride(0) != N:
             g2 = g2.contiguous()
-        if ctx.relu:
-            g2 = g2 * (y > 0)
-        dx = dw = db = None
-        # weight / bias gradients on the side stream, concurrent with the input gradient
-        # (conv._Fork: every buffer allocated here, on the current stream, before the fork)
-        want_b = ctx.has_bias and nig[2]
-        fork = None
-        if nig[1] or want_b:
-            if nig[1]:
-                dw = torch.empty(N, K, dtype=torch.float32, device=gy.device)
-                wsw = _ws(_lib.load().e2ep_gemm_rowsum_workspace(N, K, M) if want_b
-                          else _lib.load().e2ep_gemm_workspace(N, K, M), gy.device)
-            if want_b:
-                db = torch.empty(N, dtype=torch.float32, device=gy.device)
-                wsb = None if nig[1] else _ws(_lib.load().e2ep_col_sum_workspace(M, N), gy.device)
-            fork = conv._Fork(gy.device, on=nig[0])
-            with fork:
-                if nig[1] and want_b:  # dW and db in one launch
-                    with timing.region(timing.name("gemm", (N, K, M), "linear_wgrad"), 2.0 * N * K * M):
-                        _lib.call("e2ep_gemm_rowsum", _lib.ptr(g2), g2.stride(0), _lib.ptr(x2),
-                                  x2.stride(0), _lib.ptr(dw), K, _lib.ptr(db), N, K, M, _lib.ptr(wsw),
-                                  _lib.stream())
-                elif nig[1]:
-                    gemm(g2, False, x2, False, N, K, M, out=dw, ws=wsw, tag="linear_wgrad")
-                else:
-                    _lib.call("e2ep_col_sum", _lib.ptr(g2), M, N, _lib.ptr(db), _lib.ptr(wsb),
-                              _lib.stream())
-        if nig[0]:
-            cadd = gskip.reshape(M, K) if gskip is not None else None
-            if cadd is not None and cadd.stride(1) != 1:
-                cadd = cadd.contiguous()
-            dx = gemm(g2, True, weight, False, M, K, N, cadd=cadd, tag="linear_dgrad").view(ctx.xshape)
-        if fork is not None:
-            fork.join()
-        return dx, dw, db, None, None
+        if ctx.relu:  # dY * [y > 0] (relu derivative on the output), one e2ep launch
+            gr = torch.empty_like(g2)
+            _lib.call("e2ep_act_bwd", _lib.ptr(y), _lib.ptr(g2), g2.numel(), 1, _lib.ptr(gr),
+                      _lib.stream())
+            g2 = gr
+        dx, dw, db = _linear_bwd(g2, x2, weight, nig[0], nig[1], ctx.has_bias and nig[2], gskip)
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None
+
+
+def _linear_bwd(g2, x2, weight, want_x, want_w, want_b, gskip=None, dw=None, db=None):
+    """Gradients of y2 = x2 W^T + b from g2 = dY2 (M x N): dX2 = g2 W (+ gskip in the
+    epilogue), dW = g2^T x2 with db = row sums of g2^T in the same launch (e2ep_gemm_rowsum),
+    db alone by e2ep_col_sum.  dw / db may be given (row slices of a larger gradient)."""
+    M, K = x2.shape
+    N = weight.shape[0]
+    dx = None
+    # weight / bias gradients on the side stream, concurrent with the input gradient
+    # (conv._Fork: every buffer allocated here, on the current stream, before the fork)
+    fork = None
+    if want_w or want_b:
+        if want_w:
+            if dw is None:
+                dw = torch.empty(N, K, dtype=torch.float32, device=g2.device)
+            wsw = _ws(_lib.load().e2ep_gemm_rowsum_workspace(N, K, M) if want_b
+                      else _lib.load().e2ep_gemm_workspace(N, K, M), g2.device)
+        if want_b:
+            if db is None:
+                db = torch.empty(N, dtype=torch.float32, device=g2.device)
+            wsb = None if want_w else _ws(_lib.load().e2ep_col_sum_workspace(M, N), g2.device)
+        fork = conv._Fork(g2.device, on=want_x)
+        with fork:
+            if want_w and want_b:  # dW and db in one launch
+                with timing.region(timing.name("gemm", (N, K, M), "linear_wgrad"), 2.0 * N * K * M):
+                    _lib.call("e2ep_gemm_rowsum", _lib.ptr(g2), g2.stride(0), _lib.ptr(x2),
+                              x2.stride(0), _lib.ptr(dw), dw.stride(0), _lib.ptr(db), N, K, M,
+                              _lib.ptr(wsw), _lib.stream())
+            elif want_w:
+                gemm(g2, False, x2, False, N, K, M, out=dw, ws=wsw, tag="linear_wgrad")
+            else:
+                _lib.call("e2ep_col_sum", _lib.ptr(g2), M, N, _lib.ptr(db), _lib.ptr(wsb),
+                          _lib.stream())
+    if want_x:
+        cadd = gskip.reshape(M, K) if gskip is not None else None
+        if cadd is not None and cadd.stride(1) != 1:
+            cadd = cadd.contiguous()
+        dx = gemm(g2, True, weight, False, M, K, N, cadd=cadd, tag="linear_dgrad")
+    if fork is not None:
+        fork.join()
+    return dx, (dw if want_w else None), (db if want_b else None)
+
+
+def _rows2(x):
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    return x2 if (x2.stride(1) == 1 and x2.stride(0) == K) else x2.contiguous()
+
+
+class _InProjQKV(torch.autograd.Function):
+    """Cross-attention in-projection with one weight [3E, E] (nn.MultiheadAttention's
+    in_proj_weight / in_proj_bias): q = xq Wq^T + bq, kv = xkv Wkv^T + bkv with Wq = W[:E],
+    Wkv = W[E:], and xq handed back for the layer's residual (its gradient joins dxq in the
+    GEMM epilogue).  The backward writes dW / db row blocks straight into one [3E, E] / [3E]
+    gradient, so no split-backward concatenation runs."""
+
+    @staticmethod
+    def forward(ctx, xq, xkv, weight, bias, E):
+        xq2, xkv2 = _rows2(xq), _rows2(xkv)
+        K = xq2.shape[1]
+        Wq, Wkv = weight[:E], weight[E:]
+        bq, bkv = (None, None) if bias is None else (bias[:E], bias[E:])
+        q = gemm(xq2, True, Wq, True, xq2.shape[0], E, K, bias=bq, tag="linear_fwd")
+        kv = gemm(xkv2, True, Wkv, True, xkv2.shape[0], 2 * E, K, bias=bkv, tag="linear_fwd")
+        ctx.save_for_backward(xq2, xkv2, weight)
+        ctx.E, ctx.has_bias, ctx.shapes = E, bias is not None, (xq.shape, xkv.shape)
+        return q.view(*xq.shape[:-1], E), kv.view(*xkv.shape[:-1], 2 * E), xq
+
+    @staticmethod
+    def backward(ctx, gq, gkv, gskip):
+        xq2, xkv2, weight = ctx.saved_tensors
+        nig = ctx.needs_input_grad
+        E = ctx.E
+        want_b = ctx.has_bias and nig[3]
+        dw = torch.empty_like(weight) if nig[2] else None
+        db = torch.empty(3 * E, dtype=torch.float32, device=weight.device) if want_b else None
+        dxq, _, _ = _linear_bwd(_rows2(gq), xq2, weight[:E], nig[0], nig[2], want_b, gskip,
+                                dw[:E] if dw is not None else None,
+                                db[:E] if db is not None else None)
+        dxkv, _, _ = _linear_bwd(_rows2(gkv), xkv2, weight[E:], nig[1], nig[2], want_b, None,
+                                 dw[E:] if dw is not None else None,
+                                 db[E:] if db is not None else None)
+        sq, skv = ctx.shapes
+        return (dxq.view(sq) if dxq is not None else None,
+                dxkv.view(skv) if dxkv is not None else None, dw, db, None)
+
+
+def in_proj_qkv(xq, xkv, weight, bias, E):
+    """(q, kv, xq_skip) of a cross-attention in-projection (see _InProjQKV)."""
+    _dev(xq, xkv, weight, bias)
+    return _InProjQKV.apply(xq, xkv, weight, bias, int(E))
 
 
 def linear(x, weight, bias=None, skip=False, relu=False):

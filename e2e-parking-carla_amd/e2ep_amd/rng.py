@@ -30,3 +30,11 @@ def seed(device):
     s = _pool[_next:_next + 1]
     _next += 1
     return s
+
+
+def end_step():
+    """Retire the pool: later calls (outside a training forward) draw fresh seeds again, so a
+    graph captured after this step does not bake in a view of this step's pool."""
+    global _pool, _next
+    _pool = None
+    _next = 0

@@ -213,7 +213,10 @@ class TrainStep:
         if self.buckets is not None:
             self.buckets.arm()
         loss = self.module.training_step(self.batch, 0)
-        loss.backward()
+        # the seed gradient: a persistent ones scalar (loss.backward() would fill one per step)
+        if getattr(self, "_one", None) is None or self._one.device != loss.device:
+            self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(self._one)
         if self.buckets is not None:
             self.buckets.finish()
         return loss.detach()

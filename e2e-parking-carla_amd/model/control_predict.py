@@ -35,7 +35,8 @@ class ControlPredict(nn.Module):
         if getattr(self, "_causal_key", None) != (L, tgt.device):
             self._causal_mask = torch.full((L, L), float("-inf"), device=tgt.device).triu(1)
             self._causal_key = (L, tgt.device)
-        return self._causal_mask, tgt == self.pad_idx
+        pad = nn_ops.eq_mask(tgt, self.pad_idx) if tgt.is_cuda else tgt == self.pad_idx
+        return self._causal_mask, pad
 
     def decoder(self, encoder_out, tgt_embedding, tgt_mask, tgt_padding_mask):
         # A mask made by create_mask is known to be causal: saying so skips torch's

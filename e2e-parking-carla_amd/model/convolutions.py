@@ -46,7 +46,7 @@ class ASPP(nn.Module):
 
     def forward(self, x):
         branches = [_run_conv_bn_relu(self.convs[0], x)] + [m(x) for m in self.convs[1:]]
-        y = _run_conv_bn_relu(self.project, torch.cat(branches, 1))
+        y = _run_conv_bn_relu(self.project, nn_ops.cat_channels(branches))
         # Dropout(0.5) after the project BN-ReLU (reference model/convolutions.py:264): y >= 0,
         # so dropout(y) = dropout(relu(y)) runs on the fused ReLU-dropout kernel, one launch
         # each way (its backward's relu mask only drops entries whose BN-ReLU gradient is 0)
@@ -75,6 +75,6 @@ class UpsamplingConcat(nn.Module):
         self.conv = nn.Sequential(*_conv_bn(cin, cout, 3, 1), *_conv_bn(cout, cout, 3, 1))
 
     def forward(self, x_to_upsample, x):
-        y = torch.cat([x, ops.upsample2x(x_to_upsample)], 1)
+        y = nn_ops.cat_channels([x, ops.upsample2x(x_to_upsample)])
         y = _run_conv_bn_relu(self.conv, y, 0)
         return _run_conv_bn_relu(self.conv, y, 3)

@@ -79,9 +79,13 @@ class ParkingModel(nn.Module):
     def forward(self, data, noise=None):
         if self.training:  # one launch draws every dropout seed of this step (e2ep_amd.rng)
             rng.begin_step(data["image"].device)
-        fuse_feature, pred_segmentation, pred_depth, _ = self.encoder(data, noise)
-        gt = data["gt_control"].to(fuse_feature.device, non_blocking=True)
-        pred_control = self.control_predict(fuse_feature, gt)
+        try:
+            fuse_feature, pred_segmentation, pred_depth, _ = self.encoder(data, noise)
+            gt = data["gt_control"].to(fuse_feature.device, non_blocking=True)
+            pred_control = self.control_predict(fuse_feature, gt)
+        finally:
+            if self.training:
+                rng.end_step()
         return pred_control, pred_segmentation, pred_depth
 
     def predict(self, data, noise=None):

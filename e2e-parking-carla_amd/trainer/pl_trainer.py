@@ -12,6 +12,7 @@ from torch import nn
 from loss.control_loss import ControlLoss, ControlValLoss
 from loss.depth_loss import DepthLoss
 from loss.seg_loss import SegmentationLoss
+from e2ep_amd import nn_ops
 from model.parking_model import ParkingModel
 
 try:  # pragma: no cover - PL absent in this image
@@ -61,7 +62,9 @@ class ParkingTrainingModule(_Base):
                                                              batch["segmentation"]),
             "depth_loss": self.depth_loss_func(pred_depth, batch["depth"]),
         }
-        out["train_loss"] = out["control_loss"] + out["segmentation_loss"] + out["depth_loss"]
+        a, b, c = out["control_loss"], out["segmentation_loss"], out["depth_loss"]
+        # (a + b) + c as the reference sums them; one e2ep launch on the device
+        out["train_loss"] = nn_ops.sum3(a, b, c) if a.is_cuda else a + b + c
         return out, (pred_control, pred_segmentation, pred_depth)
 
     def training_step(self, batch, batch_idx=0, noise=None):

@@ -250,6 +250,29 @@ int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Layout and bookkeeping (csrc/small.hip)
+ * ------------------------------------------------------------------------------------- */
+/* torch.cat(pieces, dim=1) of n <= 8 NCHW fp32 tensors [N][chans[j]][HW] into dst
+ * [N][sum chans][HW] (ASPP branches, reference model/convolutions.py:262-263; UpsamplingConcat,
+ * model/convolutions.py:281-282), and its backward: the split of dst-shaped `src` into n
+ * contiguous pieces (torch's CatBackward slices + .contiguous() copies).  srcs / dsts / chans
+ * are HOST arrays of device pointers / channel counts; HW % 4 == 0, pointers 16-B aligned. */
+int e2ep_cat_channels(const float *const *srcs, const int *chans, int n, int N, long long HW,
+                      float *dst, void *stream);
+int e2ep_split_channels(const float *src, const int *chans, int n, int N, long long HW,
+                        float *const *dsts, void *stream);
+/* out[0] = (a[0] + b[0]) + c[0] in fp32: the training loss (trainer/pl_trainer.py:57-59,
+ * control + segmentation + depth) as one launch. */
+int e2ep_sum3(const float *a, const float *b, const float *c, float *out, void *stream);
+/* mask[b*T + t] = tok[b*rstride + t] == value (1 / 0): the decoder's PAD-key mask
+ * (model/control_predict.py create_mask, tgt == pad_idx) on int64 tokens. */
+int e2ep_eq_mask_i64(const int64_t *tok, long long rstride, int B, int T, int64_t value,
+                     uint8_t *mask, void *stream);
+/* *(int64 *)table[i] += v for i < n (device table of device addresses): every BatchNorm's
+ * num_batches_tracked increment of a forward (torch.nn.BatchNorm2d) in one launch. */
+int e2ep_add_i64_multi(const long long *table, int n, long long v, void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Squeeze-and-excitation of an MBConv block as one op (efficientnet-pytorch 0.7.1
  * MBConvBlock._se_reduce / _swish / _se_expand / sigmoid gate, reference
  * model/cam_encoder.py:69-73).  x, y [N,C,HW]; w1 [sq,C] b1 [sq] (_se_reduce), w2 [C,sq]

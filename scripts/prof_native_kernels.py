@@ -11,7 +11,6 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "e2e-parking-carla_amd"), ROOT]
 import torch  # noqa: E402
-from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
 
 def main():
@@ -36,32 +35,46 @@ def main():
     for _ in range(2):
         step()
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
-        step()
-        torch.cuda.synchronize()
-    evs = prof.events()
-    by_id = {ev.id: ev for ev in evs}
+    # every aten op that can launch a kernel, with the autograd node executing it (backward)
+    # or the first product source frame (forward)
+    import traceback
+    from torch.utils._python_dispatch import TorchDispatchMode
+    skip = ("empty", "view", "as_strided", "reshape", "detach", "t", "transpose", "expand",
+            "_unsafe_view", "slice", "select", "unsqueeze", "squeeze", "permute", "alias",
+            "empty_like", "empty_strided", "lift_fresh", "resolve_conj", "resolve_neg", "item",
+            "_local_scalar_dense", "is_nonzero", "narrow", "split", "chunk", "unbind", "split_with_sizes",
+            "new_empty", "new_empty_strided", "clone_if_view", "set_", "result_type", "size",
+            "stride", "numel", "dim", "is_contiguous", "contiguous", "_to_copy", "to", "_reshape_alias",
+            "sym_size", "sym_stride", "sym_numel", "sym_storage_offset", "storage_offset", "zeros_like")
     keys = ("model/", "e2ep_amd/", "loss/", "trainer/", "bench.py")
     rows = collections.Counter()
-    for ev in evs:
-        kern = getattr(ev, "kernels", None) or []
-        for k in kern:
-            if "at::native" not in k.name and "elementwise" not in k.name:
-                continue
-            # the innermost aten op that launched it and the first product frame up its parents
-            op = ev
-            site = None
-            p = ev
-            while p is not None and site is None:
-                st = [f for f in (p.stack or []) if any(s in f for s in keys)]
-                if st:
-                    site = st[0]
-                p = getattr(p, "cpu_parent", None)
-            kn = k.name.split("<")[0] + "<" + k.name.split("<")[1][:90] if "<" in k.name else k.name
-            rows[(op.name, kn, site or "(autograd engine)")] += 1
-    for (op, kn, site), n in sorted(rows.items(), key=lambda r: -r[1]):
-        print(f"{n:4d}  {op:32s} {site}\n        {kn}")
-    print(f"total native kernel launches: {sum(rows.values())}")
+
+    class Log(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            name = func.overloadpacket.__name__
+            tens = [t for t in torch.utils._pytree.tree_leaves((args, kwargs)) if isinstance(t, torch.Tensor)]
+            if name in skip or not any(t.is_cuda for t in tens) or all(t.numel() == 0 for t in tens):
+                return out
+            node = torch._C._current_autograd_node()
+            if node is not None:
+                site = "backward of " + node.name()
+                if name in ("add", "add_"):  # which input buffer: the node's next functions
+                    nxt = [f.name() for f, _ in node.next_functions if f is not None]
+                    site += " -> " + ",".join(nxt[:4])
+            else:
+                fr = [f for f in traceback.extract_stack() if any(k in f.filename for k in keys)]
+                site = f"{fr[-1].filename.split('/root/repo/')[-1]}:{fr[-1].lineno} {fr[-1].name}" if fr else "(no product frame)"
+            shp = [tuple(t.shape) for t in tens][:2]
+            rows[(str(func), site, str(shp))] += 1
+            return out
+
+    with Log():
+        step()
+        torch.cuda.synchronize()
+    for (fn, site, shp), n in sorted(rows.items(), key=lambda r: (-r[1], r[0])):
+        print(f"{n:4d}  {fn:40s} {site}  {shp}")
+    print(f"total aten ops on the device: {sum(rows.values())}")
 
 
 if __name__ == "__main__":

@@ -463,6 +463,8 @@ def test_dropout_seed_pool_hands_out_distinct_seeds():
     assert len(set(vals)) == 40 and all(s.numel() == 1 and s.dtype == torch.int32 for s in seeds)
     rng.begin_step(DEV)
     assert torch.cat([rng.seed(DEV) for _ in range(40)]).cpu().tolist() != vals
+    rng.end_step()
+    assert rng._pool is None  # later calls draw fresh seeds again
 
 
 @pytest.mark.parametrize("shape", [(32, 48, 32, 32), (3, 5, 7, 9), (2, 1, 4, 4)])
@@ -480,3 +482,42 @@ def test_softmax_channels_vs_fp64(shape):
     (y64 * dy.double()).sum().backward()
     assert rel_l2(y.detach().cpu(), y64) < 1e-6
     assert rel_l2(xd.grad.cpu(), x64.grad) < 1e-5
+
+
+@pytest.mark.parametrize("shapes", [[(4, 64, 16, 16)] * 5, [(3, 56, 32, 32), (3, 160, 32, 32)],
+                                    [(2, 1, 2, 2), (2, 3, 2, 2), (2, 2, 2, 2)],
+                                    [(2, 5, 4, 4)] * 8])
+def test_cat_channels_matches_torch(shapes):
+    """e2ep_cat_channels / e2ep_split_channels (ASPP and UpsamplingConcat concatenation) vs
+    torch.cat and its gradient: bit-exact (pure data movement)."""
+    from e2ep_amd import nn_ops
+    g = _g(len(shapes))
+    xs = [torch.randn(*s, generator=g) for s in shapes]
+    xd = [x.to(DEV).requires_grad_(True) for x in xs]
+    y = nn_ops.cat_channels(xd)
+    assert torch.equal(y.detach().cpu(), torch.cat(xs, 1))
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy.to(DEV))
+    c0 = 0
+    for x, s in zip(xd, shapes):
+        assert x.grad.is_contiguous()
+        assert torch.equal(x.grad.cpu(), dy[:, c0:c0 + s[1]])
+        c0 += s[1]
+
+
+def test_sum3_eq_mask_counters():
+    """e2ep_sum3 = (a + b) + c in fp32 with gradient 1 to each; e2ep_eq_mask_i64 = tok == v on
+    a row-strided token slice; e2ep_add_i64_multi adds to every counter in its table."""
+    from e2ep_amd import _lib, nn_ops
+    a, b, c = (torch.tensor(v, device=DEV, requires_grad=True) for v in (1.1, 2.0e-7, -3.3))
+    s = nn_ops.sum3(a, b, c)
+    assert s.item() == ((torch.tensor(1.1) + torch.tensor(2.0e-7)) + torch.tensor(-3.3)).item()
+    s.backward()
+    assert a.grad.item() == b.grad.item() == c.grad.item() == 1.0
+    tok = torch.randint(0, 5, (6, 15), generator=_g(3))
+    td = tok.to(DEV)[:, 1:]
+    assert torch.equal(nn_ops.eq_mask(td, 2).cpu(), tok[:, 1:] == 2)
+    ctr = [torch.full((), k, dtype=torch.int64, device=DEV) for k in range(300)]
+    table = torch.tensor([t.data_ptr() for t in ctr], dtype=torch.int64, device=DEV)
+    _lib.call("e2ep_add_i64_multi", _lib.ptr(table), len(ctr), 1, _lib.stream())
+    assert [int(t) for t in ctr] == [k + 1 for k in range(300)]
