@@ -120,30 +120,37 @@ def _fusable(mod, query, key, attn_mask, key_padding_mask, is_causal):
 
 
 def mha(mod, query, key, value, attn_mask=None, key_padding_mask=None, is_causal=False,
-        skip=False):
+        skip=False, kv_skip=False):
     """mod(query, key, value, attn_mask=..., key_padding_mask=..., need_weights=False)[0] for a
     seq-first nn.MultiheadAttention, on the fused core when possible.  `is_causal` asserts
     that attn_mask is the causal (-inf above the diagonal) mask, as torch's is_causal hint.
     skip=True returns (out, query_skip): the layer's residual reads query_skip, whose gradient
-    the query projection's input-gradient GEMM accumulates (nn_ops.linear)."""
+    the query projection's input-gradient GEMM accumulates (nn_ops.linear).  kv_skip=True
+    (cross attention, key is value) appends key_skip, to be used as the key/value input of the
+    next consumer (the next decoder layer's memory)."""
+    def ret(out, qs, ks):
+        r = (out,) + ((qs,) if skip else ()) + ((ks,) if kv_skip else ())
+        return r if len(r) > 1 else out
+
     if not _fusable(mod, query, key, attn_mask, key_padding_mask, is_causal):
         out = mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
                   need_weights=False, is_causal=bool(is_causal) and attn_mask is not None)[0]
-        return (out, query) if skip else out
+        return ret(out, query, key)
     E, H = mod.embed_dim, mod.num_heads
     W, bias = mod.in_proj_weight, mod.in_proj_bias
     p = mod.dropout if mod.training else 0.0
     if query is key and key is value:
         qkv, qs = nn_ops.linear(query, W, bias, skip=True)
+        ks = qs  # self attention: one input (kv_skip is for cross attention)
         o = attention(qkv, None, H, is_causal, key_padding_mask, p)
     else:
         if key is not value:
             out = mod(query, key, value, attn_mask=attn_mask, key_padding_mask=key_padding_mask,
                       need_weights=False)[0]
-            return (out, query) if skip else out
+            return ret(out, query, key)
         # one Function over the whole in_proj_weight: its backward writes the q and kv row
         # blocks of dW / db in place (a weight split would concatenate them: 2 cat launches)
-        q, kv, qs = nn_ops.in_proj_qkv(query, key, W, bias, E)
+        q, kv, qs, ks = nn_ops.in_proj_qkv(query, key, W, bias, E)
         o = attention(q, kv, H, is_causal, key_padding_mask, p)
     out = nn_ops.linear(o, mod.out_proj.weight, mod.out_proj.bias)
-    return (out, qs) if skip else out
+    return ret(out, qs, ks)

@@ -821,10 +821,10 @@ class _InProjQKV(torch.autograd.Function):
         kv = gemm(xkv2, True, Wkv, True, xkv2.shape[0], 2 * E, K, bias=bkv, tag="linear_fwd")
         ctx.save_for_backward(xq2, xkv2, weight)
         ctx.E, ctx.has_bias, ctx.shapes = E, bias is not None, (xq.shape, xkv.shape)
-        return q.view(*xq.shape[:-1], E), kv.view(*xkv.shape[:-1], 2 * E), xq
+        return q.view(*xq.shape[:-1], E), kv.view(*xkv.shape[:-1], 2 * E), xq, xkv
 
     @staticmethod
-    def backward(ctx, gq, gkv, gskip):
+    def backward(ctx, gq, gkv, gskip, gskip_kv):
         xq2, xkv2, weight = ctx.saved_tensors
         nig = ctx.needs_input_grad
         E = ctx.E
@@ -834,7 +834,7 @@ class _InProjQKV(torch.autograd.Function):
         dxq, _, _ = _linear_bwd(_rows2(gq), xq2, weight[:E], nig[0], nig[2], want_b, gskip,
                                 dw[:E] if dw is not None else None,
                                 db[:E] if db is not None else None)
-        dxkv, _, _ = _linear_bwd(_rows2(gkv), xkv2, weight[E:], nig[1], nig[2], want_b, None,
+        dxkv, _, _ = _linear_bwd(_rows2(gkv), xkv2, weight[E:], nig[1], nig[2], want_b, gskip_kv,
                                  dw[E:] if dw is not None else None,
                                  db[E:] if db is not None else None)
         sq, skv = ctx.shapes
@@ -843,7 +843,9 @@ class _InProjQKV(torch.autograd.Function):
 
 
 def in_proj_qkv(xq, xkv, weight, bias, E):
-    """(q, kv, xq_skip) of a cross-attention in-projection (see _InProjQKV)."""
+    """(q, kv, xq_skip, xkv_skip) of a cross-attention in-projection (see _InProjQKV):
+    xkv_skip carries the key/value input on to another consumer (the next decoder layer's
+    memory), its gradient joining dxkv in the GEMM epilogue."""
     _dev(xq, xkv, weight, bias)
     return _InProjQKV.apply(xq, xkv, weight, bias, int(E))
 

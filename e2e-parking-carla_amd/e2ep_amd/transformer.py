@@ -42,16 +42,18 @@ def encoder_layer(layer, x, mask=None, key_padding_mask=None):
 
 
 def decoder_layer(layer, x, memory, tgt_mask=None, tgt_key_padding_mask=None, tgt_is_causal=False):
-    """torch.nn.TransformerDecoderLayer.forward (norm_first=False), seq-first."""
+    """torch.nn.TransformerDecoderLayer.forward (norm_first=False), seq-first.  Returns
+    (out, memory_skip): the next layer reads memory_skip, so the memory's gradients from all
+    layers are summed in the in-projection GEMM epilogues (no autograd adds)."""
     assert not layer.norm_first
     sa, x = attention.mha(layer.self_attn, x, x, x, attn_mask=tgt_mask,
                           key_padding_mask=tgt_key_padding_mask, is_causal=bool(tgt_is_causal),
                           skip=True)
     x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
-    ca, x = attention.mha(layer.multihead_attn, x, memory, memory, skip=True)
+    ca, x, memory = attention.mha(layer.multihead_attn, x, memory, memory, skip=True, kv_skip=True)
     x = nn_ops.add_drop_layer_norm(x, ca, layer.norm2, _p(layer.dropout2, layer.training))
     ff, x = _ff(layer, x)
-    return nn_ops.add_drop_layer_norm(x, ff, layer.norm3, _p(layer.dropout3, layer.training))
+    return nn_ops.add_drop_layer_norm(x, ff, layer.norm3, _p(layer.dropout3, layer.training)), memory
 
 
 def encoder(stack, tokens):
@@ -67,7 +69,7 @@ def encoder(stack, tokens):
 def decoder(stack, tgt, memory, tgt_mask, tgt_key_padding_mask, tgt_is_causal=None):
     x, mem = tgt.transpose(0, 1), memory.transpose(0, 1)
     for layer in stack.layers:
-        x = decoder_layer(layer, x, mem, tgt_mask, tgt_key_padding_mask, tgt_is_causal)
+        x, mem = decoder_layer(layer, x, mem, tgt_mask, tgt_key_padding_mask, tgt_is_causal)
     if stack.norm is not None:
         x = stack.norm(x)
     return x.transpose(0, 1)

@@ -27,10 +27,9 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        if self.downsample is None and x.is_cuda:  # identity skip: its gradient joins conv1's dgrad
-            c1, x = ops.conv2d(x, self.conv1.weight, None, self.stride, 1, skip=True)
-        else:
-            c1 = ops.conv2d(x, self.conv1.weight, None, self.stride, 1)
+        # identity skip, or the downsample conv's input: x is conv1's skip alias either way, so
+        # its second gradient joins conv1's data gradient in the epilogue (no autograd add)
+        c1, x = ops.conv2d(x, self.conv1.weight, None, self.stride, 1, skip=True)
         y = ops.bn_act(c1, self.bn1, "relu")
         if self.downsample is not None:
             x = ops.bn_act(ops.conv2d(x, self.downsample[0].weight, None, self.stride, 0),

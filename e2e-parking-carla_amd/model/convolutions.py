@@ -45,7 +45,16 @@ class ASPP(nn.Module):
         self.project = nn.Sequential(*_conv_bn(len(mods) * cout, cout, 1), nn.Dropout(p_drop))
 
     def forward(self, x):
-        branches = [_run_conv_bn_relu(self.convs[0], x)] + [m(x) for m in self.convs[1:]]
+        # x feeds five branches: it is threaded through the four conv branches as each conv's
+        # skip alias (e2ep_amd.conv.conv2d skip=True), so its gradient is summed inside the
+        # branch convs' data-gradient epilogues instead of by four autograd adds
+        branches = []
+        for m in self.convs[:-1]:
+            conv, bn = m[0], m[1]
+            c, x = ops.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation,
+                              skip=True)
+            branches.append(ops.bn_act(c, bn, "relu"))
+        branches.append(self.convs[-1](x))
         y = _run_conv_bn_relu(self.project, nn_ops.cat_channels(branches))
         # Dropout(0.5) after the project BN-ReLU (reference model/convolutions.py:264): y >= 0,
         # so dropout(y) = dropout(relu(y)) runs on the fused ReLU-dropout kernel, one launch

@@ -65,9 +65,17 @@ class MBConv(nn.Module):
         self._project_conv = SameConv(mid, cout, 1, bias=False, size=math.ceil(size / stride))
         self._bn2 = nn.BatchNorm2d(cout, momentum=0.01, eps=1e-3)
 
-    def forward(self, x, drop_connect_rate=None, dc_rand=None):
+    def forward(self, x, drop_connect_rate=None, dc_rand=None, alias=False):
         """dc_rand: this block's per-sample uniform draws for drop-connect (training); drawn
-        here when not given (efficientnet-pytorch draws torch.rand([N,1,1,1]) per block)."""
+        here when not given (efficientnet-pytorch draws torch.rand([N,1,1,1]) per block).
+        alias=True (blocks with an expand conv): returns (out, x_alias), x_alias being the
+        expand conv's skip alias of x for another consumer of x (a trunk endpoint)."""
+        if alias:
+            assert self.expand != 1 and not self.skip
+            e, xa = self._expand_conv.forward_skip(x)
+            y = ops.bn_act_depthwise(e, self._bn0, "swish", self._depthwise_conv)
+            y = ops.bn_swish_squeeze_excite(y, self._bn1, self._se_reduce, self._se_expand)
+            return ops.bn_act(self._project_conv(y), self._bn2, None), xa
         if self.expand != 1:  # _bn0 + swish applied inside the depthwise conv's input load
             if self.skip and x.is_cuda:
                 e, x = self._expand_conv.forward_skip(x)
@@ -117,8 +125,14 @@ class EfficientNetTrunk(nn.Module):
         u = (torch.rand(n, x.shape[0], dtype=x.dtype, device=x.device)
              if self.training and self.drop_connect_rate else None)
         for i, blk in enumerate(self._blocks):
-            x = blk(x, self.drop_connect_rate * i / n if self.drop_connect_rate else None,
-                    None if u is None else u[i])
+            dcr = self.drop_connect_rate * i / n if self.drop_connect_rate else None
+            ui = None if u is None else u[i]
+            if blk.stride > 1 and blk.expand != 1 and not blk.skip:
+                # x is an endpoint and this block's input: the endpoint is the expand conv's
+                # skip alias, so the two gradients of x meet in that conv's dgrad epilogue
+                x, prev = blk(x, dcr, ui, alias=True)
+            else:
+                x = blk(x, dcr, ui)
             if prev.shape[2] > x.shape[2]:
                 ends.append(prev)
             prev = x
