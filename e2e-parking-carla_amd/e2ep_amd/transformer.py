@@ -31,45 +31,52 @@ def _ff(layer, x):
     return nn_ops.linear(h, layer.linear2.weight, layer.linear2.bias), xs
 
 
-def encoder_layer(layer, x, mask=None, key_padding_mask=None):
-    """torch.nn.TransformerEncoderLayer.forward (norm_first=False), seq-first x (S, B, E)."""
+def encoder_layer(layer, x, mask=None, key_padding_mask=None, batch_first=False):
+    """torch.nn.TransformerEncoderLayer.forward (norm_first=False), seq-first x (S, B, E), or
+    (B, S, E) with batch_first (the same math: the linears and LayerNorms are row-wise)."""
     assert not layer.norm_first
     sa, x = attention.mha(layer.self_attn, x, x, x, attn_mask=mask,
-                          key_padding_mask=key_padding_mask, skip=True)
+                          key_padding_mask=key_padding_mask, skip=True, batch_first=batch_first)
     x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
     ff, x = _ff(layer, x)
     return nn_ops.add_drop_layer_norm(x, ff, layer.norm2, _p(layer.dropout2, layer.training))
 
 
-def decoder_layer(layer, x, memory, tgt_mask=None, tgt_key_padding_mask=None, tgt_is_causal=False):
+def decoder_layer(layer, x, memory, tgt_mask=None, tgt_key_padding_mask=None, tgt_is_causal=False,
+                  batch_first=False):
     """torch.nn.TransformerDecoderLayer.forward (norm_first=False), seq-first.  Returns
     (out, memory_skip): the next layer reads memory_skip, so the memory's gradients from all
     layers are summed in the in-projection GEMM epilogues (no autograd adds)."""
     assert not layer.norm_first
     sa, x = attention.mha(layer.self_attn, x, x, x, attn_mask=tgt_mask,
                           key_padding_mask=tgt_key_padding_mask, is_causal=bool(tgt_is_causal),
-                          skip=True)
+                          skip=True, batch_first=batch_first)
     x = nn_ops.add_drop_layer_norm(x, sa, layer.norm1, _p(layer.dropout1, layer.training))
-    ca, x, memory = attention.mha(layer.multihead_attn, x, memory, memory, skip=True, kv_skip=True)
+    ca, x, memory = attention.mha(layer.multihead_attn, x, memory, memory, skip=True, kv_skip=True,
+                                  batch_first=batch_first)
     x = nn_ops.add_drop_layer_norm(x, ca, layer.norm2, _p(layer.dropout2, layer.training))
     ff, x = _ff(layer, x)
     return nn_ops.add_drop_layer_norm(x, ff, layer.norm3, _p(layer.dropout3, layer.training)), memory
 
 
 def encoder(stack, tokens):
-    """tokens (B, S, E) batch-first -> (B, S, E); the reference runs the stack seq-first."""
-    x = tokens.transpose(0, 1)
+    """tokens (B, S, E) batch-first -> (B, S, E).  The reference runs the stack seq-first; here
+    the layers run batch-first on the same rows (no transposed copies of the activations or
+    their gradients: the attention kernels take (sequence, batch) strides)."""
+    x = tokens
     for layer in stack.layers:
-        x = encoder_layer(layer, x)
+        x = encoder_layer(layer, x, batch_first=True)
     if stack.norm is not None:
         x = stack.norm(x)
-    return x.transpose(0, 1)
+    return x
 
 
 def decoder(stack, tgt, memory, tgt_mask, tgt_key_padding_mask, tgt_is_causal=None):
-    x, mem = tgt.transpose(0, 1), memory.transpose(0, 1)
+    """tgt (B, T, E), memory (B, S, E) batch-first -> (B, T, E) (see encoder)."""
+    x, mem = tgt, memory
     for layer in stack.layers:
-        x, mem = decoder_layer(layer, x, mem, tgt_mask, tgt_key_padding_mask, tgt_is_causal)
+        x, mem = decoder_layer(layer, x, mem, tgt_mask, tgt_key_padding_mask, tgt_is_causal,
+                               batch_first=True)
     if stack.norm is not None:
         x = stack.norm(x)
-    return x.transpose(0, 1)
+    return x
