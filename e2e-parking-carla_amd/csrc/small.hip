@@ -1,7 +1,9 @@
 // Step bookkeeping and layout kernels that replaced the last PyTorch-native launches of the
 // train step: channel concatenation / split (torch.cat of the ASPP branches and the
 // UpsamplingConcat inputs, and its backward's slice copies), the sum of the three losses,
-// the decoder's PAD-key mask and the BatchNorm num_batches_tracked counters.
+// the decoder's PAD-key mask, the BatchNorm num_batches_tracked counters, the gradient sum of
+// a two-consumer activation and the step's random draws (dropout seeds, drop-connect, target
+// noise) in one launch.
 #include "common.h"
 
 namespace e2ep {
@@ -38,6 +40,18 @@ __global__ void k_cat_channels(CatPlan pl, int N, long long HW4, float4 *cat, in
     cat[i] = reinterpret_cast<const float4 *>(pl.src[j])[off];
 }
 
+// out = a + b elementwise (the gradient of a tensor read by two consumers, nn_ops.fork2)
+__global__ void k_add_f32x4(const float4 *a, const float4 *b, long long n4, float4 *out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const float4 x = a[i], y = b[i];
+  out[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+}
+__global__ void k_add_f32(const float *a, const float *b, long long n, float *out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
 __global__ void k_sum3(const float *a, const float *b, const float *c, float *out) {
   if (threadIdx.x == 0) out[0] = __fadd_rn(__fadd_rn(a[0], b[0]), c[0]);  // (a + b) + c
 }
@@ -53,6 +67,32 @@ __global__ void k_eq_mask_i64(const int64_t *tok, long long rstride, int B, int 
 __global__ void k_add_i64_multi(const long long *table, int n, long long v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) *reinterpret_cast<long long *>(table[i]) += v;
+}
+
+// Counter-based step draws: value i of draw number `state[1]` is a splitmix64 hash of
+// (state[0], state[1], i); floats take the top 24 bits (uniform on [0, 1)), ints the top 31.
+// One block: every thread reads the counter before thread 0 advances it, so each launch (or
+// graph replay) draws fresh values.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(1024) k_rng_draw(long long *state, int nf, float *f, int ni,
+                                                   int *iv) {
+  const unsigned long long seed = (unsigned long long)state[0];
+  const unsigned long long ctr = (unsigned long long)state[1];
+  const unsigned long long base = mix64(seed ^ mix64(ctr));
+  for (int i = threadIdx.x; i < nf + ni; i += blockDim.x) {
+    const unsigned long long h = mix64(base + (unsigned long long)i);
+    if (i < nf)
+      f[i] = (float)(h >> 40) * 0x1p-24f;
+    else
+      iv[i - nf] = (int)(h >> 33);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) state[1] = (long long)(ctr + 1);
 }
 
 static int cat_plan(const int *chans, int n, int N, long long HW, CatPlan &pl, const char *who) {
@@ -105,6 +145,18 @@ int e2ep_split_channels(const float *src, const int *chans, int n, int N, long l
   return launch_status("e2ep_split_channels");
 }
 
+int e2ep_add_f32(const float *a, const float *b, long long n, float *out, void *stream) {
+  E2EP_REQUIRE(n >= 0, E2EP_EINVAL, "e2ep_add_f32: n < 0");
+  if (n == 0) return 0;
+  if (n % 4 == 0 && (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15) == 0)
+    hipLaunchKernelGGL(k_add_f32x4, dim3(cdiv(n / 4, 256)), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const float4 *>(a), reinterpret_cast<const float4 *>(b),
+                       n / 4, reinterpret_cast<float4 *>(out));
+  else
+    hipLaunchKernelGGL(k_add_f32, dim3(cdiv(n, 256)), dim3(256), 0, as_stream(stream), a, b, n, out);
+  return launch_status("e2ep_add_f32");
+}
+
 int e2ep_sum3(const float *a, const float *b, const float *c, float *out, void *stream) {
   hipLaunchKernelGGL(k_sum3, dim3(1), dim3(64), 0, as_stream(stream), a, b, c, out);
   return launch_status("e2ep_sum3");
@@ -117,6 +169,13 @@ int e2ep_eq_mask_i64(const int64_t *tok, long long rstride, int B, int T, int64_
   hipLaunchKernelGGL(k_eq_mask_i64, dim3(cdiv(B * T, 256)), dim3(256), 0, as_stream(stream), tok,
                      rstride, B, T, value, mask);
   return launch_status("e2ep_eq_mask_i64");
+}
+
+int e2ep_rng_draw(long long *state, int nf, float *f, int ni, int *iv, void *stream) {
+  E2EP_REQUIRE(nf >= 0 && ni >= 0 && (nf == 0 || f) && (ni == 0 || iv), E2EP_EINVAL,
+               "e2ep_rng_draw: bad arguments");
+  hipLaunchKernelGGL(k_rng_draw, dim3(1), dim3(1024), 0, as_stream(stream), state, nf, f, ni, iv);
+  return launch_status("e2ep_rng_draw");
 }
 
 int e2ep_add_i64_multi(const long long *table, int n, long long v, void *stream) {

@@ -61,6 +61,8 @@ SIGNATURES = {
     "e2ep_cat_channels": (_i, [_p, _p, _i, _i, _i64, _p, _p]),
     "e2ep_split_channels": (_i, [_p, _p, _i, _i, _i64, _p, _p]),
     "e2ep_sum3": (_i, [_p, _p, _p, _p, _p]),
+    "e2ep_add_f32": (_i, [_p, _p, _i64, _p, _p]),
+    "e2ep_rng_draw": (_i, [_p, _i, _p, _i, _p, _p]),
     "e2ep_eq_mask_i64": (_i, [_p, _i64, _i, _i, _i64, _p, _p]),
     "e2ep_add_i64_multi": (_i, [_p, _i, _i64, _p]),
     "e2ep_resize_fwd": (_i, [_p, _i, _i, _i64, _i, _i, _i, _i, _f, _f, _p, _i64, _p]),

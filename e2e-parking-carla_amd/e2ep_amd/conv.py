@@ -219,6 +219,9 @@ class _Conv2d(torch.autograd.Function):
         ctx.save_for_backward(x, wt, y if act else None)
         ctx.wshape = w.shape
         ctx.skip = skip
+        # an unused skip alias (a trunk endpoint nobody reads) arrives as None, not as a
+        # zero-filled gradient
+        ctx.set_materialize_grads(False)
         # skip: also hand x back, so the block's skip connection reads it from here and its
         # gradient arrives in this backward, where the data-gradient epilogue adds it
         return (y, x) if skip else y

@@ -604,6 +604,56 @@ def cat_channels(xs):
     return _CatChannels.apply(*xs)
 
 
+class _Transpose12(torch.autograd.Function):
+    """(B, R, C) -> (B, C, R) contiguous with e2ep_transpose each way."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        B, R, C = x.shape
+        out = torch.empty(B, C, R, dtype=torch.float32, device=x.device)
+        _lib.call("e2ep_transpose", _lib.ptr(x), R * C, B, R, C, _lib.ptr(out), _lib.stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        B, C, R = g.shape
+        dx = torch.empty(B, R, C, dtype=torch.float32, device=g.device)
+        _lib.call("e2ep_transpose", _lib.ptr(g), R * C, B, C, R, _lib.ptr(dx), _lib.stream())
+        return dx
+
+
+def transpose12(x):
+    """x.transpose(1, 2).contiguous() of a (B, R, C) fp32 device tensor, one e2ep launch each
+    way (the fusion tokens -> BEV map hand-off to the segmentation head)."""
+    _dev(x)
+    return _Transpose12.apply(x)
+
+
+class _Fork2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        if g1 is None or g2 is None:
+            return g2 if g1 is None else g1
+        g1, g2 = g1.contiguous(), g2.contiguous()
+        out = torch.empty_like(g1)
+        _lib.call("e2ep_add_f32", _lib.ptr(g1), _lib.ptr(g2), g1.numel(), _lib.ptr(out),
+                  _lib.stream())
+        return out
+
+
+def fork2(x):
+    """Two handles of x for two consumers; their gradients are summed by one e2ep launch
+    (autograd would sum them with a PyTorch add kernel)."""
+    _dev(x)
+    return _Fork2.apply(x)
+
+
 class _Sum3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, b, c):
@@ -821,6 +871,7 @@ class _InProjQKV(torch.autograd.Function):
         kv = gemm(xkv2, True, Wkv, True, xkv2.shape[0], 2 * E, K, bias=bkv, tag="linear_fwd")
         ctx.save_for_backward(xq2, xkv2, weight)
         ctx.E, ctx.has_bias, ctx.shapes = E, bias is not None, (xq.shape, xkv.shape)
+        ctx.set_materialize_grads(False)  # unused aliases (the last layer's memory) stay None
         return q.view(*xq.shape[:-1], E), kv.view(*xkv.shape[:-1], 2 * E), xq, xkv
 
     @staticmethod

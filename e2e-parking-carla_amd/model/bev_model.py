@@ -94,7 +94,10 @@ class BevModel(nn.Module):
     def calc_bev_feature(self, images, intrinsics, extrinsics, extra_channels=0):
         plan = self.plan(intrinsics, extrinsics, images.device)
         feat, prob = self.encoder_forward(images)
-        bev = lss.lift_splat(prob, feat, plan, feat.shape[1] + extra_channels)
+        # prob feeds the lift-splat and the depth loss: two handles whose gradients one e2ep
+        # launch sums (nn_ops.fork2)
+        prob_lss, prob = nn_ops.fork2(prob) if prob.is_cuda else (prob, prob)
+        bev = lss.lift_splat(prob_lss, feat, plan, feat.shape[1] + extra_channels)
         return bev, prob
 
     def forward(self, images, intrinsics, extrinsics):

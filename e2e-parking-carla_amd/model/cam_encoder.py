@@ -6,6 +6,7 @@ import math
 
 from torch import nn
 
+from e2ep_amd import nn_ops
 from model.convolutions import DeepLabHead, UpsamplingConcat
 from model.efficientnet import EfficientNetTrunk
 
@@ -37,10 +38,15 @@ class CamEncoder(nn.Module):
     def get_features_depth(self, x):
         ends = self.backbone(x)
         deep, skip = ends[self.index], ends[self.index - 1]
-        feature = self.feature_layer_2(self.feature_layer_1(deep), skip)
         depth = None
         if self.use_depth_distribution:
-            depth = self.depth_layer_2(self.depth_layer_1(deep), skip)
+            # both heads read deep and skip: two handles each, gradients summed by one e2ep
+            # launch (nn_ops.fork2)
+            deep, deep_d = nn_ops.fork2(deep)
+            skip, skip_d = nn_ops.fork2(skip)
+        feature = self.feature_layer_2(self.feature_layer_1(deep), skip)
+        if self.use_depth_distribution:
+            depth = self.depth_layer_2(self.depth_layer_1(deep_d), skip_d)
         return feature, depth
 
     def forward(self, x):

@@ -12,7 +12,7 @@ import math
 import torch
 from torch import nn
 
-from e2ep_amd import ops
+from e2ep_amd import nn_ops, ops, rng
 
 # b0 base stages: (repeats, kernel, stride, expand, in, out); b4 scales width 1.4 / depth 1.8
 _STAGES = [(1, 3, 1, 1, 32, 16), (2, 3, 2, 6, 16, 24), (2, 5, 2, 6, 24, 40), (3, 3, 2, 6, 40, 80),
@@ -82,6 +82,9 @@ class MBConv(nn.Module):
             else:
                 e = self._expand_conv(x)
             y = ops.bn_act_depthwise(e, self._bn0, "swish", self._depthwise_conv)
+        elif self.skip and x.is_cuda:  # x feeds the depthwise conv and the skip (nn_ops.fork2)
+            xd, x = nn_ops.fork2(x)
+            y = self._depthwise_conv(xd)
         else:
             y = self._depthwise_conv(x)
         y = ops.bn_swish_squeeze_excite(y, self._bn1, self._se_reduce, self._se_expand)
@@ -122,7 +125,8 @@ class EfficientNetTrunk(nn.Module):
         ends, prev = [], x
         n = len(self._blocks)
         # all blocks' drop-connect draws in one launch (one row of N per block)
-        u = (torch.rand(n, x.shape[0], dtype=x.dtype, device=x.device)
+        # (from the step's uniform pool, e2ep_amd.rng, inside a training forward)
+        u = (rng.uniform((n, x.shape[0]), x.device, x.dtype)
              if self.training and self.drop_connect_rate else None)
         for i, blk in enumerate(self._blocks):
             dcr = self.drop_connect_rate * i / n if self.drop_connect_rate else None

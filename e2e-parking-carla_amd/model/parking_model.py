@@ -29,8 +29,8 @@ class ParkingModel(nn.Module):
         self.segmentation_head = SegmentationHead(self.cfg)
 
     def _noise(self, b, device, noise):
-        if noise is None:
-            return torch.rand((b, 2), dtype=torch.float, device=device)
+        if noise is None:  # the step's uniform pool inside a training forward (e2ep_amd.rng)
+            return rng.uniform((b, 2), device)
         return noise
 
     def add_target_bev(self, bev_feature, target_point, noise=None):
@@ -73,7 +73,9 @@ class ParkingModel(nn.Module):
                        self.cfg.bev_x_bound[2], self.cfg.bev_y_bound[2])
         bev_down_sample = self.bev_encoder.forward_split(bev, bev_target)
         fuse_feature = self.feature_fusion(bev_down_sample, ego_motion)
-        pred_segmentation = self.segmentation_head(fuse_feature)
+        # fuse_feature feeds the segmentation head and the control decoder (nn_ops.fork2)
+        fuse_seg, fuse_feature = nn_ops.fork2(fuse_feature)
+        pred_segmentation = self.segmentation_head(fuse_seg)
         return fuse_feature, pred_segmentation, pred_depth, bev_target
 
     def forward(self, data, noise=None):

@@ -261,6 +261,9 @@ int e2ep_cat_channels(const float *const *srcs, const int *chans, int n, int N, 
                       float *dst, void *stream);
 int e2ep_split_channels(const float *src, const int *chans, int n, int N, long long HW,
                         float *const *dsts, void *stream);
+/* out[i] = a[i] + b[i], i < n (fp32): the gradient of an activation read by two consumers
+ * (nn_ops.fork2), in place of autograd's accumulation. */
+int e2ep_add_f32(const float *a, const float *b, long long n, float *out, void *stream);
 /* out[0] = (a[0] + b[0]) + c[0] in fp32: the training loss (trainer/pl_trainer.py:57-59,
  * control + segmentation + depth) as one launch. */
 int e2ep_sum3(const float *a, const float *b, const float *c, float *out, void *stream);
@@ -268,6 +271,13 @@ int e2ep_sum3(const float *a, const float *b, const float *c, float *out, void *
  * (model/control_predict.py create_mask, tgt == pad_idx) on int64 tokens. */
 int e2ep_eq_mask_i64(const int64_t *tok, long long rstride, int B, int T, int64_t value,
                      uint8_t *mask, void *stream);
+/* One launch of the step's random draws: f[0..nf) uniform on [0, 1) (24-bit), iv[0..ni) uniform
+ * on [0, 2^31), value i a splitmix64 hash of (state[0] = seed, state[1] = draw counter, i);
+ * the kernel then advances state[1], so every launch or graph replay draws fresh values.
+ * Replaces torch.rand / torch.randint draws of a training forward (the drop-connect uniforms
+ * of efficientnet-pytorch's MBConv, the target noise of model/parking_model.py:36, the dropout
+ * seed pool of e2ep_amd/rng.py).  nf + ni <= any; one workgroup. */
+int e2ep_rng_draw(long long *state, int nf, float *f, int ni, int *iv, void *stream);
 /* *(int64 *)table[i] += v for i < n (device table of device addresses): every BatchNorm's
  * num_batches_tracked increment of a forward (torch.nn.BatchNorm2d) in one launch. */
 int e2ep_add_i64_multi(const long long *table, int n, long long v, void *stream);

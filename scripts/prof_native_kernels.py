@@ -53,7 +53,8 @@ def main():
         def __torch_dispatch__(self, func, types, args=(), kwargs=None):
             out = func(*args, **(kwargs or {}))
             name = func.overloadpacket.__name__
-            tens = [t for t in torch.utils._pytree.tree_leaves((args, kwargs)) if isinstance(t, torch.Tensor)]
+            tens = [t for t in torch.utils._pytree.tree_leaves((args, kwargs, out))
+                    if isinstance(t, torch.Tensor)]
             if name in skip or not any(t.is_cuda for t in tens) or all(t.numel() == 0 for t in tens):
                 return out
             node = torch._C._current_autograd_node()

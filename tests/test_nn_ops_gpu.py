@@ -521,3 +521,41 @@ def test_sum3_eq_mask_counters():
     table = torch.tensor([t.data_ptr() for t in ctr], dtype=torch.int64, device=DEV)
     _lib.call("e2ep_add_i64_multi", _lib.ptr(table), len(ctr), 1, _lib.stream())
     assert [int(t) for t in ctr] == [k + 1 for k in range(300)]
+
+
+def test_step_rng_draws():
+    """e2ep_rng_draw: uniform floats in [0, 1) and non-negative int32 seeds, distinct between
+    consecutive launches and between graph replays (the kernel advances its own counter)."""
+    from e2ep_amd import _lib, rng
+    st = torch.tensor([12345, 0], dtype=torch.int64, device=DEV)
+    f = torch.empty(4096, device=DEV)
+    iv = torch.empty(64, dtype=torch.int32, device=DEV)
+
+    def draw():
+        _lib.call("e2ep_rng_draw", _lib.ptr(st), f.numel(), _lib.ptr(f), iv.numel(), _lib.ptr(iv),
+                  _lib.stream())
+
+    draw()
+    a, ai = f.clone(), iv.clone()
+    assert 0.0 <= float(a.min()) and float(a.max()) < 1.0 and abs(float(a.mean()) - 0.5) < 0.03
+    assert int(ai.min()) >= 0 and len(set(ai.tolist())) == 64
+    draw()
+    assert not torch.equal(a, f) and int(st[1]) == 2
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            draw()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
+    b = f.clone()
+    g.replay()
+    assert not torch.equal(b, f) and int(st[1]) == 4
+    # the module-level pools: views of one launch, retired by end_step
+    rng.begin_step(DEV)
+    u = rng.uniform((22, 32), DEV)
+    v = rng.uniform((8, 2), DEV)
+    assert u.shape == (22, 32) and v.shape == (8, 2) and u.data_ptr() != v.data_ptr()
+    rng.end_step()
+    assert rng.uniform((3,), DEV).shape == (3,)
