@@ -257,12 +257,13 @@ __device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, i
 // The same staging split in two for software pipelining: dw_fetch issues a unit's row loads
 // into registers (at most DW_MAXV float4 per lane), dw_put writes them (normalised) and the
 // halo zeros into LDS once they have landed.
+template <int V>
 __device__ __forceinline__ void dw_fetch(const float *__restrict__ src, int H, int W, int iy0,
-                                         int IR, int lane, float4 (&r)[DW_MAXV], bool active) {
+                                         int IR, int lane, float4 (&r)[V], bool active) {
   const int W4 = W >> 2;
   const __amdgpu_buffer_rsrc_t rs = rsrc_u(src, 4LL * H * W);
 #pragma unroll
-  for (int i = 0; i < DW_MAXV; ++i) {
+  for (int i = 0; i < V; ++i) {
     const int e = lane + 64 * i;
     const int rr = e / W4, j = e - rr * W4;
     const int iy = iy0 + rr;
@@ -270,11 +271,12 @@ __device__ __forceinline__ void dw_fetch(const float *__restrict__ src, int H, i
     r[i] = bload4(rs, ok ? (iy * W + 4 * j) * 4 : OOR);  // branch-free (see dw_stage)
   }
 }
-__device__ __forceinline__ void dw_put(const float4 (&r)[DW_MAXV], int H, int W, int iy0, int IR,
+template <int V>
+__device__ __forceinline__ void dw_put(const float4 (&r)[V], int H, int W, int iy0, int IR,
                                        int WP, float *lds, int lane, const DwT &t) {
   const int W4 = W >> 2;
 #pragma unroll
-  for (int i = 0; i < DW_MAXV; ++i) {
+  for (int i = 0; i < V; ++i) {
     const int e = lane + 64 * i;
     if (e >= IR * W4) break;
     const int rr = e / W4, j = e - rr * W4;
@@ -317,7 +319,9 @@ __device__ __forceinline__ void dw_row(const float *base, float (&v)[NV]) {
   }
 }
 
-template <int K, int ST, bool FLIP, int OFF>
+// V: float4 per lane that hold a unit's staged rows (2 or DW_MAXV; the host picks the
+// smallest that covers IR * W / 4, so short units keep fewer registers and more waves resident)
+template <int K, int ST, bool FLIP, int OFF, int V>
 __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
                                                       const float *__restrict__ w, DwGeom g,
                                                       DwStrip d, int units, float *__restrict__ y,
@@ -340,7 +344,7 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
     nc = un / d.units_per_plane;
     oy0 = (un - nc * d.units_per_plane) * d.RO;
   };
-  float4 rx[DW_MAXV];
+  float4 rx[V];
   if (u < units) unit_of(u);
   dw_fetch(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, lane, rx, u < units);
   for (; u < units; u += step) {
@@ -426,7 +430,7 @@ __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restri
 // weight gradient partials over strip units: grid (C, splits); the block's waves walk the
 // channel's units (n, strip) of its slice; per lane K*K register accumulators, fixed-order
 // wave + block reduction.
-template <int K, int ST, int OFF>
+template <int K, int ST, int OFF, int V>
 __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
                                                         const float *__restrict__ x, DwGeom g,
                                                         DwStrip d, int splits,
@@ -453,7 +457,7 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
     n = un / d.units_per_plane;
     oy0 = (un - n * d.units_per_plane) * d.RO;
   };
-  float4 rx[DW_MAXV];
+  float4 rx[V];
   float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
   const __amdgpu_buffer_rsrc_t rgy = rsrc(gy, 4LL * g.N * g.C * g.P * g.Q);
   int n = 0, oy0 = 0;
@@ -548,30 +552,52 @@ using namespace e2ep;
 static int dw_fwd_blocks(int units) { return std::min(cdiv(units, 4), g_tune[TUNE_DW_FWD_BLOCKS]); }
 static int dw_off(int pl) { return g_tune[TUNE_DW_VEC] == 1 ? -1 : ((-pl) & 3); }
 
-// launch a strip kernel with the row-read variant `off` as its compile-time OFF
-template <int K, int ST, bool FLIP>
-static void dw_fwd_strip(int off, dim3 grid, size_t shm, hipStream_t st, const float *x,
-                         const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf) {
+// launch a strip kernel with the row-read variant `off` as its compile-time OFF and the
+// staging registers V = 2 float4 per lane when `nv` (float4 per lane a unit needs) allows
+// (the scalar-read variant, an A/B switch, always takes DW_MAXV)
+template <int K, int ST, bool FLIP, int V>
+static void dw_fwd_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *x,
+                           const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf) {
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, x, w, g, d, units, y, tf); };
   switch (off) {
-    case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0>); break;
-    case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1>); break;
-    case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2>); break;
-    case 3: go(k_dw_fwd_strip<K, ST, FLIP, 3>); break;
-    default: go(k_dw_fwd_strip<K, ST, FLIP, -1>);
+    case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V>); break;
+    case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V>); break;
+    case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2, V>); break;
+    default: go(k_dw_fwd_strip<K, ST, FLIP, 3, V>);
+  }
+}
+template <int K, int ST, bool FLIP>
+static void dw_fwd_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const float *x,
+                         const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf) {
+  if (off < 0)
+    hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV>), grid, dim3(256), shm, st, x, w,
+                       g, d, units, y, tf);
+  else if (nv <= 2)
+    dw_fwd_strip_v<K, ST, FLIP, 2>(off, grid, shm, st, x, w, g, d, units, y, tf);
+  else
+    dw_fwd_strip_v<K, ST, FLIP, DW_MAXV>(off, grid, shm, st, x, w, g, d, units, y, tf);
+}
+template <int K, int ST, int V>
+static void dw_wgrad_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *gy,
+                             const float *x, DwGeom g, DwStrip d, int splits, float *part, DwIn tf) {
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, gy, x, g, d, splits, part, tf); };
+  switch (off) {
+    case 0: go(k_dw_wgrad_strip<K, ST, 0, V>); break;
+    case 1: go(k_dw_wgrad_strip<K, ST, 1, V>); break;
+    case 2: go(k_dw_wgrad_strip<K, ST, 2, V>); break;
+    default: go(k_dw_wgrad_strip<K, ST, 3, V>);
   }
 }
 template <int K, int ST>
-static void dw_wgrad_strip(int off, dim3 grid, size_t shm, hipStream_t st, const float *gy,
+static void dw_wgrad_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const float *gy,
                            const float *x, DwGeom g, DwStrip d, int splits, float *part, DwIn tf) {
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, gy, x, g, d, splits, part, tf); };
-  switch (off) {
-    case 0: go(k_dw_wgrad_strip<K, ST, 0>); break;
-    case 1: go(k_dw_wgrad_strip<K, ST, 1>); break;
-    case 2: go(k_dw_wgrad_strip<K, ST, 2>); break;
-    case 3: go(k_dw_wgrad_strip<K, ST, 3>); break;
-    default: go(k_dw_wgrad_strip<K, ST, -1>);
-  }
+  if (off < 0)
+    hipLaunchKernelGGL((k_dw_wgrad_strip<K, ST, -1, DW_MAXV>), grid, dim3(256), shm, st, gy, x, g,
+                       d, splits, part, tf);
+  else if (nv <= 2)
+    dw_wgrad_strip_v<K, ST, 2>(off, grid, shm, st, gy, x, g, d, splits, part, tf);
+  else
+    dw_wgrad_strip_v<K, ST, DW_MAXV>(off, grid, shm, st, gy, x, g, d, splits, part, tf);
 }
 
 extern "C" {
@@ -587,14 +613,15 @@ static bool dw_strip_ok(const DwGeom &g) {
 #define DW_STRIP_DISPATCH(LAUNCHER, FLIPARG, GRID, SHMEM, ...)                                   \
   do {                                                                                         \
     const int off = dw_off(g.pl);                                                              \
+    const int nv = cdiv(d.IR * (g.W / 4), 64);                                                 \
     if (g.K == 3 && g.st == 1)                                                                 \
-      LAUNCHER<3, 1 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
+      LAUNCHER<3, 1 FLIPARG>(off, nv, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
     else if (g.K == 3 && g.st == 2)                                                            \
-      LAUNCHER<3, 2 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
+      LAUNCHER<3, 2 FLIPARG>(off, nv, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
     else if (g.K == 5 && g.st == 1)                                                            \
-      LAUNCHER<5, 1 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
+      LAUNCHER<5, 1 FLIPARG>(off, nv, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
     else                                                                                       \
-      LAUNCHER<5, 2 FLIPARG>(off, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
+      LAUNCHER<5, 2 FLIPARG>(off, nv, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
   } while (0)
 #define DW_NOFLIP , false
 #define DW_NONE
@@ -636,10 +663,10 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
       const size_t shm = 4 * d.IR * d.WP * 4;
       const DwIn none{nullptr, nullptr, 0};
       if (t.K == 3)
-        dw_fwd_strip<3, 1, true>(dw_off(t.pl), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
+        dw_fwd_strip<3, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
                                  w, t, d, units, dx, none);
       else
-        dw_fwd_strip<5, 1, true>(dw_off(t.pl), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
+        dw_fwd_strip<5, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
                                  w, t, d, units, dx, none);
       return launch_status("e2ep_dwconv_dgrad");
     }

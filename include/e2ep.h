@@ -571,7 +571,7 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
 /* Launch-plan tunables (read at every launch; value <= 0 only queries; returns the previous
  * value, -1 for an unknown key), defaults in parentheses: 0 split-BN target workgroups (2048),
  * 1 minimum elements per split-BN workgroup (4096), 2 float4 vectors per BN apply workgroup
- * (1024), 3 depthwise weight-gradient target workgroups (1024), 4 K-split e2ep_gemm target
+ * (1024), 3 depthwise weight-gradient target workgroups (512), 4 K-split e2ep_gemm target
  * workgroups (768), 5 1x1 weight-gradient target workgroups (1024), 6 conv forward /
  * data-gradient grids of at least this many wide (128 / 256-column) tiles use them (512),
  * 7 k_conv_gemm block tile forced to bm * 1000 + bnt (64064, 64128, 32128, 32256; 1 =

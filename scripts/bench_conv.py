@@ -24,10 +24,10 @@ def record(batch):
     seen = {}
     orig = conv._Conv2d.apply
 
-    def rec(x, w, b, dims, act, gc):
+    def rec(x, w, b, dims, act, gc, *rest):
         key = json.dumps([list(dims), int(act), b is not None, gc])
         seen[key] = seen.get(key, 0) + 1
-        return orig(x, w, b, dims, act, gc)
+        return orig(x, w, b, dims, act, gc, *rest)
 
     conv._Conv2d.apply = rec
     mod = ParkingTrainingModule(default_cfg()).cuda().train()
