@@ -28,7 +28,8 @@ enum Tune {
   TUNE_LPW_TARGET = 22,       // workgroups the k_wgrad_lp K split aims at
   TUNE_DW_VEC = 23,           // depthwise strip kernels' LDS rows: 2 = ds_read_b128 windows, 1 = scalar reads
   TUNE_DW_FWD_BLOCKS = 24,    // depthwise forward / stride-1 data-gradient strip kernel: grid cap (blocks)
-  TUNE_N = 25
+  TUNE_BNS_WIDE = 25,         // single-launch BN, channels of 1025..2048 float4: 2 = 512 threads x 4, 1 = 256 x 8
+  TUNE_N = 26
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

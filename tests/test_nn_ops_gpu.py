@@ -15,6 +15,21 @@ def _g(seed):
     return torch.Generator().manual_seed(seed)
 
 
+@pytest.mark.parametrize("act", [None, "relu", "swish"])
+@pytest.mark.parametrize("res", [False, True])
+def test_bn_act_wide_blocks(act, res):
+    """e2ep_tune key 25 = 2: the single-launch BN of channels with 4097..8192 elements
+    (32 x 16 x 16 here) on 512-thread blocks of 4 float4 per thread, train and eval, vs fp64."""
+    from e2ep_amd import _lib
+    lib = _lib.load()
+    prev = lib.e2ep_tune(25, 2)
+    try:
+        for train in (True, False):
+            test_bn_act(train, act, res, (32, 24, 16, 16), 1)
+    finally:
+        lib.e2ep_tune(25, prev)
+
+
 @pytest.fixture(params=[0, 3], ids=["dw_grid_default", "dw_grid_3"])
 def dw_grid(request):
     """Depthwise forward grid cap (e2ep_tune key 24): default, and 3 blocks so each wave walks
@@ -44,7 +59,7 @@ def bn_path(request):
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("shape", [(4, 24, 32, 32), (3, 7, 5, 9), (32, 6, 1, 1),
                                    (4, 160, 8, 8), (16, 128, 32, 32), (8, 16, 64, 64),
-                                   (3, 12, 44, 36), (2, 8, 136, 128)])
+                                   (3, 12, 44, 36), (2, 8, 136, 128), (32, 24, 16, 16)])
 def test_bn_act(train, act, res, shape, bn_path):
     from e2ep_amd import nn_ops
     g = _g(sum(shape) + 3 * train)
