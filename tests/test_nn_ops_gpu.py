@@ -17,12 +17,14 @@ def _g(seed):
 
 @pytest.mark.parametrize("act", [None, "relu", "swish"])
 @pytest.mark.parametrize("res", [False, True])
-def test_bn_act_wide_blocks(act, res):
-    """e2ep_tune key 25 = 2: the single-launch BN of channels with 4097..8192 elements
-    (32 x 16 x 16 here) on 512-thread blocks of 4 float4 per thread, train and eval, vs fp64."""
+def test_bn_act_narrow_blocks(act, res):
+    """e2ep_tune key 25 = 1: the single-launch BN of channels with 4097..8192 elements
+    (32 x 16 x 16 here) on 256-thread blocks of 8 float4 per thread (the default, key 25 = 2,
+    runs 512 x 4 and is covered by test_bn_act's (32, 24, 16, 16) case), train and eval, vs
+    fp64."""
     from e2ep_amd import _lib
     lib = _lib.load()
-    prev = lib.e2ep_tune(25, 2)
+    prev = lib.e2ep_tune(25, 1)
     try:
         for train in (True, False):
             test_bn_act(train, act, res, (32, 24, 16, 16), 1)
