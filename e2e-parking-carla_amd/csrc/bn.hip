@@ -608,14 +608,19 @@ static int bns_r(int totv, int &threads) {
   do {                                                                                            \
     (void)(TH);                                                                                   \
     if (R == 1) hipLaunchKernelGGL((KERNEL<BNS_T, 1>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);  \
+    else if (R == 2 && g_tune[TUNE_BNS_WIDE_LO] == 2)                                             \
+      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 1>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__);      \
     else if (R == 2) hipLaunchKernelGGL((KERNEL<BNS_T, 2>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
+    else if (R == 4 && g_tune[TUNE_BNS_WIDE_LO] == 2)                                             \
+      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 2>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__);      \
     else if (R == 4) hipLaunchKernelGGL((KERNEL<BNS_T, 4>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
     else if (g_tune[TUNE_BNS_WIDE] == 2)                                                         \
       hipLaunchKernelGGL((KERNEL<2 * BNS_T, 4>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__);      \
     else hipLaunchKernelGGL((KERNEL<BNS_T, 8>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);         \
   } while (0)
 // (e2ep_tune key 25 = 2: channels that need 8 float4 per thread at 256 threads run 512-thread
-// blocks of 4 per thread instead: half the registers per thread, twice the waves per channel)
+// blocks of 4 per thread instead: half the registers per thread, twice the waves per channel;
+// key 26 = 2 does the same for the 2- and 4-vector cases)
 
 // elementwise activation forward/backward (for activations not fused into a BN)
 __global__ void k_act_fwd(const float *__restrict__ x, long long n, int act, float *__restrict__ y) {

@@ -29,7 +29,8 @@ enum Tune {
   TUNE_DW_VEC = 23,           // depthwise strip kernels' LDS rows: 2 = ds_read_b128 windows, 1 = scalar reads
   TUNE_DW_FWD_BLOCKS = 24,    // depthwise forward / stride-1 data-gradient strip kernel: grid cap (blocks)
   TUNE_BNS_WIDE = 25,         // single-launch BN, channels of 1025..2048 float4: 2 = 512 threads x 4, 1 = 256 x 8
-  TUNE_N = 26
+  TUNE_BNS_WIDE_LO = 26,      // the same for channels of 257..1024 float4: 2 = 512 threads x 1 / 2, 1 = 256 x 2 / 4
+  TUNE_N = 27
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

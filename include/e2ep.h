@@ -591,7 +591,8 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * target workgroups (1024), 23 depthwise strip kernels' LDS window reads (2 = 16-B vector
  * reads, default; 1 = scalar reads), 24 depthwise forward / stride-1 data-gradient grid cap in
  * blocks (2048; each wave walks units beyond it in a software-pipelined loop), 25 single-launch BN
- * blocks for channels of 1025..2048 float4 (2 = 512 threads x 4 float4, default; 1 = 256 x 8).
+ * blocks for channels of 1025..2048 float4 (2 = 512 threads x 4 float4, default; 1 = 256 x 8),
+ * 26 the same for channels of 257..1024 float4 (2 = 512 threads; 1 = 256, default: equal).
  * For A/B timing.
  * Contract for every plan override and tunable above (e2ep_conv_split_params,
  * e2ep_gemm_force, e2ep_gemm_split_min, e2ep_bn_small*, e2ep_tune): a launch recomputes its
