@@ -13,11 +13,13 @@ metric's configuration, configs[1] (C2).
 N>1: one rank per GPU, RCCL over xGMI.  Under torch.distributed.run (WORLD_SIZE set) the ranks
 are already there; from a plain command line `--gpus N` re-launches this script under
 torch.distributed.run with N ranks before anything touches the GPU.  Each rank runs B samples
-per step (weak scaling); the flat 78 MB gradient buffer is all-reduced once per step between
-the backward and optimizer graph replays (the only exchange; e2ep_amd.train explains why it
-is not captured).  The step is captured into HIP graphs during warm-up
-(e2ep_amd.train.TrainStep; --eager disables capture and overlaps ~25 MB bucket all-reduces
-with backward instead).
+per step (weak scaling); the flat 78 MB gradient buffer is the only exchange.  The step is
+captured into HIP graphs during warm-up (e2ep_amd.train.TrainStep): with RCCL the backward runs
+as two captured segments (cut below the BEV encoder, e2ep_amd.segments) and the host issues the
+stage-1 gradients' ~25 MB bucket all-reduces on a communication stream between the segment
+replays, so they run during the camera-encoder backward; the stage-2 bucket follows, then the
+optimizer graph (no collective is captured: e2ep_amd.train explains why).  --eager disables
+capture and overlaps the bucket all-reduces with the backward from autograd hooks instead.
 Rank 0 prints ONE JSON line.
 """
 import argparse

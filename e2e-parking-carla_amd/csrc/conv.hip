@@ -28,6 +28,7 @@
 #include "common.h"
 #include "conv.h"
 #include "gemm.h"
+#include "handoff.h"
 
 namespace e2ep {
 
@@ -52,7 +53,8 @@ constexpr int MAXPH = 4;
 template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0>
 __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
-    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
+    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    float *__restrict__ part, unsigned int *__restrict__ cnt) {
   // block tile BMT x BNT: BMT = 64 -> 2 x 2 waves of 32 x BNT/2; BMT = 32 (small-M layers:
   // Cout or Cin 24..56) -> 1 x 4 waves of 32 x BNT/4, so no MFMA rows are padding
   constexpr int WC = BMT == 64 ? BNT / 2 : BNT / 4;  // columns per wave
@@ -290,7 +292,44 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
 
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // splits == 1: final values (bias, act) into dst[img][m][pixel];
-  // splits > 1:  raw partial sums into dst = part[split][m][n] (reduced by k_conv_reduce).
+  // splits > 1:  raw partial sums into part[split][m][n]: with `cnt` (the in-launch fold)
+  // write-through, and the tile's last-arriving split sums every slab in split order
+  // (k_conv_reduce's order) and writes the final values; without, k_conv_reduce does.
+  if (splits > 1) {
+    __shared__ int s_last;
+    const int MN = M * Ntot;
+    const __amdgpu_buffer_rsrc_t rp = rsrc(part + (size_t)split * MN, 4LL * MN);
+#pragma unroll
+    for (int t = 0; t < NACC; ++t) {
+      const int n = n0 + WC * wn + 32 * t + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int off = (n < Ntot && m < M) ? (m * Ntot + n) * 4 : OOR;
+        if (cnt) bstore_sc1(rp, off, acc[t][r]);
+        else bstore(rp, off, acc[t][r]);
+      }
+    }
+    if (!cnt) return;
+    handoff_drain();
+    if (!handoff_arrive(cnt + blockIdx.x + gridDim.x * blockIdx.y, splits, &s_last)) return;
+    const __amdgpu_buffer_rsrc_t rall = rsrc(part, 4LL * splits * MN);
+#pragma unroll
+    for (int t = 0; t < NACC; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    for (int k = 0; k < splits; ++k) {
+#pragma unroll
+      for (int t = 0; t < NACC; ++t) {
+        const int n = n0 + WC * wn + 32 * t + li;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          acc[t][r] += bload_sc1(rall, (n < Ntot && m < M) ? (k * MN + m * Ntot + n) * 4 : OOR);
+        }
+      }
+    }
+  }
   const __amdgpu_buffer_rsrc_t rd = rsrc(dst, dst_bytes);
   // MODE 1: `bias` is an optional residual gradient in dst's layout, added to dx here (the
   // skip connection's gradient, so autograd needs no separate accumulation kernel)
@@ -302,7 +341,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     const int n = n0 + WC * wn + 32 * t + li;
     const bool nok = n < Ntot;
     int dbase, mstride;
-    if (splits == 1) {
+    if (true) {
       const int im = n / HWc;
       const int p = n - im * HWc;
       int dp = p;
@@ -312,22 +351,17 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       }
       dbase = im * M * HWd + dp;
       mstride = HWd;
-    } else {
-      dbase = split * M * Ntot + n;
-      mstride = Ntot;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
       float v = acc[t][r];
       const int off = (nok && m < M) ? (dbase + m * mstride) * 4 : OOR;
-      if (splits == 1) {
-        if (MODE == 0) {
-          if (bias) v += bias[min(m, M - 1)];
-          if (ACT == 1) v = fmaxf(v, 0.f);
-        } else if (bias) {
-          v += bload(rres, off);
-        }
+      if (MODE == 0) {
+        if (bias) v += bias[min(m, M - 1)];
+        if (ACT == 1) v = fmaxf(v, 0.f);
+      } else if (bias) {
+        v += bload(rres, off);
       }
       bstore(rd, off, v);
     }
@@ -1645,28 +1679,29 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     return lp_launch(mode, act, 0, w, src, bias, dst, dst_bytes, g, M, workspace, s);
   const GemmPlan p = plan_gemm(mode, g, M);
   dim3 grid(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
-  float *out = dst;
-  long long out_bytes = dst_bytes;
+  float *part = nullptr;
+  unsigned int *cnt = nullptr;
   if (p.splits > 1) {
     if (!workspace) {
       set_error("conv: split-K plan needs a workspace (query the *_workspace entry point)");
       return E2EP_EINVAL;
     }
-    out = static_cast<float *>(workspace);
-    out_bytes = (long long)gemm_workspace(p, M);
+    part = static_cast<float *>(workspace);
+    // in-launch fold (e2ep_tune key 28 = 2): one arrival counter per output tile
+    if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y);
   }
   const bool av = mode == 0 && g.wlayout == 1 && (g.Cin & 3) == 0;
 #define GEMM_LAUNCH1(MD, AC, BT, BMT, V)                                                          \
   do {                                                                                             \
     if (g_conv_precision == 1)                                                                     \
       hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 1>), grid, dim3(256), 0, s, w, src, bias, \
-                         out, out_bytes, g, M, p.splits, p.kper);                                  \
+                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt);                      \
     else if (g_conv_precision == 2)                                                                \
       hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 2>), grid, dim3(256), 0, s, w, src, bias, \
-                         out, out_bytes, g, M, p.splits, p.kper);                                  \
+                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt);                      \
     else                                                                                           \
       hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 0>), grid, dim3(256), 0, s, w, src, bias, \
-                         out, out_bytes, g, M, p.splits, p.kper);                                  \
+                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt);                      \
   } while (0)
 #define GEMM_LAUNCH(MD, AC, BT, BMT)                                  \
   do {                                                                \
@@ -1689,7 +1724,7 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
 #undef GEMM_TILES
 #undef GEMM_LAUNCH
 #undef GEMM_LAUNCH1
-  if (p.splits > 1) {
+  if (p.splits > 1 && !cnt) {
     const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
     hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
                        static_cast<const float *>(workspace), p.splits, M, HW, (int)p.ncols,

@@ -25,6 +25,7 @@
 #include <algorithm>
 
 #include "conv.h"
+#include "handoff.h"
 
 namespace e2ep {
 
@@ -70,7 +71,8 @@ __device__ __forceinline__ f32x16 mfma16(typename LpType<OP>::T8 a, typename LpT
 template <int MODE, int ACT, int WM, int WN, int OP, int LKS>
 __global__ void __launch_bounds__(256) k_conv_lp(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
-    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper) {
+    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    float *__restrict__ part, unsigned int *__restrict__ cnt) {
   typedef typename LpType<OP>::T T;
   typedef typename LpType<OP>::T8 T8;
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
@@ -331,7 +333,50 @@ __global__ void __launch_bounds__(256) k_conv_lp(
 
   // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // splits == 1: final values (bias, act; MODE 1: + residual gradient) into dst;
-  // splits > 1:  raw partial sums into dst = part[split][m][n] (k_conv_lp_reduce).
+  // splits > 1:  raw partial sums into part[split][m][n]: with `cnt` (the in-launch fold)
+  // write-through, and the tile's last-arriving split sums every slab in split order
+  // (k_conv_lp_reduce's order) and writes the final values; without, k_conv_lp_reduce does.
+  if (splits > 1) {
+    __shared__ int s_last;
+    const int MN = M * Ntot;
+    const __amdgpu_buffer_rsrc_t rp = rsrc(part + (size_t)split * MN, 4LL * MN);
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = n0 + 32 * (WN * wn + j) + li;
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + 32 * (WM * wm + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int off = (n < Ntot && m < M) ? (m * Ntot + n) * 4 : OOR;
+          if (cnt) bstore_sc1(rp, off, acc[i][j][r]);
+          else bstore(rp, off, acc[i][j][r]);
+        }
+    }
+    if (!cnt) return;
+    handoff_drain();
+    if (!handoff_arrive(cnt + bx + gridDim.x * by, splits, &s_last)) return;
+    const __amdgpu_buffer_rsrc_t rall = rsrc(part, 4LL * splits * MN);
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int k = 0; k < splits; ++k) {
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int n = n0 + 32 * (WN * wn + j) + li;
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + 32 * (WM * wm + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            acc[i][j][r] += bload_sc1(rall, (n < Ntot && m < M) ? (k * MN + m * Ntot + n) * 4 : OOR);
+          }
+      }
+    }
+  }
   const __amdgpu_buffer_rsrc_t rd = rsrc(dst, dst_bytes);
   const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes : 0);
   const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
@@ -341,7 +386,7 @@ __global__ void __launch_bounds__(256) k_conv_lp(
     const int n = n0 + 32 * (WN * wn + j) + li;
     const bool nok = n < Ntot;
     int dbase, mstride;
-    if (splits == 1) {
+    {
       const int im = n / HWc;
       const int p = n - im * HWc;
       int dp = p;
@@ -351,9 +396,6 @@ __global__ void __launch_bounds__(256) k_conv_lp(
       }
       dbase = im * M * HWd + dp;
       mstride = HWd;
-    } else {
-      dbase = split * M * Ntot + n;
-      mstride = Ntot;
     }
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
@@ -362,13 +404,11 @@ __global__ void __launch_bounds__(256) k_conv_lp(
         const int m = m0 + 32 * (WM * wm + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
         float v = acc[i][j][r];
         const int off = (nok && m < M) ? (dbase + m * mstride) * 4 : OOR;
-        if (splits == 1) {
-          if (MODE == 0) {
-            if (bias) v += bias[min(m, M - 1)];
-            if (ACT == 1) v = fmaxf(v, 0.f);
-          } else if (bias) {
-            v += bload(rres, off);
-          }
+        if (MODE == 0) {
+          if (bias) v += bias[min(m, M - 1)];
+          if (ACT == 1) v = fmaxf(v, 0.f);
+        } else if (bias) {
+          v += bload(rres, off);
         }
         bstore(rd, off, v);
       }
@@ -503,15 +543,17 @@ size_t lp_workspace(int mode, const ConvGeom &g, int M, int op) {
 
 template <int MODE, int ACT, int OP>
 static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, const float *src,
-                     const float *bias, float *out, long long out_bytes, const ConvGeom &g, int M) {
+                     const float *bias, float *out, long long out_bytes, const ConvGeom &g, int M,
+                     float *part, unsigned int *cnt) {
 #define LP_L(WMV, WNV)                                                                              \
   do {                                                                                              \
     if (OP != 0 && WNV <= 2 && p.lk == 64)                                                          \
       hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32>),     \
-                         grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits, p.kper); \
+                         grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits, p.kper, \
+                         part, cnt);                                                               \
     else                                                                                            \
       hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32>), grid, dim3(256), 0, s, w, src,   \
-                         bias, out, out_bytes, g, M, p.splits, p.kper);                             \
+                         bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt);                 \
   } while (0)
   if (p.wm == 2) {
     if (p.wn == 2) LP_L(2, 2);
@@ -534,28 +576,30 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
               hipStream_t s) {
   const LpPlan p = lp_plan(mode, g, M, op);
   const dim3 grid(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
-  float *out = dst;
-  long long out_bytes = dst_bytes;
+  float *part = nullptr;
+  unsigned int *cnt = nullptr;
   if (p.splits > 1) {
     if (!workspace) {
       set_error("conv (low precision): split-K plan needs a workspace (query the *_workspace entry point)");
       return E2EP_EINVAL;
     }
-    out = static_cast<float *>(workspace);
-    out_bytes = (long long)p.splits * M * p.ncols * 4;
+    part = static_cast<float *>(workspace);
+    // in-launch fold (e2ep_tune key 28 = 2): one arrival counter per output tile
+    if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y);
   }
-  const float *kb = p.splits > 1 ? nullptr : bias;  // bias / residual go to the reduction
+  // bias / residual: the kernel's final epilogue, or the separate reduction
+  const float *kb = (p.splits > 1 && !cnt) ? nullptr : bias;
 #define LP_OPS(MD, AC)                                                     \
   do {                                                                     \
-    if (op == 1) lp_tiles<MD, AC, 1>(p, grid, s, w, src, kb, out, out_bytes, g, M); \
-    else if (op == 2) lp_tiles<MD, AC, 2>(p, grid, s, w, src, kb, out, out_bytes, g, M); \
-    else lp_tiles<MD, AC, 0>(p, grid, s, w, src, kb, out, out_bytes, g, M); \
+    if (op == 1) lp_tiles<MD, AC, 1>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt); \
+    else if (op == 2) lp_tiles<MD, AC, 2>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt); \
+    else lp_tiles<MD, AC, 0>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt); \
   } while (0)
   if (mode == 0 && act == 0) LP_OPS(0, 0);
   else if (mode == 0) LP_OPS(0, 1);
   else LP_OPS(1, 0);
 #undef LP_OPS
-  if (p.splits > 1) {
+  if (p.splits > 1 && !cnt) {
     const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
     hipLaunchKernelGGL(k_conv_lp_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
                        static_cast<const float *>(workspace), p.splits, M, HW, (int)p.ncols,

@@ -3,8 +3,37 @@
 // forward, data gradient (gather, no atomics) and weight gradient (fixed-order split
 // reduction), NCHW fp32, for gfx950.  Memory-bound: each kernel streams its input once.
 #include "common.h"
+#include "handoff.h"
 
 namespace e2ep {
+
+// Weight-gradient output: per-split slabs part[c][split][K*K]; with one split the slab is the
+// gradient and is written to dw directly; with several and `cnt` (the in-launch fold, e2ep_tune
+// key 28 = 2) the slabs are stored write-through and the channel's last-arriving split sums
+// them in split order (k_dw_wgrad_finalize's order) into dw; otherwise k_dw_wgrad_finalize does.
+struct DwPart {
+  float *part, *dw;
+  unsigned int *cnt;
+};
+
+template <int KK>
+__device__ __forceinline__ void dw_wgrad_out(DwPart o, int c, int sp, int splits, float v,
+                                             int *s_last) {
+  const int t = threadIdx.x;
+  if (t < KK) {
+    if (splits == 1) o.dw[(long long)c * KK + t] = v;
+    else if (o.cnt) st_sc1(o.part + ((long long)c * splits + sp) * KK + t, v);
+    else o.part[((long long)c * splits + sp) * KK + t] = v;
+  }
+  if (splits == 1 || !o.cnt) return;
+  handoff_drain();
+  if (!handoff_arrive(o.cnt + c, splits, s_last)) return;
+  if (t < KK) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ld_sc1(o.part + ((long long)c * splits + k) * KK + t);
+    o.dw[(long long)c * KK + t] = s;
+  }
+}
 
 struct DwGeom {
   int N, C, H, W, K, P, Q, st, pt, pl;
@@ -94,7 +123,7 @@ __global__ void __launch_bounds__(256) k_dw_dgrad(const float *__restrict__ gy,
 template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
                                                   const float *__restrict__ x, DwGeom g,
-                                                  int splits, float *__restrict__ part,
+                                                  int splits, DwPart part,
                                                   const float *__restrict__ tsc,
                                                   const float *__restrict__ tsh, int tact) {
   const int c = blockIdx.x, sp = blockIdx.y;
@@ -135,10 +164,9 @@ __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][t] = v;
   }
   __syncthreads();
-  if (threadIdx.x < K * K) {
-    const int t = threadIdx.x;
-    part[((long long)c * splits + sp) * K * K + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-  }
+  __shared__ int s_last;
+  const int t = threadIdx.x < K * K ? threadIdx.x : 0;
+  dw_wgrad_out<K * K>(part, c, sp, splits, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]), &s_last);
 }
 
 __global__ void k_dw_wgrad_finalize(const float *__restrict__ part, int C, int KK, int splits,
@@ -434,7 +462,7 @@ template <int K, int ST, int OFF, int V>
 __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
                                                         const float *__restrict__ x, DwGeom g,
                                                         DwStrip d, int splits,
-                                                        float *__restrict__ part, DwIn tf) {
+                                                        DwPart part, DwIn tf) {
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
@@ -507,10 +535,9 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
     if (lane == 0) red[wave][t] = v;
   }
   __syncthreads();
-  if (threadIdx.x < K * K) {
-    const int t = threadIdx.x;
-    part[((long long)c * splits + sp) * K * K + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-  }
+  __shared__ int s_last;
+  const int t = threadIdx.x < K * K ? threadIdx.x : 0;
+  dw_wgrad_out<K * K>(part, c, sp, splits, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]), &s_last);
 }
 
 static int dw_splits(long long pixels, int C) {
@@ -579,7 +606,7 @@ static void dw_fwd_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st,
 }
 template <int K, int ST, int V>
 static void dw_wgrad_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *gy,
-                             const float *x, DwGeom g, DwStrip d, int splits, float *part, DwIn tf) {
+                             const float *x, DwGeom g, DwStrip d, int splits, DwPart part, DwIn tf) {
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, gy, x, g, d, splits, part, tf); };
   switch (off) {
     case 0: go(k_dw_wgrad_strip<K, ST, 0, V>); break;
@@ -590,7 +617,7 @@ static void dw_wgrad_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, con
 }
 template <int K, int ST>
 static void dw_wgrad_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const float *gy,
-                           const float *x, DwGeom g, DwStrip d, int splits, float *part, DwIn tf) {
+                           const float *x, DwGeom g, DwStrip d, int splits, DwPart part, DwIn tf) {
   if (off < 0)
     hipLaunchKernelGGL((k_dw_wgrad_strip<K, ST, -1, DW_MAXV>), grid, dim3(256), shm, st, gy, x, g,
                        d, splits, part, tf);
@@ -730,7 +757,9 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_wgrad: bad geometry");
   const int sp = dw_wgrad_splits(g);
-  float *part = static_cast<float *>(workspace);
+  // one split: the slab is the gradient; several: in-launch fold or k_dw_wgrad_finalize
+  DwPart part{static_cast<float *>(workspace), dw,
+              (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C) : nullptr};
   if (dw_wgrad_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     DW_STRIP_DISPATCH(dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
@@ -738,8 +767,9 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
   } else {
     DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part, in_scale, in_shift, in_act);
   }
-  hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0,
-                     as_stream(stream), part, g.C, g.K * g.K, sp, dw);
+  if (sp > 1 && !part.cnt)
+    hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0,
+                       as_stream(stream), part.part, g.C, g.K * g.K, sp, dw);
   return launch_status("e2ep_dwconv_wgrad");
 }
 

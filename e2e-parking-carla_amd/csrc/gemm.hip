@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "gemm.h"
+#include "handoff.h"
 
 namespace e2ep {
 
@@ -56,7 +57,8 @@ __global__ void __launch_bounds__(256)
            const float *__restrict__ B, int ldb, long long b_bytes,
            const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
            int ldadd, float *__restrict__ C, long long c_bytes, int ldc, GemmCols cols, int M,
-           int N, int K, int kper, int relu, float *__restrict__ rs) {
+           int N, int K, int kper, int relu, float *__restrict__ rs, float *__restrict__ part,
+           unsigned int *__restrict__ cnt) {
   // rs != null (only !AK, !BKC, unbatched): B gets a logical column N of ones, so column N of
   // the product is the row sum of A over k — rs[m] = sum_k A(m, k), the bias gradient of a
   // linear layer taken by its weight-gradient GEMM (no separate column-sum launches)
@@ -246,24 +248,65 @@ __global__ void __launch_bounds__(256)
   }
 
   // epilogue: C/D layout col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-  // gridDim.z > 1: raw partial sums into C = workspace[split][M][N] (dense, unbatched).
-  const bool final_ = gridDim.z == 1;
+  // gridDim.z > 1: raw partial sums into part[split][M][Nw] (dense, unbatched); with `cnt`
+  // (the in-launch fold) they are stored write-through, the tile's last-arriving split sums
+  // every slab in split order (k_gemm_reduce's order) and runs the final epilogue below; with
+  // no `cnt` k_gemm_reduce does that in a launch of its own.
   const int Nw = rs ? N + 1 : N;  // split-K partials carry the row-sum column
-  float *dst = final_ ? C : C + (long long)split * M * Nw;
-  const int ldd = final_ ? ldc : Nw;
-  const bool batched = final_ && cols.hw > 0;
+  if (gridDim.z > 1) {
+    __shared__ int s_last;
+    const long long MNw = (long long)M * Nw;
+    const __amdgpu_buffer_rsrc_t rp = rsrc(part + split * MNw, 4LL * MNw);
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const int n = n0 + 32 * TN * wn + 32 * t + li;
+      const bool nok = n < N || (rs && n == N);
+#pragma unroll
+      for (int u = 0; u < TM; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + 32 * TM * wm + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int off = (nok && m < M) ? (m * Nw + n) * 4 : OOR;
+          if (cnt) bstore_sc1(rp, off, acc[u][t][r]);
+          else bstore(rp, off, acc[u][t][r]);
+        }
+    }
+    if (!cnt) return;
+    handoff_drain();
+    if (!handoff_arrive(cnt + blockIdx.x + gridDim.x * blockIdx.y, gridDim.z, &s_last)) return;
+    const __amdgpu_buffer_rsrc_t rall = rsrc(part, 4LL * gridDim.z * MNw);
+    for (int k = 0; k < (int)gridDim.z; ++k) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const int n = n0 + 32 * TN * wn + 32 * t + li;
+        const bool nok = n < N || (rs && n == N);
+#pragma unroll
+        for (int u = 0; u < TM; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + 32 * TM * wm + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const float v = bload_sc1(rall, (nok && m < M) ? (int)((k * MNw + m * Nw + n) * 4) : OOR);
+            acc[u][t][r] = k == 0 ? v : acc[u][t][r] + v;
+          }
+      }
+    }
+  }
+  const bool final_ = true;
+  float *dst = C;
+  const int ldd = ldc;
+  const bool batched = cols.hw > 0;
   // edges: buffer stores with out-of-range offsets are dropped; the epilogue's optional
   // inputs are behind uniform branches, and the 16 Cadd values of a tile are loaded together
-  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, final_ ? c_bytes : 4LL * M * Nw);
-  const __amdgpu_buffer_rsrc_t rrs = rsrc(rs, rs && final_ ? 4LL * M : 0);
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dst, c_bytes);
+  const __amdgpu_buffer_rsrc_t rrs = rsrc(rs, rs ? 4LL * M : 0);
   const __amdgpu_buffer_rsrc_t rc =
       rsrc(Cadd, Cadd ? (batched ? c_bytes : 4LL * ((long long)(M - 1) * ldadd + N)) : 0);
   const bool add_c = final_ && Cadd != nullptr, add_b = final_ && bias != nullptr;
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
     const int n = n0 + 32 * TN * wn + 32 * t + li;
-    const bool nok = n < N || (rs && !final_ && n == N);  // partial row-sum column
-    const bool rsc = rs && final_ && n == N;
+    const bool nok = n < N;
+    const bool rsc = rs && n == N;
     const long long cbase = batched ? (long long)(n / cols.hw) * cols.c_img + n % cols.hw : n;
     const float bn_ = (add_b && !bias_rows) ? bias[min(n, N - 1)] : 0.f;
 #pragma unroll
@@ -507,26 +550,29 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
     set_error("gemm: workspace of e2ep_gemm_workspace() bytes required");
     return E2EP_EINVAL;
   }
-  float *out = p.splits > 1 ? static_cast<float *>(workspace) : C;
+  float *part = p.splits > 1 ? static_cast<float *>(workspace) : nullptr;
   const GemmTile td = tile_dims(p.tile);
+  // in-launch split-K fold (e2ep_tune key 28 = 2): one arrival counter per output tile
+  unsigned int *cnt = (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] == 2)
+                          ? handoff_slots(cdiv(Nx, td.bn) * cdiv(M, td.bm)) : nullptr;
   dim3 grid(cdiv(Nx, td.bn), cdiv(M, td.bm), p.splits);
   const int avec = vec_of(ak, lda, A), bvec = vec_of(bk, ldb, B);
   const int br = bias_rows ? 1 : 0;
 #define E2EP_GEMM_LAUNCH(AKV, BKV, WMV, TMV, TNV, AVV, BVV)                                     \
   hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, TMV, TNV, AVV, BVV>), grid, dim3(256), 0, s, A, lda,  \
-                     a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, out, c_bytes, ldc, cols, M, \
-                     N, K, p.kper, relu, rs)
+                     a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, C, c_bytes, ldc, cols, M, \
+                     N, K, p.kper, relu, rs, part, cnt)
 #define E2EP_GEMM_T(AKV, BKV, AVV, BVV)                                     \
   do {                                                                      \
     if (g_gemm_precision == 1) { /* bf16: the automatic tiles */            \
       if (p.tile == 2)                                                      \
         hipLaunchKernelGGL((k_gemm<AKV, BKV, 1, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, A, \
-                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, out, c_bytes, \
-                           ldc, cols, M, N, K, p.kper, relu, rs);           \
+                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, C, c_bytes, \
+                           ldc, cols, M, N, K, p.kper, relu, rs, part, cnt); \
       else                                                                  \
         hipLaunchKernelGGL((k_gemm<AKV, BKV, 2, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, A, \
-                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, out, c_bytes, \
-                           ldc, cols, M, N, K, p.kper, relu, rs);           \
+                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, C, c_bytes, \
+                           ldc, cols, M, N, K, p.kper, relu, rs, part, cnt); \
       break;                                                                \
     }                                                                       \
     switch (p.tile) {                                                       \
@@ -561,7 +607,7 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
 #undef E2EP_GEMM_BV
 #undef E2EP_GEMM_T
 #undef E2EP_GEMM_LAUNCH
-  if (p.splits > 1) {
+  if (p.splits > 1 && !cnt) {
     const long long MN = (long long)M * Nx;
     const bool v4 = !rs && MN % 4 == 0 && ldc == N && cols.hw == 0 && !bias_rows &&
                     (!Cadd || ldadd == N) && ((uintptr_t)C & 15) == 0;

@@ -8,6 +8,7 @@
 // dx = dy * sigmoid(a) + dpooled / HW in a single stream — no separate avg-pool backward and
 // no autograd add of the two input-gradient paths.
 #include "common.h"
+#include "handoff.h"
 
 namespace e2ep {
 
@@ -299,9 +300,193 @@ __global__ void __launch_bounds__(256) k_se_dx(const float *__restrict__ dy,
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused forms (e2ep_tune key 27 = 2, the default): the MLP on the 1x1 map runs inside the
+// streaming kernels instead of as launches of its own.
+//  * k_se_squeeze_mlp: the squeeze; a sample's C/4 workgroups store their plane means
+//    write-through and take an arrival ticket (handoff.h); the sample's last workgroup reads
+//    the C means back (sc1) and computes hpre[n][k] = W1[k] . pooled[n] + b1[k] for every k.
+//  * k_se_excite_logits: the excite; each workgroup first forms the logits a of the planes it
+//    covers (a wave per plane: W2[c] . swish(hpre[n]) + b2[c]), the workgroup holding a
+//    plane's first element stores it for the backward.
+//  * k_se_da_mlp: da per plane as k_se_da; a sample's last workgroup then forms
+//    dh = W2^T da[n], dhpre = dh * swish'(hpre), dpooled[n] = W1^T dhpre.
+// Every sum runs in a fixed order, so results are run-to-run deterministic.  Needs C % 4 == 0
+// (a workgroup's four planes belong to one sample).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_se_squeeze_mlp(const float *__restrict__ x, SeIn tf,
+                                                        int HW, const float *__restrict__ w1,
+                                                        const float *__restrict__ b1, int sq,
+                                                        float *__restrict__ pooled,
+                                                        float *__restrict__ hpre,
+                                                        unsigned int *__restrict__ cnt) {
+  __shared__ float sp[SE_MAXC];
+  __shared__ int s_last;
+  const int C = tf.C;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pl = blockIdx.x * 4 + wave;
+  const int n = (blockIdx.x * 4) / C;
+  const bool t = tf.sc != nullptr;
+  const int c = pl - n * C;
+  const float s = plane_sum(x + (size_t)pl * HW, HW, lane, t ? tf.sc[c] : 1.f, t ? tf.sh[c] : 0.f, t);
+  if (lane == 0) st_sc1(pooled + pl, s / (float)HW);
+  handoff_drain();
+  if (!handoff_arrive(cnt + n, C / 4, &s_last)) return;
+  for (int i = threadIdx.x; i < C; i += 256) sp[i] = ld_sc1(pooled + (size_t)n * C + i);
+  __syncthreads();
+  for (int k = wave; k < sq; k += 4) {  // k_se_hidden's dot, one wave per hidden unit
+    const float *wr = w1 + (size_t)k * C;
+    float s0 = 0.f, s1 = 0.f;
+    int i = lane;
+    for (; i + 64 < C; i += 128) {
+      s0 += wr[i] * sp[i];
+      s1 += wr[i + 64] * sp[i + 64];
+    }
+    if (i < C) s0 += wr[i] * sp[i];
+    const float h = wave_sum(s0 + s1);
+    if (lane == 0) hpre[(size_t)n * sq + k] = h + (b1 ? b1[k] : 0.f);
+  }
+}
+
+constexpr int SE_XPL = 32;  // planes one excite workgroup may cover (>= 16 elements per plane)
+__global__ void __launch_bounds__(256) k_se_excite_logits(const float *__restrict__ x, SeIn tf,
+                                                          const float *__restrict__ hpre,
+                                                          const float *__restrict__ w2,
+                                                          const float *__restrict__ b2, int sq,
+                                                          int HW, long long nvec, int vec,
+                                                          float *__restrict__ a,
+                                                          float *__restrict__ y) {
+  __shared__ float sa[SE_XPL];
+  const int C = tf.C;
+  const int per = vec ? HW >> 2 : HW;  // vector elements per plane
+  const long long i0 = (long long)blockIdx.x * 256;
+  const long long i1 = min(nvec, i0 + 256) - 1;
+  const long long pl0 = i0 / per;
+  const int np = (int)(i1 / per - pl0) + 1;  // host guarantees <= SE_XPL
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int j = wave; j < np; j += 4) {
+    const long long pl = pl0 + j;
+    const int n = (int)(pl / C), c = (int)(pl - (long long)n * C);
+    const float *wr = w2 + (size_t)c * sq, *hr = hpre + (size_t)n * sq;
+    float s = 0.f;
+    for (int k = lane; k < sq; k += 64) {
+      const float z = hr[k];
+      s += wr[k] * (z * sigm(z));
+    }
+    s = wave_sum(s) + (b2 ? b2[c] : 0.f);
+    if (lane == 0) {
+      sa[j] = s;
+      if (pl * per >= i0) a[pl] = s;  // the workgroup holding the plane's first element
+    }
+  }
+  __syncthreads();
+  const long long i = i0 + threadIdx.x;
+  if (i >= nvec) return;
+  const bool t = tf.sc != nullptr;
+  const long long pl = i / per;
+  const int c = (int)(pl % C);
+  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
+  const float g = sigm(sa[pl - pl0]);
+  if (vec) {
+    float4 v = se_in4(reinterpret_cast<const float4 *>(x)[i], sc, sh, t);
+    v.x *= g; v.y *= g; v.z *= g; v.w *= g;
+    reinterpret_cast<float4 *>(y)[i] = v;
+  } else {
+    y[i] = se_in(x[i], sc, sh, t) * g;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_se_da_mlp(const float *__restrict__ x, SeIn tf,
+                                                   const float *__restrict__ dy,
+                                                   const float *__restrict__ a, int HW,
+                                                   const float *__restrict__ w1,
+                                                   const float *__restrict__ w2,
+                                                   const float *__restrict__ hpre, int sq, int KT,
+                                                   float *__restrict__ da,
+                                                   float *__restrict__ dhpre,
+                                                   float *__restrict__ dpooled,
+                                                   unsigned int *__restrict__ cnt) {
+  __shared__ float sda[SE_MAXC];
+  __shared__ float red[256];
+  __shared__ float sdh[SE_MAXSQ];
+  __shared__ int s_last;
+  const int C = tf.C;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pl = blockIdx.x * 4 + wave;
+  const int n = (blockIdx.x * 4) / C;
+  const bool t = tf.sc != nullptr;
+  const int c = pl - n * C;
+  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
+  const float *xp = x + (size_t)pl * HW, *gp = dy + (size_t)pl * HW;
+  float acc = 0.f;
+  if ((HW & 3) == 0) {
+    const int HW4 = HW >> 2;
+    const float4 *x4 = reinterpret_cast<const float4 *>(xp), *g4 = reinterpret_cast<const float4 *>(gp);
+    for (int i0 = lane; i0 < HW4; i0 += 64 * SE_U) {
+      float4 xv[SE_U], gv[SE_U];
+#pragma unroll
+      for (int u = 0; u < SE_U; ++u) {
+        const int i = min(i0 + u * 64, HW4 - 1);
+        xv[u] = x4[i];
+        gv[u] = g4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < SE_U; ++u) {
+        if (i0 + u * 64 >= HW4) break;
+        const float4 w = se_in4(xv[u], sc, sh, t), g = gv[u];
+        acc += (w.x * g.x + w.y * g.y) + (w.z * g.z + w.w * g.w);
+      }
+    }
+  } else {
+    for (int i = lane; i < HW; i += 64) acc += se_in(xp[i], sc, sh, t) * gp[i];
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    const float s = sigm(a[pl]);
+    st_sc1(da + pl, acc * s * (1.f - s));
+  }
+  handoff_drain();
+  if (!handoff_arrive(cnt + n, C / 4, &s_last)) return;
+  for (int i = threadIdx.x; i < C; i += 256) sda[i] = ld_sc1(da + (size_t)n * C + i);
+  __syncthreads();
+  // dh[k] = sum_c W2[c][k] da[n][c]: KT hidden-unit lanes x 256/KT channel slices (a W2 row
+  // is read by consecutive threads), slices summed in order
+  {
+    const int k = threadIdx.x % KT, sl = threadIdx.x / KT, nsl = 256 / KT;
+    float s = 0.f;
+    if (k < sq)
+#pragma unroll 4
+      for (int i = sl; i < C; i += nsl) s += w2[(size_t)i * sq + k] * sda[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < KT && k < sq) {
+      float tt = 0.f;
+      for (int q = 0; q < nsl; ++q) tt += red[q * KT + k];
+      const float z = hpre[(size_t)n * sq + k], sg = sigm(z);
+      const float g = tt * (sg * (1.f + z * (1.f - sg)));
+      dhpre[(size_t)n * sq + k] = g;
+      sdh[k] = g;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += 256) {  // dpooled[n][c] = sum_k W1[k][c] dhpre[n][k]
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < sq; ++k) s += w1[(size_t)k * C + i] * sdh[k];
+    dpooled[(size_t)n * C + i] = s;
+  }
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
+
+// fused squeeze-excitation launches (e2ep_tune key 27 = 2): a workgroup's four planes in one
+// sample; an excite workgroup of 256 vector elements covers at most 255 / 16 + 2 <= SE_XPL
+// planes when a plane has >= 16 of them
+static bool se_fused_ok(int C, int HW) {
+  return g_tune[TUNE_SE_FUSED] == 2 && C % 4 == 0 && ((HW & 3) == 0 ? HW / 4 : HW) >= 16;
+}
 
 extern "C" {
 
@@ -315,14 +500,22 @@ int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, cons
                C, SE_MAXC, sq, SE_MAXSQ);
   hipStream_t s = as_stream(stream);
   const int planes = N * C;
+  const int vec = (HW & 3) == 0;
+  const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
+  unsigned int *cnt = se_fused_ok(C, HW) ? handoff_slots(N) : nullptr;
+  if (cnt) {  // two launches: squeeze + hidden units, logits + excite
+    hipLaunchKernelGGL(k_se_squeeze_mlp, dim3(planes / 4), dim3(256), 0, s, x, tf, HW, w1, b1, sq,
+                       pooled, hpre, cnt);
+    hipLaunchKernelGGL(k_se_excite_logits, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, tf, hpre,
+                       w2, b2, sq, HW, nvec, vec, a, y);
+    return launch_status("e2ep_se_fwd");
+  }
   hipLaunchKernelGGL(k_se_squeeze, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, planes, HW,
                      pooled);
   hipLaunchKernelGGL(k_se_hidden, dim3(N, cdiv(sq, 4)), dim3(256), 0, s, pooled, w1, b1, C, sq,
                      hpre);
   hipLaunchKernelGGL(k_se_logits, dim3(cdiv(C, SE_CT), cdiv(N, SE_NT)), dim3(256),
                      (SE_CT * (sq + 1) + SE_NT * sq) * sizeof(float), s, hpre, w2, b2, N, C, sq, a);
-  const int vec = (HW & 3) == 0;
-  const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
   hipLaunchKernelGGL(k_se_excite, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, tf, a, HW, nvec, vec,
                      y);
   return launch_status("e2ep_se_fwd");
@@ -344,14 +537,20 @@ int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, cons
   const int planes = N * C;
   float *da = workspace, *dhpre = workspace + 2 * planes;
   float *dpooled = dpooled_out ? dpooled_out : workspace + planes;
-  hipLaunchKernelGGL(k_se_da, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes, HW, da);
   float *dhp = workspace + 2 * planes + N * sq;
   const int spans = cdiv(C, SE_DH_SPAN);
   int KT = 1;
   while (KT < sq) KT *= 2;
-  hipLaunchKernelGGL(k_se_dh, dim3(N, spans), dim3(256), 0, s, da, w2, C, sq, KT, dhp);
-  hipLaunchKernelGGL(k_se_dpooled, dim3(N, cdiv(C, 256)), dim3(256), 0, s, dhp, spans, hpre, w1,
-                     C, sq, dhpre, dpooled);
+  unsigned int *cnt = se_fused_ok(C, HW) ? handoff_slots(N) : nullptr;
+  if (cnt) {  // da + the MLP backward in one launch
+    hipLaunchKernelGGL(k_se_da_mlp, dim3(planes / 4), dim3(256), 0, s, x, tf, dy, a, HW, w1, w2,
+                       hpre, sq, KT, da, dhpre, dpooled, cnt);
+  } else {
+    hipLaunchKernelGGL(k_se_da, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes, HW, da);
+    hipLaunchKernelGGL(k_se_dh, dim3(N, spans), dim3(256), 0, s, da, w2, C, sq, KT, dhp);
+    hipLaunchKernelGGL(k_se_dpooled, dim3(N, cdiv(C, 256)), dim3(256), 0, s, dhp, spans, hpre, w1,
+                       C, sq, dhpre, dpooled);
+  }
   if (dw1 || db1 || dw2 || db2) {
     const int outs = 2 * sq * C + sq + C;
     hipLaunchKernelGGL(k_se_wgrad, dim3(cdiv(outs, 256)), dim3(256), 0, s, pooled, hpre, da, dhpre,

@@ -53,9 +53,12 @@ class ParkingDataModule(_Base):
     def _cached_loader(self, dataset, split, shuffle):
         """Under DDP every rank runs setup(): rank 0 alone (re)builds the cache when it is
         missing or was built from another dataset / config (frame_cache.cache_matches), the
-        others wait at a barrier and then open it read-only — and refuse a cache that still
-        does not match rather than train on stale frames."""
-        from dataset.frame_cache import FrameCache, GpuFrameLoader, build_frame_cache, cache_matches
+        others wait for it by polling the file system (frame_cache.wait_for_cache: a build
+        can take longer than a collective's watchdog timeout, so no barrier on the process
+        group) and then open it read-only — and every rank refuses a cache that does not match
+        rather than train on stale frames."""
+        from dataset.frame_cache import (FrameCache, GpuFrameLoader, build_frame_cache,
+                                         cache_matches, wait_for_cache)
         path = os.path.join(self.cfg.frame_cache, split)
         dist = torch.distributed
         ddp = dist.is_available() and dist.is_initialized()
@@ -63,8 +66,8 @@ class ParkingDataModule(_Base):
         world = dist.get_world_size() if ddp else 1
         if rank == 0 and not cache_matches(path, dataset):
             build_frame_cache(dataset, path, workers=getattr(self.cfg, "num_workers", None) or 8)
-        if ddp:
-            dist.barrier()
+        elif rank != 0:
+            wait_for_cache(path, dataset)
         if not cache_matches(path, dataset):
             raise RuntimeError(f"frame cache {path} does not match the {split} dataset "
                                "(built from another dataset or config)")

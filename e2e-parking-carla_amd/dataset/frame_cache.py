@@ -137,18 +137,42 @@ def build_frame_cache(dataset, out_dir, workers=0, chunk=32):
     return FrameCache(out_dir)
 
 
+# every per-sample field a cache is built from, without decoding any frame: the frame file
+# paths (camera, depth and BEV images) and every label / measurement row
+_FINGERPRINT_FIELDS = ("intrinsic", "extrinsic", "front", "left", "right", "rear", "front_depth",
+                       "left_depth", "right_depth", "rear_depth", "topdown", "target_point",
+                       "control", "velocity", "acc_x", "acc_y", "throttle_brake", "steer",
+                       "reverse")
+
+
 def dataset_fingerprint(dataset):
     """SHA-256 over what identifies a CarlaDataset's samples without decoding any frame: the
-    sample count, crop, rig and the per-sample label rows (which encode the task / frame
-    ordering).  A cache whose fingerprint differs belongs to another dataset or config."""
+    sample count, crop, rig, the frame file paths of every sample (so a cache built from
+    another image set or root does not match) and the per-sample label / measurement rows
+    (acc_x / acc_y included: they feed ego_motion).  A cache whose fingerprint differs belongs
+    to another dataset or config."""
     import hashlib
     h = hashlib.sha256()
     h.update(repr((len(dataset), int(dataset.image_crop))).encode())
-    for a in (dataset.intrinsic, dataset.extrinsic, dataset.target_point, dataset.control,
-              dataset.velocity, dataset.throttle_brake, dataset.steer, dataset.reverse):
-        a = np.ascontiguousarray(np.asarray(a))
-        h.update(a.dtype.str.encode() + repr(a.shape).encode() + a.tobytes())
+    for name in _FINGERPRINT_FIELDS:
+        a = np.ascontiguousarray(np.asarray(getattr(dataset, name)))
+        h.update(name.encode() + a.dtype.str.encode() + repr(a.shape).encode() + a.tobytes())
     return h.hexdigest()
+
+
+def wait_for_cache(path, dataset, timeout_s=None, poll_s=2.0):
+    """Block until `path` holds a complete cache built from `dataset` (cache_matches), polling
+    the file system — the non-building ranks of a data-parallel job wait here while rank 0
+    builds it, instead of in a collective whose watchdog would time out a long build.  Raises
+    TimeoutError after `timeout_s` (default: E2EP_CACHE_WAIT_S or 24 h)."""
+    import time
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("E2EP_CACHE_WAIT_S", 24 * 3600))
+    t_end = time.monotonic() + timeout_s
+    while not cache_matches(path, dataset):
+        if time.monotonic() > t_end:
+            raise TimeoutError(f"frame cache {path}: no matching cache after {timeout_s:.0f} s")
+        time.sleep(poll_s)
 
 
 def cache_matches(path, dataset):

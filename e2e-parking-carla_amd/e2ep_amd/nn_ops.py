@@ -1015,6 +1015,14 @@ def embed_tokens(tok, table, pos, p=0.0, seed=None):
     if tok.dtype != torch.int64 or tok.dim() != 2 or tok.stride(1) != 1 or tok.device != table.device:
         raise _lib.E2EPError("embed_tokens: tok must be a (B, T) int64 device tensor with unit column stride")
     pos = pos.contiguous()
+    if tok.numel() and not torch.cuda.is_current_stream_capturing():
+        # nn.Embedding raises on an id outside [0, V) (a wrong token_nums or PAD arithmetic);
+        # the kernels clamp only for memory safety, so check here, outside captures (a
+        # captured step checks its tokens in the eager warm-up steps)
+        lo, hi = (int(v) for v in torch.aminmax(tok))
+        if lo < 0 or hi >= table.shape[0]:
+            raise IndexError(f"embed_tokens: token id out of range [0, {table.shape[0]}): "
+                             f"min {lo}, max {hi}")
     if p > 0.0 and seed is None:
         seed = rng.seed(table.device)
     return _EmbedTokens.apply(tok, table, pos, float(p), seed)

@@ -75,3 +75,20 @@ def backward_rest(pairs):
     outs = [a for a, slot in pairs if slot]
     if outs:
         torch.autograd.backward(outs, [slot[0] for a, slot in pairs if slot])
+
+
+def grad_marks(params):
+    """(gradient tensor id, storage address, version counter) of each parameter's .grad (None
+    when it has none): what a later backward changes when it accumulates into a gradient — in
+    place (version), or by handing autograd's result over (a new tensor)."""
+    return [None if p.grad is None else (id(p.grad), p.grad.data_ptr(), p.grad._version)
+            for p in params]
+
+
+def stage2_leaves_stage1(params, marks):
+    """True when the stage-2 backward left the stage-1 gradients (`params`, their marks taken
+    after stage 1) untouched.  A parameter used on both sides of a cut (shared weights) would
+    have its stage-1 gradient gathered and all-reduced before stage 2 adds its share, and the
+    step would train on wrong gradients — the segmented capture falls back to one backward
+    graph instead."""
+    return grad_marks(params) == marks

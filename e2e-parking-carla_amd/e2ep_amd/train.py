@@ -185,10 +185,7 @@ class TrainStep:
         # hook-driven bucket all-reduce overlapping backward: eager steps with RCCL, and host
         # tensors (gloo on CPU); never inside a captured graph (module docstring)
         self._bucket_mb = bucket_mb
-        # overlap="captured" (diagnostics only, scripts/diag_capture_hooks.py): the hook-driven
-        # buckets inside the captured backward, the round-2 design that replayed wrong gradients
-        captured_hooks = overlap == "captured"
-        self.overlap = bool(self.ddp and overlap and (not graph or captured_hooks) and
+        self.overlap = bool(self.ddp and overlap and not graph and
                             (self.backend == "nccl" or not self.flat_grad.is_cuda))
         self.buckets = (GradBuckets(self.params, self.opt, self.flat_grad, bucket_mb)
                         if self.overlap else None)
@@ -200,7 +197,7 @@ class TrainStep:
         self.loss = None
         self.g_bwd = self.g_gather = self.g_opt = None
         # segmented backward (graph mode, RCCL): stage graphs, their gathers, bucket ranges
-        self.segmented = bool(self.ddp and graph and self.backend == "nccl" and not captured_hooks)
+        self.segmented = bool(self.ddp and graph and self.backend == "nccl")
         self.g_s1 = self.g_s1g = self.g_s2 = self.g_s2g = None
         self.seg_buckets = None  # ([stage-1 (lo, hi)], [stage-2 (lo, hi)]) of the flat buffer
         self._rig = _rig_key(batch)
@@ -303,7 +300,10 @@ class TrainStep:
         g1g, _, _ = graphs.capture(lambda: self.opt.gather_grads(self.flat_grad,
                                                                  params=(i1, len(self.params))),
                                    pool=g1.pool())
+        marks = segments.grad_marks(self.params[i1:])
         g2, _, _ = graphs.capture(self._stage2, pool=g1.pool())
+        if not segments.stage2_leaves_stage1(self.params[i1:], marks):
+            return False  # a parameter on both sides of the cut: one backward graph instead
         self.opt.prepare()
         if i1 > 0:
             g2g, _, _ = graphs.capture(lambda: self.opt.gather_grads(self.flat_grad, params=(0, i1)),

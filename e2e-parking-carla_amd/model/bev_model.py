@@ -58,26 +58,34 @@ class BevModel(nn.Module):
         return lo.tolist(), res.tolist(), dims
 
     def plan(self, intrinsics, extrinsics, device):
-        """Pillar plan for this batch's rig.  The plan is a pure function of (frustum, K, E);
-        when K and E are host tensors (the dataloader / agent case) the rig algebra is the
-        reference's own fp32 CPU ops (lss.rig_transforms_host) and the plan is memoised on their
-        bytes, since the CARLA rig is constant; device K and E go through
-        the fp64 device algebra (lss.rig_transforms) with no host synchronisation.  E2EP_PLAN_CACHE=0
-        rebuilds it every call (6 kernel launches, no host synchronisation)."""
+        """Pillar plan for this batch's rig.  The plan is a pure function of (frustum, K, E).
+        The rig algebra is the reference's own fp32 CPU ops (lss.rig_transforms_host,
+        model/bev_model.py:46-53), so the pillar index is the reference's bit for bit, and the
+        plan is memoised on the K / E bytes, since the CARLA rig is constant (SURVEY.md §0
+        fact 2).  Host K / E (the dataloader / agent case) are read in place; device K / E are
+        copied to the host first (one 8-matrix synchronising copy per call, then the same
+        memoised path).  Only inside a HIP-graph capture, where no host copy can run, device
+        K / E go through the fp64 device algebra (lss.rig_transforms), which the capture
+        replays from the device rig each time; its last fp32 ulp is not LAPACK's, so a few
+        points on a cell edge may land in the neighbouring pillar (tests/test_lss_gpu.py).
+        E2EP_PLAN_CACHE=0 rebuilds the plan every call."""
         if self._host_consts is None:
             self._host_consts = self._consts()
         lo, res, dims = self._host_consts
+        on_dev = intrinsics.is_cuda or extrinsics.is_cuda
+        if on_dev and torch.cuda.is_current_stream_capturing():
+            combine, trans = lss.rig_transforms(intrinsics, extrinsics, device)
+            return lss.build_plan(self.frustum, combine, trans, lo, res, dims, device)
+        if on_dev:  # synchronising copy: the bit-exact host algebra below
+            intrinsics, extrinsics = intrinsics.detach().cpu(), extrinsics.detach().cpu()
         key = None
-        if lss.plan_cache_enabled() and not intrinsics.is_cuda and not extrinsics.is_cuda:
+        if lss.plan_cache_enabled():
             key = (str(device), intrinsics.shape, extrinsics.shape,
                    intrinsics.detach().float().contiguous().numpy().tobytes(),
                    extrinsics.detach().float().contiguous().numpy().tobytes())
             if key == self._plan_key and self._plan is not None:
                 return self._plan
-        if intrinsics.is_cuda or extrinsics.is_cuda:  # device rig: fp64 algebra on the GPU
-            combine, trans = lss.rig_transforms(intrinsics, extrinsics, device)
-        else:  # host rig: the reference's fp32 CPU ops, so the pillar index is bit-exact
-            combine, trans = lss.rig_transforms_host(intrinsics, extrinsics)
+        combine, trans = lss.rig_transforms_host(intrinsics, extrinsics)
         plan = lss.build_plan(self.frustum, combine, trans, lo, res, dims, device)
         if key is not None:
             self._plan_key, self._plan = key, plan

@@ -21,6 +21,10 @@ SHAPES = {"stem": (8, 65, 256, 256, 64, 7, 7, 128, 128, 2, 2, 3, 3, 1, 1),
           "bev256": (8, 256, 16, 16, 256, 3, 3, 16, 16, 1, 1, 1, 1, 1, 1),
           "up216": (32, 216, 32, 32, 64, 3, 3, 32, 32, 1, 1, 1, 1, 1, 1),
           "exp112": (32, 112, 16, 16, 672, 1, 1, 16, 16, 1, 1, 0, 0, 1, 1)}
+# data-gradient rows the product computes (bev_stem.py: the target-point plane, input channel
+# 64 of the stem, is a constant and gets no gradient; round 3's PMC ran 65 rows: two 64-row
+# tiles, twice the MFMA work of the product's launch)
+GRAD_CHANNELS = {"stem": 64}
 
 
 def main():
@@ -40,13 +44,14 @@ def main():
     wt = conv.tap_major(torch.randn(Cout, Cin, R, S, device="cuda", generator=g) * 0.05)
     gy = torch.randn(N, Cout, P, Q, device="cuda", generator=g)
     y = torch.empty(N, Cout, P, Q, device="cuda")
-    dx = torch.empty(N, Cin, H, W, device="cuda")
+    gc = GRAD_CHANNELS.get(which, Cin)
+    dx = torch.empty(N, gc, H, W, device="cuda")
     dw = torch.empty(Cout, Cin, R, S, device="cuda")
     for _ in range(reps):
         if kind in ("fwd", "all"):
             conv.conv_fwd(x, wt, None, d, 0, y, w_layout=1)
         if kind in ("dgrad", "all"):
-            conv.conv_dgrad(gy, wt, d, Cin, dx, w_layout=1)
+            conv.conv_dgrad(gy, wt, d, gc, dx, w_layout=1)
         if kind in ("wgrad", "all"):
             conv.conv_wgrad(gy, x, d, dw)
     torch.cuda.synchronize()

@@ -80,6 +80,18 @@ def run(tag, wgrad_fork, reprepare, hooks=True):
                            overlap="captured", optimizer=opt) if hooks else
                  TrainStep(m_ddp, _parking_batch(), graph=True, warmup=1, optimizer=opt))
         T.graphs.capture = real_capture
+        # round-4 check (verdict r3 item 8): the weights both modules carry into the capture,
+        # i.e. after their eager warm-up step, against each other and the initial weights
+        w0 = dict(_parking_module().named_parameters())
+        wr, wd = dict(m_ref.named_parameters()), dict(m_ddp.named_parameters())
+        n_ref_moved = sum(not torch.equal(wr[k], w0[k]) for k in w0 if wr[k].requires_grad)
+        n_ddp_moved = sum(not torch.equal(wd[k], w0[k]) for k in w0 if wd[k].requires_grad)
+        n_diff = sum(not torch.equal(wr[k], wd[k]) for k in w0 if wr[k].requires_grad)
+        print(f"{tag}: after warm-up: ref moved {n_ref_moved}, hooked moved {n_ddp_moved}, "
+              f"differ {n_diff} (of {sum(p.requires_grad for p in w0.values())}); hooked has-grad "
+              f"mask sum {int(s_ddp.has_grad.sum()) if s_ddp.has_grad is not None else None}",
+              flush=True)
+        del w0
         if not hooks:  # harness check: two plain captured steps
             s_ref.g_bwd.replay()
             s_ddp.g_bwd.replay()

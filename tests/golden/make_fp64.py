@@ -6,7 +6,7 @@ Deterministic-train mode (BN batch statistics at B=2) is ill-conditioned: the re
 own fp32 result differs from this fp64 value by ~1e-3 on the segmentation logits and ~2 %
 on some weight gradients (the cumsum-difference pooling noise, SURVEY.md §0 fact 4, is
 amplified by batch-statistic BN).  Parity tests therefore measure both the product and the
-reference against this fp64 value.   Run: python tests/golden/make_fp64.py [b8|c4]
+reference against this fp64 value.   Run: python tests/golden/make_fp64.py [b8|c4|c4b4]
 (b8: the same for the B=8 bench batch, model_train_b8.npz; c4: model_train_c4.npz.)
 """
 import os
@@ -139,10 +139,49 @@ def main_c4():
         print("wrote", name + "_fp64.npz")
 
 
+def main_c4b4():
+    """fp64 companion of model_train_c4b4.npz (C4 at the benched B=4, deterministic train)."""
+    import json
+    torch.set_num_threads(8)
+
+    class CfgC4(O.Cfg):
+        final_dim = [512, 512]
+
+    with open(os.path.join(HERE, "meta.json")) as f:
+        info = json.load(f)["model_train_c4b4"]
+    data = synthetic.synthetic_batch(4, seed=17, hires=True)
+    noise = synthetic.target_noise(4, seed=17)
+    d = {k: (v.double() if v.is_floating_point() and k not in ("intrinsics", "extrinsics") else v)
+         for k, v in data.items()}
+    m = oracle_model(torch.float64, CfgC4).train()
+    # 24 images at 512^2 in fp64 keep > 60 GB of activations for the backward: recompute each
+    # EfficientNet block in the backward instead (same arithmetic; no dropout / drop-connect in
+    # this protocol, so the recomputed forward is the forward)
+    from torch.utils.checkpoint import checkpoint
+    for blk in m.bev_model.cam_encoder.backbone._blocks:
+        blk.forward = (lambda f: lambda x, drop_connect_rate=None: checkpoint(
+            f, x, drop_connect_rate, use_reentrant=False))(blk.forward)
+    losses, (pc, ps, pd) = O.train_losses(m, d, noise)
+    losses["train_loss"].backward()
+    params = dict(m.named_parameters())
+    fx = {"loss_control": np.float64(losses["control_loss"].item()),
+          "loss_seg": np.float64(losses["segmentation_loss"].item()),
+          "loss_depth": np.float64(losses["depth_loss"].item()),
+          "pred_control": pc.detach().numpy(),
+          "seg_sample": sample(ps).numpy(), "depth_sample": sample(pd).numpy(),
+          "gnorm_all": np.array([float(params[k].grad.norm()) for k in info["grad_keys"]])}
+    for k in info["probe"]:
+        fx["gsample::" + k] = sample(params[k].grad).numpy()
+    np.savez_compressed(os.path.join(HERE, "model_train_c4b4_fp64.npz"), **fx)
+    print("wrote model_train_c4b4_fp64.npz")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "b8":
         main_b8()
     elif len(sys.argv) > 1 and sys.argv[1] == "c4":
         main_c4()
+    elif len(sys.argv) > 1 and sys.argv[1] == "c4b4":
+        main_c4b4()
     else:
         main()

@@ -2,7 +2,8 @@
 
 Run in the build container only (needs /root/reference):  python tests/golden/make_golden.py
 (`python tests/golden/make_golden.py b8` regenerates only the B=8 fixtures, `... c4` adds the
-C4 6-camera 512x512 fixtures, `... b8bf16` the C3 bf16-autocast comparator.)
+C4 6-camera 512x512 fixtures, `... c4b4` the C4 deterministic-train step at the benched B=4,
+`... b8bf16` the C3 bf16-autocast comparator.)
 
 The reference has no tests or fixtures of its own, so every golden vector is
 produced here by importing the reference's Python modules unmodified, with:
@@ -212,23 +213,25 @@ def b8_fixtures(ref, orc, state, cfg, closs, sloss, dloss, meta):
 
 def b8_bf16amp_fixtures(ref, state, closs, sloss, dloss, meta):
     """C3 comparator: the reference's own deterministic-train step at the B=8 bench batch run
-    the way a bf16 mixed-precision trainer runs its convolutional modules (camera encoder, BEV
-    encoder, segmentation head — the layers the product's C3 mode runs on bf16 operands) —
-    their forward under torch.autocast(bfloat16) (the CPU autocast; its bf16 op list covers
-    conv / linear / matmul like the GPU one), activations between their layers in bf16, fp32
-    parameters and gradients; the transformer, lift-splat and losses stay fp32 as in the
-    product.  Its error against the fp64 oracle is the bf16 error budget the
-    product's C3 mode is held to (tests/test_train_step_b8_gpu.py)."""
+    the way a bf16 mixed-precision trainer runs the modules the product's C3 mode puts on bf16
+    operands — the camera encoder, BEV encoder and segmentation head (conv GEMMs) and, since
+    round 3, the feature-fusion encoder and control decoder (their linear / attention
+    projections) — their forward under torch.autocast(bfloat16) (the CPU autocast; its bf16
+    op list covers conv / linear / matmul like the GPU one), fp32 parameters and gradients;
+    lift-splat, the depth softmax and the losses stay fp32 as in the product.  Its error
+    against the fp64 oracle is the bf16 error budget the product's C3 mode is held to
+    (tests/test_train_step_b8_gpu.py)."""
     data = synthetic.synthetic_batch(8, seed=11)
     noise = synthetic.target_noise(8, seed=11)
     deterministic(ref)
     ref.load_state_dict(state)
     ref.train()
     ref.zero_grad(set_to_none=True)
-    # the convolutional modules run under autocast; their outputs return to fp32 at the module
-    # boundary (the reference's lift-splat index_put and everything after it require fp32: the
-    # whole model under autocast raises in model/bev_model.py:103)
-    conv_mods = (ref.bev_model.cam_encoder, ref.bev_encoder, ref.segmentation_head)
+    # the bf16 modules run under autocast; their outputs return to fp32 at the module boundary
+    # (the reference's lift-splat index_put and everything after it require fp32: the whole
+    # model under autocast raises in model/bev_model.py:103)
+    conv_mods = (ref.bev_model.cam_encoder, ref.bev_encoder, ref.segmentation_head,
+                 ref.feature_fusion, ref.control_predict)
     saved = [m.forward for m in conv_mods]
 
     def amp(fwd):
@@ -262,7 +265,8 @@ def b8_bf16amp_fixtures(ref, state, closs, sloss, dloss, meta):
         fx["gsample::" + k] = sample(rgrad[k].grad).numpy()
     np.savez_compressed(os.path.join(OUT, "model_train_b8_bf16amp.npz"), **fx)
     meta["model_train_b8_bf16amp"] = {"batch_seed": 11, "noise_seed": 11,
-                                      "autocast": "cpu bfloat16: cam_encoder, bev_encoder, segmentation_head forward",
+                                      "autocast": "cpu bfloat16: cam_encoder, bev_encoder, segmentation_head, "
+                                                  "feature_fusion, control_predict forward",
                                       "grad_keys": "model_train_b8"}
     ref.zero_grad(set_to_none=True)
 
@@ -338,6 +342,46 @@ def c4_fixtures(cfg, meta):
     meta["model_train_c4"] = {"batch_seed": 13, "noise_seed": 13, "hires": True, "grad_keys": gkeys}
 
 
+def c4b4_fixtures(cfg, meta):
+    """The benched C4 step's batch shape (BASELINE configs[3]: 6 cameras at 512x512, B=4 per
+    GPU): one deterministic-train forward/backward of the reference (BN batch statistics over
+    24 camera images / 4 BEV samples), its three losses, control logits, every parameter's
+    gradient norm and strided samples of the probe tensors' gradients.  The captured B=4 C4
+    TrainStep is held to it (tests/test_model_c4_gpu.py)."""
+    from model.parking_model import ParkingModel
+    from loss.control_loss import ControlLoss
+    from loss.seg_loss import SegmentationLoss
+    from loss.depth_loss import DepthLoss
+    cfg.final_dim = [512, 512]
+    cfg.image_crop = 512
+    torch.manual_seed(0)
+    ref = ParkingModel(cfg)
+    state = make_state(ref.state_dict(), seed=1234)
+    deterministic(ref)
+    ref.load_state_dict(state)
+    ref.train()
+    data = synthetic.synthetic_batch(4, seed=17, hires=True)
+    noise = synthetic.target_noise(4, seed=17)
+    closs, dloss = ControlLoss(cfg), DepthLoss(cfg)
+    sloss = SegmentationLoss(class_weights=torch.Tensor(cfg.seg_vehicle_weights))
+    with FixedRand(noise):
+        pc, ps, pd = ref(data)
+    lc, ls, ld = closs(pc, data), sloss(ps.unsqueeze(1), data["segmentation"]), dloss(pd, data["depth"])
+    (lc + ls + ld).backward()
+    rgrad = dict(ref.named_parameters())
+    gkeys = [k for k, v in rgrad.items() if v.grad is not None]
+    probe = make_grad_probe_keys(state.keys())
+    fx = {"loss_control": np.float64(lc), "loss_seg": np.float64(ls), "loss_depth": np.float64(ld),
+          "pred_control": pc.detach().numpy(),
+          "seg_sample": sample(ps).numpy(), "depth_sample": sample(pd).numpy(),
+          "gnorm_all": np.array([float(rgrad[k].grad.double().norm()) for k in gkeys])}
+    for k in probe:
+        fx["gsample::" + k] = sample(rgrad[k].grad).numpy()
+    np.savez_compressed(os.path.join(OUT, "model_train_c4b4.npz"), **fx)
+    meta["model_train_c4b4"] = {"batch_seed": 17, "noise_seed": 17, "hires": True, "batch": 4,
+                                "probe": probe, "grad_keys": gkeys, "sample": SAMPLE}
+
+
 def main(only=None):
     install_shims()
     torch.set_num_threads(8)
@@ -354,10 +398,10 @@ def main(only=None):
     cfg.device = torch.device("cpu")
     meta = {"generator": "tests/golden/make_golden.py", "reference": REF,
             "torch": torch.__version__, "weights_seed": 1234}
-    if only == "c4":  # add the C4 fixtures, keep the others and their meta
+    if only in ("c4", "c4b4"):  # add the C4 fixtures, keep the others and their meta
         with open(os.path.join(OUT, "meta.json")) as f:
             meta = json.load(f)
-        c4_fixtures(cfg, meta)
+        (c4_fixtures if only == "c4" else c4b4_fixtures)(cfg, meta)
         with open(os.path.join(OUT, "meta.json"), "w") as f:
             json.dump(meta, f, indent=1)
         print("wrote C4 golden vectors to", OUT)

@@ -156,8 +156,9 @@ def test_frame_cache_holds_the_reference_inputs(root, cfg, tmp_path):
 
 def test_frame_cache_reuse_is_validated(root, cfg, tmp_path):
     """A cache directory is reused only when it is complete (meta.json, written last and
-    atomically) and was built from the same dataset (fingerprint of count, crop, rig and label
-    rows); another split or changed labels do not match, and a rebuild invalidates first."""
+    atomically) and was built from the same dataset (fingerprint of count, crop, rig, frame paths
+    and label / measurement rows); another split, changed labels, moved frames or changed
+    accelerations do not match, and a rebuild invalidates first."""
     from dataset.carla_dataset import CarlaDataset
     from dataset.frame_cache import build_frame_cache, cache_matches
     path = str(tmp_path / "fc")
@@ -170,6 +171,59 @@ def test_frame_cache_reuse_is_validated(root, cfg, tmp_path):
     changed = CarlaDataset(root, 1, cfg)
     changed.target_point = changed.target_point + 1.0
     assert not cache_matches(path, changed)
+    # same labels, other frames (another image set / root) or other ego accelerations
+    moved = CarlaDataset(root, 1, cfg)
+    moved.front = np.array([f.replace("rgb_front", "rgb_front_other") for f in moved.front])
+    assert not cache_matches(path, moved)
+    acc = CarlaDataset(root, 1, cfg)
+    acc.acc_y = acc.acc_y + 0.5
+    assert not cache_matches(path, acc)
+
+
+def _cache_rank(rank, world, port, root, cfg, path, out):
+    """One rank of the frame-cache setup under a process group whose collective timeout (2 s)
+    is shorter than rank 0's cache build (5 s)."""
+    import datetime
+    import time
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=2))
+    from dataset import frame_cache
+    from dataset.dataloader import ParkingDataModule
+    from dataset.carla_dataset import CarlaDataset
+    real_build = frame_cache.build_frame_cache
+
+    def slow_build(*a, **k):
+        time.sleep(5.0)
+        return real_build(*a, **k)
+
+    frame_cache.build_frame_cache = slow_build
+    frame_cache.GpuFrameLoader = lambda cache, *a, **k: ("loader", len(cache), k["rank"], k["world"])
+    cfg.frame_cache = path
+    got = ParkingDataModule(cfg)._cached_loader(CarlaDataset(root, 1, cfg), "train", True)
+    dist.barrier()  # the group is still healthy after the long build
+    out[rank] = got
+    dist.destroy_process_group()
+
+
+def test_ddp_cache_build_outlasts_collective_timeout(root, cfg, tmp_path):
+    """under DDP rank 0 builds the frame cache while the other ranks wait.  They
+    wait by polling the file system (frame_cache.wait_for_cache), not in a collective, so a
+    build longer than the process group's timeout does not abort them."""
+    import copy
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_cache_rank, args=(2, port, root, copy.copy(cfg), str(tmp_path / "fc"), out),
+                 nprocs=2, join=True)
+        res = dict(out)
+    assert res[0][0] == res[1][0] == "loader" and res[0][1] == res[1][1] > 0
+    assert (res[0][2], res[1][2]) == (0, 1) and res[0][3] == res[1][3] == 2
 
 
 def test_frame_cache_empty_split(tmp_path, cfg):

@@ -53,19 +53,46 @@ def test_device_rig_algebra_reproduces_reference_pillars_4cam():
     assert np.array_equal(pil, g["pillar"].reshape(-1))
 
 
-def test_device_rig_algebra_hires_6cam_band():
-    """Device rigs only (K/E already on the GPU): the fp64 device algebra vs the reference's
-    fp32 LAPACK combine at 6-cam 512^2.  The reference's last ulp is host-ISA dependent and a
-    handful of the 1.18M points sit within an ulp of a cell edge; the flip count is printed and
-    recorded (host rigs, the dataset / agent path, are bit-exact: next test)."""
+def test_captured_device_rig_algebra_hires_6cam_band():
+    """The capture-only fallback (BevModel.plan inside a HIP-graph capture with K/E on the
+    GPU, where no host copy can run): the fp64 device algebra vs the reference's fp32 LAPACK
+    combine at 6-cam 512^2.  LAPACK's last ulp is not reproducible on the device and a handful
+    of the 1.18M points sit within an ulp of a cell edge; the flip count is recorded.  Every
+    other rig path is bit-exact (0 flips): the next two tests."""
+    from test_model_b8_gpu import _record
     g = golden("geometry_6cam_512.npz")
     from oracle import geom_c
     g4 = golden("geometry_4cam_256.npz")
     ref = geom_c.geom_index(g["frustum"], g["combine"], g["trans"], g4["lo"], g4["res"], g4["dim"]).reshape(-1)
     _, pil = _pillar_from_rig(torch.from_numpy(g["K"]), torch.from_numpy(g["E"]), g["frustum"])
     flips = int((pil != ref).sum())
-    print(f"device-rig pillar flips at 6x512^2: {flips} of {pil.size}")
+    print(f"capture-path device-rig pillar flips at 6x512^2: {flips} of {pil.size}")
+    _record("rig", "capture_fp64_device_algebra_6cam_flips", flips=flips, points=int(pil.size))
     assert flips <= 16
+
+
+@pytest.mark.parametrize("rig", ["geometry_4cam_256.npz", "geometry_6cam_512.npz"])
+def test_device_rig_pillar_index_bit_exact_end_to_end(rig):
+    """K, E already on the GPU through BevModel.plan (outside a capture): the rig is copied to
+    the host and goes through the reference's own fp32 CPU algebra, so the pillar table equals
+    the reference golden bit for bit (0 flips) at both rigs, at B=1 and over a B=4 batch."""
+    from model.bev_model import BevModel
+    from tool.config import default_cfg
+    g = golden(rig)
+    hires = "6cam" in rig
+    cfg = default_cfg(final_dim=[512, 512], image_crop=512) if hires else default_cfg()
+    bm = BevModel(cfg).to(DEV)
+    for B in (1, 4):
+        K = torch.from_numpy(g["K"])[None].repeat(B, 1, 1, 1).to(DEV)
+        E = torch.from_numpy(g["E"])[None].repeat(B, 1, 1, 1).to(DEV)
+        pil = bm.plan(K, E, DEV).pillar.view(B, -1).cpu().numpy().astype(np.int32)
+        for b in range(B):
+            if hires:
+                ref = meta()["geometry_6cam_512"]["pillar_sha256"]
+                assert hashlib.sha256(pil[b].tobytes()).hexdigest() == ref
+            else:
+                flips = int((pil[b] != g["pillar"].reshape(-1)).sum())
+                assert flips == 0, flips
 
 
 @pytest.mark.parametrize("rig", ["geometry_4cam_256.npz", "geometry_6cam_512.npz"])

@@ -46,6 +46,16 @@ def dw_grid(request):
     _lib.load().e2ep_tune(24, prev)
 
 
+@pytest.fixture(params=[2, 1], ids=["se_fused", "se_separate"])
+def se_path(request):
+    """Squeeze-excitation launch plan (e2ep_tune key 27): 2 = the MLP inside the squeeze /
+    excite / da launches (in-launch last-workgroup hand-off), 1 = the separate MLP kernels."""
+    from e2ep_amd import _lib
+    prev = _lib.load().e2ep_tune(27, request.param)
+    yield request.param
+    _lib.load().e2ep_tune(27, prev)
+
+
 @pytest.fixture(params=[1, 0], ids=["bn_one_launch", "bn_split"])
 def bn_path(request):
     """Run a BN test through the single-launch block-per-channel kernels (channels of
@@ -343,9 +353,14 @@ def test_lift_splat_bwd_takes_channels_last_gradient():
 
 
 @pytest.mark.parametrize("shape", [(8, 96, 16, 16, 6), (4, 40, 9, 7, 10), (32, 672, 16, 16, 28),
-                                   (32, 1632, 8, 8, 68), (5, 300, 3, 3, 75), (2, 4096, 2, 2, 256)])
-def test_squeeze_excite_fused(shape):
-    """Fused SE (pool -> 1x1 -> swish -> 1x1 -> sigmoid gate) vs fp64 torch, all gradients."""
+                                   (32, 1632, 8, 8, 68), (5, 300, 3, 3, 75), (2, 4096, 2, 2, 256),
+                                   (3, 68, 17, 4, 8), (7, 36, 5, 5, 9), (3, 42, 10, 10, 7),
+                                   (32, 960, 16, 16, 40)])
+def test_squeeze_excite_fused(shape, se_path):
+    """Fused SE (pool -> 1x1 -> swish -> 1x1 -> sigmoid gate) vs fp64 torch, all gradients;
+    both launch plans (se_path), incl. excite workgroups straddling up to 17 planes (HW = 68),
+    scalar planes (HW = 25) and the C % 4 != 0 fallback (C = 42); the fused plan bitwise
+    deterministic run to run."""
     from e2ep_amd import nn_ops
     N, C, H, W, sq = shape
     g = _g(C + sq)
@@ -368,12 +383,18 @@ def test_squeeze_excite_fused(shape):
     assert rel_l2(y, y64) < 1e-6
     for got, ref in zip(ts, rs):
         assert rel_l2(got.grad, ref.grad) < 1e-5
+    ts2 = [t.detach().clone().requires_grad_(True) for t in ts]
+    y2 = nn_ops.squeeze_excite(*ts2)
+    y2.backward(dy.to(DEV))
+    assert torch.equal(y, y2)
+    for a, b in zip(ts, ts2):
+        assert torch.equal(a.grad, b.grad)
 
 
 @pytest.mark.parametrize("case", [(8, 96, 16, 16, 6, True), (4, 40, 9, 7, 10, True),
                                   (32, 672, 16, 16, 28, True), (5, 300, 3, 3, 75, False),
-                                  (2, 144, 64, 64, 6, True)])
-def test_bn_swish_se_fused(case, bn_path):
+                                  (2, 144, 64, 64, 6, True), (32, 144, 64, 64, 6, True)])
+def test_bn_swish_se_fused(case, bn_path, se_path):
     """MBConv _bn1 -> swish -> SE with the BN + swish applied on load by the SE kernels
     (e2ep_bn_stats + se x_scale/x_shift; backward through e2ep_bn_bwd gate_logit /
     gate_dpooled), train and eval, vs fp64 torch: output, every gradient, running stats."""

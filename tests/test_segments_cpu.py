@@ -68,3 +68,25 @@ def test_cut_is_identity_outside_record():
         u = torch.randn(3)  # no gradient: not a cut point
         assert segments.cut(u) is u
     assert rec.pairs == []
+
+
+def test_stage2_touching_a_stage1_gradient_is_detected():
+    """The segmented graph step all-reduces stage-1 gradients before stage 2 runs; a parameter
+    used on both sides of the cut (a shared weight) would be all-reduced before stage 2 adds
+    its share.  segments.stage2_leaves_stage1 sees it (TrainStep then captures one backward)."""
+    torch.manual_seed(0)
+    lin_lo, lin_hi = torch.nn.Linear(4, 4), torch.nn.Linear(4, 1)
+    shared = torch.nn.Parameter(torch.randn(4))
+    x = torch.randn(3, 4)
+    for share in (False, True):
+        for p in (*lin_lo.parameters(), *lin_hi.parameters(), shared):
+            p.grad = None
+        with segments.record() as rec:
+            a = lin_lo(x * shared) if share else lin_lo(x)   # below the cut
+            a = segments.cut(a)
+            loss = lin_hi(torch.tanh(a) * shared).sum()       # above the cut (stage 1)
+        loss.backward()
+        stage1 = [shared, *lin_hi.parameters()]
+        marks = segments.grad_marks(stage1)
+        segments.backward_rest(rec.pairs)
+        assert segments.stage2_leaves_stage1(stage1, marks) == (not share)

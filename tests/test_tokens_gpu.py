@@ -106,3 +106,17 @@ def test_embed_tokens_dropout_mask_consistent():
     want = torch.zeros_like(dtable).index_add_(0, tgt.reshape(-1), scale.reshape(-1, scale.shape[-1]))
     assert torch.allclose(dtable, want, rtol=1e-6)
     assert torch.allclose(dpos, scale.sum(0, keepdim=True), rtol=1e-6)
+
+
+def test_embed_tokens_out_of_range_raises_like_embedding():
+    """nn.Embedding raises on an id outside [0, V); so does embed_tokens (the kernels' clamp is a
+    memory-safety backstop only), for a negative id and for id == V."""
+    from e2ep_amd import nn_ops
+    table = torch.randn(10, 16, device=DEV)
+    pos = torch.randn(1, 3, 16, device=DEV)
+    for bad in (-1, 10):
+        tok = torch.tensor([[1, bad, 2]], dtype=torch.int64, device=DEV)
+        with pytest.raises(IndexError):
+            nn_ops.embed_tokens(tok, table, pos)
+        with pytest.raises(IndexError):
+            torch.nn.functional.embedding(tok.cpu(), table.cpu())
