@@ -660,9 +660,14 @@ size_t e2ep_bn_workspace(int N, int C, int H, int W) {
 int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const float *res,
                 const float *dc_rand, float dc_keep, float *running_mean, float *running_var,
                 int N, int C, int H, int W, int train, float momentum, float eps, int act,
-                float *mean, float *invstd, float *y, void *workspace, void *stream) {
+                float *mean, float *invstd, float *y, void *workspace, size_t workspace_bytes,
+                void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
                E2EP_EINVAL, "e2ep_bn_fwd: bad shape");
+  E2EP_REQUIRE(!train || (workspace && workspace_bytes >= e2ep_bn_workspace(N, C, H, W)),
+               E2EP_EINVAL, "%s: workspace %zu bytes < %zu (e2ep_bn_workspace)", "e2ep_bn_fwd",
+               workspace_bytes, e2ep_bn_workspace(N, C, H, W));
+
   E2EP_REQUIRE(act >= 0 && act <= 2, E2EP_EINVAL, "e2ep_bn_fwd: act must be 0/1/2");
   E2EP_REQUIRE(train || (running_mean && running_var), E2EP_EINVAL,
                "e2ep_bn_fwd: eval needs running stats");
@@ -708,9 +713,13 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
 int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *running_mean,
                   float *running_var, int N, int C, int H, int W, int train, float momentum,
                   float eps, float *mean, float *invstd, float *scale, float *shift,
-                  void *workspace, void *stream) {
+                  void *workspace, size_t workspace_bytes, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
                E2EP_EINVAL, "e2ep_bn_stats: bad shape");
+  E2EP_REQUIRE(!train || (workspace && workspace_bytes >= e2ep_bn_workspace(N, C, H, W)),
+               E2EP_EINVAL, "%s: workspace %zu bytes < %zu (e2ep_bn_workspace)", "e2ep_bn_stats",
+               workspace_bytes, e2ep_bn_workspace(N, C, H, W));
+
   E2EP_REQUIRE(train || (running_mean && running_var), E2EP_EINVAL,
                "e2ep_bn_stats: eval needs running stats");
   E2EP_REQUIRE(mean && invstd && scale && shift, E2EP_EINVAL, "e2ep_bn_stats: null output");
@@ -749,7 +758,7 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
                 const float *gamma, const float *beta, const float *res, const float *dc_rand,
                 float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
                 int H, int W, int train, int act, float *dx, float *dgamma, float *dbeta,
-                float *dres, void *workspace, void *stream) {
+                float *dres, void *workspace, size_t workspace_bytes, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
                E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
   E2EP_REQUIRE(!gate_logit == !gate_dpooled, E2EP_EINVAL,
@@ -770,6 +779,9 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
                N, C, HWv, act, train, dx, dres, dgamma, dbeta);
     return launch_status("e2ep_bn_bwd");
   }
+  E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_bn_workspace(N, C, H, W), E2EP_EINVAL,
+               "e2ep_bn_bwd: workspace %zu bytes < %zu (e2ep_bn_workspace)", workspace_bytes,
+               e2ep_bn_workspace(N, C, H, W));
   int sp = bn_splits(per_c, C);
   const int per = cdiv(totv, sp);
   sp = cdiv(totv, per);

@@ -1788,8 +1788,14 @@ int e2ep_conv_gemm_variant(int variant) {
 }
 
 int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
-                  int w_layout, float *y, void *workspace, void *stream) {
+                  int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream) {
   ConvGeom g = make_geom(dims);
+  {
+    const size_t need = e2ep_conv_fwd_workspace(dims);
+    E2EP_REQUIRE(!need || (workspace && workspace_bytes >= need), E2EP_EINVAL,
+                 "e2ep_conv_fwd: workspace %zu bytes < %zu the launch plan needs (query "
+                 "e2ep_conv_fwd_workspace after setting precision / tunables)", workspace_bytes, need);
+  }
   E2EP_REQUIRE(w_layout == 0 || w_layout == 1, E2EP_EINVAL, "e2ep_conv_fwd: w_layout must be 0 or 1");
   g.wlayout = w_layout;
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_fwd: bad geometry");
@@ -1806,8 +1812,15 @@ int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *
 }
 
 int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int m_channels,
-                        int w_layout, const float *res, float *dx, void *workspace, void *stream) {
+                        int w_layout, const float *res, float *dx, void *workspace,
+                        size_t workspace_bytes, void *stream) {
   ConvGeom g = make_geom(dims);
+  if (m_channels > 0 && m_channels <= g.Cin) {
+    const size_t need = e2ep_conv_dgrad_workspace(dims, m_channels);
+    E2EP_REQUIRE(!need || (workspace && workspace_bytes >= need), E2EP_EINVAL,
+                 "e2ep_conv_dgrad: workspace %zu bytes < %zu the launch plan needs (query "
+                 "e2ep_conv_dgrad_workspace after setting precision / tunables)", workspace_bytes, need);
+  }
   E2EP_REQUIRE(w_layout == 0 || w_layout == 1, E2EP_EINVAL, "e2ep_conv_dgrad: w_layout must be 0 or 1");
   g.wlayout = w_layout;
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_dgrad: bad geometry");
@@ -1820,8 +1833,9 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
 }
 
 int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
-                    int w_layout, float *dx, void *workspace, void *stream) {
-  return e2ep_conv_dgrad_acc(gout, w, dims, m_channels, w_layout, nullptr, dx, workspace, stream);
+                    int w_layout, float *dx, void *workspace, size_t workspace_bytes, void *stream) {
+  return e2ep_conv_dgrad_acc(gout, w, dims, m_channels, w_layout, nullptr, dx, workspace,
+                             workspace_bytes, stream);
 }
 
 int e2ep_conv_wgrad_splits(const int *dims) {
@@ -1848,9 +1862,14 @@ size_t e2ep_conv_wgrad_workspace(const int *dims, int splits) {
 }
 
 int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,
-                    void *workspace, float *dw, int accumulate, void *stream) {
+                    void *workspace, size_t workspace_bytes, float *dw, int accumulate,
+                    void *stream) {
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g) && splits > 0, E2EP_EINVAL, "e2ep_conv_wgrad: bad geometry");
+  // the kernels write at most `splits` slabs of Cout * Cin * R * S floats
+  E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_conv_wgrad_workspace(dims, splits),
+               E2EP_EINVAL, "e2ep_conv_wgrad: workspace %zu bytes < %zu for %d splits",
+               workspace_bytes, e2ep_conv_wgrad_workspace(dims, splits), splits);
   if (lp_wgrad_selected()) {
     const TapList tl = live_taps(g);
     if (lp_wgrad_ok(g, tl)) {

@@ -164,9 +164,13 @@ __global__ void __launch_bounds__(256) k_dw_wgrad(const float *__restrict__ gy,
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][t] = v;
   }
   __syncthreads();
-  __shared__ int s_last;
   const int t = threadIdx.x < K * K ? threadIdx.x : 0;
-  dw_wgrad_out<K * K>(part, c, sp, splits, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]), &s_last);
+  // the last-arriver flag reuses red[0][0] (read above, before dw_wgrad_out's first barrier):
+  // a static __shared__ int would leave the kernel's static LDS at 4 mod 16 bytes and shift the
+  // strip kernels' dynamic LDS base off 16-B alignment (their b128 window reads then replay:
+  // 1.5 - 2x slower; cdna_hip_programming.md Guideline 17)
+  dw_wgrad_out<K * K>(part, c, sp, splits, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]),
+                      reinterpret_cast<int *>(&red[0][0]));
 }
 
 __global__ void k_dw_wgrad_finalize(const float *__restrict__ part, int C, int KK, int splits,
@@ -535,9 +539,13 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
     if (lane == 0) red[wave][t] = v;
   }
   __syncthreads();
-  __shared__ int s_last;
   const int t = threadIdx.x < K * K ? threadIdx.x : 0;
-  dw_wgrad_out<K * K>(part, c, sp, splits, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]), &s_last);
+  // the last-arriver flag reuses red[0][0] (read above, before dw_wgrad_out's first barrier):
+  // a static __shared__ int would leave the kernel's static LDS at 4 mod 16 bytes and shift the
+  // strip kernels' dynamic LDS base off 16-B alignment (their b128 window reads then replay:
+  // 1.5 - 2x slower; cdna_hip_programming.md Guideline 17)
+  dw_wgrad_out<K * K>(part, c, sp, splits, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]),
+                      reinterpret_cast<int *>(&red[0][0]));
 }
 
 static int dw_splits(long long pixels, int C) {
@@ -749,8 +757,12 @@ size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
 }
 
 int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
-                      const float *in_shift, int in_act, void *workspace, float *dw, void *stream) {
+                      const float *in_shift, int in_act, void *workspace, size_t workspace_bytes,
+                      float *dw, void *stream) {
   DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_dwconv_wgrad_workspace(dims), E2EP_EINVAL,
+               "e2ep_dwconv_wgrad: workspace %zu bytes < %zu (e2ep_dwconv_wgrad_workspace)",
+               workspace_bytes, e2ep_dwconv_wgrad_workspace(dims));
   E2EP_REQUIRE(!in_scale == !in_shift && in_act >= 0 && in_act <= 2, E2EP_EINVAL,
                "e2ep_dwconv_wgrad: in_scale / in_shift both or neither, in_act 0..2");
   const DwIn tf{in_scale, in_shift, in_act};

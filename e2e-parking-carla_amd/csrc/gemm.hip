@@ -661,9 +661,13 @@ size_t e2ep_gemm_rowsum_workspace(int M, int N, int K) { return gemm_ws(M, N + 1
 
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
-              int K, int relu, void *workspace, void *stream) {
+              int K, int relu, void *workspace, size_t workspace_bytes, void *stream) {
   E2EP_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0, E2EP_EINVAL,
                "e2ep_gemm: bad arguments M=%d N=%d K=%d", M, N, K);
+  E2EP_REQUIRE(!gemm_ws(M, N, K) || (workspace && workspace_bytes >= gemm_ws(M, N, K)),
+               E2EP_EINVAL, "e2ep_gemm: workspace %zu bytes < %zu the launch plan needs (query "
+               "e2ep_gemm_workspace after setting precision / tunables)", workspace_bytes,
+               gemm_ws(M, N, K));
   E2EP_REQUIRE(lda >= (a_kcontig ? K : M) && ldb >= (b_kcontig ? K : N) && ldc >= N &&
                    (!Cadd || ldadd >= N),
                E2EP_EINVAL, "e2ep_gemm: leading dimension too small");
@@ -681,9 +685,13 @@ int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, i
 }
 
 int e2ep_gemm_rowsum(const float *A, int lda, const float *B, int ldb, float *C, int ldc,
-                     float *rowsum, int M, int N, int K, void *workspace, void *stream) {
+                     float *rowsum, int M, int N, int K, void *workspace,
+                     size_t workspace_bytes, void *stream) {
   E2EP_REQUIRE(A && B && C && rowsum && M > 0 && N > 0 && K > 0, E2EP_EINVAL,
                "e2ep_gemm_rowsum: bad arguments M=%d N=%d K=%d", M, N, K);
+  E2EP_REQUIRE(!gemm_ws(M, N + 1, K) || (workspace && workspace_bytes >= gemm_ws(M, N + 1, K)),
+               E2EP_EINVAL, "e2ep_gemm_rowsum: workspace %zu bytes < %zu the launch plan needs",
+               workspace_bytes, gemm_ws(M, N + 1, K));
   E2EP_REQUIRE(lda >= M && ldb >= N && ldc >= N, E2EP_EINVAL,
                "e2ep_gemm_rowsum: leading dimension too small");
   const long long a_bytes = 4LL * ((long long)(K - 1) * lda + M);

@@ -301,8 +301,13 @@ __global__ void __launch_bounds__(256) k_se_dx(const float *__restrict__ dy,
 }
 
 // ------------------------------------------------------------------------------------------
-// Fused forms (e2ep_tune key 27 = 2, the default): the MLP on the 1x1 map runs inside the
-// streaming kernels instead of as launches of its own.
+// Fused forms (e2ep_tune key 27 = 2; OFF by default): the MLP on the 1x1 map runs inside the
+// streaming kernels instead of as launches of its own.  Measured in the replayed C2 step
+// (profiles/r04/se_fold_ab.txt): 25.7 vs 23.9 ms/step — k_se_squeeze_mlp 56 us against 13 + 5
+// for squeeze + hidden, k_se_da_mlp 66 us against 20 + 8 + 6 — because every one of the
+// thousands of small streaming workgroups (4 planes, 4 KB at 16x16) now ends in a
+// write-through store drain and a returning device-scope atomic (several us each under
+// load, paid once per residency round), which costs more than the launches it saves.
 //  * k_se_squeeze_mlp: the squeeze; a sample's C/4 workgroups store their plane means
 //    write-through and take an arrival ticket (handoff.h); the sample's last workgroup reads
 //    the C means back (sc1) and computes hpre[n][k] = W1[k] . pooled[n] + b1[k] for every k.

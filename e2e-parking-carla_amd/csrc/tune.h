@@ -30,7 +30,7 @@ enum Tune {
   TUNE_DW_FWD_BLOCKS = 24,    // depthwise forward / stride-1 data-gradient strip kernel: grid cap (blocks)
   TUNE_BNS_WIDE = 25,         // single-launch BN, channels of 1025..2048 float4: 2 = 512 threads x 4, 1 = 256 x 8
   TUNE_BNS_WIDE_LO = 26,      // the same for channels of 257..1024 float4: 2 = 512 threads x 1 / 2, 1 = 256 x 2 / 4
-  TUNE_SE_FUSED = 27,         // squeeze-excitation MLP inside the squeeze / excite / da launches: 2 = on, 1 = separate kernels
+  TUNE_SE_FUSED = 27,         // squeeze-excitation MLP inside the squeeze / excite / da launches: 2 = on, 1 = separate kernels (default: measured 1.8 ms/step slower fused)
   TUNE_SPLITK_FOLD = 28,      // split-K reductions folded into the producing launch (last-arriving split sums): 2 = on, 1 = separate reduce kernels
   TUNE_N = 29
 };

@@ -32,10 +32,10 @@ SIGNATURES = {
     "e2ep_transpose_multi": (_i, [_p, _i, _i, _p]),
     "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
     "e2ep_conv_fwd_workspace": (_sz, [_p]),
-    "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _p]),
+    "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _sz, _p]),
     "e2ep_conv_dgrad_workspace": (_sz, [_p, _i]),
-    "e2ep_conv_dgrad": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),
-    "e2ep_conv_dgrad_acc": (_i, [_p, _p, _p, _i, _i, _p, _p, _p, _p]),
+    "e2ep_conv_dgrad": (_i, [_p, _p, _p, _i, _i, _p, _p, _sz, _p]),
+    "e2ep_conv_dgrad_acc": (_i, [_p, _p, _p, _i, _i, _p, _p, _p, _sz, _p]),
     "e2ep_conv_gemm_variant": (_i, [_i]),
     "e2ep_conv_split_params": (_i, [_i, _i, _i]),
     "e2ep_conv_precision": (_i, [_i]),
@@ -47,15 +47,15 @@ SIGNATURES = {
     "e2ep_conv_wgrad_kstep": (_i, [_i]),
     "e2ep_conv_wgrad_splits": (_i, [_p]),
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),
-    "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _p, _i, _p]),
+    "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _sz, _p, _i, _p]),
     "e2ep_bias_grad": (_i, [_p, _i, _i, _i, _p, _p]),
     "e2ep_col_sum_workspace": (_sz, [_i, _i]),
     "e2ep_col_sum": (_i, [_p, _i, _i, _p, _p, _p]),
     "e2ep_skinny_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _i, _i, _i, _p, _p]),
     "e2ep_bn_workspace": (_sz, [_i, _i, _i, _i]),
-    "e2ep_bn_fwd": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i, _p, _p, _p, _p, _p]),
-    "e2ep_bn_stats": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _p]),
-    "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
+    "e2ep_bn_fwd": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i, _p, _p, _p, _p, _sz, _p]),
+    "e2ep_bn_stats": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
+    "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _sz, _p]),
     "e2ep_act_fwd": (_i, [_p, _i64, _i, _p, _p]),
     "e2ep_act_bwd": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_cat_channels": (_i, [_p, _p, _i, _i, _i64, _p, _p]),
@@ -72,7 +72,7 @@ SIGNATURES = {
     "e2ep_dwconv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p]),
     "e2ep_dwconv_dgrad": (_i, [_p, _p, _p, _p, _p]),
     "e2ep_dwconv_wgrad_workspace": (_sz, [_p]),
-    "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _p]),
+    "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _i, _p, _sz, _p, _p]),
     "e2ep_maxpool3s2_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p]),
     "e2ep_maxpool3s2_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_avgpool_fwd": (_i, [_p, _i, _i, _p, _p]),
@@ -115,9 +115,9 @@ SIGNATURES = {
     "e2ep_bn_small": (_i, [_i]),
     "e2ep_bn_small_limits": (_i, [_i, _i]),
     "e2ep_tune": (_i, [_i, _i]),
-    "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _p]),
+    "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "e2ep_gemm_rowsum_workspace": (_sz, [_i, _i, _i]),
-    "e2ep_gemm_rowsum": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _p, _p]),
+    "e2ep_gemm_rowsum": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _p, _sz, _p]),
     "e2ep_decode_frames": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p]),
     "e2ep_widen_u8_i64": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_depth_bce_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p]),
@@ -182,6 +182,11 @@ def call_raw(name, *args):
 def ptr(t):
     """Device pointer of a tensor (None -> NULL)."""
     return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def nbytes(t):
+    """Size in bytes of a workspace tensor (None -> 0), passed with it as workspace_bytes."""
+    return 0 if t is None else t.numel() * t.element_size()
 
 
 def stream():

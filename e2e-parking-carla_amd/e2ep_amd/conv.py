@@ -125,7 +125,7 @@ def conv_fwd(x, w, b, dims, act, y, w_layout=0):
     ws = _ws(_lib.load().e2ep_conv_fwd_workspace(d), x.device)
     with timing.region(_rname("conv_fwd", dims), conv_flops(dims)):
         _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
-                  _lib.ptr(y), _lib.ptr(ws), _lib.stream())
+                  _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
     return y
 
 
@@ -135,7 +135,7 @@ def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0, res=None):
     ws = _ws(_lib.load().e2ep_conv_dgrad_workspace(d, m_channels), gy.device)
     with timing.region(_rname("conv_dgrad", dims, f"gc{m_channels}"), conv_flops(dims, m_channels)):
         _lib.call("e2ep_conv_dgrad_acc", _lib.ptr(gy), _lib.ptr(w), d, m_channels, w_layout,
-                  _lib.ptr(res), _lib.ptr(dx), _lib.ptr(ws), _lib.stream())
+                  _lib.ptr(res), _lib.ptr(dx), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
     return dx
 
 
@@ -145,7 +145,7 @@ def conv_wgrad(gy, x, dims, dw, ws=None):
     if ws is None:
         ws = torch.empty(splits * dw.numel(), dtype=torch.float32, device=gy.device)
     with timing.region(_rname("conv_wgrad", dims), conv_flops(dims)):
-        _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws),
+        _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws), _lib.nbytes(ws),
                   _lib.ptr(dw), 0, _lib.stream())
     return dw
 

@@ -39,7 +39,7 @@ class _BnAct(torch.autograd.Function):
             _lib.call("e2ep_bn_fwd", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res),
                       _lib.ptr(dc_rand), float(dc_keep), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W,
                       int(train), float(momentum), float(eps), act, _lib.ptr(mean),
-                      _lib.ptr(invstd), _lib.ptr(y), _lib.ptr(ws), _lib.stream())
+                      _lib.ptr(invstd), _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
         ctx.save_for_backward(x, gamma, beta, res, mean, invstd, dc_rand)
         ctx.train, ctx.act, ctx.dc_keep = train, act, dc_keep
         return y
@@ -62,7 +62,7 @@ class _BnAct(torch.autograd.Function):
             _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(mean), _lib.ptr(invstd),
                       _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), _lib.ptr(dc_rand),
                       float(ctx.dc_keep), None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx),
-                      _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.stream())
+                      _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
         if dres_is_dy:
             dres = dy
         return dx, dg, db, dres, None, None, None, None, None, None, None, None
@@ -247,7 +247,7 @@ class _DwConv(torch.autograd.Function):
             fork = conv._Fork(x.device, on=ctx.needs_input_grad[0])
             with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_DwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
-                          _lib.ptr(ws), _lib.ptr(dw), _lib.stream())
+                          _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), _lib.stream())
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             with timing.region(timing.name("dwconv_dgrad", gy.shape, "_DwConv")):
@@ -277,7 +277,7 @@ class _BnActDwConv(torch.autograd.Function):
             _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
                       _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
                       _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
-                      _lib.ptr(stats[3]), _lib.ptr(ws), s)
+                      _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
         y = torch.empty(N, C, P, Q, **f32)
         d = _lib.dims(dims)
         with timing.region(timing.name("dwconv_fwd", x.shape, "_BnActDwConv")):
@@ -303,7 +303,7 @@ class _BnActDwConv(torch.autograd.Function):
             fork = conv._Fork(x.device, on=nig[0] or nig[1] or nig[2])
             with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(stats[2]),
-                          _lib.ptr(stats[3]), ctx.act, _lib.ptr(wsw), _lib.ptr(dw), _lib.stream())
+                          _lib.ptr(stats[3]), ctx.act, _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream())
         if nig[0] or nig[1] or nig[2]:
             dt = torch.empty_like(x)  # gradient at the activation output
             with timing.region(timing.name("dwconv_dgrad", gy.shape, "_BnActDwConv")):
@@ -316,7 +316,7 @@ class _BnActDwConv(torch.autograd.Function):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dt), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx), _lib.ptr(dg),
-                          _lib.ptr(db), None, _lib.ptr(ws), s)
+                          _lib.ptr(db), None, _lib.ptr(ws), _lib.nbytes(ws), s)
         if fork is not None:
             fork.join()
         return dx, dg, db, None, None, None, None, None, None, dw, None
@@ -501,7 +501,7 @@ class _BnSwishSE(torch.autograd.Function):
             _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
                       _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
                       _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
-                      _lib.ptr(stats[3]), _lib.ptr(ws), s)
+                      _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
         pooled, hpre, a = torch.empty(N, C, **f32), torch.empty(N, sq, **f32), torch.empty(N, C, **f32)
         y = torch.empty_like(x)
         w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
@@ -545,7 +545,7 @@ class _BnSwishSE(torch.autograd.Function):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           _lib.ptr(a), _lib.ptr(dpooled), N, C, H, W, int(ctx.train), ACT["swish"],
-                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), None, _lib.ptr(bws), s)
+                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), None, _lib.ptr(bws), _lib.nbytes(bws), s)
         return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2
 
 
@@ -763,7 +763,7 @@ def gemm(A, a_kcontig, B, b_kcontig, M, N, K, bias=None, cadd=None, out=None, re
         _lib.call("e2ep_gemm", _lib.ptr(A), A.stride(0), int(a_kcontig), _lib.ptr(B), B.stride(0),
                   int(b_kcontig), _lib.ptr(bias), _lib.ptr(cadd),
                   cadd.stride(0) if cadd is not None else 0, _lib.ptr(out), out.stride(0), M, N, K,
-                  int(relu), _lib.ptr(ws), _lib.stream())
+                  int(relu), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
     return out
 
 
@@ -832,7 +832,7 @@ def _linear_bwd(g2, x2, weight, want_x, want_w, want_b, gskip=None, dw=None, db=
                 with timing.region(timing.name("gemm", (N, K, M), "linear_wgrad"), 2.0 * N * K * M):
                     _lib.call("e2ep_gemm_rowsum", _lib.ptr(g2), g2.stride(0), _lib.ptr(x2),
                               x2.stride(0), _lib.ptr(dw), dw.stride(0), _lib.ptr(db), N, K, M,
-                              _lib.ptr(wsw), _lib.stream())
+                              _lib.ptr(wsw), _lib.nbytes(wsw), _lib.stream())
             elif want_w:
                 gemm(g2, False, x2, False, N, K, M, out=dw, ws=wsw, tag="linear_wgrad")
             else:

@@ -57,7 +57,8 @@ int e2ep_geom_index(const float *frustum, const float *combine, const float *tra
 /* Bytes of int32 workspace e2ep_lss_plan needs: B*X*Y*Z*4. */
 size_t e2ep_lss_plan_workspace(int B, int XYZ);
 
-/* Pillars per output tile of e2ep_lss_fwd, and tiles per sample (= ceil(XYZ / E2EP_LSS_TILE)). */
+/* Pillars per output tile of e2ep_lss_fwd, and the tile-schedule entries to allocate per
+ * sample: ceil(XYZ / E2EP_LSS_TILE) tiles + 8 entries of lane padding. */
 #define E2EP_LSS_TILE 64
 int e2ep_lss_tiles(int XYZ);
 
@@ -68,9 +69,13 @@ int e2ep_lss_tiles(int XYZ);
  *                        offsets[b*(XYZ+1)+q+1])
  *   order   [B*P] packed point codes (n<<24 | d<<16 | h*w index), ascending within a pillar,
  *           so every later sum has a fixed, run-to-run identical order.
- *   tiles   [B*e2ep_lss_tiles(XYZ)] or NULL: per sample, the forward's output tiles ordered by
- *           point count, heaviest first (a launch schedule; any permutation is correct).
- * Limits: N < 128, D < 256, h*w < 65536; with tiles, e2ep_lss_tiles(XYZ) <= 4096. */
+ *   tiles   [B*e2ep_lss_tiles(XYZ)] or NULL: the forward's launch schedule (any order of the
+ *           tiles is correct): B = 8 (or any B not dividing 8): per sample its tiles, heaviest
+ *           first, block -> (sample id % B, rank id / B); B = 1, 2, 4: lane schedule — each
+ *           sample's tiles cut into G = 8/B contiguous pillar ranges, range g of sample s =
+ *           lane g*B + s = tiles[lane * L .. +L) (L = ceil(tiles / G)), heaviest first, -1
+ *           padded, block -> (lane id % 8, entry id / 8): a lane's blocks share an XCD and its L2.
+ * Limits: N < 128, D < 256, h*w < 65536; with tiles, ceil(XYZ / E2EP_LSS_TILE) <= 4096. */
 int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int XYZ,
                   int32_t *offsets, int32_t *order, int32_t *tiles, void *workspace,
                   void *stream);
@@ -147,20 +152,21 @@ int e2ep_target_bev(const float *target_point, const float *noise, int B, int X,
  * e2ep_conv_fwd_workspace bytes (0 = none needed; pass NULL) and are reduced in fixed order. */
 size_t e2ep_conv_fwd_workspace(const int *dims);
 int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
-                  int w_layout, float *y, void *workspace, void *stream);
+                  int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream);
 
 /* dx[N,m_channels,H,W] = conv_transpose(gout[N,Cout,P,Q], w) restricted to the first
  * m_channels input channels; split by input-pixel stride phase, so no zero taps at stride 2.
  * w_layout as for e2ep_conv_fwd. */
 size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels);
 int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
-                    int w_layout, float *dx, void *workspace, void *stream);
+                    int w_layout, float *dx, void *workspace, size_t workspace_bytes, void *stream);
 /* e2ep_conv_dgrad plus a residual gradient res (dx's layout, may be NULL) added in the
  * epilogue: dx = conv_transpose(gout, w) + res.  The skip connection around a block whose
  * first conv reads the block input (MBConv expand conv, ResNet BasicBlock conv1) gets its
  * input gradient in one pass instead of dgrad + an autograd accumulation add. */
 int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int m_channels,
-                        int w_layout, const float *res, float *dx, void *workspace, void *stream);
+                        int w_layout, const float *res, float *dx, void *workspace,
+                        size_t workspace_bytes, void *stream);
 
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of
@@ -193,7 +199,8 @@ int e2ep_conv_wgrad_kstep(int pixels);
 int e2ep_conv_wgrad_splits(const int *dims);
 size_t e2ep_conv_wgrad_workspace(const int *dims, int splits);
 int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,
-                    void *workspace, float *dw, int accumulate, void *stream);
+                    void *workspace, size_t workspace_bytes, float *dw, int accumulate,
+                    void *stream);
 
 /* db[C] = sum over (n, p) of gout[N, C, HW]. */
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream);
@@ -226,7 +233,8 @@ size_t e2ep_bn_workspace(int N, int C, int H, int W);
 int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const float *res,
                 const float *dc_rand, float dc_keep, float *running_mean, float *running_var,
                 int N, int C, int H, int W, int train, float momentum, float eps, int act,
-                float *mean, float *invstd, float *y, void *workspace, void *stream);
+                float *mean, float *invstd, float *y, void *workspace, size_t workspace_bytes,
+                void *stream);
 /* Statistics half of e2ep_bn_fwd (same fp64 reduction, same running-stat update) for a
  * consumer that applies the normalisation on load (e2ep_dwconv_fwd / _wgrad in_scale,
  * in_shift): writes mean / invstd [C] and the folded affine scale = gamma * invstd,
@@ -234,7 +242,7 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
 int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *running_mean,
                   float *running_var, int N, int C, int H, int W, int train, float momentum,
                   float eps, float *mean, float *invstd, float *scale, float *shift,
-                  void *workspace, void *stream);
+                  void *workspace, size_t workspace_bytes, void *stream);
 /* dx, dgamma, dbeta, dres (each nullable) from x, dy and the forward's mean/invstd; res and
  * dc_rand / dc_keep as in the forward (dres = gradient at the activation input).
  * gate_logit / gate_dpooled [N,C] (both or neither): the activation output fed a
@@ -244,7 +252,7 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
                 const float *gamma, const float *beta, const float *res, const float *dc_rand,
                 float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
                 int H, int W, int train, int act, float *dx, float *dgamma, float *dbeta,
-                float *dres, void *workspace, void *stream);
+                float *dres, void *workspace, size_t workspace_bytes, void *stream);
 /* Stand-alone activation (act as above) and its gradient w.r.t. the pre-activation x. */
 int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);
@@ -417,7 +425,8 @@ int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float
 int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream);
 size_t e2ep_dwconv_wgrad_workspace(const int *dims);
 int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
-                      const float *in_shift, int in_act, void *workspace, float *dw, void *stream);
+                      const float *in_shift, int in_act, void *workspace, size_t workspace_bytes,
+                      float *dw, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Pooling and squeeze-excitation gating.
@@ -599,12 +608,14 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * plan from these process-wide settings, and the *_workspace() queries size the workspace
  * from the same plan, so set them before a caller queries workspace sizes (in practice:
  * before the first step is run or captured) and never change them between a caller's
- * workspace query and its launch; a larger split count than the workspace was sized for
- * would write past it. */
+ * workspace query and its launch.  Every entry point that takes a workspace also takes its
+ * size in bytes (workspace_bytes) and returns E2EP_EINVAL, launching nothing, when the plan it
+ * would run needs more (round 4: a plan changed after the query can no longer write past the
+ * buffer). */
 int e2ep_tune(int key, int value);
 int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, int b_kcontig,
               const float *bias, const float *Cadd, int ldadd, float *C, int ldc, int M, int N,
-              int K, int relu, void *workspace, void *stream);
+              int K, int relu, void *workspace, size_t workspace_bytes, void *stream);
 /* Weight gradient of a linear layer together with its bias gradient (replaces the
  * nn.Linear backward's grad_weight = dY^T X and grad_bias = dY.sum(0), model/feature_fusion.py
  * :13-14,24-29, model/control_predict.py:18-24): C = A(m,k) B(k,n) with A(m,k) = A[k*lda + m]
@@ -613,7 +624,8 @@ int e2ep_gemm(const float *A, int lda, int a_kcontig, const float *B, int ldb, i
  * Workspace: e2ep_gemm_rowsum_workspace(M, N, K) bytes (0 when no K split). */
 size_t e2ep_gemm_rowsum_workspace(int M, int N, int K);
 int e2ep_gemm_rowsum(const float *A, int lda, const float *B, int ldb, float *C, int ldc,
-                     float *rowsum, int M, int N, int K, void *workspace, void *stream);
+                     float *rowsum, int M, int N, int K, void *workspace,
+                     size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Frame decode (dataset/carla_dataset.py:114-131, :494-515, :404-406): the per-step

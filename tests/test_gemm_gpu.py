@@ -140,7 +140,7 @@ def _rowsum_gemm(g2, x2):
     nb = _lib.load().e2ep_gemm_rowsum_workspace(N, K, rows)
     ws = torch.empty(max(1, nb // 4), dtype=torch.float32, device=DEV)
     _lib.call("e2ep_gemm_rowsum", _lib.ptr(g2), g2.stride(0), _lib.ptr(x2), x2.stride(0),
-              _lib.ptr(dw), K, _lib.ptr(db), N, K, rows, _lib.ptr(ws), _lib.stream())
+              _lib.ptr(dw), K, _lib.ptr(db), N, K, rows, _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
     return dw, db
 
 
@@ -218,3 +218,35 @@ def test_gemm_bf16_operands_vs_rounded_fp64(M, N, K, ak, bk):
     if K >= 64:
         assert rel_l2(out, ref) > 1e-4
     assert rel_l2(nn_ops.gemm(A.to(DEV), ak, B.to(DEV), bk, M, N, K), ref) < 2e-6  # fp32 again
+
+
+def test_short_workspace_is_rejected():
+    """Every workspace-taking entry point gets the workspace size and refuses (E2EP_EINVAL,
+    nothing launched) a buffer smaller than its launch plan needs: a K-split
+    GEMM and a conv weight gradient with their workspaces one float short."""
+    from e2ep_amd import _lib
+    M, N, K = 197, 301, 777
+    A = torch.randn(M, K, device=DEV)
+    B = torch.randn(N, K, device=DEV)
+    C = torch.empty(M, N, device=DEV)
+    try:
+        _lib.call("e2ep_gemm_force", 1, 3, 0)
+        need = _lib.load().e2ep_gemm_workspace(M, N, K)
+        assert need > 0
+        ws = torch.empty(need // 4, device=DEV)
+        args = lambda w, nb: (_lib.ptr(A), K, 1, _lib.ptr(B), K, 1, None, None, 0, _lib.ptr(C), N,  # noqa: E731
+                              M, N, K, 0, _lib.ptr(w), nb, _lib.stream())
+        _lib.call("e2ep_gemm", *args(ws, _lib.nbytes(ws)))
+        with pytest.raises(_lib.E2EPError, match="workspace"):
+            _lib.call("e2ep_gemm", *args(ws, _lib.nbytes(ws) - 4))
+    finally:
+        _lib.call("e2ep_gemm_force", 0, 0, 0)
+    d = _lib.dims((2, 64, 16, 16, 64, 3, 3, 16, 16, 1, 1, 1, 1, 1, 1))
+    splits = _lib.load().e2ep_conv_wgrad_splits(d)
+    nb = _lib.load().e2ep_conv_wgrad_workspace(d, splits)
+    gy, x = torch.randn(2, 64, 16, 16, device=DEV), torch.randn(2, 64, 16, 16, device=DEV)
+    dw, ws = torch.empty(64, 64, 3, 3, device=DEV), torch.empty(nb // 4, device=DEV)
+    with pytest.raises(_lib.E2EPError, match="workspace"):
+        _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws), nb - 4,
+                  _lib.ptr(dw), 0, _lib.stream())
+    torch.cuda.synchronize()

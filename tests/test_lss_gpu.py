@@ -147,25 +147,41 @@ def test_plan_invariants_batch_of_different_rigs():
             seg = codes[off[b][q]:off[b][q + 1]]
             assert np.all(np.diff(seg) > 0)
     assert not np.array_equal(pil[0], pil[1])
-    # forward tile schedule: a permutation per sample, heaviest tile first (ties by index)
-    T = 64
-    tiles = plan.tiles.view(2, -1).cpu().numpy()
-    for b in range(2):
-        nt = tiles.shape[1]
-        assert np.array_equal(np.sort(tiles[b]), np.arange(nt))
+    # forward tile schedule at B = 2 (lane schedule, include/e2ep.h): 8 lanes; lane l holds
+    # pillar range g = l // 2 of sample l % 2 (G = 4 contiguous ranges per sample), heaviest
+    # tile first (ties by index), -1 padded; each sample's tiles appear exactly once
+    T, B, G = 64, 2, 4
+    nt = -(-40000 // T)
+    L = -(-nt // G)
+    lanes = plan.tiles.cpu().numpy()[:8 * L].reshape(8, L)
+    for b in range(B):
         edges = np.minimum(np.arange(nt + 1) * T, 40000)
         cnt = off[b][edges[1:]] - off[b][edges[:-1]]
-        assert np.array_equal(tiles[b], np.lexsort((np.arange(nt), -cnt)))
+        seen = []
+        for g in range(G):
+            lo, hi = -(-g * nt // G), -(-(g + 1) * nt // G)
+            lane = lanes[g * B + b]
+            want = lo + np.lexsort((np.arange(hi - lo), -cnt[lo:hi]))
+            assert np.array_equal(lane[:hi - lo], want)
+            assert np.all(lane[hi - lo:] == -1)
+            seen.extend(lane[:hi - lo])
+        assert np.array_equal(np.sort(seen), np.arange(nt))
 
 
 def test_lss_fwd_schedule_does_not_change_result():
     """Any tile order gives the bitwise-same BEV (each pillar's sum order is fixed); the
-    natural order (tiles=NULL) vs the heaviest-first schedule, C=64 and the C%4!=0 path."""
-    from e2ep_amd import _lib, lss
+    natural order (tiles=NULL) vs the scheduled order (heaviest-first per sample at B = 3 / 8,
+    the XCD lane schedule at B = 1 / 2 / 4), C=64 and the C%4!=0 path; every cell written."""
     g = golden("geometry_4cam_256.npz")
-    B, N, D, hw = 2, 4, 48, 1024
+    for B in (1, 2, 3, 4, 8):  # lane schedules (1, 2, 4), per-sample order (3, 8)
+        _schedule_case(B, g)
+
+
+def _schedule_case(B, g):
+    from e2ep_amd import _lib
+    N, D, hw = 4, 48, 1024
     plan = _plan_from_golden(g, B)
-    gl = torch.Generator().manual_seed(5)
+    gl = torch.Generator().manual_seed(5 + B)
     prob = torch.rand(B * N, D, hw, generator=gl).to(DEV)
     for C in (64, 12, 6):
         featT = torch.randn(B * N, hw, C, generator=gl).to(DEV)

@@ -131,7 +131,7 @@ def test_gemm_split_fold_bitwise_equals_two_launch(tile, splits):
         ws = torch.empty(max(1, nb // 4), device=DEV)
         bt = B.t().contiguous()
         _lib.call("e2ep_gemm_rowsum", _lib.ptr(rows), rows.stride(0), _lib.ptr(bt), bt.stride(0),
-                  _lib.ptr(dw), N, _lib.ptr(db), M, N, K, _lib.ptr(ws), _lib.stream())
+                  _lib.ptr(dw), N, _lib.ptr(db), M, N, K, _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
         return a, c, dw, db
 
     try:
