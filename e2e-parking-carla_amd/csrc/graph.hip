@@ -91,4 +91,27 @@ int e2ep_graph_replace_memsets(void *graph, int *replaced) {
   return 0;
 }
 
+// Own executable of a captured graph, launched without PyTorch's CUDAGraph.replay(): that
+// replay's prologue refreshes the philox seed / offset tensors of torch's generators with
+// int64 fill kernels (at::native FillFunctor<long>) before the launch; the train step draws
+// its random numbers from e2ep_rng_draw, so those launches are pure overhead in the step.
+int e2ep_graph_exec_create(void *graph, void **exec) {
+  E2EP_REQUIRE(graph && exec, E2EP_EINVAL, "e2ep_graph_exec_create: null argument");
+  hipGraphExec_t e = nullptr;
+  E2EP_HIPCHECK(hipGraphInstantiate(&e, static_cast<hipGraph_t>(graph), nullptr, nullptr, 0));
+  *exec = e;
+  return 0;
+}
+
+int e2ep_graph_exec_launch(void *exec, void *stream) {
+  E2EP_REQUIRE(exec, E2EP_EINVAL, "e2ep_graph_exec_launch: null exec");
+  E2EP_HIPCHECK(hipGraphLaunch(static_cast<hipGraphExec_t>(exec), as_stream(stream)));
+  return 0;
+}
+
+int e2ep_graph_exec_destroy(void *exec) {
+  if (exec) E2EP_HIPCHECK(hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec)));
+  return 0;
+}
+
 }  // extern "C"

@@ -99,6 +99,9 @@ SIGNATURES = {
     "e2ep_adam_step": (_i, [_p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _d, _d, _d, _d, _f, _p, _p]),
     "e2ep_grad_gather": (_i, [_p, _i, _p, _p, _p, _p]),
     "e2ep_graph_replace_memsets": (_i, [_p, ctypes.POINTER(_i)]),
+    "e2ep_graph_exec_create": (_i, [_p, _p]),
+    "e2ep_graph_exec_launch": (_i, [_p, _p]),
+    "e2ep_graph_exec_destroy": (_i, [_p]),
     "e2ep_control_ce_workspace": (_sz, [_i]),
     "e2ep_control_ce_fwd": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "e2ep_control_ce_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),

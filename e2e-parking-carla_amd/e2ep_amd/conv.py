@@ -174,10 +174,13 @@ def wgrad_overlap():
 
 
 def side_stream(device):
+    """The weight-gradient side stream of the current stream (one per stream, so branches
+    already on side streams — e2ep_amd.streams — fork onto streams of their own)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _SIDE.get(idx)
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
+    st = _SIDE.get(key)
     if st is None:
-        st = _SIDE[idx] = torch.cuda.Stream(device=idx)
+        st = _SIDE[key] = torch.cuda.Stream(device=idx)
     return st
 
 

@@ -24,13 +24,39 @@ def capture_mode():
     return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
 
 
+class Graph:
+    """A captured, repaired graph with its own executable (e2ep_graph_exec_*): replay()
+    launches it on the current stream without torch.cuda.CUDAGraph.replay()'s prologue, which
+    refreshes torch's generator states with int64 fill kernels before every launch (the step
+    draws its random numbers from e2ep_rng_draw, not from torch's generators).  The torch
+    graph object stays alive: it owns the graph and its memory pool."""
+
+    def __init__(self, g):
+        self.g = g
+        ex = ctypes.c_void_p()
+        _lib.call("e2ep_graph_exec_create", ctypes.c_void_p(g.raw_cuda_graph()), ctypes.byref(ex))
+        self._exec = ex
+
+    def replay(self):
+        _lib.call("e2ep_graph_exec_launch", self._exec, _lib.stream())
+
+    def pool(self):
+        return self.g.pool()
+
+    def __del__(self):
+        try:
+            if self._exec:
+                _lib.call("e2ep_graph_exec_destroy", self._exec)
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
 def capture(fn, pool=None):
-    """Capture fn() into a repaired, instantiated graph.  Returns (graph, fn's result,
-    number of memset nodes rewritten)."""
+    """Capture fn() into a repaired graph with its own executable.  Returns (Graph, fn's
+    result, number of memset nodes rewritten)."""
     g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_mode()):
         out = fn()
     n = ctypes.c_int(0)
     _lib.call("e2ep_graph_replace_memsets", ctypes.c_void_p(g.raw_cuda_graph()), ctypes.byref(n))
-    g.instantiate()
-    return g, out, n.value
+    return Graph(g), out, n.value

@@ -1,0 +1,87 @@
+"""Independent model branches on side streams (MI355X: many of the step's launches fill a
+fraction of the 256 CUs — 16x16 camera maps, the transformer's token rows — so two
+independent chains of them overlap instead of running back to back).
+
+    with branch("cam", device) as br:
+        depth = depth_head(deep, skip)          # on a side stream
+    feature = feature_head(deep, skip)          # on the current stream, concurrently
+    depth = br.join(depth)                      # the current stream waits for the side stream
+
+The branch's ops are ordinary autograd ops recorded on the side stream, so their backward
+also runs there (PyTorch's stream semantics for autograd: a node's backward runs on its
+forward's stream, synchronised with the streams its incoming gradients come from, and the
+engine makes the caller wait for every stream it used before backward() returns), and a
+HIP-graph capture of the step records both chains as parallel branches.  Tensors that cross
+between the streams are handed to the caching allocator with record_stream, so their memory
+is not recycled while the other stream may still use it.
+
+Branches are named so each can be switched off for A/B timing: E2EP_BRANCH_STREAMS is a
+comma list of enabled names (default: none — a HIP-graph capture of the train step with
+either branch on segfaults inside hipStreamEndCapture on this ROCm (scripts/
+diag_branch_capture.py: toy two-stream captures replay fine, the model's branches crash), so
+they are opt-in for eager A/B timing):
+  cam    the camera encoder's depth head next to its feature head (model/cam_encoder.py)
+  heads  the segmentation head next to the control decoder (model/parking_model.py)
+"""
+import os
+
+import torch
+
+_ENABLED = set(x for x in os.environ.get("E2EP_BRANCH_STREAMS", "").split(",") if x and x != "none")
+_STREAMS = {}
+
+
+def enabled(name):
+    return name in _ENABLED
+
+
+def set_enabled(names):
+    """Replace the enabled set (returns the previous one)."""
+    global _ENABLED
+    prev = set(_ENABLED)
+    _ENABLED = set(names)
+    return prev
+
+
+def _side(device, name):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, name)
+    st = _STREAMS.get(key)
+    if st is None:
+        st = _STREAMS[key] = torch.cuda.Stream(device=idx)
+    return st
+
+
+class branch:
+    """Context manager running its body on a side stream forked from the current stream."""
+
+    def __init__(self, name, device, inputs=()):
+        self.on = enabled(name) and device.type == "cuda"
+        self.device, self.name, self.inputs = device, name, inputs
+        if self.on:
+            self.main = torch.cuda.current_stream(device)
+            self.side = _side(device, name)
+
+    def __enter__(self):
+        if self.on:
+            self.side.wait_stream(self.main)
+            for t in self.inputs:  # produced on the current stream, read on the side stream
+                if torch.is_tensor(t) and t.is_cuda:
+                    t.record_stream(self.side)
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self._ctx.__exit__(*exc)
+        return False
+
+    def join(self, *outs):
+        """The current stream waits for the side stream; returns `outs` (one or a tuple)."""
+        if self.on:
+            self.main.wait_stream(self.side)
+            for t in outs:
+                if torch.is_tensor(t) and t.is_cuda:
+                    t.record_stream(self.main)
+        return outs[0] if len(outs) == 1 else outs

@@ -6,7 +6,7 @@ import math
 
 from torch import nn
 
-from e2ep_amd import nn_ops
+from e2ep_amd import nn_ops, streams
 from model.convolutions import DeepLabHead, UpsamplingConcat
 from model.efficientnet import EfficientNetTrunk
 
@@ -41,12 +41,15 @@ class CamEncoder(nn.Module):
         depth = None
         if self.use_depth_distribution:
             # both heads read deep and skip: two handles each, gradients summed by one e2ep
-            # launch (nn_ops.fork2)
+            # launch (nn_ops.fork2); the depth head runs on a side stream next to the feature
+            # head (e2ep_amd.streams, branch "cam": two chains of 16x16 / 32x32 launches)
             deep, deep_d = nn_ops.fork2(deep)
             skip, skip_d = nn_ops.fork2(skip)
+            with streams.branch("cam", x.device, (deep_d, skip_d)) as br:
+                depth = self.depth_layer_2(self.depth_layer_1(deep_d), skip_d)
         feature = self.feature_layer_2(self.feature_layer_1(deep), skip)
         if self.use_depth_distribution:
-            depth = self.depth_layer_2(self.depth_layer_1(deep_d), skip_d)
+            depth = br.join(depth)
         return feature, depth
 
     def forward(self, x):

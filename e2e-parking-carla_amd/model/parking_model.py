@@ -10,7 +10,7 @@ reproducible runs; by default it is drawn on the device exactly like the referen
 import torch
 from torch import nn
 
-from e2ep_amd import conv, lss, nn_ops, rng, segments
+from e2ep_amd import conv, lss, nn_ops, rng, segments, streams
 from model.bev_encoder import BevEncoder
 from model.bev_model import BevModel
 from model.control_predict import ControlPredict
@@ -43,6 +43,14 @@ class ParkingModel(nn.Module):
         return out, out[:, c:].detach().clone()
 
     def encoder(self, data, noise=None):
+        """(fuse_feature, pred_segmentation, pred_depth, bev_target) — reference API."""
+        out, br = self._encoder_async(data, noise)
+        return (out[0], br.join(out[1]), out[2], out[3])
+
+    def _encoder_async(self, data, noise=None):
+        """encoder() whose segmentation head may still be running on a side stream (branch
+        "heads", e2ep_amd.streams): returns (outputs, branch); branch.join(pred_segmentation)
+        before using it.  forward() / predict() run the control decoder in between."""
         # every spatial conv weight's tap-major copy in one launch (e2ep_amd.conv.TapMajorBatch)
         if getattr(self, "_tap_batch", None) is None:
             self._tap_batch = conv.TapMajorBatch()
@@ -73,27 +81,32 @@ class ParkingModel(nn.Module):
                        self.cfg.bev_x_bound[2], self.cfg.bev_y_bound[2])
         bev_down_sample = self.bev_encoder.forward_split(bev, bev_target)
         fuse_feature = self.feature_fusion(bev_down_sample, ego_motion)
-        # fuse_feature feeds the segmentation head and the control decoder (nn_ops.fork2)
+        # fuse_feature feeds the segmentation head and the control decoder (nn_ops.fork2); the
+        # segmentation head (a few large 200x200 launches) runs on a side stream next to the
+        # control decoder (a chain of small token-row launches)
         fuse_seg, fuse_feature = nn_ops.fork2(fuse_feature)
-        pred_segmentation = self.segmentation_head(fuse_seg)
-        return fuse_feature, pred_segmentation, pred_depth, bev_target
+        br = streams.branch("heads", dev, (fuse_seg,))
+        with br:
+            pred_segmentation = self.segmentation_head(fuse_seg)
+        return (fuse_feature, pred_segmentation, pred_depth, bev_target), br
 
     def forward(self, data, noise=None):
         if self.training:  # one launch draws every dropout seed of this step (e2ep_amd.rng)
             rng.begin_step(data["image"].device)
         try:
-            fuse_feature, pred_segmentation, pred_depth, _ = self.encoder(data, noise)
+            (fuse_feature, pred_segmentation, pred_depth, _), br = self._encoder_async(data, noise)
             gt = data["gt_control"].to(fuse_feature.device, non_blocking=True)
             pred_control = self.control_predict(fuse_feature, gt)
+            pred_segmentation = br.join(pred_segmentation)
         finally:
             if self.training:
                 rng.end_step()
         return pred_control, pred_segmentation, pred_depth
 
     def predict(self, data, noise=None):
-        fuse_feature, pred_segmentation, pred_depth, bev_target = self.encoder(data, noise)
+        (fuse_feature, pred_segmentation, pred_depth, bev_target), br = self._encoder_async(data, noise)
         toks = data["gt_control"].to(fuse_feature.device, non_blocking=True)
         for _ in range(3):
             nxt = self.control_predict.predict(fuse_feature, toks)
             toks = torch.cat([toks, nxt], dim=1)
-        return toks, pred_segmentation, pred_depth, bev_target
+        return toks, br.join(pred_segmentation), pred_depth, bev_target

@@ -652,6 +652,12 @@ int e2ep_widen_u8_i64(const void *src, const long long *src_row, long long rows,
  * receives the number of nodes rewritten.
  * ------------------------------------------------------------------------------------- */
 int e2ep_graph_replace_memsets(void *graph, int *replaced);
+/* An executable of a (repaired) captured graph and its launch on a stream, bypassing
+ * torch.cuda.CUDAGraph.replay(), whose prologue launches int64 fill kernels to refresh torch's
+ * generator states (the step's random numbers come from e2ep_rng_draw). */
+int e2ep_graph_exec_create(void *graph, void **exec);
+int e2ep_graph_exec_launch(void *exec, void *stream);
+int e2ep_graph_exec_destroy(void *exec);
 
 #ifdef __cplusplus
 }

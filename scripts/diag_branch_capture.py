@@ -1,0 +1,102 @@
+"""Diagnostic: which side-stream branch captures crash hipStreamEndCapture (round 2 and round 4
+both saw a segfault in torch.cuda.graph's capture_end with model branches on side streams).
+
+    python scripts/diag_branch_capture.py            # runs every variant in a subprocess
+    python scripts/diag_branch_capture.py VARIANT    # one variant in this process
+
+Variants (forward on two streams, loss.backward(), all inside one graph capture, then one
+replay compared with eager):
+  toy_plain     torch ops: branch on a side stream, joined with wait_stream
+  toy_record    the same, plus record_stream on the tensors crossing the streams
+  toy_e2ep      the branch made of e2ep conv2d (whose backward forks its weight gradient)
+  model_cam     the ParkingModel B=2 train step with streams branch "cam" only
+  model_heads   the same with branch "heads" only
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "e2e-parking-carla_amd"), ROOT, os.path.join(ROOT, "tests")]
+VARIANTS = ["toy_plain", "toy_record", "toy_e2ep", "model_cam", "model_heads"]
+
+
+def toy(kind):
+    import torch
+    from e2ep_amd import conv
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    w1 = torch.randn(16, 16, 3, 3, device=dev, requires_grad=True)
+    w2 = torch.randn(16, 16, 3, 3, device=dev, requires_grad=True)
+    x = torch.randn(4, 16, 32, 32, device=dev)
+    side = torch.cuda.Stream()
+
+    def step():
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        if kind == "toy_record":
+            x.record_stream(side)
+        with torch.cuda.stream(side):
+            if kind == "toy_e2ep":
+                b = conv.conv2d(x, w2, pad=(1, 1, 1, 1))
+            else:
+                b = torch.nn.functional.conv2d(x, w2, padding=1)
+        a = conv.conv2d(x, w1, pad=(1, 1, 1, 1)) if kind == "toy_e2ep" else \
+            torch.nn.functional.conv2d(x, w1, padding=1)
+        main.wait_stream(side)
+        if kind == "toy_record":
+            b.record_stream(main)
+        loss = (a * b).square().mean()
+        w1.grad = w2.grad = None
+        loss.backward()
+        return loss.detach()
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    eager = step(), w1.grad.clone(), w2.grad.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = step()
+    g.replay()
+    torch.cuda.synchronize()
+    same = torch.equal(out, eager[0]) and torch.equal(w1.grad, eager[1]) and torch.equal(w2.grad, eager[2])
+    print(f"{kind}: captured and replayed; equal to eager: {same}", flush=True)
+
+
+def model(kind):
+    import torch
+    from e2ep_amd import streams, synthetic
+    from e2ep_amd.train import TrainStep
+    from test_train_step_b8_gpu import _module
+    streams.set_enabled({"model_cam": ["cam"], "model_heads": ["heads"]}[kind])
+    mod = _module()
+    d = synthetic.synthetic_batch(8, seed=11)
+    batch = {k: (v if k in ("intrinsics", "extrinsics") else v.cuda()) for k, v in d.items()}
+    step = TrainStep(mod, batch, graph=True, warmup=2)
+    losses = [float(step()) for _ in range(3)]
+    torch.cuda.synchronize()
+    print(f"{kind}: captured and replayed, losses {losses}", flush=True)
+
+
+def main():
+    if len(sys.argv) > 1:
+        kind = sys.argv[1]
+        (toy if kind.startswith("toy") else model)(kind)
+        return
+    for kind in VARIANTS:
+        r = subprocess.run([sys.executable, "-u", __file__, kind], capture_output=True, text=True,
+                           timeout=300)
+        tail = (r.stdout.strip().splitlines() or [""])[-1]
+        print(f"{kind}: exit {r.returncode} {tail if r.returncode == 0 else ''}", flush=True)
+        if r.returncode != 0:
+            err = [ln for ln in r.stderr.splitlines() if "File " in ln or "Error" in ln][-4:]
+            print("   ", " | ".join(err), flush=True)
+
+
+if __name__ == "__main__":
+    main()
