@@ -136,10 +136,13 @@ __global__ void __launch_bounds__(256) k_bn_apply(
     float *__restrict__ mean_out, float *__restrict__ invstd_out, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
     const float *__restrict__ dc_rand, float dc_keep, int N, int C, int HWv, int per, int act,
-    float *__restrict__ y) {
+    float *__restrict__ y, const float *__restrict__ scale, const float *__restrict__ shift) {
   const int c = blockIdx.x, j = blockIdx.y;
-  float mu, is;
-  if (part) {
+  float mu = 0.f, is = 0.f;
+  if (scale) {
+    // folded affine from e2ep_bn_finalize_part / e2ep_bn_stats (bn_finalize_channel: the same
+    // sc / sh expressions as below)
+  } else if (part) {
     double s, q;
     channel_partials(part, c, splits, s, q);
     const double m = s / (double)cnt;
@@ -164,8 +167,8 @@ __global__ void __launch_bounds__(256) k_bn_apply(
       invstd_out[c] = is;
     }
   }
-  const float sc = is * (gamma ? gamma[c] : 1.f);
-  const float sh = (beta ? beta[c] : 0.f) - mu * sc;
+  const float sc = scale ? scale[c] : is * (gamma ? gamma[c] : 1.f);
+  const float sh = scale ? shift[c] : (beta ? beta[c] : 0.f) - mu * sc;
   const int tot = N * HWv;
   const int beg = j * per, end = min(tot, beg + per);
   for (int t = beg + threadIdx.x; t < end; t += 256) {
@@ -210,6 +213,57 @@ __device__ __forceinline__ void bn_finalize_channel(
     if (threadIdx.x != 0) return;
     mu = running_mean[c];
     is = (float)(1.0 / sqrt((double)running_var[c] + (double)eps));
+  }
+  mean_out[c] = mu;
+  invstd_out[c] = is;
+  const float sc = is * (gamma ? gamma[c] : 1.f);
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - mu * sc;
+}
+
+// Finalize from a producer's tile-major partials (bnstats.h: part[(tile * C + c) * 2]):
+// block = 8 channels x 32 tile groups (lane = tid % 8 -> channel c0 + lane, group = tid / 8):
+// the 8 lanes of a group read one 128-B line per tile (channels c0 .. c0+7), group j sums tiles
+// j, j + 32, ...; the 32 group sums are added in group order through LDS, then the statistics
+// as bn_finalize_channel computes them.  grid = C / 8.  Fixed order: deterministic.  (A
+// two-level version that spread each channel's tiles over workgroups and handed the range
+// sums to the last-arriving one spent 12.7 us per launch on the hand-off's uncached loads.)
+constexpr int FT_CH = 8, FT_GROUPS = 32;
+__global__ void __launch_bounds__(256) k_bn_finalize_tiles(
+    const double *__restrict__ part, int tiles, int C, long long cnt, float eps, float momentum,
+    float *__restrict__ running_mean, float *__restrict__ running_var,
+    float *__restrict__ mean_out, float *__restrict__ invstd_out, const float *__restrict__ gamma,
+    const float *__restrict__ beta, float *__restrict__ scale, float *__restrict__ shift) {
+  __shared__ double rs[FT_GROUPS][FT_CH], rq[FT_GROUPS][FT_CH];
+  const int lane = threadIdx.x % FT_CH, grp = threadIdx.x / FT_CH;
+  const int c = blockIdx.x * FT_CH + lane;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = grp; k < tiles; k += FT_GROUPS) {
+      const double2 v = *reinterpret_cast<const double2 *>(part + ((size_t)k * C + c) * 2);
+      s += v.x;
+      q += v.y;
+    }
+  }
+  rs[grp][lane] = s;
+  rq[grp][lane] = q;
+  __syncthreads();
+  if (grp != 0 || c >= C) return;
+  double S = rs[0][lane], Q = rq[0][lane];
+  for (int j = 1; j < FT_GROUPS; ++j) {
+    S += rs[j][lane];
+    Q += rq[j][lane];
+  }
+  const double m = S / (double)cnt;
+  double var = Q / (double)cnt - m * m;
+  if (var < 0.0) var = 0.0;
+  const float mu = (float)m;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) {
+    const double unb = cnt > 1 ? var * (double)cnt / (double)(cnt - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * m);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
   }
   mean_out[c] = mu;
   invstd_out[c] = is;
@@ -702,11 +756,11 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
   if (v4)
     hipLaunchKernelGGL(k_bn_apply<4>, grid, dim3(256), 0, s, x, part, sp, per_c, eps, momentum,
                        running_mean, running_var, mean, invstd, gamma, beta, res, dc_rand, dc_keep,
-                       N, C, HWv, APPLY_PER, act, y);
+                       N, C, HWv, APPLY_PER, act, y, nullptr, nullptr);
   else
     hipLaunchKernelGGL(k_bn_apply<1>, grid, dim3(256), 0, s, x, part, sp, per_c, eps, momentum,
                        running_mean, running_var, mean, invstd, gamma, beta, res, dc_rand, dc_keep,
-                       N, C, HWv, APPLY_PER, act, y);
+                       N, C, HWv, APPLY_PER, act, y, nullptr, nullptr);
   return launch_status("e2ep_bn_fwd");
 }
 
@@ -752,6 +806,63 @@ int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *
   hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(256), 0, s, part, sp, per_c, eps, momentum,
                      running_mean, running_var, mean, invstd, gamma, beta, scale, shift);
   return launch_status("e2ep_bn_stats");
+}
+
+int e2ep_bn_fwd_split(int N, int C, int H, int W) {
+  if (N <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  const int HW = H * W;
+  const bool v4 = (HW & 3) == 0;
+  const int totv = N * (v4 ? HW / 4 : HW);
+  int th = 0;
+  return (v4 && bn_small_enabled() && totv <= g_bns_fwd_max && bns_r(totv, th)) ? 0 : 1;
+}
+
+size_t e2ep_bn_finalize_part_workspace(int C, int tiles) {
+  (void)C;
+  (void)tiles;
+  return 0;  // one launch, no workspace (kept in the ABI for a future split plan)
+}
+
+int e2ep_bn_finalize_part(const double *part, int tiles, const float *gamma, const float *beta,
+                          float *running_mean, float *running_var, int N, int C, int H, int W,
+                          float momentum, float eps, float *mean, float *invstd, float *scale,
+                          float *shift, void *workspace, size_t workspace_bytes, void *stream) {
+  E2EP_REQUIRE(part && tiles > 0 && N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535, E2EP_EINVAL,
+               "e2ep_bn_finalize_part: bad arguments");
+  E2EP_REQUIRE(mean && invstd && scale && shift, E2EP_EINVAL, "e2ep_bn_finalize_part: null output");
+  E2EP_REQUIRE(!running_mean == !running_var, E2EP_EINVAL,
+               "e2ep_bn_finalize_part: running_mean / running_var both or neither");
+  (void)workspace;
+  (void)workspace_bytes;
+  hipLaunchKernelGGL(k_bn_finalize_tiles, dim3(cdiv(C, FT_CH)), dim3(256), 0, as_stream(stream),
+                     part, tiles, C, (long long)N * H * W, eps, momentum, running_mean, running_var,
+                     mean, invstd, gamma, beta, scale, shift);
+  return launch_status("e2ep_bn_finalize_part");
+}
+
+int e2ep_bn_apply(const float *x, const float *scale, const float *shift, const float *res,
+                  const float *dc_rand, float dc_keep, int N, int C, int H, int W, int act,
+                  float *y, void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
+               E2EP_EINVAL, "e2ep_bn_apply: bad shape");
+  E2EP_REQUIRE(x && y && scale && shift && act >= 0 && act <= 2, E2EP_EINVAL,
+               "e2ep_bn_apply: bad arguments");
+  E2EP_REQUIRE(!dc_rand || dc_keep > 0.f, E2EP_EINVAL, "e2ep_bn_apply: drop-connect keep must be > 0");
+  const int HW = H * W;
+  const bool v4 = (HW & 3) == 0 && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)res) & 15) == 0;
+  const int HWv = v4 ? HW / 4 : HW;
+  const int totv = N * HWv;
+  const dim3 grid(C, cdiv(totv, APPLY_PER));
+  hipStream_t s = as_stream(stream);
+  if (v4)
+    hipLaunchKernelGGL(k_bn_apply<4>, grid, dim3(256), 0, s, x, nullptr, 1, (long long)N * HW, 0.f,
+                       0.f, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, res, dc_rand,
+                       dc_keep, N, C, HWv, APPLY_PER, act, y, scale, shift);
+  else
+    hipLaunchKernelGGL(k_bn_apply<1>, grid, dim3(256), 0, s, x, nullptr, 1, (long long)N * HW, 0.f,
+                       0.f, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, res, dc_rand,
+                       dc_keep, N, C, HWv, APPLY_PER, act, y, scale, shift);
+  return launch_status("e2ep_bn_apply");
 }
 
 int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,

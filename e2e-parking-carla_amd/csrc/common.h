@@ -49,6 +49,14 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, int byte_off)
   const e2ep_f4 v = e2ep_raw_buffer_load_v4f32(r, byte_off, 0, 0);
   return make_float4(v[0], v[1], v[2], v[3]);
 }
+// 8-B buffer load (same binding as bload4)
+typedef float e2ep_f2 __attribute__((ext_vector_type(2)));
+__device__ e2ep_f2 e2ep_raw_buffer_load_v2f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
+                                              int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.v2f32");
+__device__ __forceinline__ float2 bload2(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  const e2ep_f2 v = e2ep_raw_buffer_load_v2f32(r, byte_off, 0, 0);
+  return make_float2(v[0], v[1]);
+}
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 0);
 }

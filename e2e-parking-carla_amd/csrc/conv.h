@@ -65,9 +65,12 @@ struct TapList {
 // E2EP status.  Tap-major weights ([R*S][Cout][Cin]) or 1x1 filters only.
 bool lp_ok(int mode, const ConvGeom &g, int M, int op);
 size_t lp_workspace(int mode, const ConvGeom &g, int M, int op);
+// stats (forward only): BatchNorm partial sums of dst from the epilogue (bnstats.h), over
+// lp_stats_tiles(g, op) column tiles (0 = the plan cannot produce them).
 int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
               float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
-              hipStream_t s);
+              hipStream_t s, double *stats = nullptr);
+int lp_stats_tiles(const ConvGeom &g, int op);
 
 // Weight gradient with 32-pixel K-steps and up to 128 x 128 tiles, conv_lp.hip: bf16 operands
 // (op 1, C3) or fp32 (op 0, where TUNE_LP32W selects it).  Partial slabs

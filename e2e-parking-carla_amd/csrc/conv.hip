@@ -28,6 +28,7 @@
 #include "common.h"
 #include "conv.h"
 #include "gemm.h"
+#include "bnstats.h"
 #include "handoff.h"
 
 namespace e2ep {
@@ -50,11 +51,13 @@ constexpr int MAXPH = 4;
 // OP (0 fp32 / 1 bf16 / 2 fp16) as for k_conv_gemm2 below: for low precision one 16-deep MFMA
 // per K-step takes lane half h's k = 8h .. 8h+7 (eight LDS reads per operand, as the eight
 // fp32 MFMAs would do).
-template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0>
+// ST (forward only): the epilogue also writes BatchNorm partial sums into `stats` (bnstats.h);
+// a separate instantiation, so the plain forward keeps its register allocation.
+template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0, bool ST = false>
 __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
-    float *__restrict__ part, unsigned int *__restrict__ cnt) {
+    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
   // block tile BMT x BNT: BMT = 64 -> 2 x 2 waves of 32 x BNT/2; BMT = 32 (small-M layers:
   // Cout or Cin 24..56) -> 1 x 4 waves of 32 x BNT/4, so no MFMA rows are padding
   constexpr int WC = BMT == 64 ? BNT / 2 : BNT / 4;  // columns per wave
@@ -336,6 +339,11 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes : 0);
   const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
   const int HWd = Hd * Wd;
+  // MODE 0 with `stats`: BatchNorm partial sums of the stored values (bnstats.h)
+  constexpr bool want_stats = ST && MODE == 0;
+  float fs[16], fq[16];  // this lane's NACC (<= 4) values per row; fp64 from the butterfly on
+#pragma unroll
+  for (int r = 0; r < 16; ++r) fs[r] = fq[r] = 0.f;
 #pragma unroll
   for (int t = 0; t < NACC; ++t) {
     const int n = n0 + WC * wn + 32 * t + li;
@@ -363,8 +371,23 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       } else if (bias) {
         v += bload(rres, off);
       }
+      if (want_stats) {
+        const float d = (nok && m < M) ? v : 0.f;
+        fs[r] += d;
+        fq[r] = __builtin_fmaf(d, d, fq[r]);
+      }
       bstore(rd, off, v);
     }
+  }
+  if (want_stats) {
+    __shared__ double s_bn[2 * 64 * 2];  // [wn][row][2]: 2 x 64 or 4 x 32 rows
+    double bs[16], bq[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      bs[r] = fs[r];
+      bq[r] = fq[r];
+    }
+    bns_store_tile(bs, bq, wm, wn, BMT == 64 ? 2 : 4, BMT, m0, M, s_bn, stats);
   }
 }
 
@@ -1641,20 +1664,54 @@ static int korder_of() {
   return g_conv_precision != 0 ? 1 : 0;
 }
 
-static int launch_gemm(int mode, int act, const float *w, const float *src, const float *bias,
-                       float *dst, long long dst_bytes, const ConvGeom &g0, int M, void *workspace,
-                       hipStream_t s) {
+// The kernel family launch_gemm runs for a geometry (host only; g with korder / xcd set).
+enum ConvRoute { ROUTE_LP = 1, ROUTE_1X1 = 2, ROUTE_G2 = 3, ROUTE_LP32 = 4, ROUTE_GEMM = 5 };
+static int conv_route(int mode, const ConvGeom &g, int M) {
+  if (g_conv_precision != 0 && lp_ok(mode, g, M, g_conv_precision)) return ROUTE_LP;
+  if (conv1x1_gemm_ok(mode, g)) return ROUTE_1X1;
+  GemmPlan p2;
+  int wnt;
+  if (g.wlayout == 1 && plan_gemm2(mode, g, M, p2, wnt)) return ROUTE_G2;
+  if (g_conv_precision == 0 && g_tune[TUNE_LP32] == 2 && lp_ok(mode, g, M, 0)) return ROUTE_LP32;
+  return ROUTE_GEMM;
+}
+
+// Column tiles of the forward's BatchNorm partial statistics (e2ep_conv_fwd_stats), or 0 when
+// the routed kernel does not take them (then the BN layer computes its own).
+static int fwd_stats_tiles(const ConvGeom &g0) {
   ConvGeom g = g0;
   g.korder = korder_of();
   g.xcd = g_tune[TUNE_XCD] == 2;
-  if (g_conv_precision != 0 && lp_ok(mode, g, M, g_conv_precision))
-    return lp_launch(mode, act, g_conv_precision, w, src, bias, dst, dst_bytes, g, M, workspace, s);
-  if (conv1x1_gemm_ok(mode, g))
+  if (direct_ok(g)) return 0;
+  const int route = conv_route(0, g, g.Cout);
+  if (route == ROUTE_LP) return lp_stats_tiles(g, g_conv_precision);
+  if (route == ROUTE_LP32) return lp_stats_tiles(g, 0);
+  if (route != ROUTE_GEMM || g_conv_precision != 0) return 0;  // fp32 k_conv_gemm only
+  const GemmPlan p = plan_gemm(0, g, g.Cout);
+  if (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] != 2) return 0;  // final values in k_conv_reduce
+  return (int)cdiv(p.ncols, p.bnt);
+}
+
+static int launch_gemm(int mode, int act, const float *w, const float *src, const float *bias,
+                       float *dst, long long dst_bytes, const ConvGeom &g0, int M, void *workspace,
+                       hipStream_t s, double *stats = nullptr) {
+  ConvGeom g = g0;
+  g.korder = korder_of();
+  g.xcd = g_tune[TUNE_XCD] == 2;
+  const int route = conv_route(mode, g, M);
+  if (stats && (mode != 0 || route == ROUTE_1X1 || route == ROUTE_G2)) {
+    set_error("conv: BatchNorm statistics requested from a kernel that does not take them");
+    return E2EP_EINVAL;
+  }
+  if (route == ROUTE_LP)
+    return lp_launch(mode, act, g_conv_precision, w, src, bias, dst, dst_bytes, g, M, workspace, s,
+                     stats);
+  if (route == ROUTE_1X1)
     return conv1x1_gemm(mode, act, w, src, bias, dst, dst_bytes, g, M, workspace, s);
-  {
+  if (route == ROUTE_G2) {
     GemmPlan p2;
     int wnt;
-    if (g.wlayout == 1 && plan_gemm2(mode, g, M, p2, wnt)) {
+    if (plan_gemm2(mode, g, M, p2, wnt)) {
       dim3 grid(cdiv(p2.ncols, p2.bnt), cdiv(M, 64), p2.nph);
 #define G2(MD, AC, W)                                                                         \
   do {                                                                                        \
@@ -1675,8 +1732,8 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
       return 0;
     }
   }
-  if (g_conv_precision == 0 && g_tune[TUNE_LP32] == 2 && lp_ok(mode, g, M, 0))
-    return lp_launch(mode, act, 0, w, src, bias, dst, dst_bytes, g, M, workspace, s);
+  if (route == ROUTE_LP32)
+    return lp_launch(mode, act, 0, w, src, bias, dst, dst_bytes, g, M, workspace, s, stats);
   const GemmPlan p = plan_gemm(mode, g, M);
   dim3 grid(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
   float *part = nullptr;
@@ -1690,18 +1747,25 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     // in-launch fold (e2ep_tune key 28 = 2): one arrival counter per output tile
     if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y);
   }
+  if (stats && p.splits > 1 && !cnt) {
+    set_error("conv: BatchNorm statistics need the in-launch split-K fold (e2ep_tune key 28 = 2)");
+    return E2EP_EINVAL;
+  }
   const bool av = mode == 0 && g.wlayout == 1 && (g.Cin & 3) == 0;
 #define GEMM_LAUNCH1(MD, AC, BT, BMT, V)                                                          \
   do {                                                                                             \
     if (g_conv_precision == 1)                                                                     \
       hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 1>), grid, dim3(256), 0, s, w, src, bias, \
-                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt);                      \
+                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt, nullptr);             \
     else if (g_conv_precision == 2)                                                                \
       hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 2>), grid, dim3(256), 0, s, w, src, bias, \
-                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt);                      \
+                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt, nullptr);             \
+    else if (MD == 0 && stats)                                                                     \
+      hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 0, true>), grid, dim3(256), 0, s, w, src, \
+                         bias, dst, dst_bytes, g, M, p.splits, p.kper, part, cnt, stats);         \
     else                                                                                           \
       hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 0>), grid, dim3(256), 0, s, w, src, bias, \
-                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt);                      \
+                         dst, dst_bytes, g, M, p.splits, p.kper, part, cnt, nullptr);             \
   } while (0)
 #define GEMM_LAUNCH(MD, AC, BT, BMT)                                  \
   do {                                                                \
@@ -1787,8 +1851,22 @@ int e2ep_conv_gemm_variant(int variant) {
   return old;
 }
 
+int e2ep_conv_fwd_stats_tiles(const int *dims, int w_layout) {
+  ConvGeom g = make_geom(dims);
+  g.wlayout = w_layout;
+  if (!geom_ok(g) || (w_layout != 0 && w_layout != 1)) return 0;
+  return fwd_stats_tiles(g);
+}
+
 int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
                   int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream) {
+  return e2ep_conv_fwd_stats(x, w, bias, dims, act, w_layout, y, workspace, workspace_bytes,
+                             nullptr, 0, stream);
+}
+
+int e2ep_conv_fwd_stats(const float *x, const float *w, const float *bias, const int *dims, int act,
+                        int w_layout, float *y, void *workspace, size_t workspace_bytes,
+                        double *stats, size_t stats_bytes, void *stream) {
   ConvGeom g = make_geom(dims);
   {
     const size_t need = e2ep_conv_fwd_workspace(dims);
@@ -1800,13 +1878,22 @@ int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *
   g.wlayout = w_layout;
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_fwd: bad geometry");
   E2EP_REQUIRE(act == 0 || act == 1, E2EP_EINVAL, "e2ep_conv_fwd: act must be 0 (none) or 1 (relu)");
+  if (stats) {  // BatchNorm partials [Cout][tiles][2] from the epilogue (bnstats.h)
+    const int tiles = fwd_stats_tiles(g);
+    E2EP_REQUIRE(tiles > 0, E2EP_EINVAL,
+                 "e2ep_conv_fwd_stats: this geometry's kernel takes no statistics "
+                 "(e2ep_conv_fwd_stats_tiles returned 0)");
+    E2EP_REQUIRE(stats_bytes >= (size_t)g.Cout * tiles * 2 * sizeof(double), E2EP_EINVAL,
+                 "e2ep_conv_fwd_stats: stats %zu bytes < %zu (Cout x tiles x 2 doubles)",
+                 stats_bytes, (size_t)g.Cout * tiles * 2 * sizeof(double));
+  }
   if (direct_ok(g)) {
     hipLaunchKernelGGL(k_conv_direct, dim3(cdiv((long long)g.N * g.P * g.Q, 256)), dim3(256), 0,
                        as_stream(stream), x, w, bias, g, act, y);
     return launch_status("e2ep_conv_fwd");
   }
   const int rc = launch_gemm(0, act, w, x, bias, y, 4LL * g.N * g.Cout * g.P * g.Q, g, g.Cout,
-                             workspace, as_stream(stream));
+                             workspace, as_stream(stream), stats);
   if (rc) return rc;
   return launch_status("e2ep_conv_fwd");
 }

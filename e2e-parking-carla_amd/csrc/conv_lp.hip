@@ -25,6 +25,7 @@
 #include <algorithm>
 
 #include "conv.h"
+#include "bnstats.h"
 #include "handoff.h"
 
 namespace e2ep {
@@ -68,11 +69,11 @@ __device__ __forceinline__ f32x16 mfma16(typename LpType<OP>::T8 a, typename LpT
 // MODE 1 (data gradient): rows m = ci, K = (tap, co), src = g [N,Cout,P,Q], dst = dx
 //   [N,M,H,W]; phase z = (py, px) (blockIdx.z / splits) as in k_conv_gemm.
 // Block tile (64 WM) x (64 WN), 2 x 2 waves of (32 WM) x (32 WN).
-template <int MODE, int ACT, int WM, int WN, int OP, int LKS>
+template <int MODE, int ACT, int WM, int WN, int OP, int LKS, bool ST = false>
 __global__ void __launch_bounds__(256) k_conv_lp(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
-    float *__restrict__ part, unsigned int *__restrict__ cnt) {
+    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
   typedef typename LpType<OP>::T T;
   typedef typename LpType<OP>::T8 T8;
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
@@ -381,6 +382,13 @@ __global__ void __launch_bounds__(256) k_conv_lp(
   const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes : 0);
   const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
   const int HWd = Hd * Wd;
+  // MODE 0 with `stats`: BatchNorm partial sums of the stored values (bnstats.h)
+  constexpr bool want_stats = ST && MODE == 0;  // BatchNorm partials: separate instantiation
+  float fs[WM][16], fq[WM][16];  // this lane's WN values per row; fp64 from the butterfly on
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) fs[i][r] = fq[i][r] = 0.f;
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
     const int n = n0 + 32 * (WN * wn + j) + li;
@@ -410,9 +418,26 @@ __global__ void __launch_bounds__(256) k_conv_lp(
         } else if (bias) {
           v += bload(rres, off);
         }
+        if (want_stats) {
+          const float d = (nok && m < M) ? v : 0.f;
+          fs[i][r] += d;
+          fq[i][r] = __builtin_fmaf(d, d, fq[i][r]);
+        }
         bstore(rd, off, v);
       }
     }
+  }
+  if (want_stats) {
+    __shared__ double s_bn[2 * BMT * 2];  // [wn][row][2]
+    double bs[WM][16], bq[WM][16];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        bs[i][r] = fs[i][r];
+        bq[i][r] = fq[i][r];
+      }
+    bns_store_tile_n<WM>(bs, bq, 32 * WM * wm, wn, 2, BMT, m0, M, bx, s_bn, stats);
   }
 }
 
@@ -544,16 +569,25 @@ size_t lp_workspace(int mode, const ConvGeom &g, int M, int op) {
 template <int MODE, int ACT, int OP>
 static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, const float *src,
                      const float *bias, float *out, long long out_bytes, const ConvGeom &g, int M,
-                     float *part, unsigned int *cnt) {
+                     float *part, unsigned int *cnt, double *stats) {
 #define LP_L(WMV, WNV)                                                                              \
   do {                                                                                              \
-    if (OP != 0 && WNV <= 2 && p.lk == 64)                                                          \
-      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32>),     \
-                         grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits, p.kper, \
-                         part, cnt);                                                               \
-    else                                                                                            \
+    if (OP != 0 && WNV <= 2 && p.lk == 64) {                                                        \
+      if (MODE == 0 && stats)                                                                       \
+        hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32, true>), \
+                           grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits,     \
+                           p.kper, part, cnt, stats);                                               \
+      else                                                                                          \
+        hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32>),   \
+                           grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits,     \
+                           p.kper, part, cnt, nullptr);                                             \
+    } else if (MODE == 0 && stats) {                                                                \
+      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32, true>), grid, dim3(256), 0, s, w,  \
+                         src, bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt, stats);      \
+    } else {                                                                                        \
       hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32>), grid, dim3(256), 0, s, w, src,   \
-                         bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt);                 \
+                         bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt, nullptr);        \
+    }                                                                                               \
   } while (0)
   if (p.wm == 2) {
     if (p.wn == 2) LP_L(2, 2);
@@ -571,9 +605,15 @@ static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, 
 #undef LP_L
 }
 
+int lp_stats_tiles(const ConvGeom &g, int op) {
+  const LpPlan p = lp_plan(0, g, g.Cout, op);
+  if (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] != 2) return 0;  // final values in the reduce
+  return (int)cdiv(p.ncols, 64 * p.wn);
+}
+
 int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
               float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
-              hipStream_t s) {
+              hipStream_t s, double *stats) {
   const LpPlan p = lp_plan(mode, g, M, op);
   const dim3 grid(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
   float *part = nullptr;
@@ -587,13 +627,17 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
     // in-launch fold (e2ep_tune key 28 = 2): one arrival counter per output tile
     if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y);
   }
+  if (stats && (mode != 0 || (p.splits > 1 && !cnt))) {
+    set_error("conv (low precision): BatchNorm statistics need the forward with its final epilogue");
+    return E2EP_EINVAL;
+  }
   // bias / residual: the kernel's final epilogue, or the separate reduction
   const float *kb = (p.splits > 1 && !cnt) ? nullptr : bias;
 #define LP_OPS(MD, AC)                                                     \
   do {                                                                     \
-    if (op == 1) lp_tiles<MD, AC, 1>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt); \
-    else if (op == 2) lp_tiles<MD, AC, 2>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt); \
-    else lp_tiles<MD, AC, 0>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt); \
+    if (op == 1) lp_tiles<MD, AC, 1>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt, stats); \
+    else if (op == 2) lp_tiles<MD, AC, 2>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt, stats); \
+    else lp_tiles<MD, AC, 0>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt, stats); \
   } while (0)
   if (mode == 0 && act == 0) LP_OPS(0, 0);
   else if (mode == 0) LP_OPS(0, 1);

@@ -353,11 +353,21 @@ __device__ __forceinline__ void dw_row(const float *base, float (&v)[NV]) {
 
 // V: float4 per lane that hold a unit's staged rows (2 or DW_MAXV; the host picks the
 // smallest that covers IR * W / 4, so short units keep fewer registers and more waves resident)
-template <int K, int ST, bool FLIP, int OFF, int V>
+// BS: BatchNorm partial sums of y for the BN that follows (MBConv _bn1), one fp64 (sum, sum of
+// squares) pair per unit (a lane's 4 outputs in fp32, the wave's 64 lanes in fp64), written by
+// the unit's wave, tile-major like bnstats.h: tile = n * units_per_plane + row block,
+// stats[(tile * C + c) * 2].
+__device__ __forceinline__ double dw_wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false>
 __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
                                                       const float *__restrict__ w, DwGeom g,
                                                       DwStrip d, int units, float *__restrict__ y,
-                                                      DwIn tf) {
+                                                      DwIn tf, double *__restrict__ stats) {
   // Grid-stride over units, software-pipelined like k_dw_wgrad_strip: the wave's next unit's
   // input rows are loaded into registers before the current unit's FMAs (one unit per wave
   // with stage / wait / compute in series ran at 1.7-3.5 TB/s).  The grid is capped at
@@ -391,8 +401,9 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
     for (int t = 0; t < K * K; ++t) wr[t] = w[c * K * K + (FLIP ? K * K - 1 - t : t)];
     dw_wave_sync();
     const int oy = cur_oy0 + ro;
-    if (ro < d.RO && oy < g.P) {
-      float o[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool live = ro < d.RO && oy < g.P;
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
       const float *base = lds + (ro * ST) * d.WP + DW_PADL + ox0 * ST - g.pl;
 #pragma unroll
       for (int a = 0; a < K; ++a) {
@@ -405,6 +416,24 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
       }
       *reinterpret_cast<float4 *>(y + ((size_t)cur_nc * g.P + oy) * g.Q + ox0) =
           make_float4(o[0], o[1], o[2], o[3]);
+    }
+    if (BS) {  // BatchNorm partials (separate instantiation)
+      float f1 = 0.f, f2 = 0.f;
+      if (live) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f1 += o[q];
+          f2 = __builtin_fmaf(o[q], o[q], f2);
+        }
+      }
+      const double s1 = dw_wave_sum((double)f1);
+      const double s2 = dw_wave_sum((double)f2);
+      if (lane == 0) {
+        const int n = cur_nc / g.C, c = cur_nc - n * g.C;
+        const size_t at = (((size_t)n * d.units_per_plane + cur_oy0 / d.RO) * g.C + c) * 2;
+        stats[at] = s1;
+        stats[at + 1] = s2;
+      }
     }
     dw_wave_sync();  // LDS reuse
   }
@@ -592,8 +621,20 @@ static int dw_off(int pl) { return g_tune[TUNE_DW_VEC] == 1 ? -1 : ((-pl) & 3); 
 // (the scalar-read variant, an A/B switch, always takes DW_MAXV)
 template <int K, int ST, bool FLIP, int V>
 static void dw_fwd_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *x,
-                           const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf) {
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, x, w, g, d, units, y, tf); };
+                           const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf,
+                           double *stats) {
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, x, w, g, d, units, y, tf, stats);
+  };
+  if (stats && !FLIP) {
+    switch (off) {
+      case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V, true>); break;
+      case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V, true>); break;
+      case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2, V, true>); break;
+      default: go(k_dw_fwd_strip<K, ST, FLIP, 3, V, true>);
+    }
+    return;
+  }
   switch (off) {
     case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V>); break;
     case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V>); break;
@@ -603,14 +644,18 @@ static void dw_fwd_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const
 }
 template <int K, int ST, bool FLIP>
 static void dw_fwd_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const float *x,
-                         const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf) {
-  if (off < 0)
+                         const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf,
+                         double *stats) {
+  if (off < 0 && stats && !FLIP)
+    hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV, true>), grid, dim3(256), shm, st,
+                       x, w, g, d, units, y, tf, stats);
+  else if (off < 0)
     hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV>), grid, dim3(256), shm, st, x, w,
-                       g, d, units, y, tf);
+                       g, d, units, y, tf, nullptr);
   else if (nv <= 2)
-    dw_fwd_strip_v<K, ST, FLIP, 2>(off, grid, shm, st, x, w, g, d, units, y, tf);
+    dw_fwd_strip_v<K, ST, FLIP, 2>(off, grid, shm, st, x, w, g, d, units, y, tf, stats);
   else
-    dw_fwd_strip_v<K, ST, FLIP, DW_MAXV>(off, grid, shm, st, x, w, g, d, units, y, tf);
+    dw_fwd_strip_v<K, ST, FLIP, DW_MAXV>(off, grid, shm, st, x, w, g, d, units, y, tf, stats);
 }
 template <int K, int ST, int V>
 static void dw_wgrad_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *gy,
@@ -662,9 +707,29 @@ static bool dw_strip_ok(const DwGeom &g) {
 #define DW_NONE
 
 // dims[10] = {N, C, H, W, K, P, Q, stride, pad_top, pad_left}
+int e2ep_dwconv_fwd_stats_tiles(const int *dims) {
+  const DwGeom g = dw_geom(dims);
+  if (!(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0) || !dw_strip_ok(g)) return 0;
+  return g.N * dw_strip(g.K, g.st, g.W, g.P, g.Q).units_per_plane;
+}
+
 int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float *in_scale,
                     const float *in_shift, int in_act, float *y, void *stream) {
+  return e2ep_dwconv_fwd_stats(x, w, dims, in_scale, in_shift, in_act, y, nullptr, 0, stream);
+}
+
+int e2ep_dwconv_fwd_stats(const float *x, const float *w, const int *dims, const float *in_scale,
+                          const float *in_shift, int in_act, float *y, double *stats,
+                          size_t stats_bytes, void *stream) {
   DwGeom g = dw_geom(dims);
+  if (stats) {
+    const int tiles = e2ep_dwconv_fwd_stats_tiles(dims);
+    E2EP_REQUIRE(tiles > 0, E2EP_EINVAL,
+                 "e2ep_dwconv_fwd_stats: this geometry's kernel takes no statistics");
+    E2EP_REQUIRE(stats_bytes >= (size_t)g.C * tiles * 2 * sizeof(double), E2EP_EINVAL,
+                 "e2ep_dwconv_fwd_stats: stats %zu bytes < %zu (C x tiles x 2 doubles)",
+                 stats_bytes, (size_t)g.C * tiles * 2 * sizeof(double));
+  }
   E2EP_REQUIRE(!in_scale == !in_shift && in_act >= 0 && in_act <= 2, E2EP_EINVAL,
                "e2ep_dwconv_fwd: in_scale / in_shift both or neither, in_act 0..2");
   const DwIn tf{in_scale, in_shift, in_act};
@@ -674,7 +739,7 @@ int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     const int units = g.N * g.C * d.units_per_plane;
     DW_STRIP_DISPATCH(dw_fwd_strip, DW_NOFLIP, dim3(dw_fwd_blocks(units)), 4 * d.IR * d.WP * 4, x,
-                      w, g, d, units, y, tf);
+                      w, g, d, units, y, tf, stats);
     return launch_status("e2ep_dwconv_fwd");
   }
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_fwd: N*C > 65535");
@@ -699,10 +764,10 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
       const DwIn none{nullptr, nullptr, 0};
       if (t.K == 3)
         dw_fwd_strip<3, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
-                                 w, t, d, units, dx, none);
+                                 w, t, d, units, dx, none, nullptr);
       else
         dw_fwd_strip<5, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
-                                 w, t, d, units, dx, none);
+                                 w, t, d, units, dx, none, nullptr);
       return launch_status("e2ep_dwconv_dgrad");
     }
   }

@@ -30,13 +30,7 @@ namespace e2ep {
 typedef float g_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 g_bf16x8 __attribute__((ext_vector_type(8)));
 
-typedef float g_f2 __attribute__((ext_vector_type(2)));
-__device__ g_f2 e2ep_raw_buffer_load_v2f32(__amdgpu_buffer_rsrc_t rsrc, int voffset, int soffset,
-                                           int aux) __asm("llvm.amdgcn.raw.ptr.buffer.load.v2f32");
-__device__ __forceinline__ float2 bload2(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  const g_f2 v = e2ep_raw_buffer_load_v2f32(r, byte_off, 0, 0);
-  return make_float2(v[0], v[1]);
-}
+// bload2 (8-B buffer load): common.h
 
 // v & (ok ? ~0 : 0) as one v_and_b32 the compiler cannot turn back into a branch
 __device__ __forceinline__ float kmask(float v, bool ok) {

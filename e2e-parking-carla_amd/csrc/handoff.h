@@ -32,6 +32,16 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+__device__ __forceinline__ void st_sc1_d(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p),
+                     __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1_d(const double *p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // 16-B write-through store / sc1 load through a buffer descriptor (aux 16 = sc1).  The LLVM
 // intrinsics are bound directly, as bload4 in common.h.
 __device__ void e2ep_raw_buffer_store_v4f32(e2ep_f4 v, __amdgpu_buffer_rsrc_t rsrc, int voffset,

@@ -33,6 +33,8 @@ SIGNATURES = {
     "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
     "e2ep_conv_fwd_workspace": (_sz, [_p]),
     "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _sz, _p]),
+    "e2ep_conv_fwd_stats_tiles": (_i, [_p, _i]),
+    "e2ep_conv_fwd_stats": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _sz, _p, _sz, _p]),
     "e2ep_conv_dgrad_workspace": (_sz, [_p, _i]),
     "e2ep_conv_dgrad": (_i, [_p, _p, _p, _i, _i, _p, _p, _sz, _p]),
     "e2ep_conv_dgrad_acc": (_i, [_p, _p, _p, _i, _i, _p, _p, _p, _sz, _p]),
@@ -55,6 +57,10 @@ SIGNATURES = {
     "e2ep_bn_workspace": (_sz, [_i, _i, _i, _i]),
     "e2ep_bn_fwd": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i, _p, _p, _p, _p, _sz, _p]),
     "e2ep_bn_stats": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
+    "e2ep_bn_fwd_split": (_i, [_i, _i, _i, _i]),
+    "e2ep_bn_finalize_part_workspace": (_sz, [_i, _i]),
+    "e2ep_bn_finalize_part": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
+    "e2ep_bn_apply": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _i, _i, _p, _p]),
     "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _sz, _p]),
     "e2ep_act_fwd": (_i, [_p, _i64, _i, _p, _p]),
     "e2ep_act_bwd": (_i, [_p, _p, _i64, _i, _p, _p]),
@@ -70,6 +76,8 @@ SIGNATURES = {
     "e2ep_resize_bwd": (_i, [_p, _i64, _i, _i, _i, _i, _i, _f, _f, _p, _i, _p, _p]),
     "e2ep_resize_bwd_cl": (_i, [_p, _i64, _i, _i, _i, _i, _i, _i, _f, _f, _p, _p]),
     "e2ep_dwconv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p]),
+    "e2ep_dwconv_fwd_stats_tiles": (_i, [_p]),
+    "e2ep_dwconv_fwd_stats": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _sz, _p]),
     "e2ep_dwconv_dgrad": (_i, [_p, _p, _p, _p, _p]),
     "e2ep_dwconv_wgrad_workspace": (_sz, [_p]),
     "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _i, _p, _sz, _p, _p]),

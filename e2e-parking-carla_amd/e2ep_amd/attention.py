@@ -92,7 +92,10 @@ class _Attn(torch.autograd.Function):
                 # D first, then dq here and dk/dv on the side stream concurrently (conv._Fork:
                 # every buffer is allocated above, on the current stream)
                 _lib.call("e2ep_attn_bwd_part", *args, 1, _lib.stream())
-                fork = conv._Fork(qb.device)
+                # dk / dv: ~4 dh-long fma chains per (query, key) pair and head, vector rate
+                B_, H_, Sq_, Sk_, dh_ = dims[:5]
+                fork = conv._Fork(qb.device, work_us=conv.est_us(
+                    8.0 * B_ * H_ * Sq_ * Sk_ * dh_ * 4))
                 with fork:
                     _lib.call("e2ep_attn_bwd_part", *args, 3, _lib.stream())
                 _lib.call("e2ep_attn_bwd_part", *args, 2, _lib.stream())

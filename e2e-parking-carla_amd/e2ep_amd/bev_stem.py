@@ -51,7 +51,8 @@ class _BevStem(torch.autograd.Function):
             dw = torch.empty_like(w)
             ws = torch.empty(_lib.load().e2ep_conv_wgrad_splits(d) * dw.numel(), dtype=torch.float32,
                              device=gy.device)
-            fork = conv._Fork(gy.device, on=ctx.needs_input_grad[0])
+            fork = conv._Fork(gy.device, on=ctx.needs_input_grad[0],
+                              work_us=conv.est_us(conv.conv_flops(dims)))
             with fork:
                 conv.conv_wgrad(gy, x, dims, dw, ws)
         if ctx.needs_input_grad[0]:

@@ -119,14 +119,31 @@ def tap_major(w):
     return out
 
 
-def conv_fwd(x, w, b, dims, act, y, w_layout=0):
-    """Launch the forward conv into y (handles the split-K workspace)."""
+def conv_fwd(x, w, b, dims, act, y, w_layout=0, stats=None):
+    """Launch the forward conv into y (handles the split-K workspace).  stats: an fp64 buffer
+    for the BatchNorm partial sums of y (e2ep_conv_fwd_stats; see conv2d(bn_stats=True))."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_fwd_workspace(d), x.device)
     with timing.region(_rname("conv_fwd", dims), conv_flops(dims)):
-        _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
-                  _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
+        if stats is None:
+            _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
+                      _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
+        else:
+            _lib.call("e2ep_conv_fwd_stats", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
+                      _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(stats),
+                      _lib.nbytes(stats), _lib.stream())
     return y
+
+
+# E2EP_NO_BN_STATS=1: BN layers compute their own statistics (A/B timing of the epilogue
+# statistics; conv2d / depthwise_conv2d then ignore bn_stats=True)
+_BN_STATS = [os.environ.get("E2EP_NO_BN_STATS", "0") in ("", "0")]
+
+
+def bn_partials(y):
+    """(partials, tiles) of y's BatchNorm statistics when the conv that produced y wrote them
+    (conv2d(bn_stats=True)), else None."""
+    return getattr(y, "_e2ep_bn_part", None)
 
 
 def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0, res=None):
@@ -158,8 +175,32 @@ def conv_wgrad(gy, x, dims, dw, ws=None):
 # memory out while the side stream uses it.  Under HIP-graph capture the fork / join become
 # parallel graph branches.  Small convs (16x16 / 32x32 maps) fill a fraction of the chip, so
 # their two GEMMs overlap instead of running back to back.
+#
+# A fork is not free in a replayed HIP graph: the side branch starts ~5 us after its fork
+# point and the node after the join waits ~9-10 us for the other queue's completion signal
+# (scripts/step_sequence.py over the C2 step: 205 idle gaps of 4-10 us, 2.0 ms per step, one
+# per fork / join of the transformer's and the 16x16 stages' small layers).  A backward forks
+# only when its side work is estimated at >= E2EP_FORK_MIN_US microseconds; shorter pairs run
+# back to back on the current stream.  est_us() gives the estimate from the work the caller
+# passes (FLOPs at a nominal 40 TF/s, or bytes at 3 TB/s).  Measured (profiles/r04/
+# fork_min_us_ab.txt): C2 23.49 / 23.42 / 23.53 / 23.79 / 24.17 / 23.50 ms at 0 / 10 / 20 / 40 /
+# 80 us / never — the gaps and the overlap cancel — and C3 20.32 / 20.46 / 20.76 ms at 0 / 20 /
+# never, so the default stays 0 (every fork).
 _SIDE = {}
 _OVERLAP = [os.environ.get("E2EP_WGRAD_OVERLAP", "1") != "0"]
+_FORK_MIN_US = [float(os.environ.get("E2EP_FORK_MIN_US", "0"))]
+
+
+def est_us(flops=0.0, nbytes=0.0):
+    """Nominal duration (us) of side-stream work: FLOPs at 40 TF/s plus bytes at 3 TB/s."""
+    return flops / 4e7 + nbytes / 3e6
+
+
+def set_fork_min_us(us):
+    """Minimum estimated side work (us) for a fork (returns the previous value)."""
+    prev = _FORK_MIN_US[0]
+    _FORK_MIN_US[0] = float(us)
+    return prev
 
 
 def set_wgrad_overlap(on):
@@ -186,10 +227,11 @@ def side_stream(device):
 
 class _Fork:
     """with _Fork(dev) as side: ...launches on `side`...  — forks from the current stream on
-    entry (side waits for it); join() makes the current stream wait for the side stream."""
+    entry (side waits for it); join() makes the current stream wait for the side stream.
+    work_us: the side work's estimate (est_us); below E2EP_FORK_MIN_US it stays serial."""
 
-    def __init__(self, device, on=True):
-        self.on = on and _OVERLAP[0]
+    def __init__(self, device, on=True, work_us=float("inf")):
+        self.on = on and _OVERLAP[0] and work_us >= _FORK_MIN_US[0]
         self.main = torch.cuda.current_stream(device)
         self.side = side_stream(device) if self.on else self.main
 
@@ -212,12 +254,12 @@ class _Fork:
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, dims, act, grad_channels, skip=False):
+    def forward(ctx, x, w, b, dims, act, grad_channels, skip=False, stats=None):
         x = x.contiguous()
         wt = tap_major(w)  # one small transpose per step for R*S > 1; shared with dgrad
         N, Cin, H, W, Cout, R, S, P, Q = dims[:9]
         y = conv_fwd(x, wt, b, dims, act, torch.empty(N, Cout, P, Q, dtype=torch.float32, device=x.device),
-                     w_layout=1)
+                     w_layout=1, stats=stats)
         ctx.dims, ctx.act, ctx.has_bias, ctx.gc = dims, act, b is not None, grad_channels
         ctx.save_for_backward(x, wt, y if act else None)
         ctx.wshape = w.shape
@@ -251,7 +293,7 @@ class _Conv2d(torch.autograd.Function):
                                  dtype=torch.float32, device=x.device)
             if want_b:
                 db = torch.empty(Cout, dtype=torch.float32, device=x.device)
-            fork = _Fork(x.device, on=ctx.needs_input_grad[0])
+            fork = _Fork(x.device, on=ctx.needs_input_grad[0], work_us=est_us(conv_flops(dims)))
             with fork:
                 if want_w:
                     conv_wgrad(gy, x, dims, dw, ws)
@@ -275,7 +317,7 @@ class _Conv2d(torch.autograd.Function):
             fork.join()
         if dx is None and gskip is not None and ctx.needs_input_grad[0]:
             dx = gskip
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def _skinny(A, ai, ak, B, bk, bj, bias, Mi, Nj, K, out):
@@ -319,10 +361,14 @@ class _Linear1x1(torch.autograd.Function):
 
 
 def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0, grad_channels=None,
-           skip=False):
+           skip=False, bn_stats=False):
     """pad = (left, right, top, bottom); act 0 none, 1 relu (fused epilogue).
     skip=True returns (y, x_skip): use x_skip for the block's skip connection and its gradient
-    is added to this conv's input gradient inside the data-gradient kernel."""
+    is added to this conv's input gradient inside the data-gradient kernel.
+    bn_stats=True (a training BatchNorm reads y next): where the routed kernel takes them and
+    the BN would make a statistics pass over y (e2ep_bn_fwd_split), the epilogue also writes
+    y's per-channel partial sums (e2ep_conv_fwd_stats), attached to y for the BN
+    (bn_partials), which then never re-reads y for its statistics."""
     if not x.is_cuda:
         raise _lib.E2EPError("e2ep conv2d runs on a HIP device only")
     N, Cin, H, W = x.shape
@@ -338,4 +384,14 @@ def conv2d(x, w, b=None, stride=(1, 1), pad=(0, 0, 0, 0), dilation=(1, 1), act=0
     P = (H + t + btm - dh * (R - 1) - 1) // sh + 1
     Q = (W + l + r - dw * (S - 1) - 1) // sw + 1
     dims = (N, Cin, H, W, Cout, R, S, P, Q, sh, sw, t, l, dh, dw)
-    return _Conv2d.apply(x, w, b, dims, act, grad_channels, bool(skip))
+    # only where the BN would otherwise make a statistics pass (its split path)
+    lib = _lib.load()
+    tiles = (lib.e2ep_conv_fwd_stats_tiles(_lib.dims(dims), 1)
+             if bn_stats and _BN_STATS[0] and lib.e2ep_bn_fwd_split(N, Cout, P, Q) else 0)
+    if tiles <= 0:
+        return _Conv2d.apply(x, w, b, dims, act, grad_channels, bool(skip))
+    part = torch.empty(Cout * tiles * 2, dtype=torch.float64, device=x.device)
+    out = _Conv2d.apply(x, w, b, dims, act, grad_channels, bool(skip), part)
+    y = out[0] if skip else out
+    y._e2ep_bn_part = (part, tiles)
+    return out

@@ -27,11 +27,29 @@ def _ws(nbytes, device):
 # ------------------------------------------------------------------------------------------
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, rm, rv, train, momentum, eps, act, dc_rand, dc_keep):
+    def forward(ctx, x, gamma, beta, res, rm, rv, train, momentum, eps, act, dc_rand, dc_keep,
+                part=None, tiles=0):
         x = x.contiguous()
         res = res.contiguous() if res is not None else None
         N, C, H, W = x.shape
         y = torch.empty_like(x)
+        if part is not None and train:
+            # statistics from the producing conv's epilogue (e2ep_conv_fwd_stats): finalize the
+            # partials, then the elementwise pass with the folded affine
+            st = torch.empty(4, C, dtype=torch.float32, device=x.device)  # mean, invstd, scale, shift
+            mean, invstd = st[0], st[1]
+            with timing.region(timing.name("bn_fwd", x.shape, "_BnAct")):
+                fws = _ws(_lib.load().e2ep_bn_finalize_part_workspace(C, tiles), x.device)
+                _lib.call("e2ep_bn_finalize_part", _lib.ptr(part), tiles, _lib.ptr(gamma),
+                          _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W, float(momentum),
+                          float(eps), _lib.ptr(st[0]), _lib.ptr(st[1]), _lib.ptr(st[2]),
+                          _lib.ptr(st[3]), _lib.ptr(fws), _lib.nbytes(fws), _lib.stream())
+                _lib.call("e2ep_bn_apply", _lib.ptr(x), _lib.ptr(st[2]), _lib.ptr(st[3]),
+                          _lib.ptr(res), _lib.ptr(dc_rand), float(dc_keep), N, C, H, W, act,
+                          _lib.ptr(y), _lib.stream())
+            ctx.save_for_backward(x, gamma, beta, res, mean, invstd, dc_rand)
+            ctx.train, ctx.act, ctx.dc_keep = train, act, dc_keep
+            return y
         mean = torch.empty(C, dtype=torch.float32, device=x.device)
         invstd = torch.empty_like(mean)
         ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
@@ -65,7 +83,7 @@ class _BnAct(torch.autograd.Function):
                       _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
         if dres_is_dy:
             dres = dy
-        return dx, dg, db, dres, None, None, None, None, None, None, None, None
+        return dx, dg, db, dres, None, None, None, None, None, None, None, None, None, None
 
 
 class BnCounters:
@@ -146,8 +164,9 @@ def batch_norm_act(x, bn, act=None, res=None, dc_rand=None, dc_keep=1.0):
     mom = bn.momentum if bn.momentum is not None else 0.1
     if dc_rand is not None:
         dc_rand = dc_rand.contiguous()
+    pp = conv.bn_partials(x) if train else None
     return _BnAct.apply(x, bn.weight, bn.bias, res, rm, rv, train, mom, bn.eps, ACT[act],
-                        dc_rand, dc_keep)
+                        dc_rand, dc_keep, *(pp or (None, 0)))
 
 
 class _Act(torch.autograd.Function):
@@ -220,15 +239,15 @@ def resize(x, size=None, scale_factor=None):
 # ------------------------------------------------------------------------------------------
 class _DwConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, dims):
+    def forward(ctx, x, w, dims, ystats=None):
         x = x.contiguous()
         w = w.contiguous()
         N, C, H, W, K, P, Q = dims[:7]
         y = torch.empty(N, C, P, Q, dtype=torch.float32, device=x.device)
         d = _lib.dims(dims)
         with timing.region(timing.name("dwconv_fwd", x.shape, "_DwConv")):
-            _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, None, None, 0, _lib.ptr(y),
-                      _lib.stream())
+            _lib.call("e2ep_dwconv_fwd_stats", _lib.ptr(x), _lib.ptr(w), d, None, None, 0,
+                      _lib.ptr(y), _lib.ptr(ystats), _lib.nbytes(ystats), _lib.stream())
         ctx.save_for_backward(x, w)
         ctx.dims = dims
         return y
@@ -244,7 +263,8 @@ class _DwConv(torch.autograd.Function):
         if ctx.needs_input_grad[1]:  # weight gradient on the side stream (conv._Fork)
             dw = torch.empty_like(w)
             ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
-            fork = conv._Fork(x.device, on=ctx.needs_input_grad[0])
+            fork = conv._Fork(x.device, on=ctx.needs_input_grad[0],
+                              work_us=conv.est_us(nbytes=4.0 * (x.numel() + gy.numel())))
             with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_DwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
                           _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), _lib.stream())
@@ -254,7 +274,7 @@ class _DwConv(torch.autograd.Function):
                 _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s)
         if fork is not None:
             fork.join()
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class _BnActDwConv(torch.autograd.Function):
@@ -265,24 +285,32 @@ class _BnActDwConv(torch.autograd.Function):
     depthwise_conv2d."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, act, w, dims):
+    def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, act, w, dims, part=None, tiles=0,
+                ystats=None):
         x = x.contiguous()
         w = w.contiguous()
         N, C, H, W, K, P, Q = dims[:7]
         f32 = dict(dtype=torch.float32, device=x.device)
         stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
-        ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
         s = _lib.stream()
         with timing.region(timing.name("bn_fwd", x.shape, "_BnActDwConv")):
-            _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
-                      _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
-                      _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
-                      _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
+            if part is not None and train:  # partials from the expand conv's epilogue
+                fws = _ws(_lib.load().e2ep_bn_finalize_part_workspace(C, tiles), x.device)
+                _lib.call("e2ep_bn_finalize_part", _lib.ptr(part), tiles, _lib.ptr(gamma),
+                          _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W, float(momentum),
+                          float(eps), _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
+                          _lib.ptr(stats[3]), _lib.ptr(fws), _lib.nbytes(fws), s)
+            else:
+                ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
+                _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
+                          _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
+                          _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
+                          _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
         y = torch.empty(N, C, P, Q, **f32)
         d = _lib.dims(dims)
         with timing.region(timing.name("dwconv_fwd", x.shape, "_BnActDwConv")):
-            _lib.call("e2ep_dwconv_fwd", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(stats[2]),
-                      _lib.ptr(stats[3]), act, _lib.ptr(y), s)
+            _lib.call("e2ep_dwconv_fwd_stats", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(stats[2]),
+                      _lib.ptr(stats[3]), act, _lib.ptr(y), _lib.ptr(ystats), _lib.nbytes(ystats), s)
         ctx.save_for_backward(x, gamma, beta, w, stats)
         ctx.dims, ctx.train, ctx.act = dims, train, act
         return y
@@ -300,7 +328,8 @@ class _BnActDwConv(torch.autograd.Function):
         if nig[9]:  # weight gradient on the side stream (conv._Fork)
             dw = torch.empty_like(w)
             wsw = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
-            fork = conv._Fork(x.device, on=nig[0] or nig[1] or nig[2])
+            fork = conv._Fork(x.device, on=nig[0] or nig[1] or nig[2],
+                              work_us=conv.est_us(nbytes=4.0 * (x.numel() + gy.numel())))
             with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(stats[2]),
                           _lib.ptr(stats[3]), ctx.act, _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream())
@@ -319,22 +348,42 @@ class _BnActDwConv(torch.autograd.Function):
                           _lib.ptr(db), None, _lib.ptr(ws), _lib.nbytes(ws), s)
         if fork is not None:
             fork.join()
-        return dx, dg, db, None, None, None, None, None, None, dw, None
+        return dx, dg, db, None, None, None, None, None, None, dw, None, None, None, None
 
 
-def depthwise_conv2d(x, w, stride, pad):
-    """pad = (left, right, top, bottom); w [C, 1, K, K]."""
+def depthwise_conv2d(x, w, stride, pad, bn_stats=False):
+    """pad = (left, right, top, bottom); w [C, 1, K, K].  bn_stats: see
+    bn_act_depthwise_conv2d."""
     _dev(x)
     N, C, H, W = x.shape
     K = w.shape[-1]
     l, r, t, b = pad
     P = (H + t + b - K) // stride + 1
     Q = (W + l + r - K) // stride + 1
-    return _DwConv.apply(x, w, (N, C, H, W, K, P, Q, stride, t, l))
+    dims = (N, C, H, W, K, P, Q, stride, t, l)
+    ys, tiles = _dw_stats_buffer(dims, x.device, bn_stats)
+    y = _DwConv.apply(x, w, dims, ys)
+    if ys is not None:
+        y._e2ep_bn_part = (ys, tiles)
+    return y
 
 
-def bn_act_depthwise_conv2d(x, bn, act, w, stride, pad):
-    """depthwise_conv2d(batch_norm_act(x, bn, act), w, stride, pad) as one fused op."""
+def _dw_stats_buffer(dims, device, want):
+    """(fp64 partials buffer, tiles) for the depthwise forward's BatchNorm statistics
+    (e2ep_dwconv_fwd_stats), or (None, 0) when not wanted or the kernel takes none."""
+    lib = _lib.load()
+    if not want or not conv._BN_STATS[0] or not lib.e2ep_bn_fwd_split(dims[0], dims[1], dims[5], dims[6]):
+        return None, 0
+    tiles = lib.e2ep_dwconv_fwd_stats_tiles(_lib.dims(dims))
+    if tiles <= 0:
+        return None, 0
+    return torch.empty(dims[1] * tiles * 2, dtype=torch.float64, device=device), tiles
+
+
+def bn_act_depthwise_conv2d(x, bn, act, w, stride, pad, bn_stats=False):
+    """depthwise_conv2d(batch_norm_act(x, bn, act), w, stride, pad) as one fused op.
+    bn_stats: a training BatchNorm reads the output next (its partial sums come from the
+    depthwise kernel, attached as for conv.conv2d(bn_stats=True))."""
     _dev(x)
     train = _bn_train_and_count(bn)
     rm = bn.running_mean if bn.track_running_stats else None
@@ -345,8 +394,14 @@ def bn_act_depthwise_conv2d(x, bn, act, w, stride, pad):
     l, r, t, b = pad
     P = (H + t + b - K) // stride + 1
     Q = (W + l + r - K) // stride + 1
-    return _BnActDwConv.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, ACT[act], w,
-                              (N, C, H, W, K, P, Q, stride, t, l))
+    pp = conv.bn_partials(x) if train else None
+    dims = (N, C, H, W, K, P, Q, stride, t, l)
+    ys, tiles = _dw_stats_buffer(dims, x.device, bn_stats)
+    y = _BnActDwConv.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, ACT[act], w, dims,
+                           *(pp or (None, 0)), ys)
+    if ys is not None:
+        y._e2ep_bn_part = (ys, tiles)
+    return y
 
 
 # ------------------------------------------------------------------------------------------
@@ -488,20 +543,28 @@ class _BnSwishSE(torch.autograd.Function):
     the backward forms its gradient inside the BN backward (gate_logit / gate_dpooled)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, w1, b1, w2, b2):
+    def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, w1, b1, w2, b2, part=None,
+                tiles=0):
         x = x.contiguous()
         N, C, H, W = x.shape
         sq = w1.shape[0]
         dev = x.device
         f32 = dict(dtype=torch.float32, device=dev)
         stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
-        ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
         s = _lib.stream()
         with timing.region(timing.name("bn_fwd", x.shape, "_BnSwishSE")):
-            _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
-                      _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
-                      _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
-                      _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
+            if part is not None and train:  # partials from the depthwise kernel
+                fws = _ws(_lib.load().e2ep_bn_finalize_part_workspace(C, tiles), x.device)
+                _lib.call("e2ep_bn_finalize_part", _lib.ptr(part), tiles, _lib.ptr(gamma),
+                          _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W, float(momentum),
+                          float(eps), _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
+                          _lib.ptr(stats[3]), _lib.ptr(fws), _lib.nbytes(fws), s)
+            else:
+                ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
+                _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
+                          _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
+                          _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
+                          _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
         pooled, hpre, a = torch.empty(N, C, **f32), torch.empty(N, sq, **f32), torch.empty(N, C, **f32)
         y = torch.empty_like(x)
         w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
@@ -546,7 +609,7 @@ class _BnSwishSE(torch.autograd.Function):
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           _lib.ptr(a), _lib.ptr(dpooled), N, C, H, W, int(ctx.train), ACT["swish"],
                           _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), None, _lib.ptr(bws), _lib.nbytes(bws), s)
-        return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2
+        return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None
 
 
 def bn_swish_squeeze_excite(x, bn, w1, b1, w2, b2):
@@ -556,7 +619,9 @@ def bn_swish_squeeze_excite(x, bn, w1, b1, w2, b2):
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     mom = bn.momentum if bn.momentum is not None else 0.1
-    return _BnSwishSE.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, w1, b1, w2, b2)
+    pp = conv.bn_partials(x) if train else None
+    return _BnSwishSE.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, w1, b1, w2, b2,
+                            *(pp or (None, 0)))
 
 
 def squeeze_excite(x, w1, b1, w2, b2):
@@ -826,7 +891,7 @@ def _linear_bwd(g2, x2, weight, want_x, want_w, want_b, gskip=None, dw=None, db=
             if db is None:
                 db = torch.empty(N, dtype=torch.float32, device=g2.device)
             wsb = None if want_w else _ws(_lib.load().e2ep_col_sum_workspace(M, N), g2.device)
-        fork = conv._Fork(g2.device, on=want_x)
+        fork = conv._Fork(g2.device, on=want_x, work_us=conv.est_us(2.0 * N * K * M))
         with fork:
             if want_w and want_b:  # dW and db in one launch
                 with timing.region(timing.name("gemm", (N, K, M), "linear_wgrad"), 2.0 * N * K * M):

@@ -29,13 +29,17 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         # identity skip, or the downsample conv's input: x is conv1's skip alias either way, so
         # its second gradient joins conv1's data gradient in the epilogue (no autograd add)
-        c1, x = ops.conv2d(x, self.conv1.weight, None, self.stride, 1, skip=True)
+        # bn_stats: each BN's batch statistics from its conv's epilogue where it takes them
+        c1, x = ops.conv2d(x, self.conv1.weight, None, self.stride, 1, skip=True,
+                           bn_stats=self.bn1.training)
         y = ops.bn_act(c1, self.bn1, "relu")
         if self.downsample is not None:
-            x = ops.bn_act(ops.conv2d(x, self.downsample[0].weight, None, self.stride, 0),
-                           self.downsample[1], None)
+            ds = self.downsample[1]
+            x = ops.bn_act(ops.conv2d(x, self.downsample[0].weight, None, self.stride, 0,
+                                      bn_stats=ds.training), ds, None)
         # relu(bn2(conv2(y)) + identity) as one fused BN/residual/activation kernel
-        return ops.bn_act(ops.conv2d(y, self.conv2.weight, None, 1, 1), self.bn2, "relu", res=x)
+        return ops.bn_act(ops.conv2d(y, self.conv2.weight, None, 1, 1, bn_stats=self.bn2.training),
+                          self.bn2, "relu", res=x)
 
 
 def _layer(cin, cout, stride):

@@ -14,8 +14,8 @@ def _conv_bn(cin, cout, k, pad=0, dil=1):
 
 def _run_conv_bn_relu(seq, x, first=0):
     conv, bn = seq[first], seq[first + 1]
-    return ops.bn_act(ops.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation),
-                      bn, "relu")
+    return ops.bn_act(ops.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation,
+                                 bn_stats=bn.training), bn, "relu")
 
 
 class ASPPConv(nn.Sequential):
@@ -52,7 +52,7 @@ class ASPP(nn.Module):
         for m in self.convs[:-1]:
             conv, bn = m[0], m[1]
             c, x = ops.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation,
-                              skip=True)
+                              skip=True, bn_stats=bn.training)
             branches.append(ops.bn_act(c, bn, "relu"))
         branches.append(self.convs[-1](x))
         y = _run_conv_bn_relu(self.project, nn_ops.cat_channels(branches))
@@ -73,7 +73,8 @@ class DeepLabHead(nn.Sequential):
 
     def forward(self, x):
         y = self[0](x)
-        y = ops.bn_act(ops.conv2d(y, self[1].weight, None, 1, 1), self[2], "relu")
+        y = ops.bn_act(ops.conv2d(y, self[1].weight, None, 1, 1, bn_stats=self[2].training),
+                       self[2], "relu")
         return ops.conv2d(y, self[4].weight, self[4].bias)
 
 

@@ -39,13 +39,17 @@ class SameConv(nn.Conv2d):
         super().__init__(cin, cout, k, stride=stride, padding=0, groups=groups, bias=bias)
         self.same = _same(size, k, stride)
 
-    def forward(self, x):
-        return ops.conv2d(x, self.weight, self.bias, self.stride, self.same, 1, self.groups)
+    def forward(self, x, bn_stats=False):
+        """bn_stats: a training BatchNorm reads the output next (its statistics come from this
+        conv's epilogue where the kernel takes them, e2ep_conv_fwd_stats)."""
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.same, 1, self.groups,
+                          bn_stats=bn_stats)
 
-    def forward_skip(self, x):
+    def forward_skip(self, x, bn_stats=False):
         """(conv(x), x_skip): x_skip feeds the block's skip connection; its gradient is added
         inside this conv's data-gradient kernel (e2ep_conv_dgrad_acc)."""
-        return ops.conv2d(x, self.weight, self.bias, self.stride, self.same, 1, self.groups, skip=True)
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.same, 1, self.groups, skip=True,
+                          bn_stats=bn_stats)
 
 
 class MBConv(nn.Module):
@@ -70,33 +74,34 @@ class MBConv(nn.Module):
         here when not given (efficientnet-pytorch draws torch.rand([N,1,1,1]) per block).
         alias=True (blocks with an expand conv): returns (out, x_alias), x_alias being the
         expand conv's skip alias of x for another consumer of x (a trunk endpoint)."""
+        st = self.training  # BN statistics from the 1x1 convs' epilogues (training BN)
         if alias:
             assert self.expand != 1 and not self.skip
-            e, xa = self._expand_conv.forward_skip(x)
-            y = ops.bn_act_depthwise(e, self._bn0, "swish", self._depthwise_conv)
+            e, xa = self._expand_conv.forward_skip(x, st)
+            y = ops.bn_act_depthwise(e, self._bn0, "swish", self._depthwise_conv, st)
             y = ops.bn_swish_squeeze_excite(y, self._bn1, self._se_reduce, self._se_expand)
-            return ops.bn_act(self._project_conv(y), self._bn2, None), xa
+            return ops.bn_act(self._project_conv(y, st), self._bn2, None), xa
         if self.expand != 1:  # _bn0 + swish applied inside the depthwise conv's input load
             if self.skip and x.is_cuda:
-                e, x = self._expand_conv.forward_skip(x)
+                e, x = self._expand_conv.forward_skip(x, st)
             else:
-                e = self._expand_conv(x)
-            y = ops.bn_act_depthwise(e, self._bn0, "swish", self._depthwise_conv)
+                e = self._expand_conv(x, st)
+            y = ops.bn_act_depthwise(e, self._bn0, "swish", self._depthwise_conv, st)
         elif self.skip and x.is_cuda:  # x feeds the depthwise conv and the skip (nn_ops.fork2)
             xd, x = nn_ops.fork2(x)
-            y = self._depthwise_conv(xd)
+            y = self._depthwise_conv(xd, st)
         else:
-            y = self._depthwise_conv(x)
+            y = self._depthwise_conv(x, st)
         y = ops.bn_swish_squeeze_excite(y, self._bn1, self._se_reduce, self._se_expand)
         if not self.skip:
-            return ops.bn_act(self._project_conv(y), self._bn2, None)
+            return ops.bn_act(self._project_conv(y, st), self._bn2, None)
         if drop_connect_rate and self.training:
             # bn2 -> x / keep * floor(keep + u) -> + inputs, fused into the BN kernels
             if dc_rand is None:
                 dc_rand = torch.rand(x.shape[0], dtype=x.dtype, device=x.device)
-            return ops.bn_act(self._project_conv(y), self._bn2, None, res=x, dc_rand=dc_rand,
+            return ops.bn_act(self._project_conv(y, st), self._bn2, None, res=x, dc_rand=dc_rand,
                               dc_keep=1.0 - drop_connect_rate)
-        return ops.bn_act(self._project_conv(y), self._bn2, None, res=x)  # fused skip add
+        return ops.bn_act(self._project_conv(y, st), self._bn2, None, res=x)  # fused skip add
 
 
 class EfficientNetTrunk(nn.Module):

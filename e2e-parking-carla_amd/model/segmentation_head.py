@@ -40,5 +40,6 @@ class SegmentationHead(nn.Module):
         b, c, s = t.shape
         x = self.top_down(t.reshape(b, c, int(math.sqrt(s)), -1))
         head = self.segmentation_head
-        x = ops.bn_act(ops.conv2d(x, head[0].weight, None, 1, 1), head[1], "relu")
+        x = ops.bn_act(ops.conv2d(x, head[0].weight, None, 1, 1, bn_stats=head[1].training),
+                       head[1], "relu")
         return ops.conv2d(x, head[3].weight, head[3].bias)

@@ -153,6 +153,18 @@ int e2ep_target_bev(const float *target_point, const float *noise, int B, int X,
 size_t e2ep_conv_fwd_workspace(const int *dims);
 int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
                   int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream);
+/* e2ep_conv_fwd plus the batch statistics of y for the BatchNorm that follows the conv
+ * (MBConv _expand_conv -> _bn0, _project_conv -> _bn2; reference model/cam_encoder.py:69-82
+ * via efficientnet-pytorch): the epilogue writes, per output channel c and column tile t
+ * (tiles over the N*P*Q output pixels), the fp64 sum and sum of squares of the stored values
+ * into stats[(t * Cout + c) * 2 + {0, 1}] — the partials e2ep_bn_finalize_part reduces, so
+ * the BN layer never re-reads y for its statistics.  tiles = e2ep_conv_fwd_stats_tiles(dims,
+ * w_layout), which is 0 when the geometry's kernel takes no statistics (then stats must be
+ * NULL and the BN computes its own); stats_bytes >= Cout * tiles * 16.  Deterministic. */
+int e2ep_conv_fwd_stats_tiles(const int *dims, int w_layout);
+int e2ep_conv_fwd_stats(const float *x, const float *w, const float *bias, const int *dims, int act,
+                        int w_layout, float *y, void *workspace, size_t workspace_bytes,
+                        double *stats, size_t stats_bytes, void *stream);
 
 /* dx[N,m_channels,H,W] = conv_transpose(gout[N,Cout,P,Q], w) restricted to the first
  * m_channels input channels; split by input-pixel stride phase, so no zero taps at stride 2.
@@ -243,6 +255,27 @@ int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *
                   float *running_var, int N, int C, int H, int W, int train, float momentum,
                   float eps, float *mean, float *invstd, float *scale, float *shift,
                   void *workspace, size_t workspace_bytes, void *stream);
+/* 1 when the training forward of this shape takes the split path (a statistics pass over x,
+ * then the elementwise pass), 0 when it runs the single-launch kernel that keeps each channel
+ * in registers — where a producer's partial sums (e2ep_conv_fwd_stats) save nothing. */
+int e2ep_bn_fwd_split(int N, int C, int H, int W);
+/* Training statistics from a producer's partial sums (e2ep_conv_fwd_stats /
+ * e2ep_dwconv_fwd_stats): part[tiles][C][2] fp64 (sum, sum of squares) over the N*H*W elements
+ * of each channel, reduced in fixed order; writes mean / invstd / scale / shift [C] and updates
+ * the running stats as e2ep_bn_stats does.  One launch of C/8 workgroups reading whole
+ * 128-B lines (8 channels of one tile); e2ep_bn_finalize_part_workspace returns 0 today (the
+ * workspace arguments are kept for a split plan). */
+size_t e2ep_bn_finalize_part_workspace(int C, int tiles);
+int e2ep_bn_finalize_part(const double *part, int tiles, const float *gamma, const float *beta,
+                          float *running_mean, float *running_var, int N, int C, int H, int W,
+                          float momentum, float eps, float *mean, float *invstd, float *scale,
+                          float *shift, void *workspace, size_t workspace_bytes, void *stream);
+/* Elementwise half of e2ep_bn_fwd with the affine already folded: y = act(dc(x * scale[c] +
+ * shift[c]) + res) (scale / shift from e2ep_bn_finalize_part or e2ep_bn_stats; res, dc_rand,
+ * dc_keep, act as in e2ep_bn_fwd) — the same arithmetic as e2ep_bn_fwd's apply pass. */
+int e2ep_bn_apply(const float *x, const float *scale, const float *shift, const float *res,
+                  const float *dc_rand, float dc_keep, int N, int C, int H, int W, int act,
+                  float *y, void *stream);
 /* dx, dgamma, dbeta, dres (each nullable) from x, dy and the forward's mean/invstd; res and
  * dc_rand / dc_keep as in the forward (dres = gradient at the activation input).
  * gate_logit / gate_dpooled [N,C] (both or neither): the activation output fed a
@@ -422,6 +455,15 @@ int e2ep_resize_bwd_cl(const float *g, long long g_pstride, int N, int C, int Hi
  * gradient w.r.t. the transformed input (feed it to e2ep_bn_bwd with the same act). */
 int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float *in_scale,
                     const float *in_shift, int in_act, float *y, void *stream);
+/* e2ep_dwconv_fwd plus the batch statistics of y for the BatchNorm that follows (MBConv
+ * _depthwise_conv -> _bn1): per channel c and tile t (t = n * units + the output-row block
+ * of one wave), the fp64 sum and sum of squares of y into stats[(t * C + c) * 2 + {0, 1}]
+ * (e2ep_bn_finalize_part's input).  tiles = e2ep_dwconv_fwd_stats_tiles(dims), 0 when the
+ * geometry runs the generic kernel (then stats must be NULL); stats_bytes >= C * tiles * 16. */
+int e2ep_dwconv_fwd_stats_tiles(const int *dims);
+int e2ep_dwconv_fwd_stats(const float *x, const float *w, const int *dims, const float *in_scale,
+                          const float *in_shift, int in_act, float *y, double *stats,
+                          size_t stats_bytes, void *stream);
 int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream);
 size_t e2ep_dwconv_wgrad_workspace(const int *dims);
 int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,

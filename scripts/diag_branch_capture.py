@@ -9,8 +9,11 @@ replay compared with eager):
   toy_plain     torch ops: branch on a side stream, joined with wait_stream
   toy_record    the same, plus record_stream on the tensors crossing the streams
   toy_e2ep      the branch made of e2ep conv2d (whose backward forks its weight gradient)
+  toy_keep      toy_e2ep captured through e2ep_amd.graphs.capture (keep_graph=True, own exec)
   model_cam     the ParkingModel B=2 train step with streams branch "cam" only
   model_heads   the same with branch "heads" only
+  *_nofork      a model variant with the conv weight-gradient side streams off (no stream
+                forked from inside a branch)
 """
 import os
 import subprocess
@@ -18,7 +21,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "e2e-parking-carla_amd"), ROOT, os.path.join(ROOT, "tests")]
-VARIANTS = ["toy_plain", "toy_record", "toy_e2ep", "model_cam", "model_heads"]
+VARIANTS = os.environ.get("DIAG_VARIANTS", "toy_plain,toy_record,toy_e2ep,model_cam,model_heads").split(",")
 
 
 def toy(kind):
@@ -37,11 +40,11 @@ def toy(kind):
         if kind == "toy_record":
             x.record_stream(side)
         with torch.cuda.stream(side):
-            if kind == "toy_e2ep":
+            if kind in ("toy_e2ep", "toy_keep"):
                 b = conv.conv2d(x, w2, pad=(1, 1, 1, 1))
             else:
                 b = torch.nn.functional.conv2d(x, w2, padding=1)
-        a = conv.conv2d(x, w1, pad=(1, 1, 1, 1)) if kind == "toy_e2ep" else \
+        a = conv.conv2d(x, w1, pad=(1, 1, 1, 1)) if kind in ("toy_e2ep", "toy_keep") else \
             torch.nn.functional.conv2d(x, w1, padding=1)
         main.wait_stream(side)
         if kind == "toy_record":
@@ -59,9 +62,13 @@ def toy(kind):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     eager = step(), w1.grad.clone(), w2.grad.clone()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        out = step()
+    if kind == "toy_keep":  # the product's capture: keep_graph=True, memset repair, own exec
+        from e2ep_amd import graphs
+        g, out, _ = graphs.capture(step)
+    else:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = step()
     g.replay()
     torch.cuda.synchronize()
     same = torch.equal(out, eager[0]) and torch.equal(w1.grad, eager[1]) and torch.equal(w2.grad, eager[2])
@@ -70,9 +77,12 @@ def toy(kind):
 
 def model(kind):
     import torch
-    from e2ep_amd import streams, synthetic
+    from e2ep_amd import conv, streams, synthetic
     from e2ep_amd.train import TrainStep
     from test_train_step_b8_gpu import _module
+    if kind.endswith("_nofork"):  # no nested weight-gradient side streams inside the branch
+        conv.set_wgrad_overlap(False)
+        kind = kind[:-len("_nofork")]
     streams.set_enabled({"model_cam": ["cam"], "model_heads": ["heads"]}[kind])
     mod = _module()
     d = synthetic.synthetic_batch(8, seed=11)
@@ -89,13 +99,14 @@ def main():
         (toy if kind.startswith("toy") else model)(kind)
         return
     for kind in VARIANTS:
-        r = subprocess.run([sys.executable, "-u", __file__, kind], capture_output=True, text=True,
-                           timeout=300)
+        env = dict(os.environ, AMD_LOG_LEVEL="1")  # HIP runtime errors on stderr
+        r = subprocess.run([sys.executable, "-X", "faulthandler", "-u", __file__, kind],
+                           capture_output=True, text=True, timeout=300, env=env)
         tail = (r.stdout.strip().splitlines() or [""])[-1]
         print(f"{kind}: exit {r.returncode} {tail if r.returncode == 0 else ''}", flush=True)
         if r.returncode != 0:
-            err = [ln for ln in r.stderr.splitlines() if "File " in ln or "Error" in ln][-4:]
-            print("   ", " | ".join(err), flush=True)
+            for ln in r.stderr.splitlines()[-40:]:  # faulthandler's Python stack + HIP errors
+                print("   ", ln[:200], flush=True)
 
 
 if __name__ == "__main__":

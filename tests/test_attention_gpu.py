@@ -245,6 +245,7 @@ def test_split_backward_equals_serial(packed, causal, p):
     res = []
     for on in (False, True):
         prev = conv.set_wgrad_overlap(on)
+        prev_us = conv.set_fork_min_us(0)  # fork at this size too
         try:
             for t in (qb, kvb):
                 if t is not None:
@@ -254,6 +255,7 @@ def test_split_backward_equals_serial(packed, causal, p):
             res.append([t.grad.clone() for t in (qb, kvb) if t is not None])
         finally:
             conv.set_wgrad_overlap(prev)
+            conv.set_fork_min_us(prev_us)
     attention._SPLIT_BWD = split0
     for a, b in zip(*res):
         assert torch.equal(a, b)

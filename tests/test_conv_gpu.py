@@ -265,6 +265,7 @@ def test_side_stream_weight_gradient_equals_serial():
         return [t.grad.clone() for t in (x, w, b, lx, lw, lb)]
 
     prev = conv.set_wgrad_overlap(False)
+    prev_us = conv.set_fork_min_us(0)  # fork every layer, however small
     try:
         serial = run()
         conv.set_wgrad_overlap(True)
@@ -273,6 +274,7 @@ def test_side_stream_weight_gradient_equals_serial():
             assert all(torch.equal(a, c) for a, c in zip(got, serial))
     finally:
         conv.set_wgrad_overlap(prev)
+        conv.set_fork_min_us(prev_us)
 
 
 # k_conv_lp (csrc/conv_lp.hip): the bf16 / fp16 forward and data-gradient kernel, every conv
