@@ -222,14 +222,14 @@ __device__ __forceinline__ void bn_finalize_channel(
 }
 
 // Finalize from a producer's tile-major partials (bnstats.h: part[(tile * C + c) * 2]):
-// block = 8 channels x 32 tile groups (lane = tid % 8 -> channel c0 + lane, group = tid / 8):
+// block = 8 channels x 128 tile groups (lane = tid % 8 -> channel c0 + lane, group = tid / 8):
 // the 8 lanes of a group read one 128-B line per tile (channels c0 .. c0+7), group j sums tiles
-// j, j + 32, ...; the 32 group sums are added in group order through LDS, then the statistics
+// j, j + 128, ...; the group sums are added in group order through LDS, then the statistics
 // as bn_finalize_channel computes them.  grid = C / 8.  Fixed order: deterministic.  (A
 // two-level version that spread each channel's tiles over workgroups and handed the range
 // sums to the last-arriving one spent 12.7 us per launch on the hand-off's uncached loads.)
-constexpr int FT_CH = 8, FT_GROUPS = 32;
-__global__ void __launch_bounds__(256) k_bn_finalize_tiles(
+constexpr int FT_CH = 8, FT_GROUPS = 128;  // 1024 threads: a few loads per thread, all in flight
+__global__ void __launch_bounds__(FT_CH * FT_GROUPS) k_bn_finalize_tiles(
     const double *__restrict__ part, int tiles, int C, long long cnt, float eps, float momentum,
     float *__restrict__ running_mean, float *__restrict__ running_var,
     float *__restrict__ mean_out, float *__restrict__ invstd_out, const float *__restrict__ gamma,
@@ -249,9 +249,25 @@ __global__ void __launch_bounds__(256) k_bn_finalize_tiles(
   rs[grp][lane] = s;
   rq[grp][lane] = q;
   __syncthreads();
+  // fixed two-level order: groups j, j + 16, ..., j + 112 for j < 16, then the 16 in order
+  double s2 = 0.0, q2 = 0.0;
+  if (grp < 16) {
+    s2 = rs[grp][lane];
+    q2 = rq[grp][lane];
+    for (int j = grp + 16; j < FT_GROUPS; j += 16) {
+      s2 += rs[j][lane];
+      q2 += rq[j][lane];
+    }
+  }
+  __syncthreads();  // every thread: the first-level sums are read before they are overwritten
+  if (grp < 16) {
+    rs[grp][lane] = s2;
+    rq[grp][lane] = q2;
+  }
+  __syncthreads();
   if (grp != 0 || c >= C) return;
   double S = rs[0][lane], Q = rq[0][lane];
-  for (int j = 1; j < FT_GROUPS; ++j) {
+  for (int j = 1; j < 16; ++j) {
     S += rs[j][lane];
     Q += rq[j][lane];
   }
@@ -834,7 +850,7 @@ int e2ep_bn_finalize_part(const double *part, int tiles, const float *gamma, con
                "e2ep_bn_finalize_part: running_mean / running_var both or neither");
   (void)workspace;
   (void)workspace_bytes;
-  hipLaunchKernelGGL(k_bn_finalize_tiles, dim3(cdiv(C, FT_CH)), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(k_bn_finalize_tiles, dim3(cdiv(C, FT_CH)), dim3(FT_CH * FT_GROUPS), 0, as_stream(stream),
                      part, tiles, C, (long long)N * H * W, eps, momentum, running_mean, running_var,
                      mean, invstd, gamma, beta, scale, shift);
   return launch_status("e2ep_bn_finalize_part");

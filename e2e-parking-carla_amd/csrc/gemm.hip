@@ -45,27 +45,77 @@ constexpr int G_LDW = 36;  // LDS row stride in floats (32 k + 4 pad)
 // OP: MFMA operand precision, 0 = fp32 (v_mfma_f32_32x32x2_f32, exact), 1 = bf16 (BASELINE
 // C3: the fragments are rounded to bf16 when read from LDS, two v_mfma_f32_32x32x16_bf16 per
 // 32-deep step, products and sums fp32; HBM tensors stay fp32)
-template <bool AK, bool BKC, int WM, int TM, int TN, int AVEC, int BVEC, int OP = 0>
-__global__ void __launch_bounds__(256)
-    k_gemm(const float *__restrict__ A, int lda, long long a_bytes,
-           const float *__restrict__ B, int ldb, long long b_bytes,
-           const float *__restrict__ bias, int bias_rows, const float *__restrict__ Cadd,
-           int ldadd, float *__restrict__ C, long long c_bytes, int ldc, GemmCols cols, int M,
-           int N, int K, int kper, int relu, float *__restrict__ rs, float *__restrict__ part,
-           unsigned int *__restrict__ cnt) {
+// One GEMM problem of a launch: operands, epilogue inputs, its tile grid (gx column tiles x gy
+// row tiles x gz K splits) and split-K fold state.
+struct GemmArgs {
+  const float *A;
+  int lda;
+  long long a_bytes;
+  const float *B;
+  int ldb;
+  long long b_bytes;
+  const float *bias;
+  int bias_rows;
+  const float *Cadd;
+  int ldadd;
+  float *C;
+  long long c_bytes;
+  int ldc;
+  GemmCols cols;
+  int M, N, K, kper, relu;
+  float *rs, *part;
+  unsigned int *cnt;
+  int gx, gy, gz;
+};
+
+template <bool AK_, bool BKC_, int WM_, int TM_, int TN_, int AVEC_, int BVEC_, int OP_>
+struct GemmCfg {
+  static constexpr bool AK = AK_, BKC = BKC_;
+  static constexpr int WM = WM_, TM = TM_, TN = TN_, AVEC = AVEC_, BVEC = BVEC_, OP = OP_;
+  static constexpr int BM = 32 * TM * WM, BN = 32 * TN * (4 / WM);
+  static constexpr int LDS_FLOATS = 2 * (BM + BN) * G_LDW;  // As[2][BM][G_LDW], Bs[2][BN][G_LDW]
+};
+
+// The block body of k_gemm for block (bx, by, bz) of problem g; `lds` holds CFG::LDS_FLOATS
+// floats (16-B aligned) and s_last one int, both __shared__ of the calling kernel (so a kernel
+// running two problems, k_gemm_pair, shares one LDS allocation between them).
+template <class CFG>
+__device__ __forceinline__ void gemm_block(const GemmArgs &g, int bx, int by, int bz, float *lds,
+                                           int *s_last) {
+  constexpr bool AK = CFG::AK, BKC = CFG::BKC;
+  constexpr int WM = CFG::WM, TM = CFG::TM, TN = CFG::TN, AVEC = CFG::AVEC, BVEC = CFG::BVEC,
+                OP = CFG::OP;
+  const float *__restrict__ A = g.A;
+  const int lda = g.lda;
+  const long long a_bytes = g.a_bytes;
+  const float *__restrict__ B = g.B;
+  const int ldb = g.ldb;
+  const long long b_bytes = g.b_bytes;
+  const float *__restrict__ bias = g.bias;
+  const int bias_rows = g.bias_rows;
+  const float *__restrict__ Cadd = g.Cadd;
+  const int ldadd = g.ldadd;
+  float *__restrict__ C = g.C;
+  const long long c_bytes = g.c_bytes;
+  const int ldc = g.ldc;
+  const GemmCols cols = g.cols;
+  const int M = g.M, N = g.N, K = g.K, kper = g.kper, relu = g.relu;
+  float *__restrict__ rs = g.rs;
+  float *__restrict__ part = g.part;
+  unsigned int *__restrict__ cnt = g.cnt;
   // rs != null (only !AK, !BKC, unbatched): B gets a logical column N of ones, so column N of
   // the product is the row sum of A over k — rs[m] = sum_k A(m, k), the bias gradient of a
   // linear layer taken by its weight-gradient GEMM (no separate column-sum launches)
   constexpr int WN = 4 / WM;                      // waves along N
-  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+  constexpr int BM = CFG::BM, BN = CFG::BN;
   constexpr int GA = BM / 32, GB = BN / 32;       // 32-row load groups per operand tile
-  __shared__ __attribute__((aligned(16))) float As[2][BM][G_LDW];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN][G_LDW];
+  float(*As)[BM][G_LDW] = reinterpret_cast<float(*)[BM][G_LDW]>(lds);
+  float(*Bs)[BN][G_LDW] = reinterpret_cast<float(*)[BN][G_LDW]>(lds + 2 * BM * G_LDW);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wn = wave / WM;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int split = blockIdx.z;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int split = bz;
   const int ksteps = (K + G_BK - 1) / G_BK;
   const int kbeg = split * kper;
   const int kend = min(ksteps, kbeg + kper);
@@ -247,8 +297,7 @@ __global__ void __launch_bounds__(256)
   // every slab in split order (k_gemm_reduce's order) and runs the final epilogue below; with
   // no `cnt` k_gemm_reduce does that in a launch of its own.
   const int Nw = rs ? N + 1 : N;  // split-K partials carry the row-sum column
-  if (gridDim.z > 1) {
-    __shared__ int s_last;
+  if (g.gz > 1) {
     const long long MNw = (long long)M * Nw;
     const __amdgpu_buffer_rsrc_t rp = rsrc(part + split * MNw, 4LL * MNw);
 #pragma unroll
@@ -267,9 +316,9 @@ __global__ void __launch_bounds__(256)
     }
     if (!cnt) return;
     handoff_drain();
-    if (!handoff_arrive(cnt + blockIdx.x + gridDim.x * blockIdx.y, gridDim.z, &s_last)) return;
-    const __amdgpu_buffer_rsrc_t rall = rsrc(part, 4LL * gridDim.z * MNw);
-    for (int k = 0; k < (int)gridDim.z; ++k) {
+    if (!handoff_arrive(cnt + bx + g.gx * by, g.gz, s_last)) return;
+    const __amdgpu_buffer_rsrc_t rall = rsrc(part, 4LL * g.gz * MNw);
+    for (int k = 0; k < g.gz; ++k) {
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
         const int n = n0 + 32 * TN * wn + 32 * t + li;
@@ -325,6 +374,34 @@ __global__ void __launch_bounds__(256)
         if (rs) bstore(rrs, (rsc && m < M) ? m * 4 : OOR, v);
       }
     }
+  }
+}
+
+template <bool AK, bool BKC, int WM, int TM, int TN, int AVEC, int BVEC, int OP = 0>
+__global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
+  typedef GemmCfg<AK, BKC, WM, TM, TN, AVEC, BVEC, OP> CFG;
+  __shared__ __attribute__((aligned(16))) float lds[CFG::LDS_FLOATS];
+  __shared__ int s_last;
+  gemm_block<CFG>(g, blockIdx.x, blockIdx.y, blockIdx.z, lds, &s_last);
+}
+
+// Two independent GEMM problems in one launch (a linear layer's input gradient and its
+// weight + bias gradient, e2ep_linear_bwd): blocks [0, n1) run problem 1, the rest problem 2,
+// each with its own tile grid, splits and fold counters.  One launch instead of two on forked
+// streams: in a replayed graph a fork / join costs ~5 + ~10 us of idle GPU (scripts/
+// step_sequence.py), more than either product of the control decoder takes.
+template <class C1, class C2>
+__global__ void __launch_bounds__(256) k_gemm_pair(GemmArgs g1, GemmArgs g2) {
+  constexpr int L = C1::LDS_FLOATS > C2::LDS_FLOATS ? C1::LDS_FLOATS : C2::LDS_FLOATS;
+  __shared__ __attribute__((aligned(16))) float lds[L];
+  __shared__ int s_last;
+  const int n1 = g1.gx * g1.gy * g1.gz;
+  int id = blockIdx.x;
+  if (id < n1) {
+    gemm_block<C1>(g1, id % g1.gx, (id / g1.gx) % g1.gy, id / (g1.gx * g1.gy), lds, &s_last);
+  } else {
+    id -= n1;
+    gemm_block<C2>(g2, id % g2.gx, (id / g2.gx) % g2.gy, id / (g2.gx * g2.gy), lds, &s_last);
   }
 }
 
@@ -552,21 +629,18 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
   dim3 grid(cdiv(Nx, td.bn), cdiv(M, td.bm), p.splits);
   const int avec = vec_of(ak, lda, A), bvec = vec_of(bk, ldb, B);
   const int br = bias_rows ? 1 : 0;
+  const GemmArgs ga{A, lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, C, c_bytes, ldc,
+                    cols, M, N, K, p.kper, relu, rs, part, cnt, (int)grid.x, (int)grid.y,
+                    (int)grid.z};
 #define E2EP_GEMM_LAUNCH(AKV, BKV, WMV, TMV, TNV, AVV, BVV)                                     \
-  hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, TMV, TNV, AVV, BVV>), grid, dim3(256), 0, s, A, lda,  \
-                     a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, C, c_bytes, ldc, cols, M, \
-                     N, K, p.kper, relu, rs, part, cnt)
+  hipLaunchKernelGGL((k_gemm<AKV, BKV, WMV, TMV, TNV, AVV, BVV>), grid, dim3(256), 0, s, ga)
 #define E2EP_GEMM_T(AKV, BKV, AVV, BVV)                                     \
   do {                                                                      \
     if (g_gemm_precision == 1) { /* bf16: the automatic tiles */            \
       if (p.tile == 2)                                                      \
-        hipLaunchKernelGGL((k_gemm<AKV, BKV, 1, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, A, \
-                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, C, c_bytes, \
-                           ldc, cols, M, N, K, p.kper, relu, rs, part, cnt); \
+        hipLaunchKernelGGL((k_gemm<AKV, BKV, 1, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, ga); \
       else                                                                  \
-        hipLaunchKernelGGL((k_gemm<AKV, BKV, 2, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, A, \
-                           lda, a_bytes, B, ldb, b_bytes, bias, br, Cadd, ldadd, C, c_bytes, \
-                           ldc, cols, M, N, K, p.kper, relu, rs, part, cnt); \
+        hipLaunchKernelGGL((k_gemm<AKV, BKV, 2, 1, 1, AVV, BVV, 1>), grid, dim3(256), 0, s, ga); \
       break;                                                                \
     }                                                                       \
     switch (p.tile) {                                                       \
@@ -617,11 +691,108 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
   return 0;
 }
 
+// One problem of a k_gemm_pair launch: its plan, fold counters and arguments; false when the
+// pair kernel cannot take it (benchmark-forced tiles, or K splits without the in-launch fold).
+static bool gemm_prepare(const float *A, int lda, bool ak, long long a_bytes, const float *B,
+                         int ldb, bool bk, long long b_bytes, const float *Cadd, int ldadd,
+                         float *C, long long c_bytes, int ldc, int M, int N, int K,
+                         void *workspace, float *rs, GemmArgs &ga, int &wm, int &avec) {
+  const int Nx = rs ? N + 1 : N;
+  GemmLaunch p = gemm_plan(M, Nx, K);
+  if (g_gemm_precision == 1 && p.tile != 1 && p.tile != 2) p.tile = 1;
+  if (p.tile != 1 && p.tile != 2) return false;
+  if (p.splits > 1 && (!workspace || g_tune[TUNE_SPLITK_FOLD] != 2)) return false;
+  const GemmTile td = tile_dims(p.tile);
+  const int gx = cdiv(Nx, td.bn), gy = cdiv(M, td.bm);
+  unsigned int *cnt = p.splits > 1 ? handoff_slots(gx * gy) : nullptr;
+  ga = GemmArgs{A, lda, a_bytes, B, ldb, b_bytes, nullptr, 0, Cadd, ldadd, C, c_bytes, ldc,
+                GemmCols{0, 0, 0}, M, N, K, p.kper, 0, rs,
+                p.splits > 1 ? static_cast<float *>(workspace) : nullptr, cnt, gx, gy, p.splits};
+  wm = p.tile == 2 ? 1 : 2;  // tile 1: 64 x 64 (2 x 2 waves); tile 2: 32 x 128 (1 x 4)
+  avec = vec_of(ak, lda, A);
+  (void)bk;
+  return true;
+}
+
+// k_gemm_pair for (input gradient: A k-contiguous, B row-contiguous) + (weight gradient with
+// the row-sum column: both row-contiguous), dispatched over the tiles / vector width / precision
+template <int OP, int WM1, int AV1, int WM2>
+static void pair4(dim3 grid, hipStream_t s, const GemmArgs &g1, const GemmArgs &g2) {
+  hipLaunchKernelGGL((k_gemm_pair<GemmCfg<true, false, WM1, 1, 1, AV1, 0, OP>,
+                                  GemmCfg<false, false, WM2, 1, 1, 0, 0, OP>>),
+                     grid, dim3(256), 0, s, g1, g2);
+}
+template <int OP, int WM1, int AV1>
+static void pair3(int wm2, dim3 grid, hipStream_t s, const GemmArgs &g1, const GemmArgs &g2) {
+  if (wm2 == 2) pair4<OP, WM1, AV1, 2>(grid, s, g1, g2);
+  else pair4<OP, WM1, AV1, 1>(grid, s, g1, g2);
+}
+template <int OP, int WM1>
+static void pair2(int av1, int wm2, dim3 grid, hipStream_t s, const GemmArgs &g1, const GemmArgs &g2) {
+  if (av1 == 2) pair3<OP, WM1, 2>(wm2, grid, s, g1, g2);
+  else if (av1 == 1) pair3<OP, WM1, 1>(wm2, grid, s, g1, g2);
+  else pair3<OP, WM1, 0>(wm2, grid, s, g1, g2);
+}
+template <int OP>
+static void pair1(int wm1, int av1, int wm2, dim3 grid, hipStream_t s, const GemmArgs &g1,
+                  const GemmArgs &g2) {
+  if (wm1 == 2) pair2<OP, 2>(av1, wm2, grid, s, g1, g2);
+  else pair2<OP, 1>(av1, wm2, grid, s, g1, g2);
+}
+
 }  // namespace e2ep
 
 using namespace e2ep;
 
 extern "C" {
+
+int e2ep_linear_bwd(const float *dy, int ldy, const float *x, int ldx, const float *w, int ldw,
+                    const float *gskip, int ldskip, float *dx, int lddx, float *dw, int lddw,
+                    float *db, int M, int N, int K, void *ws_dx, size_t ws_dx_bytes, void *ws_dw,
+                    size_t ws_dw_bytes, void *stream) {
+  E2EP_REQUIRE(dy && x && w && dx && dw && db && M > 0 && N > 0 && K > 0, E2EP_EINVAL,
+               "e2ep_linear_bwd: bad arguments M=%d N=%d K=%d", M, N, K);
+  E2EP_REQUIRE(ldy >= N && ldx >= K && ldw >= K && lddx >= K && lddw >= K &&
+                   (!gskip || ldskip >= K),
+               E2EP_EINVAL, "e2ep_linear_bwd: leading dimension too small");
+  const size_t need_dx = gemm_ws(M, K, N), need_dw = gemm_ws(N, K + 1, M);
+  E2EP_REQUIRE((!need_dx || (ws_dx && ws_dx_bytes >= need_dx)) &&
+                   (!need_dw || (ws_dw && ws_dw_bytes >= need_dw)),
+               E2EP_EINVAL, "e2ep_linear_bwd: workspaces %zu / %zu bytes < %zu / %zu "
+               "(e2ep_gemm_workspace(M, K, N) / e2ep_gemm_rowsum_workspace(N, K, M))",
+               ws_dx_bytes, ws_dw_bytes, need_dx, need_dw);
+  const long long y_bytes = 4LL * ((long long)(M - 1) * ldy + N);
+  const long long x_bytes = 4LL * ((long long)(M - 1) * ldx + K);
+  const long long w_bytes = 4LL * ((long long)(N - 1) * ldw + K);
+  const long long dx_bytes = 4LL * ((long long)(M - 1) * lddx + K);
+  const long long dw_bytes = 4LL * ((long long)(N - 1) * lddw + K);
+  E2EP_REQUIRE(y_bytes < 0x7fffffffLL && x_bytes < 0x7fffffffLL && w_bytes < 0x7fffffffLL &&
+                   dx_bytes < 0x7fffffffLL && dw_bytes < 0x7fffffffLL &&
+                   4LL * N * (K + 1) * 8 < 0x7fffffffLL,
+               E2EP_ERANGE, "e2ep_linear_bwd: operand larger than 2 GB");
+  hipStream_t s = as_stream(stream);
+  // dX[M][K] = dY[M][N] W[N][K] (+ gskip);  dW[N][K] = dY^T X with db[N] = row sums of dY^T
+  GemmArgs g1, g2;
+  int wm1, av1, wm2, av2;
+  if (g_force_tile == 0 &&
+      gemm_prepare(dy, ldy, true, y_bytes, w, ldw, false, w_bytes, gskip, ldskip, dx, dx_bytes,
+                   lddx, M, K, N, ws_dx, nullptr, g1, wm1, av1) &&
+      gemm_prepare(dy, ldy, false, y_bytes, x, ldx, false, x_bytes, nullptr, 0, dw, dw_bytes,
+                   lddw, N, K, M, ws_dw, db, g2, wm2, av2)) {
+    const dim3 grid(g1.gx * g1.gy * g1.gz + g2.gx * g2.gy * g2.gz);
+    if (g_gemm_precision == 1) pair1<1>(wm1, av1, wm2, grid, s, g1, g2);
+    else pair1<0>(wm1, av1, wm2, grid, s, g1, g2);
+    return launch_status("e2ep_linear_bwd");
+  }
+  // fallback (benchmark-forced tiles, folds off): the two launches in order on one stream
+  int rc = gemm_run(dy, ldy, true, y_bytes, w, ldw, false, w_bytes, nullptr, false, gskip, ldskip,
+                    dx, dx_bytes, lddx, GemmCols{0, 0, 0}, M, K, N, 0, ws_dx, s, nullptr);
+  if (rc) return rc;
+  rc = gemm_run(dy, ldy, false, y_bytes, x, ldx, false, x_bytes, nullptr, false, nullptr, 0, dw,
+                dw_bytes, lddw, GemmCols{0, 0, 0}, N, K, M, 0, ws_dw, s, db);
+  if (rc) return rc;
+  return launch_status("e2ep_linear_bwd");
+}
 
 int e2ep_gemm_force(int tile, int splits, int unused) {
   (void)unused;

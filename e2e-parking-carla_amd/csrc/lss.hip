@@ -359,7 +359,11 @@ __global__ void __launch_bounds__(NG * 16) k_lss_fwd(
     float *tile_l = tile + 4 * lg * TP;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     // point codes are prefetched one 16-point batch ahead (branch-free loads, so the
-    // compiler can leave the prefetch in flight)
+    // compiler can leave the prefetch in flight).  (A deeper pipeline — codes two batches and
+    // feature rows one 8-point step ahead — took 102 VGPRs: C4 111.6 -> 104.8 us but C2 37.7 ->
+    // 49.4 us; the backward with all of a pixel's gathers issued together and the next pixel
+    // prefetched, 117 VGPRs: 58 -> 63 us (C2), 153 -> 158 us (C4); profiles/r04/
+    // lss_pipeline_ab.txt.  Fewer resident waves cost more than the deeper prefetch saved.)
     const __amdgpu_buffer_rsrc_t ro_ = rsrc(order + (long long)b * P, 4LL * P);
     int code_n = bload_i(ro_, ks + lg < ke ? (ks + lg) * 4 : OOR);
     for (int k0 = ks; k0 < ke; k0 += 16) {

@@ -129,6 +129,7 @@ SIGNATURES = {
     "e2ep_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _p, _i, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "e2ep_gemm_rowsum_workspace": (_sz, [_i, _i, _i]),
     "e2ep_gemm_rowsum": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _p, _sz, _p]),
+    "e2ep_linear_bwd": (_i, [_p, _i, _p, _i, _p, _i, _p, _i, _p, _i, _p, _i, _p, _i, _i, _i, _p, _sz, _p, _sz, _p]),
     "e2ep_decode_frames": (_i, [_p, _p, _p, _i64, _i, _p, _p, _p]),
     "e2ep_widen_u8_i64": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_depth_bce_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _p]),

@@ -2,6 +2,7 @@
 resize.hip, dwconv.hip, pool.hip).  Each forward enqueues on torch's current HIP stream;
 each backward is the matching e2ep gradient kernel (no PyTorch arithmetic)."""
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -871,6 +872,10 @@ class _Linear(torch.autograd.Function):
         return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None
 
 
+# E2EP_LINEAR_PAIR=0: a linear backward as two launches on forked streams (A/B timing)
+_PAIR = [os.environ.get("E2EP_LINEAR_PAIR", "1") != "0"]
+
+
 def _linear_bwd(g2, x2, weight, want_x, want_w, want_b, gskip=None, dw=None, db=None):
     """Gradients of y2 = x2 W^T + b from g2 = dY2 (M x N): dX2 = g2 W (+ gskip in the
     epilogue), dW = g2^T x2 with db = row sums of g2^T in the same launch (e2ep_gemm_rowsum),
@@ -878,6 +883,27 @@ def _linear_bwd(g2, x2, weight, want_x, want_w, want_b, gskip=None, dw=None, db=
     M, K = x2.shape
     N = weight.shape[0]
     dx = None
+    if want_x and want_w and want_b and _PAIR[0]:
+        # all three in one launch (e2ep_linear_bwd: k_gemm_pair), no side-stream fork / join
+        if dw is None:
+            dw = torch.empty(N, K, dtype=torch.float32, device=g2.device)
+        if db is None:
+            db = torch.empty(N, dtype=torch.float32, device=g2.device)
+        cadd = gskip.reshape(M, K) if gskip is not None else None
+        if cadd is not None and cadd.stride(1) != 1:
+            cadd = cadd.contiguous()
+        dx = torch.empty(M, K, dtype=torch.float32, device=g2.device)
+        lib = _lib.load()
+        wsx = _ws(lib.e2ep_gemm_workspace(M, K, N), g2.device)
+        wsw = _ws(lib.e2ep_gemm_rowsum_workspace(N, K, M), g2.device)
+        w2 = weight if weight.stride(1) == 1 else weight.contiguous()
+        with timing.region(timing.name("gemm", (M, N, K), "linear_bwd_pair"), 4.0 * M * N * K):
+            _lib.call("e2ep_linear_bwd", _lib.ptr(g2), g2.stride(0), _lib.ptr(x2), x2.stride(0),
+                      _lib.ptr(w2), w2.stride(0), _lib.ptr(cadd),
+                      cadd.stride(0) if cadd is not None else 0, _lib.ptr(dx), dx.stride(0),
+                      _lib.ptr(dw), dw.stride(0), _lib.ptr(db), M, N, K, _lib.ptr(wsx),
+                      _lib.nbytes(wsx), _lib.ptr(wsw), _lib.nbytes(wsw), _lib.stream())
+        return dx, dw, db
     # weight / bias gradients on the side stream, concurrent with the input gradient
     # (conv._Fork: every buffer allocated here, on the current stream, before the fork)
     fork = None

@@ -668,6 +668,19 @@ size_t e2ep_gemm_rowsum_workspace(int M, int N, int K);
 int e2ep_gemm_rowsum(const float *A, int lda, const float *B, int ldb, float *C, int ldc,
                      float *rowsum, int M, int N, int K, void *workspace,
                      size_t workspace_bytes, void *stream);
+/* A linear layer's backward in one launch (k_gemm_pair): dx[M][K] = dy[M][N] w[N][K] (+ gskip,
+ * nullable, a residual gradient in dx's layout) and dw[N][K] = dy^T x[M][K] with db[N] = the
+ * row sums of dy^T (the bias gradient) — the two products of e2ep_gemm / e2ep_gemm_rowsum,
+ * their blocks sharing one grid instead of two launches on forked streams (a fork / join of a
+ * replayed HIP graph idles the GPU ~15 us, longer than either product of the control decoder).
+ * Replaces nn.Linear's backward in the transformer layers (model/feature_fusion.py:13-14,
+ * model/control_predict.py:19-20).  Workspaces: ws_dx of e2ep_gemm_workspace(M, K, N) bytes,
+ * ws_dw of e2ep_gemm_rowsum_workspace(N, K, M) bytes (either may be NULL when that query is 0).
+ * Results are bitwise those of the two separate launches. */
+int e2ep_linear_bwd(const float *dy, int ldy, const float *x, int ldx, const float *w, int ldw,
+                    const float *gskip, int ldskip, float *dx, int lddx, float *dw, int lddw,
+                    float *db, int M, int N, int K, void *ws_dx, size_t ws_dx_bytes, void *ws_dw,
+                    size_t ws_dw_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Frame decode (dataset/carla_dataset.py:114-131, :494-515, :404-406): the per-step

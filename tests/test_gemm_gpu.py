@@ -250,3 +250,73 @@ def test_short_workspace_is_rejected():
         _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws), nb - 4,
                   _lib.ptr(dw), 0, _lib.stream())
     torch.cuda.synchronize()
+
+
+# (rows M, out N, in K): the control decoder (B = 8: 112 rows; 14 tokens x 8), the fusion
+# encoder (2048 rows), the FFN, odd shapes that split K and pad every tile edge
+PAIR_SHAPES = [(112, 258, 258), (112, 774, 258), (112, 2048, 258), (112, 258, 2048),
+               (2048, 258, 258), (2048, 2048, 258), (97, 130, 333), (33, 64, 1500)]
+
+
+@pytest.mark.parametrize("shape", PAIR_SHAPES, ids=[str(s) for s in PAIR_SHAPES])
+@pytest.mark.parametrize("skip", [False, True])
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_linear_bwd_pair_bitwise_equals_two_launches(shape, skip, prec):
+    """e2ep_linear_bwd (dX, dW and db in one k_gemm_pair launch) == e2ep_gemm + e2ep_gemm_rowsum
+    launched separately, bit for bit, for fp32 and bf16 operands; and close to fp64."""
+    from e2ep_amd import _lib, nn_ops, precision
+    M, N, K = shape
+    g = torch.Generator().manual_seed(M + N + K)
+    dy = torch.randn(M, N, generator=g).to(DEV)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    gs = torch.randn(M, K, generator=g).to(DEV) if skip else None
+    lib = _lib.load()
+    with precision.use(prec):
+        dx = torch.empty(M, K, device=DEV)
+        dw = torch.empty(N, K, device=DEV)
+        db = torch.empty(N, device=DEV)
+        wsx = torch.empty(max(16, lib.e2ep_gemm_workspace(M, K, N)), dtype=torch.uint8, device=DEV)
+        wsw = torch.empty(max(16, lib.e2ep_gemm_rowsum_workspace(N, K, M)), dtype=torch.uint8, device=DEV)
+        _lib.call("e2ep_linear_bwd", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(w), K, _lib.ptr(gs),
+                  K if skip else 0, _lib.ptr(dx), K, _lib.ptr(dw), K, _lib.ptr(db), M, N, K,
+                  _lib.ptr(wsx), _lib.nbytes(wsx), _lib.ptr(wsw), _lib.nbytes(wsw), _lib.stream())
+        dx2 = nn_ops.gemm(dy, True, w, False, M, K, N, cadd=gs)
+        dw2 = torch.empty(N, K, device=DEV)
+        db2 = torch.empty(N, device=DEV)
+        _lib.call("e2ep_gemm_rowsum", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(dw2), K, _lib.ptr(db2),
+                  N, K, M, _lib.ptr(wsw), _lib.nbytes(wsw), _lib.stream())
+        torch.cuda.synchronize()
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2) and torch.equal(db, db2)
+    if prec == "fp32":
+        want_dx = dy.double() @ w.double() + (gs.double() if skip else 0)
+        assert rel_l2(dx, want_dx) < 2e-6
+        assert rel_l2(dw, dy.double().t() @ x.double()) < 2e-6
+        assert rel_l2(db, dy.double().sum(0)) < 2e-6
+
+
+def test_linear_bwd_pair_fallback_with_forced_tiles():
+    """With a benchmark-forced tile the pair falls back to two launches on one stream: same
+    results."""
+    from e2ep_amd import _lib
+    M, N, K = 112, 258, 258
+    g = torch.Generator().manual_seed(4)
+    dy, x = torch.randn(M, N, generator=g).to(DEV), torch.randn(M, K, generator=g).to(DEV)
+    w = torch.randn(N, K, generator=g).to(DEV)
+    lib = _lib.load()
+    outs = []
+    for forced in (False, True):
+        if forced:
+            _lib.call("e2ep_gemm_force", 4, 1, 0)
+        try:
+            dx, dw, db = torch.empty(M, K, device=DEV), torch.empty(N, K, device=DEV), torch.empty(N, device=DEV)
+            wsx = torch.empty(max(16, lib.e2ep_gemm_workspace(M, K, N)), dtype=torch.uint8, device=DEV)
+            wsw = torch.empty(max(16, lib.e2ep_gemm_rowsum_workspace(N, K, M)), dtype=torch.uint8, device=DEV)
+            _lib.call("e2ep_linear_bwd", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(w), K, None, 0,
+                      _lib.ptr(dx), K, _lib.ptr(dw), K, _lib.ptr(db), M, N, K, _lib.ptr(wsx),
+                      _lib.nbytes(wsx), _lib.ptr(wsw), _lib.nbytes(wsw), _lib.stream())
+            outs.append((dx, dw, db))
+        finally:
+            _lib.call("e2ep_gemm_force", 0, 0, 0)
+    for a, b in zip(*outs):
+        assert rel_l2(a, b.double()) < 2e-6
