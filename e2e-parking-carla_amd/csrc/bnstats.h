@@ -74,13 +74,13 @@ __device__ __forceinline__ void bns_store_tile_n(const double (&bs)[NI][16],
   }
 }
 
-// one 32-row block per wave (k_conv_gemm), tile = blockIdx.x
+// one 32-row block per wave (k_conv_gemm)
 __device__ __forceinline__ void bns_store_tile(const double (&bs)[16], const double (&bq)[16],
                                                int wm, int wn, int nwn, int bmt, int m0, int M,
-                                               double *red, double *__restrict__ stats) {
+                                               int tile, double *red, double *__restrict__ stats) {
   const double(&b1)[1][16] = reinterpret_cast<const double(&)[1][16]>(bs);
   const double(&q1)[1][16] = reinterpret_cast<const double(&)[1][16]>(bq);
-  bns_store_tile_n<1>(b1, q1, 32 * wm, wn, nwn, bmt, m0, M, blockIdx.x, red, stats);
+  bns_store_tile_n<1>(b1, q1, 32 * wm, wn, nwn, bmt, m0, M, tile, red, stats);
 }
 
 }  // namespace e2ep

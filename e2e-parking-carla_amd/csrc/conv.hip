@@ -51,13 +51,18 @@ constexpr int MAXPH = 4;
 // OP (0 fp32 / 1 bf16 / 2 fp16) as for k_conv_gemm2 below: for low precision one 16-deep MFMA
 // per K-step takes lane half h's k = 8h .. 8h+7 (eight LDS reads per operand, as the eight
 // fp32 MFMAs would do).
-// ST (forward only): the epilogue also writes BatchNorm partial sums into `stats` (bnstats.h);
-// a separate instantiation, so the plain forward keeps its register allocation.
-template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0, bool ST = false>
-__global__ void __launch_bounds__(256, 2) k_conv_gemm(
+template <int BNT, int BMT>
+constexpr int conv_gemm_lds_floats() { return 2 * BK * (BMT + PADA) + 2 * BK * (BNT + PADB); }
+
+// The block body of k_conv_gemm for block (bx, by, bz) of a grid gx blocks wide; `lds` holds
+// conv_gemm_lds_floats<BNT, BMT>() floats of the caller's __shared__ memory (so a kernel can run
+// two problems in one grid: k_conv_bwd_pair).
+template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP, bool ST>
+__device__ __forceinline__ void conv_gemm_block(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
-    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
+    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats, int bx,
+    int by, int bz, int gx, float *lds) {
   // block tile BMT x BNT: BMT = 64 -> 2 x 2 waves of 32 x BNT/2; BMT = 32 (small-M layers:
   // Cout or Cin 24..56) -> 1 x 4 waves of 32 x BNT/4, so no MFMA rows are padding
   constexpr int WC = BMT == 64 ? BNT / 2 : BNT / 4;  // columns per wave
@@ -65,16 +70,16 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
   constexpr int BROWS = 256 / BNT;  // B rows per pass (1, 2 or 4)
   constexpr int BPER = BK / BROWS;  // B loads per thread (16, 8 or 4)
   constexpr int NA = BK * BMT / 256;  // A loads per thread (4 or 2)
-  __shared__ float As[2][BK][BMT + PADA];
-  __shared__ float Bs[2][BK][BNT + PADB];
+  float(*As)[BK][BMT + PADA] = reinterpret_cast<float(*)[BK][BMT + PADA]>(lds);
+  float(*Bs)[BK][BNT + PADB] = reinterpret_cast<float(*)[BK][BNT + PADB]>(lds + 2 * BK * (BMT + PADA));
   __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
   __shared__ int s_ntaps;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = BMT == 64 ? (wave & 1) : 0, wn = BMT == 64 ? (wave >> 1) : wave;
-  const int m0 = blockIdx.y * BMT, n0 = blockIdx.x * BNT;
-  const int split = blockIdx.z % splits, z = blockIdx.z / splits;
+  const int m0 = by * BMT, n0 = bx * BNT;
+  const int split = bz % splits, z = bz / splits;
   const int RS = g.R * g.S;
 
   // phase / pixel space of the columns
@@ -315,7 +320,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
     }
     if (!cnt) return;
     handoff_drain();
-    if (!handoff_arrive(cnt + blockIdx.x + gridDim.x * blockIdx.y, splits, &s_last)) return;
+    if (!handoff_arrive(cnt + bx + gx * by, splits, &s_last)) return;
     const __amdgpu_buffer_rsrc_t rall = rsrc(part, 4LL * splits * MN);
 #pragma unroll
     for (int t = 0; t < NACC; ++t)
@@ -387,8 +392,21 @@ __global__ void __launch_bounds__(256, 2) k_conv_gemm(
       bs[r] = fs[r];
       bq[r] = fq[r];
     }
-    bns_store_tile(bs, bq, wm, wn, BMT == 64 ? 2 : 4, BMT, m0, M, s_bn, stats);
+    bns_store_tile(bs, bq, wm, wn, BMT == 64 ? 2 : 4, BMT, m0, M, bx, s_bn, stats);
   }
+}
+
+// ST (forward only): the epilogue also writes BatchNorm partial sums into `stats` (bnstats.h);
+// a separate instantiation, so the plain forward keeps its register allocation.
+template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0, bool ST = false>
+__global__ void __launch_bounds__(256, 2) k_conv_gemm(
+    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
+    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) float lds[conv_gemm_lds_floats<BNT, BMT>()];
+  conv_gemm_block<MODE, ACT, BNT, BMT, AV, OP, ST>(w, src, bias, dst, dst_bytes, g, M, splits,
+                                                   kper, part, cnt, stats, blockIdx.x, blockIdx.y,
+                                                   blockIdx.z, gridDim.x, lds);
 }
 
 // split-K reduction (fixed order) + bias / relu epilogue:
@@ -872,12 +890,16 @@ __global__ void __launch_bounds__(256, 2) k_conv_wgrad(
 // ------------------------------------------------------------------------------------------
 constexpr int W2K = 32, W2LD = 36;
 
+constexpr int W2_LDS_FLOATS = 2 * 2 * 64 * W2LD;  // As[2][64][W2LD] (co x pixel), Bs likewise
+
+// The block body of k_conv_wgrad2 for block (bx, by, bz) of a grid with gz splits; `lds` holds
+// W2_LDS_FLOATS floats (16-B aligned) of the caller's __shared__ memory (k_conv_bwd_pair).
 template <int OP>
-__global__ void __launch_bounds__(256) k_conv_wgrad2(
+__device__ __forceinline__ void conv_wgrad2_block(
     const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
-    ConvGeom g, int pix_per_split, TapList tl) {
-  __shared__ __attribute__((aligned(16))) float As[2][64][W2LD];  // As[co][pixel]
-  __shared__ __attribute__((aligned(16))) float Bs[2][64][W2LD];  // Bs[column][pixel]
+    ConvGeom g, int pix_per_split, TapList tl, int bx, int by, int bz, int gz, float *lds) {
+  float(*As)[64][W2LD] = reinterpret_cast<float(*)[64][W2LD]>(lds);                 // As[co][pixel]
+  float(*Bs)[64][W2LD] = reinterpret_cast<float(*)[64][W2LD]>(lds + 2 * 64 * W2LD);  // Bs[column][pixel]
   __shared__ int s_tap[MAXTAPS];
   if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
   __syncthreads();
@@ -888,8 +910,8 @@ __global__ void __launch_bounds__(256) k_conv_wgrad2(
   const int RS = g.R * g.S;
   const int Kw = g.Cin * RS;    // columns of dW (ci-major, tap-minor)
   const int Kl = g.Cin * tl.n;  // live columns (ci, live tap index)
-  const int n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
-  const int split = blockIdx.z;
+  const int n0 = bx * 64, m0 = by * 64;
+  const int split = bz;
   const int PQ = g.P * g.Q;
   const int Ptot = g.N * PQ;
   const int pbeg = split * pix_per_split;  // a multiple of W2K
@@ -990,7 +1012,7 @@ __global__ void __launch_bounds__(256) k_conv_wgrad2(
       __syncthreads();
     }
   }
-  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
+  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gz * g.Cout * Kw);
   const int lcol = n0 + 32 * wn + li;
   const int lci = lcol < Kl ? lcol / tl.n : 0;
   const int col = lci * RS + s_tap[lcol < Kl ? lcol - lci * tl.n : 0];  // dW column
@@ -999,6 +1021,43 @@ __global__ void __launch_bounds__(256) k_conv_wgrad2(
     const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
     const bool ok = co < g.Cout && lcol < Kl;
     bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[rr]);
+  }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(256) k_conv_wgrad2(
+    const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
+    ConvGeom g, int pix_per_split, TapList tl) {
+  __shared__ __attribute__((aligned(16))) float lds[W2_LDS_FLOATS];
+  conv_wgrad2_block<OP>(gout, x, part, g, pix_per_split, tl, blockIdx.x, blockIdx.y, blockIdx.z,
+                        gridDim.z, lds);
+}
+
+// A conv layer's data gradient (k_conv_gemm MODE 1, fp32) and spatial / small-map weight
+// gradient (k_conv_wgrad2, fp32) in one grid: blocks [0, n1) run the data gradient, the rest
+// the weight gradient's split slabs (reduced by k_reduce_splits after the launch).  One launch
+// instead of two on forked streams (e2ep_conv_bwd): in a replayed graph a fork / join costs
+// ~5 + ~10 us of idle GPU, and the 16 x 16 / 32 x 32 layers' gradients take 20 - 50 us each.
+template <int BNT, int BMT>
+__global__ void __launch_bounds__(256, 2) k_conv_bwd_pair(
+    const float *__restrict__ w, const float *__restrict__ gout, const float *__restrict__ res,
+    float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
+    float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
+    const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
+    int gx2, int gy2, int gz2) {
+  constexpr int L1 = conv_gemm_lds_floats<BNT, BMT>();
+  constexpr int L = L1 > W2_LDS_FLOATS ? L1 : W2_LDS_FLOATS;
+  __shared__ __attribute__((aligned(16))) float lds[L];
+  const int n1 = gx1 * gy1 * gz1;
+  int id = blockIdx.x;
+  if (id < n1) {
+    conv_gemm_block<1, 0, BNT, BMT, false, 0, false>(w, gout, res, dx, dx_bytes, g, M, splits, kper,
+                                                     part1, cnt, nullptr, id % gx1,
+                                                     (id / gx1) % gy1, id / (gx1 * gy1), gx1, lds);
+  } else {
+    id -= n1;
+    conv_wgrad2_block<0>(gout, x, part2, g, pix_per_split, tl, id % gx2, (id / gx2) % gy2,
+                         id / (gx2 * gy2), gz2, lds);
   }
 }
 
@@ -2026,6 +2085,81 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
   const int n = g.Cout * g.Cin * g.R * g.S;
   reduce_splits(part, used, n, dw, accumulate, g.R * g.S, tl.mask, s);
   return launch_status("e2ep_conv_wgrad");
+}
+
+// The paired backward of e2ep_conv_bwd: the data gradient on fp32 k_conv_gemm with its final
+// epilogue in-launch (one split, or folded splits) and a tile k_conv_bwd_pair instantiates, the
+// weight gradient on fp32 k_conv_wgrad2.  Fills the data-gradient plan; false otherwise.
+static bool conv_bwd_pair_plan(ConvGeom &g, int m_channels, GemmPlan &p, TapList &tl) {
+  g.wlayout = 1;
+  g.korder = korder_of();
+  g.xcd = g_tune[TUNE_XCD] == 2;
+  if (g_conv_precision != 0 || !geom_ok(g) || m_channels <= 0 || m_channels > g.Cin) return false;
+  if (conv_route(1, g, m_channels) != ROUTE_GEMM) return false;
+  p = plan_gemm(1, g, m_channels);
+  if (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] != 2) return false;
+  const bool tile_ok = (p.bm == 64 && (p.bnt == 64 || p.bnt == 128)) ||
+                       (p.bm == 32 && (p.bnt == 128 || p.bnt == 256));
+  if (!tile_ok) return false;
+  if (lp_wgrad_selected() || wgrad1x1_ok(g)) return false;
+  if ((g.P * g.Q) % W2K != 0 || g_tune[TUNE_WGRAD_GEN] == 1) return false;
+  tl = live_taps(g);
+  return tl.n > 0;
+}
+
+int e2ep_conv_bwd_pair_ok(const int *dims, int m_channels) {
+  ConvGeom g = make_geom(dims);
+  GemmPlan p;
+  TapList tl;
+  return conv_bwd_pair_plan(g, m_channels, p, tl) ? 1 : 0;
+}
+
+int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *dims,
+                  int m_channels, const float *res, float *dx, void *ws_dgrad,
+                  size_t ws_dgrad_bytes, int wsplits, void *ws_wgrad, size_t ws_wgrad_bytes,
+                  float *dw, void *stream) {
+  ConvGeom g = make_geom(dims);
+  GemmPlan p;
+  TapList tl;
+  E2EP_REQUIRE(conv_bwd_pair_plan(g, m_channels, p, tl), E2EP_EINVAL,
+               "e2ep_conv_bwd: this geometry / setting has no paired backward "
+               "(e2ep_conv_bwd_pair_ok returned 0)");
+  E2EP_REQUIRE(gout && x && w && dx && dw && wsplits > 0, E2EP_EINVAL, "e2ep_conv_bwd: bad arguments");
+  const size_t need_d = gemm_workspace(p, m_channels);
+  E2EP_REQUIRE(!need_d || (ws_dgrad && ws_dgrad_bytes >= need_d), E2EP_EINVAL,
+               "e2ep_conv_bwd: data-gradient workspace %zu bytes < %zu", ws_dgrad_bytes, need_d);
+  E2EP_REQUIRE(ws_wgrad && ws_wgrad_bytes >= e2ep_conv_wgrad_workspace(dims, wsplits), E2EP_EINVAL,
+               "e2ep_conv_bwd: weight-gradient workspace %zu bytes < %zu for %d splits",
+               ws_wgrad_bytes, e2ep_conv_wgrad_workspace(dims, wsplits), wsplits);
+  hipStream_t s = as_stream(stream);
+  const int M = m_channels;
+  // data gradient grid (launch_gemm's), fold counters
+  const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
+  float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
+  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+  // weight gradient grid (e2ep_conv_wgrad's k_conv_wgrad2 path)
+  const int Ptot = g.N * g.P * g.Q;
+  int per = (Ptot + wsplits - 1) / wsplits;
+  per = (per + W2K - 1) / W2K * W2K;
+  const int used = (Ptot + per - 1) / per;
+  const dim3 g2(cdiv(g.Cin * tl.n, 64), cdiv(g.Cout, 64), used);
+  float *part2 = static_cast<float *>(ws_wgrad);
+  const dim3 grid(g1.x * g1.y * g1.z + g2.x * g2.y * g2.z);
+  const long long dx_bytes = 4LL * g.N * M * g.H * g.W;
+#define E2EP_PAIR(BNTV, BMTV)                                                                     \
+  hipLaunchKernelGGL((k_conv_bwd_pair<BNTV, BMTV>), grid, dim3(256), 0, s, w, gout, res, dx,      \
+                     dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, (int)g1.y,           \
+                     (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
+  if (p.bm == 64) {
+    if (p.bnt == 128) E2EP_PAIR(128, 64);
+    else E2EP_PAIR(64, 64);
+  } else {
+    if (p.bnt == 256) E2EP_PAIR(256, 32);
+    else E2EP_PAIR(128, 32);
+  }
+#undef E2EP_PAIR
+  reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
+  return launch_status("e2ep_conv_bwd");
 }
 
 size_t e2ep_col_sum_workspace(int rows, int C) {

@@ -50,6 +50,8 @@ SIGNATURES = {
     "e2ep_conv_wgrad_splits": (_i, [_p]),
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),
     "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _sz, _p, _i, _p]),
+    "e2ep_conv_bwd_pair_ok": (_i, [_p, _i]),
+    "e2ep_conv_bwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _sz, _i, _p, _sz, _p, _p]),
     "e2ep_bias_grad": (_i, [_p, _i, _i, _i, _p, _p]),
     "e2ep_col_sum_workspace": (_sz, [_i, _i]),
     "e2ep_col_sum": (_i, [_p, _i, _i, _p, _p, _p]),

@@ -252,6 +252,45 @@ class _Fork:
             self.main.wait_stream(self.side)
 
 
+# Both gradients of a conv layer in one launch (e2ep_conv_bwd, k_conv_bwd_pair) where the
+# geometry allows it (e2ep_conv_bwd_pair_ok): no fork / join, the two GEMMs' blocks still run
+# concurrently.  E2EP_CONV_PAIR=0 keeps the forked two-launch backward (A/B).
+_CONV_PAIR = [os.environ.get("E2EP_CONV_PAIR", "1") != "0"]
+
+
+def set_conv_pair(on):
+    """Enable / disable the one-launch conv backward (returns the previous setting)."""
+    prev = _CONV_PAIR[0]
+    _CONV_PAIR[0] = bool(on)
+    return prev
+
+
+def _conv_bwd_pair(gy, x, wt, dims, gc, gskip, wshape):
+    """(dx, dw) of a conv through e2ep_conv_bwd; dx as _Conv2d.backward's dgrad path builds it."""
+    N, Cin, H, W = dims[:4]
+    lib = _lib.load()
+    d = _lib.dims(dims)
+    dw = torch.empty(wshape, dtype=torch.float32, device=x.device)
+    splits = lib.e2ep_conv_wgrad_splits(d)
+    wsw = torch.empty(splits * dw.numel(), dtype=torch.float32, device=x.device)
+    wsd = _ws(lib.e2ep_conv_dgrad_workspace(d, gc), gy.device)
+    res = gskip.contiguous() if (gskip is not None and gc == Cin) else None
+    dxg = torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device)
+    with timing.region(_rname("conv_bwd", dims, f"gc{gc}"), conv_flops(dims, gc) + conv_flops(dims)):
+        _lib.call("e2ep_conv_bwd", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(wt), d, gc, _lib.ptr(res),
+                  _lib.ptr(dxg), _lib.ptr(wsd), _lib.nbytes(wsd), splits, _lib.ptr(wsw),
+                  _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream())
+    if gc == Cin:
+        dx = dxg
+    elif gskip is not None:  # channels past gc get only the skip gradient
+        dx = gskip.clone()
+        dx[:, :gc] += dxg
+    else:
+        dx = torch.zeros_like(x)
+        dx[:, :gc] = dxg
+    return dx, dw
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, dims, act, grad_channels, skip=False, stats=None):
@@ -285,6 +324,14 @@ class _Conv2d(torch.autograd.Function):
         dx = dw = db = None
         # weight / bias gradients on the side stream, concurrent with the data gradient
         want_w, want_b = ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2]
+        gc = ctx.gc or Cin
+        if want_w and ctx.needs_input_grad[0] and _CONV_PAIR[0] and \
+                _lib.load().e2ep_conv_bwd_pair_ok(_lib.dims(dims), gc):
+            dx, dw = _conv_bwd_pair(gy, x, wt, dims, gc, gskip, ctx.wshape)
+            if want_b:
+                db = torch.empty(Cout, dtype=torch.float32, device=x.device)
+                _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db), s)
+            return dx, dw, db, None, None, None, None, None
         fork = None
         if want_w or want_b:
             if want_w:  # allocated on the current stream (see _Fork)
@@ -301,7 +348,6 @@ class _Conv2d(torch.autograd.Function):
                     _lib.call("e2ep_bias_grad", _lib.ptr(gy), N, Cout, P * Q, _lib.ptr(db),
                               _lib.stream())
         if ctx.needs_input_grad[0]:
-            gc = ctx.gc or Cin
             res = gskip.contiguous() if (gskip is not None and gc == Cin) else None
             dxg = conv_dgrad(gy, wt, dims, gc, torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device),
                              w_layout=1, res=res)

@@ -180,6 +180,20 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
                         int w_layout, const float *res, float *dx, void *workspace,
                         size_t workspace_bytes, void *stream);
 
+/* A conv layer's backward in one launch (k_conv_bwd_pair): dx (e2ep_conv_dgrad_acc with res,
+ * w tap-major) and dw (e2ep_conv_wgrad with `wsplits`, accumulate 0), their blocks sharing one
+ * grid instead of two launches on forked streams (a fork / join of a replayed HIP graph idles
+ * the GPU ~15 us; the 16x16 / 32x32 layers' gradients take 20 - 50 us each), then the weight
+ * gradient's fixed-order split reduction.  Where e2ep_conv_bwd_pair_ok is 0 (low precision,
+ * the large-map kernels, the 1x1 weight-gradient path) the caller launches the two separately.
+ * Workspaces: e2ep_conv_dgrad_workspace(dims, m_channels), e2ep_conv_wgrad_workspace(dims,
+ * wsplits).  Results bitwise those of the two separate launches. */
+int e2ep_conv_bwd_pair_ok(const int *dims, int m_channels);
+int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *dims,
+                  int m_channels, const float *res, float *dx, void *ws_dgrad,
+                  size_t ws_dgrad_bytes, int wsplits, void *ws_wgrad, size_t ws_wgrad_bytes,
+                  float *dw, void *stream);
+
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of
  * e2ep_conv_wgrad_workspace bytes) are summed in a fixed order: deterministic. */

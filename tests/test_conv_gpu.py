@@ -401,3 +401,55 @@ def test_conv_lp_fp32_all_geometries(case, tile):
     assert rel_l2(y, y64) < 2e-6
     assert rel_l2(xd.grad, x64.grad) < 2e-6
     assert rel_l2(wd.grad, w64.grad) < 2e-6
+
+
+@pytest.mark.parametrize("case", CASES + [(2, 160, 8, 8, 960, 1, 1, 1, (0, 0, 0, 0), 1, False, 0),
+                                          (8, 256, 16, 16, 256, 3, 3, 1, (1, 1, 1, 1), 1, False, 1),
+                                          (8, 512, 8, 8, 512, 3, 3, 1, (1, 1, 1, 1), 1, True, 0)],
+                         ids=[str(i) for i in range(len(CASES) + 3)])
+@pytest.mark.parametrize("skip", [False, True], ids=["noskip", "skip"])
+def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip):
+    """e2ep_conv_bwd (data and weight gradient in one k_conv_bwd_pair launch, where
+    e2ep_conv_bwd_pair_ok) == e2ep_conv_dgrad_acc + e2ep_conv_wgrad on forked streams, bitwise,
+    with and without the skip gradient added in the data gradient's epilogue."""
+    from e2ep_amd import conv
+    N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
+    g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV)
+    w = (torch.randn(Cout, Cin, R, S, generator=g) / (Cin * R * S) ** 0.5).to(DEV)
+    b = torch.randn(Cout, generator=g).to(DEV) if has_b else None
+    gs = torch.randn(x.shape, generator=g).to(DEV) if skip else None
+
+    def run():
+        xd, wd = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        bd = b.clone().requires_grad_(True) if has_b else None
+        out = conv.conv2d(xd, wd, bd, (st, st), pad, (dil, dil), act, skip=skip)
+        y = out[0] if skip else out
+        gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).to(DEV)
+        loss = (y * gy).sum() + ((out[1] * gs).sum() if skip else 0)
+        loss.backward()
+        return [t.grad.clone() for t in (xd, wd, bd) if t is not None]
+
+    prev = conv.set_conv_pair(False)
+    try:
+        two = run()
+        conv.set_conv_pair(True)
+        one = run()
+    finally:
+        conv.set_conv_pair(prev)
+    assert all(torch.equal(a, c) for a, c in zip(one, two))
+
+
+def test_conv_bwd_pair_covers_small_map_layers():
+    """The EfficientNet 1x1 convs on 32x32 and smaller maps and the 16x16 heads' 1x1s take the
+    paired backward (their two GEMMs each fill a fraction of the chip) — a plan change that
+    drops them back to two forked launches shows up here."""
+    from e2ep_amd import _lib
+    lib = _lib.load()
+
+    def d1(N, C, H, W, Co):  # (N, Cin, H, W, Cout, R, S, P, Q, sh, sw, pt, pl, dh, dw)
+        return (N, C, H, W, Co, 1, 1, H, W, 1, 1, 0, 0, 1, 1)
+    layers = [d1(32, 192, 32, 32, 32), d1(32, 336, 16, 16, 56), d1(32, 1152, 8, 8, 192),
+              d1(32, 64, 16, 16, 160)]
+    ok = [lib.e2ep_conv_bwd_pair_ok(_lib.dims(d), d[1]) for d in layers]
+    assert all(ok), ok
