@@ -21,6 +21,11 @@ struct ConvGeom {
 // speed only, never for correctness); logical = the i-th block of that XCD's contiguous share
 // of the grid, so neighbouring tiles (shared input rows, shared gradient rows) meet in one XCD's
 // L2.  A bijection for any grid size.
+__device__ __forceinline__ int xcd_linear(int i, int total) {
+  const int q = total >> 3, r = total & 7, x = i & 7, j = i >> 3;
+  return x * q + min(x, r) + j;
+}
+
 __device__ __forceinline__ void xcd_block(bool on, int &bx, int &by, int &bz) {
   bx = blockIdx.x;
   by = blockIdx.y;
@@ -28,9 +33,7 @@ __device__ __forceinline__ void xcd_block(bool on, int &bx, int &by, int &bz) {
   if (!on) return;
   const int gx = gridDim.x, gy = gridDim.y;
   const int total = gx * gy * gridDim.z;
-  const int i = bx + gx * (by + gy * bz);
-  const int q = total >> 3, r = total & 7, x = i & 7, j = i >> 3;
-  const int L = x * q + min(x, r) + j;
+  const int L = xcd_linear(bx + gx * (by + gy * bz), total);
   bx = L % gx;
   by = (L / gx) % gy;
   bz = L / (gx * gy);
@@ -80,5 +83,15 @@ bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl);
 int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op);
 int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
                     int splits, float *part, hipStream_t s, int op);
+
+// A conv layer's data gradient on k_conv_lp (route ROUTE_LP / ROUTE_LP32 of conv.hip) and
+// weight gradient (op 1: k_wgrad_lp; op 0: the k_conv_wgrad2-equivalent 64 x 64 tile) in one
+// k_lp_bwd_pair launch (e2ep_conv_bwd).  lp_bwd_pair_launch returns the weight-gradient slabs
+// written to part2 (for the split reduction), -1 if the plan has no instantiated pair.
+bool lp_bwd_pair_ok(const ConvGeom &g, int M, int op, const TapList &tl);
+int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, float *dx,
+                       long long dx_bytes, const ConvGeom &g, int M, int op, void *ws_dgrad,
+                       const float *x, const TapList &tl, int wsplits, float *part2,
+                       hipStream_t s);
 
 }  // namespace e2ep

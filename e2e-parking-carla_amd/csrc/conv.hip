@@ -2087,31 +2087,42 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
   return launch_status("e2ep_conv_wgrad");
 }
 
-// The paired backward of e2ep_conv_bwd: the data gradient on fp32 k_conv_gemm with its final
-// epilogue in-launch (one split, or folded splits) and a tile k_conv_bwd_pair instantiates, the
-// weight gradient on fp32 k_conv_wgrad2.  Fills the data-gradient plan; false otherwise.
-static bool conv_bwd_pair_plan(ConvGeom &g, int m_channels, GemmPlan &p, TapList &tl) {
+// The paired backward of e2ep_conv_bwd, where the two-launch path's kernels have a paired
+// instantiation: PAIR_GEMM = fp32 k_conv_gemm data gradient (one split or folded splits) with
+// k_conv_wgrad2 (k_conv_bwd_pair); PAIR_LP = k_conv_lp data gradient (fp32 where TUNE_LP32
+// routes it, bf16 in C3) with the k_wgrad_lp / k_conv_wgrad2 weight gradient (k_lp_bwd_pair).
+enum PairKind { PAIR_NONE = 0, PAIR_GEMM = 1, PAIR_LP = 2 };
+static int conv_bwd_pair_plan(ConvGeom &g, int m_channels, GemmPlan &p, TapList &tl) {
   g.wlayout = 1;
   g.korder = korder_of();
   g.xcd = g_tune[TUNE_XCD] == 2;
-  if (g_conv_precision != 0 || !geom_ok(g) || m_channels <= 0 || m_channels > g.Cin) return false;
-  if (conv_route(1, g, m_channels) != ROUTE_GEMM) return false;
-  p = plan_gemm(1, g, m_channels);
-  if (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] != 2) return false;
-  const bool tile_ok = (p.bm == 64 && (p.bnt == 64 || p.bnt == 128)) ||
-                       (p.bm == 32 && (p.bnt == 128 || p.bnt == 256));
-  if (!tile_ok) return false;
-  if (lp_wgrad_selected() || wgrad1x1_ok(g)) return false;
-  if ((g.P * g.Q) % W2K != 0 || g_tune[TUNE_WGRAD_GEN] == 1) return false;
+  if (!geom_ok(g) || m_channels <= 0 || m_channels > g.Cin) return PAIR_NONE;
   tl = live_taps(g);
-  return tl.n > 0;
+  if (tl.n <= 0) return PAIR_NONE;
+  // the weight-gradient kernel e2ep_conv_wgrad would run
+  const bool wg_lp = lp_wgrad_selected() && lp_wgrad_ok(g, tl);
+  const bool wg_2 = !wg_lp && !wgrad1x1_ok(g) && (g.P * g.Q) % W2K == 0 &&
+                    g_tune[TUNE_WGRAD_GEN] != 1;
+  const int route = conv_route(1, g, m_channels);
+  if (g_conv_precision == 0 && route == ROUTE_GEMM && wg_2) {
+    p = plan_gemm(1, g, m_channels);
+    if (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] != 2) return PAIR_NONE;
+    const bool tile_ok = (p.bm == 64 && (p.bnt == 64 || p.bnt == 128)) ||
+                         (p.bm == 32 && (p.bnt == 128 || p.bnt == 256));
+    return tile_ok ? PAIR_GEMM : PAIR_NONE;
+  }
+  if (g_conv_precision == 0 && route == ROUTE_LP32 && wg_2)
+    return lp_bwd_pair_ok(g, m_channels, 0, tl) ? PAIR_LP : PAIR_NONE;
+  if (g_conv_precision == 1 && route == ROUTE_LP && wg_lp)
+    return lp_bwd_pair_ok(g, m_channels, 1, tl) ? PAIR_LP : PAIR_NONE;
+  return PAIR_NONE;
 }
 
 int e2ep_conv_bwd_pair_ok(const int *dims, int m_channels) {
   ConvGeom g = make_geom(dims);
   GemmPlan p;
   TapList tl;
-  return conv_bwd_pair_plan(g, m_channels, p, tl) ? 1 : 0;
+  return conv_bwd_pair_plan(g, m_channels, p, tl) != PAIR_NONE ? 1 : 0;
 }
 
 int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *dims,
@@ -2121,11 +2132,12 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
   ConvGeom g = make_geom(dims);
   GemmPlan p;
   TapList tl;
-  E2EP_REQUIRE(conv_bwd_pair_plan(g, m_channels, p, tl), E2EP_EINVAL,
+  const int kind = conv_bwd_pair_plan(g, m_channels, p, tl);
+  E2EP_REQUIRE(kind != PAIR_NONE, E2EP_EINVAL,
                "e2ep_conv_bwd: this geometry / setting has no paired backward "
                "(e2ep_conv_bwd_pair_ok returned 0)");
   E2EP_REQUIRE(gout && x && w && dx && dw && wsplits > 0, E2EP_EINVAL, "e2ep_conv_bwd: bad arguments");
-  const size_t need_d = gemm_workspace(p, m_channels);
+  const size_t need_d = e2ep_conv_dgrad_workspace(dims, m_channels);
   E2EP_REQUIRE(!need_d || (ws_dgrad && ws_dgrad_bytes >= need_d), E2EP_EINVAL,
                "e2ep_conv_bwd: data-gradient workspace %zu bytes < %zu", ws_dgrad_bytes, need_d);
   E2EP_REQUIRE(ws_wgrad && ws_wgrad_bytes >= e2ep_conv_wgrad_workspace(dims, wsplits), E2EP_EINVAL,
@@ -2133,31 +2145,38 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
                ws_wgrad_bytes, e2ep_conv_wgrad_workspace(dims, wsplits), wsplits);
   hipStream_t s = as_stream(stream);
   const int M = m_channels;
-  // data gradient grid (launch_gemm's), fold counters
-  const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
-  float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
-  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
-  // weight gradient grid (e2ep_conv_wgrad's k_conv_wgrad2 path)
-  const int Ptot = g.N * g.P * g.Q;
-  int per = (Ptot + wsplits - 1) / wsplits;
-  per = (per + W2K - 1) / W2K * W2K;
-  const int used = (Ptot + per - 1) / per;
-  const dim3 g2(cdiv(g.Cin * tl.n, 64), cdiv(g.Cout, 64), used);
-  float *part2 = static_cast<float *>(ws_wgrad);
-  const dim3 grid(g1.x * g1.y * g1.z + g2.x * g2.y * g2.z);
   const long long dx_bytes = 4LL * g.N * M * g.H * g.W;
+  float *part2 = static_cast<float *>(ws_wgrad);
+  int used;
+  if (kind == PAIR_LP) {
+    used = lp_bwd_pair_launch(w, gout, res, dx, dx_bytes, g, M, g_conv_precision == 1 ? 1 : 0,
+                              ws_dgrad, x, tl, wsplits, part2, s);
+    E2EP_REQUIRE(used > 0, E2EP_EINVAL, "e2ep_conv_bwd: no paired k_conv_lp plan");
+  } else {
+    // data gradient grid (launch_gemm's), fold counters
+    const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
+    float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
+    unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+    // weight gradient grid (e2ep_conv_wgrad's k_conv_wgrad2 path)
+    const int Ptot = g.N * g.P * g.Q;
+    int per = (Ptot + wsplits - 1) / wsplits;
+    per = (per + W2K - 1) / W2K * W2K;
+    used = (Ptot + per - 1) / per;
+    const dim3 g2(cdiv(g.Cin * tl.n, 64), cdiv(g.Cout, 64), used);
+    const dim3 grid(g1.x * g1.y * g1.z + g2.x * g2.y * g2.z);
 #define E2EP_PAIR(BNTV, BMTV)                                                                     \
   hipLaunchKernelGGL((k_conv_bwd_pair<BNTV, BMTV>), grid, dim3(256), 0, s, w, gout, res, dx,      \
                      dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, (int)g1.y,           \
                      (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
-  if (p.bm == 64) {
-    if (p.bnt == 128) E2EP_PAIR(128, 64);
-    else E2EP_PAIR(64, 64);
-  } else {
-    if (p.bnt == 256) E2EP_PAIR(256, 32);
-    else E2EP_PAIR(128, 32);
-  }
+    if (p.bm == 64) {
+      if (p.bnt == 128) E2EP_PAIR(128, 64);
+      else E2EP_PAIR(64, 64);
+    } else {
+      if (p.bnt == 256) E2EP_PAIR(256, 32);
+      else E2EP_PAIR(128, 32);
+    }
 #undef E2EP_PAIR
+  }
   reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
   return launch_status("e2ep_conv_bwd");
 }

@@ -69,11 +69,16 @@ __device__ __forceinline__ f32x16 mfma16(typename LpType<OP>::T8 a, typename LpT
 // MODE 1 (data gradient): rows m = ci, K = (tap, co), src = g [N,Cout,P,Q], dst = dx
 //   [N,M,H,W]; phase z = (py, px) (blockIdx.z / splits) as in k_conv_gemm.
 // Block tile (64 WM) x (64 WN), 2 x 2 waves of (32 WM) x (32 WN).
+// The block body for block (bx, by, bz) of a grid gx blocks wide, its operand tiles in the
+// caller's LDS (As[2][BMT][LD], Bs[2][BNT][LD]): k_conv_lp, and the data-gradient half of
+// k_lp_bwd_pair.
 template <int MODE, int ACT, int WM, int WN, int OP, int LKS, bool ST = false>
-__global__ void __launch_bounds__(256) k_conv_lp(
+__device__ __forceinline__ void conv_lp_block(
     const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
     float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
-    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
+    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats, int bx,
+    int by, int bz, int gx, typename LpType<OP>::T (*As)[64 * WM][lld_of(OP, LKS)],
+    typename LpType<OP>::T (*Bs)[64 * WN][lld_of(OP, LKS)]) {
   typedef typename LpType<OP>::T T;
   typedef typename LpType<OP>::T8 T8;
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
@@ -84,16 +89,12 @@ __global__ void __launch_bounds__(256) k_conv_lp(
   constexpr int LD = lld_of(OP, LKS);
   static_assert(OP != 0 || (WN <= 2 && LKS == 32), "fp32: 32-deep steps, tiles up to 128 x 128");
   static_assert(LKS == 32 || LKS == 64, "K step 32 or 64");
-  __shared__ __attribute__((aligned(16))) T As[2][BMT][LD];
-  __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LD];
   __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
   __shared__ int s_ntaps;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
-  int bx, by, bz;
-  xcd_block(g.xcd != 0, bx, by, bz);
   const int m0 = by * BMT, n0 = bx * BNT;
   const int split = bz % splits, z = bz / splits;
 
@@ -356,7 +357,7 @@ __global__ void __launch_bounds__(256) k_conv_lp(
     }
     if (!cnt) return;
     handoff_drain();
-    if (!handoff_arrive(cnt + bx + gridDim.x * by, splits, &s_last)) return;
+    if (!handoff_arrive(cnt + bx + gx * by, splits, &s_last)) return;
     const __amdgpu_buffer_rsrc_t rall = rsrc(part, 4LL * splits * MN);
 #pragma unroll
     for (int i = 0; i < WM; ++i)
@@ -439,6 +440,21 @@ __global__ void __launch_bounds__(256) k_conv_lp(
       }
     bns_store_tile_n<WM>(bs, bq, 32 * WM * wm, wn, 2, BMT, m0, M, bx, s_bn, stats);
   }
+}
+
+template <int MODE, int ACT, int WM, int WN, int OP, int LKS, bool ST = false>
+__global__ void __launch_bounds__(256) k_conv_lp(
+    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
+    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
+  typedef typename LpType<OP>::T T;
+  constexpr int LD = lld_of(OP, LKS);
+  __shared__ __attribute__((aligned(16))) T As[2][64 * WM][LD];
+  __shared__ __attribute__((aligned(16))) T Bs[2][64 * WN][LD];
+  int bx, by, bz;
+  xcd_block(g.xcd != 0, bx, by, bz);
+  conv_lp_block<MODE, ACT, WM, WN, OP, LKS, ST>(w, src, bias, dst, dst_bytes, g, M, splits, kper,
+                                                 part, cnt, stats, bx, by, bz, gridDim.x, As, Bs);
 }
 
 // split-K reduction (fixed order) + bias / relu / residual epilogue:
@@ -671,11 +687,14 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // OP 0: the same GEMM on the exact-f32 MFMA with fp32 LDS rows (k_conv_lp's fp32 K order).
+// The block body for block (bx, by, bz) of a grid with gz pixel splits, its operand tiles in
+// the caller's LDS: k_wgrad_lp, and the weight-gradient half of k_lp_bwd_pair.
 template <int WM, int WN, int OP, int LKS>
-__global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout,
-                                                  const float *__restrict__ x,
-                                                  float *__restrict__ part, ConvGeom g,
-                                                  int pix_per_split, TapList tl) {
+__device__ __forceinline__ void wgrad_lp_block(
+    const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
+    ConvGeom g, int pix_per_split, TapList tl, int bx, int by, int bz, int gz,
+    typename LpType<OP == 0 ? 0 : 1>::T (*As)[64 * WM][lld_of(OP, LKS)],
+    typename LpType<OP == 0 ? 0 : 1>::T (*Bs)[64 * WN][lld_of(OP, LKS)]) {
   typedef typename LpType<OP == 0 ? 0 : 1>::T T;
   constexpr int LD = lld_of(OP, LKS);
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
@@ -685,8 +704,7 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   constexpr int PP = LKS / 2;              // B pixel pairs per step
   constexpr int CG = 256 / PP;             // B column groups
   constexpr int NBC = BNT / CG;            // B columns per thread
-  __shared__ __attribute__((aligned(16))) T As[2][BMT][LD];  // As[co][pixel]
-  __shared__ __attribute__((aligned(16))) T Bs[2][BNT][LD];  // Bs[column][pixel]
+  // As[co][pixel], Bs[column][pixel]
   __shared__ int s_tap[MAXTAPS];
   if (threadIdx.x < MAXTAPS) s_tap[threadIdx.x] = threadIdx.x < tl.n ? tl.tap[threadIdx.x] : 0;
   __syncthreads();
@@ -697,8 +715,6 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   const int RS = g.R * g.S;
   const int Kw = g.Cin * RS;    // columns of dW (ci-major, tap-minor)
   const int Kl = g.Cin * tl.n;  // live columns (ci, live tap index)
-  int bx, by, bz;
-  xcd_block(g.xcd != 0, bx, by, bz);
   const int n0 = bx * BNT, m0 = by * BMT;
   const int split = bz;
   const int PQ = g.P * g.Q;
@@ -837,7 +853,7 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
       __syncthreads();
     }
   }
-  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.z * g.Cout * Kw);
+  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gz * g.Cout * Kw);
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
     const int lcol = n0 + 32 * (WN * wn + j) + li;
@@ -852,6 +868,56 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
         bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[i][j][rr]);
       }
     }
+  }
+}
+
+template <int WM, int WN, int OP, int LKS>
+__global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout,
+                                                  const float *__restrict__ x,
+                                                  float *__restrict__ part, ConvGeom g,
+                                                  int pix_per_split, TapList tl) {
+  typedef typename LpType<OP == 0 ? 0 : 1>::T T;
+  constexpr int LD = lld_of(OP, LKS);
+  __shared__ __attribute__((aligned(16))) T As[2][64 * WM][LD];
+  __shared__ __attribute__((aligned(16))) T Bs[2][64 * WN][LD];
+  int bx, by, bz;
+  xcd_block(g.xcd != 0, bx, by, bz);
+  wgrad_lp_block<WM, WN, OP, LKS>(gout, x, part, g, pix_per_split, tl, bx, by, bz, gridDim.z, As, Bs);
+}
+
+// A conv layer's data gradient (k_conv_lp MODE 1) and weight gradient (k_wgrad_lp slabs) in
+// one grid: blocks [0, n1) run the data gradient, the rest the weight gradient (reduced by
+// k_reduce_splits after the launch).  One launch instead of two on forked streams
+// (e2ep_conv_bwd): in a replayed graph a fork / join idles the GPU ~15 us.  LDS: the larger
+// of the two halves' operand tiles, one buffer.  fp32 (OP 0) pairs the 64 x 64 weight-gradient
+// tile, whose K order and slabs are k_conv_wgrad2's (the kernel the two-launch fp32 path runs).
+template <int DWM, int DWN, int OP, int WWM, int WWN>
+__global__ void __launch_bounds__(256) k_lp_bwd_pair(
+    const float *__restrict__ w, const float *__restrict__ gout, const float *__restrict__ res,
+    float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
+    float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
+    const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
+    int gx2, int gy2, int gz2) {
+  typedef typename LpType<OP>::T T;
+  constexpr int LD = lld_of(OP, LK);
+  constexpr int L1 = 2 * 64 * (DWM + DWN) * LD, L2 = 2 * 64 * (WWM + WWN) * LD;
+  __shared__ __attribute__((aligned(16))) T lds[L1 > L2 ? L1 : L2];
+  const int n1 = gx1 * gy1 * gz1;
+  int id = blockIdx.x;
+  if (id < n1) {
+    if (g.xcd) id = xcd_linear(id, n1);
+    conv_lp_block<1, 0, DWM, DWN, OP, LK>(
+        w, gout, res, dx, dx_bytes, g, M, splits, kper, part1, cnt, nullptr, id % gx1,
+        (id / gx1) % gy1, id / (gx1 * gy1), gx1, reinterpret_cast<T(*)[64 * DWM][LD]>(lds),
+        reinterpret_cast<T(*)[64 * DWN][LD]>(lds + 2 * 64 * DWM * LD));
+  } else {
+    id -= n1;
+    const int n2 = gx2 * gy2 * gz2;
+    if (g.xcd) id = xcd_linear(id, n2);
+    wgrad_lp_block<WWM, WWN, OP, LK>(
+        gout, x, part2, g, pix_per_split, tl, id % gx2, (id / gx2) % gy2, id / (gx2 * gy2), gz2,
+        reinterpret_cast<T(*)[64 * WWM][LD]>(lds),
+        reinterpret_cast<T(*)[64 * WWN][LD]>(lds + 2 * 64 * WWM * LD));
   }
 }
 
@@ -926,6 +992,70 @@ int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const 
   else if (wn == 2) WL(1, 2);
   else WL(1, 1);
 #undef WL
+  return used;
+}
+
+// ---- paired backward (k_lp_bwd_pair) ------------------------------------------------------
+// Instantiated pairs: fp32 (op 0) 64 x 64 data-gradient tiles with the 64 x 64 weight-gradient
+// tile; bf16 (op 1) data-gradient tiles 64 x 64, 128 x 64 and 64 x 128 with weight-gradient
+// tiles 64 / 128 x 64 / 128, 32-deep K-steps on both (the plans' defaults).
+static bool lp_pair_tiles(const ConvGeom &g, int M, int op, const TapList &tl, LpPlan &p,
+                          int &wwm, int &wwn) {
+  p = lp_plan(1, g, M, op);
+  if (p.lk != LK || (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] != 2)) return false;
+  if (op == 0) {
+    wwm = wwn = 1;
+    return p.wm == 1 && p.wn == 1 && (g.P * g.Q) % LK == 0;
+  }
+  // not the 128 x 128 data-gradient tile: its ~200 VGPRs hold the whole paired grid to one
+  // workgroup per SIMD, and the weight-gradient blocks then run at a third of their occupancy
+  // (C3: 87 us paired against ~39 + 44 us overlapped on two streams)
+  if (op != 1 || p.wn > 2 || (p.wm == 2 && p.wn == 2) || !lp_wgrad_ok(g, tl) ||
+      lp_wgrad_lk(g, op) != LK)
+    return false;
+  lp_wgrad_tile(g, tl, wwm, wwn);
+  return true;
+}
+
+bool lp_bwd_pair_ok(const ConvGeom &g, int M, int op, const TapList &tl) {
+  LpPlan p;
+  int wwm, wwn;
+  return lp_pair_tiles(g, M, op, tl, p, wwm, wwn);
+}
+
+int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, float *dx,
+                       long long dx_bytes, const ConvGeom &g, int M, int op, void *ws_dgrad,
+                       const float *x, const TapList &tl, int wsplits, float *part2,
+                       hipStream_t s) {
+  LpPlan p;
+  int wwm, wwn;
+  if (!lp_pair_tiles(g, M, op, tl, p, wwm, wwn)) return -1;
+  const dim3 g1(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
+  float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
+  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+  const int Ptot = g.N * g.P * g.Q;
+  int per = (Ptot + wsplits - 1) / wsplits;
+  per = (per + LK - 1) / LK * LK;
+  const int used = (Ptot + per - 1) / per;
+  const dim3 g2(cdiv(g.Cin * tl.n, 64 * wwn), cdiv(g.Cout, 64 * wwm), used);
+  const dim3 grid(g1.x * g1.y * g1.z + g2.x * g2.y * g2.z);
+#define PAIR_L(DM, DN, OPV, WMV, WNV)                                                           \
+  hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV>), grid, dim3(256), 0, s, w, gout,    \
+                     res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x,           \
+                     (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
+#define PAIR_W(DM, DN)                                     \
+  do {                                                     \
+    if (wwm == 2 && wwn == 2) PAIR_L(DM, DN, 1, 2, 2);     \
+    else if (wwm == 2) PAIR_L(DM, DN, 1, 2, 1);            \
+    else if (wwn == 2) PAIR_L(DM, DN, 1, 1, 2);            \
+    else PAIR_L(DM, DN, 1, 1, 1);                          \
+  } while (0)
+  if (op == 0) PAIR_L(1, 1, 0, 1, 1);
+  else if (p.wm == 2) PAIR_W(2, 1);
+  else if (p.wn == 2) PAIR_W(1, 2);
+  else PAIR_W(1, 1);
+#undef PAIR_W
+#undef PAIR_L
   return used;
 }
 

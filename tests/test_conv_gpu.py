@@ -408,11 +408,13 @@ def test_conv_lp_fp32_all_geometries(case, tile):
                                           (8, 512, 8, 8, 512, 3, 3, 1, (1, 1, 1, 1), 1, True, 0)],
                          ids=[str(i) for i in range(len(CASES) + 3)])
 @pytest.mark.parametrize("skip", [False, True], ids=["noskip", "skip"])
-def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip):
-    """e2ep_conv_bwd (data and weight gradient in one k_conv_bwd_pair launch, where
-    e2ep_conv_bwd_pair_ok) == e2ep_conv_dgrad_acc + e2ep_conv_wgrad on forked streams, bitwise,
-    with and without the skip gradient added in the data gradient's epilogue."""
-    from e2ep_amd import conv
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode):
+    """e2ep_conv_bwd (data and weight gradient in one k_conv_bwd_pair / k_lp_bwd_pair launch,
+    where e2ep_conv_bwd_pair_ok) == e2ep_conv_dgrad_acc + e2ep_conv_wgrad on forked streams,
+    bitwise, with and without the skip gradient added in the data gradient's epilogue; fp32
+    (k_conv_gemm or k_conv_lp data gradient) and C3 bf16 operands (k_conv_lp + k_wgrad_lp)."""
+    from e2ep_amd import conv, precision
     N, Cin, H, W, Cout, R, S, st, pad, dil, has_b, act = case
     g = torch.Generator().manual_seed(hash(case) & 0xFFFF)
     x = torch.randn(N, Cin, H, W, generator=g).to(DEV)
@@ -432,9 +434,10 @@ def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip):
 
     prev = conv.set_conv_pair(False)
     try:
-        two = run()
-        conv.set_conv_pair(True)
-        one = run()
+        with precision.use(mode):
+            two = run()
+            conv.set_conv_pair(True)
+            one = run()
     finally:
         conv.set_conv_pair(prev)
     assert all(torch.equal(a, c) for a, c in zip(one, two))
@@ -453,3 +456,11 @@ def test_conv_bwd_pair_covers_small_map_layers():
               d1(32, 64, 16, 16, 160)]
     ok = [lib.e2ep_conv_bwd_pair_ok(_lib.dims(d), d[1]) for d in layers]
     assert all(ok), ok
+    # BEV encoder / head 3x3s: k_conv_lp data gradient (fp32 and C3 bf16)
+    from e2ep_amd import precision
+    d3 = [(32, 256, 16, 16, 256, 3, 3, 16, 16, 1, 1, 1, 1, 1, 1),
+          (32, 128, 32, 32, 128, 3, 3, 32, 32, 1, 1, 1, 1, 1, 1)]
+    for mode in ("fp32", "bf16"):
+        with precision.use(mode):
+            ok = [lib.e2ep_conv_bwd_pair_ok(_lib.dims(d), d[1]) for d in d3]
+        assert all(ok), (mode, ok)
