@@ -363,24 +363,26 @@ __device__ __forceinline__ double dw_wave_sum(double v) {
   return v;
 }
 
+// The block body for block blk of nblk (k_dw_fwd_strip, and the data-gradient half of
+// k_dw_bwd_pair), over the kernel's dynamic LDS.
 template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false>
-__global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
-                                                      const float *__restrict__ w, DwGeom g,
-                                                      DwStrip d, int units, float *__restrict__ y,
-                                                      DwIn tf, double *__restrict__ stats) {
+__device__ __forceinline__ void dw_fwd_strip_body(const float *__restrict__ x,
+                                                  const float *__restrict__ w, DwGeom g, DwStrip d,
+                                                  int units, float *__restrict__ y, DwIn tf,
+                                                  double *__restrict__ stats, int blk, int nblk) {
+  extern __shared__ float dw_lds[];
   // Grid-stride over units, software-pipelined like k_dw_wgrad_strip: the wave's next unit's
   // input rows are loaded into registers before the current unit's FMAs (one unit per wave
   // with stage / wait / compute in series ran at 1.7-3.5 TB/s).  The grid is capped at
   // e2ep_tune key 24 blocks, so each wave walks several units.
-  extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
   float *lds = dw_lds + wave * d.IR * d.WP;
   const int QL = g.Q >> 2;  // lanes per output row
   const int ro = lane / QL, ox0 = 4 * (lane - ro * QL);
   constexpr int NV = 3 * ST + K;
-  const int step = gridDim.x * 4;
-  int u = blockIdx.x * 4 + wave;  // wave-uniform
+  const int step = nblk * 4;
+  int u = blk * 4 + wave;  // wave-uniform
   int nc = 0, oy0 = 0;
   auto unit_of = [&](int un) {
     nc = un / d.units_per_plane;
@@ -439,6 +441,15 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
   }
 }
 
+template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false>
+__global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
+                                                      const float *__restrict__ w, DwGeom g,
+                                                      DwStrip d, int units, float *__restrict__ y,
+                                                      DwIn tf, double *__restrict__ stats) {
+  dw_fwd_strip_body<K, ST, FLIP, OFF, V, BS>(x, w, g, d, units, y, tf, stats, blockIdx.x,
+                                             gridDim.x);
+}
+
 // stride-2 data gradient over strip units: a wave owns RO = 64/(W/4) rows of dx of one plane,
 // each lane 4 adjacent dx pixels; the gy rows those rows read are staged in LDS.  For dx
 // pixel ix only taps b with (ix + pl - b) even contribute; ix0 is a multiple of 4, so the
@@ -491,15 +502,16 @@ __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restri
 // weight gradient partials over strip units: grid (C, splits); the block's waves walk the
 // channel's units (n, strip) of its slice; per lane K*K register accumulators, fixed-order
 // wave + block reduction.
+// The block body for channel c, split sp (k_dw_wgrad_strip, and the weight-gradient half of
+// k_dw_bwd_pair), over the kernel's dynamic LDS.
 template <int K, int ST, int OFF, int V>
-__global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
-                                                        const float *__restrict__ x, DwGeom g,
-                                                        DwStrip d, int splits,
-                                                        DwPart part, DwIn tf) {
+__device__ __forceinline__ void dw_wgrad_strip_body(const float *__restrict__ gy,
+                                                    const float *__restrict__ x, DwGeom g,
+                                                    DwStrip d, int splits, DwPart part, DwIn tf,
+                                                    int c, int sp) {
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
-  const int c = blockIdx.x, sp = blockIdx.y;
   float *lds = dw_lds + wave * d.IR * d.WP;
   const int cunits = g.N * d.units_per_plane;  // units of this channel
   const int per = (cunits + splits - 1) / splits;
@@ -575,6 +587,38 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
   // 1.5 - 2x slower; cdna_hip_programming.md Guideline 17)
   dw_wgrad_out<K * K>(part, c, sp, splits, (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]),
                       reinterpret_cast<int *>(&red[0][0]));
+}
+
+template <int K, int ST, int OFF, int V>
+__global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
+                                                        const float *__restrict__ x, DwGeom g,
+                                                        DwStrip d, int splits,
+                                                        DwPart part, DwIn tf) {
+  dw_wgrad_strip_body<K, ST, OFF, V>(gy, x, g, d, splits, part, tf, blockIdx.x, blockIdx.y);
+}
+
+// A stride-1 depthwise layer's data gradient (the flipped-filter strip forward over gy, gt /
+// dt its geometry) and weight gradient (strip partials, g / d) in one grid: block c + C * sp
+// (< nw = C * splits) the weight gradient of channel c, split sp, the nd blocks after them
+// walk the data-gradient units grid-stride.  The weight-gradient blocks go first: each walks
+// a channel's units of its split (tens per wave) and ends in a block reduction, the long
+// poles of the launch; queued behind the data-gradient blocks they ran last and serial
+// (67.5 us against 52 us for the weight gradient alone).  One launch instead of two on
+// forked streams (e2ep_dwconv_bwd): in a replayed graph the fork / join idles the GPU ~17 us
+// per layer.  Dynamic LDS: the larger of the two halves' per-wave row buffers.
+template <int K, int OFF, int VD, int VW>
+__global__ void __launch_bounds__(256) k_dw_bwd_pair(const float *__restrict__ gy,
+                                                     const float *__restrict__ w, DwGeom gt,
+                                                     DwStrip dt, int units, float *__restrict__ dx,
+                                                     int nd, const float *__restrict__ x, DwGeom g,
+                                                     DwStrip d, int splits, DwPart part, DwIn tf) {
+  const int b = blockIdx.x, nw = g.C * splits;
+  if (b < nw) {
+    dw_wgrad_strip_body<K, 1, OFF, VW>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
+  } else {
+    dw_fwd_strip_body<K, 1, true, OFF, VD>(gy, w, gt, dt, units, dx, DwIn{nullptr, nullptr, 0},
+                                           nullptr, b - nw, nd);
+  }
 }
 
 static int dw_splits(long long pixels, int C) {
@@ -816,6 +860,25 @@ static int dw_wgrad_splits(const DwGeom &g) {
   return dw_splits((long long)g.N * g.P * g.Q, g.C);
 }
 
+// The paired backward's plan (stride 1, both strip kernels, vector row reads with one OFF for
+// both halves: symmetric padding, K = 3 pad 1 -> 3, K = 5 pad 2 -> 2).
+static bool dw_bwd_pair_plan(const DwGeom &g, DwGeom &t, int &off) {
+  if (g.st != 1 || g_tune[TUNE_DW_VEC] == 1 || !dw_wgrad_strip_ok(g)) return false;
+  t = g;
+  t.H = g.P; t.W = g.Q; t.P = g.H; t.Q = g.W;
+  t.pt = g.K - 1 - g.pt; t.pl = g.K - 1 - g.pl;
+  if (!(dw_strip_ok(t) && t.pt >= 0 && t.pl >= 0 && t.pl <= DW_PADL)) return false;
+  off = dw_off(g.pl);
+  return off == dw_off(t.pl) && ((g.K == 3 && off == 3) || (g.K == 5 && off == 2));
+}
+
+int e2ep_dwconv_bwd_pair_ok(const int *dims) {
+  const DwGeom g = dw_geom(dims);
+  DwGeom t;
+  int off;
+  return (g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0 && dw_bwd_pair_plan(g, t, off)) ? 1 : 0;
+}
+
 size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
   DwGeom g = dw_geom(dims);
   return (size_t)g.C * dw_wgrad_splits(g) * g.K * g.K * sizeof(float);
@@ -848,6 +911,54 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
     hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0,
                        as_stream(stream), part.part, g.C, g.K * g.K, sp, dw);
   return launch_status("e2ep_dwconv_wgrad");
+}
+
+int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *dims,
+                    const float *in_scale, const float *in_shift, int in_act, float *dx,
+                    void *workspace, size_t workspace_bytes, float *dw, void *stream) {
+  const DwGeom g = dw_geom(dims);
+  DwGeom t;
+  int off;
+  E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0 && dw_bwd_pair_plan(g, t, off),
+               E2EP_EINVAL, "e2ep_dwconv_bwd: no paired backward for this geometry "
+               "(e2ep_dwconv_bwd_pair_ok returned 0)");
+  E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_dwconv_wgrad_workspace(dims), E2EP_EINVAL,
+               "e2ep_dwconv_bwd: workspace %zu bytes < %zu (e2ep_dwconv_wgrad_workspace)",
+               workspace_bytes, e2ep_dwconv_wgrad_workspace(dims));
+  E2EP_REQUIRE(!in_scale == !in_shift && in_act >= 0 && in_act <= 2, E2EP_EINVAL,
+               "e2ep_dwconv_bwd: in_scale / in_shift both or neither, in_act 0..2");
+  E2EP_REQUIRE(gy && x && w && dx && dw, E2EP_EINVAL, "e2ep_dwconv_bwd: null tensor");
+  const DwIn tf{in_scale, in_shift, in_act};
+  const DwStrip dt = dw_strip(t.K, 1, t.W, t.P, t.Q);
+  const int units = t.N * t.C * dt.units_per_plane;
+  const int nd = dw_fwd_blocks(units);
+  const int vd = cdiv(dt.IR * (t.W / 4), 64) <= 2 ? 2 : DW_MAXV;
+  const DwStrip d = dw_strip(g.K, 1, g.W, g.P, g.Q);
+  const int vw = cdiv(d.IR * (g.W / 4), 64) <= 2 ? 2 : DW_MAXV;
+  const int sp = dw_wgrad_splits(g);
+  DwPart part{static_cast<float *>(workspace), dw,
+              (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C) : nullptr};
+  const size_t shm = 4 * (size_t)std::max(dt.IR * dt.WP, d.IR * d.WP) * 4;
+  const dim3 grid(nd + g.C * sp);
+  hipStream_t s = as_stream(stream);
+#define DWP(KV, OFFV, VDV, VWV)                                                                   \
+  hipLaunchKernelGGL((k_dw_bwd_pair<KV, OFFV, VDV, VWV>), grid, dim3(256), shm, s, gy, w, t, dt, \
+                     units, dx, nd, x, g, d, sp, part, tf)
+#define DWP_V(KV, OFFV)                                  \
+  do {                                                   \
+    if (vd == 2 && vw == 2) DWP(KV, OFFV, 2, 2);         \
+    else if (vd == 2) DWP(KV, OFFV, 2, DW_MAXV);         \
+    else if (vw == 2) DWP(KV, OFFV, DW_MAXV, 2);         \
+    else DWP(KV, OFFV, DW_MAXV, DW_MAXV);                \
+  } while (0)
+  if (g.K == 3) DWP_V(3, 3);
+  else DWP_V(5, 2);
+#undef DWP_V
+#undef DWP
+  if (sp > 1 && !part.cnt)
+    hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0, s,
+                       part.part, g.C, g.K * g.K, sp, dw);
+  return launch_status("e2ep_dwconv_bwd");
 }
 
 }  // extern "C"

@@ -83,6 +83,8 @@ SIGNATURES = {
     "e2ep_dwconv_dgrad": (_i, [_p, _p, _p, _p, _p]),
     "e2ep_dwconv_wgrad_workspace": (_sz, [_p]),
     "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _i, _p, _sz, _p, _p]),
+    "e2ep_dwconv_bwd_pair_ok": (_i, [_p]),
+    "e2ep_dwconv_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _sz, _p, _p]),
     "e2ep_maxpool3s2_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p]),
     "e2ep_maxpool3s2_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_avgpool_fwd": (_i, [_p, _i, _i, _p, _p]),

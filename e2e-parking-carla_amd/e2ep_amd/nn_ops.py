@@ -237,6 +237,23 @@ def resize(x, size=None, scale_factor=None):
 
 # ------------------------------------------------------------------------------------------
 # depthwise conv
+# Both gradients of a stride-1 depthwise layer in one launch (e2ep_dwconv_bwd, k_dw_bwd_pair)
+# where e2ep_dwconv_bwd_pair_ok: no fork / join.  E2EP_DW_PAIR=0 keeps the forked two-launch
+# backward (A/B).
+_DW_PAIR = [os.environ.get("E2EP_DW_PAIR", "1") != "0"]
+
+
+def set_dw_pair(on):
+    """Enable / disable the one-launch depthwise backward (returns the previous setting)."""
+    prev = _DW_PAIR[0]
+    _DW_PAIR[0] = bool(on)
+    return prev
+
+
+def _dw_pairable(d):
+    return _DW_PAIR[0] and _lib.load().e2ep_dwconv_bwd_pair_ok(d) == 1
+
+
 # ------------------------------------------------------------------------------------------
 class _DwConv(torch.autograd.Function):
     @staticmethod
@@ -260,6 +277,13 @@ class _DwConv(torch.autograd.Function):
         d = _lib.dims(ctx.dims)
         s = _lib.stream()
         dx = dw = None
+        if ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and _dw_pairable(d):
+            dx, dw = torch.empty_like(x), torch.empty_like(w)
+            ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
+            with timing.region(timing.name("dwconv_bwd", gy.shape, "_DwConv")):
+                _lib.call("e2ep_dwconv_bwd", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(w), d, None, None, 0,
+                          _lib.ptr(dx), _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), s)
+            return dx, dw, None, None
         fork = None
         if ctx.needs_input_grad[1]:  # weight gradient on the side stream (conv._Fork)
             dw = torch.empty_like(w)
@@ -326,18 +350,29 @@ class _BnActDwConv(torch.autograd.Function):
         nig = ctx.needs_input_grad
         dw = dx = dg = db = None
         fork = None
-        if nig[9]:  # weight gradient on the side stream (conv._Fork)
+        want_t = nig[0] or nig[1] or nig[2]
+        paired = nig[9] and want_t and _dw_pairable(d)
+        if paired:  # both gradients in one launch
+            dw = torch.empty_like(w)
+            dt = torch.empty_like(x)  # gradient at the activation output
+            wsw = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
+            with timing.region(timing.name("dwconv_bwd", gy.shape, "_BnActDwConv")):
+                _lib.call("e2ep_dwconv_bwd", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(w), d,
+                          _lib.ptr(stats[2]), _lib.ptr(stats[3]), ctx.act, _lib.ptr(dt),
+                          _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), s)
+        elif nig[9]:  # weight gradient on the side stream (conv._Fork)
             dw = torch.empty_like(w)
             wsw = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
-            fork = conv._Fork(x.device, on=nig[0] or nig[1] or nig[2],
+            fork = conv._Fork(x.device, on=want_t,
                               work_us=conv.est_us(nbytes=4.0 * (x.numel() + gy.numel())))
             with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(stats[2]),
                           _lib.ptr(stats[3]), ctx.act, _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream())
-        if nig[0] or nig[1] or nig[2]:
-            dt = torch.empty_like(x)  # gradient at the activation output
-            with timing.region(timing.name("dwconv_dgrad", gy.shape, "_BnActDwConv")):
-                _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s)
+        if want_t:
+            if not paired:
+                dt = torch.empty_like(x)  # gradient at the activation output
+                with timing.region(timing.name("dwconv_dgrad", gy.shape, "_BnActDwConv")):
+                    _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s)
             dx = torch.empty_like(x) if nig[0] else None
             dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
             db = torch.empty_like(beta) if (beta is not None and nig[2]) else None

@@ -479,6 +479,16 @@ int e2ep_dwconv_fwd_stats(const float *x, const float *w, const int *dims, const
                           const float *in_shift, int in_act, float *y, double *stats,
                           size_t stats_bytes, void *stream);
 int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream);
+/* A stride-1 depthwise layer's backward in one launch (k_dw_bwd_pair): dx as
+ * e2ep_dwconv_dgrad, dw as e2ep_dwconv_wgrad (in_scale / in_shift / in_act: the input
+ * transform of the weight gradient's x, as there), their blocks sharing one grid instead of
+ * two launches on forked streams.  Where e2ep_dwconv_bwd_pair_ok is 0 the caller launches the
+ * two separately.  Workspace: e2ep_dwconv_wgrad_workspace.  Results bitwise those of the two
+ * separate launches. */
+int e2ep_dwconv_bwd_pair_ok(const int *dims);
+int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *dims,
+                    const float *in_scale, const float *in_shift, int in_act, float *dx,
+                    void *workspace, size_t workspace_bytes, float *dw, void *stream);
 size_t e2ep_dwconv_wgrad_workspace(const int *dims);
 int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
                       const float *in_shift, int in_act, void *workspace, size_t workspace_bytes,

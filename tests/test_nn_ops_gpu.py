@@ -198,6 +198,50 @@ def test_depthwise(case, variant):
             lib.e2ep_tune(24, prevb)
 
 
+@pytest.mark.parametrize("case", [(4, 48, 32, 32, 3, 1, (1, 1, 1, 1)), (2, 672, 16, 16, 5, 1, (2, 2, 2, 2)),
+                                  (2, 24, 128, 128, 3, 1, (1, 1, 1, 1)), (2, 32, 64, 64, 3, 1, (1, 1, 1, 1)),
+                                  (2, 40, 32, 32, 5, 1, (2, 2, 2, 2)), (3, 16, 16, 16, 3, 1, (1, 1, 1, 1)),
+                                  (2, 12, 24, 20, 5, 1, (2, 2, 2, 2)), (32, 192, 32, 32, 5, 1, (2, 2, 2, 2)),
+                                  (32, 96, 64, 64, 3, 1, (1, 1, 1, 1))])
+@pytest.mark.parametrize("fused", [False, True], ids=["dw", "bn_swish_dw"])
+def test_depthwise_bwd_pair_bitwise_equals_two_launches(case, fused):
+    """e2ep_dwconv_bwd (data and weight gradient in one k_dw_bwd_pair launch) == the forked
+    e2ep_dwconv_dgrad + e2ep_dwconv_wgrad, bitwise, for the plain depthwise conv and the
+    MBConv _bn0 -> swish -> depthwise form (the weight gradient's input transform)."""
+    from e2ep_amd import _lib, nn_ops, ops
+    N, C, H, W, K, s, pad = case
+    lib = _lib.load()
+    P, Q = (H + pad[2] + pad[3] - K) // s + 1, (W + pad[0] + pad[1] - K) // s + 1
+    assert lib.e2ep_dwconv_bwd_pair_ok(_lib.dims((N, C, H, W, K, P, Q, s, pad[2], pad[0]))) == 1
+    g = _g(C + H + 5)
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 0.5).to(DEV)
+    w = (torch.randn(C, 1, K, K, generator=g) / K).to(DEV)
+    dy = torch.randn(N, C, P, Q, generator=g).to(DEV)
+    bn = nn.BatchNorm2d(C, momentum=0.01, eps=1e-3).to(DEV)
+
+    def run():
+        xd, wd = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        bn.zero_grad()
+        if fused:
+            y = nn_ops.bn_act_depthwise_conv2d(xd, bn, "swish", wd, s, pad)
+        else:
+            y = ops.conv2d(xd, wd, None, s, pad, 1, groups=C)
+        y.backward(dy)
+        out = [xd.grad.clone(), wd.grad.clone()]
+        if fused:
+            out += [bn.weight.grad.clone(), bn.bias.grad.clone()]
+        return out
+
+    prev = nn_ops.set_dw_pair(False)
+    try:
+        two = run()
+        nn_ops.set_dw_pair(True)
+        one = run()
+    finally:
+        nn_ops.set_dw_pair(prev)
+    assert all(torch.equal(a, c) for a, c in zip(one, two))
+
+
 def _depthwise_case(ops, case):
     N, C, H, W, K, s, pad = case
     g = _g(C + H)
