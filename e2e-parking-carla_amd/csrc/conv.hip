@@ -1044,12 +1044,13 @@ __global__ void __launch_bounds__(256, 2) k_conv_bwd_pair(
     float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
     const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
-    int gx2, int gy2, int gz2) {
+    int gx2, int gy2, int gz2, int wfirst) {
   constexpr int L1 = conv_gemm_lds_floats<BNT, BMT>();
   constexpr int L = L1 > W2_LDS_FLOATS ? L1 : W2_LDS_FLOATS;
   __shared__ __attribute__((aligned(16))) float lds[L];
-  const int n1 = gx1 * gy1 * gz1;
-  int id = blockIdx.x;
+  const int n1 = gx1 * gy1 * gz1, n2 = gx2 * gy2 * gz2;
+  // wfirst: weight-gradient blocks [0, n2), then the data gradient's (e2ep_tune key 29)
+  int id = wfirst ? (blockIdx.x >= n2 ? blockIdx.x - n2 : n1 + blockIdx.x) : blockIdx.x;
   if (id < n1) {
     conv_gemm_block<1, 0, BNT, BMT, false, 0, false>(w, gout, res, dx, dx_bytes, g, M, splits, kper,
                                                      part1, cnt, nullptr, id % gx1,
@@ -2167,7 +2168,8 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
 #define E2EP_PAIR(BNTV, BMTV)                                                                     \
   hipLaunchKernelGGL((k_conv_bwd_pair<BNTV, BMTV>), grid, dim3(256), 0, s, w, gout, res, dx,      \
                      dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, (int)g1.y,           \
-                     (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
+                     (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z,           \
+                     g_tune[TUNE_PAIR_ORDER] == 2 ? 1 : 0)
     if (p.bm == 64) {
       if (p.bnt == 128) E2EP_PAIR(128, 64);
       else E2EP_PAIR(64, 64);

@@ -897,13 +897,15 @@ __global__ void __launch_bounds__(256) k_lp_bwd_pair(
     float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
     const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
-    int gx2, int gy2, int gz2) {
+    int gx2, int gy2, int gz2, int wfirst) {
   typedef typename LpType<OP>::T T;
   constexpr int LD = lld_of(OP, LK);
   constexpr int L1 = 2 * 64 * (DWM + DWN) * LD, L2 = 2 * 64 * (WWM + WWN) * LD;
   __shared__ __attribute__((aligned(16))) T lds[L1 > L2 ? L1 : L2];
   const int n1 = gx1 * gy1 * gz1;
-  int id = blockIdx.x;
+  // wfirst: weight-gradient blocks first (e2ep_tune key 29)
+  const int n2b = gx2 * gy2 * gz2;
+  int id = wfirst ? ((int)blockIdx.x >= n2b ? (int)blockIdx.x - n2b : n1 + (int)blockIdx.x) : (int)blockIdx.x;
   if (id < n1) {
     if (g.xcd) id = xcd_linear(id, n1);
     conv_lp_block<1, 0, DWM, DWN, OP, LK>(
@@ -1042,7 +1044,8 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, floa
 #define PAIR_L(DM, DN, OPV, WMV, WNV)                                                           \
   hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV>), grid, dim3(256), 0, s, w, gout,    \
                      res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x,           \
-                     (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
+                     (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z,   \
+                     g_tune[TUNE_PAIR_ORDER] == 2 ? 1 : 0)
 #define PAIR_W(DM, DN)                                     \
   do {                                                     \
     if (wwm == 2 && wwn == 2) PAIR_L(DM, DN, 1, 2, 2);     \

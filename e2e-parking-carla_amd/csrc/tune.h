@@ -32,7 +32,8 @@ enum Tune {
   TUNE_BNS_WIDE_LO = 26,      // the same for channels of 257..1024 float4: 2 = 512 threads x 1 / 2, 1 = 256 x 2 / 4
   TUNE_SE_FUSED = 27,         // squeeze-excitation MLP inside the squeeze / excite / da launches: 2 = on, 1 = separate kernels (default: measured 1.8 ms/step slower fused)
   TUNE_SPLITK_FOLD = 28,      // split-K reductions folded into the producing launch (last-arriving split sums): 2 = on, 1 = separate reduce kernels
-  TUNE_N = 29
+  TUNE_PAIR_ORDER = 29,       // conv paired backward (k_conv_bwd_pair, k_lp_bwd_pair): 2 = weight-gradient blocks first, 1 = data-gradient blocks first
+  TUNE_N = 30
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

@@ -409,7 +409,8 @@ def test_conv_lp_fp32_all_geometries(case, tile):
                          ids=[str(i) for i in range(len(CASES) + 3)])
 @pytest.mark.parametrize("skip", [False, True], ids=["noskip", "skip"])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
-def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode):
+@pytest.mark.parametrize("order", [1, 2], ids=["dgrad_first", "wgrad_first"])
+def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode, order):
     """e2ep_conv_bwd (data and weight gradient in one k_conv_bwd_pair / k_lp_bwd_pair launch,
     where e2ep_conv_bwd_pair_ok) == e2ep_conv_dgrad_acc + e2ep_conv_wgrad on forked streams,
     bitwise, with and without the skip gradient added in the data gradient's epilogue; fp32
@@ -432,7 +433,10 @@ def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode):
         loss.backward()
         return [t.grad.clone() for t in (xd, wd, bd) if t is not None]
 
+    from e2ep_amd import _lib
+    lib = _lib.load()
     prev = conv.set_conv_pair(False)
+    prev_order = lib.e2ep_tune(29, order)  # block order of the paired grid
     try:
         with precision.use(mode):
             two = run()
@@ -440,6 +444,7 @@ def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode):
             one = run()
     finally:
         conv.set_conv_pair(prev)
+        lib.e2ep_tune(29, prev_order)
     assert all(torch.equal(a, c) for a, c in zip(one, two))
 
 
