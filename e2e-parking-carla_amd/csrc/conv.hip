@@ -1116,18 +1116,19 @@ static int wgrad1x1_splits(const ConvGeom &g) {
   return wgrad1x1_splits_for(g, to, tc);
 }
 
+// The block body for tile bt of split `split`, its wave-sum tile in the caller's LDS
+// (red[TI * TJ * 16][64]): k_wgrad_1x1, and the weight-gradient half of k_conv_bwd_pair1x1.
 template <int TI, int TJ, int OP>
-__global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gout,
-                                                   const float *__restrict__ x,
-                                                   float *__restrict__ part, ConvGeom g,
-                                                   int splits, int groups_per_split) {
+__device__ __forceinline__ void wgrad1x1_block(const float *__restrict__ gout,
+                                               const float *__restrict__ x,
+                                               float *__restrict__ part, ConvGeom g, int splits,
+                                               int groups_per_split, int bt, int split,
+                                               float (*red)[64]) {
   // wave tile (32*TI co) x (32*TJ ci): TI*TJ accumulators share each loaded operand
   constexpr int NT = TI * TJ;
-  __shared__ float red[NT * 16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ntj = (g.Cin + 32 * TJ - 1) / (32 * TJ);
-  const int ti = blockIdx.x / ntj, tj = blockIdx.x - ti * ntj;
-  const int split = blockIdx.y;
+  const int ti = bt / ntj, tj = bt - ti * ntj;
   const int PQ = g.P * g.Q;
   const int ngroups = g.N * PQ / 8;  // 8-pixel groups (never straddle an image: PQ % 8 == 0)
   const int gb = split * groups_per_split;
@@ -1211,6 +1212,45 @@ __global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gou
     if (oc < g.Cout && ic < g.Cin) {
       part[((long long)split * g.Cout + oc) * Kw + ic] = red[tr][l];
     }
+  }
+}
+
+template <int TI, int TJ, int OP>
+__global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gout,
+                                                   const float *__restrict__ x,
+                                                   float *__restrict__ part, ConvGeom g,
+                                                   int splits, int groups_per_split) {
+  __shared__ float red[TI * TJ * 16][64];
+  wgrad1x1_block<TI, TJ, OP>(gout, x, part, g, splits, groups_per_split, blockIdx.x, blockIdx.y,
+                             red);
+}
+
+// A 1x1 conv layer's data gradient (k_conv_gemm MODE 1, fp32) and weight gradient (the
+// LDS-free k_wgrad_1x1 wave tiles: the large-map EfficientNet expand / project convs) in one
+// grid, as k_conv_bwd_pair; wfirst puts the weight-gradient blocks first (e2ep_tune key 30,
+// the default: each walks a long pixel range, the long poles of the launch; C2 22.73 -> 22.50
+// ms against data-gradient-first, profiles/r04/conv_pair1x1_ab.txt).
+template <int BNT, int BMT, int TI, int TJ>
+__global__ void __launch_bounds__(256, 2) k_conv_bwd_pair1x1(
+    const float *__restrict__ w, const float *__restrict__ gout, const float *__restrict__ res,
+    float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
+    float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
+    const float *__restrict__ x, float *__restrict__ part2, int splits2, int gps, int nt2,
+    int wfirst) {
+  constexpr int L1 = conv_gemm_lds_floats<BNT, BMT>();
+  constexpr int L2 = TI * TJ * 16 * 64;
+  __shared__ __attribute__((aligned(16))) float lds[L1 > L2 ? L1 : L2];
+  const int n1 = gx1 * gy1 * gz1, n2 = nt2 * splits2;
+  const int id = wfirst ? ((int)blockIdx.x >= n2 ? (int)blockIdx.x - n2 : n1 + (int)blockIdx.x)
+                        : (int)blockIdx.x;
+  if (id < n1) {
+    conv_gemm_block<1, 0, BNT, BMT, false, 0, false>(w, gout, res, dx, dx_bytes, g, M, splits, kper,
+                                                     part1, cnt, nullptr, id % gx1,
+                                                     (id / gx1) % gy1, id / (gx1 * gy1), gx1, lds);
+  } else {
+    const int j = id - n1;
+    wgrad1x1_block<TI, TJ, 0>(gout, x, part2, g, splits2, gps, j % nt2, j / nt2,
+                              reinterpret_cast<float(*)[64]>(lds));
   }
 }
 
@@ -2092,7 +2132,7 @@ int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int spli
 // instantiation: PAIR_GEMM = fp32 k_conv_gemm data gradient (one split or folded splits) with
 // k_conv_wgrad2 (k_conv_bwd_pair); PAIR_LP = k_conv_lp data gradient (fp32 where TUNE_LP32
 // routes it, bf16 in C3) with the k_wgrad_lp / k_conv_wgrad2 weight gradient (k_lp_bwd_pair).
-enum PairKind { PAIR_NONE = 0, PAIR_GEMM = 1, PAIR_LP = 2 };
+enum PairKind { PAIR_NONE = 0, PAIR_GEMM = 1, PAIR_LP = 2, PAIR_GEMM1X1 = 3 };
 static int conv_bwd_pair_plan(ConvGeom &g, int m_channels, GemmPlan &p, TapList &tl) {
   g.wlayout = 1;
   g.korder = korder_of();
@@ -2105,12 +2145,13 @@ static int conv_bwd_pair_plan(ConvGeom &g, int m_channels, GemmPlan &p, TapList 
   const bool wg_2 = !wg_lp && !wgrad1x1_ok(g) && (g.P * g.Q) % W2K == 0 &&
                     g_tune[TUNE_WGRAD_GEN] != 1;
   const int route = conv_route(1, g, m_channels);
-  if (g_conv_precision == 0 && route == ROUTE_GEMM && wg_2) {
+  const bool wg_1x1 = !wg_lp && wgrad1x1_ok(g);
+  if (g_conv_precision == 0 && route == ROUTE_GEMM && (wg_2 || wg_1x1)) {
     p = plan_gemm(1, g, m_channels);
     if (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] != 2) return PAIR_NONE;
     const bool tile_ok = (p.bm == 64 && (p.bnt == 64 || p.bnt == 128)) ||
                          (p.bm == 32 && (p.bnt == 128 || p.bnt == 256));
-    return tile_ok ? PAIR_GEMM : PAIR_NONE;
+    return tile_ok ? (wg_1x1 ? PAIR_GEMM1X1 : PAIR_GEMM) : PAIR_NONE;
   }
   if (g_conv_precision == 0 && route == ROUTE_LP32 && wg_2)
     return lp_bwd_pair_ok(g, m_channels, 0, tl) ? PAIR_LP : PAIR_NONE;
@@ -2153,6 +2194,41 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
     used = lp_bwd_pair_launch(w, gout, res, dx, dx_bytes, g, M, g_conv_precision == 1 ? 1 : 0,
                               ws_dgrad, x, tl, wsplits, part2, s);
     E2EP_REQUIRE(used > 0, E2EP_EINVAL, "e2ep_conv_bwd: no paired k_conv_lp plan");
+  } else if (kind == PAIR_GEMM1X1) {
+    const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
+    float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
+    unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+    // e2ep_conv_wgrad's k_wgrad_1x1 plan
+    const int groups = g.N * g.P * g.Q / 8;
+    const int gps = cdiv(groups, wsplits);
+    used = cdiv(groups, gps);
+    int to, tc;
+    wgrad1x1_tiles(g, to, tc);
+    const int nt2 = cdiv(g.Cout, to) * cdiv(g.Cin, tc);
+    const dim3 grid(g1.x * g1.y * g1.z + nt2 * used);
+    const int wfirst = g_tune[TUNE_PAIR1X1_ORDER] == 2 ? 1 : 0;
+#define E2EP_PAIR1(BNTV, BMTV, TIV, TJV)                                                          \
+  hipLaunchKernelGGL((k_conv_bwd_pair1x1<BNTV, BMTV, TIV, TJV>), grid, dim3(256), 0, s, w, gout,  \
+                     res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, (int)g1.y,  \
+                     (int)g1.z, x, part2, used, gps, nt2, wfirst)
+#define E2EP_PAIR1_W(BNTV, BMTV)                                          \
+  do {                                                                    \
+    if (to == 64 && tc == 64) E2EP_PAIR1(BNTV, BMTV, 2, 2);               \
+    else if (to == 64) E2EP_PAIR1(BNTV, BMTV, 2, 1);                      \
+    else if (tc == 64) E2EP_PAIR1(BNTV, BMTV, 1, 2);                      \
+    else E2EP_PAIR1(BNTV, BMTV, 1, 1);                                    \
+  } while (0)
+    if (p.bm == 64) {
+      if (p.bnt == 128) E2EP_PAIR1_W(128, 64);
+      else E2EP_PAIR1_W(64, 64);
+    } else {
+      if (p.bnt == 256) E2EP_PAIR1_W(256, 32);
+      else E2EP_PAIR1_W(128, 32);
+    }
+#undef E2EP_PAIR1_W
+#undef E2EP_PAIR1
+    reduce_splits(part2, used, g.Cout * g.Cin, dw, 0, 1, 1ULL, s);
+    return launch_status("e2ep_conv_bwd");
   } else {
     // data gradient grid (launch_gemm's), fold counters
     const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);

@@ -180,14 +180,16 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
                         int w_layout, const float *res, float *dx, void *workspace,
                         size_t workspace_bytes, void *stream);
 
-/* A conv layer's backward in one launch (k_conv_bwd_pair): dx (e2ep_conv_dgrad_acc with res,
- * w tap-major) and dw (e2ep_conv_wgrad with `wsplits`, accumulate 0), their blocks sharing one
- * grid instead of two launches on forked streams (a fork / join of a replayed HIP graph idles
- * the GPU ~15 us; the 16x16 / 32x32 layers' gradients take 20 - 50 us each), then the weight
- * gradient's fixed-order split reduction.  Where e2ep_conv_bwd_pair_ok is 0 (low precision,
- * the large-map kernels, the 1x1 weight-gradient path) the caller launches the two separately.
- * Workspaces: e2ep_conv_dgrad_workspace(dims, m_channels), e2ep_conv_wgrad_workspace(dims,
- * wsplits).  Results bitwise those of the two separate launches. */
+/* A conv layer's backward in one launch: dx (e2ep_conv_dgrad_acc with res, w tap-major) and
+ * dw (e2ep_conv_wgrad with `wsplits`, accumulate 0), their blocks sharing one grid instead of
+ * two launches on forked streams (a fork / join of a replayed HIP graph idles the GPU
+ * ~15 us; the small-map layers' gradients take 20 - 50 us each), then the weight gradient's
+ * fixed-order split reduction.  Kernels: k_conv_bwd_pair (fp32 k_conv_gemm data gradient +
+ * k_conv_wgrad2), k_conv_bwd_pair1x1 (+ the large-map k_wgrad_1x1), k_lp_bwd_pair (k_conv_lp
+ * data gradient, fp32 or C3 bf16, + k_wgrad_lp).  Where e2ep_conv_bwd_pair_ok is 0 (fp16,
+ * the large-map k_conv_gemm2 kernels, tiles without a paired instantiation) the caller
+ * launches the two separately.  Workspaces: e2ep_conv_dgrad_workspace(dims, m_channels),
+ * e2ep_conv_wgrad_workspace(dims, wsplits).  Results bitwise those of the two launches. */
 int e2ep_conv_bwd_pair_ok(const int *dims, int m_channels);
 int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *dims,
                   int m_channels, const float *res, float *dx, void *ws_dgrad,

@@ -409,7 +409,7 @@ def test_conv_lp_fp32_all_geometries(case, tile):
                          ids=[str(i) for i in range(len(CASES) + 3)])
 @pytest.mark.parametrize("skip", [False, True], ids=["noskip", "skip"])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
-@pytest.mark.parametrize("order", [1, 2], ids=["dgrad_first", "wgrad_first"])
+@pytest.mark.parametrize("order", [1, 2], ids=["dgrad_first", "wgrad_first"])  # keys 29 / 30
 def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode, order):
     """e2ep_conv_bwd (data and weight gradient in one k_conv_bwd_pair / k_lp_bwd_pair launch,
     where e2ep_conv_bwd_pair_ok) == e2ep_conv_dgrad_acc + e2ep_conv_wgrad on forked streams,
@@ -436,7 +436,8 @@ def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode, order):
     from e2ep_amd import _lib
     lib = _lib.load()
     prev = conv.set_conv_pair(False)
-    prev_order = lib.e2ep_tune(29, order)  # block order of the paired grid
+    prev_order = lib.e2ep_tune(29, order)  # block order of the paired grids
+    prev_order1 = lib.e2ep_tune(30, order)
     try:
         with precision.use(mode):
             two = run()
@@ -445,6 +446,7 @@ def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode, order):
     finally:
         conv.set_conv_pair(prev)
         lib.e2ep_tune(29, prev_order)
+        lib.e2ep_tune(30, prev_order1)
     assert all(torch.equal(a, c) for a, c in zip(one, two))
 
 
@@ -458,7 +460,9 @@ def test_conv_bwd_pair_covers_small_map_layers():
     def d1(N, C, H, W, Co):  # (N, Cin, H, W, Cout, R, S, P, Q, sh, sw, pt, pl, dh, dw)
         return (N, C, H, W, Co, 1, 1, H, W, 1, 1, 0, 0, 1, 1)
     layers = [d1(32, 192, 32, 32, 32), d1(32, 336, 16, 16, 56), d1(32, 1152, 8, 8, 192),
-              d1(32, 64, 16, 16, 160)]
+              d1(32, 64, 16, 16, 160),
+              # 64x64 / 128x128 maps: the k_wgrad_1x1 weight gradient (k_conv_bwd_pair1x1)
+              d1(32, 32, 64, 64, 192), d1(32, 192, 64, 64, 32), d1(32, 24, 128, 128, 144)]
     ok = [lib.e2ep_conv_bwd_pair_ok(_lib.dims(d), d[1]) for d in layers]
     assert all(ok), ok
     # BEV encoder / head 3x3s: k_conv_lp data gradient (fp32 and C3 bf16)
