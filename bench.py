@@ -299,13 +299,16 @@ def conv_roofline(step, lowp, n_eager=3):
     from e2ep_amd import conv, timing
     timing.reset()
     timing.enable(True)
-    # serial weight gradients here: a kernel's events then time that kernel alone, not its
-    # overlap with a side-stream weight gradient (the timed step runs them forked)
+    # serial weight gradients and no paired conv backward here: a kernel's events then time
+    # that kernel alone, not its overlap with a side-stream or same-grid weight gradient (the
+    # timed step runs them forked / paired)
     prev_overlap = conv.set_wgrad_overlap(False)
+    prev_pair = conv.set_conv_pair(False)
     for _ in range(n_eager):
         step._fwd_bwd()
     timing.enable(False)
     conv.set_wgrad_overlap(prev_overlap)
+    conv.set_conv_pair(prev_pair)
     kern = timing.summary()
     work = timing.work()
     gemm = [k for k in ("conv_fwd", "conv_dgrad") if k in kern]

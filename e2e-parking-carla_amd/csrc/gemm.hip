@@ -391,12 +391,14 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
 // streams: in a replayed graph a fork / join costs ~5 + ~10 us of idle GPU (scripts/
 // step_sequence.py), more than either product of the control decoder takes.
 template <class C1, class C2>
-__global__ void __launch_bounds__(256) k_gemm_pair(GemmArgs g1, GemmArgs g2) {
+__global__ void __launch_bounds__(256) k_gemm_pair(GemmArgs g1, GemmArgs g2, int second_first) {
   constexpr int L = C1::LDS_FLOATS > C2::LDS_FLOATS ? C1::LDS_FLOATS : C2::LDS_FLOATS;
   __shared__ __attribute__((aligned(16))) float lds[L];
   __shared__ int s_last;
-  const int n1 = g1.gx * g1.gy * g1.gz;
-  int id = blockIdx.x;
+  const int n1 = g1.gx * g1.gy * g1.gz, n2 = g2.gx * g2.gy * g2.gz;
+  // second_first: the second problem's blocks first in the grid (e2ep_tune key 31)
+  int id = second_first ? ((int)blockIdx.x >= n2 ? (int)blockIdx.x - n2 : n1 + (int)blockIdx.x)
+                        : (int)blockIdx.x;
   if (id < n1) {
     gemm_block<C1>(g1, id % g1.gx, (id / g1.gx) % g1.gy, id / (g1.gx * g1.gy), lds, &s_last);
   } else {
@@ -720,7 +722,7 @@ template <int OP, int WM1, int AV1, int WM2>
 static void pair4(dim3 grid, hipStream_t s, const GemmArgs &g1, const GemmArgs &g2) {
   hipLaunchKernelGGL((k_gemm_pair<GemmCfg<true, false, WM1, 1, 1, AV1, 0, OP>,
                                   GemmCfg<false, false, WM2, 1, 1, 0, 0, OP>>),
-                     grid, dim3(256), 0, s, g1, g2);
+                     grid, dim3(256), 0, s, g1, g2, g_tune[TUNE_LINEAR_PAIR_ORDER] == 2 ? 1 : 0);
 }
 template <int OP, int WM1, int AV1>
 static void pair3(int wm2, dim3 grid, hipStream_t s, const GemmArgs &g1, const GemmArgs &g2) {

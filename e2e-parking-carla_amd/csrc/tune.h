@@ -34,7 +34,8 @@ enum Tune {
   TUNE_SPLITK_FOLD = 28,      // split-K reductions folded into the producing launch (last-arriving split sums): 2 = on, 1 = separate reduce kernels
   TUNE_PAIR_ORDER = 29,       // conv paired backward (k_conv_bwd_pair, k_lp_bwd_pair): 2 = weight-gradient blocks first, 1 = data-gradient blocks first
   TUNE_PAIR1X1_ORDER = 30,    // 1x1 paired backward (k_conv_bwd_pair1x1): 2 = weight-gradient blocks first (default: C2 22.73 -> 22.50 ms), 1 = data-gradient blocks first
-  TUNE_N = 31
+  TUNE_LINEAR_PAIR_ORDER = 31, // linear paired backward (k_gemm_pair): 2 = weight-gradient blocks first, 1 = input-gradient blocks first
+  TUNE_N = 32
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep
