@@ -454,16 +454,17 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
 // each lane 4 adjacent dx pixels; the gy rows those rows read are staged in LDS.  For dx
 // pixel ix only taps b with (ix + pl - b) even contribute; ix0 is a multiple of 4, so the
 // parity of (u + pl - b) is compile-time given PLP = pl & 1.
+// The block body for block blk (k_dw_dgrad_s2_strip, and the data-gradient half of
+// k_dw_bwd_pair_s2), over the kernel's dynamic LDS.
 template <int K, int PLP>
-__global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restrict__ gy,
-                                                           const float *__restrict__ w, DwGeom g,
-                                                           int RO, int GR, int WPg,
-                                                           int units_per_plane, int units,
-                                                           float *__restrict__ dx) {
+__device__ __forceinline__ void dw_dgrad_s2_body(const float *__restrict__ gy,
+                                                 const float *__restrict__ w, DwGeom g, int RO,
+                                                 int GR, int WPg, int units_per_plane, int units,
+                                                 float *__restrict__ dx, int blk) {
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
-  const int unit = blockIdx.x * 4 + wave;
+  const int unit = blk * 4 + wave;
   float *lds = dw_lds + wave * GR * WPg;
   const bool active = unit < units;
   int nc = 0, iy0 = 0, oyA = 0;
@@ -497,6 +498,15 @@ __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restri
         if (((u + PLP - b) & 1) == 0) o[u] = __builtin_fmaf(wr[a * K + b], row[(u + PLP - b) >> 1], o[u]);
   }
   *reinterpret_cast<float4 *>(dx + ((size_t)nc * g.H + iy) * g.W + ix0) = make_float4(o[0], o[1], o[2], o[3]);
+}
+
+template <int K, int PLP>
+__global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restrict__ gy,
+                                                           const float *__restrict__ w, DwGeom g,
+                                                           int RO, int GR, int WPg,
+                                                           int units_per_plane, int units,
+                                                           float *__restrict__ dx) {
+  dw_dgrad_s2_body<K, PLP>(gy, w, g, RO, GR, WPg, units_per_plane, units, dx, blockIdx.x);
 }
 
 // weight gradient partials over strip units: grid (C, splits); the block's waves walk the
@@ -619,6 +629,22 @@ __global__ void __launch_bounds__(256) k_dw_bwd_pair(const float *__restrict__ g
     dw_fwd_strip_body<K, 1, true, OFF, VD>(gy, w, gt, dt, units, dx, DwIn{nullptr, nullptr, 0},
                                            nullptr, b - nw, nd);
   }
+}
+
+// The stride-2 form of k_dw_bwd_pair: weight-gradient blocks first (channel c, split sp), then
+// the k_dw_dgrad_s2_strip blocks (one unit per wave).
+template <int K, int PLP, int OFF, int VW>
+__global__ void __launch_bounds__(256) k_dw_bwd_pair_s2(const float *__restrict__ gy,
+                                                        const float *__restrict__ w, int RO, int GR,
+                                                        int WPg, int upp2, int units2,
+                                                        float *__restrict__ dx,
+                                                        const float *__restrict__ x, DwGeom g,
+                                                        DwStrip d, int splits, DwPart part, DwIn tf) {
+  const int b = blockIdx.x, nw = g.C * splits;
+  if (b < nw)
+    dw_wgrad_strip_body<K, 2, OFF, VW>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
+  else
+    dw_dgrad_s2_body<K, PLP>(gy, w, g, RO, GR, WPg, upp2, units2, dx, b - nw);
 }
 
 static int dw_splits(long long pixels, int C) {
@@ -792,6 +818,24 @@ int e2ep_dwconv_fwd_stats(const float *x, const float *w, const int *dims, const
   return launch_status("e2ep_dwconv_fwd");
 }
 
+// The stride-2 data-gradient strip plan of e2ep_dwconv_dgrad (RO output rows per unit, GR gy
+// rows staged); false where that entry point runs the generic kernel.
+struct DwS2 {
+  int RO, GR, WPg, upp, units;
+};
+static bool dw_s2_plan(const DwGeom &g, DwS2 &p) {
+  if (!(g.st == 2 && g.W % 4 == 0 && g.W <= 256 && g.Q % 4 == 0 && (g.K == 3 || g.K == 5) &&
+        g.pl <= 2 && g.pt <= 2))
+    return false;
+  p.RO = 64 / (g.W / 4);
+  p.GR = ((p.RO - 1 + g.pt) >> 1) - ((g.pt - (g.K - 1)) >> 1) + 2;
+  if (p.GR * (g.Q / 4) > 64 * DW_MAXV) return false;
+  p.WPg = g.Q + 2 * DW_PADL;
+  p.upp = (g.H + p.RO - 1) / p.RO;
+  p.units = g.N * g.C * p.upp;
+  return true;
+}
+
 int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream) {
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
@@ -815,14 +859,9 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
       return launch_status("e2ep_dwconv_dgrad");
     }
   }
-  const int RO2 = g.W % 4 == 0 && g.W <= 256 ? 64 / (g.W / 4) : 0;
-  const int GR2 = ((RO2 - 1 + g.pt) >> 1) - ((g.pt - (g.K - 1)) >> 1) + 2;
-  if (g.st == 2 && g.W % 4 == 0 && g.W <= 256 && g.Q % 4 == 0 && (g.K == 3 || g.K == 5) &&
-      g.pl <= 2 && g.pt <= 2 && GR2 * (g.Q / 4) <= 64 * DW_MAXV) {
-    const int RO = RO2;
-    const int GR = GR2;
-    const int WPg = g.Q + 2 * DW_PADL;
-    const int upp = (g.H + RO - 1) / RO, units = g.N * g.C * upp;
+  DwS2 p2;
+  if (dw_s2_plan(g, p2)) {
+    const int RO = p2.RO, GR = p2.GR, WPg = p2.WPg, upp = p2.upp, units = p2.units;
     const size_t shm = 4 * GR * WPg * sizeof(float);
     const dim3 grid(cdiv(units, 4));
     const bool odd = g.pl & 1;
@@ -860,6 +899,14 @@ static int dw_wgrad_splits(const DwGeom &g) {
   return dw_splits((long long)g.N * g.P * g.Q, g.C);
 }
 
+// The stride-2 paired backward's plan: both strip kernels, weight-gradient row reads at an
+// instantiated (K, pad_left): K = 3 pad 0 / 1, K = 5 pad 1 / 2.
+static bool dw_bwd_pair_s2_plan(const DwGeom &g, DwS2 &p) {
+  if (g.st != 2 || g_tune[TUNE_DW_VEC] == 1 || !dw_wgrad_strip_ok(g) || !dw_s2_plan(g, p))
+    return false;
+  return (g.K == 3 && (g.pl == 0 || g.pl == 1)) || (g.K == 5 && (g.pl == 1 || g.pl == 2));
+}
+
 // The paired backward's plan (stride 1, both strip kernels, vector row reads with one OFF for
 // both halves: symmetric padding, K = 3 pad 1 -> 3, K = 5 pad 2 -> 2).
 static bool dw_bwd_pair_plan(const DwGeom &g, DwGeom &t, int &off) {
@@ -876,7 +923,9 @@ int e2ep_dwconv_bwd_pair_ok(const int *dims) {
   const DwGeom g = dw_geom(dims);
   DwGeom t;
   int off;
-  return (g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0 && dw_bwd_pair_plan(g, t, off)) ? 1 : 0;
+  DwS2 p2;
+  return (g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0 &&
+          (dw_bwd_pair_plan(g, t, off) || dw_bwd_pair_s2_plan(g, p2))) ? 1 : 0;
 }
 
 size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
@@ -919,8 +968,10 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
   const DwGeom g = dw_geom(dims);
   DwGeom t;
   int off;
-  E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0 && dw_bwd_pair_plan(g, t, off),
-               E2EP_EINVAL, "e2ep_dwconv_bwd: no paired backward for this geometry "
+  DwS2 p2;
+  const bool geo = g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0;
+  const bool s1 = geo && dw_bwd_pair_plan(g, t, off), s2 = geo && !s1 && dw_bwd_pair_s2_plan(g, p2);
+  E2EP_REQUIRE(s1 || s2, E2EP_EINVAL, "e2ep_dwconv_bwd: no paired backward for this geometry "
                "(e2ep_dwconv_bwd_pair_ok returned 0)");
   E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_dwconv_wgrad_workspace(dims), E2EP_EINVAL,
                "e2ep_dwconv_bwd: workspace %zu bytes < %zu (e2ep_dwconv_wgrad_workspace)",
@@ -929,6 +980,35 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
                "e2ep_dwconv_bwd: in_scale / in_shift both or neither, in_act 0..2");
   E2EP_REQUIRE(gy && x && w && dx && dw, E2EP_EINVAL, "e2ep_dwconv_bwd: null tensor");
   const DwIn tf{in_scale, in_shift, in_act};
+  hipStream_t s = as_stream(stream);
+  if (s2) {
+    const DwStrip d = dw_strip(g.K, 2, g.W, g.P, g.Q);
+    const int vw = cdiv(d.IR * (g.W / 4), 64) <= 2 ? 2 : DW_MAXV;
+    const int sp = dw_wgrad_splits(g);
+    DwPart part{static_cast<float *>(workspace), dw,
+                (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C) : nullptr};
+    const size_t shm = 4 * (size_t)std::max(p2.GR * p2.WPg, d.IR * d.WP) * 4;
+    const dim3 grid(g.C * sp + cdiv(p2.units, 4));
+#define DWP2(KV, PLPV, OFFV)                                                                       \
+  do {                                                                                             \
+    if (vw == 2)                                                                                   \
+      hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, 2>), grid, dim3(256), shm, s, gy, w,    \
+                         p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf);       \
+    else                                                                                           \
+      hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, DW_MAXV>), grid, dim3(256), shm, s, gy, \
+                         w, p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf);    \
+  } while (0)
+    // PLP = pad_left & 1, OFF = -pad_left mod 4 (dw_off)
+    if (g.K == 3 && g.pl == 0) DWP2(3, 0, 0);
+    else if (g.K == 3) DWP2(3, 1, 3);
+    else if (g.pl == 1) DWP2(5, 1, 3);
+    else DWP2(5, 0, 2);
+#undef DWP2
+    if (sp > 1 && !part.cnt)
+      hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0, s,
+                         part.part, g.C, g.K * g.K, sp, dw);
+    return launch_status("e2ep_dwconv_bwd");
+  }
   const DwStrip dt = dw_strip(t.K, 1, t.W, t.P, t.Q);
   const int units = t.N * t.C * dt.units_per_plane;
   const int nd = dw_fwd_blocks(units);
@@ -940,7 +1020,6 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
               (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C) : nullptr};
   const size_t shm = 4 * (size_t)std::max(dt.IR * dt.WP, d.IR * d.WP) * 4;
   const dim3 grid(nd + g.C * sp);
-  hipStream_t s = as_stream(stream);
 #define DWP(KV, OFFV, VDV, VWV)                                                                   \
   hipLaunchKernelGGL((k_dw_bwd_pair<KV, OFFV, VDV, VWV>), grid, dim3(256), shm, s, gy, w, t, dt, \
                      units, dx, nd, x, g, d, sp, part, tf)

@@ -202,10 +202,14 @@ def test_depthwise(case, variant):
                                   (2, 24, 128, 128, 3, 1, (1, 1, 1, 1)), (2, 32, 64, 64, 3, 1, (1, 1, 1, 1)),
                                   (2, 40, 32, 32, 5, 1, (2, 2, 2, 2)), (3, 16, 16, 16, 3, 1, (1, 1, 1, 1)),
                                   (2, 12, 24, 20, 5, 1, (2, 2, 2, 2)), (32, 192, 32, 32, 5, 1, (2, 2, 2, 2)),
-                                  (32, 96, 64, 64, 3, 1, (1, 1, 1, 1))])
+                                  (32, 96, 64, 64, 3, 1, (1, 1, 1, 1)),
+                                  # stride 2 (k_dw_bwd_pair_s2): K 3 pad-left 0 / 1, K 5 pad-left 1 / 2
+                                  (4, 144, 64, 64, 3, 2, (0, 1, 0, 1)), (2, 16, 32, 32, 3, 2, (1, 1, 1, 1)),
+                                  (4, 192, 32, 32, 5, 2, (2, 2, 2, 2)), (2, 16, 32, 32, 5, 2, (1, 2, 1, 2)),
+                                  (32, 144, 128, 128, 3, 2, (0, 1, 0, 1)), (2, 6, 64, 48, 5, 2, (2, 2, 2, 2))])
 @pytest.mark.parametrize("fused", [False, True], ids=["dw", "bn_swish_dw"])
 def test_depthwise_bwd_pair_bitwise_equals_two_launches(case, fused):
-    """e2ep_dwconv_bwd (data and weight gradient in one k_dw_bwd_pair launch) == the forked
+    """e2ep_dwconv_bwd (data and weight gradient in one k_dw_bwd_pair / k_dw_bwd_pair_s2 launch) == the forked
     e2ep_dwconv_dgrad + e2ep_dwconv_wgrad, bitwise, for the plain depthwise conv and the
     MBConv _bn0 -> swish -> depthwise form (the weight gradient's input transform)."""
     from e2ep_amd import _lib, nn_ops, ops
