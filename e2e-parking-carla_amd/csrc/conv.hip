@@ -2194,10 +2194,14 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
     used = lp_bwd_pair_launch(w, gout, res, dx, dx_bytes, g, M, g_conv_precision == 1 ? 1 : 0,
                               ws_dgrad, x, tl, wsplits, part2, s);
     E2EP_REQUIRE(used > 0, E2EP_EINVAL, "e2ep_conv_bwd: no paired k_conv_lp plan");
-  } else if (kind == PAIR_GEMM1X1) {
-    const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
-    float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
-    unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+    reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
+    return launch_status("e2ep_conv_bwd");
+  }
+  // k_conv_gemm data gradient: launch_gemm's grid and fold counters
+  const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
+  float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
+  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+  if (kind == PAIR_GEMM1X1) {
     // e2ep_conv_wgrad's k_wgrad_1x1 plan
     const int groups = g.N * g.P * g.Q / 8;
     const int gps = cdiv(groups, wsplits);
@@ -2230,10 +2234,6 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
     reduce_splits(part2, used, g.Cout * g.Cin, dw, 0, 1, 1ULL, s);
     return launch_status("e2ep_conv_bwd");
   } else {
-    // data gradient grid (launch_gemm's), fold counters
-    const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
-    float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
-    unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
     // weight gradient grid (e2ep_conv_wgrad's k_conv_wgrad2 path)
     const int Ptot = g.N * g.P * g.Q;
     int per = (Ptot + wsplits - 1) / wsplits;
