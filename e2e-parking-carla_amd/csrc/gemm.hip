@@ -106,7 +106,6 @@ __device__ __forceinline__ void gemm_block(const GemmArgs &g, int bx, int by, in
   // rs != null (only !AK, !BKC, unbatched): B gets a logical column N of ones, so column N of
   // the product is the row sum of A over k — rs[m] = sum_k A(m, k), the bias gradient of a
   // linear layer taken by its weight-gradient GEMM (no separate column-sum launches)
-  constexpr int WN = 4 / WM;                      // waves along N
   constexpr int BM = CFG::BM, BN = CFG::BN;
   constexpr int GA = BM / 32, GB = BN / 32;       // 32-row load groups per operand tile
   float(*As)[BM][G_LDW] = reinterpret_cast<float(*)[BM][G_LDW]>(lds);
