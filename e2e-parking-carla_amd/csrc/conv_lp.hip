@@ -79,14 +79,12 @@ __device__ __forceinline__ void conv_lp_block(
     float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats, int bx,
     int by, int bz, int gx, typename LpType<OP>::T (*As)[64 * WM][lld_of(OP, LKS)],
     typename LpType<OP>::T (*Bs)[64 * WN][lld_of(OP, LKS)]) {
-  typedef typename LpType<OP>::T T;
   typedef typename LpType<OP>::T8 T8;
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
   constexpr int KGB = 256 / BNT;  // B k-groups (4, 2, 1)
   constexpr int RPB = LKS / KGB;   // B k rows per thread (8, 16, 32)
   constexpr int KGA = 256 / BMT;  // A k-groups (4, 2)
   constexpr int RPA = LKS / KGA;   // A k per thread (8, 16)
-  constexpr int LD = lld_of(OP, LKS);
   static_assert(OP != 0 || (WN <= 2 && LKS == 32), "fp32: 32-deep steps, tiles up to 128 x 128");
   static_assert(LKS == 32 || LKS == 64, "K step 32 or 64");
   __shared__ int s_tdy[MAXTAPS], s_tdx[MAXTAPS], s_trs[MAXTAPS];
@@ -695,8 +693,6 @@ __device__ __forceinline__ void wgrad_lp_block(
     ConvGeom g, int pix_per_split, TapList tl, int bx, int by, int bz, int gz,
     typename LpType<OP == 0 ? 0 : 1>::T (*As)[64 * WM][lld_of(OP, LKS)],
     typename LpType<OP == 0 ? 0 : 1>::T (*Bs)[64 * WN][lld_of(OP, LKS)]) {
-  typedef typename LpType<OP == 0 ? 0 : 1>::T T;
-  constexpr int LD = lld_of(OP, LKS);
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
   static_assert(OP != 0 || LKS == 32, "fp32: 32-pixel steps");
   constexpr int OPR = LKS / 8;             // A pixel octets per row
@@ -1011,7 +1007,10 @@ static bool lp_pair_tiles(const ConvGeom &g, int M, int op, const TapList &tl, L
   }
   // not the 128 x 128 data-gradient tile: its ~200 VGPRs hold the whole paired grid to one
   // workgroup per SIMD, and the weight-gradient blocks then run at a third of their occupancy
-  // (C3: 87 us paired against ~39 + 44 us overlapped on two streams)
+  // (C3: 87 us paired against ~39 + 44 us overlapped on two streams).  Without a K split the
+  // pair runs that data gradient on 128 x 64 tiles instead: every output's K order is the
+  // same whatever the tile, so the results stay bitwise those of the two-launch path.
+  if (op == 1 && p.wm == 2 && p.wn == 2 && p.splits == 1) p.wn = 1;
   if (op != 1 || p.wn > 2 || (p.wm == 2 && p.wn == 2) || !lp_wgrad_ok(g, tl) ||
       lp_wgrad_lk(g, op) != LK)
     return false;
