@@ -900,9 +900,14 @@ static int dw_wgrad_splits(const DwGeom &g) {
 }
 
 // The stride-2 paired backward's plan: both strip kernels, weight-gradient row reads at an
-// instantiated (K, pad_left): K = 3 pad 0 / 1, K = 5 pad 1 / 2.
+// instantiated (K, pad_left): K = 3 pad 0 / 1, K = 5 pad 1 / 2.  Not for data gradients of
+// more than DW_S2_PAIR_UNITS units: the 128 x 128-map layer (294 912 units) ran 220 us paired
+// against ~183 us as two forked launches, while the 43 008- and 98 304-unit layers ran 37 / 87
+// us paired against ~44 / ~86 us forked (step_sequence_fp32_final.txt against _r4z.txt).
+constexpr int DW_S2_PAIR_UNITS = 131072;
 static bool dw_bwd_pair_s2_plan(const DwGeom &g, DwS2 &p) {
-  if (g.st != 2 || g_tune[TUNE_DW_VEC] == 1 || !dw_wgrad_strip_ok(g) || !dw_s2_plan(g, p))
+  if (g.st != 2 || g_tune[TUNE_DW_VEC] == 1 || !dw_wgrad_strip_ok(g) || !dw_s2_plan(g, p) ||
+      p.units > DW_S2_PAIR_UNITS)
     return false;
   return (g.K == 3 && (g.pl == 0 || g.pl == 1)) || (g.K == 5 && (g.pl == 1 || g.pl == 2));
 }

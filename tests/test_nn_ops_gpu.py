@@ -206,7 +206,7 @@ def test_depthwise(case, variant):
                                   # stride 2 (k_dw_bwd_pair_s2): K 3 pad-left 0 / 1, K 5 pad-left 1 / 2
                                   (4, 144, 64, 64, 3, 2, (0, 1, 0, 1)), (2, 16, 32, 32, 3, 2, (1, 1, 1, 1)),
                                   (4, 192, 32, 32, 5, 2, (2, 2, 2, 2)), (2, 16, 32, 32, 5, 2, (1, 2, 1, 2)),
-                                  (32, 144, 128, 128, 3, 2, (0, 1, 0, 1)), (2, 6, 64, 48, 5, 2, (2, 2, 2, 2))])
+                                  (8, 144, 128, 128, 3, 2, (0, 1, 0, 1)), (2, 6, 64, 48, 5, 2, (2, 2, 2, 2))])
 @pytest.mark.parametrize("fused", [False, True], ids=["dw", "bn_swish_dw"])
 def test_depthwise_bwd_pair_bitwise_equals_two_launches(case, fused):
     """e2ep_dwconv_bwd (data and weight gradient in one k_dw_bwd_pair / k_dw_bwd_pair_s2 launch) == the forked
@@ -217,6 +217,9 @@ def test_depthwise_bwd_pair_bitwise_equals_two_launches(case, fused):
     lib = _lib.load()
     P, Q = (H + pad[2] + pad[3] - K) // s + 1, (W + pad[0] + pad[1] - K) // s + 1
     assert lib.e2ep_dwconv_bwd_pair_ok(_lib.dims((N, C, H, W, K, P, Q, s, pad[2], pad[0]))) == 1
+    # the large stride-2 layer stays on two forked launches (DW_S2_PAIR_UNITS)
+    big = (32, 144, 128, 128, 3, 64, 64, 2, 0, 0)
+    assert lib.e2ep_dwconv_bwd_pair_ok(_lib.dims(big)) == 0
     g = _g(C + H + 5)
     x = (torch.randn(N, C, H, W, generator=g) * 2 + 0.5).to(DEV)
     w = (torch.randn(C, 1, K, K, generator=g) / K).to(DEV)
