@@ -328,7 +328,11 @@ def conv_roofline(step, lowp, n_eager=3):
              "flop_per_step": g_flop / n_eager, "ms_per_step": round(g_ms / n_eager, 4),
              "launches_per_step": g_launch // n_eager,
              "timing": f"HIP events around every conv fwd/dgrad launch of {n_eager} eager fwd+bwd "
-                       "passes on the launch stream; FLOPs = 2*N*Cout*P*Q*Cin*R*S per launch"}
+                       "passes on the launch stream; FLOPs = 2*N*Cout*P*Q*Cin*R*S per launch; "
+                       "these passes run each data gradient as its own launch (pairs and forks "
+                       "off), while the timed step runs most of them paired with their weight "
+                       "gradient in one grid (k_conv_bwd_pair / k_conv_bwd_pair1x1 / "
+                       "k_lp_bwd_pair), so this is a per-kernel figure, not the step's"}
     return entry, kern
 
 

@@ -455,10 +455,23 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(
     const float *__restrict__ dc_rand, float dc_keep, BnGate gt, const double *__restrict__ part,
     int splits, long long cnt, int N, int C, int HWv, int per, int act, int train,
     float *__restrict__ dx, float *__restrict__ dres, float *__restrict__ dgamma,
-    float *__restrict__ dbeta) {
+    float *__restrict__ dbeta, const double *__restrict__ planes) {
   const int c = blockIdx.x, j = blockIdx.y;
   double s, q;
-  channel_partials(part, c, splits, s, q);
+  if (planes) {  // e2ep_bn_bwd_planes: the sums from the SE pass's per-plane factors
+    s = 0.0;
+    q = 0.0;
+    for (int n = threadIdx.x; n < N; n += 256) {
+      float gs, gd;
+      gt.coef(n, C, c, gs, gd);
+      const double *a = planes + 4LL * ((long long)n * C + c);
+      s += (double)gs * a[0] + (double)gd * a[1];
+      q += (double)gs * a[2] + (double)gd * a[3];
+    }
+    block_sum2(s, q);
+  } else {
+    channel_partials(part, c, splits, s, q);
+  }
   if (j == 0 && threadIdx.x == 0) {
     if (dbeta) dbeta[c] = (float)s;
     if (dgamma) dgamma[c] = (float)q;
@@ -924,15 +937,52 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
     if (v4)
       hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
                          res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
-                         dx, dres, dgamma, dbeta);
+                         dx, dres, dgamma, dbeta, nullptr);
     else
       hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
                          res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
-                         dx, dres, dgamma, dbeta);
+                         dx, dres, dgamma, dbeta, nullptr);
   } else if (dgamma || dbeta) {
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(256), 0, s, part, sp, dgamma, dbeta);
   }
   return launch_status("e2ep_bn_bwd");
+}
+
+int e2ep_bn_bwd_split(int N, int C, int H, int W) {
+  if (N <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  const int HW = H * W;
+  const bool v4 = (HW & 3) == 0;
+  const int totv = N * (v4 ? HW / 4 : HW);
+  int th = 0;
+  return (v4 && bn_small_enabled() && totv <= g_bns_bwd_max && bns_r(totv, th)) ? 0 : 1;
+}
+
+int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const float *invstd,
+                       const float *gamma, const float *beta, const float *gate_logit,
+                       const float *gate_dpooled, const double *plane_sums, int N, int C, int H,
+                       int W, int act, float *dx, float *dgamma, float *dbeta, void *stream) {
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
+               E2EP_EINVAL, "e2ep_bn_bwd_planes: bad shape");
+  E2EP_REQUIRE(x && dy && mean && invstd && gate_logit && gate_dpooled && plane_sums && dx,
+               E2EP_EINVAL, "e2ep_bn_bwd_planes: null argument");
+  E2EP_REQUIRE(act >= 0 && act <= 2, E2EP_EINVAL, "e2ep_bn_bwd_planes: act must be 0/1/2");
+  const BnGate gt{gate_logit, gate_dpooled, 1.f / (float)(H * W)};
+  const int HW = H * W;
+  const long long per_c = (long long)N * HW;
+  const bool v4 = (HW & 3) == 0;
+  const int HWv = v4 ? HW / 4 : HW;
+  const int totv = N * HWv;
+  const dim3 grid(C, cdiv(totv, APPLY_PER));
+  hipStream_t s = as_stream(stream);
+  if (v4)
+    hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
+                       nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
+                       dx, nullptr, dgamma, dbeta, plane_sums);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
+                       nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
+                       dx, nullptr, dgamma, dbeta, plane_sums);
+  return launch_status("e2ep_bn_bwd_planes");
 }
 
 int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec) {

@@ -1044,13 +1044,14 @@ __global__ void __launch_bounds__(256, 2) k_conv_bwd_pair(
     float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
     const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
-    int gx2, int gy2, int gz2, int wfirst) {
+    int gx2, int gy2, int gz2) {
   constexpr int L1 = conv_gemm_lds_floats<BNT, BMT>();
   constexpr int L = L1 > W2_LDS_FLOATS ? L1 : W2_LDS_FLOATS;
   __shared__ __attribute__((aligned(16))) float lds[L];
-  const int n1 = gx1 * gy1 * gz1, n2 = gx2 * gy2 * gz2;
-  // wfirst: weight-gradient blocks [0, n2), then the data gradient's (e2ep_tune key 29)
-  int id = wfirst ? (blockIdx.x >= n2 ? blockIdx.x - n2 : n1 + blockIdx.x) : blockIdx.x;
+  // data-gradient blocks [0, n1) first: the weight-gradient-first order measured 0.15 ms/step
+  // slower in C2 and C3 (profiles/r04/conv_pair_order_ab.txt; the switch is retired)
+  const int n1 = gx1 * gy1 * gz1;
+  int id = blockIdx.x;
   if (id < n1) {
     conv_gemm_block<1, 0, BNT, BMT, false, 0, false>(w, gout, res, dx, dx_bytes, g, M, splits, kper,
                                                      part1, cnt, nullptr, id % gx1,
@@ -1845,7 +1846,7 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     }
     part = static_cast<float *>(workspace);
     // in-launch fold (e2ep_tune key 28 = 2): one arrival counter per output tile
-    if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y);
+    if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y, s);
   }
   if (stats && p.splits > 1 && !cnt) {
     set_error("conv: BatchNorm statistics need the in-launch split-K fold (e2ep_tune key 28 = 2)");
@@ -2200,7 +2201,7 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
   // k_conv_gemm data gradient: launch_gemm's grid and fold counters
   const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
   float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
-  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y, s) : nullptr;
   if (kind == PAIR_GEMM1X1) {
     // e2ep_conv_wgrad's k_wgrad_1x1 plan
     const int groups = g.N * g.P * g.Q / 8;
@@ -2231,6 +2232,9 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
     }
 #undef E2EP_PAIR1_W
 #undef E2EP_PAIR1
+    if (p.splits > 1 && !cnt)  // no fold counters: the data gradient's slabs reduced here
+      hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s, part1,
+                         p.splits, M, g.H * g.W, (int)p.ncols, nullptr, 0, res, dx);
     reduce_splits(part2, used, g.Cout * g.Cin, dw, 0, 1, 1ULL, s);
     return launch_status("e2ep_conv_bwd");
   } else {
@@ -2244,8 +2248,7 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
 #define E2EP_PAIR(BNTV, BMTV)                                                                     \
   hipLaunchKernelGGL((k_conv_bwd_pair<BNTV, BMTV>), grid, dim3(256), 0, s, w, gout, res, dx,      \
                      dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, (int)g1.y,           \
-                     (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z,           \
-                     g_tune[TUNE_PAIR_ORDER] == 2 ? 1 : 0)
+                     (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
     if (p.bm == 64) {
       if (p.bnt == 128) E2EP_PAIR(128, 64);
       else E2EP_PAIR(64, 64);
@@ -2255,6 +2258,9 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
     }
 #undef E2EP_PAIR
   }
+  if (p.splits > 1 && !cnt)  // no fold counters: the data gradient's slabs reduced here
+    hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s, part1,
+                       p.splits, M, g.H * g.W, (int)p.ncols, nullptr, 0, res, dx);
   reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
   return launch_status("e2ep_conv_bwd");
 }

@@ -639,7 +639,7 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
     }
     part = static_cast<float *>(workspace);
     // in-launch fold (e2ep_tune key 28 = 2): one arrival counter per output tile
-    if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y);
+    if (g_tune[TUNE_SPLITK_FOLD] == 2) cnt = handoff_slots((int)grid.x * (int)grid.y, s);
   }
   if (stats && (mode != 0 || (p.splits > 1 && !cnt))) {
     set_error("conv (low precision): BatchNorm statistics need the forward with its final epilogue");
@@ -893,15 +893,13 @@ __global__ void __launch_bounds__(256) k_lp_bwd_pair(
     float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
     const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
-    int gx2, int gy2, int gz2, int wfirst) {
+    int gx2, int gy2, int gz2) {
   typedef typename LpType<OP>::T T;
   constexpr int LD = lld_of(OP, LK);
   constexpr int L1 = 2 * 64 * (DWM + DWN) * LD, L2 = 2 * 64 * (WWM + WWN) * LD;
   __shared__ __attribute__((aligned(16))) T lds[L1 > L2 ? L1 : L2];
-  const int n1 = gx1 * gy1 * gz1;
-  // wfirst: weight-gradient blocks first (e2ep_tune key 29)
-  const int n2b = gx2 * gy2 * gz2;
-  int id = wfirst ? ((int)blockIdx.x >= n2b ? (int)blockIdx.x - n2b : n1 + (int)blockIdx.x) : (int)blockIdx.x;
+  const int n1 = gx1 * gy1 * gz1;  // data-gradient blocks first (as k_conv_bwd_pair)
+  int id = (int)blockIdx.x;
   if (id < n1) {
     if (g.xcd) id = xcd_linear(id, n1);
     conv_lp_block<1, 0, DWM, DWN, OP, LK>(
@@ -1033,7 +1031,7 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, floa
   if (!lp_pair_tiles(g, M, op, tl, p, wwm, wwn)) return -1;
   const dim3 g1(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
   float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
-  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y) : nullptr;
+  unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y, s) : nullptr;
   const int Ptot = g.N * g.P * g.Q;
   int per = (Ptot + wsplits - 1) / wsplits;
   per = (per + LK - 1) / LK * LK;
@@ -1043,8 +1041,7 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, floa
 #define PAIR_L(DM, DN, OPV, WMV, WNV)                                                           \
   hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV>), grid, dim3(256), 0, s, w, gout,    \
                      res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x,           \
-                     (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z,   \
-                     g_tune[TUNE_PAIR_ORDER] == 2 ? 1 : 0)
+                     (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
 #define PAIR_W(DM, DN)                                     \
   do {                                                     \
     if (wwm == 2 && wwn == 2) PAIR_L(DM, DN, 1, 2, 2);     \
@@ -1058,6 +1055,10 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, floa
   else PAIR_W(1, 1);
 #undef PAIR_W
 #undef PAIR_L
+  if (p.splits > 1 && !cnt)  // no fold counters: the data gradient's slabs reduced here
+    hipLaunchKernelGGL(k_conv_lp_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
+                       static_cast<const float *>(part1), p.splits, M, g.H * g.W, (int)p.ncols,
+                       nullptr, 0, res, dx);
   return used;
 }
 

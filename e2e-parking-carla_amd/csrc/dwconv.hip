@@ -953,7 +953,7 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
   const int sp = dw_wgrad_splits(g);
   // one split: the slab is the gradient; several: in-launch fold or k_dw_wgrad_finalize
   DwPart part{static_cast<float *>(workspace), dw,
-              (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C) : nullptr};
+              (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C, as_stream(stream)) : nullptr};
   if (dw_wgrad_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     DW_STRIP_DISPATCH(dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
@@ -991,7 +991,7 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
     const int vw = cdiv(d.IR * (g.W / 4), 64) <= 2 ? 2 : DW_MAXV;
     const int sp = dw_wgrad_splits(g);
     DwPart part{static_cast<float *>(workspace), dw,
-                (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C) : nullptr};
+                (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C, s) : nullptr};
     const size_t shm = 4 * (size_t)std::max(p2.GR * p2.WPg, d.IR * d.WP) * 4;
     const dim3 grid(g.C * sp + cdiv(p2.units, 4));
 #define DWP2(KV, PLPV, OFFV)                                                                       \
@@ -1022,7 +1022,7 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
   const int vw = cdiv(d.IR * (g.W / 4), 64) <= 2 ? 2 : DW_MAXV;
   const int sp = dw_wgrad_splits(g);
   DwPart part{static_cast<float *>(workspace), dw,
-              (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C) : nullptr};
+              (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C, s) : nullptr};
   const size_t shm = 4 * (size_t)std::max(dt.IR * dt.WP, d.IR * d.WP) * 4;
   const dim3 grid(nd + g.C * sp);
 #define DWP(KV, OFFV, VDV, VWV)                                                                   \

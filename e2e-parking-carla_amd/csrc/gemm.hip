@@ -390,14 +390,14 @@ __global__ void __launch_bounds__(256) k_gemm(GemmArgs g) {
 // streams: in a replayed graph a fork / join costs ~5 + ~10 us of idle GPU (scripts/
 // step_sequence.py), more than either product of the control decoder takes.
 template <class C1, class C2>
-__global__ void __launch_bounds__(256) k_gemm_pair(GemmArgs g1, GemmArgs g2, int second_first) {
+__global__ void __launch_bounds__(256) k_gemm_pair(GemmArgs g1, GemmArgs g2) {
   constexpr int L = C1::LDS_FLOATS > C2::LDS_FLOATS ? C1::LDS_FLOATS : C2::LDS_FLOATS;
   __shared__ __attribute__((aligned(16))) float lds[L];
   __shared__ int s_last;
-  const int n1 = g1.gx * g1.gy * g1.gz, n2 = g2.gx * g2.gy * g2.gz;
-  // second_first: the second problem's blocks first in the grid (e2ep_tune key 31)
-  int id = second_first ? ((int)blockIdx.x >= n2 ? (int)blockIdx.x - n2 : n1 + (int)blockIdx.x)
-                        : (int)blockIdx.x;
+  // the first problem's blocks first (the reverse order was within noise,
+  // profiles/r04/linear_pair_order_ab.txt; the switch is retired)
+  const int n1 = g1.gx * g1.gy * g1.gz;
+  int id = (int)blockIdx.x;
   if (id < n1) {
     gemm_block<C1>(g1, id % g1.gx, (id / g1.gx) % g1.gy, id / (g1.gx * g1.gy), lds, &s_last);
   } else {
@@ -626,7 +626,7 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
   const GemmTile td = tile_dims(p.tile);
   // in-launch split-K fold (e2ep_tune key 28 = 2): one arrival counter per output tile
   unsigned int *cnt = (p.splits > 1 && g_tune[TUNE_SPLITK_FOLD] == 2)
-                          ? handoff_slots(cdiv(Nx, td.bn) * cdiv(M, td.bm)) : nullptr;
+                          ? handoff_slots(cdiv(Nx, td.bn) * cdiv(M, td.bm), s) : nullptr;
   dim3 grid(cdiv(Nx, td.bn), cdiv(M, td.bm), p.splits);
   const int avec = vec_of(ak, lda, A), bvec = vec_of(bk, ldb, B);
   const int br = bias_rows ? 1 : 0;
@@ -697,7 +697,8 @@ int gemm_run(const float *A, int lda, bool ak, long long a_bytes, const float *B
 static bool gemm_prepare(const float *A, int lda, bool ak, long long a_bytes, const float *B,
                          int ldb, bool bk, long long b_bytes, const float *Cadd, int ldadd,
                          float *C, long long c_bytes, int ldc, int M, int N, int K,
-                         void *workspace, float *rs, GemmArgs &ga, int &wm, int &avec) {
+                         void *workspace, float *rs, hipStream_t s, GemmArgs &ga, int &wm,
+                         int &avec) {
   const int Nx = rs ? N + 1 : N;
   GemmLaunch p = gemm_plan(M, Nx, K);
   if (g_gemm_precision == 1 && p.tile != 1 && p.tile != 2) p.tile = 1;
@@ -705,7 +706,8 @@ static bool gemm_prepare(const float *A, int lda, bool ak, long long a_bytes, co
   if (p.splits > 1 && (!workspace || g_tune[TUNE_SPLITK_FOLD] != 2)) return false;
   const GemmTile td = tile_dims(p.tile);
   const int gx = cdiv(Nx, td.bn), gy = cdiv(M, td.bm);
-  unsigned int *cnt = p.splits > 1 ? handoff_slots(gx * gy) : nullptr;
+  unsigned int *cnt = p.splits > 1 ? handoff_slots(gx * gy, s) : nullptr;
+  if (p.splits > 1 && !cnt) return false;  // no counters: the two-launch path reduces
   ga = GemmArgs{A, lda, a_bytes, B, ldb, b_bytes, nullptr, 0, Cadd, ldadd, C, c_bytes, ldc,
                 GemmCols{0, 0, 0}, M, N, K, p.kper, 0, rs,
                 p.splits > 1 ? static_cast<float *>(workspace) : nullptr, cnt, gx, gy, p.splits};
@@ -721,7 +723,7 @@ template <int OP, int WM1, int AV1, int WM2>
 static void pair4(dim3 grid, hipStream_t s, const GemmArgs &g1, const GemmArgs &g2) {
   hipLaunchKernelGGL((k_gemm_pair<GemmCfg<true, false, WM1, 1, 1, AV1, 0, OP>,
                                   GemmCfg<false, false, WM2, 1, 1, 0, 0, OP>>),
-                     grid, dim3(256), 0, s, g1, g2, g_tune[TUNE_LINEAR_PAIR_ORDER] == 2 ? 1 : 0);
+                     grid, dim3(256), 0, s, g1, g2);
 }
 template <int OP, int WM1, int AV1>
 static void pair3(int wm2, dim3 grid, hipStream_t s, const GemmArgs &g1, const GemmArgs &g2) {
@@ -777,9 +779,9 @@ int e2ep_linear_bwd(const float *dy, int ldy, const float *x, int ldx, const flo
   int wm1, av1, wm2, av2;
   if (g_force_tile == 0 &&
       gemm_prepare(dy, ldy, true, y_bytes, w, ldw, false, w_bytes, gskip, ldskip, dx, dx_bytes,
-                   lddx, M, K, N, ws_dx, nullptr, g1, wm1, av1) &&
+                   lddx, M, K, N, ws_dx, nullptr, s, g1, wm1, av1) &&
       gemm_prepare(dy, ldy, false, y_bytes, x, ldx, false, x_bytes, nullptr, 0, dw, dw_bytes,
-                   lddw, N, K, M, ws_dw, db, g2, wm2, av2)) {
+                   lddw, N, K, M, ws_dw, db, s, g2, wm2, av2)) {
     const dim3 grid(g1.gx * g1.gy * g1.gz + g2.gx * g2.gy * g2.gz);
     if (g_gemm_precision == 1) pair1<1>(wm1, av1, wm2, grid, s, g1, g2);
     else pair1<0>(wm1, av1, wm2, grid, s, g1, g2);

@@ -8,20 +8,26 @@
 // (no acquire fence, no plain load of them).  The last arriver also resets its counter, so a
 // counter slot is zero again when the launch ends.
 //
-// Counters come from one zero-initialised device pool (handoff.hip): each launch takes a
-// fresh slot range from a rotating host-side cursor, so kernels that may run concurrently
+// Counters come from one zero-initialised device pool per device (handoff.hip): each launch
+// takes a fresh slot range from a host-side cursor, so kernels that may run concurrently
 // (side-stream weight gradients, several captured graphs) never share a slot; a captured
 // launch keeps its range on every replay (kernels of one graph replay never overlap
-// themselves).
+// themselves).  Launches captured into a graph take their ranges from a region that is
+// handed out once (HANDOFF_CAPTURED counters, not reused while the process lives unless it
+// runs out, ~500 captured train steps); eager launches rotate through the other region, so an
+// eager launch never shares a slot with a live graph's launch.
 #pragma once
 #include "common.h"
 
 namespace e2ep {
 
-constexpr int HANDOFF_POOL = 1 << 20;  // counters in the pool (4 MB)
+constexpr int HANDOFF_POOL = 1 << 24;      // counters in a device's pool (64 MB)
+constexpr int HANDOFF_CAPTURED = 15 << 20; // of them for launches captured into graphs
 
-// n zeroed counters for one launch (host; the pool is fetched once, outside any capture)
-unsigned int *handoff_slots(int n);
+// n zeroed counters for one launch on `stream` (host; the current device's pool), or nullptr
+// when n is out of range or the pool cannot be fetched: the callers then run their split-K
+// reductions as separate launches
+unsigned int *handoff_slots(int n, hipStream_t stream);
 
 __device__ __forceinline__ void st_sc1(float *p, float v) {
   __hip_atomic_store(reinterpret_cast<unsigned int *>(p), __builtin_bit_cast(unsigned int, v),

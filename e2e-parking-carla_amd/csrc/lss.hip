@@ -264,20 +264,23 @@ __device__ __forceinline__ float row_bcast(float v) {
 // offsets / probabilities.  Slots past the chunk end carry probability 0 and row 0 (a valid
 // row), and their position is clamped to the chunk's last point, so they add exactly 0 and
 // never trigger a pillar change: no per-slot guards.
-template <int J0>
+template <int J0, int UN>
 __device__ __forceinline__ void fwd_step8(const __amdgpu_buffer_rsrc_t rf, int rowoff, float pr,
                                           int lane_off, int kbase, int klast, int &p, int &pend,
                                           const int *O, float4 &acc, bool &first, float *carry4,
                                           int *carry_pg, float *tile_l, int TP, int lg) {
-  float4 f[8];
-  float w[8];
+  float4 f[UN];
+  float w[UN];
 #define E2EP_LD(U)                                               \
   f[U] = bload4(rf, row_bcast<J0 + U>(rowoff) + lane_off);      \
   w[U] = row_bcast<J0 + U>(pr);
   E2EP_LD(0) E2EP_LD(1) E2EP_LD(2) E2EP_LD(3) E2EP_LD(4) E2EP_LD(5) E2EP_LD(6) E2EP_LD(7)
+  if constexpr (UN == 16) {
+    E2EP_LD(8) E2EP_LD(9) E2EP_LD(10) E2EP_LD(11) E2EP_LD(12) E2EP_LD(13) E2EP_LD(14) E2EP_LD(15)
+  }
 #undef E2EP_LD
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < UN; ++u) {
     if (min(kbase + J0 + u, klast) >= pend) {  // pillar p complete (group-uniform)
       if (first) {
         *reinterpret_cast<float4 *>(carry4) = acc;
@@ -304,7 +307,7 @@ __device__ __forceinline__ void fwd_step8(const __amdgpu_buffer_rsrc_t rf, int r
 
 __device__ long long *g_fwd_trace;  // diagnostics: per-block (start, end, hw id, points)
 
-template <int T, int NG>
+template <int T, int NG, int UN>
 __global__ void __launch_bounds__(NG * 16) k_lss_fwd(
     const float *__restrict__ prob, const float *__restrict__ featT,
     const int *__restrict__ offsets, const int *__restrict__ order,
@@ -375,11 +378,16 @@ __global__ void __launch_bounds__(NG * 16) k_lss_fwd(
       const float pr = bload(rp, valid ? (bn * DHW + d * HW + pix) * 4 : OOR);
       const int rowoff = valid ? (bn * HWC + pix * C) * 4 : 0;
       const int klast = ke - 1;
-      fwd_step8<0>(rf, rowoff, pr, lane_off, k0, klast, p, pend, O, acc, first, &carry[g][4 * lg],
-                   &carry_p[g], tile_l, TP, lg);
-      if (k0 + 8 < ke)
-        fwd_step8<8>(rf, rowoff, pr, lane_off, k0, klast, p, pend, O, acc, first,
-                     &carry[g][4 * lg], &carry_p[g], tile_l, TP, lg);
+      if constexpr (UN == 16) {  // all 16 rows of the batch in flight together
+        fwd_step8<0, 16>(rf, rowoff, pr, lane_off, k0, klast, p, pend, O, acc, first,
+                         &carry[g][4 * lg], &carry_p[g], tile_l, TP, lg);
+      } else {
+        fwd_step8<0, 8>(rf, rowoff, pr, lane_off, k0, klast, p, pend, O, acc, first,
+                        &carry[g][4 * lg], &carry_p[g], tile_l, TP, lg);
+        if (k0 + 8 < ke)
+          fwd_step8<8, 8>(rf, rowoff, pr, lane_off, k0, klast, p, pend, O, acc, first,
+                          &carry[g][4 * lg], &carry_p[g], tile_l, TP, lg);
+      }
     }
     if (first) {  // the chunk's last pillar
       *reinterpret_cast<float4 *>(&carry[g][4 * lg]) = acc;
@@ -808,9 +816,17 @@ int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
     const int vec = ((uintptr_t)bev & 15) == 0 && XYZ % 4 == 0 && bev_bstride % 4 == 0;
     const int ll = tiles ? lss_lane_len(B, XYZ) : 0;
     const int gx = ll ? 8 * ll : cdiv(XYZ, E2EP_LSS_TILE) * B;
-    hipLaunchKernelGGL((k_lss_fwd<E2EP_LSS_TILE, 16>), dim3(gx, cdiv(C, 64)), dim3(256), 0,
-                       as_stream(stream), prob, featT, offsets, order, tiles, B, N, D, hw, C, XYZ,
-                       N * D * hw, bev, bev_bstride, vec, ll);
+    // e2ep_tune key 32: groups per block x rows in flight per group (A/B)
+    const int v = g_tune[TUNE_LSS_FWD];
+#define E2EP_LSSF(NGV, UNV)                                                                      \
+  hipLaunchKernelGGL((k_lss_fwd<E2EP_LSS_TILE, NGV, UNV>), dim3(gx, cdiv(C, 64)), dim3(NGV * 16), \
+                     0, as_stream(stream), prob, featT, offsets, order, tiles, B, N, D, hw, C,    \
+                     XYZ, N * D * hw, bev, bev_bstride, vec, ll)
+    if (v == 2) E2EP_LSSF(32, 8);
+    else if (v == 3) E2EP_LSSF(16, 16);
+    else if (v == 4) E2EP_LSSF(32, 16);
+    else E2EP_LSSF(16, 8);
+#undef E2EP_LSSF
   }
   return launch_status("e2ep_lss_fwd");
 }

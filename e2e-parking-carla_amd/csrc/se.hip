@@ -8,7 +8,6 @@
 // dx = dy * sigmoid(a) + dpooled / HW in a single stream — no separate avg-pool backward and
 // no autograd add of the two input-gradient paths.
 #include "common.h"
-#include "handoff.h"
 
 namespace e2ep {
 
@@ -147,16 +146,41 @@ __global__ void __launch_bounds__(256) k_se_excite(const float *__restrict__ x, 
   }
 }
 
+// The block's _bn1 backward sums, taken in the same pass (BNS, training BN with the SE input
+// transform): with xhat = (x - mean) invstd, zb = xhat gamma + beta (the arithmetic of
+// bn.hip's BnBwdElem) and sp = swish'(zb), the BN backward's channel sums of
+// dzb = (dy sigmoid(a) + dpooled / HW) sp factor per plane into
+//   A1 = sum dy sp,  A2 = sum sp,  A3 = sum dy sp xhat,  A4 = sum sp xhat
+// (fp64 per plane), which e2ep_bn_bwd_planes combines with the gate once dpooled is known —
+// the BN backward's own reduction pass over x and dy is not run.
+struct SeBn {
+  const float *mean, *invstd, *gamma, *beta;
+  double *sums;  // [planes][4]
+};
+__device__ __forceinline__ float swish_d(float z) {
+  const float s = 1.f / (1.f + expf(-z));
+  return s * (1.f + z * (1.f - s));
+}
+
 // da[plane] = s (1 - s) sum_hw dy * x      (wave per plane)
+template <bool BNS>
 __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn tf,
                                                const float *__restrict__ dy,
                                                const float *__restrict__ a, int planes, int HW,
-                                               float *__restrict__ da) {
+                                               float *__restrict__ da, SeBn bn) {
   const int pl = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (pl >= planes) return;
   const bool t = tf.sc != nullptr;
   const int c = pl % tf.C;
   const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
+  float mu = 0.f, is = 1.f, gm = 1.f, bt = 0.f;
+  if constexpr (BNS) {
+    mu = bn.mean[c];
+    is = bn.invstd[c];
+    gm = bn.gamma ? bn.gamma[c] : 1.f;
+    bt = bn.beta ? bn.beta[c] : 0.f;
+  }
+  double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
   const float *xp = x + (size_t)pl * HW, *gp = dy + (size_t)pl * HW;
   float acc = 0.f;
   if ((HW & 3) == 0) {
@@ -175,12 +199,48 @@ __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn
         if (i0 + u * 64 >= HW4) break;
         const float4 w = se_in4(xv[u], sc, sh, t), g = gv[u];
         acc += (w.x * g.x + w.y * g.y) + (w.z * g.z + w.w * g.w);
+        if constexpr (BNS) {
+          const float xv4[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+          const float gv4[4] = {g.x, g.y, g.z, g.w};
+          float a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float xh = (xv4[j] - mu) * is;
+            const float sp = swish_d(xh * gm + bt);
+            a1 += gv4[j] * sp;
+            a2 += sp;
+            a3 += gv4[j] * sp * xh;
+            a4 += sp * xh;
+          }
+          s1 += a1; s2 += a2; s3 += a3; s4 += a4;
+        }
       }
     }
   } else {
-    for (int i = lane; i < HW; i += 64) acc += se_in(xp[i], sc, sh, t) * gp[i];
+    for (int i = lane; i < HW; i += 64) {
+      const float xv = xp[i], g = gp[i];
+      acc += se_in(xv, sc, sh, t) * g;
+      if constexpr (BNS) {
+        const float xh = (xv - mu) * is;
+        const float sp = swish_d(xh * gm + bt);
+        s1 += g * sp; s2 += sp; s3 += g * sp * xh; s4 += sp * xh;
+      }
+    }
   }
   acc = wave_sum(acc);
+  if constexpr (BNS) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+      s3 += __shfl_xor(s3, o, 64);
+      s4 += __shfl_xor(s4, o, 64);
+    }
+    if (lane == 0) {
+      double *o = bn.sums + 4LL * pl;
+      o[0] = s1; o[1] = s2; o[2] = s3; o[3] = s4;
+    }
+  }
   if (lane == 0) {
     const float s = sigm(a[pl]);
     da[pl] = acc * s * (1.f - s);
@@ -300,198 +360,9 @@ __global__ void __launch_bounds__(256) k_se_dx(const float *__restrict__ dy,
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Fused forms (e2ep_tune key 27 = 2; OFF by default): the MLP on the 1x1 map runs inside the
-// streaming kernels instead of as launches of its own.  Measured in the replayed C2 step
-// (profiles/r04/se_fold_ab.txt): 25.7 vs 23.9 ms/step — k_se_squeeze_mlp 56 us against 13 + 5
-// for squeeze + hidden, k_se_da_mlp 66 us against 20 + 8 + 6 — because every one of the
-// thousands of small streaming workgroups (4 planes, 4 KB at 16x16) now ends in a
-// write-through store drain and a returning device-scope atomic (several us each under
-// load, paid once per residency round), which costs more than the launches it saves.
-//  * k_se_squeeze_mlp: the squeeze; a sample's C/4 workgroups store their plane means
-//    write-through and take an arrival ticket (handoff.h); the sample's last workgroup reads
-//    the C means back (sc1) and computes hpre[n][k] = W1[k] . pooled[n] + b1[k] for every k.
-//  * k_se_excite_logits: the excite; each workgroup first forms the logits a of the planes it
-//    covers (a wave per plane: W2[c] . swish(hpre[n]) + b2[c]), the workgroup holding a
-//    plane's first element stores it for the backward.
-//  * k_se_da_mlp: da per plane as k_se_da; a sample's last workgroup then forms
-//    dh = W2^T da[n], dhpre = dh * swish'(hpre), dpooled[n] = W1^T dhpre.
-// Every sum runs in a fixed order, so results are run-to-run deterministic.  Needs C % 4 == 0
-// (a workgroup's four planes belong to one sample).
-// ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_se_squeeze_mlp(const float *__restrict__ x, SeIn tf,
-                                                        int HW, const float *__restrict__ w1,
-                                                        const float *__restrict__ b1, int sq,
-                                                        float *__restrict__ pooled,
-                                                        float *__restrict__ hpre,
-                                                        unsigned int *__restrict__ cnt) {
-  __shared__ float sp[SE_MAXC];
-  __shared__ int s_last;
-  const int C = tf.C;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pl = blockIdx.x * 4 + wave;
-  const int n = (blockIdx.x * 4) / C;
-  const bool t = tf.sc != nullptr;
-  const int c = pl - n * C;
-  const float s = plane_sum(x + (size_t)pl * HW, HW, lane, t ? tf.sc[c] : 1.f, t ? tf.sh[c] : 0.f, t);
-  if (lane == 0) st_sc1(pooled + pl, s / (float)HW);
-  handoff_drain();
-  if (!handoff_arrive(cnt + n, C / 4, &s_last)) return;
-  for (int i = threadIdx.x; i < C; i += 256) sp[i] = ld_sc1(pooled + (size_t)n * C + i);
-  __syncthreads();
-  for (int k = wave; k < sq; k += 4) {  // k_se_hidden's dot, one wave per hidden unit
-    const float *wr = w1 + (size_t)k * C;
-    float s0 = 0.f, s1 = 0.f;
-    int i = lane;
-    for (; i + 64 < C; i += 128) {
-      s0 += wr[i] * sp[i];
-      s1 += wr[i + 64] * sp[i + 64];
-    }
-    if (i < C) s0 += wr[i] * sp[i];
-    const float h = wave_sum(s0 + s1);
-    if (lane == 0) hpre[(size_t)n * sq + k] = h + (b1 ? b1[k] : 0.f);
-  }
-}
-
-constexpr int SE_XPL = 32;  // planes one excite workgroup may cover (>= 16 elements per plane)
-__global__ void __launch_bounds__(256) k_se_excite_logits(const float *__restrict__ x, SeIn tf,
-                                                          const float *__restrict__ hpre,
-                                                          const float *__restrict__ w2,
-                                                          const float *__restrict__ b2, int sq,
-                                                          int HW, long long nvec, int vec,
-                                                          float *__restrict__ a,
-                                                          float *__restrict__ y) {
-  __shared__ float sa[SE_XPL];
-  const int C = tf.C;
-  const int per = vec ? HW >> 2 : HW;  // vector elements per plane
-  const long long i0 = (long long)blockIdx.x * 256;
-  const long long i1 = min(nvec, i0 + 256) - 1;
-  const long long pl0 = i0 / per;
-  const int np = (int)(i1 / per - pl0) + 1;  // host guarantees <= SE_XPL
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int j = wave; j < np; j += 4) {
-    const long long pl = pl0 + j;
-    const int n = (int)(pl / C), c = (int)(pl - (long long)n * C);
-    const float *wr = w2 + (size_t)c * sq, *hr = hpre + (size_t)n * sq;
-    float s = 0.f;
-    for (int k = lane; k < sq; k += 64) {
-      const float z = hr[k];
-      s += wr[k] * (z * sigm(z));
-    }
-    s = wave_sum(s) + (b2 ? b2[c] : 0.f);
-    if (lane == 0) {
-      sa[j] = s;
-      if (pl * per >= i0) a[pl] = s;  // the workgroup holding the plane's first element
-    }
-  }
-  __syncthreads();
-  const long long i = i0 + threadIdx.x;
-  if (i >= nvec) return;
-  const bool t = tf.sc != nullptr;
-  const long long pl = i / per;
-  const int c = (int)(pl % C);
-  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
-  const float g = sigm(sa[pl - pl0]);
-  if (vec) {
-    float4 v = se_in4(reinterpret_cast<const float4 *>(x)[i], sc, sh, t);
-    v.x *= g; v.y *= g; v.z *= g; v.w *= g;
-    reinterpret_cast<float4 *>(y)[i] = v;
-  } else {
-    y[i] = se_in(x[i], sc, sh, t) * g;
-  }
-}
-
-__global__ void __launch_bounds__(256) k_se_da_mlp(const float *__restrict__ x, SeIn tf,
-                                                   const float *__restrict__ dy,
-                                                   const float *__restrict__ a, int HW,
-                                                   const float *__restrict__ w1,
-                                                   const float *__restrict__ w2,
-                                                   const float *__restrict__ hpre, int sq, int KT,
-                                                   float *__restrict__ da,
-                                                   float *__restrict__ dhpre,
-                                                   float *__restrict__ dpooled,
-                                                   unsigned int *__restrict__ cnt) {
-  __shared__ float sda[SE_MAXC];
-  __shared__ float red[256];
-  __shared__ float sdh[SE_MAXSQ];
-  __shared__ int s_last;
-  const int C = tf.C;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pl = blockIdx.x * 4 + wave;
-  const int n = (blockIdx.x * 4) / C;
-  const bool t = tf.sc != nullptr;
-  const int c = pl - n * C;
-  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
-  const float *xp = x + (size_t)pl * HW, *gp = dy + (size_t)pl * HW;
-  float acc = 0.f;
-  if ((HW & 3) == 0) {
-    const int HW4 = HW >> 2;
-    const float4 *x4 = reinterpret_cast<const float4 *>(xp), *g4 = reinterpret_cast<const float4 *>(gp);
-    for (int i0 = lane; i0 < HW4; i0 += 64 * SE_U) {
-      float4 xv[SE_U], gv[SE_U];
-#pragma unroll
-      for (int u = 0; u < SE_U; ++u) {
-        const int i = min(i0 + u * 64, HW4 - 1);
-        xv[u] = x4[i];
-        gv[u] = g4[i];
-      }
-#pragma unroll
-      for (int u = 0; u < SE_U; ++u) {
-        if (i0 + u * 64 >= HW4) break;
-        const float4 w = se_in4(xv[u], sc, sh, t), g = gv[u];
-        acc += (w.x * g.x + w.y * g.y) + (w.z * g.z + w.w * g.w);
-      }
-    }
-  } else {
-    for (int i = lane; i < HW; i += 64) acc += se_in(xp[i], sc, sh, t) * gp[i];
-  }
-  acc = wave_sum(acc);
-  if (lane == 0) {
-    const float s = sigm(a[pl]);
-    st_sc1(da + pl, acc * s * (1.f - s));
-  }
-  handoff_drain();
-  if (!handoff_arrive(cnt + n, C / 4, &s_last)) return;
-  for (int i = threadIdx.x; i < C; i += 256) sda[i] = ld_sc1(da + (size_t)n * C + i);
-  __syncthreads();
-  // dh[k] = sum_c W2[c][k] da[n][c]: KT hidden-unit lanes x 256/KT channel slices (a W2 row
-  // is read by consecutive threads), slices summed in order
-  {
-    const int k = threadIdx.x % KT, sl = threadIdx.x / KT, nsl = 256 / KT;
-    float s = 0.f;
-    if (k < sq)
-#pragma unroll 4
-      for (int i = sl; i < C; i += nsl) s += w2[(size_t)i * sq + k] * sda[i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x < KT && k < sq) {
-      float tt = 0.f;
-      for (int q = 0; q < nsl; ++q) tt += red[q * KT + k];
-      const float z = hpre[(size_t)n * sq + k], sg = sigm(z);
-      const float g = tt * (sg * (1.f + z * (1.f - sg)));
-      dhpre[(size_t)n * sq + k] = g;
-      sdh[k] = g;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < C; i += 256) {  // dpooled[n][c] = sum_k W1[k][c] dhpre[n][k]
-    float s = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < sq; ++k) s += w1[(size_t)k * C + i] * sdh[k];
-    dpooled[(size_t)n * C + i] = s;
-  }
-}
-
 }  // namespace e2ep
 
 using namespace e2ep;
-
-// fused squeeze-excitation launches (e2ep_tune key 27 = 2): a workgroup's four planes in one
-// sample; an excite workgroup of 256 vector elements covers at most 255 / 16 + 2 <= SE_XPL
-// planes when a plane has >= 16 of them
-static bool se_fused_ok(int C, int HW) {
-  return g_tune[TUNE_SE_FUSED] == 2 && C % 4 == 0 && ((HW & 3) == 0 ? HW / 4 : HW) >= 16;
-}
 
 extern "C" {
 
@@ -507,14 +378,6 @@ int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, cons
   const int planes = N * C;
   const int vec = (HW & 3) == 0;
   const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
-  unsigned int *cnt = se_fused_ok(C, HW) ? handoff_slots(N) : nullptr;
-  if (cnt) {  // two launches: squeeze + hidden units, logits + excite
-    hipLaunchKernelGGL(k_se_squeeze_mlp, dim3(planes / 4), dim3(256), 0, s, x, tf, HW, w1, b1, sq,
-                       pooled, hpre, cnt);
-    hipLaunchKernelGGL(k_se_excite_logits, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, tf, hpre,
-                       w2, b2, sq, HW, nvec, vec, a, y);
-    return launch_status("e2ep_se_fwd");
-  }
   hipLaunchKernelGGL(k_se_squeeze, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, planes, HW,
                      pooled);
   hipLaunchKernelGGL(k_se_hidden, dim3(N, cdiv(sq, 4)), dim3(256), 0, s, pooled, w1, b1, C, sq,
@@ -526,10 +389,11 @@ int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, cons
   return launch_status("e2ep_se_fwd");
 }
 
-int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, const float *dy,
-                const float *w1, const float *w2, const float *pooled, const float *hpre,
-                const float *a, int N, int C, int HW, int sq, float *dx, float *dpooled_out,
-                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream) {
+static int se_bwd_impl(const float *x, const float *x_scale, const float *x_shift,
+                       const float *dy, const float *w1, const float *w2, const float *pooled,
+                       const float *hpre, const float *a, int N, int C, int HW, int sq, float *dx,
+                       float *dpooled_out, float *dw1, float *db1, float *dw2, float *db2,
+                       float *workspace, const SeBn &bn, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && HW > 0 && sq > 0, E2EP_EINVAL, "e2ep_se_bwd: bad shape");
   E2EP_REQUIRE(!x_scale == !x_shift, E2EP_EINVAL, "e2ep_se_bwd: x_scale / x_shift both or neither");
   E2EP_REQUIRE(!(x_scale && dx), E2EP_EINVAL,
@@ -546,16 +410,15 @@ int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, cons
   const int spans = cdiv(C, SE_DH_SPAN);
   int KT = 1;
   while (KT < sq) KT *= 2;
-  unsigned int *cnt = se_fused_ok(C, HW) ? handoff_slots(N) : nullptr;
-  if (cnt) {  // da + the MLP backward in one launch
-    hipLaunchKernelGGL(k_se_da_mlp, dim3(planes / 4), dim3(256), 0, s, x, tf, dy, a, HW, w1, w2,
-                       hpre, sq, KT, da, dhpre, dpooled, cnt);
-  } else {
-    hipLaunchKernelGGL(k_se_da, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes, HW, da);
-    hipLaunchKernelGGL(k_se_dh, dim3(N, spans), dim3(256), 0, s, da, w2, C, sq, KT, dhp);
-    hipLaunchKernelGGL(k_se_dpooled, dim3(N, cdiv(C, 256)), dim3(256), 0, s, dhp, spans, hpre, w1,
-                       C, sq, dhpre, dpooled);
-  }
+  if (bn.sums)
+    hipLaunchKernelGGL(k_se_da<true>, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes,
+                       HW, da, bn);
+  else
+    hipLaunchKernelGGL(k_se_da<false>, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes,
+                       HW, da, bn);
+  hipLaunchKernelGGL(k_se_dh, dim3(N, spans), dim3(256), 0, s, da, w2, C, sq, KT, dhp);
+  hipLaunchKernelGGL(k_se_dpooled, dim3(N, cdiv(C, 256)), dim3(256), 0, s, dhp, spans, hpre, w1,
+                     C, sq, dhpre, dpooled);
   if (dw1 || db1 || dw2 || db2) {
     const int outs = 2 * sq * C + sq + C;
     hipLaunchKernelGGL(k_se_wgrad, dim3(cdiv(outs, 256)), dim3(256), 0, s, pooled, hpre, da, dhpre,
@@ -568,6 +431,28 @@ int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, cons
                        dx);
   }
   return launch_status("e2ep_se_bwd");
+}
+
+int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, const float *dy,
+                const float *w1, const float *w2, const float *pooled, const float *hpre,
+                const float *a, int N, int C, int HW, int sq, float *dx, float *dpooled_out,
+                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream) {
+  return se_bwd_impl(x, x_scale, x_shift, dy, w1, w2, pooled, hpre, a, N, C, HW, sq, dx,
+                     dpooled_out, dw1, db1, dw2, db2, workspace, SeBn{}, stream);
+}
+
+int e2ep_se_bwd_bn(const float *x, const float *x_scale, const float *x_shift,
+                   const float *bn_mean, const float *bn_invstd, const float *gamma,
+                   const float *beta, const float *dy, const float *w1, const float *w2,
+                   const float *pooled, const float *hpre, const float *a, int N, int C, int HW,
+                   int sq, float *dpooled_out, float *dw1, float *db1, float *dw2, float *db2,
+                   double *plane_sums, float *workspace, void *stream) {
+  E2EP_REQUIRE(x_scale && x_shift && bn_mean && bn_invstd && dpooled_out && plane_sums,
+               E2EP_EINVAL, "e2ep_se_bwd_bn: the BN transform, its statistics, dpooled_out and "
+               "plane_sums are required");
+  return se_bwd_impl(x, x_scale, x_shift, dy, w1, w2, pooled, hpre, a, N, C, HW, sq, nullptr,
+                     dpooled_out, dw1, db1, dw2, db2, workspace,
+                     SeBn{bn_mean, bn_invstd, gamma, beta, plane_sums}, stream);
 }
 
 }  // extern "C"

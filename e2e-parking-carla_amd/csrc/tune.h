@@ -30,12 +30,13 @@ enum Tune {
   TUNE_DW_FWD_BLOCKS = 24,    // depthwise forward / stride-1 data-gradient strip kernel: grid cap (blocks)
   TUNE_BNS_WIDE = 25,         // single-launch BN, channels of 1025..2048 float4: 2 = 512 threads x 4, 1 = 256 x 8
   TUNE_BNS_WIDE_LO = 26,      // the same for channels of 257..1024 float4: 2 = 512 threads x 1 / 2, 1 = 256 x 2 / 4
-  TUNE_SE_FUSED = 27,         // squeeze-excitation MLP inside the squeeze / excite / da launches: 2 = on, 1 = separate kernels (default: measured 1.8 ms/step slower fused)
+  TUNE_RETIRED_27 = 27,       // retired (was the fused squeeze-excitation MLP: 1.8 ms/step slower, removed)
   TUNE_SPLITK_FOLD = 28,      // split-K reductions folded into the producing launch (last-arriving split sums): 2 = on, 1 = separate reduce kernels
-  TUNE_PAIR_ORDER = 29,       // conv paired backward (k_conv_bwd_pair, k_lp_bwd_pair): 2 = weight-gradient blocks first, 1 = data-gradient blocks first
+  TUNE_RETIRED_29 = 29,       // retired (was the conv pair block order: data-gradient first kept)
   TUNE_PAIR1X1_ORDER = 30,    // 1x1 paired backward (k_conv_bwd_pair1x1): 2 = weight-gradient blocks first (default: C2 22.73 -> 22.50 ms), 1 = data-gradient blocks first
-  TUNE_LINEAR_PAIR_ORDER = 31, // linear paired backward (k_gemm_pair): 2 = weight-gradient blocks first, 1 = input-gradient blocks first
-  TUNE_N = 32
+  TUNE_RETIRED_31 = 31,       // retired (was the linear pair block order: input-gradient first kept)
+  TUNE_LSS_FWD = 32,          // k_lss_fwd shape: 1 = 16 groups x 8 rows in flight, 2 = 32 x 8, 3 = 16 x 16, 4 = 32 x 16
+  TUNE_N = 33
 };
 extern int g_tune[TUNE_N];
 }  // namespace e2ep

@@ -9,7 +9,7 @@ import os
 
 import torch
 
-from . import _lib, timing
+from . import _lib, streams, timing
 
 
 def _ws(nbytes, device):
@@ -215,8 +215,7 @@ def wgrad_overlap():
 
 
 def side_stream(device):
-    """The weight-gradient side stream of the current stream (one per stream, so branches
-    already on side streams — e2ep_amd.streams — fork onto streams of their own)."""
+    """The weight-gradient side stream of the current stream (one per stream)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     st = _SIDE.get(key)
@@ -228,11 +227,19 @@ def side_stream(device):
 class _Fork:
     """with _Fork(dev) as side: ...launches on `side`...  — forks from the current stream on
     entry (side waits for it); join() makes the current stream wait for the side stream.
-    work_us: the side work's estimate (est_us); below E2EP_FORK_MIN_US it stays serial."""
+    work_us: the side work's estimate (est_us); below E2EP_FORK_MIN_US it stays serial.
+
+    Never forks from a model-branch side stream (e2ep_amd.streams): a stream forked from a
+    stream that is itself forked from the capture origin made hipStreamEndCapture segfault
+    when the step was graph-captured (scripts/diag_branch_capture.py: model_cam crashed, the
+    same capture with no fork inside the branch — model_cam_nofork — replayed correctly;
+    profiles/r05/diag_branch_capture.log).  Inside a branch the weight gradient runs after
+    the data gradient on the branch's stream, which still overlaps the main stream."""
 
     def __init__(self, device, on=True, work_us=float("inf")):
-        self.on = on and _OVERLAP[0] and work_us >= _FORK_MIN_US[0]
         self.main = torch.cuda.current_stream(device)
+        self.on = (on and _OVERLAP[0] and work_us >= _FORK_MIN_US[0]
+                   and not streams.is_branch_stream(self.main))
         self.side = side_stream(device) if self.on else self.main
 
     def __enter__(self):

@@ -8,6 +8,7 @@ import ctypes
 
 import torch
 import torch.distributed as dist
+from torch.utils._python_dispatch import TorchDispatchMode
 
 from . import _lib
 
@@ -24,20 +25,48 @@ def capture_mode():
     return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
 
 
+class _SeededOps(TorchDispatchMode):
+    """Records the aten ops tagged nondeterministic_seeded (torch.rand, dropout, bernoulli_,
+    ...) that run while a graph is captured: they draw from torch's generators, whose state a
+    captured graph reads from the per-replay prologue of torch.cuda.CUDAGraph.replay()."""
+
+    def __init__(self):
+        super().__init__()
+        self.seen = []
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        if torch.Tag.nondeterministic_seeded in func.tags:
+            self.seen.append(str(func))
+        return func(*args, **(kwargs or {}))
+
+
 class Graph:
     """A captured, repaired graph with its own executable (e2ep_graph_exec_*): replay()
     launches it on the current stream without torch.cuda.CUDAGraph.replay()'s prologue, which
     refreshes torch's generator states with int64 fill kernels before every launch (the step
     draws its random numbers from e2ep_rng_draw, not from torch's generators).  The torch
-    graph object stays alive: it owns the graph and its memory pool."""
+    graph object stays alive: it owns the graph and its memory pool.
 
-    def __init__(self, g):
+    A capture that drew from torch's generators (`torch_rng`: e.g. a user module's nn.Dropout,
+    or rng.py's torch fallbacks when no step pool is active) replays through torch's own
+    replay instead, whose prologue advances the generator offsets, so those draws differ from
+    replay to replay as they would eagerly."""
+
+    def __init__(self, g, torch_rng=()):
         self.g = g
+        self.torch_rng = tuple(torch_rng)
+        self._exec = None
+        if self.torch_rng:
+            g.instantiate()  # torch's executable of the repaired graph
+            return
         ex = ctypes.c_void_p()
         _lib.call("e2ep_graph_exec_create", ctypes.c_void_p(g.raw_cuda_graph()), ctypes.byref(ex))
         self._exec = ex
 
     def replay(self):
+        if self._exec is None:
+            self.g.replay()
+            return
         _lib.call("e2ep_graph_exec_launch", self._exec, _lib.stream())
 
     def pool(self):
@@ -52,11 +81,14 @@ class Graph:
 
 
 def capture(fn, pool=None):
-    """Capture fn() into a repaired graph with its own executable.  Returns (Graph, fn's
-    result, number of memset nodes rewritten)."""
+    """Capture fn() into a repaired graph with its own executable (torch's, when fn drew from
+    torch's generators: Graph).  Returns (Graph, fn's result, number of memset nodes
+    rewritten)."""
     g = torch.cuda.CUDAGraph(keep_graph=True)
+    seeded = _SeededOps()
     with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_mode()):
-        out = fn()
+        with seeded:
+            out = fn()
     n = ctypes.c_int(0)
     _lib.call("e2ep_graph_replace_memsets", ctypes.c_void_p(g.raw_cuda_graph()), ctypes.byref(n))
-    return Graph(g), out, n.value
+    return Graph(g, seeded.seen), out, n.value

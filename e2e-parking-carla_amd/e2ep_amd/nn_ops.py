@@ -572,6 +572,18 @@ class _SqueezeExcite(torch.autograd.Function):
         return dx, dw1, db1, dw2, db2
 
 
+# E2EP_BN_SE_SUMS=0: the _bn1 backward takes its own reduction pass (e2ep_bn_bwd) instead of
+# the sums from the SE's da pass (A/B)
+_SE_BN_SUMS = [os.environ.get("E2EP_BN_SE_SUMS", "1") != "0"]
+
+
+def set_se_bn_sums(on):
+    """Enable / disable the _bn1 backward sums from the SE pass (returns the previous setting)."""
+    prev = _SE_BN_SUMS[0]
+    _SE_BN_SUMS[0] = bool(on)
+    return prev
+
+
 class _BnSwishSE(torch.autograd.Function):
     """squeeze_excite(batch_norm_act(x, bn, 'swish'), ...) with the BN + swish applied on load
     by the SE kernels (MBConv _bn1 -> swish -> SE, reference model/cam_encoder.py:69-73 via
@@ -630,14 +642,33 @@ class _BnSwishSE(torch.autograd.Function):
         db2 = torch.empty(C, **f32) if (hb2 and nig[11]) else None
         dpooled = torch.empty(N, C, **f32)
         ws = torch.empty(2 * N * C + 17 * N * sq, **f32)
+        dx = torch.empty_like(x) if nig[0] else None
+        dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
+        db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
+        # training BN on the split path: its channel sums are taken in the SE's da pass
+        # (e2ep_se_bwd_bn), so the BN backward is its apply pass alone
+        fused = (_SE_BN_SUMS[0] and ctx.train and dx is not None
+                 and _lib.load().e2ep_bn_bwd_split(N, C, H, W) == 1)
+        if fused:
+            planes = torch.empty(N * C * 4, dtype=torch.float64, device=dev)
+            with timing.region(timing.name("se_bwd", x.shape, "_BnSwishSE")):
+                _lib.call("e2ep_se_bwd_bn", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
+                          _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta),
+                          _lib.ptr(dy), _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled),
+                          _lib.ptr(hpre), _lib.ptr(a), N, C, H * W, sq, _lib.ptr(dpooled),
+                          _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2),
+                          _lib.ptr(planes), _lib.ptr(ws), s)
+            with timing.region(timing.name("bn_bwd", x.shape, "_BnSwishSE")):
+                _lib.call("e2ep_bn_bwd_planes", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(stats[0]),
+                          _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(a),
+                          _lib.ptr(dpooled), _lib.ptr(planes), N, C, H, W, ACT["swish"],
+                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), s)
+            return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None
         with timing.region(timing.name("se_bwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
                       _lib.ptr(dy), _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled),
                       _lib.ptr(hpre), _lib.ptr(a), N, C, H * W, sq, None, _lib.ptr(dpooled),
                       _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2), _lib.ptr(ws), s)
-        dx = torch.empty_like(x) if nig[0] else None
-        dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
-        db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
         if dx is not None or dg is not None or db is not None:
             bws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
             with timing.region(timing.name("bn_bwd", x.shape, "_BnSwishSE")):

@@ -15,11 +15,14 @@ HIP-graph capture of the step records both chains as parallel branches.  Tensors
 between the streams are handed to the caching allocator with record_stream, so their memory
 is not recycled while the other stream may still use it.
 
-Branches are named so each can be switched off for A/B timing: E2EP_BRANCH_STREAMS is a
-comma list of enabled names (default: none — a HIP-graph capture of the train step with
-either branch on segfaults inside hipStreamEndCapture on this ROCm (scripts/
-diag_branch_capture.py: toy two-stream captures replay fine, the model's branches crash), so
-they are opt-in for eager A/B timing):
+No stream is forked from a branch's stream: the conv / depthwise / linear backward's
+weight-gradient fork (conv._Fork) stays on the branch stream there.  With such nested forks a
+HIP-graph capture of the train step segfaulted inside hipStreamEndCapture (rounds 2 and 4);
+without them the same capture replays correctly (scripts/diag_branch_capture.py, variants
+model_cam / model_cam_nofork).
+
+Branches are named so each can be switched on for A/B timing: E2EP_BRANCH_STREAMS is a
+comma list of enabled names (default: none, see DESIGN.md for the measurement):
   cam    the camera encoder's depth head next to its feature head (model/cam_encoder.py)
   heads  the segmentation head next to the control decoder (model/parking_model.py)
 """
@@ -41,6 +44,11 @@ def set_enabled(names):
     prev = set(_ENABLED)
     _ENABLED = set(names)
     return prev
+
+
+def is_branch_stream(stream):
+    """True when `stream` is one of the branch side streams."""
+    return any(stream == st for st in _STREAMS.values())
 
 
 def _side(device, name):

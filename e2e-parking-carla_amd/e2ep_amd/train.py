@@ -13,18 +13,23 @@ __call__ refreshes from param_groups[0]['lr'] before each replay, so an LR sched
 Data parallelism (one process per GPU, RCCL over xGMI; DistributedDataParallel semantics
 without its module wrapper), one flat fp32 gradient buffer in FlatAdam's layout; the
 1/world mean is folded into the Adam launch.
-  * graph mode with RCCL (the bench at N > 1): the backward runs in two segments
+  * graph mode (the bench at N > 1): the backward runs in two segments
     (e2ep_amd.segments; the model cuts its forward below the BEV encoder): g_s1 (fwd + losses
     + stage-1 backward: heads, transformer, BEV encoder) -> g_s1g (their gradients -> the flat
     buffer) -> the host issues the stage-1 buckets' all-reduces (~25 MB each, reverse layout
     order) on a communication stream -> g_s2 (stage 2: lift-splat + camera encoder backward,
     concurrent with those all-reduces) -> g_s2g -> the stage-2 bucket(s) -> the compute stream
-    waits for every bucket -> g_opt.  No collective is captured: on this stack (torch 2.10 /
+    waits for every bucket -> g_opt.  With gloo and device tensors (the one-GPU rehearsal of
+    this path) the same graphs and bucket ranges run, each bucket staged through pinned host
+    memory: after g_s1g the comm stream copies the stage-1 buckets out, g_s2 is replayed, the
+    host waits for those copies only, all-reduces the buckets on the host (while stage 2 runs
+    on the GPU) and the comm stream copies them back; then the same for stage 2.  No
+    collective is captured: on this stack (torch 2.10 /
     RCCL 2.26) a captured ProcessGroupNCCL collective made the c10d watchdog fault on its
     capture-time event, and a backward graph with bucket gathers forked onto a side stream
     replayed wrong camera-encoder gradients (profiles/r02/ddp_diag/); here every
     collective is an ordinary host-issued RCCL call between graph replays.
-  * graph mode without cut points (or gloo): g_bwd (fwd + losses + bwd) -> g_gather -> ONE
+  * graph mode without cut points (or segment=False): g_bwd (fwd + losses + bwd) -> g_gather -> ONE
     all-reduce of the flat buffer issued from the host between the replays -> g_opt.
   * eager mode: DDP-style overlap — the buffer is cut into ~25 MB buckets in reverse layout
     order; a post-accumulate-grad hook per parameter counts arrivals and, when a bucket is
@@ -160,7 +165,8 @@ class GradBuckets:
 
 class TrainStep:
     def __init__(self, module, batch, lr=1e-4, weight_decay=1e-4, world=1, graph=True,
-                 warmup=3, optimizer=None, bucket_mb=BUCKET_MB, overlap=None, ddp=None):
+                 warmup=3, optimizer=None, bucket_mb=BUCKET_MB, overlap=None, ddp=None,
+                 segment=True):
         self.module = module
         self.batch = batch
         self.world = world
@@ -196,8 +202,10 @@ class TrainStep:
                       and self.flat_grad.is_cuda else None)
         self.loss = None
         self.g_bwd = self.g_gather = self.g_opt = None
-        # segmented backward (graph mode, RCCL): stage graphs, their gathers, bucket ranges
-        self.segmented = bool(self.ddp and graph and self.backend == "nccl")
+        # segmented backward (graph mode; RCCL, or gloo staged through self._host): stage
+        # graphs, their gathers, bucket ranges.  segment=False keeps one backward graph.
+        self.segmented = bool(segment and self.ddp and graph and
+                              (self.backend == "nccl" or self._host is not None))
         self.g_s1 = self.g_s1g = self.g_s2 = self.g_s2g = None
         self.seg_buckets = None  # ([stage-1 (lo, hi)], [stage-2 (lo, hi)]) of the flat buffer
         self._rig = _rig_key(batch)
@@ -316,10 +324,18 @@ class TrainStep:
         self.comm = torch.cuda.Stream(device=self.flat_grad.device)
         # which tensors have a gradient is fixed by the captured graphs: all-reduced once (MAX)
         self.opt.has_grad(self.has_grad)
-        dist.all_reduce(self.has_grad, op=dist.ReduceOp.MAX)
+        if self._host is None:
+            dist.all_reduce(self.has_grad, op=dist.ReduceOp.MAX)
+        else:
+            has = self.has_grad.cpu()  # synchronises the stream
+            dist.all_reduce(has, op=dist.ReduceOp.MAX)
+            self.has_grad.copy_(has)
         return True
 
     def _replay_segmented(self):
+        if self._host is not None:
+            self._replay_segmented_host()
+            return
         main = torch.cuda.current_stream()
         works = []
 
@@ -340,6 +356,46 @@ class TrainStep:
         issue(self.seg_buckets[1])
         for w in works:
             w.wait()  # the compute stream waits for every bucket
+        self.g_opt.replay()
+
+    def _replay_segmented_host(self):
+        """_replay_segmented for gloo with device tensors: the same graphs and bucket ranges,
+        each bucket staged through the pinned host buffer.  The comm stream copies a stage's
+        buckets out after its gather graph, the host waits for those copies only, all-reduces
+        the buckets on the host while the GPU runs on, and the comm stream copies them back;
+        the compute stream waits for the comm stream before the optimizer graph."""
+        main = torch.cuda.current_stream()
+        h, flat = self._host, self.flat_grad
+
+        def copy_out(ranges):
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                for lo, hi in ranges:
+                    h[lo:hi].copy_(flat[lo:hi], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(self.comm)
+            return done
+
+        def exchange(ranges, done):
+            done.synchronize()  # the host waits for this stage's copies, not for the GPU
+            works = [dist.all_reduce(h[lo:hi], async_op=True) for lo, hi in ranges]
+            for w in works:
+                w.wait()
+            with torch.cuda.stream(self.comm):
+                for lo, hi in ranges:
+                    flat[lo:hi].copy_(h[lo:hi], non_blocking=True)
+
+        self.g_s1.replay()
+        self.g_s1g.replay()
+        d1 = copy_out(self.seg_buckets[0])
+        self.g_s2.replay()  # stage 2 on the GPU while the host exchanges stage 1
+        exchange(self.seg_buckets[0], d1)
+        if self.g_s2g is not None:
+            self.g_s2g.replay()
+        exchange(self.seg_buckets[1], copy_out(self.seg_buckets[1]))
+        main.wait_stream(self.comm)
         self.g_opt.replay()
 
     # -- capture --------------------------------------------------------------------------

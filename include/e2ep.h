@@ -302,6 +302,17 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
                 float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
                 int H, int W, int train, int act, float *dx, float *dgamma, float *dbeta,
                 float *dres, void *workspace, size_t workspace_bytes, void *stream);
+/* 1 when e2ep_bn_bwd runs this shape as the split reduce + apply pair (a channel of more
+ * than 8192 elements, or the single-launch kernels switched off), 0 for the single launch. */
+int e2ep_bn_bwd_split(int N, int C, int H, int W);
+/* The apply half of e2ep_bn_bwd (training statistics, squeeze-excitation gate) whose channel
+ * sums come from e2ep_se_bwd_bn's per-plane factors instead of a reduction pass over x and dy:
+ * sum dzb = sum_n sigmoid(logit) A1 + dpooled / HW A2, sum dzb xhat = ... A3 / A4 (fp64).
+ * Same arguments and element arithmetic as e2ep_bn_bwd; no workspace. */
+int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const float *invstd,
+                       const float *gamma, const float *beta, const float *gate_logit,
+                       const float *gate_dpooled, const double *plane_sums, int N, int C, int H,
+                       int W, int act, float *dx, float *dgamma, float *dbeta, void *stream);
 /* Stand-alone activation (act as above) and its gradient w.r.t. the pre-activation x. */
 int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);
@@ -361,6 +372,18 @@ int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, cons
                 const float *w1, const float *w2, const float *pooled, const float *hpre,
                 const float *a, int N, int C, int HW, int sq, float *dx, float *dpooled_out,
                 float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream);
+/* e2ep_se_bwd (x_scale / x_shift transform, dx left to the BN) that also takes the block's
+ * _bn1 backward sums in its da pass over x and dy (MBConv _bn1 -> swish -> SE, reference
+ * model/cam_encoder.py:69-73): with xhat = (x - bn_mean) bn_invstd and sp = swish'(xhat gamma +
+ * beta), plane_sums [N*C][4] (fp64) = (sum dy sp, sum sp, sum dy sp xhat, sum sp xhat) per
+ * (n, c) plane, for e2ep_bn_bwd_planes (which then skips e2ep_bn_bwd's reduction pass).
+ * gamma / beta nullable (1 / 0). */
+int e2ep_se_bwd_bn(const float *x, const float *x_scale, const float *x_shift,
+                   const float *bn_mean, const float *bn_invstd, const float *gamma,
+                   const float *beta, const float *dy, const float *w1, const float *w2,
+                   const float *pooled, const float *hpre, const float *a, int N, int C, int HW,
+                   int sq, float *dpooled_out, float *dw1, float *db1, float *dw2, float *db2,
+                   double *plane_sums, float *workspace, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Residual add + dropout + LayerNorm of the post-norm transformer layers (torch
@@ -669,7 +692,11 @@ int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec);
  * reads, default; 1 = scalar reads), 24 depthwise forward / stride-1 data-gradient grid cap in
  * blocks (2048; each wave walks units beyond it in a software-pipelined loop), 25 single-launch BN
  * blocks for channels of 1025..2048 float4 (2 = 512 threads x 4 float4, default; 1 = 256 x 8),
- * 26 the same for channels of 257..1024 float4 (2 = 512 threads; 1 = 256, default: equal).
+ * 26 the same for channels of 257..1024 float4 (2 = 512 threads; 1 = 256, default: equal),
+ * 28 split-K reductions folded into the producing launch (2, default) or separate reduce
+ * kernels (1), 30 1x1 paired backward block order (2 = weight-gradient blocks first, default;
+ * 1 = data-gradient first).  Keys 27, 29 and 31 are retired (their A/B kept the default and the
+ * alternative code is removed): they return -1 like an unknown key.
  * For A/B timing.
  * Contract for every plan override and tunable above (e2ep_conv_split_params,
  * e2ep_gemm_force, e2ep_gemm_split_min, e2ep_bn_small*, e2ep_tune): a launch recomputes its

@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--cams", type=int, default=4)
     ap.add_argument("--image", type=int, default=256)
+    ap.add_argument("--fwd-variants", type=lambda t: [int(x) for x in t.split(",")], default=[1])
     a = ap.parse_args()
     dev = torch.device("cuda")
     cfg = default_cfg()
@@ -79,10 +80,22 @@ def main():
 
     fb = 4 * B * (N * C * hw + N * D * hw + C * XY)
     bb = 4 * B * (C * XY + 2 * N * C * hw + 2 * N * D * hw)
-    for name, fn, nb in (("lss_fwd", fwd, fb), ("lss_bwd", bwd, bb)):
-        t1, t2 = timeit(fn, a.iters), timeit_b2b(fn, a.iters)
-        print(f"{name} B={B} N={N} {a.image}^2: single {t1 * 1e3:.1f} us ({nb / t1 / 1e6:.0f} GB/s), "
-              f"back-to-back {t2 * 1e3:.1f} us ({nb / t2 / 1e6:.0f} GB/s); {nb / 1e6:.1f} MB algorithmic")
+    ref = None
+    for v in a.fwd_variants:  # e2ep_tune key 32: the forward's groups x rows in flight
+        prev = _lib.load().e2ep_tune(32, v)
+        fwd()
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = bev.clone()
+        same = torch.equal(bev, ref)  # every variant sums each pillar in the same order
+        t1, t2 = timeit(fwd, a.iters), timeit_b2b(fwd, a.iters)
+        print(f"lss_fwd[variant {v}] B={B} N={N} {a.image}^2: single {t1 * 1e3:.1f} us "
+              f"({fb / t1 / 1e6:.0f} GB/s), back-to-back {t2 * 1e3:.1f} us ({fb / t2 / 1e6:.0f} GB/s); "
+              f"{fb / 1e6:.1f} MB algorithmic; bitwise equal to variant {a.fwd_variants[0]}: {same}")
+        _lib.load().e2ep_tune(32, prev)
+    t1, t2 = timeit(bwd, a.iters), timeit_b2b(bwd, a.iters)
+    print(f"lss_bwd B={B} N={N} {a.image}^2: single {t1 * 1e3:.1f} us ({bb / t1 / 1e6:.0f} GB/s), "
+          f"back-to-back {t2 * 1e3:.1f} us ({bb / t2 / 1e6:.0f} GB/s); {bb / 1e6:.1f} MB algorithmic")
 
 
 if __name__ == "__main__":

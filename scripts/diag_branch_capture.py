@@ -14,6 +14,10 @@ replay compared with eager):
   model_heads   the same with branch "heads" only
   *_nofork      a model variant with the conv weight-gradient side streams off (no stream
                 forked from inside a branch)
+Round 5: model_cam crashed (exit -11 in capture_end) and model_cam_nofork / model_heads_nofork
+replayed, so the crash needs a stream forked from a branch stream; conv._Fork no longer forks
+from a branch stream, and model_cam / model_heads are expected to replay too
+(profiles/r05/diag_branch_capture*.log).
 """
 import os
 import subprocess
@@ -21,7 +25,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "e2e-parking-carla_amd"), ROOT, os.path.join(ROOT, "tests")]
-VARIANTS = os.environ.get("DIAG_VARIANTS", "toy_plain,toy_record,toy_e2ep,model_cam,model_heads").split(",")
+VARIANTS = os.environ.get("DIAG_VARIANTS", "model_cam,model_heads,model_cam_nofork,model_heads_nofork").split(",")
 
 
 def toy(kind):

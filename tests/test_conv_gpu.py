@@ -409,7 +409,7 @@ def test_conv_lp_fp32_all_geometries(case, tile):
                          ids=[str(i) for i in range(len(CASES) + 3)])
 @pytest.mark.parametrize("skip", [False, True], ids=["noskip", "skip"])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
-@pytest.mark.parametrize("order", [1, 2], ids=["dgrad_first", "wgrad_first"])  # keys 29 / 30
+@pytest.mark.parametrize("order", [1, 2], ids=["dgrad_first", "wgrad_first"])  # 1x1 pair order (key 30)
 def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode, order):
     """e2ep_conv_bwd (data and weight gradient in one k_conv_bwd_pair / k_lp_bwd_pair launch,
     where e2ep_conv_bwd_pair_ok) == e2ep_conv_dgrad_acc + e2ep_conv_wgrad on forked streams,
@@ -436,8 +436,7 @@ def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode, order):
     from e2ep_amd import _lib
     lib = _lib.load()
     prev = conv.set_conv_pair(False)
-    prev_order = lib.e2ep_tune(29, order)  # block order of the paired grids
-    prev_order1 = lib.e2ep_tune(30, order)
+    prev_order1 = lib.e2ep_tune(30, order)  # block order of the paired 1x1 grids
     try:
         with precision.use(mode):
             two = run()
@@ -445,7 +444,6 @@ def test_conv_bwd_pair_bitwise_equals_two_launches(case, skip, mode, order):
             one = run()
     finally:
         conv.set_conv_pair(prev)
-        lib.e2ep_tune(29, prev_order)
         lib.e2ep_tune(30, prev_order1)
     assert all(torch.equal(a, c) for a, c in zip(one, two))
 

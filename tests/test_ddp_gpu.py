@@ -8,9 +8,11 @@
   they overlap the stage-2 backward, captured Adam) and the eager step with the bucketed,
   hook-driven all-reduce overlapping backward both give the same parameters as the step
   without an exchange, bit for bit.
-* gloo at world 2, both ranks on cuda:0 (the one-GPU rehearsal of the N>1 path): the
-  host-staged flat gradient all-reduce of the real ParkingModel TrainStep with the same batch
-  on both ranks equals the one-process step (mean of two equal gradients), replay for replay.
+* gloo at world 2, both ranks on cuda:0 (the one-GPU rehearsal of the N>1 path): the default
+  graph-mode exchange — the segmented backward with the stage-1 buckets exchanged while stage 2
+  runs, each bucket staged through pinned host memory — of the real ParkingModel TrainStep with
+  the same batch on both ranks equals the one-process step (mean of two equal gradients) and
+  the single-graph exchange (segment=False), replay for replay.
 """
 import os
 import socket
@@ -143,11 +145,23 @@ def _gloo_worker(rank, world, port, out):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from e2ep_amd.train import TrainStep
-    m = _parking_module()
-    s = TrainStep(m, _parking_batch(), world=world, graph=True, warmup=1)
-    assert s.buckets is None and s._host is not None
-    losses = [float(s()) for _ in range(2)]
-    out[rank] = (losses, _flat_params(m))
+    for segment in (True, False):
+        m = _parking_module()
+        s = TrainStep(m, _parking_batch(), world=world, graph=True, warmup=1, bucket_mb=4.0,
+                      segment=segment)
+        assert s.buckets is None and s._host is not None
+        if segment:  # the default graph-mode exchange: stage buckets between segment replays
+            assert s.segmented and s.g_bwd is None and s.g_s2 is not None
+            b1, b2 = s.seg_buckets
+            assert len(b1) >= 3 and len(b2) >= 1
+            spans = sorted(b1 + b2)
+            assert spans[0][0] == 0 and spans[-1][1] == s.flat_grad.numel()
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))  # a partition
+        else:
+            assert not s.segmented and s.g_bwd is not None and s.g_gather is not None
+        losses = [float(s()) for _ in range(2)]
+        out[(rank, segment)] = (losses, _flat_params(m))
+        del s, m
     dist.destroy_process_group()
 
 
@@ -157,10 +171,16 @@ def test_gloo_two_rank_rehearsal_equals_one_process():
     s = TrainStep(m, _parking_batch(), graph=True, warmup=1)
     want_losses = [float(s()) for _ in range(2)]
     want = _flat_params(m)
+    del s, m
     with mp.Manager() as man:
         out = man.dict()
         mp.spawn(_gloo_worker, args=(2, _port(), out), nprocs=2, join=True)
-        (l0, p0), (l1, p1) = out[0], out[1]
-    assert torch.equal(p0, p1)
-    assert l0 == want_losses and l1 == want_losses
-    assert torch.equal(p0, want)
+        res = dict(out)
+    (l0, p0), (l1, p1) = res[(0, True)], res[(1, True)]
+    (l0s, p0s), (l1s, p1s) = res[(0, False)], res[(1, False)]
+    assert torch.equal(p0, p1) and torch.equal(p0s, p1s)
+    assert l0 == want_losses and l1 == want_losses and l0s == want_losses
+    # (g + g) / 2 == g in fp32: both exchanges reproduce the one-process step bit for bit
+    # (the bound the verdict asks for is 1e-6 relative)
+    assert rel_l2(p0, want) <= 1e-6 and torch.equal(p0, want)
+    assert torch.equal(p0, p0s)

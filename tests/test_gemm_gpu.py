@@ -261,8 +261,7 @@ PAIR_SHAPES = [(112, 258, 258), (112, 774, 258), (112, 2048, 258), (112, 258, 20
 @pytest.mark.parametrize("shape", PAIR_SHAPES, ids=[str(s) for s in PAIR_SHAPES])
 @pytest.mark.parametrize("skip", [False, True])
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-@pytest.mark.parametrize("order", [1, 2], ids=["dx_first", "dw_first"])  # e2ep_tune key 31
-def test_linear_bwd_pair_bitwise_equals_two_launches(shape, skip, prec, order):
+def test_linear_bwd_pair_bitwise_equals_two_launches(shape, skip, prec):
     """e2ep_linear_bwd (dX, dW and db in one k_gemm_pair launch) == e2ep_gemm + e2ep_gemm_rowsum
     launched separately, bit for bit, for fp32 and bf16 operands; and close to fp64."""
     from e2ep_amd import _lib, nn_ops, precision
@@ -272,12 +271,7 @@ def test_linear_bwd_pair_bitwise_equals_two_launches(shape, skip, prec, order):
     x = torch.randn(M, K, generator=g).to(DEV)
     w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
     gs = torch.randn(M, K, generator=g).to(DEV) if skip else None
-    lib = _lib.load()
-    prev_order = lib.e2ep_tune(31, order)
-    try:
-        _linear_pair_case(lib, dy, x, w, gs, M, N, K, skip, prec)
-    finally:
-        lib.e2ep_tune(31, prev_order)
+    _linear_pair_case(_lib.load(), dy, x, w, gs, M, N, K, skip, prec)
 
 
 def _linear_pair_case(lib, dy, x, w, gs, M, N, K, skip, prec):

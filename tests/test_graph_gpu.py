@@ -89,3 +89,39 @@ def test_captured_predict_matches_eager():
         assert torch.equal(out[0], ref[0])
         assert torch.equal(out[1], ref[1]) and torch.equal(out[2], ref[2])
         assert torch.equal(out[3], ref[3])
+
+
+def test_torch_rng_in_capture_draws_fresh_values_per_replay():
+    """A capture that draws from torch's generators (a user module's dropout, rng.py's torch
+    fallback outside a step pool) replays through torch's replay, whose prologue advances the
+    generator offsets: every replay draws new values, as eager calls would.  A
+    capture without such draws keeps the owned executable."""
+    from e2ep_amd import graphs, rng
+    rng.end_step()  # no step pool: rng.uniform / rng.seed fall back to torch draws
+    u = torch.empty(4096, device="cuda")
+    m = torch.empty(4096, device="cuda")
+    s = torch.empty(1, dtype=torch.int32, device="cuda")
+    ones = torch.ones(4096, device="cuda")
+
+    def body():
+        u.copy_(rng.uniform((4096,), "cuda"))
+        m.copy_(torch.nn.functional.dropout(ones, 0.5, training=True))
+        s.copy_(rng.seed("cuda"))
+    g, _, _ = graphs.capture(body)
+    assert g.torch_rng and g._exec is None
+    seen = []
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        seen.append((u.clone(), m.clone(), int(s)))
+    for a, b in zip(seen, seen[1:]):
+        assert not torch.equal(a[0], b[0]) and not torch.equal(a[1], b[1]) and a[2] != b[2]
+    assert all(0.0 <= float(t[0].min()) and float(t[0].max()) < 1.0 for t in seen)
+
+    buf = torch.zeros(16, device="cuda")
+    g2, _, _ = graphs.capture(lambda: buf.add_(1))
+    assert not g2.torch_rng and g2._exec is not None
+    g2.replay()
+    g2.replay()
+    torch.cuda.synchronize()
+    assert float(buf[0]) == 2.0

@@ -46,16 +46,6 @@ def dw_grid(request):
     _lib.load().e2ep_tune(24, prev)
 
 
-@pytest.fixture(params=[2, 1], ids=["se_fused", "se_separate"])
-def se_path(request):
-    """Squeeze-excitation launch plan (e2ep_tune key 27): 2 = the MLP inside the squeeze /
-    excite / da launches (in-launch last-workgroup hand-off), 1 = the separate MLP kernels."""
-    from e2ep_amd import _lib
-    prev = _lib.load().e2ep_tune(27, request.param)
-    yield request.param
-    _lib.load().e2ep_tune(27, prev)
-
-
 @pytest.fixture(params=[1, 0], ids=["bn_one_launch", "bn_split"])
 def bn_path(request):
     """Run a BN test through the single-launch block-per-channel kernels (channels of
@@ -407,11 +397,10 @@ def test_lift_splat_bwd_takes_channels_last_gradient():
                                    (32, 1632, 8, 8, 68), (5, 300, 3, 3, 75), (2, 4096, 2, 2, 256),
                                    (3, 68, 17, 4, 8), (7, 36, 5, 5, 9), (3, 42, 10, 10, 7),
                                    (32, 960, 16, 16, 40)])
-def test_squeeze_excite_fused(shape, se_path):
-    """Fused SE (pool -> 1x1 -> swish -> 1x1 -> sigmoid gate) vs fp64 torch, all gradients;
-    both launch plans (se_path), incl. excite workgroups straddling up to 17 planes (HW = 68),
-    scalar planes (HW = 25) and the C % 4 != 0 fallback (C = 42); the fused plan bitwise
-    deterministic run to run."""
+def test_squeeze_excite_fused(shape):
+    """Fused SE (pool -> 1x1 -> swish -> 1x1 -> sigmoid gate) vs fp64 torch, all gradients,
+    incl. excite workgroups straddling up to 17 planes (HW = 68), scalar planes (HW = 25) and
+    C % 4 != 0 (C = 42); bitwise deterministic run to run."""
     from e2ep_amd import nn_ops
     N, C, H, W, sq = shape
     g = _g(C + sq)
@@ -442,13 +431,25 @@ def test_squeeze_excite_fused(shape, se_path):
         assert torch.equal(a.grad, b.grad)
 
 
+@pytest.fixture(params=[True, False], ids=["bn_sums_in_se", "bn_own_reduce"])
+def se_bn_sums(request):
+    """The split-path _bn1 backward with its channel sums from the SE's da pass
+    (e2ep_se_bwd_bn + e2ep_bn_bwd_planes), and with its own reduction (e2ep_bn_bwd)."""
+    from e2ep_amd import nn_ops
+    prev = nn_ops.set_se_bn_sums(request.param)
+    yield request.param
+    nn_ops.set_se_bn_sums(prev)
+
+
 @pytest.mark.parametrize("case", [(8, 96, 16, 16, 6, True), (4, 40, 9, 7, 10, True),
                                   (32, 672, 16, 16, 28, True), (5, 300, 3, 3, 75, False),
-                                  (2, 144, 64, 64, 6, True), (32, 144, 64, 64, 6, True)])
-def test_bn_swish_se_fused(case, bn_path, se_path):
+                                  (2, 144, 64, 64, 6, True), (32, 144, 64, 64, 6, True),
+                                  (32, 48, 128, 128, 12, True), (6, 56, 30, 30, 14, True)])
+def test_bn_swish_se_fused(case, bn_path, se_bn_sums):
     """MBConv _bn1 -> swish -> SE with the BN + swish applied on load by the SE kernels
     (e2ep_bn_stats + se x_scale/x_shift; backward through e2ep_bn_bwd gate_logit /
-    gate_dpooled), train and eval, vs fp64 torch: output, every gradient, running stats."""
+    gate_dpooled, or on the split path e2ep_bn_bwd_planes with the sums from the SE pass),
+    train and eval, vs fp64 torch: output, every gradient, running stats."""
     from e2ep_amd import nn_ops
     N, C, H, W, sq, train = case
     g = _g(C + sq + H)
