@@ -157,10 +157,6 @@ struct SeBn {
   const float *mean, *invstd, *gamma, *beta;
   double *sums;  // [planes][4]
 };
-__device__ __forceinline__ float swish_d(float z) {
-  const float s = 1.f / (1.f + expf(-z));
-  return s * (1.f + z * (1.f - s));
-}
 
 // da[plane] = s (1 - s) sum_hw dy * x      (wave per plane)
 template <bool BNS>
@@ -197,33 +193,46 @@ __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn
 #pragma unroll
       for (int u = 0; u < SE_U; ++u) {
         if (i0 + u * 64 >= HW4) break;
-        const float4 w = se_in4(xv[u], sc, sh, t), g = gv[u];
-        acc += (w.x * g.x + w.y * g.y) + (w.z * g.z + w.w * g.w);
+        const float4 g = gv[u];
         if constexpr (BNS) {
+          // one sigmoid per element serves the SE input t = zb s and the BN's swish'(zb)
+          // (zb = xhat gamma + beta: the BN backward's arithmetic; t equals the forward's
+          // swish(x scale + shift) up to rounding)
           const float xv4[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
           const float gv4[4] = {g.x, g.y, g.z, g.w};
-          float a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
+          float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const float xh = (xv4[j] - mu) * is;
-            const float sp = swish_d(xh * gm + bt);
+            const float zb = xh * gm + bt;
+            const float sg = 1.f / (1.f + expf(-zb));
+            const float sp = sg * (1.f + zb * (1.f - sg));
+            a0 += (zb * sg) * gv4[j];
             a1 += gv4[j] * sp;
             a2 += sp;
             a3 += gv4[j] * sp * xh;
             a4 += sp * xh;
           }
+          acc += a0;
           s1 += a1; s2 += a2; s3 += a3; s4 += a4;
+        } else {
+          const float4 w = se_in4(xv[u], sc, sh, t);
+          acc += (w.x * g.x + w.y * g.y) + (w.z * g.z + w.w * g.w);
         }
       }
     }
   } else {
     for (int i = lane; i < HW; i += 64) {
       const float xv = xp[i], g = gp[i];
-      acc += se_in(xv, sc, sh, t) * g;
       if constexpr (BNS) {
         const float xh = (xv - mu) * is;
-        const float sp = swish_d(xh * gm + bt);
+        const float zb = xh * gm + bt;
+        const float sg = 1.f / (1.f + expf(-zb));
+        const float sp = sg * (1.f + zb * (1.f - sg));
+        acc += (zb * sg) * g;
         s1 += g * sp; s2 += sp; s3 += g * sp * xh; s4 += sp * xh;
+      } else {
+        acc += se_in(xv, sc, sh, t) * g;
       }
     }
   }

@@ -21,8 +21,9 @@ HIP-graph capture of the train step segfaulted inside hipStreamEndCapture (round
 without them the same capture replays correctly (scripts/diag_branch_capture.py, variants
 model_cam / model_cam_nofork).
 
-Branches are named so each can be switched on for A/B timing: E2EP_BRANCH_STREAMS is a
-comma list of enabled names (default: none, see DESIGN.md for the measurement):
+Branches are named so each can be switched off for A/B timing: E2EP_BRANCH_STREAMS is a
+comma list of enabled names, "none" for none (default: both; replayed C2 step 22.78 -> 21.73
+ms, C3 19.94 -> 18.84 ms, profiles/r05/branch_streams_ab.txt):
   cam    the camera encoder's depth head next to its feature head (model/cam_encoder.py)
   heads  the segmentation head next to the control decoder (model/parking_model.py)
 """
@@ -30,7 +31,8 @@ import os
 
 import torch
 
-_ENABLED = set(x for x in os.environ.get("E2EP_BRANCH_STREAMS", "").split(",") if x and x != "none")
+_ENABLED = set(x for x in os.environ.get("E2EP_BRANCH_STREAMS", "cam,heads").split(",")
+               if x and x != "none")
 _STREAMS = {}
 
 
@@ -61,10 +63,13 @@ def _side(device, name):
 
 
 class branch:
-    """Context manager running its body on a side stream forked from the current stream."""
+    """Context manager running its body on a side stream forked from the current stream.
+    training=False (an inference forward: predict, validation) keeps the body on the current
+    stream: at B = 1 the fork / join costs more than the overlap gains (C5 predict p50 4.41 ms
+    with the branches, 4.20 ms without, profiles/r05/c5_ab.txt)."""
 
-    def __init__(self, name, device, inputs=()):
-        self.on = enabled(name) and device.type == "cuda"
+    def __init__(self, name, device, inputs=(), training=True):
+        self.on = training and enabled(name) and device.type == "cuda"
         self.device, self.name, self.inputs = device, name, inputs
         if self.on:
             self.main = torch.cuda.current_stream(device)

@@ -45,7 +45,7 @@ class CamEncoder(nn.Module):
             # head (e2ep_amd.streams, branch "cam": two chains of 16x16 / 32x32 launches)
             deep, deep_d = nn_ops.fork2(deep)
             skip, skip_d = nn_ops.fork2(skip)
-            with streams.branch("cam", x.device, (deep_d, skip_d)) as br:
+            with streams.branch("cam", x.device, (deep_d, skip_d), self.training) as br:
                 depth = self.depth_layer_2(self.depth_layer_1(deep_d), skip_d)
         feature = self.feature_layer_2(self.feature_layer_1(deep), skip)
         if self.use_depth_distribution:

@@ -85,7 +85,7 @@ class ParkingModel(nn.Module):
         # segmentation head (a few large 200x200 launches) runs on a side stream next to the
         # control decoder (a chain of small token-row launches)
         fuse_seg, fuse_feature = nn_ops.fork2(fuse_feature)
-        br = streams.branch("heads", dev, (fuse_seg,))
+        br = streams.branch("heads", dev, (fuse_seg,), self.training)
         with br:
             pred_segmentation = self.segmentation_head(fuse_seg)
         return (fuse_feature, pred_segmentation, pred_depth, bev_target), br
