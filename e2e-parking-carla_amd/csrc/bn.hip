@@ -444,29 +444,6 @@ __global__ void __launch_bounds__(256) k_bn_bwd_finalize(const double *__restric
   }
 }
 
-// per-channel (sum dzb, sum dzb xhat) from tile-major partials tiles[(t * C + c) * 2] (the
-// depthwise data gradient's BB sums, dwconv.hip), summed in tile order: part[c][1][2] for
-// k_bn_bwd_apply.  grid (cdiv(C, 64)); thread (channel c0 + tid % 64, group tid / 64) takes
-// tiles group, group + 4, ...; the four groups are added in order.
-__global__ void __launch_bounds__(256) k_bn_tiles_sum(const double *__restrict__ tiles, int ntiles,
-                                                      int C, double *__restrict__ part) {
-  __shared__ double ss[4][64], sq[4][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
-  double s = 0.0, q = 0.0;
-  if (c < C)
-    for (int t = grp; t < ntiles; t += 4) {
-      s += tiles[((long long)t * C + c) * 2];
-      q += tiles[((long long)t * C + c) * 2 + 1];
-    }
-  ss[grp][cl] = s;
-  sq[grp][cl] = q;
-  __syncthreads();
-  if (grp == 0 && c < C) {
-    part[2LL * c] = (ss[0][cl] + ss[1][cl]) + (ss[2][cl] + ss[3][cl]);
-    part[2LL * c + 1] = (sq[0][cl] + sq[1][cl]) + (sq[2][cl] + sq[3][cl]);
-  }
-}
-
 // dres = dz;  dx = gamma * invstd * (dzb - (sum_dzb + xhat * sum_dzbxhat) / M)   (train)
 //             dx = gamma * invstd * dzb                                          (eval)
 // grid (C, chunks); chunk 0 of each channel writes dgamma / dbeta.
@@ -1006,39 +983,6 @@ int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const
                        nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
                        dx, nullptr, dgamma, dbeta, plane_sums);
   return launch_status("e2ep_bn_bwd_planes");
-}
-
-int e2ep_bn_bwd_tiles(const float *x, const float *dy, const float *mean, const float *invstd,
-                      const float *gamma, const float *beta, const double *tiles, int ntiles,
-                      int N, int C, int H, int W, int act, float *dx, float *dgamma, float *dbeta,
-                      void *workspace, size_t workspace_bytes, void *stream) {
-  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
-               E2EP_EINVAL, "e2ep_bn_bwd_tiles: bad shape");
-  E2EP_REQUIRE(x && dy && mean && invstd && tiles && ntiles > 0 && dx, E2EP_EINVAL,
-               "e2ep_bn_bwd_tiles: null argument");
-  E2EP_REQUIRE(act >= 0 && act <= 2, E2EP_EINVAL, "e2ep_bn_bwd_tiles: act must be 0/1/2");
-  E2EP_REQUIRE(workspace && workspace_bytes >= (size_t)C * 2 * sizeof(double), E2EP_EINVAL,
-               "e2ep_bn_bwd_tiles: workspace %zu bytes < %zu (C x 2 doubles)", workspace_bytes,
-               (size_t)C * 2 * sizeof(double));
-  const int HW = H * W;
-  const long long per_c = (long long)N * HW;
-  const bool v4 = (HW & 3) == 0;
-  const int HWv = v4 ? HW / 4 : HW;
-  const int totv = N * HWv;
-  hipStream_t s = as_stream(stream);
-  double *part = static_cast<double *>(workspace);
-  hipLaunchKernelGGL(k_bn_tiles_sum, dim3(cdiv(C, 64)), dim3(256), 0, s, tiles, ntiles, C, part);
-  const BnGate gt{nullptr, nullptr, 0.f};
-  const dim3 grid(C, cdiv(totv, APPLY_PER));
-  if (v4)
-    hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                       nullptr, nullptr, 1.f, gt, part, 1, per_c, N, C, HWv, APPLY_PER, act, 1, dx,
-                       nullptr, dgamma, dbeta, nullptr);
-  else
-    hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                       nullptr, nullptr, 1.f, gt, part, 1, per_c, N, C, HWv, APPLY_PER, act, 1, dx,
-                       nullptr, dgamma, dbeta, nullptr);
-  return launch_status("e2ep_bn_bwd_tiles");
 }
 
 int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec) {

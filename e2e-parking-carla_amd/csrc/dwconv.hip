@@ -52,44 +52,6 @@ __device__ __forceinline__ float dw_in(float v, float sc, float sh, int act) {
   return act == 2 ? z / (1.f + expf(-z)) : act == 1 ? fmaxf(z, 0.f) : z;
 }
 
-// BatchNorm backward sums taken by the data-gradient kernels (BB instantiations): the data
-// gradient dt of a depthwise conv whose input was act(bn(e)) (MBConv _bn0 -> swish ->
-// _depthwise_conv) is the gradient at that activation's output; with e read at the same
-// positions, xhat = (e - mean) invstd and dzb = dt act'(xhat gamma + beta) (bn.hip
-// BnBwdElem's arithmetic), each unit adds (sum dzb, sum dzb xhat) to a tile-major fp64 slot
-// tiles[(n * units_per_plane + row block) * C + c][2] (a lane's 4 values in fp32, the wave in
-// fp64), which e2ep_bn_bwd_tiles reduces in fixed order: the BN backward's own reduction pass
-// over e and dt is not run.
-struct DwBnB {
-  const float *e, *mean, *invstd, *gamma, *beta;
-  int act;
-  double *tiles;
-};
-__device__ __forceinline__ float dw_act_d(float z, int act) {
-  if (act == 1) return z > 0.f ? 1.f : 0.f;
-  if (act == 2) {
-    const float s = 1.f / (1.f + expf(-z));
-    return s * (1.f + z * (1.f - s));
-  }
-  return 1.f;
-}
-// (sum dzb, sum dzb xhat) of a lane's 4 data-gradient values o[] at its e values ev
-__device__ __forceinline__ void dw_bnb_lane(const DwBnB &bb, int c, const float (&o)[4], float4 ev,
-                                            bool live, float &f1, float &f2) {
-  f1 = f2 = 0.f;
-  if (!live) return;
-  const float mu = bb.mean[c], is = bb.invstd[c];
-  const float gm = bb.gamma ? bb.gamma[c] : 1.f, bt = bb.beta ? bb.beta[c] : 0.f;
-  const float e4[4] = {ev.x, ev.y, ev.z, ev.w};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float xh = (e4[q] - mu) * is;
-    const float dzb = o[q] * dw_act_d(xh * gm + bt, bb.act);
-    f1 += dzb;
-    f2 += dzb * xh;
-  }
-}
-
 // forward: one thread per output pixel; taps unrolled; branch-free guarded loads
 template <int K, int ST>
 __global__ void __launch_bounds__(256) k_dw_fwd(const float *__restrict__ x,
@@ -403,12 +365,11 @@ __device__ __forceinline__ double dw_wave_sum(double v) {
 
 // The block body for block blk of nblk (k_dw_fwd_strip, and the data-gradient half of
 // k_dw_bwd_pair), over the kernel's dynamic LDS.
-template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false, bool BB = false>
+template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false>
 __device__ __forceinline__ void dw_fwd_strip_body(const float *__restrict__ x,
                                                   const float *__restrict__ w, DwGeom g, DwStrip d,
                                                   int units, float *__restrict__ y, DwIn tf,
-                                                  double *__restrict__ stats, int blk, int nblk,
-                                                  DwBnB bb = DwBnB{}) {
+                                                  double *__restrict__ stats, int blk, int nblk) {
   extern __shared__ float dw_lds[];
   // Grid-stride over units, software-pipelined like k_dw_wgrad_strip: the wave's next unit's
   // input rows are loaded into registers before the current unit's FMAs (one unit per wave
@@ -428,25 +389,15 @@ __device__ __forceinline__ void dw_fwd_strip_body(const float *__restrict__ x,
     oy0 = (un - nc * d.units_per_plane) * d.RO;
   };
   float4 rx[V];
-  // BB: the unit's e values (the data gradient's output positions), fetched with its rows
-  float4 re = make_float4(0.f, 0.f, 0.f, 0.f);
-  const __amdgpu_buffer_rsrc_t rbe = rsrc(bb.e, BB ? 4LL * g.N * g.C * g.P * g.Q : 0);
-  auto fetch_e = [&](bool act) {
-    const int oy = oy0 + ro;
-    re = bload4(rbe, (act && ro < d.RO && oy < g.P) ? (((size_t)nc * g.P + oy) * g.Q + ox0) * 4 : OOR);
-  };
   if (u < units) unit_of(u);
   dw_fetch(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, lane, rx, u < units);
-  if (BB) fetch_e(u < units);
   for (; u < units; u += step) {
     const int c = nc % g.C;
     dw_put(rx, g.H, g.W, oy0 * ST - g.pt, d.IR, d.WP, lds, lane, dw_t(tf, c));
     const int cur_nc = nc, cur_oy0 = oy0;
-    const float4 ecur = re;
     const bool nxt = u + step < units;
     if (nxt) unit_of(u + step);
     dw_fetch(x + (size_t)nc * g.H * g.W, g.H, g.W, oy0 * ST - g.pt, d.IR, lane, rx, nxt);
-    if (BB) fetch_e(nxt);
     float wr[K * K];
 #pragma unroll
     for (int t = 0; t < K * K; ++t) wr[t] = w[c * K * K + (FLIP ? K * K - 1 - t : t)];
@@ -486,30 +437,17 @@ __device__ __forceinline__ void dw_fwd_strip_body(const float *__restrict__ x,
         stats[at + 1] = s2;
       }
     }
-    if (BB) {  // BatchNorm backward sums of the data gradient (separate instantiation)
-      float f1, f2;
-      dw_bnb_lane(bb, c, o, ecur, live, f1, f2);
-      const double s1 = dw_wave_sum((double)f1);
-      const double s2 = dw_wave_sum((double)f2);
-      if (lane == 0) {
-        const int n = cur_nc / g.C;
-        const size_t at = (((size_t)n * d.units_per_plane + cur_oy0 / d.RO) * g.C + c) * 2;
-        bb.tiles[at] = s1;
-        bb.tiles[at + 1] = s2;
-      }
-    }
     dw_wave_sync();  // LDS reuse
   }
 }
 
-template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false, bool BB = false>
+template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false>
 __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
                                                       const float *__restrict__ w, DwGeom g,
                                                       DwStrip d, int units, float *__restrict__ y,
-                                                      DwIn tf, double *__restrict__ stats,
-                                                      DwBnB bb) {
-  dw_fwd_strip_body<K, ST, FLIP, OFF, V, BS, BB>(x, w, g, d, units, y, tf, stats, blockIdx.x,
-                                                 gridDim.x, bb);
+                                                      DwIn tf, double *__restrict__ stats) {
+  dw_fwd_strip_body<K, ST, FLIP, OFF, V, BS>(x, w, g, d, units, y, tf, stats, blockIdx.x,
+                                             gridDim.x);
 }
 
 // stride-2 data gradient over strip units: a wave owns RO = 64/(W/4) rows of dx of one plane,
@@ -518,12 +456,11 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
 // parity of (u + pl - b) is compile-time given PLP = pl & 1.
 // The block body for block blk (k_dw_dgrad_s2_strip, and the data-gradient half of
 // k_dw_bwd_pair_s2), over the kernel's dynamic LDS.
-template <int K, int PLP, bool BB = false>
+template <int K, int PLP>
 __device__ __forceinline__ void dw_dgrad_s2_body(const float *__restrict__ gy,
                                                  const float *__restrict__ w, DwGeom g, int RO,
                                                  int GR, int WPg, int units_per_plane, int units,
-                                                 float *__restrict__ dx, int blk,
-                                                 DwBnB bb = DwBnB{}) {
+                                                 float *__restrict__ dx, int blk) {
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
@@ -531,65 +468,45 @@ __device__ __forceinline__ void dw_dgrad_s2_body(const float *__restrict__ gy,
   float *lds = dw_lds + wave * GR * WPg;
   const bool active = unit < units;
   int nc = 0, iy0 = 0, oyA = 0;
-  const int WL = g.W >> 2;
-  const int r = lane / WL, ix0 = 4 * (lane - r * WL);
-  float4 ev = make_float4(0.f, 0.f, 0.f, 0.f);
   if (active) {
     nc = unit / units_per_plane;
     iy0 = (unit - nc * units_per_plane) * RO;
     oyA = (iy0 + g.pt - (K - 1)) >> 1;  // floor division by 2
-    if (BB) {  // the unit's e values, in flight with the staging
-      const __amdgpu_buffer_rsrc_t rbe = rsrc(bb.e, 4LL * g.N * g.C * g.H * g.W);
-      const bool ok = r < RO && iy0 + r < g.H;
-      ev = bload4(rbe, ok ? (((size_t)nc * g.H + iy0 + r) * g.W + ix0) * 4 : OOR);
-    }
     dw_stage(gy + (size_t)nc * g.P * g.Q, g.P, g.Q, oyA, GR, WPg, lds, lane);
   }
   dw_wave_sync();
-  if (!active) return;  // wave-uniform
+  if (!active) return;
   const int c = nc % g.C;
   float wr[K * K];
 #pragma unroll
   for (int t = 0; t < K * K; ++t) wr[t] = w[c * K * K + t];
+  const int WL = g.W >> 2;
+  const int r = lane / WL, ix0 = 4 * (lane - r * WL);
   const int iy = iy0 + r;
-  const bool live = r < RO && iy < g.H;
+  if (r >= RO || iy >= g.H) return;
   const int xoff = (ix0 >> 1) + ((g.pl - PLP) >> 1) + DW_PADL;
   float o[4] = {0.f, 0.f, 0.f, 0.f};
-  if (live) {
 #pragma unroll
-    for (int a = 0; a < K; ++a) {
-      const int ny = iy + g.pt - a;
-      if (ny & 1) continue;
-      const float *row = lds + ((ny >> 1) - oyA) * WPg + xoff;
+  for (int a = 0; a < K; ++a) {
+    const int ny = iy + g.pt - a;
+    if (ny & 1) continue;
+    const float *row = lds + ((ny >> 1) - oyA) * WPg + xoff;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int b = 0; b < K; ++b)
-          if (((u + PLP - b) & 1) == 0) o[u] = __builtin_fmaf(wr[a * K + b], row[(u + PLP - b) >> 1], o[u]);
-    }
-    *reinterpret_cast<float4 *>(dx + ((size_t)nc * g.H + iy) * g.W + ix0) = make_float4(o[0], o[1], o[2], o[3]);
+      for (int b = 0; b < K; ++b)
+        if (((u + PLP - b) & 1) == 0) o[u] = __builtin_fmaf(wr[a * K + b], row[(u + PLP - b) >> 1], o[u]);
   }
-  if (BB) {  // BatchNorm backward sums (all lanes take part in the wave reduction)
-    float f1, f2;
-    dw_bnb_lane(bb, c, o, ev, live, f1, f2);
-    const double s1 = dw_wave_sum((double)f1);
-    const double s2 = dw_wave_sum((double)f2);
-    if (lane == 0) {
-      const int n = nc / g.C;
-      const size_t at = (((size_t)n * units_per_plane + iy0 / RO) * g.C + c) * 2;
-      bb.tiles[at] = s1;
-      bb.tiles[at + 1] = s2;
-    }
-  }
+  *reinterpret_cast<float4 *>(dx + ((size_t)nc * g.H + iy) * g.W + ix0) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
-template <int K, int PLP, bool BB = false>
+template <int K, int PLP>
 __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restrict__ gy,
                                                            const float *__restrict__ w, DwGeom g,
                                                            int RO, int GR, int WPg,
                                                            int units_per_plane, int units,
-                                                           float *__restrict__ dx, DwBnB bb) {
-  dw_dgrad_s2_body<K, PLP, BB>(gy, w, g, RO, GR, WPg, units_per_plane, units, dx, blockIdx.x, bb);
+                                                           float *__restrict__ dx) {
+  dw_dgrad_s2_body<K, PLP>(gy, w, g, RO, GR, WPg, units_per_plane, units, dx, blockIdx.x);
 }
 
 // weight gradient partials over strip units: grid (C, splits); the block's waves walk the
@@ -699,38 +616,35 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
 // (67.5 us against 52 us for the weight gradient alone).  One launch instead of two on
 // forked streams (e2ep_dwconv_bwd): in a replayed graph the fork / join idles the GPU ~17 us
 // per layer.  Dynamic LDS: the larger of the two halves' per-wave row buffers.
-template <int K, int OFF, int VD, int VW, bool BB = false>
+template <int K, int OFF, int VD, int VW>
 __global__ void __launch_bounds__(256) k_dw_bwd_pair(const float *__restrict__ gy,
                                                      const float *__restrict__ w, DwGeom gt,
                                                      DwStrip dt, int units, float *__restrict__ dx,
                                                      int nd, const float *__restrict__ x, DwGeom g,
-                                                     DwStrip d, int splits, DwPart part, DwIn tf,
-                                                     DwBnB bb) {
+                                                     DwStrip d, int splits, DwPart part, DwIn tf) {
   const int b = blockIdx.x, nw = g.C * splits;
   if (b < nw) {
     dw_wgrad_strip_body<K, 1, OFF, VW>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
   } else {
-    dw_fwd_strip_body<K, 1, true, OFF, VD, false, BB>(gy, w, gt, dt, units, dx,
-                                                      DwIn{nullptr, nullptr, 0}, nullptr, b - nw,
-                                                      nd, bb);
+    dw_fwd_strip_body<K, 1, true, OFF, VD>(gy, w, gt, dt, units, dx, DwIn{nullptr, nullptr, 0},
+                                           nullptr, b - nw, nd);
   }
 }
 
 // The stride-2 form of k_dw_bwd_pair: weight-gradient blocks first (channel c, split sp), then
 // the k_dw_dgrad_s2_strip blocks (one unit per wave).
-template <int K, int PLP, int OFF, int VW, bool BB = false>
+template <int K, int PLP, int OFF, int VW>
 __global__ void __launch_bounds__(256) k_dw_bwd_pair_s2(const float *__restrict__ gy,
                                                         const float *__restrict__ w, int RO, int GR,
                                                         int WPg, int upp2, int units2,
                                                         float *__restrict__ dx,
                                                         const float *__restrict__ x, DwGeom g,
-                                                        DwStrip d, int splits, DwPart part, DwIn tf,
-                                                        DwBnB bb) {
+                                                        DwStrip d, int splits, DwPart part, DwIn tf) {
   const int b = blockIdx.x, nw = g.C * splits;
   if (b < nw)
     dw_wgrad_strip_body<K, 2, OFF, VW>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
   else
-    dw_dgrad_s2_body<K, PLP, BB>(gy, w, g, RO, GR, WPg, upp2, units2, dx, b - nw, bb);
+    dw_dgrad_s2_body<K, PLP>(gy, w, g, RO, GR, WPg, upp2, units2, dx, b - nw);
 }
 
 static int dw_splits(long long pixels, int C) {
@@ -778,21 +692,10 @@ static int dw_off(int pl) { return g_tune[TUNE_DW_VEC] == 1 ? -1 : ((-pl) & 3); 
 template <int K, int ST, bool FLIP, int V>
 static void dw_fwd_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *x,
                            const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf,
-                           double *stats, const DwBnB &bb = DwBnB{}) {
+                           double *stats) {
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, x, w, g, d, units, y, tf, stats, bb);
+    hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, x, w, g, d, units, y, tf, stats);
   };
-  if constexpr (FLIP) {
-    if (bb.tiles) {  // data gradient with the BatchNorm backward sums
-      switch (off) {
-        case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V, false, true>); break;
-        case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V, false, true>); break;
-        case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2, V, false, true>); break;
-        default: go(k_dw_fwd_strip<K, ST, FLIP, 3, V, false, true>);
-      }
-      return;
-    }
-  }
   if (stats && !FLIP) {
     switch (off) {
       case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V, true>); break;
@@ -812,24 +715,17 @@ static void dw_fwd_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const
 template <int K, int ST, bool FLIP>
 static void dw_fwd_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const float *x,
                          const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf,
-                         double *stats, const DwBnB &bb = DwBnB{}) {
-  if constexpr (FLIP) {
-    if (off < 0 && bb.tiles) {
-      hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV, false, true>), grid, dim3(256),
-                         shm, st, x, w, g, d, units, y, tf, nullptr, bb);
-      return;
-    }
-  }
+                         double *stats) {
   if (off < 0 && stats && !FLIP)
     hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV, true>), grid, dim3(256), shm, st,
-                       x, w, g, d, units, y, tf, stats, DwBnB{});
+                       x, w, g, d, units, y, tf, stats);
   else if (off < 0)
     hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV>), grid, dim3(256), shm, st, x, w,
-                       g, d, units, y, tf, nullptr, DwBnB{});
+                       g, d, units, y, tf, nullptr);
   else if (nv <= 2)
-    dw_fwd_strip_v<K, ST, FLIP, 2>(off, grid, shm, st, x, w, g, d, units, y, tf, stats, bb);
+    dw_fwd_strip_v<K, ST, FLIP, 2>(off, grid, shm, st, x, w, g, d, units, y, tf, stats);
   else
-    dw_fwd_strip_v<K, ST, FLIP, DW_MAXV>(off, grid, shm, st, x, w, g, d, units, y, tf, stats, bb);
+    dw_fwd_strip_v<K, ST, FLIP, DW_MAXV>(off, grid, shm, st, x, w, g, d, units, y, tf, stats);
 }
 template <int K, int ST, int V>
 static void dw_wgrad_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *gy,
@@ -940,31 +836,7 @@ static bool dw_s2_plan(const DwGeom &g, DwS2 &p) {
   return true;
 }
 
-// tiles of the data gradient's strip plan (the BB sums' slots): N * units per plane, 0 where
-// the data gradient runs the generic kernel (no sums)
-static int dw_dgrad_tiles(const DwGeom &g) {
-  if (!(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0)) return 0;
-  if (g.st == 1) {
-    DwGeom t = g;
-    t.H = g.P; t.W = g.Q; t.P = g.H; t.Q = g.W;
-    t.pt = g.K - 1 - g.pt; t.pl = g.K - 1 - g.pl;
-    if (dw_strip_ok(t) && t.pt >= 0 && t.pl >= 0 && t.pl <= DW_PADL)
-      return t.N * dw_strip(t.K, 1, t.W, t.P, t.Q).units_per_plane;
-    return 0;
-  }
-  DwS2 p2;
-  return dw_s2_plan(g, p2) ? g.N * p2.upp : 0;
-}
-
-static int dw_dgrad_impl(const float *gy, const float *w, const int *dims, float *dx,
-                         const DwBnB &bb, void *stream);
-
 int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream) {
-  return dw_dgrad_impl(gy, w, dims, dx, DwBnB{}, stream);
-}
-
-static int dw_dgrad_impl(const float *gy, const float *w, const int *dims, float *dx,
-                         const DwBnB &bb, void *stream) {
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_dgrad: bad geometry");
@@ -980,10 +852,10 @@ static int dw_dgrad_impl(const float *gy, const float *w, const int *dims, float
       const DwIn none{nullptr, nullptr, 0};
       if (t.K == 3)
         dw_fwd_strip<3, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
-                                 w, t, d, units, dx, none, nullptr, bb);
+                                 w, t, d, units, dx, none, nullptr);
       else
         dw_fwd_strip<5, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
-                                 w, t, d, units, dx, none, nullptr, bb);
+                                 w, t, d, units, dx, none, nullptr);
       return launch_status("e2ep_dwconv_dgrad");
     }
   }
@@ -993,24 +865,16 @@ static int dw_dgrad_impl(const float *gy, const float *w, const int *dims, float
     const size_t shm = 4 * GR * WPg * sizeof(float);
     const dim3 grid(cdiv(units, 4));
     const bool odd = g.pl & 1;
-#define DWS2(KV, PV)                                                                                 \
-  do {                                                                                               \
-    if (bb.tiles)                                                                                    \
-      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<KV, PV, true>), grid, dim3(256), shm, as_stream(stream), \
-                         gy, w, g, RO, GR, WPg, upp, units, dx, bb);                                  \
-    else                                                                                             \
-      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<KV, PV>), grid, dim3(256), shm, as_stream(stream), gy,  \
-                         w, g, RO, GR, WPg, upp, units, dx, bb);                                      \
-  } while (0)
-    if (g.K == 3 && !odd) DWS2(3, 0);
-    else if (g.K == 3) DWS2(3, 1);
-    else if (!odd) DWS2(5, 0);
-    else DWS2(5, 1);
-#undef DWS2
+    if (g.K == 3 && !odd)
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<3, 0>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+    else if (g.K == 3)
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<3, 1>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+    else if (!odd)
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<5, 0>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+    else
+      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<5, 1>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
     return launch_status("e2ep_dwconv_dgrad");
   }
-  E2EP_REQUIRE(!bb.tiles, E2EP_EINVAL, "e2ep_dwconv_dgrad_bn: this geometry takes no BN sums "
-               "(e2ep_dwconv_bn_tiles returned 0)");
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_dgrad: N*C > 65535");
   DW_DISPATCH(k_dw_dgrad, dim3(cdiv(g.H * g.W, 256), g.N * g.C), gy, w, g, dx);
   return launch_status("e2ep_dwconv_dgrad");
@@ -1103,54 +967,9 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
   return launch_status("e2ep_dwconv_wgrad");
 }
 
-static int dw_bwd_impl(const float *gy, const float *x, const float *w, const int *dims,
-                       const float *in_scale, const float *in_shift, int in_act, float *dx,
-                       void *workspace, size_t workspace_bytes, float *dw, const DwBnB &bb,
-                       void *stream);
-
 int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *dims,
                     const float *in_scale, const float *in_shift, int in_act, float *dx,
                     void *workspace, size_t workspace_bytes, float *dw, void *stream) {
-  return dw_bwd_impl(gy, x, w, dims, in_scale, in_shift, in_act, dx, workspace, workspace_bytes,
-                     dw, DwBnB{}, stream);
-}
-
-int e2ep_dwconv_bn_tiles(const int *dims) { return dw_dgrad_tiles(dw_geom(dims)); }
-
-int e2ep_dwconv_bwd_bn(const float *gy, const float *x, const float *w, const int *dims,
-                       const float *in_scale, const float *in_shift, int in_act, float *dx,
-                       void *workspace, size_t workspace_bytes, float *dw,
-                       const float *bn_mean, const float *bn_invstd, const float *gamma,
-                       const float *beta, double *tiles, size_t tiles_bytes, void *stream) {
-  const DwGeom g = dw_geom(dims);
-  const int nt = dw_dgrad_tiles(g);
-  E2EP_REQUIRE(nt > 0 && tiles && tiles_bytes >= (size_t)nt * g.C * 2 * sizeof(double),
-               E2EP_EINVAL, "e2ep_dwconv_bwd_bn: tiles %zu bytes < %zu (e2ep_dwconv_bn_tiles x C "
-               "x 2 doubles)", tiles_bytes, (size_t)(nt > 0 ? nt : 0) * g.C * 2 * sizeof(double));
-  E2EP_REQUIRE(x && bn_mean && bn_invstd, E2EP_EINVAL, "e2ep_dwconv_bwd_bn: null BN argument");
-  return dw_bwd_impl(gy, x, w, dims, in_scale, in_shift, in_act, dx, workspace, workspace_bytes,
-                     dw, DwBnB{x, bn_mean, bn_invstd, gamma, beta, in_act, tiles}, stream);
-}
-
-int e2ep_dwconv_dgrad_bn(const float *gy, const float *w, const int *dims, float *dx,
-                         const float *e, const float *bn_mean, const float *bn_invstd,
-                         const float *gamma, const float *beta, int act, double *tiles,
-                         size_t tiles_bytes, void *stream) {
-  const DwGeom g = dw_geom(dims);
-  const int nt = dw_dgrad_tiles(g);
-  E2EP_REQUIRE(nt > 0 && tiles && tiles_bytes >= (size_t)nt * g.C * 2 * sizeof(double),
-               E2EP_EINVAL, "e2ep_dwconv_dgrad_bn: tiles %zu bytes < %zu (e2ep_dwconv_bn_tiles x "
-               "C x 2 doubles)", tiles_bytes, (size_t)(nt > 0 ? nt : 0) * g.C * 2 * sizeof(double));
-  E2EP_REQUIRE(e && bn_mean && bn_invstd && act >= 0 && act <= 2, E2EP_EINVAL,
-               "e2ep_dwconv_dgrad_bn: bad BN argument");
-  return dw_dgrad_impl(gy, w, dims, dx, DwBnB{e, bn_mean, bn_invstd, gamma, beta, act, tiles},
-                       stream);
-}
-
-static int dw_bwd_impl(const float *gy, const float *x, const float *w, const int *dims,
-                       const float *in_scale, const float *in_shift, int in_act, float *dx,
-                       void *workspace, size_t workspace_bytes, float *dw, const DwBnB &bb,
-                       void *stream) {
   const DwGeom g = dw_geom(dims);
   DwGeom t;
   int off;
@@ -1177,19 +996,12 @@ static int dw_bwd_impl(const float *gy, const float *x, const float *w, const in
     const dim3 grid(g.C * sp + cdiv(p2.units, 4));
 #define DWP2(KV, PLPV, OFFV)                                                                       \
   do {                                                                                             \
-    if (bb.tiles && vw == 2)                                                                       \
-      hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, 2, true>), grid, dim3(256), shm, s, gy, \
-                         w, p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf, bb); \
-    else if (bb.tiles)                                                                             \
-      hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, DW_MAXV, true>), grid, dim3(256), shm,  \
-                         s, gy, w, p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part,  \
-                         tf, bb);                                                                  \
-    else if (vw == 2)                                                                              \
+    if (vw == 2)                                                                                   \
       hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, 2>), grid, dim3(256), shm, s, gy, w,    \
-                         p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf, bb);   \
+                         p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf);       \
     else                                                                                           \
       hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, DW_MAXV>), grid, dim3(256), shm, s, gy, \
-                         w, p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf, bb); \
+                         w, p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf);    \
   } while (0)
     // PLP = pad_left & 1, OFF = -pad_left mod 4 (dw_off)
     if (g.K == 3 && g.pl == 0) DWP2(3, 0, 0);
@@ -1214,14 +1026,8 @@ static int dw_bwd_impl(const float *gy, const float *x, const float *w, const in
   const size_t shm = 4 * (size_t)std::max(dt.IR * dt.WP, d.IR * d.WP) * 4;
   const dim3 grid(nd + g.C * sp);
 #define DWP(KV, OFFV, VDV, VWV)                                                                   \
-  do {                                                                                             \
-    if (bb.tiles)                                                                                  \
-      hipLaunchKernelGGL((k_dw_bwd_pair<KV, OFFV, VDV, VWV, true>), grid, dim3(256), shm, s, gy, w, \
-                         t, dt, units, dx, nd, x, g, d, sp, part, tf, bb);                         \
-    else                                                                                           \
-      hipLaunchKernelGGL((k_dw_bwd_pair<KV, OFFV, VDV, VWV>), grid, dim3(256), shm, s, gy, w, t,   \
-                         dt, units, dx, nd, x, g, d, sp, part, tf, bb);                            \
-  } while (0)
+  hipLaunchKernelGGL((k_dw_bwd_pair<KV, OFFV, VDV, VWV>), grid, dim3(256), shm, s, gy, w, t, dt, \
+                     units, dx, nd, x, g, d, sp, part, tf)
 #define DWP_V(KV, OFFV)                                  \
   do {                                                   \
     if (vd == 2 && vw == 2) DWP(KV, OFFV, 2, 2);         \

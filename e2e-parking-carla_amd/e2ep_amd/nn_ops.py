@@ -302,19 +302,6 @@ class _DwConv(torch.autograd.Function):
         return dx, dw, None, None
 
 
-# E2EP_BN_DW_SUMS=0: the _bn0 backward takes its own reduction pass (e2ep_bn_bwd) instead of
-# the sums from the depthwise data gradient (A/B)
-_DW_BN_SUMS = [os.environ.get("E2EP_BN_DW_SUMS", "1") != "0"]
-
-
-def set_dw_bn_sums(on):
-    """Enable / disable the _bn0 backward sums from the depthwise data gradient (returns the
-    previous setting)."""
-    prev = _DW_BN_SUMS[0]
-    _DW_BN_SUMS[0] = bool(on)
-    return prev
-
-
 class _BnActDwConv(torch.autograd.Function):
     """depthwise_conv(act(bn(x))) with the BN + activation applied while the depthwise
     kernel stages its input: the normalised tensor is never stored (MBConv's
@@ -365,25 +352,7 @@ class _BnActDwConv(torch.autograd.Function):
         fork = None
         want_t = nig[0] or nig[1] or nig[2]
         paired = nig[9] and want_t and _dw_pairable(d)
-        lib = _lib.load()
-        # training BN on the split path: its channel sums are taken by the depthwise data
-        # gradient (e2ep_dwconv_*_bn), so the BN backward is its apply pass alone
-        ntiles = (lib.e2ep_dwconv_bn_tiles(d) if (_DW_BN_SUMS[0] and ctx.train and nig[0]
-                                                  and lib.e2ep_bn_bwd_split(N, C, H, W) == 1)
-                  else 0)
-        tiles = (torch.empty(ntiles * C * 2, dtype=torch.float64, device=x.device)
-                 if ntiles > 0 else None)
-        bnargs = (_lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta))
-        if paired and tiles is not None:
-            dw = torch.empty_like(w)
-            dt = torch.empty_like(x)
-            wsw = _ws(lib.e2ep_dwconv_wgrad_workspace(d), x.device)
-            with timing.region(timing.name("dwconv_bwd", gy.shape, "_BnActDwConv")):
-                _lib.call("e2ep_dwconv_bwd_bn", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(w), d,
-                          _lib.ptr(stats[2]), _lib.ptr(stats[3]), ctx.act, _lib.ptr(dt),
-                          _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), *bnargs, _lib.ptr(tiles),
-                          _lib.nbytes(tiles), s)
-        elif paired:  # both gradients in one launch
+        if paired:  # both gradients in one launch
             dw = torch.empty_like(w)
             dt = torch.empty_like(x)  # gradient at the activation output
             wsw = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
@@ -403,24 +372,10 @@ class _BnActDwConv(torch.autograd.Function):
             if not paired:
                 dt = torch.empty_like(x)  # gradient at the activation output
                 with timing.region(timing.name("dwconv_dgrad", gy.shape, "_BnActDwConv")):
-                    if tiles is not None:
-                        _lib.call("e2ep_dwconv_dgrad_bn", _lib.ptr(gy), _lib.ptr(w), d,
-                                  _lib.ptr(dt), _lib.ptr(x), *bnargs, ctx.act, _lib.ptr(tiles),
-                                  _lib.nbytes(tiles), s)
-                    else:
-                        _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s)
+                    _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s)
             dx = torch.empty_like(x) if nig[0] else None
             dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
             db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
-            if tiles is not None:
-                pws = _ws(C * 16, x.device)
-                with timing.region(timing.name("bn_bwd", x.shape, "_BnActDwConv")):
-                    _lib.call("e2ep_bn_bwd_tiles", _lib.ptr(x), _lib.ptr(dt), *bnargs,
-                              _lib.ptr(tiles), ntiles, N, C, H, W, ctx.act, _lib.ptr(dx),
-                              _lib.ptr(dg), _lib.ptr(db), _lib.ptr(pws), _lib.nbytes(pws), s)
-                if fork is not None:
-                    fork.join()
-                return dx, dg, db, None, None, None, None, None, None, dw, None, None, None, None
             ws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), x.device)
             with timing.region(timing.name("bn_bwd", x.shape, "_BnActDwConv")):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dt), _lib.ptr(stats[0]),

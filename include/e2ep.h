@@ -313,15 +313,6 @@ int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const
                        const float *gamma, const float *beta, const float *gate_logit,
                        const float *gate_dpooled, const double *plane_sums, int N, int C, int H,
                        int W, int act, float *dx, float *dgamma, float *dbeta, void *stream);
-/* The apply half of e2ep_bn_bwd (training statistics; no residual / gate / drop-connect) whose
- * channel sums come from tile-major partials tiles [ntiles][C][2] = (sum dzb, sum dzb xhat)
- * taken by the kernel that produced dy (e2ep_dwconv_bwd_bn / e2ep_dwconv_dgrad_bn): one small
- * launch sums them in tile order into workspace (C x 2 doubles), then the apply pass.  Same
- * element arithmetic as e2ep_bn_bwd. */
-int e2ep_bn_bwd_tiles(const float *x, const float *dy, const float *mean, const float *invstd,
-                      const float *gamma, const float *beta, const double *tiles, int ntiles,
-                      int N, int C, int H, int W, int act, float *dx, float *dgamma, float *dbeta,
-                      void *workspace, size_t workspace_bytes, void *stream);
 /* Stand-alone activation (act as above) and its gradient w.r.t. the pre-activation x. */
 int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);
@@ -523,25 +514,6 @@ int e2ep_dwconv_bwd_pair_ok(const int *dims);
 int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *dims,
                     const float *in_scale, const float *in_shift, int in_act, float *dx,
                     void *workspace, size_t workspace_bytes, float *dw, void *stream);
-/* The same backward (e2ep_dwconv_bwd; e2ep_dwconv_dgrad_bn: the data gradient alone, for
- * layers whose pair plan is 0) when x = e is the raw input of the depthwise conv's input
- * transform, i.e. the conv reads act(bn(e)) (MBConv _bn0 -> swish -> _depthwise_conv,
- * reference model/cam_encoder.py:69-73): the data-gradient kernel also takes that BN's
- * backward sums (sum dzb, sum dzb xhat) of its output dt, xhat = (e - bn_mean) bn_invstd,
- * dzb = dt act'(xhat gamma + beta), one fp64 pair per (tile, channel) into tiles
- * [e2ep_dwconv_bn_tiles(dims)][C][2] for e2ep_bn_bwd_tiles, which then skips the BN's
- * reduction pass over e and dt.  dx / dw bitwise those of the plain entry points.
- * e2ep_dwconv_bn_tiles returns 0 where the data gradient runs the generic kernel. */
-int e2ep_dwconv_bn_tiles(const int *dims);
-int e2ep_dwconv_bwd_bn(const float *gy, const float *x, const float *w, const int *dims,
-                       const float *in_scale, const float *in_shift, int in_act, float *dx,
-                       void *workspace, size_t workspace_bytes, float *dw,
-                       const float *bn_mean, const float *bn_invstd, const float *gamma,
-                       const float *beta, double *tiles, size_t tiles_bytes, void *stream);
-int e2ep_dwconv_dgrad_bn(const float *gy, const float *w, const int *dims, float *dx,
-                         const float *e, const float *bn_mean, const float *bn_invstd,
-                         const float *gamma, const float *beta, int act, double *tiles,
-                         size_t tiles_bytes, void *stream);
 size_t e2ep_dwconv_wgrad_workspace(const int *dims);
 int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
                       const float *in_shift, int in_act, void *workspace, size_t workspace_bytes,

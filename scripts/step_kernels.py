@@ -19,13 +19,19 @@ def main():
     ap.add_argument("steps", type=int, nargs="?", default=20)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--csv", default=None)
+    ap.add_argument("--marker", default=None,
+                    help="kernel name that ends each step instead of k_adam (e.g. the last kernel "
+                         "of a replayed predict graph)")
     args = ap.parse_args()
     c = sqlite3.connect(args.db)
     rows = c.execute("select name, start, end from kernels order by start").fetchall()
-    adam = [r for r in rows if "k_adam(" in r[0] or r[0].startswith("e2ep::k_adam")]
-    adam = [r for r in adam if "k_adam_count" not in r[0]]
+    if args.marker:
+        adam = [r for r in rows if args.marker in r[0]]
+    else:
+        adam = [r for r in rows if "k_adam(" in r[0] or r[0].startswith("e2ep::k_adam")]
+        adam = [r for r in adam if "k_adam_count" not in r[0]]
     if len(adam) < args.steps + 1:
-        raise SystemExit(f"only {len(adam)} k_adam dispatches")
+        raise SystemExit(f"only {len(adam)} marker dispatches")
     t0, t1 = adam[-args.steps - 1][2], adam[-1][2]
     K = args.steps
     per = collections.defaultdict(lambda: [0, 0.0])

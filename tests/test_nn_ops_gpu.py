@@ -259,17 +259,6 @@ def _depthwise_case(ops, case):
     assert rel_l2(wd.grad, w64.grad) < 1e-5
 
 
-@pytest.fixture(params=[True, False], ids=["bn_sums_in_dgrad", "bn_own_reduce"])
-def dw_bn_sums(request):
-    """The split-path _bn0 backward with its channel sums from the depthwise data gradient
-    (e2ep_dwconv_bwd_bn / e2ep_dwconv_dgrad_bn + e2ep_bn_bwd_tiles), and with its own
-    reduction (e2ep_bn_bwd)."""
-    from e2ep_amd import nn_ops
-    prev = nn_ops.set_dw_bn_sums(request.param)
-    yield request.param
-    nn_ops.set_dw_bn_sums(prev)
-
-
 @pytest.mark.parametrize("case", [(4, 144, 64, 64, 3, 2, (0, 1, 0, 1), True),
                                   (2, 192, 32, 32, 5, 1, (2, 2, 2, 2), True),
                                   (2, 40, 32, 32, 5, 2, (1, 2, 1, 2), False),
@@ -278,12 +267,10 @@ def dw_bn_sums(request):
                                   (8, 144, 128, 128, 3, 2, (0, 1, 0, 1), True),
                                   (8, 192, 64, 64, 3, 1, (1, 1, 1, 1), True),
                                   (8, 336, 32, 32, 5, 1, (2, 2, 2, 2), True)])
-def test_bn_swish_depthwise_fused(case, bn_path, dw_grid, dw_bn_sums):
+def test_bn_swish_depthwise_fused(case, bn_path, dw_grid):
     """MBConv _bn0 -> swish -> _depthwise_conv with the BN + swish applied inside the
     depthwise input load (e2ep_bn_stats + dwconv in_scale/in_shift), train and eval, vs fp64
-    torch: output, x / gamma / beta / weight gradients and running statistics; the training
-    BN backward on the split path with its sums from the depthwise data gradient or its own
-    reduction (dw_bn_sums)."""
+    torch: output, x / gamma / beta / weight gradients and running statistics."""
     from e2ep_amd import nn_ops
     N, C, H, W, K, s, pad, train = case
     g = _g(C + H + K)
