@@ -676,8 +676,14 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
 // 128 x 128 (wave tiles up to 64 x 64: 8 MFMAs per wave per step), and:
 //  * A = g rows: a thread owns 8 consecutive pixels of a row (two float4 loads, one b128
 //    LDS write);
-//  * B = im2col x columns: a thread owns a pixel PAIR of BNT/16 columns (lanes on consecutive
-//    pairs: coalesced along the image rows), packed to bf16x2 per column (one b32 write);
+//  * B = im2col x columns (16-bit operands, round 5): a thread owns (column, pixel octet)
+//    pairs — 8 consecutive output pixels of one column, inside one output row (Q % 8 == 0) —
+//    whose input window is read as 2 float4 (stride 1) or 4 float4 (stride 2, every other
+//    value kept) when it lies inside the input row, value by value at the row ends, and
+//    written as one bf16x8 (b128) LDS row segment: 2 (stride 1) / 4 (stride 2) loads and 1 LDS
+//    write per 8 values where the pixel-pair form took 8 scalar loads and 4 b32 writes
+//    (the fp32 form, OP 0, keeps the pixel pairs: a thread owns a pixel PAIR of BNT/16
+//    columns, packed per column);
 //  * a step never straddles two images (P*Q % 32 == 0, every hot-path map), so its image and
 //    first pixel are block-uniform.
 // ------------------------------------------------------------------------------------------
@@ -721,12 +727,18 @@ __device__ __forceinline__ void wgrad_lp_block(
   const int HW = g.H * g.W;
 
   // A: octet o = tid + 256 i -> (co row o / OPR, pixel octet o % OPR)
-  // B: thread = (pixel pair tid % PP, column group tid / PP): columns bcg + CG j
+  // B (OP 0): thread = (pixel pair tid % PP, column group tid / PP): columns bcg + CG j
+  // B (16-bit): thread = (pixel octet tid % OCT, column tid / OCT + (256 / OCT) j)
+  constexpr int OCT = LKS / 8;                    // pixel octets per column per step
+  constexpr int NOC = OP == 0 ? 1 : BNT * OCT / 256;  // (column, octet) pairs per thread
+  static_assert(OP == 0 || (BNT * OCT) % 256 == 0, "whole (column, octet) pairs per thread");
+  constexpr int NCOL = OP == 0 ? NBC : NOC;       // columns per thread
   const int bq = tid % PP, bcg = tid / PP;
-  int cconst[NBC], cdy[NBC], cdx[NBC];
+  const int boc = tid % OCT, bcol = tid / OCT;
+  int cconst[NCOL], cdy[NCOL], cdx[NCOL];
 #pragma unroll
-  for (int j = 0; j < NBC; ++j) {
-    const int col = n0 + bcg + CG * j;
+  for (int j = 0; j < NCOL; ++j) {
+    const int col = n0 + (OP == 0 ? bcg + CG * j : bcol + (256 / OCT) * j);
     const int cc = col < Kl ? col : 0;
     const int ci = cc / tl.n, tap = s_tap[cc - ci * tl.n];
     const int r = tap / g.S, sx = tap - r * g.S;
@@ -741,6 +753,7 @@ __device__ __forceinline__ void wgrad_lp_block(
 
   float4 ra[NA8][2];
   float rb[NBC][2];
+  float4 rv[NOC][4];  // 16-bit B: a pair's window (stride 1: [0..1]; stride 2: [0..3], .x / .z kept)
   auto load_tiles = [&](int ks) {
     const int p0 = pbeg + min(ks, nk - 1) * LKS;  // past the range: re-read, never stored
     const int im = p0 / PQ, od0 = p0 - im * PQ;    // block-uniform
@@ -752,16 +765,52 @@ __device__ __forceinline__ void wgrad_lp_block(
       ra[i][0] = bload4(rg, base);
       ra[i][1] = bload4(rg, base + 16);
     }
+    if constexpr (OP == 0) {
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int od = od0 + 2 * bq + e;
+      for (int e = 0; e < 2; ++e) {
+        const int od = od0 + 2 * bq + e;
+        const int oy = od / g.Q, ox = od - oy * g.Q;
+        const int yb = oy * g.sh, xb = ox * g.sw;
+        const int pbase = im * g.Cin * HW + yb * g.W + xb;
+#pragma unroll
+        for (int j = 0; j < NBC; ++j) {
+          const bool ok = (unsigned)(yb + cdy[j]) < (unsigned)g.H && (unsigned)(xb + cdx[j]) < (unsigned)g.W;
+          rb[j][e] = bload(rx, ok ? (pbase + cconst[j]) * 4 : nrx);
+        }
+      }
+    } else {
+      const int od = od0 + 8 * boc;  // the octet's first output pixel (one output row)
       const int oy = od / g.Q, ox = od - oy * g.Q;
       const int yb = oy * g.sh, xb = ox * g.sw;
       const int pbase = im * g.Cin * HW + yb * g.W + xb;
+      const int last = 7 * g.sw;  // the window's last input column past its first
 #pragma unroll
-      for (int j = 0; j < NBC; ++j) {
-        const bool ok = (unsigned)(yb + cdy[j]) < (unsigned)g.H && (unsigned)(xb + cdx[j]) < (unsigned)g.W;
-        rb[j][e] = bload(rx, ok ? (pbase + cconst[j]) * 4 : nrx);
+      for (int j = 0; j < NOC; ++j) {
+        const int x0 = xb + cdx[j];
+        const bool rowok = (unsigned)(yb + cdy[j]) < (unsigned)g.H;  // dead columns: never
+        const int base = pbase + cconst[j];  // element offset of the window's first value
+        if (rowok && x0 >= 0 && x0 + last < g.W) {  // inside the row: vector loads
+          rv[j][0] = bload4(rx, base * 4);
+          rv[j][1] = bload4(rx, base * 4 + 16);
+          if (g.sw == 2) {
+            rv[j][2] = bload4(rx, base * 4 + 32);
+            rv[j][3] = bload4(rx, base * 4 + 48);
+          }
+        } else {  // a row end (zero padding) or a dead column: value by value
+          float t[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const bool ok = rowok && (unsigned)(x0 + q * g.sw) < (unsigned)g.W;
+            t[q] = bload(rx, ok ? (base + q * g.sw) * 4 : nrx);
+          }
+          if (g.sw == 2) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rv[j][q] = make_float4(t[2 * q], 0.f, t[2 * q + 1], 0.f);
+          } else {
+            rv[j][0] = make_float4(t[0], t[1], t[2], t[3]);
+            rv[j][1] = make_float4(t[4], t[5], t[6], t[7]);
+          }
+        }
       }
     }
   };
@@ -778,13 +827,28 @@ __device__ __forceinline__ void wgrad_lp_block(
         *reinterpret_cast<bf16x8 *>(&As[buf][ar][8 * ao]) = cvt8<1>(v);
       }
     }
+    if constexpr (OP == 0) {
 #pragma unroll
-    for (int j = 0; j < NBC; ++j) {
-      const f32x2 f = {rb[j][0], rb[j][1]};
-      if constexpr (OP == 0)
+      for (int j = 0; j < NBC; ++j) {
+        const f32x2 f = {rb[j][0], rb[j][1]};
         *reinterpret_cast<f32x2 *>(&Bs[buf][bcg + CG * j][2 * bq]) = f;
-      else
-        *reinterpret_cast<bf16x2 *>(&Bs[buf][bcg + CG * j][2 * bq]) = __builtin_convertvector(f, bf16x2);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NOC; ++j) {
+        float v[8];
+        if (g.sw == 2) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] = rv[j][q].x;
+            v[2 * q + 1] = rv[j][q].z;
+          }
+        } else {
+          v[0] = rv[j][0].x; v[1] = rv[j][0].y; v[2] = rv[j][0].z; v[3] = rv[j][0].w;
+          v[4] = rv[j][1].x; v[5] = rv[j][1].y; v[6] = rv[j][1].z; v[7] = rv[j][1].w;
+        }
+        *reinterpret_cast<bf16x8 *>(&Bs[buf][bcol + (256 / OCT) * j][8 * boc]) = cvt8<1>(v);
+      }
     }
   };
 
@@ -918,11 +982,11 @@ __global__ void __launch_bounds__(256) k_lp_bwd_pair(
 }
 
 // pixels per K-step of k_wgrad_lp: 32 (bf16 64-pixel steps measured equal, 128 slower: register
-// pressure; e2ep_tune key 17 forces 32 / 64 / 128 for A/B), fp32 32
+// pressure, removed in round 5; e2ep_tune key 17 forces 32 / 64 for A/B), fp32 32
 static int lp_wgrad_lk(const ConvGeom &g, int op) {
   const int pq = g.P * g.Q, f = g_tune[TUNE_LPW_LK];
   if (op == 0) return 32;
-  if ((f == 32 || f == 64 || f == 128) && pq % f == 0) return f;
+  if ((f == 32 || f == 64) && pq % f == 0) return f;
   return 32;
 }
 
@@ -946,7 +1010,9 @@ static void lp_wgrad_tile(const ConvGeom &g, const TapList &tl, int &wm, int &wn
 // Few (Cout, column) pairs over many pixels (the 128x128 maps' 24 / 48-channel 1x1s, the
 // segmentation classifier) stay on k_wgrad_1x1 / k_conv_wgrad2, measured faster there.
 bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl) {
-  if (tl.n <= 0 || (g.P * g.Q) % LK != 0) return false;
+  // Q % 8 == 0 and stride 1 / 2 along x: the 16-bit B staging's pixel octets (one output row,
+  // 2 or 4 float4 per input window); the fp32 form (OP 0) reads pixel pairs but shares the rule
+  if (tl.n <= 0 || (g.P * g.Q) % LK != 0 || g.Q % 8 != 0 || (g.sw != 1 && g.sw != 2)) return false;
   return g_tune[TUNE_LP_WGRAD_TILE] > 1 || (long long)g.Cout * g.Cin * tl.n >= 2048;
 }
 
@@ -976,8 +1042,6 @@ int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const 
   do {                                                                                           \
     if (op != 1)                                                                                 \
       hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 0, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
-    else if (lk == 128)                                                                          \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 128>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
     else if (lk == 64)                                                                           \
       hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
     else                                                                                         \

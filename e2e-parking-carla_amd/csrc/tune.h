@@ -20,7 +20,7 @@ enum Tune {
   TUNE_LP32 = 14,             // fp32 conv forward / data gradient: 2 = k_conv_lp<OP 0> where lp_ok, 1 = conv.hip kernels
   TUNE_LP32W = 15,            // fp32 weight gradient: 2 = k_wgrad_lp<OP 0> where lp_wgrad_ok, 1 = conv.hip kernels
   TUNE_LP_LK = 16,            // k_conv_lp K step (16-bit operands): 32 / 64 forced, 1 = automatic
-  TUNE_LPW_LK = 17,           // k_wgrad_lp pixels per step (bf16): 32 / 64 / 128 forced, 1 = automatic
+  TUNE_LPW_LK = 17,           // k_wgrad_lp pixels per step (bf16): 32 / 64 forced, 1 = automatic
   TUNE_KORDER = 18,           // conv forward / data-gradient K order: 1 = automatic, 2 = channel chunk outer, 3 = tap outer
   TUNE_XCD = 19,              // conv_lp.hip kernels: 2 = XCD-contiguous block order, 1 = hardware order
   TUNE_ATT_LANES = 20,        // attention lanes per query / key for long sequences: 1 (automatic), 2, 4
