@@ -288,6 +288,29 @@ __global__ void __launch_bounds__(FT_CH * FT_GROUPS) k_bn_finalize_tiles(
   shift[c] = (beta ? beta[c] : 0.f) - mu * sc;
 }
 
+// Eval statistics of many BatchNorm layers in one launch (e2ep_bn_eval_multi): block = one
+// table row {running_mean, running_var, gamma, beta, out, C, eps bits}; out = [mean | invstd |
+// scale | shift] (4 x C), the arithmetic of bn_finalize_channel's eval branch.
+__global__ void __launch_bounds__(256) k_bn_eval_multi(const long long *__restrict__ tab) {
+  const long long *r = tab + 7LL * blockIdx.x;
+  const float *rm = reinterpret_cast<const float *>(r[0]);
+  const float *rv = reinterpret_cast<const float *>(r[1]);
+  const float *gamma = reinterpret_cast<const float *>(r[2]);
+  const float *beta = reinterpret_cast<const float *>(r[3]);
+  float *out = reinterpret_cast<float *>(r[4]);
+  const int C = (int)r[5];
+  const float eps = __builtin_bit_cast(float, (int)r[6]);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float mu = rm[c];
+    const float is = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+    const float sc = is * (gamma ? gamma[c] : 1.f);
+    out[c] = mu;
+    out[C + c] = is;
+    out[2 * C + c] = sc;
+    out[3 * C + c] = (beta ? beta[c] : 0.f) - mu * sc;
+  }
+}
+
 // grid (C): eval (part == null) or a separate finalize after k_bn_stats
 __global__ void __launch_bounds__(256) k_bn_finalize(
     const double *__restrict__ part, int splits, long long cnt, float eps, float momentum,
@@ -983,6 +1006,12 @@ int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const
                        nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
                        dx, nullptr, dgamma, dbeta, plane_sums);
   return launch_status("e2ep_bn_bwd_planes");
+}
+
+int e2ep_bn_eval_multi(const long long *table, int n, void *stream) {
+  E2EP_REQUIRE(table && n > 0 && n <= 65535, E2EP_EINVAL, "e2ep_bn_eval_multi: bad table (n %d)", n);
+  hipLaunchKernelGGL(k_bn_eval_multi, dim3(n), dim3(256), 0, as_stream(stream), table);
+  return launch_status("e2ep_bn_eval_multi");
 }
 
 int e2ep_bn_small_limits(int fwd_max_vec, int bwd_max_vec) {

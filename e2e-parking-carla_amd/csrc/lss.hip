@@ -816,8 +816,12 @@ int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
     const int vec = ((uintptr_t)bev & 15) == 0 && XYZ % 4 == 0 && bev_bstride % 4 == 0;
     const int ll = tiles ? lss_lane_len(B, XYZ) : 0;
     const int gx = ll ? 8 * ll : cdiv(XYZ, E2EP_LSS_TILE) * B;
-    // e2ep_tune key 32: groups per block x rows in flight per group (A/B)
-    const int v = g_tune[TUNE_LSS_FWD];
+    // groups per block x feature rows in flight per group.  Automatic (e2ep_tune key 32 = 1):
+    // 16 rows when a sample's featT exceeds an XCD's 4 MB L2 (C4: 6.3 MB, its rows come from
+    // MALL / HBM: 89.8 -> 82.1 us, bitwise equal), else 8 (C2, 1 MB: 37.9 us against 44.8 us
+    // with 16, the extra VGPRs cost occupancy); profiles/r05/lss_fwd_variants.txt
+    int v = g_tune[TUNE_LSS_FWD];
+    if (v == 1 && 4LL * N * hw * C > (4LL << 20)) v = 3;
 #define E2EP_LSSF(NGV, UNV)                                                                      \
   hipLaunchKernelGGL((k_lss_fwd<E2EP_LSS_TILE, NGV, UNV>), dim3(gx, cdiv(C, 64)), dim3(NGV * 16), \
                      0, as_stream(stream), prob, featT, offsets, order, tiles, B, N, D, hw, C,    \
@@ -825,6 +829,7 @@ int e2ep_lss_fwd(const float *prob, const float *featT, const int32_t *offsets,
     if (v == 2) E2EP_LSSF(32, 8);
     else if (v == 3) E2EP_LSSF(16, 16);
     else if (v == 4) E2EP_LSSF(32, 16);
+    else if (v == 5) E2EP_LSSF(16, 8);
     else E2EP_LSSF(16, 8);
 #undef E2EP_LSSF
   }

@@ -108,6 +108,7 @@ SIGNATURES = {
     "e2ep_se_bwd_bn": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
     "e2ep_bn_bwd_planes": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
     "e2ep_bn_bwd_split": (_i, [_i, _i, _i, _i]),
+    "e2ep_bn_eval_multi": (_i, [_p, _i, _p]),
     "e2ep_se_gate_fwd": (_i, [_p, _p, _i, _i, _p, _p]),
     "e2ep_se_gate_bwd": (_i, [_p, _p, _p, _i, _i, _p, _p, _p]),
     "e2ep_adam_chunk_elems": (_i, []),

@@ -144,6 +144,98 @@ class BnCounters:
 _COUNTERS = []  # stack of active BnCounters (innermost last)
 
 
+class EvalBnBatch:
+    """Eval statistics (mean, invstd, folded scale / shift) of every BatchNorm whose
+    normalisation an inference forward hands to a fused consumer (the depthwise conv's and the
+    squeeze-excitation's input transforms) in ONE launch at scope entry (e2ep_bn_eval_multi)
+    instead of one e2ep_bn_stats launch per layer (42 of C5 predict's launches).
+
+    The first forward inside the scope records the BN modules in call order (each computing its
+    own statistics); later forwards compute every recorded layer's statistics into one
+    persistent buffer (stable addresses, so a captured predict graph replays the launch) and
+    hand out views.  Active only without autograd (torch.no_grad, the predict / agent path): a
+    view is rewritten by the next forward, so it must not be saved for a backward.  A layer that
+    was not recorded, or whose buffers moved, computes its own statistics."""
+
+    def __init__(self):
+        self.recorded = None
+        self._log = None
+        self._views = {}
+        self._key = None
+        self._table = None
+        self._buf = None
+        self.active = False
+
+    @staticmethod
+    def _key_of(bns):
+        return [(b.running_mean.data_ptr(), b.running_var.data_ptr(),
+                 b.weight.data_ptr() if b.weight is not None else 0,
+                 b.bias.data_ptr() if b.bias is not None else 0, b.num_features, float(b.eps))
+                for b in bns]
+
+    def _build(self, bns):
+        import struct
+        dev = bns[0].running_mean.device
+        self._buf = torch.empty(4 * sum(b.num_features for b in bns), dtype=torch.float32, device=dev)
+        rows, views, off = [], [], 0
+        for b in bns:
+            C = b.num_features
+            v = self._buf[off:off + 4 * C].view(4, C)
+            eps_bits = struct.unpack("<i", struct.pack("<f", float(b.eps)))[0]
+            rows.append([b.running_mean.data_ptr(), b.running_var.data_ptr(),
+                         b.weight.data_ptr() if b.weight is not None else 0,
+                         b.bias.data_ptr() if b.bias is not None else 0, v.data_ptr(), C, eps_bits])
+            views.append(v)
+            off += 4 * C
+        self._table = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self._key = self._key_of(bns)
+        self._vlist = views
+
+    def __enter__(self):
+        self.active = not torch.is_grad_enabled()
+        if self.active:
+            bns = self.recorded
+            if bns is None:
+                self._log = []
+            elif self._key_of(bns) != self._key:
+                self.recorded, self._log = None, []  # buffers moved: record again
+            else:
+                _lib.call("e2ep_bn_eval_multi", _lib.ptr(self._table), len(bns), _lib.stream())
+                self._views = {id(b): v for b, v in zip(bns, self._vlist)}
+        _EVAL_BN.append(self)
+        return self
+
+    def __exit__(self, *exc):
+        _EVAL_BN.pop()
+        if self.active and self.recorded is None and self._log and not exc[0]:
+            log = [b for b in self._log if b.track_running_stats and b.running_mean.is_cuda]
+            if 0 < len(log) <= 4096:
+                self.recorded = log
+                self._build(log)
+        self._log = None
+        self._views = {}
+        self.active = False
+        return False
+
+    def lookup(self, bn):
+        if not self.active:
+            return None
+        v = self._views.get(id(bn))
+        if v is None and self._log is not None and all(bn is not o for o in self._log):
+            self._log.append(bn)
+        return v
+
+
+_EVAL_BN = []  # active EvalBnBatch scopes (innermost last)
+
+
+def _eval_bn_stats(bn):
+    """This eval BN's (4, C) statistics from the active EvalBnBatch launch, or None."""
+    if not _EVAL_BN or not bn.track_running_stats or torch.is_grad_enabled():
+        return None
+    return _EVAL_BN[-1].lookup(bn)
+
+
 def _bn_train_and_count(bn):
     """BatchNorm2d.forward's mode choice and num_batches_tracked increment."""
     if bn.training and bn.track_running_stats:
@@ -311,15 +403,17 @@ class _BnActDwConv(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, act, w, dims, part=None, tiles=0,
-                ystats=None):
+                ystats=None, pre=None):
         x = x.contiguous()
         w = w.contiguous()
         N, C, H, W, K, P, Q = dims[:7]
         f32 = dict(dtype=torch.float32, device=x.device)
-        stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
+        stats = pre if pre is not None else torch.empty(4, C, **f32)  # mean, invstd, scale, shift
         s = _lib.stream()
         with timing.region(timing.name("bn_fwd", x.shape, "_BnActDwConv")):
-            if part is not None and train:  # partials from the expand conv's epilogue
+            if pre is not None:  # eval statistics of the forward's EvalBnBatch launch
+                pass
+            elif part is not None and train:  # partials from the expand conv's epilogue
                 fws = _ws(_lib.load().e2ep_bn_finalize_part_workspace(C, tiles), x.device)
                 _lib.call("e2ep_bn_finalize_part", _lib.ptr(part), tiles, _lib.ptr(gamma),
                           _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W, float(momentum),
@@ -384,7 +478,7 @@ class _BnActDwConv(torch.autograd.Function):
                           _lib.ptr(db), None, _lib.ptr(ws), _lib.nbytes(ws), s)
         if fork is not None:
             fork.join()
-        return dx, dg, db, None, None, None, None, None, None, dw, None, None, None, None
+        return dx, dg, db, None, None, None, None, None, None, dw, None, None, None, None, None
 
 
 def depthwise_conv2d(x, w, stride, pad, bn_stats=False):
@@ -434,7 +528,7 @@ def bn_act_depthwise_conv2d(x, bn, act, w, stride, pad, bn_stats=False):
     dims = (N, C, H, W, K, P, Q, stride, t, l)
     ys, tiles = _dw_stats_buffer(dims, x.device, bn_stats)
     y = _BnActDwConv.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, ACT[act], w, dims,
-                           *(pp or (None, 0)), ys)
+                           *(pp or (None, 0)), ys, None if train else _eval_bn_stats(bn))
     if ys is not None:
         y._e2ep_bn_part = (ys, tiles)
     return y
@@ -592,16 +686,18 @@ class _BnSwishSE(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, rm, rv, train, momentum, eps, w1, b1, w2, b2, part=None,
-                tiles=0):
+                tiles=0, pre=None):
         x = x.contiguous()
         N, C, H, W = x.shape
         sq = w1.shape[0]
         dev = x.device
         f32 = dict(dtype=torch.float32, device=dev)
-        stats = torch.empty(4, C, **f32)  # mean, invstd, scale, shift
+        stats = pre if pre is not None else torch.empty(4, C, **f32)  # mean, invstd, scale, shift
         s = _lib.stream()
         with timing.region(timing.name("bn_fwd", x.shape, "_BnSwishSE")):
-            if part is not None and train:  # partials from the depthwise kernel
+            if pre is not None:  # eval statistics of the forward's EvalBnBatch launch
+                pass
+            elif part is not None and train:  # partials from the depthwise kernel
                 fws = _ws(_lib.load().e2ep_bn_finalize_part_workspace(C, tiles), x.device)
                 _lib.call("e2ep_bn_finalize_part", _lib.ptr(part), tiles, _lib.ptr(gamma),
                           _lib.ptr(beta), _lib.ptr(rm), _lib.ptr(rv), N, C, H, W, float(momentum),
@@ -663,7 +759,7 @@ class _BnSwishSE(torch.autograd.Function):
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(a),
                           _lib.ptr(dpooled), _lib.ptr(planes), N, C, H, W, ACT["swish"],
                           _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), s)
-            return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None
+            return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None, None
         with timing.region(timing.name("se_bwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
                       _lib.ptr(dy), _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled),
@@ -676,7 +772,7 @@ class _BnSwishSE(torch.autograd.Function):
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           _lib.ptr(a), _lib.ptr(dpooled), N, C, H, W, int(ctx.train), ACT["swish"],
                           _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), None, _lib.ptr(bws), _lib.nbytes(bws), s)
-        return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None
+        return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None, None
 
 
 def bn_swish_squeeze_excite(x, bn, w1, b1, w2, b2):
@@ -688,7 +784,7 @@ def bn_swish_squeeze_excite(x, bn, w1, b1, w2, b2):
     mom = bn.momentum if bn.momentum is not None else 0.1
     pp = conv.bn_partials(x) if train else None
     return _BnSwishSE.apply(x, bn.weight, bn.bias, rm, rv, train, mom, bn.eps, w1, b1, w2, b2,
-                            *(pp or (None, 0)))
+                            *(pp or (None, 0)), None if train else _eval_bn_stats(bn))
 
 
 def squeeze_excite(x, w1, b1, w2, b2):

@@ -60,7 +60,11 @@ class ParkingModel(nn.Module):
                     self._bn_counters = nn_ops.BnCounters()
                 with self._bn_counters:
                     return self._encoder(data, noise)
-            return self._encoder(data, noise)
+            # inference: the fused BN consumers' eval statistics in one launch (no_grad only)
+            if getattr(self, "_eval_bn", None) is None:
+                self._eval_bn = nn_ops.EvalBnBatch()
+            with self._eval_bn:
+                return self._encoder(data, noise)
 
     def _encoder(self, data, noise=None):
         dev = self.bev_model.frustum.device

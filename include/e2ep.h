@@ -313,6 +313,12 @@ int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const
                        const float *gamma, const float *beta, const float *gate_logit,
                        const float *gate_dpooled, const double *plane_sums, int N, int C, int H,
                        int W, int act, float *dx, float *dgamma, float *dbeta, void *stream);
+/* Eval-mode statistics of n BatchNorm layers in one launch (the per-layer e2ep_bn_stats calls
+ * of an inference forward, 42 launches of C5 predict): table = DEVICE array of n rows of 7
+ * int64 {running_mean, running_var, gamma (nullable), beta (nullable), out, C, eps as fp32
+ * bits}; out [4][C] = mean, invstd, scale, shift, the same arithmetic as e2ep_bn_stats with
+ * train = 0. */
+int e2ep_bn_eval_multi(const long long *table, int n, void *stream);
 /* Stand-alone activation (act as above) and its gradient w.r.t. the pre-activation x. */
 int e2ep_act_fwd(const float *x, long long n, int act, float *y, void *stream);
 int e2ep_act_bwd(const float *x, const float *dy, long long n, int act, float *dx, void *stream);

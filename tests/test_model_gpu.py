@@ -134,3 +134,32 @@ def test_low_precision_predict_tokens_match_reference(mode, tol):
     e_seg, e_dep = rel_l2(ps, g["pred_segmentation"]), rel_l2(pd, g["pred_depth"])
     print(f"{mode} predict: seg rel-L2 {e_seg:.2e}, depth rel-L2 {e_dep:.2e}")
     assert e_seg < tol and e_dep < tol
+
+
+def test_eval_bn_batch_equals_per_layer_statistics():
+    """nn_ops.EvalBnBatch: the second and later no_grad forwards compute the fused BN
+    consumers' eval statistics in one e2ep_bn_eval_multi launch; outputs are bitwise those of
+    the first forward (per-layer e2ep_bn_stats), also after the running statistics change and
+    under a captured graph; with autograd on the batch stays inactive."""
+    from e2ep_amd import graphs, nn_ops, synthetic
+    m = _model(True).eval()
+    data = synthetic.synthetic_batch(1, seed=5)
+    data = {k: (v if k in ("intrinsics", "extrinsics") else v.to(DEV)) for k, v in data.items()}
+    noise = synthetic.target_noise(1, seed=5).to(DEV)
+    with torch.no_grad():
+        first = [t.clone() for t in m(data, noise)]
+        assert m._eval_bn.recorded is not None and len(m._eval_bn.recorded) >= 40
+        second = m(data, noise)
+        assert all(torch.equal(a, b) for a, b in zip(first, second))
+        # new running statistics: the batch launch reads them at every forward
+        bns = m._eval_bn.recorded
+        for b in bns:
+            b.running_var.mul_(1.5).add_(0.01)
+        m._eval_bn.recorded = None  # record again: per-layer statistics of the new values
+        ref = [t.clone() for t in m(data, noise)]
+        g, out, _ = graphs.capture(lambda: m(data, noise))
+        g.replay()
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(ref, out))
+        assert not all(torch.equal(a, b) for a, b in zip(ref, first))
+    assert nn_ops._eval_bn_stats(bns[0]) is None  # autograd on: no shared views
