@@ -1,10 +1,10 @@
 // Squeeze-and-excitation of efficientnet-pytorch's MBConv as one fused op, NCHW fp32, gfx950
 // (reference: efficientnet-pytorch 0.7.1 MBConvBlock, used through model/cam_encoder.py:69-73):
 //   pooled = mean_hw(x);  h = swish(W1 pooled + b1);  a = W2 h + b2;  y = x * sigmoid(a)
-// Forward: squeeze (wave per plane), the MLP on the 1x1 map as one launch (k_se_mlp_fwd),
-// excite (float4 stream).  Backward: da (wave per plane), the MLP backward as one launch
-// (k_se_mlp_bwd: dh over channel spans, dhpre, dpooled), one weight-gradient kernel (sums
-// over the batch in fixed order), and
+// Forward: squeeze (wave per plane), the MLP on the 1x1 map as two small kernels (hidden
+// units, wave per output; logits, LDS-staged W2 tile), excite (float4 stream).  Backward: da
+// (wave per plane), MLP backward (dh partials over channel spans, then dhpre + dpooled), one
+// weight-gradient kernel (sums over the batch in fixed order), and
 // dx = dy * sigmoid(a) + dpooled / HW in a single stream — no separate avg-pool backward and
 // no autograd add of the two input-gradient paths.
 #include "common.h"
@@ -72,45 +72,57 @@ __global__ void __launch_bounds__(256) k_se_squeeze(const float *__restrict__ x,
   if ((threadIdx.x & 63) == 0) pooled[pl] = s / (float)HW;
 }
 
-// The MLP on the 1x1 map in ONE launch (round 5; k_se_hidden + k_se_logits were two
-// launch-latency-bound ~5 us kernels per layer): grid (N, C / 256), block (n, chunk) computes
-// sample n's whole hidden layer (sq dots of length C, k_se_hidden's lane order) into LDS —
-// each chunk recomputes it, sq * C MACs — then the logits of its 256 channels (k_se_logits'
-// k order).  Bitwise the two-kernel results; chunk 0 stores hpre for the backward.
-__global__ void __launch_bounds__(256) k_se_mlp_fwd(const float *__restrict__ pooled,
-                                                    const float *__restrict__ w1,
-                                                    const float *__restrict__ b1,
-                                                    const float *__restrict__ w2,
-                                                    const float *__restrict__ b2, int C, int sq,
-                                                    float *__restrict__ hpre,
-                                                    float *__restrict__ a) {
-  __shared__ float sh[SE_MAXSQ];
-  const int n = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const float *pn = pooled + (size_t)n * C;
-  for (int k = wave; k < sq; k += 4) {  // k_se_hidden's dot
-    const float *wr = w1 + (size_t)k * C;
-    float s0 = 0.f, s1 = 0.f;
-    int c = lane;
-    for (; c + 64 < C; c += 128) {
-      s0 += wr[c] * pn[c];
-      s1 += wr[c + 64] * pn[c + 64];
-    }
-    if (c < C) s0 += wr[c] * pn[c];
-    const float s = wave_sum(s0 + s1);
-    if (lane == 0) {
-      const float z = s + (b1 ? b1[k] : 0.f);
-      if (blockIdx.y == 0) hpre[(size_t)n * sq + k] = z;
-      sh[k] = z * sigm(z);
-    }
+// hpre[n][k] = W1[k] . pooled[n] + b1[k]  (W1 [sq][C]): one wave per (n, k), lanes along
+// the W1 row and pooled[n] (coalesced), fixed-order wave reduction.  grid (N, sq / 4).
+__global__ void __launch_bounds__(256) k_se_hidden(const float *__restrict__ pooled,
+                                                   const float *__restrict__ w1,
+                                                   const float *__restrict__ b1, int C, int sq,
+                                                   float *__restrict__ hpre) {
+  const int n = blockIdx.x, k = blockIdx.y * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (k >= sq) return;
+  const float *pn = pooled + (size_t)n * C, *wr = w1 + (size_t)k * C;
+  float s0 = 0.f, s1 = 0.f;
+  int c = lane;
+  for (; c + 64 < C; c += 128) {
+    s0 += wr[c] * pn[c];
+    s1 += wr[c + 64] * pn[c + 64];
+  }
+  if (c < C) s0 += wr[c] * pn[c];
+  const float s = wave_sum(s0 + s1);
+  if (lane == 0) hpre[(size_t)n * sq + k] = s + (b1 ? b1[k] : 0.f);
+}
+
+// a[n][c] = W2[c] . swish(hpre[n]) + b2[c]  (W2 [C][sq]).  A block owns SE_CT channels x
+// SE_NT samples: the W2 rows of its channels (one contiguous span, loaded coalesced) and the
+// samples' hidden vectors are staged in LDS; thread (c, n) then dots them.  grid
+// (C / SE_CT, N / SE_NT), dynamic LDS (SE_CT * (sq + 1) + SE_NT * sq) floats.
+constexpr int SE_CT = 32, SE_NT = 8;
+__global__ void __launch_bounds__(256) k_se_logits(const float *__restrict__ hpre,
+                                                   const float *__restrict__ w2,
+                                                   const float *__restrict__ b2, int N, int C,
+                                                   int sq, float *__restrict__ a) {
+  extern __shared__ float lds[];
+  const int ld = sq + 1;  // odd row stride: the 32 rows sit in distinct banks
+  float *sw = lds, *sh = lds + SE_CT * ld;
+  const int c0 = blockIdx.x * SE_CT, n0 = blockIdx.y * SE_NT;
+  const int nc = min(SE_CT, C - c0), nn = min(SE_NT, N - n0);
+  const float *src = w2 + (size_t)c0 * sq;
+  for (int e = threadIdx.x; e < nc * sq; e += 256) {
+    const int r = e / sq;
+    sw[r * ld + (e - r * sq)] = src[e];
+  }
+  for (int e = threadIdx.x; e < nn * sq; e += 256) {
+    const float z = hpre[(size_t)n0 * sq + e];
+    sh[e] = z * sigm(z);
   }
   __syncthreads();
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= C) return;
-  const float *wr = w2 + (size_t)c * sq;
+  const int ci = threadIdx.x % SE_CT, ni = threadIdx.x / SE_CT;
+  if (ci >= nc || ni >= nn) return;
+  const float *wr = sw + ci * ld, *hr = sh + ni * sq;
   float s = 0.f;
 #pragma unroll 4
-  for (int k = 0; k < sq; ++k) s += wr[k] * sh[k];
-  a[(size_t)n * C + c] = s + (b2 ? b2[c] : 0.f);
+  for (int k = 0; k < sq; ++k) s += wr[k] * hr[k];
+  a[(size_t)(n0 + ni) * C + c0 + ci] = s + (b2 ? b2[c0 + ci] : 0.f);
 }
 
 // y = x * sigmoid(a[plane]); float4 stream (HW % 4 == 0) or scalar
@@ -244,44 +256,47 @@ __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn
   }
 }
 
-// channels per dh span of the MLP backward (the span partials are summed in span order)
+// Partial dh over one span of SE_DH_SPAN channels: dhp[n][j][k] = sum_{c in span j} W2[c][k]
+// da[n][c].  Threads form KT hidden-unit lanes (KT = sq rounded up to a power of two, <= 256)
+// x 256/KT channel slices, so a row of W2 is read by consecutive threads; the slices are
+// summed in fixed order through LDS.  grid (N, C / SE_DH_SPAN).
 constexpr int SE_DH_SPAN = 256;
+static_assert(SE_MAXC / SE_DH_SPAN == 16, "e2ep_se_bwd workspace (e2ep.h) holds 16 dh partials");
+__global__ void __launch_bounds__(256) k_se_dh(const float *__restrict__ da,
+                                               const float *__restrict__ w2, int C, int sq, int KT,
+                                               float *__restrict__ dhp) {
+  __shared__ float red[256];
+  const int n = blockIdx.x, j = blockIdx.y;
+  const int k = threadIdx.x % KT, sl = threadIdx.x / KT, nsl = 256 / KT;
+  const int cb = j * SE_DH_SPAN, ce = min(C, cb + SE_DH_SPAN);
+  const float *dn = da + (size_t)n * C;
+  float s = 0.f;
+  if (k < sq)
+#pragma unroll 4
+    for (int c = cb + sl; c < ce; c += nsl) s += w2[(size_t)c * sq + k] * dn[c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < KT && k < sq) {
+    float t = 0.f;
+    for (int q = 0; q < nsl; ++q) t += red[q * KT + k];
+    dhp[((size_t)n * gridDim.y + j) * sq + k] = t;
+  }
+}
 
-// The MLP backward in ONE launch (round 5; was k_se_dh + k_se_dpooled): grid (N, C / 256),
-// block (n, chunk) computes sample n's dh over every channel span in k_se_dh's order (KT
-// hidden-unit lanes x 256/KT channel slices per span, slices summed in order, spans summed in
-// order), dhpre = dh swish'(hpre), then dpooled for its 256 channels (k_se_dpooled's order).
-// Bitwise the two-kernel results; chunk 0 stores dhpre for the weight gradients.
-__global__ void __launch_bounds__(256) k_se_mlp_bwd(const float *__restrict__ da,
-                                                    const float *__restrict__ w2,
+// dhpre = (sum of the dh partials) * swish'(hpre);  dpooled[n][c] = sum_k W1[k][c] dhpre[n][k]
+// (thread per c, coalesced W1 columns).  grid (N, C-chunks of 256).
+__global__ void __launch_bounds__(256) k_se_dpooled(const float *__restrict__ dhp, int spans,
                                                     const float *__restrict__ hpre,
                                                     const float *__restrict__ w1, int C, int sq,
-                                                    int KT, float *__restrict__ dhpre,
+                                                    float *__restrict__ dhpre,
                                                     float *__restrict__ dpooled) {
-  __shared__ float red[256];
   __shared__ float sd[SE_MAXSQ];
   const int n = blockIdx.x;
-  const int k = threadIdx.x % KT, sl = threadIdx.x / KT, nsl = 256 / KT;
-  const float *dn = da + (size_t)n * C;
-  float tot = 0.f;  // threads < KT: the span partials' running sum, span order
-  for (int cb = 0; cb < C; cb += SE_DH_SPAN) {
-    const int ce = min(C, cb + SE_DH_SPAN);
-    float s = 0.f;
-    if (k < sq)
-#pragma unroll 4
-      for (int c = cb + sl; c < ce; c += nsl) s += w2[(size_t)c * sq + k] * dn[c];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x < KT && k < sq) {
-      float t = 0.f;
-      for (int q = 0; q < nsl; ++q) t += red[q * KT + k];
-      tot += t;
-    }
-    __syncthreads();  // red is rewritten by the next span
-  }
-  if (threadIdx.x < KT && k < sq) {
+  for (int k = threadIdx.x; k < sq; k += 256) {
+    float t = 0.f;
+    for (int j = 0; j < spans; ++j) t += dhp[((size_t)n * spans + j) * sq + k];
     const float z = hpre[(size_t)n * sq + k], sg = sigm(z);
-    const float g = tot * (sg * (1.f + z * (1.f - sg)));
+    const float g = t * (sg * (1.f + z * (1.f - sg)));
     if (blockIdx.y == 0) dhpre[(size_t)n * sq + k] = g;
     sd[k] = g;
   }
@@ -290,7 +305,7 @@ __global__ void __launch_bounds__(256) k_se_mlp_bwd(const float *__restrict__ da
   if (c < C) {
     float s = 0.f;
 #pragma unroll 8
-    for (int kk = 0; kk < sq; ++kk) s += w1[(size_t)kk * C + c] * sd[kk];
+    for (int k = 0; k < sq; ++k) s += w1[(size_t)k * C + c] * sd[k];
     dpooled[(size_t)n * C + c] = s;
   }
 }
@@ -374,8 +389,10 @@ int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, cons
   const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
   hipLaunchKernelGGL(k_se_squeeze, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, planes, HW,
                      pooled);
-  hipLaunchKernelGGL(k_se_mlp_fwd, dim3(N, cdiv(C, 256)), dim3(256), 0, s, pooled, w1, b1, w2, b2,
-                     C, sq, hpre, a);
+  hipLaunchKernelGGL(k_se_hidden, dim3(N, cdiv(sq, 4)), dim3(256), 0, s, pooled, w1, b1, C, sq,
+                     hpre);
+  hipLaunchKernelGGL(k_se_logits, dim3(cdiv(C, SE_CT), cdiv(N, SE_NT)), dim3(256),
+                     (SE_CT * (sq + 1) + SE_NT * sq) * sizeof(float), s, hpre, w2, b2, N, C, sq, a);
   hipLaunchKernelGGL(k_se_excite, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, tf, a, HW, nvec, vec,
                      y);
   return launch_status("e2ep_se_fwd");
@@ -398,6 +415,8 @@ static int se_bwd_impl(const float *x, const float *x_scale, const float *x_shif
   const int planes = N * C;
   float *da = workspace, *dhpre = workspace + 2 * planes;
   float *dpooled = dpooled_out ? dpooled_out : workspace + planes;
+  float *dhp = workspace + 2 * planes + N * sq;
+  const int spans = cdiv(C, SE_DH_SPAN);
   int KT = 1;
   while (KT < sq) KT *= 2;
   if (bn.sums)
@@ -406,8 +425,9 @@ static int se_bwd_impl(const float *x, const float *x_scale, const float *x_shif
   else
     hipLaunchKernelGGL(k_se_da<false>, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes,
                        HW, da, bn);
-  hipLaunchKernelGGL(k_se_mlp_bwd, dim3(N, cdiv(C, 256)), dim3(256), 0, s, da, w2, hpre, w1, C,
-                     sq, KT, dhpre, dpooled);
+  hipLaunchKernelGGL(k_se_dh, dim3(N, spans), dim3(256), 0, s, da, w2, C, sq, KT, dhp);
+  hipLaunchKernelGGL(k_se_dpooled, dim3(N, cdiv(C, 256)), dim3(256), 0, s, dhp, spans, hpre, w1,
+                     C, sq, dhpre, dpooled);
   if (dw1 || db1 || dw2 || db2) {
     const int outs = 2 * sq * C + sq + C;
     hipLaunchKernelGGL(k_se_wgrad, dim3(cdiv(outs, 256)), dim3(256), 0, s, pooled, hpre, da, dhpre,

@@ -7,7 +7,8 @@
 #   bench             the default bench line (C2 + secondary C3 / C4 / C5 + cpu_baseline)
 #   c2 | c3           one bench line, no CPU baseline / secondaries (c3: --precision bf16)
 #   ab:VAR:REP:v1,v2  interleaved in-step A/B of an environment switch on C2 (c3ab: on C3);
-#                     values separated by '/' when they contain commas
+#                     values separated by '/' when they contain commas, by '|' when they
+#                     contain '/' (library paths for E2EP_LIB)
 #   table:PREC        rocprofv3 kernel trace of 10 replayed steps (PREC fp32 | bf16) ->
 #                     step_kernels_PREC.txt + step_sequence_PREC.txt
 #   stats             rocprofv3 --kernel-trace --stats of the default bench command
@@ -37,11 +38,11 @@ for st in "$@"; do
     ab:*|c3ab:*)
       IFS=: read -r kind var rep vals <<< "$st"
       p=""; [ "$kind" = c3ab ] && p="--precision bf16"
-      sep=','; [[ "$vals" == */* ]] && sep='/'
+      sep=','; [[ "$vals" == */* ]] && sep='/'; [[ "$vals" == *"|"* ]] && sep='|'
       IFS="$sep" read -r -a vs <<< "$vals"
       for i in $(seq 1 "$rep"); do
         for v in "${vs[@]}"; do
-          log="$O/${kind}_${var}_${v//,/_}_$i.log"
+          tag=${v//,/_}; tag=${tag//\//_}; log="$O/${kind}_${var}_${tag}_$i.log"
           env "$var=$v" timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary $p > "$log" 2>&1 || { tail -20 "$log"; exit 1; }
           echo "$kind $var=$v run $i: $(val ms_per_step "$log")"
         done
