@@ -86,7 +86,10 @@ class TapMajorBatch:
         _TAP_BATCH.pop()
         self.active = False
         self._views = {}
-        if self.recorded is None and self._log is not None and not exc[0]:
+        # the table is built outside any graph capture (a host->device copy): a capture-only
+        # process records again on its first eager forward
+        if (self.recorded is None and self._log is not None and not exc[0]
+                and not torch.cuda.is_current_stream_capturing()):
             log = [w for w in self._log if w.dtype == torch.float32 and w.is_contiguous()]
             if 0 < len(log) <= 256:
                 self.recorded = log

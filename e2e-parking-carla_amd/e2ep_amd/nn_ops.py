@@ -207,7 +207,8 @@ class EvalBnBatch:
 
     def __exit__(self, *exc):
         _EVAL_BN.pop()
-        if self.active and self.recorded is None and self._log and not exc[0]:
+        if (self.active and self.recorded is None and self._log and not exc[0]
+                and not torch.cuda.is_current_stream_capturing()):  # host->device table copy
             log = [b for b in self._log if b.track_running_stats and b.running_mean.is_cuda]
             if 0 < len(log) <= 4096:
                 self.recorded = log

@@ -34,7 +34,11 @@ class BevModel(nn.Module):
         self.frustum = self.create_frustum()
         self.depth_channel = self.frustum.shape[0]
         self.cam_encoder = CamEncoder(cfg, self.depth_channel)
-        self._host_consts = None
+        # the grid constants as host values, computed here from the (host) parameters and again
+        # whenever the parameters change (load_state_dict): a capture-only process (no eager
+        # forward before the graph capture) can then plan without a device->host copy
+        self._host_consts = self._consts()
+        self._consts_key = self._consts_version()
         self._plan_key = None
         self._plan = None
 
@@ -48,6 +52,10 @@ class BevModel(nn.Module):
         v = torch.linspace(0, H - 1, h, dtype=torch.float).view(1, h, 1).expand(D, h, w)
         return nn.Parameter(torch.stack((u, v, depth.view(D, 1, 1).expand(D, h, w)), -1),
                             requires_grad=False)
+
+    def _consts_version(self):
+        return tuple((p.data_ptr(), p._version) for p in (self.bev_res, self.bev_start_pos,
+                                                           self.bev_dim))
 
     def _consts(self):
         # lo = start - res/2 in fp32 exactly as the reference evaluates it (bev_model.py:85)
@@ -69,8 +77,10 @@ class BevModel(nn.Module):
         replays from the device rig each time; its last fp32 ulp is not LAPACK's, so a few
         points on a cell edge may land in the neighbouring pillar (tests/test_lss_gpu.py).
         E2EP_PLAN_CACHE=0 rebuilds the plan every call."""
-        if self._host_consts is None:
-            self._host_consts = self._consts()
+        if not torch.cuda.is_current_stream_capturing():
+            key = self._consts_version()
+            if key != self._consts_key:  # moved or reloaded parameters (no copy inside capture)
+                self._host_consts, self._consts_key = self._consts(), key
         lo, res, dims = self._host_consts
         on_dev = intrinsics.is_cuda or extrinsics.is_cuda
         if on_dev and torch.cuda.is_current_stream_capturing():
