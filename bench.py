@@ -230,6 +230,19 @@ def load_traffic(batch):
     return float(j["hbm_bytes_per_launch"])
 
 
+def load_conv_traffic(batch, lowp):
+    """HBM bytes per step of the conv forward + data-gradient family from the committed
+    rocprofv3 PMC summary (scripts/conv_family_pmc.py), or None."""
+    path = os.path.join(ROOT, "profiles", f"conv_family_pmc_{'bf16' if lowp else 'fp32'}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        j = json.load(f)
+    if int(j.get("batch", -1)) != batch:
+        return None
+    return j
+
+
 def _free_port():
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -291,7 +304,7 @@ def train_step_rate(dev, world, rank, batch, steps, warmup, hires=False, eager=F
             "loss": loss, "module": mod, "step": step}
 
 
-def conv_roofline(step, lowp, n_eager=3):
+def conv_roofline(step, lowp, n_eager=3, batch=8):
     """The headline roofline entry: the conv GEMM family (forward + data gradient), its FLOPs
     (2*N*Cout*P*Q*Cin*R*S per launch) over its summed HIP-event time in `n_eager` eager
     forward+backward passes on the launch stream after the timed region (graph replays cannot
@@ -325,6 +338,8 @@ def conv_roofline(step, lowp, n_eager=3):
                        "; the step's largest kernel family",
              "bound": "mfma", "achieved": round(g_tfs, 2), "peak": g_peak,
              "unit": "TFLOP/s", "frac": round(g_tfs / g_peak, 4), "traffic": None,
+             "traffic_note": "HBM bytes per step of the family (2 x FETCH_SIZE + WRITE_SIZE over its "
+                             "dispatches, profiles/conv_family_pmc_<precision>.json)",
              "flop_per_step": g_flop / n_eager, "ms_per_step": round(g_ms / n_eager, 4),
              "launches_per_step": g_launch // n_eager,
              "timing": f"HIP events around every conv fwd/dgrad launch of {n_eager} eager fwd+bwd "
@@ -333,6 +348,10 @@ def conv_roofline(step, lowp, n_eager=3):
                        "off), while the timed step runs most of them paired with their weight "
                        "gradient in one grid (k_conv_bwd_pair / k_conv_bwd_pair1x1 / "
                        "k_lp_bwd_pair), so this is a per-kernel figure, not the step's"}
+    tj = load_conv_traffic(batch, lowp)
+    if tj is not None:
+        entry["traffic"] = tj["hbm_bytes_per_step"]
+        entry["traffic_over_algorithmic"] = tj["traffic_over_algorithmic"]
     return entry, kern
 
 
@@ -519,7 +538,7 @@ def main():
     data = step.batch
 
     lowp = args.precision != "fp32"
-    roofline, kern = conv_roofline(step, lowp)
+    roofline, kern = conv_roofline(step, lowp, batch=args.batch)
     step_tfs = STEP_GFLOP_PER_SAMPLE * 1e9 * args.batch / (ms_step * 1e-3) / 1e12
     step_roofline = None if hires else {"bound": "mfma", "achieved": round(step_tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": round(step_tfs / FP32_MFMA_PEAK_TFS, 4),
