@@ -21,7 +21,7 @@ int g_tune[TUNE_N] = {2048, 4096, 1024, 512, 768, 1024, 512, 1, 1, 2, 1, 2, 2, 1
 }  // namespace e2ep
 
 extern "C" {
-int e2ep_abi_version(void) { return 2; }
+int e2ep_abi_version(void) { return 3; }
 int e2ep_tune(int key, int value) {
   if (key < 0 || key >= e2ep::TUNE_N || key == e2ep::TUNE_RETIRED_27 ||
       key == e2ep::TUNE_RETIRED_29 || key == e2ep::TUNE_RETIRED_31)

@@ -48,7 +48,9 @@ template <>
 struct Vec<4> {
   typedef float4 T;
   static __device__ __forceinline__ float4 ld(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+  static __device__ __forceinline__ float4 ld(const bf16_t *p) { return ld4(p); }
   static __device__ __forceinline__ void st(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+  static __device__ __forceinline__ void st(bf16_t *p, float4 v) { st4(p, v); }
   static __device__ __forceinline__ float get(const float4 &v, int i) {
     return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
   }
@@ -61,7 +63,9 @@ template <>
 struct Vec<1> {
   typedef float T;
   static __device__ __forceinline__ float ld(const float *p) { return *p; }
+  static __device__ __forceinline__ float ld(const bf16_t *p) { return ld1(p); }
   static __device__ __forceinline__ void st(float *p, float v) { *p = v; }
+  static __device__ __forceinline__ void st(bf16_t *p, float v) { st1(p, v); }
   static __device__ __forceinline__ float get(const float &v, int) { return v; }
   static __device__ __forceinline__ void set(float &v, int, float f) { v = f; }
   static __device__ __forceinline__ float zero() { return 0.f; }
@@ -100,8 +104,8 @@ __device__ __forceinline__ float dc_scale(const float *dc_rand, float keep, int 
 }
 
 // partial sums over a slice of channel c: grid (C, splits); slice = `per` vectors
-template <int VEC>
-__global__ void __launch_bounds__(256) k_bn_stats(const float *__restrict__ x, int N, int C,
+template <int VEC, typename TX = float>
+__global__ void __launch_bounds__(256) k_bn_stats(const TX *__restrict__ x, int N, int C,
                                                   int HWv, int splits, int per,
                                                   double *__restrict__ part) {
   const int c = blockIdx.x, sp = blockIdx.y;
@@ -420,9 +424,9 @@ __device__ __forceinline__ void bns_factors_finish(const float *dc_rand, float k
 }
 
 // backward reduction: per channel sums of dzb and dzb * xhat (fp64); grid (C, splits)
-template <int VEC>
+template <int VEC, typename TX = float, typename TD = float>
 __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
-    const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
+    const TX *__restrict__ x, const TD *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
     const float *__restrict__ dc_rand, float dc_keep, BnGate gt, int N, int C, int HWv,
@@ -470,14 +474,14 @@ __global__ void __launch_bounds__(256) k_bn_bwd_finalize(const double *__restric
 // dres = dz;  dx = gamma * invstd * (dzb - (sum_dzb + xhat * sum_dzbxhat) / M)   (train)
 //             dx = gamma * invstd * dzb                                          (eval)
 // grid (C, chunks); chunk 0 of each channel writes dgamma / dbeta.
-template <int VEC>
+template <int VEC, typename TX = float, typename TD = float, typename TO = float>
 __global__ void __launch_bounds__(256) k_bn_bwd_apply(
-    const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
+    const TX *__restrict__ x, const TD *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
     const float *__restrict__ dc_rand, float dc_keep, BnGate gt, const double *__restrict__ part,
     int splits, long long cnt, int N, int C, int HWv, int per, int act, int train,
-    float *__restrict__ dx, float *__restrict__ dres, float *__restrict__ dgamma,
+    TO *__restrict__ dx, float *__restrict__ dres, float *__restrict__ dgamma,
     float *__restrict__ dbeta, const double *__restrict__ planes) {
   const int c = blockIdx.x, j = blockIdx.y;
   double s, q;
@@ -570,9 +574,9 @@ __device__ __forceinline__ size_t bns_off(int t, int HWv, int C, int c) {
 }
 
 // train-mode forward; y == null: statistics only (scale / shift for an apply-on-load consumer)
-template <int T, int R>
+template <int T, int R, typename TX = float>
 __global__ void __launch_bounds__(T) k_bn_fwd_small(
-    const float *__restrict__ x, long long cnt, float eps, float momentum,
+    const TX *__restrict__ x, long long cnt, float eps, float momentum,
     float *__restrict__ running_mean, float *__restrict__ running_var, float *__restrict__ mean_out,
     float *__restrict__ invstd_out, const float *__restrict__ gamma, const float *__restrict__ beta,
     const float *__restrict__ res, const float *__restrict__ dc_rand, float dc_keep, int N, int C,
@@ -636,13 +640,13 @@ __global__ void __launch_bounds__(T) k_bn_fwd_small(
   }
 }
 
-template <int T, int R>
+template <int T, int R, typename TX = float, typename TD = float, typename TO = float>
 __global__ void __launch_bounds__(T) k_bn_bwd_small(
-    const float *__restrict__ x, const float *__restrict__ dy, const float *__restrict__ mean,
+    const TX *__restrict__ x, const TD *__restrict__ dy, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
     const float *__restrict__ dc_rand, float dc_keep, BnGate gt, long long cnt, int N, int C,
-    int HWv, int act, int train, float *__restrict__ dx, float *__restrict__ dres,
+    int HWv, int act, int train, TO *__restrict__ dx, float *__restrict__ dres,
     float *__restrict__ dgamma, float *__restrict__ dbeta) {
   const int c = blockIdx.x, tot = N * HWv;
   const BnBwdElem<4> el{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f,
@@ -710,19 +714,22 @@ static int bns_r(int totv, int &threads) {
   if (per <= BNS_R) return 8;
   return 0;
 }
-#define BNS_LAUNCH(KERNEL, R, TH, ...)                                                            \
+#define BNS_LAUNCH(KERNEL, R, TH, ...) BNS_LAUNCH_T(KERNEL, , R, TH, __VA_ARGS__)
+// TYPES: the kernel's storage-type template arguments after <threads, R> (", bf16_t, float, ..."
+// or empty)
+#define BNS_LAUNCH_T(KERNEL, TYPES, R, TH, ...)                                                   \
   do {                                                                                            \
     (void)(TH);                                                                                   \
-    if (R == 1) hipLaunchKernelGGL((KERNEL<BNS_T, 1>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);  \
+    if (R == 1) hipLaunchKernelGGL((KERNEL<BNS_T, 1 TYPES>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);  \
     else if (R == 2 && g_tune[TUNE_BNS_WIDE_LO] == 2)                                             \
-      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 1>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__);      \
-    else if (R == 2) hipLaunchKernelGGL((KERNEL<BNS_T, 2>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
+      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 1 TYPES>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__); \
+    else if (R == 2) hipLaunchKernelGGL((KERNEL<BNS_T, 2 TYPES>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
     else if (R == 4 && g_tune[TUNE_BNS_WIDE_LO] == 2)                                             \
-      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 2>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__);      \
-    else if (R == 4) hipLaunchKernelGGL((KERNEL<BNS_T, 4>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
+      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 2 TYPES>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__); \
+    else if (R == 4) hipLaunchKernelGGL((KERNEL<BNS_T, 4 TYPES>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__); \
     else if (g_tune[TUNE_BNS_WIDE] == 2)                                                         \
-      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 4>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__);      \
-    else hipLaunchKernelGGL((KERNEL<BNS_T, 8>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);         \
+      hipLaunchKernelGGL((KERNEL<2 * BNS_T, 4 TYPES>), dim3(C), dim3(2 * BNS_T), 0, s, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<BNS_T, 8 TYPES>), dim3(C), dim3(BNS_T), 0, s, __VA_ARGS__);   \
   } while (0)
 // (e2ep_tune key 25 = 2: channels that need 8 float4 per thread at 256 threads run 512-thread
 // blocks of 4 per thread instead: half the registers per thread, twice the waves per channel;
@@ -816,10 +823,13 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
   return launch_status("e2ep_bn_fwd");
 }
 
-int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *running_mean,
-                  float *running_var, int N, int C, int H, int W, int train, float momentum,
-                  float eps, float *mean, float *invstd, float *scale, float *shift,
-                  void *workspace, size_t workspace_bytes, void *stream) {
+}  // extern "C"
+
+template <typename TX>
+static int bn_stats_impl(const TX *x, const float *gamma, const float *beta, float *running_mean,
+                         float *running_var, int N, int C, int H, int W, int train, float momentum,
+                         float eps, float *mean, float *invstd, float *scale, float *shift,
+                         void *workspace, size_t workspace_bytes, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
                E2EP_EINVAL, "e2ep_bn_stats: bad shape");
   E2EP_REQUIRE(!train || (workspace && workspace_bytes >= e2ep_bn_workspace(N, C, H, W)),
@@ -839,8 +849,10 @@ int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *
   int th = 0;
   const int R = (train && v4 && small_ok && totv <= g_bns_fwd_max) ? bns_r(totv, th) : 0;
   if (R) {
-    BNS_LAUNCH(k_bn_fwd_small, R, th, x, per_c, eps, momentum, running_mean, running_var, mean, invstd,
-               gamma, beta, nullptr, nullptr, 1.f, N, C, HWv, 0, nullptr, scale, shift);
+#define E2EP_BN_TYPES , TX
+    BNS_LAUNCH_T(k_bn_fwd_small, E2EP_BN_TYPES, R, th, x, per_c, eps, momentum, running_mean, running_var,
+                 mean, invstd, gamma, beta, nullptr, nullptr, 1.f, N, C, HWv, 0, nullptr, scale, shift);
+#undef E2EP_BN_TYPES
     return launch_status("e2ep_bn_stats");
   }
   double *part = nullptr;
@@ -851,13 +863,30 @@ int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *
     sp = cdiv(totv, per);
     part = static_cast<double *>(workspace);
     if (v4)
-      hipLaunchKernelGGL(k_bn_stats<4>, dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
+      hipLaunchKernelGGL((k_bn_stats<4, TX>), dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
     else
-      hipLaunchKernelGGL(k_bn_stats<1>, dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
+      hipLaunchKernelGGL((k_bn_stats<1, TX>), dim3(C, sp), dim3(256), 0, s, x, N, C, HWv, sp, per, part);
   }
   hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(256), 0, s, part, sp, per_c, eps, momentum,
                      running_mean, running_var, mean, invstd, gamma, beta, scale, shift);
   return launch_status("e2ep_bn_stats");
+}
+
+extern "C" {
+
+int e2ep_bn_stats(const void *x, const float *gamma, const float *beta, float *running_mean,
+                  float *running_var, int N, int C, int H, int W, int train, float momentum,
+                  float eps, float *mean, float *invstd, float *scale, float *shift,
+                  void *workspace, size_t workspace_bytes, void *stream, int io) {
+  E2EP_REQUIRE(io == 0 || (io == E2EP_IO_X_BF16 && (H * W) % 4 == 0), E2EP_EINVAL,
+               "e2ep_bn_stats: storage mask %d not supported (0 or X bf16, H*W %% 4 == 0)", io);
+  if (io)
+    return bn_stats_impl(static_cast<const bf16_t *>(x), gamma, beta, running_mean, running_var, N, C,
+                         H, W, train, momentum, eps, mean, invstd, scale, shift, workspace,
+                         workspace_bytes, stream);
+  return bn_stats_impl(static_cast<const float *>(x), gamma, beta, running_mean, running_var, N, C, H,
+                       W, train, momentum, eps, mean, invstd, scale, shift, workspace, workspace_bytes,
+                       stream);
 }
 
 int e2ep_bn_fwd_split(int N, int C, int H, int W) {
@@ -917,18 +946,28 @@ int e2ep_bn_apply(const float *x, const float *scale, const float *shift, const 
   return launch_status("e2ep_bn_apply");
 }
 
-int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
-                const float *gamma, const float *beta, const float *res, const float *dc_rand,
-                float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
-                int H, int W, int train, int act, float *dx, float *dgamma, float *dbeta,
-                float *dres, void *workspace, size_t workspace_bytes, void *stream) {
-  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
-               E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
-  E2EP_REQUIRE(!gate_logit == !gate_dpooled, E2EP_EINVAL,
-               "e2ep_bn_bwd: gate_logit / gate_dpooled both or neither");
-  const BnGate gt{gate_logit, gate_dpooled, 1.f / (float)(H * W)};
-  E2EP_REQUIRE(!dc_rand || dc_keep > 0.f, E2EP_EINVAL, "e2ep_bn_bwd: drop-connect keep must be > 0");
-  hipStream_t s = as_stream(stream);
+}  // extern "C"
+
+// storage types of (x, dy, dx) for an io mask (e2ep.h E2EP_IO_*): fp32, or the bf16
+// combinations the step stores — the depthwise output's BN (_bn1: x and dx bf16, dy bf16 too
+// when the squeeze-excitation output is stored bf16) and the expand output's BN (_bn0: the
+// depthwise data gradient dy bf16)
+enum BnIo {
+  BNIO_F32 = 0,
+  BNIO_XDX = E2EP_IO_X_BF16 | E2EP_IO_DX_BF16,
+  BNIO_ALL = E2EP_IO_X_BF16 | E2EP_IO_DY_BF16 | E2EP_IO_DX_BF16,
+  BNIO_DY = E2EP_IO_DY_BF16
+};
+static bool bn_io_ok(int io) {
+  return io == BNIO_F32 || io == BNIO_XDX || io == BNIO_ALL || io == BNIO_DY;
+}
+
+template <typename TX, typename TD, typename TO>
+static int bn_bwd_impl(const TX *x, const TD *dy, const float *mean, const float *invstd,
+                       const float *gamma, const float *beta, const float *res,
+                       const float *dc_rand, float dc_keep, const BnGate &gt, int N, int C, int H,
+                       int W, int train, int act, TO *dx, float *dgamma, float *dbeta, float *dres,
+                       void *workspace, size_t workspace_bytes, hipStream_t s) {
   const int HW = H * W;
   const long long per_c = (long long)N * HW;
   const bool v4 = (HW & 3) == 0;
@@ -938,8 +977,10 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
   int th = 0;
   const int R = (v4 && small_ok && totv <= g_bns_bwd_max) ? bns_r(totv, th) : 0;
   if (R) {
-    BNS_LAUNCH(k_bn_bwd_small, R, th, x, dy, mean, invstd, gamma, beta, res, dc_rand, dc_keep, gt, per_c,
-               N, C, HWv, act, train, dx, dres, dgamma, dbeta);
+#define E2EP_BN_TYPES , TX, TD, TO
+    BNS_LAUNCH_T(k_bn_bwd_small, E2EP_BN_TYPES, R, th, x, dy, mean, invstd, gamma, beta, res, dc_rand,
+                 dc_keep, gt, per_c, N, C, HWv, act, train, dx, dres, dgamma, dbeta);
+#undef E2EP_BN_TYPES
     return launch_status("e2ep_bn_bwd");
   }
   E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_bn_workspace(N, C, H, W), E2EP_EINVAL,
@@ -950,25 +991,59 @@ int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float 
   sp = cdiv(totv, per);
   double *part = static_cast<double *>(workspace);
   if (v4)
-    hipLaunchKernelGGL(k_bn_bwd_reduce<4>, dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd, gamma,
-                       beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
+    hipLaunchKernelGGL((k_bn_bwd_reduce<4, TX, TD>), dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd,
+                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
   else
-    hipLaunchKernelGGL(k_bn_bwd_reduce<1>, dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd, gamma,
-                       beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
+    hipLaunchKernelGGL((k_bn_bwd_reduce<1, TX, TD>), dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd,
+                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
   if (dx || dres) {
     const dim3 grid(C, cdiv(totv, APPLY_PER));
     if (v4)
-      hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                         res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
-                         dx, dres, dgamma, dbeta, nullptr);
+      hipLaunchKernelGGL((k_bn_bwd_apply<4, TX, TD, TO>), grid, dim3(256), 0, s, x, dy, mean, invstd,
+                         gamma, beta, res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER,
+                         act, train, dx, dres, dgamma, dbeta, nullptr);
     else
-      hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                         res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER, act, train,
-                         dx, dres, dgamma, dbeta, nullptr);
+      hipLaunchKernelGGL((k_bn_bwd_apply<1, TX, TD, TO>), grid, dim3(256), 0, s, x, dy, mean, invstd,
+                         gamma, beta, res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER,
+                         act, train, dx, dres, dgamma, dbeta, nullptr);
   } else if (dgamma || dbeta) {
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(256), 0, s, part, sp, dgamma, dbeta);
   }
   return launch_status("e2ep_bn_bwd");
+}
+
+extern "C" {
+
+int e2ep_bn_bwd(const void *x, const void *dy, const float *mean, const float *invstd,
+                const float *gamma, const float *beta, const float *res, const float *dc_rand,
+                float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
+                int H, int W, int train, int act, void *dx, float *dgamma, float *dbeta,
+                float *dres, void *workspace, size_t workspace_bytes, void *stream, int io) {
+  E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
+               E2EP_EINVAL, "e2ep_bn_bwd: bad shape");
+  E2EP_REQUIRE(!gate_logit == !gate_dpooled, E2EP_EINVAL,
+               "e2ep_bn_bwd: gate_logit / gate_dpooled both or neither");
+  E2EP_REQUIRE(!dc_rand || dc_keep > 0.f, E2EP_EINVAL, "e2ep_bn_bwd: drop-connect keep must be > 0");
+  E2EP_REQUIRE(bn_io_ok(io) && (io == 0 || (H * W) % 4 == 0), E2EP_EINVAL,
+               "e2ep_bn_bwd: storage mask %d not supported (0, X|DX, X|DY|DX or DY bf16, "
+               "H*W %% 4 == 0)", io);
+  const BnGate gt{gate_logit, gate_dpooled, 1.f / (float)(H * W)};
+  hipStream_t s = as_stream(stream);
+  if (io == BNIO_XDX)
+    return bn_bwd_impl(static_cast<const bf16_t *>(x), static_cast<const float *>(dy), mean, invstd,
+                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, H, W, train, act,
+                       static_cast<bf16_t *>(dx), dgamma, dbeta, dres, workspace, workspace_bytes, s);
+  if (io == BNIO_ALL)
+    return bn_bwd_impl(static_cast<const bf16_t *>(x), static_cast<const bf16_t *>(dy), mean, invstd,
+                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, H, W, train, act,
+                       static_cast<bf16_t *>(dx), dgamma, dbeta, dres, workspace, workspace_bytes, s);
+  if (io == BNIO_DY)
+    return bn_bwd_impl(static_cast<const float *>(x), static_cast<const bf16_t *>(dy), mean, invstd,
+                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, H, W, train, act,
+                       static_cast<float *>(dx), dgamma, dbeta, dres, workspace, workspace_bytes, s);
+  return bn_bwd_impl(static_cast<const float *>(x), static_cast<const float *>(dy), mean, invstd, gamma,
+                     beta, res, dc_rand, dc_keep, gt, N, C, H, W, train, act, static_cast<float *>(dx),
+                     dgamma, dbeta, dres, workspace, workspace_bytes, s);
 }
 
 int e2ep_bn_bwd_split(int N, int C, int H, int W) {
@@ -980,15 +1055,18 @@ int e2ep_bn_bwd_split(int N, int C, int H, int W) {
   return (v4 && bn_small_enabled() && totv <= g_bns_bwd_max && bns_r(totv, th)) ? 0 : 1;
 }
 
-int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const float *invstd,
+int e2ep_bn_bwd_planes(const void *x, const void *dy, const float *mean, const float *invstd,
                        const float *gamma, const float *beta, const float *gate_logit,
                        const float *gate_dpooled, const double *plane_sums, int N, int C, int H,
-                       int W, int act, float *dx, float *dgamma, float *dbeta, void *stream) {
+                       int W, int act, void *dx, float *dgamma, float *dbeta, void *stream, int io) {
   E2EP_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && C <= 65535 && (long long)N * H * W < (1LL << 31),
                E2EP_EINVAL, "e2ep_bn_bwd_planes: bad shape");
   E2EP_REQUIRE(x && dy && mean && invstd && gate_logit && gate_dpooled && plane_sums && dx,
                E2EP_EINVAL, "e2ep_bn_bwd_planes: null argument");
   E2EP_REQUIRE(act >= 0 && act <= 2, E2EP_EINVAL, "e2ep_bn_bwd_planes: act must be 0/1/2");
+  E2EP_REQUIRE((io == BNIO_F32 || io == BNIO_XDX || io == BNIO_ALL) && (io == 0 || (H * W) % 4 == 0),
+               E2EP_EINVAL, "e2ep_bn_bwd_planes: storage mask %d not supported (0, X|DX or X|DY|DX "
+               "bf16, H*W %% 4 == 0)", io);
   const BnGate gt{gate_logit, gate_dpooled, 1.f / (float)(H * W)};
   const int HW = H * W;
   const long long per_c = (long long)N * HW;
@@ -997,14 +1075,25 @@ int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const
   const int totv = N * HWv;
   const dim3 grid(C, cdiv(totv, APPLY_PER));
   hipStream_t s = as_stream(stream);
-  if (v4)
-    hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                       nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
-                       dx, nullptr, dgamma, dbeta, plane_sums);
+  const float *dyf = static_cast<const float *>(dy);
+  if (io == BNIO_ALL)
+    hipLaunchKernelGGL((k_bn_bwd_apply<4, bf16_t, bf16_t, bf16_t>), grid, dim3(256), 0, s,
+                       static_cast<const bf16_t *>(x), static_cast<const bf16_t *>(dy), mean, invstd,
+                       gamma, beta, nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER,
+                       act, 1, static_cast<bf16_t *>(dx), nullptr, dgamma, dbeta, plane_sums);
+  else if (io == BNIO_XDX)
+    hipLaunchKernelGGL((k_bn_bwd_apply<4, bf16_t, float, bf16_t>), grid, dim3(256), 0, s,
+                       static_cast<const bf16_t *>(x), dyf, mean, invstd, gamma, beta, nullptr, nullptr,
+                       1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
+                       static_cast<bf16_t *>(dx), nullptr, dgamma, dbeta, plane_sums);
+  else if (v4)
+    hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, static_cast<const float *>(x), dyf, mean,
+                       invstd, gamma, beta, nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv,
+                       APPLY_PER, act, 1, static_cast<float *>(dx), nullptr, dgamma, dbeta, plane_sums);
   else
-    hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, x, dy, mean, invstd, gamma, beta,
-                       nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
-                       dx, nullptr, dgamma, dbeta, plane_sums);
+    hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, static_cast<const float *>(x), dyf, mean,
+                       invstd, gamma, beta, nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv,
+                       APPLY_PER, act, 1, static_cast<float *>(dx), nullptr, dgamma, dbeta, plane_sums);
   return launch_status("e2ep_bn_bwd_planes");
 }
 

@@ -61,6 +61,53 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int byte_off, f
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 0);
 }
 
+// bf16 activation storage (C3: the depthwise outputs and their gradients, e2ep.h E2EP_IO_*):
+// typed 4-wide loads / stores whose arithmetic stays fp32 — a bf16 tensor element is widened
+// on load and rounded to nearest-even (v_cvt_pk_bf16_f32) on store.
+typedef __bf16 bf16_t;
+typedef __bf16 e2ep_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 ld4(const bf16_t *p) {
+  const e2ep_bf16x4 h = *reinterpret_cast<const e2ep_bf16x4 *>(p);
+  return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+}
+__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+__device__ __forceinline__ void st4(bf16_t *p, float4 v) {
+  const e2ep_bf16x4 h = {(bf16_t)v.x, (bf16_t)v.y, (bf16_t)v.z, (bf16_t)v.w};
+  *reinterpret_cast<e2ep_bf16x4 *>(p) = h;
+}
+__device__ __forceinline__ float ld1(const float *p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t *p) { return (float)*p; }
+__device__ __forceinline__ void st1(float *p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16_t *p, float v) { *p = (bf16_t)v; }
+// the value a store of v into a T tensor keeps (statistics of stored outputs)
+template <typename T>
+__device__ __forceinline__ float stored(float v) { return (float)(T)v; }
+// 4 elements of a T tensor through a buffer descriptor (byte offset of the first element)
+__device__ __forceinline__ float4 bload4t(__amdgpu_buffer_rsrc_t r, int byte_off, const float *) {
+  return bload4(r, byte_off);
+}
+__device__ __forceinline__ float4 bload4t(__amdgpu_buffer_rsrc_t r, int byte_off, const bf16_t *) {
+  const e2ep_f2 u = e2ep_raw_buffer_load_v2f32(r, byte_off, 0, 0);
+  const e2ep_bf16x4 h = __builtin_bit_cast(e2ep_bf16x4, u);
+  return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+}
+
+// one element of a T tensor through a buffer descriptor (load widened, store rounded)
+__device__ __forceinline__ float bload_t(__amdgpu_buffer_rsrc_t r, int byte_off, const float *) {
+  return bload(r, byte_off);
+}
+__device__ __forceinline__ float bload_t(__amdgpu_buffer_rsrc_t r, int byte_off, const bf16_t *) {
+  const unsigned short h = __builtin_amdgcn_raw_buffer_load_b16(r, byte_off, 0, 0);
+  return __builtin_bit_cast(float, (unsigned)h << 16);
+}
+__device__ __forceinline__ void bstore_t(__amdgpu_buffer_rsrc_t r, int byte_off, float v, float *) {
+  bstore(r, byte_off, v);
+}
+__device__ __forceinline__ void bstore_t(__amdgpu_buffer_rsrc_t r, int byte_off, float v, bf16_t *) {
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (bf16_t)v), r, byte_off, 0, 0);
+}
+
 // 64-lane wave helpers
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

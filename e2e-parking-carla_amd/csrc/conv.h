@@ -70,9 +70,11 @@ bool lp_ok(int mode, const ConvGeom &g, int M, int op);
 size_t lp_workspace(int mode, const ConvGeom &g, int M, int op);
 // stats (forward only): BatchNorm partial sums of dst from the epilogue (bnstats.h), over
 // lp_stats_tiles(g, op) column tiles (0 = the plan cannot produce them).
-int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
-              float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
-              hipStream_t s, double *stats = nullptr);
+// io (e2ep.h E2EP_IO_*, op 1 only): mode 0 with E2EP_IO_X_BF16 reads a bf16 src, mode 1 with
+// E2EP_IO_DX_BF16 writes a bf16 dst (dst_bytes: its size in bytes); E2EP_EINVAL otherwise.
+int lp_launch(int mode, int act, int op, const float *w, const void *src, const float *bias,
+              void *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
+              hipStream_t s, double *stats = nullptr, int io = 0);
 int lp_stats_tiles(const ConvGeom &g, int op);
 
 // Weight gradient with 32-pixel K-steps and up to 128 x 128 tiles, conv_lp.hip: bf16 operands
@@ -81,17 +83,19 @@ int lp_stats_tiles(const ConvGeom &g, int op);
 // lp_wgrad_launch returns the slabs written.
 bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl);
 int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op);
-int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
-                    int splits, float *part, hipStream_t s, int op);
+// xb: x is bf16 (op 1 only)
+int lp_wgrad_launch(const float *gout, const void *x, const ConvGeom &g, const TapList &tl,
+                    int splits, float *part, hipStream_t s, int op, bool xb = false);
 
 // A conv layer's data gradient on k_conv_lp (route ROUTE_LP / ROUTE_LP32 of conv.hip) and
 // weight gradient (op 1: k_wgrad_lp; op 0: the k_conv_wgrad2-equivalent 64 x 64 tile) in one
 // k_lp_bwd_pair launch (e2ep_conv_bwd).  lp_bwd_pair_launch returns the weight-gradient slabs
 // written to part2 (for the split reduction), -1 if the plan has no instantiated pair.
 bool lp_bwd_pair_ok(const ConvGeom &g, int M, int op, const TapList &tl);
-int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, float *dx,
+// xb: x and dx are bf16 (op 1 only; dx_bytes its size in bytes)
+int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void *dx,
                        long long dx_bytes, const ConvGeom &g, int M, int op, void *ws_dgrad,
-                       const float *x, const TapList &tl, int wsplits, float *part2,
-                       hipStream_t s);
+                       const void *x, const TapList &tl, int wsplits, float *part2,
+                       hipStream_t s, bool xb = false);
 
 }  // namespace e2ep

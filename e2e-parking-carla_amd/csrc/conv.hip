@@ -57,10 +57,13 @@ constexpr int conv_gemm_lds_floats() { return 2 * BK * (BMT + PADA) + 2 * BK * (
 // The block body of k_conv_gemm for block (bx, by, bz) of a grid gx blocks wide; `lds` holds
 // conv_gemm_lds_floats<BNT, BMT>() floats of the caller's __shared__ memory (so a kernel can run
 // two problems in one grid: k_conv_bwd_pair).
-template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP, bool ST>
+// TS / TD: element types of src / dst (bf16_t: C3's bf16-stored activations, e2ep.h
+// E2EP_IO_*; the weights and the MODE 1 residual gradient stay fp32)
+template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP, bool ST, typename TS = float,
+          typename TD = float>
 __device__ __forceinline__ void conv_gemm_block(
-    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
-    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    const float *__restrict__ w, const TS *__restrict__ src, const float *__restrict__ bias,
+    TD *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats, int bx,
     int by, int bz, int gx, float *lds) {
   // block tile BMT x BNT: BMT = 64 -> 2 x 2 waves of 32 x BNT/2; BMT = 32 (small-M layers:
@@ -137,8 +140,9 @@ __device__ __forceinline__ void conv_gemm_block(
 
   const int Hs = MODE == 0 ? g.H : g.P, Ws = MODE == 0 ? g.W : g.Q;  // src spatial
   const int HWs = Hs * Ws;
+  constexpr int ES = sizeof(TS);  // bytes per src element
   const __amdgpu_buffer_rsrc_t rw = rsrc(w, 4LL * g.Cout * g.Cin * RS);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(src, 4LL * g.N * Kc * HWs);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(src, (long long)ES * g.N * Kc * HWs);
 
   // B-load column of this thread (fixed); its rows are wave-uniform
   const int bn = tid % BNT;
@@ -181,7 +185,7 @@ __device__ __forceinline__ void conv_gemm_block(
   // scalar unit; row terms are uniform strides, so each element costs one add.  Sums stay
   // below 2^32: the base is < 2^31 and so is every row term.
   const int nrw = (int)min(4LL * g.Cout * g.Cin * RS, 0x7fffffffLL);
-  const int nrx = (int)min(4LL * g.N * Kc * HWs, 0x7fffffffLL);
+  const int nrx = (int)min((long long)ES * g.N * Kc * HWs, 0x7fffffffLL);
 
   // global -> register loads run two K-steps ahead of the MFMAs (two register sets), LDS
   // is double buffered: one barrier per K-step, ~2 steps of MFMA work to cover a load.  (A
@@ -221,12 +225,12 @@ __device__ __forceinline__ void conv_gemm_block(
     const int iy = ybase + dy, ix = xbase + dx;
     const bool pix_ok = live && col_ok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
     // rows c0 + bk0 + BROWS j: wave-uniform (bk0 = tid / BNT, BNT >= 64)
-    const int bbase = pix_ok ? (simg + iy * Ws + ix) * 4 : nrx;
+    const int bbase = pix_ok ? (simg + iy * Ws + ix) * ES : nrx;
 #pragma unroll
     for (int j = 0; j < BPER; ++j) {
       const int c = c0 + bk0 + BROWS * j;
-      const int rterm = c < Kc ? c * HWs * 4 : nrx;
-      rb[j] = bload(rx, bbase + rterm);
+      const int rterm = c < Kc ? c * HWs * ES : nrx;
+      rb[j] = bload_t(rx, bbase + rterm, src);
     }
   };
   auto store_tiles = [&](int buf, const float(&ra)[NA], const float(&rb)[BPER]) {
@@ -339,9 +343,10 @@ __device__ __forceinline__ void conv_gemm_block(
     }
   }
   const __amdgpu_buffer_rsrc_t rd = rsrc(dst, dst_bytes);
+  constexpr int ED = sizeof(TD);  // bytes per dst element (the fp32 residual: 4)
   // MODE 1: `bias` is an optional residual gradient in dst's layout, added to dx here (the
   // skip connection's gradient, so autograd needs no separate accumulation kernel)
-  const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes : 0);
+  const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes / ED * 4 : 0);
   const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
   const int HWd = Hd * Wd;
   // MODE 0 with `stats`: BatchNorm partial sums of the stored values (bnstats.h)
@@ -369,19 +374,20 @@ __device__ __forceinline__ void conv_gemm_block(
     for (int r = 0; r < 16; ++r) {
       const int m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
       float v = acc[t][r];
-      const int off = (nok && m < M) ? (dbase + m * mstride) * 4 : OOR;
+      const bool in = nok && m < M;
+      const int e = dbase + m * mstride;  // element offset (res: 4 B, dst: ED B)
       if (MODE == 0) {
         if (bias) v += bias[min(m, M - 1)];
         if (ACT == 1) v = fmaxf(v, 0.f);
       } else if (bias) {
-        v += bload(rres, off);
+        v += bload(rres, in ? e * 4 : OOR);
       }
       if (want_stats) {
-        const float d = (nok && m < M) ? v : 0.f;
+        const float d = in ? stored<TD>(v) : 0.f;
         fs[r] += d;
         fq[r] = __builtin_fmaf(d, d, fq[r]);
       }
-      bstore(rd, off, v);
+      bstore_t(rd, in ? e * ED : OOR, v, dst);
     }
   }
   if (want_stats) {
@@ -398,15 +404,17 @@ __device__ __forceinline__ void conv_gemm_block(
 
 // ST (forward only): the epilogue also writes BatchNorm partial sums into `stats` (bnstats.h);
 // a separate instantiation, so the plain forward keeps its register allocation.
-template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0, bool ST = false>
+template <int MODE, int ACT, int BNT, int BMT, bool AV, int OP = 0, bool ST = false,
+          typename TS = float, typename TD = float>
 __global__ void __launch_bounds__(256, 2) k_conv_gemm(
-    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
-    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    const float *__restrict__ w, const TS *__restrict__ src, const float *__restrict__ bias,
+    TD *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
   __shared__ __attribute__((aligned(16))) float lds[conv_gemm_lds_floats<BNT, BMT>()];
-  conv_gemm_block<MODE, ACT, BNT, BMT, AV, OP, ST>(w, src, bias, dst, dst_bytes, g, M, splits,
-                                                   kper, part, cnt, stats, blockIdx.x, blockIdx.y,
-                                                   blockIdx.z, gridDim.x, lds);
+  conv_gemm_block<MODE, ACT, BNT, BMT, AV, OP, ST, TS, TD>(w, src, bias, dst, dst_bytes, g, M,
+                                                           splits, kper, part, cnt, stats,
+                                                           blockIdx.x, blockIdx.y, blockIdx.z,
+                                                           gridDim.x, lds);
 }
 
 // split-K reduction (fixed order) + bias / relu epilogue:
@@ -1793,9 +1801,11 @@ static int fwd_stats_tiles(const ConvGeom &g0) {
   return (int)cdiv(p.ncols, p.bnt);
 }
 
-static int launch_gemm(int mode, int act, const float *w, const float *src, const float *bias,
-                       float *dst, long long dst_bytes, const ConvGeom &g0, int M, void *workspace,
-                       hipStream_t s, double *stats = nullptr) {
+// io (e2ep.h E2EP_IO_*): bf16 storage of the forward input (mode 0, E2EP_IO_X_BF16) or of the
+// data gradient (mode 1, E2EP_IO_DX_BF16), on the bf16-operand kernels (C3) only
+static int launch_gemm(int mode, int act, const float *w, const void *srcv, const float *bias,
+                       void *dstv, long long dst_bytes, const ConvGeom &g0, int M, void *workspace,
+                       hipStream_t s, double *stats = nullptr, int io = 0) {
   ConvGeom g = g0;
   g.korder = korder_of();
   g.xcd = g_tune[TUNE_XCD] == 2;
@@ -1805,8 +1815,17 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     return E2EP_EINVAL;
   }
   if (route == ROUTE_LP)
-    return lp_launch(mode, act, g_conv_precision, w, src, bias, dst, dst_bytes, g, M, workspace, s,
-                     stats);
+    return lp_launch(mode, act, g_conv_precision, w, srcv, bias, dstv, dst_bytes, g, M, workspace, s,
+                     stats, io);
+  const bool sb = io && mode == 0 && io == E2EP_IO_X_BF16;
+  const bool db = io && mode == 1 && io == E2EP_IO_DX_BF16;
+  if (io && (route != ROUTE_GEMM || g_conv_precision != 1 || !(sb || db))) {
+    set_error("conv: storage mask %d not supported on this route (bf16 operands: the forward input "
+              "or the data-gradient output on k_conv_lp / k_conv_gemm)", io);
+    return E2EP_EINVAL;
+  }
+  const float *src = static_cast<const float *>(srcv);
+  float *dst = static_cast<float *>(dstv);
   if (route == ROUTE_1X1)
     return conv1x1_gemm(mode, act, w, src, bias, dst, dst_bytes, g, M, workspace, s);
   if (route == ROUTE_G2) {
@@ -1852,10 +1871,22 @@ static int launch_gemm(int mode, int act, const float *w, const float *src, cons
     set_error("conv: BatchNorm statistics need the in-launch split-K fold (e2ep_tune key 28 = 2)");
     return E2EP_EINVAL;
   }
+  if (db && p.splits > 1 && !cnt) {
+    set_error("conv: a bf16 data gradient needs the in-launch split-K fold (e2ep_tune key 28 = 2)");
+    return E2EP_EINVAL;
+  }
   const bool av = mode == 0 && g.wlayout == 1 && (g.Cin & 3) == 0;
 #define GEMM_LAUNCH1(MD, AC, BT, BMT, V)                                                          \
   do {                                                                                             \
-    if (g_conv_precision == 1)                                                                     \
+    if (g_conv_precision == 1 && MD == 0 && sb)                                                    \
+      hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 1, false, bf16_t, float>), grid, dim3(256), 0, s, \
+                         w, static_cast<const bf16_t *>(srcv), bias, dst, dst_bytes, g, M, p.splits, \
+                         p.kper, part, cnt, nullptr);                                              \
+    else if (g_conv_precision == 1 && MD == 1 && db)                                               \
+      hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 1, false, float, bf16_t>), grid, dim3(256), 0, s, \
+                         w, src, bias, static_cast<bf16_t *>(dstv), dst_bytes, g, M, p.splits,     \
+                         p.kper, part, cnt, nullptr);                                              \
+    else if (g_conv_precision == 1)                                                                \
       hipLaunchKernelGGL((k_conv_gemm<MD, AC, BT, BMT, V, 1>), grid, dim3(256), 0, s, w, src, bias, \
                          dst, dst_bytes, g, M, p.splits, p.kper, part, cnt, nullptr);             \
     else if (g_conv_precision == 2)                                                                \
@@ -1959,15 +1990,16 @@ int e2ep_conv_fwd_stats_tiles(const int *dims, int w_layout) {
   return fwd_stats_tiles(g);
 }
 
-int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
-                  int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream) {
+int e2ep_conv_fwd(const void *x, const float *w, const float *bias, const int *dims, int act,
+                  int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream,
+                  int io) {
   return e2ep_conv_fwd_stats(x, w, bias, dims, act, w_layout, y, workspace, workspace_bytes,
-                             nullptr, 0, stream);
+                             nullptr, 0, stream, io);
 }
 
-int e2ep_conv_fwd_stats(const float *x, const float *w, const float *bias, const int *dims, int act,
+int e2ep_conv_fwd_stats(const void *x, const float *w, const float *bias, const int *dims, int act,
                         int w_layout, float *y, void *workspace, size_t workspace_bytes,
-                        double *stats, size_t stats_bytes, void *stream) {
+                        double *stats, size_t stats_bytes, void *stream, int io) {
   ConvGeom g = make_geom(dims);
   {
     const size_t need = e2ep_conv_fwd_workspace(dims);
@@ -1988,20 +2020,23 @@ int e2ep_conv_fwd_stats(const float *x, const float *w, const float *bias, const
                  "e2ep_conv_fwd_stats: stats %zu bytes < %zu (Cout x tiles x 2 doubles)",
                  stats_bytes, (size_t)g.Cout * tiles * 2 * sizeof(double));
   }
+  E2EP_REQUIRE(io == 0 || io == E2EP_IO_X_BF16, E2EP_EINVAL,
+               "e2ep_conv_fwd: storage mask %d not supported (0 or X bf16)", io);
   if (direct_ok(g)) {
+    E2EP_REQUIRE(io == 0, E2EP_EINVAL, "e2ep_conv_fwd: the direct kernel reads fp32 x only");
     hipLaunchKernelGGL(k_conv_direct, dim3(cdiv((long long)g.N * g.P * g.Q, 256)), dim3(256), 0,
-                       as_stream(stream), x, w, bias, g, act, y);
+                       as_stream(stream), static_cast<const float *>(x), w, bias, g, act, y);
     return launch_status("e2ep_conv_fwd");
   }
   const int rc = launch_gemm(0, act, w, x, bias, y, 4LL * g.N * g.Cout * g.P * g.Q, g, g.Cout,
-                             workspace, as_stream(stream), stats);
+                             workspace, as_stream(stream), stats, io);
   if (rc) return rc;
   return launch_status("e2ep_conv_fwd");
 }
 
 int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int m_channels,
-                        int w_layout, const float *res, float *dx, void *workspace,
-                        size_t workspace_bytes, void *stream) {
+                        int w_layout, const float *res, void *dx, void *workspace,
+                        size_t workspace_bytes, void *stream, int io) {
   ConvGeom g = make_geom(dims);
   if (m_channels > 0 && m_channels <= g.Cin) {
     const size_t need = e2ep_conv_dgrad_workspace(dims, m_channels);
@@ -2014,8 +2049,11 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
   E2EP_REQUIRE(geom_ok(g), E2EP_EINVAL, "e2ep_conv_dgrad: bad geometry");
   E2EP_REQUIRE(m_channels > 0 && m_channels <= g.Cin, E2EP_EINVAL,
                "e2ep_conv_dgrad: m_channels must be in [1, Cin]");
-  const int rc = launch_gemm(1, 0, w, gout, res, dx, 4LL * g.N * m_channels * g.H * g.W, g,
-                             m_channels, workspace, as_stream(stream));
+  E2EP_REQUIRE(io == 0 || io == E2EP_IO_DX_BF16, E2EP_EINVAL,
+               "e2ep_conv_dgrad: storage mask %d not supported (0 or DX bf16)", io);
+  const long long esz = io ? 2 : 4;
+  const int rc = launch_gemm(1, 0, w, gout, res, dx, esz * g.N * m_channels * g.H * g.W, g,
+                             m_channels, workspace, as_stream(stream), nullptr, io);
   if (rc) return rc;
   return launch_status("e2ep_conv_dgrad");
 }
@@ -2023,7 +2061,7 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
 int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_channels,
                     int w_layout, float *dx, void *workspace, size_t workspace_bytes, void *stream) {
   return e2ep_conv_dgrad_acc(gout, w, dims, m_channels, w_layout, nullptr, dx, workspace,
-                             workspace_bytes, stream);
+                             workspace_bytes, stream, 0);
 }
 
 int e2ep_conv_wgrad_splits(const int *dims) {
@@ -2049,25 +2087,33 @@ size_t e2ep_conv_wgrad_workspace(const int *dims, int splits) {
   return (size_t)splits * g.Cout * g.Cin * g.R * g.S * sizeof(float);
 }
 
-int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,
+int e2ep_conv_wgrad(const float *gout, const void *xv, const int *dims, int splits,
                     void *workspace, size_t workspace_bytes, float *dw, int accumulate,
-                    void *stream) {
+                    void *stream, int io) {
+  const float *x = static_cast<const float *>(xv);
   ConvGeom g = make_geom(dims);
   E2EP_REQUIRE(geom_ok(g) && splits > 0, E2EP_EINVAL, "e2ep_conv_wgrad: bad geometry");
   // the kernels write at most `splits` slabs of Cout * Cin * R * S floats
   E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_conv_wgrad_workspace(dims, splits),
                E2EP_EINVAL, "e2ep_conv_wgrad: workspace %zu bytes < %zu for %d splits",
                workspace_bytes, e2ep_conv_wgrad_workspace(dims, splits), splits);
+  E2EP_REQUIRE(io == 0 || io == E2EP_IO_X_BF16, E2EP_EINVAL,
+               "e2ep_conv_wgrad: storage mask %d not supported (0 or X bf16)", io);
   if (lp_wgrad_selected()) {
     const TapList tl = live_taps(g);
     if (lp_wgrad_ok(g, tl)) {
+      E2EP_REQUIRE(io == 0 || g_conv_precision == 1, E2EP_EINVAL,
+                   "e2ep_conv_wgrad: a bf16 x needs the bf16-operand weight gradient");
       hipStream_t s = as_stream(stream);
       float *part = static_cast<float *>(workspace);
-      const int used = lp_wgrad_launch(gout, x, g, tl, splits, part, s, g_conv_precision == 1 ? 1 : 0);
+      const int used = lp_wgrad_launch(gout, xv, g, tl, splits, part, s, g_conv_precision == 1 ? 1 : 0,
+                                       io != 0);
       reduce_splits(part, used, g.Cout * g.Cin * g.R * g.S, dw, accumulate, g.R * g.S, tl.mask, s);
       return launch_status("e2ep_conv_wgrad");
     }
   }
+  E2EP_REQUIRE(io == 0, E2EP_EINVAL,
+               "e2ep_conv_wgrad: a bf16 x runs on the bf16-operand weight gradient (k_wgrad_lp) only");
   if (wgrad1x1_ok(g)) {
     const int groups = g.N * g.P * g.Q / 8;
     const int gps = cdiv(groups, splits);
@@ -2168,10 +2214,12 @@ int e2ep_conv_bwd_pair_ok(const int *dims, int m_channels) {
   return conv_bwd_pair_plan(g, m_channels, p, tl) != PAIR_NONE ? 1 : 0;
 }
 
-int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *dims,
-                  int m_channels, const float *res, float *dx, void *ws_dgrad,
+int e2ep_conv_bwd(const float *gout, const void *xv, const float *w, const int *dims,
+                  int m_channels, const float *res, void *dxv, void *ws_dgrad,
                   size_t ws_dgrad_bytes, int wsplits, void *ws_wgrad, size_t ws_wgrad_bytes,
-                  float *dw, void *stream) {
+                  float *dw, void *stream, int io) {
+  const float *x = static_cast<const float *>(xv);
+  float *dx = static_cast<float *>(dxv);
   ConvGeom g = make_geom(dims);
   GemmPlan p;
   TapList tl;
@@ -2186,14 +2234,19 @@ int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *
   E2EP_REQUIRE(ws_wgrad && ws_wgrad_bytes >= e2ep_conv_wgrad_workspace(dims, wsplits), E2EP_EINVAL,
                "e2ep_conv_bwd: weight-gradient workspace %zu bytes < %zu for %d splits",
                ws_wgrad_bytes, e2ep_conv_wgrad_workspace(dims, wsplits), wsplits);
+  // bf16 storage (io = X|DX): x and dx bf16 on the bf16-operand pair (k_lp_bwd_pair) only
+  const bool xb = io == (E2EP_IO_X_BF16 | E2EP_IO_DX_BF16);
+  E2EP_REQUIRE(io == 0 || (xb && kind == PAIR_LP && g_conv_precision == 1 && !res), E2EP_EINVAL,
+               "e2ep_conv_bwd: storage mask %d not supported (0, or X|DX bf16 on the bf16 k_lp_bwd_pair "
+               "without a residual gradient)", io);
   hipStream_t s = as_stream(stream);
   const int M = m_channels;
-  const long long dx_bytes = 4LL * g.N * M * g.H * g.W;
+  const long long dx_bytes = (xb ? 2LL : 4LL) * g.N * M * g.H * g.W;
   float *part2 = static_cast<float *>(ws_wgrad);
   int used;
   if (kind == PAIR_LP) {
-    used = lp_bwd_pair_launch(w, gout, res, dx, dx_bytes, g, M, g_conv_precision == 1 ? 1 : 0,
-                              ws_dgrad, x, tl, wsplits, part2, s);
+    used = lp_bwd_pair_launch(w, gout, res, dxv, dx_bytes, g, M, g_conv_precision == 1 ? 1 : 0,
+                              ws_dgrad, xv, tl, wsplits, part2, s, xb);
     E2EP_REQUIRE(used > 0, E2EP_EINVAL, "e2ep_conv_bwd: no paired k_conv_lp plan");
     reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
     return launch_status("e2ep_conv_bwd");

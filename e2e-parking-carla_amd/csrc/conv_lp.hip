@@ -72,10 +72,14 @@ __device__ __forceinline__ f32x16 mfma16(typename LpType<OP>::T8 a, typename LpT
 // The block body for block (bx, by, bz) of a grid gx blocks wide, its operand tiles in the
 // caller's LDS (As[2][BMT][LD], Bs[2][BNT][LD]): k_conv_lp, and the data-gradient half of
 // k_lp_bwd_pair.
-template <int MODE, int ACT, int WM, int WN, int OP, int LKS, bool ST = false>
+// TS / TD: element types of src and dst (bf16_t: C3's bf16-stored squeeze-excitation output
+// as the project conv's input, and its gradient as the project conv's data gradient; e2ep.h
+// E2EP_IO_*); the MODE 1 residual gradient (`bias`) stays fp32.
+template <int MODE, int ACT, int WM, int WN, int OP, int LKS, bool ST = false,
+          typename TS = float, typename TD = float>
 __device__ __forceinline__ void conv_lp_block(
-    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
-    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    const float *__restrict__ w, const TS *__restrict__ src, const float *__restrict__ bias,
+    TD *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats, int bx,
     int by, int bz, int gx, typename LpType<OP>::T (*As)[64 * WM][lld_of(OP, LKS)],
     typename LpType<OP>::T (*Bs)[64 * WN][lld_of(OP, LKS)]) {
@@ -154,9 +158,10 @@ __device__ __forceinline__ void conv_lp_block(
   const int HWs = Hs * Ws;
   const int RS = g.R * g.S;
   const __amdgpu_buffer_rsrc_t rw = rsrc(w, 4LL * g.Cout * g.Cin * RS);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(src, 4LL * g.N * Kc * HWs);
+  constexpr int ES = sizeof(TS);  // bytes per src element
+  const __amdgpu_buffer_rsrc_t rx = rsrc(src, (long long)ES * g.N * Kc * HWs);
   const int nrw = (int)min(4LL * g.Cout * g.Cin * RS, 0x7fffffffLL);
-  const int nrx = (int)min(4LL * g.N * Kc * HWs, 0x7fffffffLL);
+  const int nrx = (int)min((long long)ES * g.N * Kc * HWs, 0x7fffffffLL);
   const int tapstride = g.Cout * g.Cin;  // tap-major weights [RS][Cout][Cin]
 
   // B: this thread's column (fixed) and k group (rows kg*RPB .. +RPB-1 of each step)
@@ -209,9 +214,9 @@ __device__ __forceinline__ void conv_lp_block(
       }
       const int iy = ybase + dy, ix = xbase + dx;
       const bool pix_ok = live && col_ok && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
-      const int bbase = pix_ok ? (simg + (c0 + kg * RPB) * HWs + iy * Ws + ix) * 4 : nrx;
+      const int bbase = pix_ok ? (simg + (c0 + kg * RPB) * HWs + iy * Ws + ix) * ES : nrx;
 #pragma unroll
-      for (int r = 0; r < RPB; ++r) rb[r] = bload(rx, bbase + r * HWs * 4);
+      for (int r = 0; r < RPB; ++r) rb[r] = bload_t(rx, bbase + r * HWs * ES, src);
     } else {  // tail step: 32 flattened (remainder channel, tap) rows
       // a thread's rows are consecutive flattened indices: decode the first (one division),
       // then step the (channel, tap) pair
@@ -238,7 +243,7 @@ __device__ __forceinline__ void conv_lp_block(
           const int tt = in ? t : 0;
           const int iy = ybase + s_tdy[tt], ix = xbase + s_tdx[tt];
           const bool ok = live && col_ok && in && (unsigned)iy < (unsigned)Hs && (unsigned)ix < (unsigned)Ws;
-          rb[r] = bload(rx, ok ? (simg + (cfull * LKS + cq) * HWs + iy * Ws + ix) * 4 : OOR);
+          rb[r] = bload_t(rx, ok ? (simg + (cfull * LKS + cq) * HWs + iy * Ws + ix) * ES : OOR, src);
           const bool wrap = ++t == ntaps;
           t = wrap ? 0 : t;
           cq += wrap ? 1 : 0;
@@ -378,7 +383,8 @@ __device__ __forceinline__ void conv_lp_block(
     }
   }
   const __amdgpu_buffer_rsrc_t rd = rsrc(dst, dst_bytes);
-  const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes : 0);
+  constexpr int ED = sizeof(TD);  // bytes per dst element (the fp32 residual: 4)
+  const __amdgpu_buffer_rsrc_t rres = rsrc(bias, MODE == 1 && bias ? dst_bytes / ED * 4 : 0);
   const int Hd = MODE == 0 ? g.P : g.H, Wd = MODE == 0 ? g.Q : g.W;
   const int HWd = Hd * Wd;
   // MODE 0 with `stats`: BatchNorm partial sums of the stored values (bnstats.h)
@@ -410,19 +416,20 @@ __device__ __forceinline__ void conv_lp_block(
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + 32 * (WM * wm + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
         float v = acc[i][j][r];
-        const int off = (nok && m < M) ? (dbase + m * mstride) * 4 : OOR;
+        const bool in = nok && m < M;
+        const int e = dbase + m * mstride;  // element offset (res: 4 B, dst: ED B)
         if (MODE == 0) {
           if (bias) v += bias[min(m, M - 1)];
           if (ACT == 1) v = fmaxf(v, 0.f);
         } else if (bias) {
-          v += bload(rres, off);
+          v += bload(rres, in ? e * 4 : OOR);
         }
         if (want_stats) {
-          const float d = (nok && m < M) ? v : 0.f;
+          const float d = in ? stored<TD>(v) : 0.f;
           fs[i][r] += d;
           fq[i][r] = __builtin_fmaf(d, d, fq[i][r]);
         }
-        bstore(rd, off, v);
+        bstore_t(rd, in ? e * ED : OOR, v, dst);
       }
     }
   }
@@ -440,10 +447,11 @@ __device__ __forceinline__ void conv_lp_block(
   }
 }
 
-template <int MODE, int ACT, int WM, int WN, int OP, int LKS, bool ST = false>
+template <int MODE, int ACT, int WM, int WN, int OP, int LKS, bool ST = false,
+          typename TS = float, typename TD = float>
 __global__ void __launch_bounds__(256) k_conv_lp(
-    const float *__restrict__ w, const float *__restrict__ src, const float *__restrict__ bias,
-    float *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
+    const float *__restrict__ w, const TS *__restrict__ src, const float *__restrict__ bias,
+    TD *__restrict__ dst, long long dst_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part, unsigned int *__restrict__ cnt, double *__restrict__ stats) {
   typedef typename LpType<OP>::T T;
   constexpr int LD = lld_of(OP, LKS);
@@ -451,8 +459,9 @@ __global__ void __launch_bounds__(256) k_conv_lp(
   __shared__ __attribute__((aligned(16))) T Bs[2][64 * WN][LD];
   int bx, by, bz;
   xcd_block(g.xcd != 0, bx, by, bz);
-  conv_lp_block<MODE, ACT, WM, WN, OP, LKS, ST>(w, src, bias, dst, dst_bytes, g, M, splits, kper,
-                                                 part, cnt, stats, bx, by, bz, gridDim.x, As, Bs);
+  conv_lp_block<MODE, ACT, WM, WN, OP, LKS, ST, TS, TD>(w, src, bias, dst, dst_bytes, g, M, splits,
+                                                         kper, part, cnt, stats, bx, by, bz,
+                                                         gridDim.x, As, Bs);
 }
 
 // split-K reduction (fixed order) + bias / relu / residual epilogue:
@@ -580,27 +589,27 @@ size_t lp_workspace(int mode, const ConvGeom &g, int M, int op) {
   return p.splits > 1 ? (size_t)p.splits * M * p.ncols * sizeof(float) : 0;
 }
 
-template <int MODE, int ACT, int OP>
-static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, const float *src,
-                     const float *bias, float *out, long long out_bytes, const ConvGeom &g, int M,
+template <int MODE, int ACT, int OP, typename TS = float, typename TD = float>
+static void lp_tiles(const LpPlan &p, dim3 grid, hipStream_t s, const float *w, const TS *src,
+                     const float *bias, TD *out, long long out_bytes, const ConvGeom &g, int M,
                      float *part, unsigned int *cnt, double *stats) {
 #define LP_L(WMV, WNV)                                                                              \
   do {                                                                                              \
     if (OP != 0 && WNV <= 2 && p.lk == 64) {                                                        \
       if (MODE == 0 && stats)                                                                       \
-        hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32, true>), \
+        hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32, true, TS, TD>), \
                            grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits,     \
                            p.kper, part, cnt, stats);                                               \
       else                                                                                          \
-        hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32>),   \
+        hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, (OP != 0 && WNV <= 2) ? 64 : 32, false, TS, TD>), \
                            grid, dim3(256), 0, s, w, src, bias, out, out_bytes, g, M, p.splits,     \
                            p.kper, part, cnt, nullptr);                                             \
     } else if (MODE == 0 && stats) {                                                                \
-      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32, true>), grid, dim3(256), 0, s, w,  \
-                         src, bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt, stats);      \
+      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32, true, TS, TD>), grid, dim3(256), 0, s, \
+                         w, src, bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt, stats);   \
     } else {                                                                                        \
-      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32>), grid, dim3(256), 0, s, w, src,   \
-                         bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt, nullptr);        \
+      hipLaunchKernelGGL((k_conv_lp<MODE, ACT, WMV, WNV, OP, 32, false, TS, TD>), grid, dim3(256), 0, s, \
+                         w, src, bias, out, out_bytes, g, M, p.splits, p.kper, part, cnt, nullptr); \
     }                                                                                               \
   } while (0)
   if (p.wm == 2) {
@@ -625,9 +634,9 @@ int lp_stats_tiles(const ConvGeom &g, int op) {
   return (int)cdiv(p.ncols, 64 * p.wn);
 }
 
-int lp_launch(int mode, int act, int op, const float *w, const float *src, const float *bias,
-              float *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
-              hipStream_t s, double *stats) {
+int lp_launch(int mode, int act, int op, const float *w, const void *src, const float *bias,
+              void *dst, long long dst_bytes, const ConvGeom &g, int M, void *workspace,
+              hipStream_t s, double *stats, int io) {
   const LpPlan p = lp_plan(mode, g, M, op);
   const dim3 grid(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
   float *part = nullptr;
@@ -645,13 +654,29 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
     set_error("conv (low precision): BatchNorm statistics need the forward with its final epilogue");
     return E2EP_EINVAL;
   }
+  // bf16 storage: a bf16 forward input, or a bf16 data gradient written by the kernel's own
+  // final epilogue (the separate split reduction writes fp32)
+  const bool sb = mode == 0 && io == E2EP_IO_X_BF16, db = mode == 1 && io == E2EP_IO_DX_BF16;
+  if (io && (op != 1 || !(sb || db) || (db && p.splits > 1 && !cnt))) {
+    set_error("conv (low precision): storage mask %d not supported here (bf16 operands; forward "
+              "input or data-gradient output; the in-launch split-K fold)", io);
+    return E2EP_EINVAL;
+  }
   // bias / residual: the kernel's final epilogue, or the separate reduction
   const float *kb = (p.splits > 1 && !cnt) ? nullptr : bias;
+  const float *srcf = static_cast<const float *>(src);
+  float *dstf = static_cast<float *>(dst);
 #define LP_OPS(MD, AC)                                                     \
   do {                                                                     \
-    if (op == 1) lp_tiles<MD, AC, 1>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt, stats); \
-    else if (op == 2) lp_tiles<MD, AC, 2>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt, stats); \
-    else lp_tiles<MD, AC, 0>(p, grid, s, w, src, kb, dst, dst_bytes, g, M, part, cnt, stats); \
+    if (op == 1 && sb)                                                     \
+      lp_tiles<MD, AC, 1, bf16_t, float>(p, grid, s, w, static_cast<const bf16_t *>(src), kb, dstf, \
+                                         dst_bytes, g, M, part, cnt, stats); \
+    else if (op == 1 && db)                                                \
+      lp_tiles<MD, AC, 1, float, bf16_t>(p, grid, s, w, srcf, kb, static_cast<bf16_t *>(dst), \
+                                         dst_bytes, g, M, part, cnt, stats); \
+    else if (op == 1) lp_tiles<MD, AC, 1>(p, grid, s, w, srcf, kb, dstf, dst_bytes, g, M, part, cnt, stats); \
+    else if (op == 2) lp_tiles<MD, AC, 2>(p, grid, s, w, srcf, kb, dstf, dst_bytes, g, M, part, cnt, stats); \
+    else lp_tiles<MD, AC, 0>(p, grid, s, w, srcf, kb, dstf, dst_bytes, g, M, part, cnt, stats); \
   } while (0)
   if (mode == 0 && act == 0) LP_OPS(0, 0);
   else if (mode == 0) LP_OPS(0, 1);
@@ -661,7 +686,7 @@ int lp_launch(int mode, int act, int op, const float *w, const float *src, const
     const int HW = mode == 0 ? g.P * g.Q : g.H * g.W;
     hipLaunchKernelGGL(k_conv_lp_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s,
                        static_cast<const float *>(workspace), p.splits, M, HW, (int)p.ncols,
-                       mode == 0 ? bias : nullptr, act, mode == 1 ? bias : nullptr, dst);
+                       mode == 0 ? bias : nullptr, act, mode == 1 ? bias : nullptr, dstf);
   }
   return 0;
 }
@@ -693,9 +718,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // OP 0: the same GEMM on the exact-f32 MFMA with fp32 LDS rows (k_conv_lp's fp32 K order).
 // The block body for block (bx, by, bz) of a grid with gz pixel splits, its operand tiles in
 // the caller's LDS: k_wgrad_lp, and the weight-gradient half of k_lp_bwd_pair.
-template <int WM, int WN, int OP, int LKS>
+template <int WM, int WN, int OP, int LKS, typename TX = float>
 __device__ __forceinline__ void wgrad_lp_block(
-    const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
+    const float *__restrict__ gout, const TX *__restrict__ x, float *__restrict__ part,
     ConvGeom g, int pix_per_split, TapList tl, int bx, int by, int bz, int gz,
     typename LpType<OP == 0 ? 0 : 1>::T (*As)[64 * WM][lld_of(OP, LKS)],
     typename LpType<OP == 0 ? 0 : 1>::T (*Bs)[64 * WN][lld_of(OP, LKS)]) {
@@ -748,8 +773,9 @@ __device__ __forceinline__ void wgrad_lp_block(
     if (col >= Kl) cdy[j] = -(1 << 29);  // never in bounds
   }
   const __amdgpu_buffer_rsrc_t rg = rsrc(gout, 4LL * g.N * g.Cout * PQ);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
-  const int nrx = (int)min(4LL * g.N * g.Cin * HW, 0x7fffffffLL);
+  constexpr int EX = sizeof(TX);  // bytes per x element (bf16: C3's stored SE output)
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, (long long)EX * g.N * g.Cin * HW);
+  const int nrx = (int)min((long long)EX * g.N * g.Cin * HW, 0x7fffffffLL);
 
   float4 ra[NA8][2];
   float rb[NBC][2];
@@ -775,7 +801,7 @@ __device__ __forceinline__ void wgrad_lp_block(
 #pragma unroll
         for (int j = 0; j < NBC; ++j) {
           const bool ok = (unsigned)(yb + cdy[j]) < (unsigned)g.H && (unsigned)(xb + cdx[j]) < (unsigned)g.W;
-          rb[j][e] = bload(rx, ok ? (pbase + cconst[j]) * 4 : nrx);
+          rb[j][e] = bload_t(rx, ok ? (pbase + cconst[j]) * EX : nrx, x);
         }
       }
     } else {
@@ -790,18 +816,27 @@ __device__ __forceinline__ void wgrad_lp_block(
         const bool rowok = (unsigned)(yb + cdy[j]) < (unsigned)g.H;  // dead columns: never
         const int base = pbase + cconst[j];  // element offset of the window's first value
         if (rowok && x0 >= 0 && x0 + last < g.W) {  // inside the row: vector loads
-          rv[j][0] = bload4(rx, base * 4);
-          rv[j][1] = bload4(rx, base * 4 + 16);
-          if (g.sw == 2) {
-            rv[j][2] = bload4(rx, base * 4 + 32);
-            rv[j][3] = bload4(rx, base * 4 + 48);
+          if constexpr (EX == 2) {  // bf16 x: 4 (stride 1) / 8 (stride 2) values per 8-B load
+            rv[j][0] = bload4t(rx, base * 2, x);
+            rv[j][1] = bload4t(rx, base * 2 + 8, x);
+            if (g.sw == 2) {
+              rv[j][2] = bload4t(rx, base * 2 + 16, x);
+              rv[j][3] = bload4t(rx, base * 2 + 24, x);
+            }
+          } else {
+            rv[j][0] = bload4(rx, base * 4);
+            rv[j][1] = bload4(rx, base * 4 + 16);
+            if (g.sw == 2) {
+              rv[j][2] = bload4(rx, base * 4 + 32);
+              rv[j][3] = bload4(rx, base * 4 + 48);
+            }
           }
         } else {  // a row end (zero padding) or a dead column: value by value
           float t[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const bool ok = rowok && (unsigned)(x0 + q * g.sw) < (unsigned)g.W;
-            t[q] = bload(rx, ok ? (base + q * g.sw) * 4 : nrx);
+            t[q] = bload_t(rx, ok ? (base + q * g.sw) * EX : nrx, x);
           }
           if (g.sw == 2) {
 #pragma unroll
@@ -931,9 +966,9 @@ __device__ __forceinline__ void wgrad_lp_block(
   }
 }
 
-template <int WM, int WN, int OP, int LKS>
+template <int WM, int WN, int OP, int LKS, typename TX = float>
 __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout,
-                                                  const float *__restrict__ x,
+                                                  const TX *__restrict__ x,
                                                   float *__restrict__ part, ConvGeom g,
                                                   int pix_per_split, TapList tl) {
   typedef typename LpType<OP == 0 ? 0 : 1>::T T;
@@ -942,7 +977,8 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   __shared__ __attribute__((aligned(16))) T Bs[2][64 * WN][LD];
   int bx, by, bz;
   xcd_block(g.xcd != 0, bx, by, bz);
-  wgrad_lp_block<WM, WN, OP, LKS>(gout, x, part, g, pix_per_split, tl, bx, by, bz, gridDim.z, As, Bs);
+  wgrad_lp_block<WM, WN, OP, LKS, TX>(gout, x, part, g, pix_per_split, tl, bx, by, bz, gridDim.z, As,
+                                      Bs);
 }
 
 // A conv layer's data gradient (k_conv_lp MODE 1) and weight gradient (k_wgrad_lp slabs) in
@@ -951,12 +987,12 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
 // (e2ep_conv_bwd): in a replayed graph a fork / join idles the GPU ~15 us.  LDS: the larger
 // of the two halves' operand tiles, one buffer.  fp32 (OP 0) pairs the 64 x 64 weight-gradient
 // tile, whose K order and slabs are k_conv_wgrad2's (the kernel the two-launch fp32 path runs).
-template <int DWM, int DWN, int OP, int WWM, int WWN>
+template <int DWM, int DWN, int OP, int WWM, int WWN, typename TX = float>
 __global__ void __launch_bounds__(256) k_lp_bwd_pair(
     const float *__restrict__ w, const float *__restrict__ gout, const float *__restrict__ res,
-    float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
+    TX *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
-    const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
+    const TX *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
     int gx2, int gy2, int gz2) {
   typedef typename LpType<OP>::T T;
   constexpr int LD = lld_of(OP, LK);
@@ -966,7 +1002,7 @@ __global__ void __launch_bounds__(256) k_lp_bwd_pair(
   int id = (int)blockIdx.x;
   if (id < n1) {
     if (g.xcd) id = xcd_linear(id, n1);
-    conv_lp_block<1, 0, DWM, DWN, OP, LK>(
+    conv_lp_block<1, 0, DWM, DWN, OP, LK, false, float, TX>(
         w, gout, res, dx, dx_bytes, g, M, splits, kper, part1, cnt, nullptr, id % gx1,
         (id / gx1) % gy1, id / (gx1 * gy1), gx1, reinterpret_cast<T(*)[64 * DWM][LD]>(lds),
         reinterpret_cast<T(*)[64 * DWN][LD]>(lds + 2 * 64 * DWM * LD));
@@ -974,7 +1010,7 @@ __global__ void __launch_bounds__(256) k_lp_bwd_pair(
     id -= n1;
     const int n2 = gx2 * gy2 * gz2;
     if (g.xcd) id = xcd_linear(id, n2);
-    wgrad_lp_block<WWM, WWN, OP, LK>(
+    wgrad_lp_block<WWM, WWN, OP, LK, TX>(
         gout, x, part2, g, pix_per_split, tl, id % gx2, (id / gx2) % gy2, id / (gx2 * gy2), gz2,
         reinterpret_cast<T(*)[64 * WWM][LD]>(lds),
         reinterpret_cast<T(*)[64 * WWN][LD]>(lds + 2 * 64 * WWM * LD));
@@ -1028,8 +1064,10 @@ int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op) {
   return (int)std::max(1LL, std::min(s, 256LL));
 }
 
-int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const TapList &tl,
-                    int splits, float *part, hipStream_t s, int op) {
+int lp_wgrad_launch(const float *gout, const void *xv, const ConvGeom &g, const TapList &tl,
+                    int splits, float *part, hipStream_t s, int op, bool xb) {
+  const float *x = static_cast<const float *>(xv);
+  const bf16_t *xh = static_cast<const bf16_t *>(xv);
   int wm, wn;
   lp_wgrad_tile(g, tl, wm, wn);
   const int lk = lp_wgrad_lk(g, op);
@@ -1042,6 +1080,10 @@ int lp_wgrad_launch(const float *gout, const float *x, const ConvGeom &g, const 
   do {                                                                                           \
     if (op != 1)                                                                                 \
       hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 0, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
+    else if (xb && lk == 64)                                                                     \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64, bf16_t>), grid, dim3(256), 0, s, gout, xh, part, g, per, tl); \
+    else if (xb)                                                                                 \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 32, bf16_t>), grid, dim3(256), 0, s, gout, xh, part, g, per, tl); \
     else if (lk == 64)                                                                           \
       hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
     else                                                                                         \
@@ -1086,13 +1128,18 @@ bool lp_bwd_pair_ok(const ConvGeom &g, int M, int op, const TapList &tl) {
   return lp_pair_tiles(g, M, op, tl, p, wwm, wwn);
 }
 
-int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, float *dx,
+int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void *dxv,
                        long long dx_bytes, const ConvGeom &g, int M, int op, void *ws_dgrad,
-                       const float *x, const TapList &tl, int wsplits, float *part2,
-                       hipStream_t s) {
+                       const void *xv, const TapList &tl, int wsplits, float *part2,
+                       hipStream_t s, bool xb) {
   LpPlan p;
   int wwm, wwn;
   if (!lp_pair_tiles(g, M, op, tl, p, wwm, wwn)) return -1;
+  if (xb && op != 1) return -1;
+  float *dx = static_cast<float *>(dxv);
+  const float *x = static_cast<const float *>(xv);
+  bf16_t *dxh = static_cast<bf16_t *>(dxv);
+  const bf16_t *xh = static_cast<const bf16_t *>(xv);
   const dim3 g1(cdiv(p.ncols, 64 * p.wn), cdiv(M, 64 * p.wm), p.nph * p.splits);
   float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
   unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y, s) : nullptr;
@@ -1103,9 +1150,16 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, floa
   const dim3 g2(cdiv(g.Cin * tl.n, 64 * wwn), cdiv(g.Cout, 64 * wwm), used);
   const dim3 grid(g1.x * g1.y * g1.z + g2.x * g2.y * g2.z);
 #define PAIR_L(DM, DN, OPV, WMV, WNV)                                                           \
-  hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV>), grid, dim3(256), 0, s, w, gout,    \
-                     res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x,           \
-                     (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
+  do {                                                                                          \
+    if (OPV == 1 && xb)                                                                         \
+      hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV, bf16_t>), grid, dim3(256), 0, s, w, \
+                         gout, res, dxh, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, \
+                         (int)g1.y, (int)g1.z, xh, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z); \
+    else                                                                                        \
+      hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV>), grid, dim3(256), 0, s, w, gout,  \
+                         res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x,       \
+                         (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z); \
+  } while (0)
 #define PAIR_W(DM, DN)                                     \
   do {                                                     \
     if (wwm == 2 && wwn == 2) PAIR_L(DM, DN, 1, 2, 2);     \

@@ -2,6 +2,8 @@
 // (efficientnet-pytorch 0.7.1 _depthwise_conv: k3/k5, stride 1/2, static SAME padding),
 // forward, data gradient (gather, no atomics) and weight gradient (fixed-order split
 // reduction), NCHW fp32, for gfx950.  Memory-bound: each kernel streams its input once.
+#include <type_traits>
+
 #include "common.h"
 #include "handoff.h"
 
@@ -247,7 +249,7 @@ __device__ __forceinline__ float4 dw_tf4(float4 v, const DwT &t, bool in) {
 // buffer descriptor of a wave-uniform plane: the base pointer and size go through
 // readfirstlane so the descriptor lives in SGPRs (a VGPR descriptor makes hipcc wrap every
 // buffer load in a waterfall loop)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_u(const float *p, long long bytes) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_u(const void *p, long long bytes) {
   const unsigned long long a = reinterpret_cast<unsigned long long>(p);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
@@ -255,12 +257,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_u(const float *p, long lo
   return __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void *>(((unsigned long long)hi << 32) | lo), (short)0, nb, 0x00020000);
 }
-__device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, int W, int iy0,
+template <typename TI>
+__device__ __forceinline__ void dw_stage(const TI *__restrict__ src, int H, int W, int iy0,
                                          int IR, int WP, float *lds, int lane,
                                          DwIn tf = DwIn{nullptr, nullptr, 0}, int c = 0) {
   const int W4 = W >> 2;
   const DwT t = dw_t(tf, c);
-  const __amdgpu_buffer_rsrc_t rs = rsrc_u(src, 4LL * H * W);
+  constexpr int EB = sizeof(TI);  // bytes per element (4 fp32, 2 bf16 storage)
+  const __amdgpu_buffer_rsrc_t rs = rsrc_u(src, (long long)EB * H * W);
   float4 v[DW_MAXV];
   bool in[DW_MAXV];
 #pragma unroll
@@ -269,7 +273,7 @@ __device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, i
     const int r = e / W4, j = e - r * W4;
     const int iy = iy0 + r;
     in[i] = e < IR * W4 && (unsigned)iy < (unsigned)H;
-    v[i] = bload4(rs, in[i] ? (iy * W + 4 * j) * 4 : OOR);
+    v[i] = bload4t(rs, in[i] ? (iy * W + 4 * j) * EB : OOR, src);
   }
 #pragma unroll
   for (int i = 0; i < DW_MAXV; ++i) {
@@ -289,18 +293,19 @@ __device__ __forceinline__ void dw_stage(const float *__restrict__ src, int H, i
 // The same staging split in two for software pipelining: dw_fetch issues a unit's row loads
 // into registers (at most DW_MAXV float4 per lane), dw_put writes them (normalised) and the
 // halo zeros into LDS once they have landed.
-template <int V>
-__device__ __forceinline__ void dw_fetch(const float *__restrict__ src, int H, int W, int iy0,
+template <int V, typename TI>
+__device__ __forceinline__ void dw_fetch(const TI *__restrict__ src, int H, int W, int iy0,
                                          int IR, int lane, float4 (&r)[V], bool active) {
   const int W4 = W >> 2;
-  const __amdgpu_buffer_rsrc_t rs = rsrc_u(src, 4LL * H * W);
+  constexpr int EB = sizeof(TI);
+  const __amdgpu_buffer_rsrc_t rs = rsrc_u(src, (long long)EB * H * W);
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int e = lane + 64 * i;
     const int rr = e / W4, j = e - rr * W4;
     const int iy = iy0 + rr;
     const bool ok = active && e < IR * W4 && (unsigned)iy < (unsigned)H;
-    r[i] = bload4(rs, ok ? (iy * W + 4 * j) * 4 : OOR);  // branch-free (see dw_stage)
+    r[i] = bload4t(rs, ok ? (iy * W + 4 * j) * EB : OOR, src);  // branch-free (see dw_stage)
   }
 }
 template <int V>
@@ -363,12 +368,22 @@ __device__ __forceinline__ double dw_wave_sum(double v) {
   return v;
 }
 
+// bf16 activation storage (B, e2ep.h E2EP_IO_*): the forward's output y (the MBConv depthwise
+// output, read by the squeeze-excitation and the _bn1 backward) and, in the backward, the
+// incoming gradient gy and the data gradient dx are bf16; the forward's input (the raw expand
+// conv output, normalised on load) stays fp32.  FLIP (the stride-1 data gradient) reads gy.
+template <bool FLIP, bool B>
+using dw_ti = std::conditional_t<FLIP && B, bf16_t, float>;
+template <bool B>
+using dw_to = std::conditional_t<B, bf16_t, float>;
+
 // The block body for block blk of nblk (k_dw_fwd_strip, and the data-gradient half of
-// k_dw_bwd_pair), over the kernel's dynamic LDS.
-template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false>
-__device__ __forceinline__ void dw_fwd_strip_body(const float *__restrict__ x,
+// k_dw_bwd_pair), over the kernel's dynamic LDS.  BS statistics are of the stored (rounded)
+// values.
+template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false, bool B = false>
+__device__ __forceinline__ void dw_fwd_strip_body(const dw_ti<FLIP, B> *__restrict__ x,
                                                   const float *__restrict__ w, DwGeom g, DwStrip d,
-                                                  int units, float *__restrict__ y, DwIn tf,
+                                                  int units, dw_to<B> *__restrict__ y, DwIn tf,
                                                   double *__restrict__ stats, int blk, int nblk) {
   extern __shared__ float dw_lds[];
   // Grid-stride over units, software-pipelined like k_dw_wgrad_strip: the wave's next unit's
@@ -416,16 +431,16 @@ __device__ __forceinline__ void dw_fwd_strip_body(const float *__restrict__ x,
 #pragma unroll
           for (int b = 0; b < K; ++b) o[q] = __builtin_fmaf(wr[a * K + b], v[q * ST + b], o[q]);
       }
-      *reinterpret_cast<float4 *>(y + ((size_t)cur_nc * g.P + oy) * g.Q + ox0) =
-          make_float4(o[0], o[1], o[2], o[3]);
+      st4(y + ((size_t)cur_nc * g.P + oy) * g.Q + ox0, make_float4(o[0], o[1], o[2], o[3]));
     }
     if (BS) {  // BatchNorm partials (separate instantiation)
       float f1 = 0.f, f2 = 0.f;
       if (live) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          f1 += o[q];
-          f2 = __builtin_fmaf(o[q], o[q], f2);
+          const float v = stored<dw_to<B>>(o[q]);
+          f1 += v;
+          f2 = __builtin_fmaf(v, v, f2);
         }
       }
       const double s1 = dw_wave_sum((double)f1);
@@ -441,13 +456,13 @@ __device__ __forceinline__ void dw_fwd_strip_body(const float *__restrict__ x,
   }
 }
 
-template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false>
-__global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ x,
+template <int K, int ST, bool FLIP, int OFF, int V, bool BS = false, bool B = false>
+__global__ void __launch_bounds__(256) k_dw_fwd_strip(const dw_ti<FLIP, B> *__restrict__ x,
                                                       const float *__restrict__ w, DwGeom g,
-                                                      DwStrip d, int units, float *__restrict__ y,
+                                                      DwStrip d, int units, dw_to<B> *__restrict__ y,
                                                       DwIn tf, double *__restrict__ stats) {
-  dw_fwd_strip_body<K, ST, FLIP, OFF, V, BS>(x, w, g, d, units, y, tf, stats, blockIdx.x,
-                                             gridDim.x);
+  dw_fwd_strip_body<K, ST, FLIP, OFF, V, BS, B>(x, w, g, d, units, y, tf, stats, blockIdx.x,
+                                                gridDim.x);
 }
 
 // stride-2 data gradient over strip units: a wave owns RO = 64/(W/4) rows of dx of one plane,
@@ -456,11 +471,11 @@ __global__ void __launch_bounds__(256) k_dw_fwd_strip(const float *__restrict__ 
 // parity of (u + pl - b) is compile-time given PLP = pl & 1.
 // The block body for block blk (k_dw_dgrad_s2_strip, and the data-gradient half of
 // k_dw_bwd_pair_s2), over the kernel's dynamic LDS.
-template <int K, int PLP>
-__device__ __forceinline__ void dw_dgrad_s2_body(const float *__restrict__ gy,
+template <int K, int PLP, bool B = false>
+__device__ __forceinline__ void dw_dgrad_s2_body(const dw_to<B> *__restrict__ gy,
                                                  const float *__restrict__ w, DwGeom g, int RO,
                                                  int GR, int WPg, int units_per_plane, int units,
-                                                 float *__restrict__ dx, int blk) {
+                                                 dw_to<B> *__restrict__ dx, int blk) {
   extern __shared__ float dw_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR descriptors
@@ -497,16 +512,16 @@ __device__ __forceinline__ void dw_dgrad_s2_body(const float *__restrict__ gy,
       for (int b = 0; b < K; ++b)
         if (((u + PLP - b) & 1) == 0) o[u] = __builtin_fmaf(wr[a * K + b], row[(u + PLP - b) >> 1], o[u]);
   }
-  *reinterpret_cast<float4 *>(dx + ((size_t)nc * g.H + iy) * g.W + ix0) = make_float4(o[0], o[1], o[2], o[3]);
+  st4(dx + ((size_t)nc * g.H + iy) * g.W + ix0, make_float4(o[0], o[1], o[2], o[3]));
 }
 
-template <int K, int PLP>
-__global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restrict__ gy,
+template <int K, int PLP, bool B = false>
+__global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const dw_to<B> *__restrict__ gy,
                                                            const float *__restrict__ w, DwGeom g,
                                                            int RO, int GR, int WPg,
                                                            int units_per_plane, int units,
-                                                           float *__restrict__ dx) {
-  dw_dgrad_s2_body<K, PLP>(gy, w, g, RO, GR, WPg, units_per_plane, units, dx, blockIdx.x);
+                                                           dw_to<B> *__restrict__ dx) {
+  dw_dgrad_s2_body<K, PLP, B>(gy, w, g, RO, GR, WPg, units_per_plane, units, dx, blockIdx.x);
 }
 
 // weight gradient partials over strip units: grid (C, splits); the block's waves walk the
@@ -514,8 +529,8 @@ __global__ void __launch_bounds__(256) k_dw_dgrad_s2_strip(const float *__restri
 // wave + block reduction.
 // The block body for channel c, split sp (k_dw_wgrad_strip, and the weight-gradient half of
 // k_dw_bwd_pair), over the kernel's dynamic LDS.
-template <int K, int ST, int OFF, int V>
-__device__ __forceinline__ void dw_wgrad_strip_body(const float *__restrict__ gy,
+template <int K, int ST, int OFF, int V, bool B = false>
+__device__ __forceinline__ void dw_wgrad_strip_body(const dw_to<B> *__restrict__ gy,
                                                     const float *__restrict__ x, DwGeom g,
                                                     DwStrip d, int splits, DwPart part, DwIn tf,
                                                     int c, int sp) {
@@ -542,7 +557,8 @@ __device__ __forceinline__ void dw_wgrad_strip_body(const float *__restrict__ gy
   };
   float4 rx[V];
   float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
-  const __amdgpu_buffer_rsrc_t rgy = rsrc(gy, 4LL * g.N * g.C * g.P * g.Q);
+  constexpr int GB = sizeof(dw_to<B>);  // bytes per gy element
+  const __amdgpu_buffer_rsrc_t rgy = rsrc(gy, (long long)GB * g.N * g.C * g.P * g.Q);
   int n = 0, oy0 = 0;
   bool active = beg + wave < end;
   if (active) unit_of(beg + wave, n, oy0);
@@ -550,7 +566,7 @@ __device__ __forceinline__ void dw_wgrad_strip_body(const float *__restrict__ gy
     dw_fetch(x + ((size_t)nn * g.C + c) * g.H * g.W, g.H, g.W, yy0 * ST - g.pt, d.IR, lane, rx, act);
     const int oy = yy0 + ro;
     const bool ok = act && ro < d.RO && oy < g.P;
-    gq = bload4(rgy, ok ? ((nn * g.C + c) * g.P + oy) * g.Q * 4 + ox0 * 4 : OOR);
+    gq = bload4t(rgy, ok ? (((nn * g.C + c) * g.P + oy) * g.Q + ox0) * GB : OOR, gy);
   };
   const DwT tfc = dw_t(tf, c);  // the block's channel: read once
   fetch(active, n, oy0);
@@ -599,12 +615,12 @@ __device__ __forceinline__ void dw_wgrad_strip_body(const float *__restrict__ gy
                       reinterpret_cast<int *>(&red[0][0]));
 }
 
-template <int K, int ST, int OFF, int V>
-__global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict__ gy,
+template <int K, int ST, int OFF, int V, bool B = false>
+__global__ void __launch_bounds__(256) k_dw_wgrad_strip(const dw_to<B> *__restrict__ gy,
                                                         const float *__restrict__ x, DwGeom g,
                                                         DwStrip d, int splits,
                                                         DwPart part, DwIn tf) {
-  dw_wgrad_strip_body<K, ST, OFF, V>(gy, x, g, d, splits, part, tf, blockIdx.x, blockIdx.y);
+  dw_wgrad_strip_body<K, ST, OFF, V, B>(gy, x, g, d, splits, part, tf, blockIdx.x, blockIdx.y);
 }
 
 // A stride-1 depthwise layer's data gradient (the flipped-filter strip forward over gy, gt /
@@ -616,35 +632,35 @@ __global__ void __launch_bounds__(256) k_dw_wgrad_strip(const float *__restrict_
 // (67.5 us against 52 us for the weight gradient alone).  One launch instead of two on
 // forked streams (e2ep_dwconv_bwd): in a replayed graph the fork / join idles the GPU ~17 us
 // per layer.  Dynamic LDS: the larger of the two halves' per-wave row buffers.
-template <int K, int OFF, int VD, int VW>
-__global__ void __launch_bounds__(256) k_dw_bwd_pair(const float *__restrict__ gy,
+template <int K, int OFF, int VD, int VW, bool B = false>
+__global__ void __launch_bounds__(256) k_dw_bwd_pair(const dw_to<B> *__restrict__ gy,
                                                      const float *__restrict__ w, DwGeom gt,
-                                                     DwStrip dt, int units, float *__restrict__ dx,
+                                                     DwStrip dt, int units, dw_to<B> *__restrict__ dx,
                                                      int nd, const float *__restrict__ x, DwGeom g,
                                                      DwStrip d, int splits, DwPart part, DwIn tf) {
   const int b = blockIdx.x, nw = g.C * splits;
   if (b < nw) {
-    dw_wgrad_strip_body<K, 1, OFF, VW>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
+    dw_wgrad_strip_body<K, 1, OFF, VW, B>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
   } else {
-    dw_fwd_strip_body<K, 1, true, OFF, VD>(gy, w, gt, dt, units, dx, DwIn{nullptr, nullptr, 0},
-                                           nullptr, b - nw, nd);
+    dw_fwd_strip_body<K, 1, true, OFF, VD, false, B>(gy, w, gt, dt, units, dx,
+                                                     DwIn{nullptr, nullptr, 0}, nullptr, b - nw, nd);
   }
 }
 
 // The stride-2 form of k_dw_bwd_pair: weight-gradient blocks first (channel c, split sp), then
 // the k_dw_dgrad_s2_strip blocks (one unit per wave).
-template <int K, int PLP, int OFF, int VW>
-__global__ void __launch_bounds__(256) k_dw_bwd_pair_s2(const float *__restrict__ gy,
+template <int K, int PLP, int OFF, int VW, bool B = false>
+__global__ void __launch_bounds__(256) k_dw_bwd_pair_s2(const dw_to<B> *__restrict__ gy,
                                                         const float *__restrict__ w, int RO, int GR,
                                                         int WPg, int upp2, int units2,
-                                                        float *__restrict__ dx,
+                                                        dw_to<B> *__restrict__ dx,
                                                         const float *__restrict__ x, DwGeom g,
                                                         DwStrip d, int splits, DwPart part, DwIn tf) {
   const int b = blockIdx.x, nw = g.C * splits;
   if (b < nw)
-    dw_wgrad_strip_body<K, 2, OFF, VW>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
+    dw_wgrad_strip_body<K, 2, OFF, VW, B>(gy, x, g, d, splits, part, tf, b % g.C, b / g.C);
   else
-    dw_dgrad_s2_body<K, PLP>(gy, w, g, RO, GR, WPg, upp2, units2, dx, b - nw);
+    dw_dgrad_s2_body<K, PLP, B>(gy, w, g, RO, GR, WPg, upp2, units2, dx, b - nw);
 }
 
 static int dw_splits(long long pixels, int C) {
@@ -689,65 +705,70 @@ static int dw_off(int pl) { return g_tune[TUNE_DW_VEC] == 1 ? -1 : ((-pl) & 3); 
 // launch a strip kernel with the row-read variant `off` as its compile-time OFF and the
 // staging registers V = 2 float4 per lane when `nv` (float4 per lane a unit needs) allows
 // (the scalar-read variant, an A/B switch, always takes DW_MAXV)
-template <int K, int ST, bool FLIP, int V>
-static void dw_fwd_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *x,
-                           const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf,
+template <int K, int ST, bool FLIP, int V, bool B>
+static void dw_fwd_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const void *xv,
+                           const float *w, DwGeom g, DwStrip d, int units, void *yv, DwIn tf,
                            double *stats) {
+  const auto *x = static_cast<const dw_ti<FLIP, B> *>(xv);
+  auto *y = static_cast<dw_to<B> *>(yv);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, x, w, g, d, units, y, tf, stats);
   };
   if (stats && !FLIP) {
     switch (off) {
-      case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V, true>); break;
-      case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V, true>); break;
-      case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2, V, true>); break;
-      default: go(k_dw_fwd_strip<K, ST, FLIP, 3, V, true>);
+      case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V, true, B>); break;
+      case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V, true, B>); break;
+      case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2, V, true, B>); break;
+      default: go(k_dw_fwd_strip<K, ST, FLIP, 3, V, true, B>);
     }
     return;
   }
   switch (off) {
-    case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V>); break;
-    case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V>); break;
-    case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2, V>); break;
-    default: go(k_dw_fwd_strip<K, ST, FLIP, 3, V>);
+    case 0: go(k_dw_fwd_strip<K, ST, FLIP, 0, V, false, B>); break;
+    case 1: go(k_dw_fwd_strip<K, ST, FLIP, 1, V, false, B>); break;
+    case 2: go(k_dw_fwd_strip<K, ST, FLIP, 2, V, false, B>); break;
+    default: go(k_dw_fwd_strip<K, ST, FLIP, 3, V, false, B>);
   }
 }
-template <int K, int ST, bool FLIP>
-static void dw_fwd_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const float *x,
-                         const float *w, DwGeom g, DwStrip d, int units, float *y, DwIn tf,
+template <int K, int ST, bool FLIP, bool B>
+static void dw_fwd_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const void *xv,
+                         const float *w, DwGeom g, DwStrip d, int units, void *yv, DwIn tf,
                          double *stats) {
+  const auto *x = static_cast<const dw_ti<FLIP, B> *>(xv);
+  auto *y = static_cast<dw_to<B> *>(yv);
   if (off < 0 && stats && !FLIP)
-    hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV, true>), grid, dim3(256), shm, st,
+    hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV, true, B>), grid, dim3(256), shm, st,
                        x, w, g, d, units, y, tf, stats);
   else if (off < 0)
-    hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV>), grid, dim3(256), shm, st, x, w,
-                       g, d, units, y, tf, nullptr);
+    hipLaunchKernelGGL((k_dw_fwd_strip<K, ST, FLIP, -1, DW_MAXV, false, B>), grid, dim3(256), shm, st,
+                       x, w, g, d, units, y, tf, nullptr);
   else if (nv <= 2)
-    dw_fwd_strip_v<K, ST, FLIP, 2>(off, grid, shm, st, x, w, g, d, units, y, tf, stats);
+    dw_fwd_strip_v<K, ST, FLIP, 2, B>(off, grid, shm, st, xv, w, g, d, units, yv, tf, stats);
   else
-    dw_fwd_strip_v<K, ST, FLIP, DW_MAXV>(off, grid, shm, st, x, w, g, d, units, y, tf, stats);
+    dw_fwd_strip_v<K, ST, FLIP, DW_MAXV, B>(off, grid, shm, st, xv, w, g, d, units, yv, tf, stats);
 }
-template <int K, int ST, int V>
-static void dw_wgrad_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const float *gy,
+template <int K, int ST, int V, bool B>
+static void dw_wgrad_strip_v(int off, dim3 grid, size_t shm, hipStream_t st, const void *gyv,
                              const float *x, DwGeom g, DwStrip d, int splits, DwPart part, DwIn tf) {
+  const auto *gy = static_cast<const dw_to<B> *>(gyv);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), shm, st, gy, x, g, d, splits, part, tf); };
   switch (off) {
-    case 0: go(k_dw_wgrad_strip<K, ST, 0, V>); break;
-    case 1: go(k_dw_wgrad_strip<K, ST, 1, V>); break;
-    case 2: go(k_dw_wgrad_strip<K, ST, 2, V>); break;
-    default: go(k_dw_wgrad_strip<K, ST, 3, V>);
+    case 0: go(k_dw_wgrad_strip<K, ST, 0, V, B>); break;
+    case 1: go(k_dw_wgrad_strip<K, ST, 1, V, B>); break;
+    case 2: go(k_dw_wgrad_strip<K, ST, 2, V, B>); break;
+    default: go(k_dw_wgrad_strip<K, ST, 3, V, B>);
   }
 }
-template <int K, int ST>
-static void dw_wgrad_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const float *gy,
+template <int K, int ST, bool B>
+static void dw_wgrad_strip(int off, int nv, dim3 grid, size_t shm, hipStream_t st, const void *gyv,
                            const float *x, DwGeom g, DwStrip d, int splits, DwPart part, DwIn tf) {
   if (off < 0)
-    hipLaunchKernelGGL((k_dw_wgrad_strip<K, ST, -1, DW_MAXV>), grid, dim3(256), shm, st, gy, x, g,
-                       d, splits, part, tf);
+    hipLaunchKernelGGL((k_dw_wgrad_strip<K, ST, -1, DW_MAXV, B>), grid, dim3(256), shm, st,
+                       static_cast<const dw_to<B> *>(gyv), x, g, d, splits, part, tf);
   else if (nv <= 2)
-    dw_wgrad_strip_v<K, ST, 2>(off, grid, shm, st, gy, x, g, d, splits, part, tf);
+    dw_wgrad_strip_v<K, ST, 2, B>(off, grid, shm, st, gyv, x, g, d, splits, part, tf);
   else
-    dw_wgrad_strip_v<K, ST, DW_MAXV>(off, grid, shm, st, gy, x, g, d, splits, part, tf);
+    dw_wgrad_strip_v<K, ST, DW_MAXV, B>(off, grid, shm, st, gyv, x, g, d, splits, part, tf);
 }
 
 extern "C" {
@@ -773,8 +794,10 @@ static bool dw_strip_ok(const DwGeom &g) {
     else                                                                                       \
       LAUNCHER<5, 2 FLIPARG>(off, nv, GRID, SHMEM, as_stream(stream), __VA_ARGS__);                \
   } while (0)
-#define DW_NOFLIP , false
-#define DW_NONE
+#define DW_NOFLIP , false, false
+#define DW_NOFLIP_B16 , false, true
+#define DW_NONE , false
+#define DW_B16 , true
 
 // dims[10] = {N, C, H, W, K, P, Q, stride, pad_top, pad_left}
 int e2ep_dwconv_fwd_stats_tiles(const int *dims) {
@@ -785,13 +808,16 @@ int e2ep_dwconv_fwd_stats_tiles(const int *dims) {
 
 int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float *in_scale,
                     const float *in_shift, int in_act, float *y, void *stream) {
-  return e2ep_dwconv_fwd_stats(x, w, dims, in_scale, in_shift, in_act, y, nullptr, 0, stream);
+  return e2ep_dwconv_fwd_stats(x, w, dims, in_scale, in_shift, in_act, y, nullptr, 0, stream, 0);
 }
 
 int e2ep_dwconv_fwd_stats(const float *x, const float *w, const int *dims, const float *in_scale,
-                          const float *in_shift, int in_act, float *y, double *stats,
-                          size_t stats_bytes, void *stream) {
+                          const float *in_shift, int in_act, void *y, double *stats,
+                          size_t stats_bytes, void *stream, int io) {
   DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(io == 0 || (io == E2EP_IO_DX_BF16 && dw_strip_ok(g)), E2EP_EINVAL,
+               "e2ep_dwconv_fwd_stats: storage mask %d not supported (0, or y bf16 on the strip "
+               "kernels)", io);
   if (stats) {
     const int tiles = e2ep_dwconv_fwd_stats_tiles(dims);
     E2EP_REQUIRE(tiles > 0, E2EP_EINVAL,
@@ -808,13 +834,17 @@ int e2ep_dwconv_fwd_stats(const float *x, const float *w, const int *dims, const
   if (dw_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
     const int units = g.N * g.C * d.units_per_plane;
-    DW_STRIP_DISPATCH(dw_fwd_strip, DW_NOFLIP, dim3(dw_fwd_blocks(units)), 4 * d.IR * d.WP * 4, x,
-                      w, g, d, units, y, tf, stats);
+    if (io)
+      DW_STRIP_DISPATCH(dw_fwd_strip, DW_NOFLIP_B16, dim3(dw_fwd_blocks(units)), 4 * d.IR * d.WP * 4,
+                        x, w, g, d, units, y, tf, stats);
+    else
+      DW_STRIP_DISPATCH(dw_fwd_strip, DW_NOFLIP, dim3(dw_fwd_blocks(units)), 4 * d.IR * d.WP * 4, x,
+                        w, g, d, units, y, tf, stats);
     return launch_status("e2ep_dwconv_fwd");
   }
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_fwd: N*C > 65535");
-  DW_DISPATCH(k_dw_fwd, dim3(cdiv(g.P * g.Q, 256), g.N * g.C), x, w, g, y, in_scale, in_shift,
-              in_act);
+  DW_DISPATCH(k_dw_fwd, dim3(cdiv(g.P * g.Q, 256), g.N * g.C), x, w, g, static_cast<float *>(y),
+              in_scale, in_shift, in_act);
   return launch_status("e2ep_dwconv_fwd");
 }
 
@@ -836,10 +866,13 @@ static bool dw_s2_plan(const DwGeom &g, DwS2 &p) {
   return true;
 }
 
-int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream) {
+int e2ep_dwconv_dgrad(const void *gy, const float *w, const int *dims, void *dx, void *stream,
+                      int io) {
   DwGeom g = dw_geom(dims);
   E2EP_REQUIRE(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0, E2EP_EINVAL,
                "e2ep_dwconv_dgrad: bad geometry");
+  E2EP_REQUIRE(io == 0 || io == (E2EP_IO_DY_BF16 | E2EP_IO_DX_BF16), E2EP_EINVAL,
+               "e2ep_dwconv_dgrad: storage mask %d not supported (0 or DY|DX bf16)", io);
   if (g.st == 1) {
     // stride 1: dx = gy (P x Q) correlated with the flipped filter, pads K-1-pad, output H x W
     DwGeom t = g;
@@ -850,12 +883,17 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
       const int units = t.N * t.C * d.units_per_plane;
       const size_t shm = 4 * d.IR * d.WP * 4;
       const DwIn none{nullptr, nullptr, 0};
-      if (t.K == 3)
-        dw_fwd_strip<3, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
-                                 w, t, d, units, dx, none, nullptr);
+      const int nv = cdiv(d.IR * (t.W / 4), 64);
+      const dim3 grid(dw_fwd_blocks(units));
+      hipStream_t s = as_stream(stream);
+      if (t.K == 3 && io)
+        dw_fwd_strip<3, 1, true, true>(dw_off(t.pl), nv, grid, shm, s, gy, w, t, d, units, dx, none, nullptr);
+      else if (t.K == 3)
+        dw_fwd_strip<3, 1, true, false>(dw_off(t.pl), nv, grid, shm, s, gy, w, t, d, units, dx, none, nullptr);
+      else if (io)
+        dw_fwd_strip<5, 1, true, true>(dw_off(t.pl), nv, grid, shm, s, gy, w, t, d, units, dx, none, nullptr);
       else
-        dw_fwd_strip<5, 1, true>(dw_off(t.pl), cdiv(d.IR * (t.W / 4), 64), dim3(dw_fwd_blocks(units)), shm, as_stream(stream), gy,
-                                 w, t, d, units, dx, none, nullptr);
+        dw_fwd_strip<5, 1, true, false>(dw_off(t.pl), nv, grid, shm, s, gy, w, t, d, units, dx, none, nullptr);
       return launch_status("e2ep_dwconv_dgrad");
     }
   }
@@ -865,18 +903,21 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
     const size_t shm = 4 * GR * WPg * sizeof(float);
     const dim3 grid(cdiv(units, 4));
     const bool odd = g.pl & 1;
-    if (g.K == 3 && !odd)
-      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<3, 0>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
-    else if (g.K == 3)
-      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<3, 1>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
-    else if (!odd)
-      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<5, 0>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
-    else
-      hipLaunchKernelGGL((k_dw_dgrad_s2_strip<5, 1>), grid, dim3(256), shm, as_stream(stream), gy, w, g, RO, GR, WPg, upp, units, dx);
+#define DWS2(KV, PV, BV)                                                                           \
+  hipLaunchKernelGGL((k_dw_dgrad_s2_strip<KV, PV, BV>), grid, dim3(256), shm, as_stream(stream),      \
+                     static_cast<const dw_to<BV> *>(gy), w, g, RO, GR, WPg, upp, units,             \
+                     static_cast<dw_to<BV> *>(dx))
+    if (g.K == 3 && !odd) { if (io) DWS2(3, 0, true); else DWS2(3, 0, false); }
+    else if (g.K == 3) { if (io) DWS2(3, 1, true); else DWS2(3, 1, false); }
+    else if (!odd) { if (io) DWS2(5, 0, true); else DWS2(5, 0, false); }
+    else { if (io) DWS2(5, 1, true); else DWS2(5, 1, false); }
+#undef DWS2
     return launch_status("e2ep_dwconv_dgrad");
   }
+  E2EP_REQUIRE(io == 0, E2EP_EINVAL, "e2ep_dwconv_dgrad: bf16 storage needs the strip kernels");
   E2EP_REQUIRE(g.N * g.C <= 65535, E2EP_ERANGE, "e2ep_dwconv_dgrad: N*C > 65535");
-  DW_DISPATCH(k_dw_dgrad, dim3(cdiv(g.H * g.W, 256), g.N * g.C), gy, w, g, dx);
+  DW_DISPATCH(k_dw_dgrad, dim3(cdiv(g.H * g.W, 256), g.N * g.C), static_cast<const float *>(gy), w, g,
+              static_cast<float *>(dx));
   return launch_status("e2ep_dwconv_dgrad");
 }
 
@@ -938,10 +979,13 @@ size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
   return (size_t)g.C * dw_wgrad_splits(g) * g.K * g.K * sizeof(float);
 }
 
-int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
+int e2ep_dwconv_wgrad(const void *gy, const float *x, const int *dims, const float *in_scale,
                       const float *in_shift, int in_act, void *workspace, size_t workspace_bytes,
-                      float *dw, void *stream) {
+                      float *dw, void *stream, int io) {
   DwGeom g = dw_geom(dims);
+  E2EP_REQUIRE(io == 0 || (io == E2EP_IO_DY_BF16 && dw_wgrad_strip_ok(g)), E2EP_EINVAL,
+               "e2ep_dwconv_wgrad: storage mask %d not supported (0, or gy bf16 on the strip "
+               "kernels)", io);
   E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_dwconv_wgrad_workspace(dims), E2EP_EINVAL,
                "e2ep_dwconv_wgrad: workspace %zu bytes < %zu (e2ep_dwconv_wgrad_workspace)",
                workspace_bytes, e2ep_dwconv_wgrad_workspace(dims));
@@ -956,10 +1000,15 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
               (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C, as_stream(stream)) : nullptr};
   if (dw_wgrad_strip_ok(g)) {
     const DwStrip d = dw_strip(g.K, g.st, g.W, g.P, g.Q);
-    DW_STRIP_DISPATCH(dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
-                      sp, part, tf);
+    if (io)
+      DW_STRIP_DISPATCH(dw_wgrad_strip, DW_B16, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d, sp,
+                        part, tf);
+    else
+      DW_STRIP_DISPATCH(dw_wgrad_strip, DW_NONE, dim3(g.C, sp), 4 * d.IR * d.WP * 4, gy, x, g, d,
+                        sp, part, tf);
   } else {
-    DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), gy, x, g, sp, part, in_scale, in_shift, in_act);
+    DW_DISPATCH(k_dw_wgrad, dim3(g.C, sp), static_cast<const float *>(gy), x, g, sp, part, in_scale,
+                in_shift, in_act);
   }
   if (sp > 1 && !part.cnt)
     hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0,
@@ -967,9 +1016,12 @@ int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const fl
   return launch_status("e2ep_dwconv_wgrad");
 }
 
-int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *dims,
-                    const float *in_scale, const float *in_shift, int in_act, float *dx,
-                    void *workspace, size_t workspace_bytes, float *dw, void *stream) {
+int e2ep_dwconv_bwd(const void *gy, const float *x, const float *w, const int *dims,
+                    const float *in_scale, const float *in_shift, int in_act, void *dx,
+                    void *workspace, size_t workspace_bytes, float *dw, void *stream, int io) {
+  E2EP_REQUIRE(io == 0 || io == (E2EP_IO_DY_BF16 | E2EP_IO_DX_BF16), E2EP_EINVAL,
+               "e2ep_dwconv_bwd: storage mask %d not supported (0 or DY|DX bf16)", io);
+  const bool hb = io != 0;
   const DwGeom g = dw_geom(dims);
   DwGeom t;
   int off;
@@ -994,14 +1046,16 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
                 (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C, s) : nullptr};
     const size_t shm = 4 * (size_t)std::max(p2.GR * p2.WPg, d.IR * d.WP) * 4;
     const dim3 grid(g.C * sp + cdiv(p2.units, 4));
+#define DWP2B(KV, PLPV, OFFV, VWV, BV)                                                             \
+  hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, VWV, BV>), grid, dim3(256), shm, s,         \
+                     static_cast<const dw_to<BV> *>(gy), w, p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, \
+                     static_cast<dw_to<BV> *>(dx), x, g, d, sp, part, tf)
 #define DWP2(KV, PLPV, OFFV)                                                                       \
   do {                                                                                             \
-    if (vw == 2)                                                                                   \
-      hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, 2>), grid, dim3(256), shm, s, gy, w,    \
-                         p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf);       \
-    else                                                                                           \
-      hipLaunchKernelGGL((k_dw_bwd_pair_s2<KV, PLPV, OFFV, DW_MAXV>), grid, dim3(256), shm, s, gy, \
-                         w, p2.RO, p2.GR, p2.WPg, p2.upp, p2.units, dx, x, g, d, sp, part, tf);    \
+    if (vw == 2 && hb) DWP2B(KV, PLPV, OFFV, 2, true);                                             \
+    else if (vw == 2) DWP2B(KV, PLPV, OFFV, 2, false);                                             \
+    else if (hb) DWP2B(KV, PLPV, OFFV, DW_MAXV, true);                                             \
+    else DWP2B(KV, PLPV, OFFV, DW_MAXV, false);                                                    \
   } while (0)
     // PLP = pad_left & 1, OFF = -pad_left mod 4 (dw_off)
     if (g.K == 3 && g.pl == 0) DWP2(3, 0, 0);
@@ -1009,6 +1063,7 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
     else if (g.pl == 1) DWP2(5, 1, 3);
     else DWP2(5, 0, 2);
 #undef DWP2
+#undef DWP2B
     if (sp > 1 && !part.cnt)
       hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0, s,
                          part.part, g.C, g.K * g.K, sp, dw);
@@ -1025,9 +1080,15 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
               (sp > 1 && g_tune[TUNE_SPLITK_FOLD] == 2) ? handoff_slots(g.C, s) : nullptr};
   const size_t shm = 4 * (size_t)std::max(dt.IR * dt.WP, d.IR * d.WP) * 4;
   const dim3 grid(nd + g.C * sp);
-#define DWP(KV, OFFV, VDV, VWV)                                                                   \
-  hipLaunchKernelGGL((k_dw_bwd_pair<KV, OFFV, VDV, VWV>), grid, dim3(256), shm, s, gy, w, t, dt, \
-                     units, dx, nd, x, g, d, sp, part, tf)
+#define DWPB(KV, OFFV, VDV, VWV, BV)                                                              \
+  hipLaunchKernelGGL((k_dw_bwd_pair<KV, OFFV, VDV, VWV, BV>), grid, dim3(256), shm, s,             \
+                     static_cast<const dw_to<BV> *>(gy), w, t, dt, units, static_cast<dw_to<BV> *>(dx), \
+                     nd, x, g, d, sp, part, tf)
+#define DWP(KV, OFFV, VDV, VWV)                          \
+  do {                                                   \
+    if (hb) DWPB(KV, OFFV, VDV, VWV, true);              \
+    else DWPB(KV, OFFV, VDV, VWV, false);                \
+  } while (0)
 #define DWP_V(KV, OFFV)                                  \
   do {                                                   \
     if (vd == 2 && vw == 2) DWP(KV, OFFV, 2, 2);         \
@@ -1039,6 +1100,7 @@ int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *
   else DWP_V(5, 2);
 #undef DWP_V
 #undef DWP
+#undef DWPB
   if (sp > 1 && !part.cnt)
     hipLaunchKernelGGL(k_dw_wgrad_finalize, dim3(cdiv(g.C * g.K * g.K, 256)), dim3(256), 0, s,
                        part.part, g.C, g.K * g.K, sp, dw);

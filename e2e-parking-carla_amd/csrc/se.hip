@@ -34,19 +34,20 @@ __device__ __forceinline__ float4 se_in4(float4 v, float sc, float sh, bool t) {
                      se_in(v.w, sc, sh, t));
 }
 
-// sum over one plane (HW floats, float4 when HW % 4 == 0) by one wave
-__device__ __forceinline__ float plane_sum(const float *__restrict__ p, int HW, int lane,
+// sum over one plane (HW values, 4 at a time when HW % 4 == 0) by one wave; TX = float or
+// bf16_t (bf16 activation storage, E2EP_IO_X_BF16)
+template <typename TX>
+__device__ __forceinline__ float plane_sum(const TX *__restrict__ p, int HW, int lane,
                                            float sc, float sh, bool t) {
   float s = 0.f;
   if ((HW & 3) == 0) {
     const int HW4 = HW >> 2;
-    const float4 *p4 = reinterpret_cast<const float4 *>(p);
     // SE_U loads in flight per lane (clamped, unconditional); the lane still sums i, i + 64,
     // ... in ascending order
     for (int i0 = lane; i0 < HW4; i0 += 64 * SE_U) {
       float4 v[SE_U];
 #pragma unroll
-      for (int u = 0; u < SE_U; ++u) v[u] = p4[min(i0 + u * 64, HW4 - 1)];
+      for (int u = 0; u < SE_U; ++u) v[u] = ld4(p + 4 * min(i0 + u * 64, HW4 - 1));
 #pragma unroll
       for (int u = 0; u < SE_U; ++u) {
         if (i0 + u * 64 >= HW4) break;
@@ -55,12 +56,13 @@ __device__ __forceinline__ float plane_sum(const float *__restrict__ p, int HW, 
       }
     }
   } else {
-    for (int i = lane; i < HW; i += 64) s += se_in(p[i], sc, sh, t);
+    for (int i = lane; i < HW; i += 64) s += se_in(ld1(p + i), sc, sh, t);
   }
   return wave_sum(s);
 }
 
-__global__ void __launch_bounds__(256) k_se_squeeze(const float *__restrict__ x, SeIn tf,
+template <typename TX>
+__global__ void __launch_bounds__(256) k_se_squeeze(const TX *__restrict__ x, SeIn tf,
                                                     int planes, int HW,
                                                     float *__restrict__ pooled) {
   const int pl = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -126,10 +128,11 @@ __global__ void __launch_bounds__(256) k_se_logits(const float *__restrict__ hpr
 }
 
 // y = x * sigmoid(a[plane]); float4 stream (HW % 4 == 0) or scalar
-__global__ void __launch_bounds__(256) k_se_excite(const float *__restrict__ x, SeIn tf,
+template <typename TX, typename TY = float>
+__global__ void __launch_bounds__(256) k_se_excite(const TX *__restrict__ x, SeIn tf,
                                                    const float *__restrict__ a, int HW,
                                                    long long nvec, int vec,
-                                                   float *__restrict__ y) {
+                                                   TY *__restrict__ y) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nvec) return;
   const bool t = tf.sc != nullptr;
@@ -138,11 +141,11 @@ __global__ void __launch_bounds__(256) k_se_excite(const float *__restrict__ x, 
   const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
   const float s = sigm(a[pl]);
   if (vec) {
-    float4 v = se_in4(reinterpret_cast<const float4 *>(x)[i], sc, sh, t);
+    float4 v = se_in4(ld4(x + 4 * i), sc, sh, t);
     v.x *= s; v.y *= s; v.z *= s; v.w *= s;
-    reinterpret_cast<float4 *>(y)[i] = v;
+    st4(y + 4 * i, v);
   } else {
-    y[i] = se_in(x[i], sc, sh, t) * s;
+    st1(y + i, se_in(ld1(x + i), sc, sh, t) * s);
   }
 }
 
@@ -159,9 +162,9 @@ struct SeBn {
 };
 
 // da[plane] = s (1 - s) sum_hw dy * x      (wave per plane)
-template <bool BNS>
-__global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn tf,
-                                               const float *__restrict__ dy,
+template <bool BNS, typename TX, typename TD = float>
+__global__ void __launch_bounds__(256) k_se_da(const TX *__restrict__ x, SeIn tf,
+                                               const TD *__restrict__ dy,
                                                const float *__restrict__ a, int planes, int HW,
                                                float *__restrict__ da, SeBn bn) {
   const int pl = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -177,18 +180,18 @@ __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn
     bt = bn.beta ? bn.beta[c] : 0.f;
   }
   double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
-  const float *xp = x + (size_t)pl * HW, *gp = dy + (size_t)pl * HW;
+  const TX *xp = x + (size_t)pl * HW;
+  const TD *gp = dy + (size_t)pl * HW;
   float acc = 0.f;
   if ((HW & 3) == 0) {
     const int HW4 = HW >> 2;
-    const float4 *x4 = reinterpret_cast<const float4 *>(xp), *g4 = reinterpret_cast<const float4 *>(gp);
     for (int i0 = lane; i0 < HW4; i0 += 64 * SE_U) {
       float4 xv[SE_U], gv[SE_U];
 #pragma unroll
       for (int u = 0; u < SE_U; ++u) {
         const int i = min(i0 + u * 64, HW4 - 1);
-        xv[u] = x4[i];
-        gv[u] = g4[i];
+        xv[u] = ld4(xp + 4 * i);
+        gv[u] = ld4(gp + 4 * i);
       }
 #pragma unroll
       for (int u = 0; u < SE_U; ++u) {
@@ -223,7 +226,7 @@ __global__ void __launch_bounds__(256) k_se_da(const float *__restrict__ x, SeIn
     }
   } else {
     for (int i = lane; i < HW; i += 64) {
-      const float xv = xp[i], g = gp[i];
+      const float xv = ld1(xp + i), g = ld1(gp + i);
       if constexpr (BNS) {
         const float xh = (xv - mu) * is;
         const float zb = xh * gm + bt;
@@ -375,9 +378,13 @@ using namespace e2ep;
 
 extern "C" {
 
-int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, const float *w1,
+int e2ep_se_fwd(const void *x, const float *x_scale, const float *x_shift, const float *w1,
                 const float *b1, const float *w2, const float *b2, int N, int C, int HW, int sq,
-                float *pooled, float *hpre, float *a, float *y, void *stream) {
+                float *pooled, float *hpre, float *a, void *y, void *stream, int io) {
+  E2EP_REQUIRE(io == 0 || ((io == E2EP_IO_X_BF16 || io == (E2EP_IO_X_BF16 | E2EP_IO_DX_BF16)) &&
+                           HW % 4 == 0),
+               E2EP_EINVAL, "e2ep_se_fwd: storage mask %d not supported (0, X or X|DX bf16, "
+               "HW %% 4 == 0)", io);
   E2EP_REQUIRE(N > 0 && C > 0 && HW > 0 && sq > 0, E2EP_EINVAL, "e2ep_se_fwd: bad shape");
   E2EP_REQUIRE(!x_scale == !x_shift, E2EP_EINVAL, "e2ep_se_fwd: x_scale / x_shift both or neither");
   const SeIn tf{x_scale, x_shift, C};
@@ -387,24 +394,39 @@ int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, cons
   const int planes = N * C;
   const int vec = (HW & 3) == 0;
   const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
-  hipLaunchKernelGGL(k_se_squeeze, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, planes, HW,
-                     pooled);
+  if (io)
+    hipLaunchKernelGGL(k_se_squeeze<bf16_t>, dim3(cdiv(planes, 4)), dim3(256), 0, s,
+                       static_cast<const bf16_t *>(x), tf, planes, HW, pooled);
+  else
+    hipLaunchKernelGGL(k_se_squeeze<float>, dim3(cdiv(planes, 4)), dim3(256), 0, s,
+                       static_cast<const float *>(x), tf, planes, HW, pooled);
   hipLaunchKernelGGL(k_se_hidden, dim3(N, cdiv(sq, 4)), dim3(256), 0, s, pooled, w1, b1, C, sq,
                      hpre);
   hipLaunchKernelGGL(k_se_logits, dim3(cdiv(C, SE_CT), cdiv(N, SE_NT)), dim3(256),
                      (SE_CT * (sq + 1) + SE_NT * sq) * sizeof(float), s, hpre, w2, b2, N, C, sq, a);
-  hipLaunchKernelGGL(k_se_excite, dim3(cdiv(nvec, 256)), dim3(256), 0, s, x, tf, a, HW, nvec, vec,
-                     y);
+  if (io & E2EP_IO_DX_BF16)
+    hipLaunchKernelGGL((k_se_excite<bf16_t, bf16_t>), dim3(cdiv(nvec, 256)), dim3(256), 0, s,
+                       static_cast<const bf16_t *>(x), tf, a, HW, nvec, vec, static_cast<bf16_t *>(y));
+  else if (io)
+    hipLaunchKernelGGL((k_se_excite<bf16_t, float>), dim3(cdiv(nvec, 256)), dim3(256), 0, s,
+                       static_cast<const bf16_t *>(x), tf, a, HW, nvec, vec, static_cast<float *>(y));
+  else
+    hipLaunchKernelGGL((k_se_excite<float, float>), dim3(cdiv(nvec, 256)), dim3(256), 0, s,
+                       static_cast<const float *>(x), tf, a, HW, nvec, vec, static_cast<float *>(y));
   return launch_status("e2ep_se_fwd");
 }
 
-static int se_bwd_impl(const float *x, const float *x_scale, const float *x_shift,
-                       const float *dy, const float *w1, const float *w2, const float *pooled,
+static int se_bwd_impl(const void *x, int io, const float *x_scale, const float *x_shift,
+                       const void *dy, const float *w1, const float *w2, const float *pooled,
                        const float *hpre, const float *a, int N, int C, int HW, int sq, float *dx,
                        float *dpooled_out, float *dw1, float *db1, float *dw2, float *db2,
                        float *workspace, const SeBn &bn, void *stream) {
   E2EP_REQUIRE(N > 0 && C > 0 && HW > 0 && sq > 0, E2EP_EINVAL, "e2ep_se_bwd: bad shape");
   E2EP_REQUIRE(!x_scale == !x_shift, E2EP_EINVAL, "e2ep_se_bwd: x_scale / x_shift both or neither");
+  E2EP_REQUIRE(io == 0 || ((io == E2EP_IO_X_BF16 || io == (E2EP_IO_X_BF16 | E2EP_IO_DY_BF16)) &&
+                           HW % 4 == 0 && !dx),
+               E2EP_EINVAL, "e2ep_se_bwd: storage mask %d not supported (0, X or X|DY bf16 with "
+               "dx formed by the BN backward, HW %% 4 == 0)", io);
   E2EP_REQUIRE(!(x_scale && dx), E2EP_EINVAL,
                "e2ep_se_bwd: with an input transform dx is formed by e2ep_bn_bwd (gate_logit / "
                "gate_dpooled); pass dx = NULL");
@@ -419,12 +441,27 @@ static int se_bwd_impl(const float *x, const float *x_scale, const float *x_shif
   const int spans = cdiv(C, SE_DH_SPAN);
   int KT = 1;
   while (KT < sq) KT *= 2;
-  if (bn.sums)
-    hipLaunchKernelGGL(k_se_da<true>, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes,
-                       HW, da, bn);
-  else
-    hipLaunchKernelGGL(k_se_da<false>, dim3(cdiv(planes, 4)), dim3(256), 0, s, x, tf, dy, a, planes,
-                       HW, da, bn);
+  const float *xf = static_cast<const float *>(x);
+  const bf16_t *xh = static_cast<const bf16_t *>(x);
+  const float *df = static_cast<const float *>(dy);
+  const bf16_t *dh = static_cast<const bf16_t *>(dy);
+  const dim3 gda(cdiv(planes, 4));
+  const bool hx = io & E2EP_IO_X_BF16, hd = io & E2EP_IO_DY_BF16;
+#define SE_DA(BNSV)                                                                                   \
+  do {                                                                                                \
+    if (hx && hd)                                                                                     \
+      hipLaunchKernelGGL((k_se_da<BNSV, bf16_t, bf16_t>), gda, dim3(256), 0, s, xh, tf, dh, a, planes, \
+                         HW, da, bn);                                                                 \
+    else if (hx)                                                                                      \
+      hipLaunchKernelGGL((k_se_da<BNSV, bf16_t, float>), gda, dim3(256), 0, s, xh, tf, df, a, planes, \
+                         HW, da, bn);                                                                 \
+    else                                                                                              \
+      hipLaunchKernelGGL((k_se_da<BNSV, float, float>), gda, dim3(256), 0, s, xf, tf, df, a, planes,  \
+                         HW, da, bn);                                                                 \
+  } while (0)
+  if (bn.sums) SE_DA(true);
+  else SE_DA(false);
+#undef SE_DA
   hipLaunchKernelGGL(k_se_dh, dim3(N, spans), dim3(256), 0, s, da, w2, C, sq, KT, dhp);
   hipLaunchKernelGGL(k_se_dpooled, dim3(N, cdiv(C, 256)), dim3(256), 0, s, dhp, spans, hpre, w1,
                      C, sq, dhpre, dpooled);
@@ -436,30 +473,31 @@ static int se_bwd_impl(const float *x, const float *x_scale, const float *x_shif
   if (dx) {
     const int vec = (HW & 3) == 0;
     const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
-    hipLaunchKernelGGL(k_se_dx, dim3(cdiv(nvec, 256)), dim3(256), 0, s, dy, a, dpooled, HW, nvec, vec,
-                       dx);
+    hipLaunchKernelGGL(k_se_dx, dim3(cdiv(nvec, 256)), dim3(256), 0, s, static_cast<const float *>(dy), a,
+                       dpooled, HW, nvec, vec, dx);
   }
   return launch_status("e2ep_se_bwd");
 }
 
-int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, const float *dy,
+int e2ep_se_bwd(const void *x, const float *x_scale, const float *x_shift, const void *dy,
                 const float *w1, const float *w2, const float *pooled, const float *hpre,
                 const float *a, int N, int C, int HW, int sq, float *dx, float *dpooled_out,
-                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream) {
-  return se_bwd_impl(x, x_scale, x_shift, dy, w1, w2, pooled, hpre, a, N, C, HW, sq, dx,
+                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream,
+                int io) {
+  return se_bwd_impl(x, io, x_scale, x_shift, dy, w1, w2, pooled, hpre, a, N, C, HW, sq, dx,
                      dpooled_out, dw1, db1, dw2, db2, workspace, SeBn{}, stream);
 }
 
-int e2ep_se_bwd_bn(const float *x, const float *x_scale, const float *x_shift,
+int e2ep_se_bwd_bn(const void *x, const float *x_scale, const float *x_shift,
                    const float *bn_mean, const float *bn_invstd, const float *gamma,
-                   const float *beta, const float *dy, const float *w1, const float *w2,
+                   const float *beta, const void *dy, const float *w1, const float *w2,
                    const float *pooled, const float *hpre, const float *a, int N, int C, int HW,
                    int sq, float *dpooled_out, float *dw1, float *db1, float *dw2, float *db2,
-                   double *plane_sums, float *workspace, void *stream) {
+                   double *plane_sums, float *workspace, void *stream, int io) {
   E2EP_REQUIRE(x_scale && x_shift && bn_mean && bn_invstd && dpooled_out && plane_sums,
                E2EP_EINVAL, "e2ep_se_bwd_bn: the BN transform, its statistics, dpooled_out and "
                "plane_sums are required");
-  return se_bwd_impl(x, x_scale, x_shift, dy, w1, w2, pooled, hpre, a, N, C, HW, sq, nullptr,
+  return se_bwd_impl(x, io, x_scale, x_shift, dy, w1, w2, pooled, hpre, a, N, C, HW, sq, nullptr,
                      dpooled_out, dw1, db1, dw2, db2, workspace,
                      SeBn{bn_mean, bn_invstd, gamma, beta, plane_sums}, stream);
 }

@@ -32,12 +32,12 @@ SIGNATURES = {
     "e2ep_transpose_multi": (_i, [_p, _i, _i, _p]),
     "e2ep_target_bev": (_i, [_p, _p, _i, _i, _i, _f, _f, _p, _i64, _p]),
     "e2ep_conv_fwd_workspace": (_sz, [_p]),
-    "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _sz, _p]),
+    "e2ep_conv_fwd": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _sz, _p, _i]),
     "e2ep_conv_fwd_stats_tiles": (_i, [_p, _i]),
-    "e2ep_conv_fwd_stats": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _sz, _p, _sz, _p]),
+    "e2ep_conv_fwd_stats": (_i, [_p, _p, _p, _p, _i, _i, _p, _p, _sz, _p, _sz, _p, _i]),
     "e2ep_conv_dgrad_workspace": (_sz, [_p, _i]),
     "e2ep_conv_dgrad": (_i, [_p, _p, _p, _i, _i, _p, _p, _sz, _p]),
-    "e2ep_conv_dgrad_acc": (_i, [_p, _p, _p, _i, _i, _p, _p, _p, _sz, _p]),
+    "e2ep_conv_dgrad_acc": (_i, [_p, _p, _p, _i, _i, _p, _p, _p, _sz, _p, _i]),
     "e2ep_conv_gemm_variant": (_i, [_i]),
     "e2ep_conv_split_params": (_i, [_i, _i, _i]),
     "e2ep_conv_precision": (_i, [_i]),
@@ -49,21 +49,21 @@ SIGNATURES = {
     "e2ep_conv_wgrad_kstep": (_i, [_i]),
     "e2ep_conv_wgrad_splits": (_i, [_p]),
     "e2ep_conv_wgrad_workspace": (_sz, [_p, _i]),
-    "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _sz, _p, _i, _p]),
+    "e2ep_conv_wgrad": (_i, [_p, _p, _p, _i, _p, _sz, _p, _i, _p, _i]),
     "e2ep_conv_bwd_pair_ok": (_i, [_p, _i]),
-    "e2ep_conv_bwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _sz, _i, _p, _sz, _p, _p]),
+    "e2ep_conv_bwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _sz, _i, _p, _sz, _p, _p, _i]),
     "e2ep_bias_grad": (_i, [_p, _i, _i, _i, _p, _p]),
     "e2ep_col_sum_workspace": (_sz, [_i, _i]),
     "e2ep_col_sum": (_i, [_p, _i, _i, _p, _p, _p]),
     "e2ep_skinny_gemm": (_i, [_p, _i, _i, _p, _i, _i, _p, _i, _i, _i, _p, _p]),
     "e2ep_bn_workspace": (_sz, [_i, _i, _i, _i]),
     "e2ep_bn_fwd": (_i, [_p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i, _p, _p, _p, _p, _sz, _p]),
-    "e2ep_bn_stats": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
+    "e2ep_bn_stats": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _sz, _p, _i]),
     "e2ep_bn_fwd_split": (_i, [_i, _i, _i, _i]),
     "e2ep_bn_finalize_part_workspace": (_sz, [_i, _i]),
     "e2ep_bn_finalize_part": (_i, [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
     "e2ep_bn_apply": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _i, _i, _p, _p]),
-    "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _sz, _p]),
+    "e2ep_bn_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _sz, _p, _i]),
     "e2ep_act_fwd": (_i, [_p, _i64, _i, _p, _p]),
     "e2ep_act_bwd": (_i, [_p, _p, _i64, _i, _p, _p]),
     "e2ep_cat_channels": (_i, [_p, _p, _i, _i, _i64, _p, _p]),
@@ -79,12 +79,12 @@ SIGNATURES = {
     "e2ep_resize_bwd_cl": (_i, [_p, _i64, _i, _i, _i, _i, _i, _i, _f, _f, _p, _p]),
     "e2ep_dwconv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _p, _p]),
     "e2ep_dwconv_fwd_stats_tiles": (_i, [_p]),
-    "e2ep_dwconv_fwd_stats": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _sz, _p]),
-    "e2ep_dwconv_dgrad": (_i, [_p, _p, _p, _p, _p]),
+    "e2ep_dwconv_fwd_stats": (_i, [_p, _p, _p, _p, _p, _i, _p, _p, _sz, _p, _i]),
+    "e2ep_dwconv_dgrad": (_i, [_p, _p, _p, _p, _p, _i]),
     "e2ep_dwconv_wgrad_workspace": (_sz, [_p]),
-    "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _i, _p, _sz, _p, _p]),
+    "e2ep_dwconv_wgrad": (_i, [_p, _p, _p, _p, _p, _i, _p, _sz, _p, _p, _i]),
     "e2ep_dwconv_bwd_pair_ok": (_i, [_p]),
-    "e2ep_dwconv_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _sz, _p, _p]),
+    "e2ep_dwconv_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _p, _p, _sz, _p, _p, _i]),
     "e2ep_maxpool3s2_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p]),
     "e2ep_maxpool3s2_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_avgpool_fwd": (_i, [_p, _i, _i, _p, _p]),
@@ -103,10 +103,10 @@ SIGNATURES = {
     "e2ep_softmax_c_bwd": (_i, [_p, _p, _i, _i, _i, _p, _p]),
     "e2ep_relu_dropout_fwd": (_i, [_p, _i64, _f, _p, _p, _p]),
     "e2ep_relu_dropout_bwd": (_i, [_p, _p, _i64, _f, _p, _p, _p]),
-    "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
-    "e2ep_se_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
-    "e2ep_se_bwd_bn": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
-    "e2ep_bn_bwd_planes": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p]),
+    "e2ep_se_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i]),
+    "e2ep_se_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i]),
+    "e2ep_se_bwd_bn": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i]),
+    "e2ep_bn_bwd_planes": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i]),
     "e2ep_bn_bwd_split": (_i, [_i, _i, _i, _i]),
     "e2ep_bn_eval_multi": (_i, [_p, _i, _p]),
     "e2ep_se_gate_fwd": (_i, [_p, _p, _i, _i, _p, _p]),

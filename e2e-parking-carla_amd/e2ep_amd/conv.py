@@ -122,6 +122,16 @@ def tap_major(w):
     return out
 
 
+# bf16 activation storage (e2ep.h E2EP_IO_*; nn_ops._store_bf16): a bf16 input of a conv (the
+# MBConv project conv reading the bf16-stored squeeze-excitation output, C3) is read as bf16 by
+# the bf16-operand kernels, and its data gradient is written bf16
+_IO_X, _IO_DX = 1, 4
+
+
+def _io_x(x):
+    return _IO_X if x.dtype == torch.bfloat16 else 0
+
+
 def conv_fwd(x, w, b, dims, act, y, w_layout=0, stats=None):
     """Launch the forward conv into y (handles the split-K workspace).  stats: an fp64 buffer
     for the BatchNorm partial sums of y (e2ep_conv_fwd_stats; see conv2d(bn_stats=True))."""
@@ -130,11 +140,11 @@ def conv_fwd(x, w, b, dims, act, y, w_layout=0, stats=None):
     with timing.region(_rname("conv_fwd", dims), conv_flops(dims)):
         if stats is None:
             _lib.call("e2ep_conv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
-                      _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
+                      _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream(), _io_x(x))
         else:
             _lib.call("e2ep_conv_fwd_stats", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), d, act, w_layout,
                       _lib.ptr(y), _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(stats),
-                      _lib.nbytes(stats), _lib.stream())
+                      _lib.nbytes(stats), _lib.stream(), _io_x(x))
     return y
 
 
@@ -150,12 +160,14 @@ def bn_partials(y):
 
 
 def conv_dgrad(gy, w, dims, m_channels, dx, w_layout=0, res=None):
-    """dx = data gradient (+ res, a residual gradient in dx's layout, added in the epilogue)."""
+    """dx = data gradient (+ res, a residual gradient in dx's layout, added in the epilogue);
+    a bf16 dx is written bf16."""
     d = _lib.dims(dims)
     ws = _ws(_lib.load().e2ep_conv_dgrad_workspace(d, m_channels), gy.device)
     with timing.region(_rname("conv_dgrad", dims, f"gc{m_channels}"), conv_flops(dims, m_channels)):
         _lib.call("e2ep_conv_dgrad_acc", _lib.ptr(gy), _lib.ptr(w), d, m_channels, w_layout,
-                  _lib.ptr(res), _lib.ptr(dx), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
+                  _lib.ptr(res), _lib.ptr(dx), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream(),
+                  _IO_DX if dx.dtype == torch.bfloat16 else 0)
     return dx
 
 
@@ -166,7 +178,7 @@ def conv_wgrad(gy, x, dims, dw, ws=None):
         ws = torch.empty(splits * dw.numel(), dtype=torch.float32, device=gy.device)
     with timing.region(_rname("conv_wgrad", dims), conv_flops(dims)):
         _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws), _lib.nbytes(ws),
-                  _lib.ptr(dw), 0, _lib.stream())
+                  _lib.ptr(dw), 0, _lib.stream(), _io_x(x))
     return dw
 
 
@@ -285,11 +297,11 @@ def _conv_bwd_pair(gy, x, wt, dims, gc, gskip, wshape):
     wsw = torch.empty(splits * dw.numel(), dtype=torch.float32, device=x.device)
     wsd = _ws(lib.e2ep_conv_dgrad_workspace(d, gc), gy.device)
     res = gskip.contiguous() if (gskip is not None and gc == Cin) else None
-    dxg = torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device)
+    dxg = torch.empty(N, gc, H, W, dtype=x.dtype, device=x.device)  # bf16 for a bf16-stored x
     with timing.region(_rname("conv_bwd", dims, f"gc{gc}"), conv_flops(dims, gc) + conv_flops(dims)):
         _lib.call("e2ep_conv_bwd", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(wt), d, gc, _lib.ptr(res),
                   _lib.ptr(dxg), _lib.ptr(wsd), _lib.nbytes(wsd), splits, _lib.ptr(wsw),
-                  _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream())
+                  _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream(), (_IO_X | _IO_DX) if _io_x(x) else 0)
     if gc == Cin:
         dx = dxg
     elif gskip is not None:  # channels past gc get only the skip gradient
@@ -335,7 +347,10 @@ class _Conv2d(torch.autograd.Function):
         # weight / bias gradients on the side stream, concurrent with the data gradient
         want_w, want_b = ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2]
         gc = ctx.gc or Cin
-        if want_w and ctx.needs_input_grad[0] and _CONV_PAIR[0] and \
+        # a bf16-stored x (C3 precision: the pair is then k_lp_bwd_pair) pairs without a skip
+        # gradient only
+        xb = x.dtype == torch.bfloat16
+        if want_w and ctx.needs_input_grad[0] and _CONV_PAIR[0] and (not xb or gskip is None) and \
                 _lib.load().e2ep_conv_bwd_pair_ok(_lib.dims(dims), gc):
             dx, dw = _conv_bwd_pair(gy, x, wt, dims, gc, gskip, ctx.wshape)
             if want_b:
@@ -359,7 +374,7 @@ class _Conv2d(torch.autograd.Function):
                               _lib.stream())
         if ctx.needs_input_grad[0]:
             res = gskip.contiguous() if (gskip is not None and gc == Cin) else None
-            dxg = conv_dgrad(gy, wt, dims, gc, torch.empty(N, gc, H, W, dtype=torch.float32, device=x.device),
+            dxg = conv_dgrad(gy, wt, dims, gc, torch.empty(N, gc, H, W, dtype=x.dtype, device=x.device),
                              w_layout=1, res=res)
             if gc == Cin:
                 dx = dxg

@@ -22,6 +22,34 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+# bf16 activation storage (C3, e2ep.h E2EP_IO_*): in a bf16-precision training forward the
+# MBConv depthwise output (the squeeze-excitation's input) is stored bf16, and so are the two
+# activation gradients on either side of the depthwise conv (the gradient at that output, and
+# the depthwise data gradient feeding _bn0's backward); statistics, parameters and their
+# gradients stay fp32.  E2EP_BF16_STORE=0 keeps every activation fp32 (A/B).
+_IO_X, _IO_DY, _IO_DX = 1, 2, 4
+_BF16_STORE = [os.environ.get("E2EP_BF16_STORE", "1") != "0"]
+
+
+def set_bf16_store(on):
+    """Enable / disable the bf16 activation storage of the C3 mode (returns the previous
+    setting)."""
+    prev = _BF16_STORE[0]
+    _BF16_STORE[0] = bool(on)
+    return prev
+
+
+def _store_bf16(train):
+    if not (train and _BF16_STORE[0]):
+        return False
+    from . import precision
+    return precision.get() == "bf16"
+
+
+def _is_bf16(t):
+    return t is not None and t.dtype == torch.bfloat16
+
+
 
 # ------------------------------------------------------------------------------------------
 # BatchNorm2d + activation (+ residual)
@@ -81,7 +109,8 @@ class _BnAct(torch.autograd.Function):
             _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(mean), _lib.ptr(invstd),
                       _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(res), _lib.ptr(dc_rand),
                       float(ctx.dc_keep), None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx),
-                      _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream())
+                      _lib.ptr(dg), _lib.ptr(db), _lib.ptr(dres), _lib.ptr(ws), _lib.nbytes(ws), _lib.stream(),
+                      0)
         if dres_is_dy:
             dres = dy
         return dx, dg, db, dres, None, None, None, None, None, None, None, None, None, None
@@ -358,7 +387,7 @@ class _DwConv(torch.autograd.Function):
         d = _lib.dims(dims)
         with timing.region(timing.name("dwconv_fwd", x.shape, "_DwConv")):
             _lib.call("e2ep_dwconv_fwd_stats", _lib.ptr(x), _lib.ptr(w), d, None, None, 0,
-                      _lib.ptr(y), _lib.ptr(ystats), _lib.nbytes(ystats), _lib.stream())
+                      _lib.ptr(y), _lib.ptr(ystats), _lib.nbytes(ystats), _lib.stream(), 0)
         ctx.save_for_backward(x, w)
         ctx.dims = dims
         return y
@@ -375,7 +404,7 @@ class _DwConv(torch.autograd.Function):
             ws = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
             with timing.region(timing.name("dwconv_bwd", gy.shape, "_DwConv")):
                 _lib.call("e2ep_dwconv_bwd", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(w), d, None, None, 0,
-                          _lib.ptr(dx), _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), s)
+                          _lib.ptr(dx), _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), s, 0)
             return dx, dw, None, None
         fork = None
         if ctx.needs_input_grad[1]:  # weight gradient on the side stream (conv._Fork)
@@ -385,11 +414,11 @@ class _DwConv(torch.autograd.Function):
                               work_us=conv.est_us(nbytes=4.0 * (x.numel() + gy.numel())))
             with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_DwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
-                          _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), _lib.stream())
+                          _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), _lib.stream(), 0)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             with timing.region(timing.name("dwconv_dgrad", gy.shape, "_DwConv")):
-                _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s)
+                _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s, 0)
         if fork is not None:
             fork.join()
         return dx, dw, None, None
@@ -425,12 +454,15 @@ class _BnActDwConv(torch.autograd.Function):
                 _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
                           _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
                           _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
-                          _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
-        y = torch.empty(N, C, P, Q, **f32)
+                          _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s, 0)
+        # bf16 storage of the depthwise output (C3 training, _store_bf16)
+        hb = _store_bf16(train) and (P * Q) % 4 == 0
+        y = torch.empty(N, C, P, Q, dtype=torch.bfloat16 if hb else torch.float32, device=x.device)
         d = _lib.dims(dims)
         with timing.region(timing.name("dwconv_fwd", x.shape, "_BnActDwConv")):
             _lib.call("e2ep_dwconv_fwd_stats", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(stats[2]),
-                      _lib.ptr(stats[3]), act, _lib.ptr(y), _lib.ptr(ystats), _lib.nbytes(ystats), s)
+                      _lib.ptr(stats[3]), act, _lib.ptr(y), _lib.ptr(ystats), _lib.nbytes(ystats), s,
+                      _IO_DX if hb else 0)
         ctx.save_for_backward(x, gamma, beta, w, stats)
         ctx.dims, ctx.train, ctx.act = dims, train, act
         return y
@@ -447,14 +479,19 @@ class _BnActDwConv(torch.autograd.Function):
         fork = None
         want_t = nig[0] or nig[1] or nig[2]
         paired = nig[9] and want_t and _dw_pairable(d)
+        # bf16 storage: the incoming gradient (at the stored bf16 output) is bf16, and so is the
+        # data gradient handed to the BN backward
+        hb = _is_bf16(gy)
+        tdt = torch.bfloat16 if hb else torch.float32
         if paired:  # both gradients in one launch
             dw = torch.empty_like(w)
-            dt = torch.empty_like(x)  # gradient at the activation output
+            dt = torch.empty(x.shape, dtype=tdt, device=x.device)  # gradient at the activation output
             wsw = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
             with timing.region(timing.name("dwconv_bwd", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_bwd", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(w), d,
                           _lib.ptr(stats[2]), _lib.ptr(stats[3]), ctx.act, _lib.ptr(dt),
-                          _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), s)
+                          _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), s,
+                          (_IO_DY | _IO_DX) if hb else 0)
         elif nig[9]:  # weight gradient on the side stream (conv._Fork)
             dw = torch.empty_like(w)
             wsw = _ws(_lib.load().e2ep_dwconv_wgrad_workspace(d), x.device)
@@ -462,12 +499,14 @@ class _BnActDwConv(torch.autograd.Function):
                               work_us=conv.est_us(nbytes=4.0 * (x.numel() + gy.numel())))
             with fork, timing.region(timing.name("dwconv_wgrad", gy.shape, "_BnActDwConv")):
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, _lib.ptr(stats[2]),
-                          _lib.ptr(stats[3]), ctx.act, _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream())
+                          _lib.ptr(stats[3]), ctx.act, _lib.ptr(wsw), _lib.nbytes(wsw), _lib.ptr(dw), _lib.stream(),
+                          _IO_DY if hb else 0)
         if want_t:
             if not paired:
-                dt = torch.empty_like(x)  # gradient at the activation output
+                dt = torch.empty(x.shape, dtype=tdt, device=x.device)  # gradient at the activation output
                 with timing.region(timing.name("dwconv_dgrad", gy.shape, "_BnActDwConv")):
-                    _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s)
+                    _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dt), s,
+                              (_IO_DY | _IO_DX) if hb else 0)
             dx = torch.empty_like(x) if nig[0] else None
             dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
             db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
@@ -476,7 +515,7 @@ class _BnActDwConv(torch.autograd.Function):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dt), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           None, None, N, C, H, W, int(ctx.train), ctx.act, _lib.ptr(dx), _lib.ptr(dg),
-                          _lib.ptr(db), None, _lib.ptr(ws), _lib.nbytes(ws), s)
+                          _lib.ptr(db), None, _lib.ptr(ws), _lib.nbytes(ws), s, _IO_DY if hb else 0)
         if fork is not None:
             fork.join()
         return dx, dg, db, None, None, None, None, None, None, dw, None, None, None, None, None
@@ -640,7 +679,7 @@ class _SqueezeExcite(torch.autograd.Function):
         with timing.region(timing.name("se_fwd", x.shape, "_SqueezeExcite")):
             _lib.call("e2ep_se_fwd", _lib.ptr(x), None, None, _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c),
                       _lib.ptr(b2), N, C, H * W, sq, _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a),
-                      _lib.ptr(y), _lib.stream())
+                      _lib.ptr(y), _lib.stream(), 0)
         ctx.save_for_backward(x, w1c, w2c, pooled, hpre, a)
         ctx.shapes = (w1.shape, w2.shape, b1 is not None, b2 is not None)
         return y
@@ -663,7 +702,7 @@ class _SqueezeExcite(torch.autograd.Function):
             _lib.call("e2ep_se_bwd", _lib.ptr(x), None, None, _lib.ptr(dy.contiguous()),
                       _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a),
                       N, C, H * W, sq, _lib.ptr(dx), None, _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2),
-                      _lib.ptr(ws), _lib.stream())
+                      _lib.ptr(ws), _lib.stream(), 0)
         return dx, dw1, db1, dw2, db2
 
 
@@ -709,14 +748,19 @@ class _BnSwishSE(torch.autograd.Function):
                 _lib.call("e2ep_bn_stats", _lib.ptr(x), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm),
                           _lib.ptr(rv), N, C, H, W, int(train), float(momentum), float(eps),
                           _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
-                          _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s)
+                          _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s,
+                          _IO_X if _is_bf16(x) else 0)
         pooled, hpre, a = torch.empty(N, C, **f32), torch.empty(N, sq, **f32), torch.empty(N, C, **f32)
-        y = torch.empty_like(x)
+        # a bf16-stored input (bf16 storage, _store_bf16): the output — the project conv's input
+        # — is stored bf16 too
+        hb = _is_bf16(x)
+        y = torch.empty(x.shape, dtype=x.dtype, device=dev)
         w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
         with timing.region(timing.name("se_fwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_se_fwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
                       _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c), _lib.ptr(b2), N, C, H * W, sq,
-                      _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), _lib.ptr(y), s)
+                      _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), _lib.ptr(y), s,
+                      (_IO_X | _IO_DX) if hb else 0)
         ctx.save_for_backward(x, gamma, beta, stats, w1c, w2c, pooled, hpre, a)
         ctx.shapes = (w1.shape, w2.shape, b1 is not None, b2 is not None)
         ctx.train = train
@@ -739,9 +783,12 @@ class _BnSwishSE(torch.autograd.Function):
         db2 = torch.empty(C, **f32) if (hb2 and nig[11]) else None
         dpooled = torch.empty(N, C, **f32)
         ws = torch.empty(2 * N * C + 17 * N * sq, **f32)
-        dx = torch.empty_like(x) if nig[0] else None
+        dx = torch.empty_like(x) if nig[0] else None  # bf16 with a bf16-stored x
         dg = torch.empty_like(gamma) if (gamma is not None and nig[1]) else None
         db = torch.empty_like(beta) if (beta is not None and nig[2]) else None
+        hb = _is_bf16(x)
+        # storage of the incoming gradient (bf16 at a bf16-stored output)
+        io_in = (_IO_X | (_IO_DY if _is_bf16(dy) else 0)) if hb else 0
         # training BN on the split path: its channel sums are taken in the SE's da pass
         # (e2ep_se_bwd_bn), so the BN backward is its apply pass alone
         fused = (_SE_BN_SUMS[0] and ctx.train and dx is not None
@@ -754,25 +801,27 @@ class _BnSwishSE(torch.autograd.Function):
                           _lib.ptr(dy), _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled),
                           _lib.ptr(hpre), _lib.ptr(a), N, C, H * W, sq, _lib.ptr(dpooled),
                           _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2),
-                          _lib.ptr(planes), _lib.ptr(ws), s)
+                          _lib.ptr(planes), _lib.ptr(ws), s, io_in)
             with timing.region(timing.name("bn_bwd", x.shape, "_BnSwishSE")):
                 _lib.call("e2ep_bn_bwd_planes", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(a),
                           _lib.ptr(dpooled), _lib.ptr(planes), N, C, H, W, ACT["swish"],
-                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), s)
+                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), s, (io_in | _IO_DX) if hb else 0)
             return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None, None
         with timing.region(timing.name("se_bwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_se_bwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
                       _lib.ptr(dy), _lib.ptr(w1c), _lib.ptr(w2c), _lib.ptr(pooled),
                       _lib.ptr(hpre), _lib.ptr(a), N, C, H * W, sq, None, _lib.ptr(dpooled),
-                      _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2), _lib.ptr(ws), s)
+                      _lib.ptr(dw1), _lib.ptr(db1), _lib.ptr(dw2), _lib.ptr(db2), _lib.ptr(ws), s,
+                      io_in)
         if dx is not None or dg is not None or db is not None:
             bws = _ws(_lib.load().e2ep_bn_workspace(N, C, H, W), dev)
             with timing.region(timing.name("bn_bwd", x.shape, "_BnSwishSE")):
                 _lib.call("e2ep_bn_bwd", _lib.ptr(x), _lib.ptr(dy), _lib.ptr(stats[0]),
                           _lib.ptr(stats[1]), _lib.ptr(gamma), _lib.ptr(beta), None, None, 1.0,
                           _lib.ptr(a), _lib.ptr(dpooled), N, C, H, W, int(ctx.train), ACT["swish"],
-                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), None, _lib.ptr(bws), _lib.nbytes(bws), s)
+                          _lib.ptr(dx), _lib.ptr(dg), _lib.ptr(db), None, _lib.ptr(bws), _lib.nbytes(bws), s,
+                          (io_in | _IO_DX) if hb else 0)
         return dx, dg, db, None, None, None, None, None, dw1, db1, dw2, db2, None, None, None
 
 

@@ -29,6 +29,16 @@ extern "C" {
 int e2ep_abi_version(void);
 const char *e2ep_last_error(void);
 
+/* bf16 activation storage (ABI 3; BASELINE C3, the bf16 training mode): the entry points that
+ * take an `io` mask read / write the named tensors as bf16 (torch.bfloat16 bits) instead of
+ * fp32; their pointers are then void*.  The arithmetic stays fp32: a bf16 element is widened on
+ * load, a stored value is rounded to nearest-even, and statistics / gradients of parameters /
+ * partial sums stay fp32 / fp64.  io = 0 is the fp32 behaviour of ABI 2.  Each entry point
+ * lists the masks it supports (others: E2EP_EINVAL); every bf16 tensor needs H*W % 4 == 0. */
+#define E2EP_IO_X_BF16 1  /* the input activation x (a depthwise strip kernel's input plane) */
+#define E2EP_IO_DY_BF16 2 /* the incoming gradient dy / gy */
+#define E2EP_IO_DX_BF16 4 /* the produced tensor: y of a forward, dx of a backward */
+
 /* ---------------------------------------------------------------------------------------
  * Lift-splat
  * ------------------------------------------------------------------------------------- */
@@ -151,8 +161,11 @@ int e2ep_target_bev(const float *target_point, const float *noise, int B, int X,
  * Grids that cannot fill the chip split K; the partial sums then need a workspace of
  * e2ep_conv_fwd_workspace bytes (0 = none needed; pass NULL) and are reduced in fixed order. */
 size_t e2ep_conv_fwd_workspace(const int *dims);
-int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *dims, int act,
-                  int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream);
+/* io: 0, or E2EP_IO_X_BF16 (x bf16: C3's bf16-stored squeeze-excitation output as the MBConv
+ * project conv's input; the bf16-operand kernels only, precision 1). */
+int e2ep_conv_fwd(const void *x, const float *w, const float *bias, const int *dims, int act,
+                  int w_layout, float *y, void *workspace, size_t workspace_bytes, void *stream,
+                  int io);
 /* e2ep_conv_fwd plus the batch statistics of y for the BatchNorm that follows the conv
  * (MBConv _expand_conv -> _bn0, _project_conv -> _bn2; reference model/cam_encoder.py:69-82
  * via efficientnet-pytorch): the epilogue writes, per output channel c and column tile t
@@ -162,9 +175,9 @@ int e2ep_conv_fwd(const float *x, const float *w, const float *bias, const int *
  * w_layout), which is 0 when the geometry's kernel takes no statistics (then stats must be
  * NULL and the BN computes its own); stats_bytes >= Cout * tiles * 16.  Deterministic. */
 int e2ep_conv_fwd_stats_tiles(const int *dims, int w_layout);
-int e2ep_conv_fwd_stats(const float *x, const float *w, const float *bias, const int *dims, int act,
+int e2ep_conv_fwd_stats(const void *x, const float *w, const float *bias, const int *dims, int act,
                         int w_layout, float *y, void *workspace, size_t workspace_bytes,
-                        double *stats, size_t stats_bytes, void *stream);
+                        double *stats, size_t stats_bytes, void *stream, int io /* as e2ep_conv_fwd */);
 
 /* dx[N,m_channels,H,W] = conv_transpose(gout[N,Cout,P,Q], w) restricted to the first
  * m_channels input channels; split by input-pixel stride phase, so no zero taps at stride 2.
@@ -176,9 +189,11 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
  * epilogue: dx = conv_transpose(gout, w) + res.  The skip connection around a block whose
  * first conv reads the block input (MBConv expand conv, ResNet BasicBlock conv1) gets its
  * input gradient in one pass instead of dgrad + an autograd accumulation add. */
+/* io: 0, or E2EP_IO_DX_BF16 (dx written bf16 — the gradient at a bf16-stored input; the
+ * bf16-operand kernels with the in-launch split-K fold; res stays fp32). */
 int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int m_channels,
-                        int w_layout, const float *res, float *dx, void *workspace,
-                        size_t workspace_bytes, void *stream);
+                        int w_layout, const float *res, void *dx, void *workspace,
+                        size_t workspace_bytes, void *stream, int io);
 
 /* A conv layer's backward in one launch: dx (e2ep_conv_dgrad_acc with res, w tap-major) and
  * dw (e2ep_conv_wgrad with `wsplits`, accumulate 0), their blocks sharing one grid instead of
@@ -191,10 +206,11 @@ int e2ep_conv_dgrad_acc(const float *gout, const float *w, const int *dims, int 
  * launches the two separately.  Workspaces: e2ep_conv_dgrad_workspace(dims, m_channels),
  * e2ep_conv_wgrad_workspace(dims, wsplits).  Results bitwise those of the two launches. */
 int e2ep_conv_bwd_pair_ok(const int *dims, int m_channels);
-int e2ep_conv_bwd(const float *gout, const float *x, const float *w, const int *dims,
-                  int m_channels, const float *res, float *dx, void *ws_dgrad,
+int e2ep_conv_bwd(const float *gout, const void *x, const float *w, const int *dims,
+                  int m_channels, const float *res, void *dx, void *ws_dgrad,
                   size_t ws_dgrad_bytes, int wsplits, void *ws_wgrad, size_t ws_wgrad_bytes,
-                  float *dw, void *stream);
+                  float *dw, void *stream,
+                  int io /* 0, or X|DX bf16 on the C3 k_lp_bwd_pair without res */);
 
 /* dw[Cout,Cin,R,S] (=, or += when accumulate) = sum over pixels of gout x im2col(x).
  * The pixel reduction is split over `splits` workgroups; partial slabs (workspace of
@@ -226,9 +242,9 @@ int e2ep_conv_precision(int precision);
 int e2ep_conv_wgrad_kstep(int pixels);
 int e2ep_conv_wgrad_splits(const int *dims);
 size_t e2ep_conv_wgrad_workspace(const int *dims, int splits);
-int e2ep_conv_wgrad(const float *gout, const float *x, const int *dims, int splits,
+int e2ep_conv_wgrad(const float *gout, const void *x, const int *dims, int splits,
                     void *workspace, size_t workspace_bytes, float *dw, int accumulate,
-                    void *stream);
+                    void *stream, int io /* 0, or E2EP_IO_X_BF16 on k_wgrad_lp (C3) */);
 
 /* db[C] = sum over (n, p) of gout[N, C, HW]. */
 int e2ep_bias_grad(const float *gout, int N, int C, int HW, float *db, void *stream);
@@ -267,10 +283,11 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
  * consumer that applies the normalisation on load (e2ep_dwconv_fwd / _wgrad in_scale,
  * in_shift): writes mean / invstd [C] and the folded affine scale = gamma * invstd,
  * shift = beta - mean * scale [C].  The backward is e2ep_bn_bwd on the same x. */
-int e2ep_bn_stats(const float *x, const float *gamma, const float *beta, float *running_mean,
+int e2ep_bn_stats(const void *x, const float *gamma, const float *beta, float *running_mean,
                   float *running_var, int N, int C, int H, int W, int train, float momentum,
                   float eps, float *mean, float *invstd, float *scale, float *shift,
-                  void *workspace, size_t workspace_bytes, void *stream);
+                  void *workspace, size_t workspace_bytes, void *stream,
+                  int io /* 0 or E2EP_IO_X_BF16 */);
 /* 1 when the training forward of this shape takes the split path (a statistics pass over x,
  * then the elementwise pass), 0 when it runs the single-launch kernel that keeps each channel
  * in registers — where a producer's partial sums (e2ep_conv_fwd_stats) save nothing. */
@@ -297,11 +314,12 @@ int e2ep_bn_apply(const float *x, const float *scale, const float *shift, const 
  * gate_logit / gate_dpooled [N,C] (both or neither): the activation output fed a
  * squeeze-excitation gate (e2ep_se_fwd with x_scale / x_shift), so the gradient at it is
  * dy * sigmoid(gate_logit) + gate_dpooled / (H*W), formed on the fly from the gate's dy. */
-int e2ep_bn_bwd(const float *x, const float *dy, const float *mean, const float *invstd,
+int e2ep_bn_bwd(const void *x, const void *dy, const float *mean, const float *invstd,
                 const float *gamma, const float *beta, const float *res, const float *dc_rand,
                 float dc_keep, const float *gate_logit, const float *gate_dpooled, int N, int C,
-                int H, int W, int train, int act, float *dx, float *dgamma, float *dbeta,
-                float *dres, void *workspace, size_t workspace_bytes, void *stream);
+                int H, int W, int train, int act, void *dx, float *dgamma, float *dbeta,
+                float *dres, void *workspace, size_t workspace_bytes, void *stream,
+                int io /* 0, X|DX or X|DY|DX (the depthwise output's _bn1) or DY (_bn0) */);
 /* 1 when e2ep_bn_bwd runs this shape as the split reduce + apply pair (a channel of more
  * than 8192 elements, or the single-launch kernels switched off), 0 for the single launch. */
 int e2ep_bn_bwd_split(int N, int C, int H, int W);
@@ -309,10 +327,11 @@ int e2ep_bn_bwd_split(int N, int C, int H, int W);
  * sums come from e2ep_se_bwd_bn's per-plane factors instead of a reduction pass over x and dy:
  * sum dzb = sum_n sigmoid(logit) A1 + dpooled / HW A2, sum dzb xhat = ... A3 / A4 (fp64).
  * Same arguments and element arithmetic as e2ep_bn_bwd; no workspace. */
-int e2ep_bn_bwd_planes(const float *x, const float *dy, const float *mean, const float *invstd,
+int e2ep_bn_bwd_planes(const void *x, const void *dy, const float *mean, const float *invstd,
                        const float *gamma, const float *beta, const float *gate_logit,
                        const float *gate_dpooled, const double *plane_sums, int N, int C, int H,
-                       int W, int act, float *dx, float *dgamma, float *dbeta, void *stream);
+                       int W, int act, void *dx, float *dgamma, float *dbeta, void *stream,
+                       int io /* 0, X|DX or X|DY|DX */);
 /* Eval-mode statistics of n BatchNorm layers in one launch (the per-layer e2ep_bn_stats calls
  * of an inference forward, 42 launches of C5 predict): table = DEVICE array of n rows of 7
  * int64 {running_mean, running_var, gamma (nullable), beta (nullable), out, C, eps as fp32
@@ -371,25 +390,28 @@ int e2ep_add_i64_multi(const long long *table, int n, long long v, void *stream)
  * then the backward leaves dx to e2ep_bn_bwd (pass dx = NULL, dpooled_out [N,C], and hand a
  * and dpooled_out to e2ep_bn_bwd as gate_logit / gate_dpooled).
  * ------------------------------------------------------------------------------------- */
-int e2ep_se_fwd(const float *x, const float *x_scale, const float *x_shift, const float *w1,
+int e2ep_se_fwd(const void *x, const float *x_scale, const float *x_shift, const float *w1,
                 const float *b1, const float *w2, const float *b2, int N, int C, int HW, int sq,
-                float *pooled, float *hpre, float *a, float *y, void *stream);
-int e2ep_se_bwd(const float *x, const float *x_scale, const float *x_shift, const float *dy,
+                float *pooled, float *hpre, float *a, void *y, void *stream,
+                int io /* 0, E2EP_IO_X_BF16 or X|DX (y bf16 too) */);
+int e2ep_se_bwd(const void *x, const float *x_scale, const float *x_shift, const void *dy,
                 const float *w1, const float *w2, const float *pooled, const float *hpre,
                 const float *a, int N, int C, int HW, int sq, float *dx, float *dpooled_out,
-                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream);
+                float *dw1, float *db1, float *dw2, float *db2, float *workspace, void *stream,
+                int io /* 0, X or X|DY bf16 (dx = NULL: formed by the BN backward) */);
 /* e2ep_se_bwd (x_scale / x_shift transform, dx left to the BN) that also takes the block's
  * _bn1 backward sums in its da pass over x and dy (MBConv _bn1 -> swish -> SE, reference
  * model/cam_encoder.py:69-73): with xhat = (x - bn_mean) bn_invstd and sp = swish'(xhat gamma +
  * beta), plane_sums [N*C][4] (fp64) = (sum dy sp, sum sp, sum dy sp xhat, sum sp xhat) per
  * (n, c) plane, for e2ep_bn_bwd_planes (which then skips e2ep_bn_bwd's reduction pass).
  * gamma / beta nullable (1 / 0). */
-int e2ep_se_bwd_bn(const float *x, const float *x_scale, const float *x_shift,
+int e2ep_se_bwd_bn(const void *x, const float *x_scale, const float *x_shift,
                    const float *bn_mean, const float *bn_invstd, const float *gamma,
-                   const float *beta, const float *dy, const float *w1, const float *w2,
+                   const float *beta, const void *dy, const float *w1, const float *w2,
                    const float *pooled, const float *hpre, const float *a, int N, int C, int HW,
                    int sq, float *dpooled_out, float *dw1, float *db1, float *dw2, float *db2,
-                   double *plane_sums, float *workspace, void *stream);
+                   double *plane_sums, float *workspace, void *stream,
+                   int io /* 0, X or X|DY bf16 */);
 
 /* ---------------------------------------------------------------------------------------
  * Residual add + dropout + LayerNorm of the post-norm transformer layers (torch
@@ -506,10 +528,14 @@ int e2ep_dwconv_fwd(const float *x, const float *w, const int *dims, const float
  * (e2ep_bn_finalize_part's input).  tiles = e2ep_dwconv_fwd_stats_tiles(dims), 0 when the
  * geometry runs the generic kernel (then stats must be NULL); stats_bytes >= C * tiles * 16. */
 int e2ep_dwconv_fwd_stats_tiles(const int *dims);
+/* io: 0, or E2EP_IO_DX_BF16 (y stored bf16 — C3's depthwise output; x stays fp32; the statistics
+ * are those of the stored bf16 values).  The bf16 forms run on the strip kernels only. */
 int e2ep_dwconv_fwd_stats(const float *x, const float *w, const int *dims, const float *in_scale,
-                          const float *in_shift, int in_act, float *y, double *stats,
-                          size_t stats_bytes, void *stream);
-int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *dx, void *stream);
+                          const float *in_shift, int in_act, void *y, double *stats,
+                          size_t stats_bytes, void *stream, int io);
+/* io: 0, or E2EP_IO_DY_BF16 | E2EP_IO_DX_BF16 (gy and dx bf16) */
+int e2ep_dwconv_dgrad(const void *gy, const float *w, const int *dims, void *dx, void *stream,
+                      int io);
 /* A stride-1 depthwise layer's backward in one launch (k_dw_bwd_pair): dx as
  * e2ep_dwconv_dgrad, dw as e2ep_dwconv_wgrad (in_scale / in_shift / in_act: the input
  * transform of the weight gradient's x, as there), their blocks sharing one grid instead of
@@ -517,13 +543,14 @@ int e2ep_dwconv_dgrad(const float *gy, const float *w, const int *dims, float *d
  * two separately.  Workspace: e2ep_dwconv_wgrad_workspace.  Results bitwise those of the two
  * separate launches. */
 int e2ep_dwconv_bwd_pair_ok(const int *dims);
-int e2ep_dwconv_bwd(const float *gy, const float *x, const float *w, const int *dims,
-                    const float *in_scale, const float *in_shift, int in_act, float *dx,
-                    void *workspace, size_t workspace_bytes, float *dw, void *stream);
+int e2ep_dwconv_bwd(const void *gy, const float *x, const float *w, const int *dims,
+                    const float *in_scale, const float *in_shift, int in_act, void *dx,
+                    void *workspace, size_t workspace_bytes, float *dw, void *stream,
+                    int io /* 0 or E2EP_IO_DY_BF16 | E2EP_IO_DX_BF16 (x stays fp32) */);
 size_t e2ep_dwconv_wgrad_workspace(const int *dims);
-int e2ep_dwconv_wgrad(const float *gy, const float *x, const int *dims, const float *in_scale,
+int e2ep_dwconv_wgrad(const void *gy, const float *x, const int *dims, const float *in_scale,
                       const float *in_shift, int in_act, void *workspace, size_t workspace_bytes,
-                      float *dw, void *stream);
+                      float *dw, void *stream, int io /* 0 or E2EP_IO_DY_BF16 */);
 
 /* ---------------------------------------------------------------------------------------
  * Pooling and squeeze-excitation gating.

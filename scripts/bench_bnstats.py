@@ -55,7 +55,7 @@ def main():
         def bn_stats():
             _lib.call("e2ep_bn_stats", _lib.ptr(y), _lib.ptr(g), _lib.ptr(b), None, None, N, Cout, H, W,
                       1, 0.1, 1e-3, _lib.ptr(out[0]), _lib.ptr(out[1]), _lib.ptr(out[2]),
-                      _lib.ptr(out[3]), _lib.ptr(bws), _lib.nbytes(bws), _lib.stream())
+                      _lib.ptr(out[3]), _lib.ptr(bws), _lib.nbytes(bws), _lib.stream(), 0)
         bst = timed(bn_stats)
         fin = 0.0
         if tiles:
@@ -84,7 +84,7 @@ def main():
 
         def run(stats):
             _lib.call("e2ep_dwconv_fwd_stats", _lib.ptr(x), _lib.ptr(w), d, None, None, 0, _lib.ptr(y),
-                      _lib.ptr(stats), _lib.nbytes(stats) if stats is not None else 0, _lib.stream())
+                      _lib.ptr(stats), _lib.nbytes(stats) if stats is not None else 0, _lib.stream(), 0)
         plain = timed(lambda: run(None))
         withs = timed(lambda: run(st)) if tiles else 0.0
         print(f"  {(N, C, H, W, K, st_)}: {plain:7.1f} / {withs:7.1f} ({withs - plain:+6.1f})  tiles {tiles}")

@@ -62,11 +62,11 @@ def main():
                           _lib.ptr(y), s())
 
             def dgr():
-                _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s())
+                _lib.call("e2ep_dwconv_dgrad", _lib.ptr(gy), _lib.ptr(w), d, _lib.ptr(dx), s(), 0)
 
             def wgr():
                 _lib.call("e2ep_dwconv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, None, None, 0,
-                          _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), s())
+                          _lib.ptr(ws), _lib.nbytes(ws), _lib.ptr(dw), s(), 0)
 
             us = {"fwd": timed(fwd, 20), "dgrad": timed(dgr, 20), "wgrad": timed(wgr, 20)}
             mb = 4 * N * C * (H * H + P * P) / 1e6

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(lib, name), name
     assert set(_declared()) <= set(_lib.SIGNATURES), "ctypes table misses a declared entry point"
-    assert lib.e2ep_abi_version() == 2
+    assert lib.e2ep_abi_version() == 3
 
 
 def test_library_is_gfx950_code_object():

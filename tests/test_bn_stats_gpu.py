@@ -104,7 +104,7 @@ def test_stats_tiles_zero_where_the_kernel_takes_none():
     st = torch.empty(4096, dtype=torch.float64, device=DEV)
     with pytest.raises(_lib.E2EPError):
         _lib.call("e2ep_conv_fwd_stats", _lib.ptr(x), _lib.ptr(w), None, _lib.dims(d), 0, 1,
-                  _lib.ptr(y), None, 0, _lib.ptr(st), _lib.nbytes(st), _lib.stream())
+                  _lib.ptr(y), None, 0, _lib.ptr(st), _lib.nbytes(st), _lib.stream(), 0)
 
 
 @pytest.mark.parametrize("fused", ["bn_act", "bn_act_res_dc", "bn_act_depthwise"])

@@ -248,7 +248,7 @@ def test_short_workspace_is_rejected():
     dw, ws = torch.empty(64, 64, 3, 3, device=DEV), torch.empty(nb // 4, device=DEV)
     with pytest.raises(_lib.E2EPError, match="workspace"):
         _lib.call("e2ep_conv_wgrad", _lib.ptr(gy), _lib.ptr(x), d, splits, _lib.ptr(ws), nb - 4,
-                  _lib.ptr(dw), 0, _lib.stream())
+                  _lib.ptr(dw), 0, _lib.stream(), 0)
     torch.cuda.synchronize()
 
 
