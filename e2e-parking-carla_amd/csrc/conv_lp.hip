@@ -28,6 +28,12 @@
 #include "bnstats.h"
 #include "handoff.h"
 
+// Contraction only within one expression (a*b + c -> fma): the fp32 and bf16-storage
+// instantiations of a kernel (E2EP_IO_*) then fuse the same operations and round alike —
+// under the default cross-statement contraction hipcc may pick a different multiply to fuse
+// in each instantiation (tests/test_bf16_store_gpu.py holds them bitwise equal).
+#pragma clang fp contract(on)
+
 namespace e2ep {
 
 constexpr int MAXPH_LP = 4;  // stride phases of the data gradient (sh * sw <= 4, conv.hip)

@@ -26,21 +26,26 @@ def _ws(nbytes, device):
 # MBConv depthwise output (the squeeze-excitation's input) is stored bf16, and so are the two
 # activation gradients on either side of the depthwise conv (the gradient at that output, and
 # the depthwise data gradient feeding _bn0's backward); statistics, parameters and their
-# gradients stay fp32.  E2EP_BF16_STORE=0 keeps every activation fp32 (A/B).
+# gradients stay fp32.  E2EP_BF16_STORE: 0 (default) keeps every activation fp32, 1 stores the
+# depthwise output (and the two gradients beside it) bf16, 2 also the squeeze-excitation
+# output — the project conv's input — and the gradient at it.  Off by default: level 2 saves
+# 0.27 ms of the 18.4 ms C3 step (most of these tensors are presumably served from the 256 MB MALL, not
+# HBM) and puts the step's gradient-norm median error above the bf16 AMP comparator's
+# (0.0355 vs 0.0318; level 1: 0.0362) — profiles/r05/bf16_store_ab.txt.
 _IO_X, _IO_DY, _IO_DX = 1, 2, 4
-_BF16_STORE = [os.environ.get("E2EP_BF16_STORE", "1") != "0"]
+_BF16_STORE = [int(os.environ.get("E2EP_BF16_STORE", "0"))]
 
 
-def set_bf16_store(on):
-    """Enable / disable the bf16 activation storage of the C3 mode (returns the previous
-    setting)."""
+def set_bf16_store(level):
+    """Set the bf16 activation storage level of the C3 mode (0 off, 1 depthwise output, 2 also
+    the squeeze-excitation output; True = 2); returns the previous level."""
     prev = _BF16_STORE[0]
-    _BF16_STORE[0] = bool(on)
+    _BF16_STORE[0] = int(level) * (2 if level is True else 1)
     return prev
 
 
-def _store_bf16(train):
-    if not (train and _BF16_STORE[0]):
+def _store_bf16(train, level=1):
+    if not (train and _BF16_STORE[0] >= level):
         return False
     from . import precision
     return precision.get() == "bf16"
@@ -751,16 +756,17 @@ class _BnSwishSE(torch.autograd.Function):
                           _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s,
                           _IO_X if _is_bf16(x) else 0)
         pooled, hpre, a = torch.empty(N, C, **f32), torch.empty(N, sq, **f32), torch.empty(N, C, **f32)
-        # a bf16-stored input (bf16 storage, _store_bf16): the output — the project conv's input
-        # — is stored bf16 too
+        # a bf16-stored input (bf16 storage, _store_bf16): at level 2 the output — the project
+        # conv's input — is stored bf16 too
         hb = _is_bf16(x)
-        y = torch.empty(x.shape, dtype=x.dtype, device=dev)
+        yb = hb and _BF16_STORE[0] >= 2  # the output stored bf16 as well (level 2)
+        y = torch.empty(x.shape, dtype=torch.bfloat16 if yb else torch.float32, device=dev)
         w1c, w2c = w1.reshape(sq, C).contiguous(), w2.reshape(C, sq).contiguous()
         with timing.region(timing.name("se_fwd", x.shape, "_BnSwishSE")):
             _lib.call("e2ep_se_fwd", _lib.ptr(x), _lib.ptr(stats[2]), _lib.ptr(stats[3]),
                       _lib.ptr(w1c), _lib.ptr(b1), _lib.ptr(w2c), _lib.ptr(b2), N, C, H * W, sq,
                       _lib.ptr(pooled), _lib.ptr(hpre), _lib.ptr(a), _lib.ptr(y), s,
-                      (_IO_X | _IO_DX) if hb else 0)
+                      (_IO_X | (_IO_DX if yb else 0)) if hb else 0)
         ctx.save_for_backward(x, gamma, beta, stats, w1c, w2c, pooled, hpre, a)
         ctx.shapes = (w1.shape, w2.shape, b1 is not None, b2 is not None)
         ctx.train = train

@@ -145,6 +145,9 @@ def test_bn_bwd_bf16_io_bitwise(shape, bn_small):
         a = bwd(x32, dy32, 0, True, torch.float32)
         b = bwd(x32.to(BF), dy32, IO_X | IO_DX, True, BF)
         assert torch.equal(b[0], a[0].to(BF)) and torch.equal(b[1], a[1]) and torch.equal(b[2], a[2])
+        # _bn1 behind a bf16-stored squeeze-excitation output: x, dy and dx bf16, gated
+        b = bwd(x32.to(BF), dy32.to(BF), IO_X | IO_DY | IO_DX, True, BF)
+        assert torch.equal(b[0], a[0].to(BF)) and torch.equal(b[1], a[1]) and torch.equal(b[2], a[2])
         # _bn0: dy bf16
         a = bwd(x32, dy32, 0, False, torch.float32)
         b = bwd(x32, dy32.to(BF), IO_DY, False, torch.float32)
@@ -187,6 +190,7 @@ def test_squeeze_excite_bf16_input_bitwise(case):
     fp32 one rounded), with and without the SE-pass BN sums."""
     from e2ep_amd import nn_ops
     N, C, H, W, sq = case
+    lv = nn_ops.set_bf16_store(2)  # the output stored bf16 as well
     for sums in (True, False):
         prev = nn_ops.set_se_bn_sums(sums)
         try:
@@ -214,6 +218,7 @@ def test_squeeze_excite_bf16_input_bitwise(case):
             assert torch.equal(rm1, rm0) and torch.equal(rv1, rv0)
         finally:
             nn_ops.set_se_bn_sums(prev)
+    nn_ops.set_bf16_store(lv)
 
 
 # (N, Cin, H, W, Cout): MBConv project convs (1x1); Cout 32 runs k_conv_gemm forward and data
@@ -239,7 +244,7 @@ def test_project_conv_bf16_input_bitwise(case, pair):
     try:
         with precision.use("bf16"):
             for dt in (torch.float32, BF):
-                xd = x.to(dt).requires_grad_(True)
+                xd = x.to(dt).clone().requires_grad_(True)
                 wd = w.clone().requires_grad_(True)
                 y = ops.conv2d(xd, wd, None, 1, (0, 0, 0, 0))
                 y.backward(gy)
@@ -295,9 +300,16 @@ def test_bf16_store_only_in_bf16_training():
     x = torch.randn(2, C, 16, 16, device=DEV)
     w = torch.randn(C, 1, 3, 3, device=DEV)
     bn = _bn(C, _g(3))
-    assert nn_ops.bn_act_depthwise_conv2d(x, bn, "swish", w, 1, (1, 1, 1, 1)).dtype == torch.float32
-    with precision.use("bf16"):
-        assert nn_ops.bn_act_depthwise_conv2d(x, bn, "swish", w, 1, (1, 1, 1, 1)).dtype == BF
-        bn.eval()
-        with torch.no_grad():
+    prev = nn_ops.set_bf16_store(1)
+    try:
+        assert nn_ops.bn_act_depthwise_conv2d(x, bn, "swish", w, 1, (1, 1, 1, 1)).dtype == torch.float32
+        with precision.use("bf16"):
+            assert nn_ops.bn_act_depthwise_conv2d(x, bn, "swish", w, 1, (1, 1, 1, 1)).dtype == BF
+            nn_ops.set_bf16_store(0)  # the default: fp32 storage
             assert nn_ops.bn_act_depthwise_conv2d(x, bn, "swish", w, 1, (1, 1, 1, 1)).dtype == torch.float32
+            nn_ops.set_bf16_store(1)
+            bn.eval()
+            with torch.no_grad():
+                assert nn_ops.bn_act_depthwise_conv2d(x, bn, "swish", w, 1, (1, 1, 1, 1)).dtype == torch.float32
+    finally:
+        nn_ops.set_bf16_store(prev)
