@@ -57,7 +57,7 @@ for st in "$@"; do
       tail -1 "$O/step_sequence_$prec.txt"; head -1 "$O/step_kernels_$prec.txt" ;;
     stats)
       d=$O/prof_bench
-      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 bench.py > "$d.log" 2>&1 || { tail -20 "$d.log"; exit 1; }
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -o run -- python3 bench.py > "$d.log" 2>&1 || { tail -20 "$d.log"; exit 1; }
       find "$d" -name "*kernel_stats.csv" -exec cp {} "$O/bench_kernel_stats.csv" \;
       rm -f $(find "$d" -name "*.db") $(find "$d" -name "*kernel_trace.csv") ;;
     cmd:*)
