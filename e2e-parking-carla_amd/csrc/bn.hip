@@ -26,14 +26,14 @@ enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2 };
 
 __device__ __forceinline__ float act_fwd(float z, int act) {
   if (act == ACT_RELU) return fmaxf(z, 0.f);
-  if (act == ACT_SWISH) return z / (1.f + expf(-z));
+  if (act == ACT_SWISH) return swish_f(z);
   return z;
 }
 // d act / dz
 __device__ __forceinline__ float act_bwd(float z, int act) {
   if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
   if (act == ACT_SWISH) {
-    const float s = 1.f / (1.f + expf(-z));
+    const float s = sigmoid_f(z);
     return s * (1.f + z * (1.f - s));
   }
   return 1.f;
@@ -340,7 +340,7 @@ struct BnGate {
   __device__ __forceinline__ bool on() const { return logit != nullptr; }
   __device__ __forceinline__ void coef(int n, int C, int c, float &s, float &d) const {
     const int i = n * C + c;
-    s = 1.f / (1.f + expf(-logit[i]));
+    s = sigmoid_f(logit[i]);
     d = dpooled[i] * inv_hw;
   }
 };
@@ -423,7 +423,7 @@ __device__ __forceinline__ void bns_factors_finish(const float *dc_rand, float k
   if (gt && gt->on()) {
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      gs[u] = 1.f / (1.f + expf(-gs[u]));  // = BnGate::coef
+      gs[u] = sigmoid_f(gs[u]);  // = BnGate::coef
       gd[u] = gd[u] * gt->inv_hw;
     }
   }

@@ -108,6 +108,17 @@ __device__ __forceinline__ void bstore_t(__amdgpu_buffer_rsrc_t r, int byte_off,
   __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (bf16_t)v), r, byte_off, 0, 0);
 }
 
+// sigmoid(z) = 1 / (1 + e^-z) for the per-element activations (swish and its derivative in the
+// BatchNorm / depthwise / squeeze-excitation kernels, the SE gate): e^-z as v_exp_f32 of
+// -z log2(e) and the reciprocal as v_rcp_f32 (1 ulp) instead of the correctly rounded divide
+// this library is built with (-fhip-fp32-correctly-rounded-divide-sqrt: ~10 instructions per
+// divide).  Within a few ulp of the divide form; those kernels run one or two sigmoids per
+// element and were ALU-bound on the 128² maps.  The losses keep expf (loss.hip).
+__device__ __forceinline__ float sigmoid_f(float z) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
+}
+__device__ __forceinline__ float swish_f(float z) { return z * sigmoid_f(z); }
+
 // 64-lane wave helpers
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -57,7 +57,7 @@ struct DwIn {
 };
 __device__ __forceinline__ float dw_in(float v, float sc, float sh, int act) {
   const float z = v * sc + sh;
-  return act == 2 ? z / (1.f + expf(-z)) : act == 1 ? fmaxf(z, 0.f) : z;
+  return act == 2 ? swish_f(z) : act == 1 ? fmaxf(z, 0.f) : z;
 }
 
 // forward: one thread per output pixel; taps unrolled; branch-free guarded loads
@@ -245,7 +245,7 @@ __device__ __forceinline__ float4 dw_tf4(float4 v, const DwT &t, bool in) {
   float z[4] = {v.x * t.sc + t.sh, v.y * t.sc + t.sh, v.z * t.sc + t.sh, v.w * t.sc + t.sh};
   if (t.act == 2) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) z[i] = z[i] / (1.f + expf(-z[i]));
+    for (int i = 0; i < 4; ++i) z[i] = swish_f(z[i]);
   } else if (t.act == 1) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) z[i] = fmaxf(z[i], 0.f);

@@ -89,7 +89,7 @@ __global__ void k_se_gate_fwd(const float *__restrict__ x, const float *__restri
                               long long total, float *__restrict__ y) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
-  const float s = 1.f / (1.f + expf(-a[i / HW]));
+  const float s = sigmoid_f(a[i / HW]);
   y[i] = x[i] * s;
 }
 
@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(256) k_se_gate_bwd(const float *__restrict__ x
                                                      float *__restrict__ da) {
   const int pl = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pl >= planes) return;
-  const float s = 1.f / (1.f + expf(-a[pl]));
+  const float s = sigmoid_f(a[pl]);
   const long long base = (long long)pl * HW;
   float acc = 0.f;
   for (int i = threadIdx.x & 63; i < HW; i += 64) {

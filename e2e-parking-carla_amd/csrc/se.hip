@@ -21,7 +21,7 @@ constexpr int SE_MAXC = 4096, SE_MAXSQ = 256;
 // float4 loads in flight per lane in the per-plane reductions (squeeze, da)
 constexpr int SE_U = 4;
 
-__device__ __forceinline__ float sigm(float v) { return 1.f / (1.f + expf(-v)); }
+__device__ __forceinline__ float sigm(float v) { return sigmoid_f(v); }
 
 // Optional input transform: when the SE input is the raw output of the depthwise conv, the
 // block's _bn1 + swish is applied on load, x -> swish(x * sc[c] + sh[c]) (sc / sh from
@@ -33,7 +33,7 @@ struct SeIn {
 __device__ __forceinline__ float se_in(float v, float sc, float sh, bool t) {
   if (!t) return v;
   const float z = v * sc + sh;
-  return z / (1.f + expf(-z));
+  return swish_f(z);
 }
 __device__ __forceinline__ float4 se_in4(float4 v, float sc, float sh, bool t) {
   return make_float4(se_in(v.x, sc, sh, t), se_in(v.y, sc, sh, t), se_in(v.z, sc, sh, t),
@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(256) k_se_da(const TX *__restrict__ x, SeIn tf
           for (int j = 0; j < 4; ++j) {
             const float xh = (xv4[j] - mu) * is;
             const float zb = xh * gm + bt;
-            const float sg = 1.f / (1.f + expf(-zb));
+            const float sg = sigmoid_f(zb);
             const float sp = sg * (1.f + zb * (1.f - sg));
             a0 += (zb * sg) * gv4[j];
             a1 += gv4[j] * sp;
@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) k_se_da(const TX *__restrict__ x, SeIn tf
       if constexpr (BNS) {
         const float xh = (xv - mu) * is;
         const float zb = xh * gm + bt;
-        const float sg = 1.f / (1.f + expf(-zb));
+        const float sg = sigmoid_f(zb);
         const float sp = sg * (1.f + zb * (1.f - sg));
         acc += (zb * sg) * g;
         s1 += g * sp; s2 += sp; s3 += g * sp * xh; s4 += sp * xh;
