@@ -449,13 +449,18 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
     const auto xv = Vec<VEC>::ld(x + off);
     const auto dv = gate_dy<VEC>(Vec<VEC>::ld(dy + off), gt, n, C, c);
     const auto rv = res ? Vec<VEC>::ld(res + off) : Vec<VEC>::zero();
+    // a vector's VEC terms summed in fp32 first, then into the fp64 sums (one fp64 add per
+    // vector and sum instead of an add, a multiply and two conversions per element)
+    float s4 = 0.f, q4 = 0.f;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       float xh, dz, dzb;
       el(Vec<VEC>::get(xv, i), Vec<VEC>::get(dv, i), Vec<VEC>::get(rv, i), n, xh, dz, dzb);
-      s += dzb;
-      q += (double)dzb * xh;
+      s4 += dzb;
+      q4 = __builtin_fmaf(dzb, xh, q4);
     }
+    s += s4;
+    q += q4;
   }
   block_sum2(s, q);
   if (threadIdx.x == 0) {
@@ -675,14 +680,17 @@ __global__ void __launch_bounds__(T) k_bn_bwd_small(
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const int t = threadIdx.x + u * T;
+    float s4 = 0.f, q4 = 0.f;  // fp32 over the vector, then fp64 (as k_bn_bwd_reduce)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       el.with_factor(Vec<4>::get(xv[u], i), Vec<4>::get(dv[u], i) * gs[u] + gd[u],
                      Vec<4>::get(rv[u], i), dcf[u], xh[u][i], dz[u][i], dzb[u][i]);
-      if (t < tot) {
-        s += dzb[u][i];
-        q += (double)dzb[u][i] * xh[u][i];
-      }
+      s4 += dzb[u][i];
+      q4 = __builtin_fmaf(dzb[u][i], xh[u][i], q4);
+    }
+    if (t < tot) {
+      s += s4;
+      q += q4;
     }
   }
   block_sum2_t<T>(s, q);
