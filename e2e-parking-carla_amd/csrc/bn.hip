@@ -77,6 +77,27 @@ struct Vec<1> {
   static __device__ __forceinline__ float zero() { return 0.f; }
 };
 
+// (n, p) = divmod(t, HWv) for t = t0, t0 + 256, t0 + 512, ... (a 256-thread block's strided
+// walk over a channel's N x HWv vectors): one division up front, then a carry per step instead
+// of an integer division (~25 instructions) per vector
+struct PlaneWalk {
+  int n, p, dq, dr, hw;
+  __device__ __forceinline__ PlaneWalk(int t0, int hw_) : hw(hw_) {
+    n = t0 / hw;
+    p = t0 - n * hw;
+    dq = 256 / hw;
+    dr = 256 - dq * hw;
+  }
+  __device__ __forceinline__ void next() {
+    p += dr;
+    n += dq;
+    if (p >= hw) {
+      p -= hw;
+      ++n;
+    }
+  }
+};
+
 // fixed-order fp64 block reduction of two values (256 threads); result valid in every thread
 __device__ __forceinline__ void block_sum2(double &s, double &q) {
   __shared__ double rs[4], rq[4];
@@ -118,8 +139,9 @@ __global__ void __launch_bounds__(256) k_bn_stats(const TX *__restrict__ x, int 
   const int tot = N * HWv;
   const int beg = sp * per, end = min(tot, beg + per);
   double s = 0.0, q = 0.0;
-  for (int t = beg + threadIdx.x; t < end; t += 256) {
-    const int n = t / HWv, p = t - n * HWv;
+  PlaneWalk w(beg + (int)threadIdx.x, HWv);
+  for (int t = beg + threadIdx.x; t < end; t += 256, w.next()) {
+    const int n = w.n, p = w.p;
     const auto v = Vec<VEC>::ld(x + (((size_t)n * C + c) * HWv + p) * VEC);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -181,8 +203,9 @@ __global__ void __launch_bounds__(256) k_bn_apply(
   const float sh = scale ? shift[c] : (beta ? beta[c] : 0.f) - mu * sc;
   const int tot = N * HWv;
   const int beg = j * per, end = min(tot, beg + per);
-  for (int t = beg + threadIdx.x; t < end; t += 256) {
-    const int n = t / HWv, p = t - n * HWv;
+  PlaneWalk w(beg + (int)threadIdx.x, HWv);
+  for (int t = beg + threadIdx.x; t < end; t += 256, w.next()) {
+    const int n = w.n, p = w.p;
     const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
     auto v = Vec<VEC>::ld(x + off);
     const auto r = res ? Vec<VEC>::ld(res + off) : Vec<VEC>::zero();
@@ -443,8 +466,9 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
   const BnBwdElem<VEC> el{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f,
                           dc_rand, dc_keep, act};
   double s = 0.0, q = 0.0;
-  for (int t = beg + threadIdx.x; t < end; t += 256) {
-    const int n = t / HWv, p = t - n * HWv;
+  PlaneWalk w(beg + (int)threadIdx.x, HWv);
+  for (int t = beg + threadIdx.x; t < end; t += 256, w.next()) {
+    const int n = w.n, p = w.p;
     const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
     const auto xv = Vec<VEC>::ld(x + off);
     const auto dv = gate_dy<VEC>(Vec<VEC>::ld(dy + off), gt, n, C, c);
@@ -520,8 +544,9 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(
   const float gis = el.g * el.is;
   const int tot = N * HWv;
   const int beg = j * per, end = min(tot, beg + per);
-  for (int t = beg + threadIdx.x; t < end; t += 256) {
-    const int n = t / HWv, p = t - n * HWv;
+  PlaneWalk w(beg + (int)threadIdx.x, HWv);
+  for (int t = beg + threadIdx.x; t < end; t += 256, w.next()) {
+    const int n = w.n, p = w.p;
     const size_t off = (((size_t)n * C + c) * HWv + p) * VEC;
     const auto xv = Vec<VEC>::ld(x + off);
     const auto dv = gate_dy<VEC>(Vec<VEC>::ld(dy + off), gt, n, C, c);

@@ -139,11 +139,13 @@ __global__ void __launch_bounds__(256) k_se_excite(const TX *__restrict__ x, SeI
                                                    const float *__restrict__ a, int HW,
                                                    long long nvec, int vec,
                                                    TY *__restrict__ y) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // 32-bit indices (nvec < 2^29, checked by e2ep_se_fwd): a 64-bit division and remainder per
+  // thread cost more than the float4's arithmetic
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i >= nvec) return;
   const bool t = tf.sc != nullptr;
-  const long long pl = vec ? i / (HW >> 2) : i / HW;
-  const int c = (int)(pl % tf.C);
+  const int pl = vec ? i / (HW >> 2) : i / HW;
+  const int c = pl % tf.C;
   const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
   const float s = sigm(a[pl]);
   if (vec) {
@@ -400,6 +402,7 @@ int e2ep_se_fwd(const void *x, const float *x_scale, const float *x_shift, const
   const int planes = N * C;
   const int vec = (HW & 3) == 0;
   const long long nvec = (long long)planes * HW / (vec ? 4 : 1);
+  E2EP_REQUIRE(nvec < (1LL << 29), E2EP_ERANGE, "e2ep_se_fwd: %lld vectors >= 2^29", nvec);
   if (io)
     hipLaunchKernelGGL(k_se_squeeze<bf16_t>, dim3(cdiv(planes, 4)), dim3(256), 0, s,
                        static_cast<const bf16_t *>(x), tf, planes, HW, pooled);
