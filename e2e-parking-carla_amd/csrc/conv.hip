@@ -955,16 +955,33 @@ __device__ __forceinline__ void conv_wgrad2_block(
 
   float4 ra[2];
   float rb[8];
-  auto load_tiles = [&](int ks) {
-    const int p0 = pbeg + min(ks, nk - 1) * W2K;  // past the range: re-read, never stored
-    const int im = p0 / PQ, od0 = p0 - im * PQ;   // wave-uniform
+  // the step's (image, first pixel) and this lane's output pixel (oy, ox), advanced by W2K
+  // pixels per step with carries instead of a scalar and a per-lane division per step (a step
+  // never straddles images: PQ % W2K == 0)
+  int im = pbeg / PQ, od0 = pbeg - im * PQ;
+  int oy = (od0 + bp) / g.Q, ox = od0 + bp - oy * g.Q;
+  const int q32 = W2K / g.Q, r32 = W2K - q32 * g.Q;
+  auto advance = [&]() {
+    od0 += W2K;
+    if (od0 >= PQ) {
+      od0 -= PQ;
+      ++im;
+    }
+    ox += r32;
+    oy += q32;
+    if (ox >= g.Q) {
+      ox -= g.Q;
+      ++oy;
+    }
+    if (oy >= g.P) oy -= g.P;
+  };
+  auto load_tiles = [&](int ks) {  // ks = 0, 1, ... in order; ks >= nk re-reads step nk - 1
+    if (ks > 0 && ks < nk) advance();
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int co = m0 + ar + 32 * i;
       ra[i] = bload4(rg, co < g.Cout ? ((im * g.Cout + co) * PQ + od0 + 4 * aq) * 4 : OOR);
     }
-    const int od = od0 + bp;
-    const int oy = od / g.Q, ox = od - oy * g.Q;
     const int yb = oy * g.sh, xb = ox * g.sw;
     const int pbase = im * g.Cin * HW + yb * g.W + xb;
 #pragma unroll
