@@ -168,8 +168,11 @@ __global__ void __launch_bounds__(256) k_bn_apply(
     float *__restrict__ mean_out, float *__restrict__ invstd_out, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
     const float *__restrict__ dc_rand, float dc_keep, int N, int C, int HWv, int per, int act,
-    float *__restrict__ y, const float *__restrict__ scale, const float *__restrict__ shift) {
-  const int c = blockIdx.x, j = blockIdx.y;
+    float *__restrict__ y, const float *__restrict__ scale, const float *__restrict__ shift,
+    int rev) {
+  // rev: back-to-front sweep, starting on the rows the producing conv wrote last (e2ep_tune 33)
+  const int c = rev ? C - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int j = rev ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
   float mu = 0.f, is = 0.f;
   if (scale) {
     // folded affine from e2ep_bn_finalize_part / e2ep_bn_stats (bn_finalize_channel: the same
@@ -459,8 +462,11 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(
     const float *__restrict__ invstd, const float *__restrict__ gamma,
     const float *__restrict__ beta, const float *__restrict__ res,
     const float *__restrict__ dc_rand, float dc_keep, BnGate gt, int N, int C, int HWv,
-    int splits, int per, int act, double *__restrict__ part) {
-  const int c = blockIdx.x, sp = blockIdx.y;
+    int splits, int per, int act, double *__restrict__ part, int rev) {
+  // rev: walk the tensor back to front (blocks are dispatched x fastest, so the forward order
+  // sweeps memory front to back; e2ep_tune key 33)
+  const int c = rev ? C - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int sp = rev ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
   const int tot = N * HWv;
   const int beg = sp * per, end = min(tot, beg + per);
   const BnBwdElem<VEC> el{mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f,
@@ -517,8 +523,11 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(
     const float *__restrict__ dc_rand, float dc_keep, BnGate gt, const double *__restrict__ part,
     int splits, long long cnt, int N, int C, int HWv, int per, int act, int train,
     TO *__restrict__ dx, float *__restrict__ dres, float *__restrict__ dgamma,
-    float *__restrict__ dbeta, const double *__restrict__ planes) {
-  const int c = blockIdx.x, j = blockIdx.y;
+    float *__restrict__ dbeta, const double *__restrict__ planes, int rev) {
+  // rev: back-to-front sweep, so the apply pass starts on the rows the reduction (or the
+  // producer) touched last, while they may still sit in the 256 MB MALL (e2ep_tune key 33)
+  const int c = rev ? C - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int j = rev ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
   double s, q;
   if (planes) {  // e2ep_bn_bwd_planes: the sums from the SE pass's per-plane factors
     s = 0.0;
@@ -798,6 +807,12 @@ static int bn_splits(long long per_channel, int C) {
 // vectors per apply workgroup (4 per thread)
 #define APPLY_PER (g_tune[TUNE_BN_APPLY_PER])
 
+// sweep direction of the split BN passes (e2ep_tune key 33 = 1 + mask): mask bit 0 backward
+// apply back to front, bit 1 backward reduction back to front, bit 2 forward apply back to front
+static int bn_rev_apply() { return ((g_tune[TUNE_BN_ORDER] - 1) >> 0) & 1; }
+static int bn_rev_reduce() { return ((g_tune[TUNE_BN_ORDER] - 1) >> 1) & 1; }
+static int bn_rev_fwd() { return ((g_tune[TUNE_BN_ORDER] - 1) >> 2) & 1; }
+
 }  // namespace e2ep
 
 using namespace e2ep;
@@ -854,11 +869,11 @@ int e2ep_bn_fwd(const float *x, const float *gamma, const float *beta, const flo
   if (v4)
     hipLaunchKernelGGL(k_bn_apply<4>, grid, dim3(256), 0, s, x, part, sp, per_c, eps, momentum,
                        running_mean, running_var, mean, invstd, gamma, beta, res, dc_rand, dc_keep,
-                       N, C, HWv, APPLY_PER, act, y, nullptr, nullptr);
+                       N, C, HWv, APPLY_PER, act, y, nullptr, nullptr, bn_rev_fwd());
   else
     hipLaunchKernelGGL(k_bn_apply<1>, grid, dim3(256), 0, s, x, part, sp, per_c, eps, momentum,
                        running_mean, running_var, mean, invstd, gamma, beta, res, dc_rand, dc_keep,
-                       N, C, HWv, APPLY_PER, act, y, nullptr, nullptr);
+                       N, C, HWv, APPLY_PER, act, y, nullptr, nullptr, bn_rev_fwd());
   return launch_status("e2ep_bn_fwd");
 }
 
@@ -977,11 +992,11 @@ int e2ep_bn_apply(const float *x, const float *scale, const float *shift, const 
   if (v4)
     hipLaunchKernelGGL(k_bn_apply<4>, grid, dim3(256), 0, s, x, nullptr, 1, (long long)N * HW, 0.f,
                        0.f, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, res, dc_rand,
-                       dc_keep, N, C, HWv, APPLY_PER, act, y, scale, shift);
+                       dc_keep, N, C, HWv, APPLY_PER, act, y, scale, shift, bn_rev_fwd());
   else
     hipLaunchKernelGGL(k_bn_apply<1>, grid, dim3(256), 0, s, x, nullptr, 1, (long long)N * HW, 0.f,
                        0.f, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, res, dc_rand,
-                       dc_keep, N, C, HWv, APPLY_PER, act, y, scale, shift);
+                       dc_keep, N, C, HWv, APPLY_PER, act, y, scale, shift, bn_rev_fwd());
   return launch_status("e2ep_bn_apply");
 }
 
@@ -1031,20 +1046,22 @@ static int bn_bwd_impl(const TX *x, const TD *dy, const float *mean, const float
   double *part = static_cast<double *>(workspace);
   if (v4)
     hipLaunchKernelGGL((k_bn_bwd_reduce<4, TX, TD>), dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd,
-                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
+                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part,
+                       bn_rev_reduce());
   else
     hipLaunchKernelGGL((k_bn_bwd_reduce<1, TX, TD>), dim3(C, sp), dim3(256), 0, s, x, dy, mean, invstd,
-                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part);
+                       gamma, beta, res, dc_rand, dc_keep, gt, N, C, HWv, sp, per, act, part,
+                       bn_rev_reduce());
   if (dx || dres) {
     const dim3 grid(C, cdiv(totv, APPLY_PER));
     if (v4)
       hipLaunchKernelGGL((k_bn_bwd_apply<4, TX, TD, TO>), grid, dim3(256), 0, s, x, dy, mean, invstd,
                          gamma, beta, res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER,
-                         act, train, dx, dres, dgamma, dbeta, nullptr);
+                         act, train, dx, dres, dgamma, dbeta, nullptr, bn_rev_apply());
     else
       hipLaunchKernelGGL((k_bn_bwd_apply<1, TX, TD, TO>), grid, dim3(256), 0, s, x, dy, mean, invstd,
                          gamma, beta, res, dc_rand, dc_keep, gt, part, sp, per_c, N, C, HWv, APPLY_PER,
-                         act, train, dx, dres, dgamma, dbeta, nullptr);
+                         act, train, dx, dres, dgamma, dbeta, nullptr, bn_rev_apply());
   } else if (dgamma || dbeta) {
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(C), dim3(256), 0, s, part, sp, dgamma, dbeta);
   }
@@ -1119,20 +1136,24 @@ int e2ep_bn_bwd_planes(const void *x, const void *dy, const float *mean, const f
     hipLaunchKernelGGL((k_bn_bwd_apply<4, bf16_t, bf16_t, bf16_t>), grid, dim3(256), 0, s,
                        static_cast<const bf16_t *>(x), static_cast<const bf16_t *>(dy), mean, invstd,
                        gamma, beta, nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER,
-                       act, 1, static_cast<bf16_t *>(dx), nullptr, dgamma, dbeta, plane_sums);
+                       act, 1, static_cast<bf16_t *>(dx), nullptr, dgamma, dbeta, plane_sums,
+                       bn_rev_apply());
   else if (io == BNIO_XDX)
     hipLaunchKernelGGL((k_bn_bwd_apply<4, bf16_t, float, bf16_t>), grid, dim3(256), 0, s,
                        static_cast<const bf16_t *>(x), dyf, mean, invstd, gamma, beta, nullptr, nullptr,
                        1.f, gt, nullptr, 1, per_c, N, C, HWv, APPLY_PER, act, 1,
-                       static_cast<bf16_t *>(dx), nullptr, dgamma, dbeta, plane_sums);
+                       static_cast<bf16_t *>(dx), nullptr, dgamma, dbeta, plane_sums,
+                       bn_rev_apply());
   else if (v4)
     hipLaunchKernelGGL(k_bn_bwd_apply<4>, grid, dim3(256), 0, s, static_cast<const float *>(x), dyf, mean,
                        invstd, gamma, beta, nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv,
-                       APPLY_PER, act, 1, static_cast<float *>(dx), nullptr, dgamma, dbeta, plane_sums);
+                       APPLY_PER, act, 1, static_cast<float *>(dx), nullptr, dgamma, dbeta, plane_sums,
+                       bn_rev_apply());
   else
     hipLaunchKernelGGL(k_bn_bwd_apply<1>, grid, dim3(256), 0, s, static_cast<const float *>(x), dyf, mean,
                        invstd, gamma, beta, nullptr, nullptr, 1.f, gt, nullptr, 1, per_c, N, C, HWv,
-                       APPLY_PER, act, 1, static_cast<float *>(dx), nullptr, dgamma, dbeta, plane_sums);
+                       APPLY_PER, act, 1, static_cast<float *>(dx), nullptr, dgamma, dbeta, plane_sums,
+                       bn_rev_apply());
   return launch_status("e2ep_bn_bwd_planes");
 }
 

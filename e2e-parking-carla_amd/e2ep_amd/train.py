@@ -43,9 +43,11 @@ without its module wrapper), one flat fp32 gradient buffer in FlatAdam's layout;
 Graphs are captured through e2ep_amd.graphs.capture, which repairs memset nodes (they do
 not replay correctly on this ROCm stack) before instantiation.
 
-Graph mode captures the lift-splat pillar plan of the batch's (host) rig: a later batch with
-a different intrinsics/extrinsics rig raises instead of silently training on the captured
-plan (the CARLA rig is constant).
+Graph mode captures the lift-splat pillar plan of the batch's rig, planned before the capture
+with the reference's fp32 host algebra whether the rig arrives as host or device tensors
+(BevModel.prepare_capture; the plans are kept alive with the graphs): a later batch with a
+different intrinsics/extrinsics rig raises instead of silently training on the captured plan
+(the CARLA rig is constant).
 """
 import os
 
@@ -59,11 +61,13 @@ BUCKET_MB = 25.0  # DistributedDataParallel's default bucket_cap_mb
 
 
 def _rig_key(batch):
+    """The rig's shapes and fp32 bytes (a device rig is copied to the host: one small
+    synchronising copy, only when a batch is handed to a graph-mode step)."""
     k, e = batch.get("intrinsics"), batch.get("extrinsics")
-    if not (torch.is_tensor(k) and torch.is_tensor(e)) or k.is_cuda or e.is_cuda:
-        return None  # device rig: the plan is rebuilt inside the step, nothing captured
-    return (tuple(k.shape), tuple(e.shape), k.detach().float().contiguous().numpy().tobytes(),
-            e.detach().float().contiguous().numpy().tobytes())
+    if not (torch.is_tensor(k) and torch.is_tensor(e)):
+        return None
+    k, e = k.detach().float().cpu().contiguous(), e.detach().float().cpu().contiguous()
+    return (tuple(k.shape), tuple(e.shape), k.numpy().tobytes(), e.numpy().tobytes())
 
 
 class GradBuckets:
@@ -111,6 +115,7 @@ class GradBuckets:
         stream the gradient kernels were issued on (under capture it can be a stream outside
         the capture), so the bucket fork waits on an event of THIS stream."""
         self.pending = [i1 - i0 for (i0, i1, _, _) in self.buckets]
+        self.streams = [[] for _ in self.buckets]  # non-main streams gradients arrived on
         self.next = 0
         self.works = []
         self.active = True
@@ -120,6 +125,13 @@ class GradBuckets:
 
     def _arrived(self, i):
         b = self.of[i]
+        if self.cuda and not self.capturing:
+            # the stream this gradient was produced on (a model branch's side stream for the
+            # segmentation / depth heads): the bucket's gather waits for every one of them,
+            # not only for the stream of the hook that completes the bucket
+            here = torch.cuda.current_stream()
+            if here != self.main and all(here != s for s in self.streams[b]):
+                self.streams[b].append(here)
         self.pending[b] -= 1
         while self.next < len(self.buckets) and self.pending[self.next] == 0:
             self._launch(self.next)
@@ -135,10 +147,9 @@ class GradBuckets:
         ev = torch.cuda.Event()
         ev.record(self.main)
         self.comm.wait_event(ev)
-        here = torch.cuda.current_stream()
-        if not self.capturing and here != self.main:  # eager: also the hook thread's stream
+        for st in self.streams[b]:  # eager: every stream a gradient of the bucket came from
             ev2 = torch.cuda.Event()
-            ev2.record(here)
+            ev2.record(st)
             self.comm.wait_event(ev2)
         with torch.cuda.stream(self.comm):
             if not self.capturing:
@@ -209,7 +220,15 @@ class TrainStep:
         self.g_s1 = self.g_s1g = self.g_s2 = self.g_s2g = None
         self.seg_buckets = None  # ([stage-1 (lo, hi)], [stage-2 (lo, hi)]) of the flat buffer
         self._rig = _rig_key(batch)
+        # test-only: (stage, bucket index) of a segmented-exchange bucket whose all-reduce is
+        # skipped (tests/test_ddp_gpu.py proves the parity check fails without it)
+        self._test_skip = None
+        self._plans = []
         if graph:
+            # plan every rig the capture will meet outside it (host algebra, bit-exact), and
+            # keep those plans as long as the graphs that read them
+            self._plans = [m.prepare_capture(batch) for m in module.modules()
+                           if hasattr(m, "prepare_capture")]
             self._capture(warmup)
 
     # -- pieces ---------------------------------------------------------------------------
@@ -339,21 +358,22 @@ class TrainStep:
         main = torch.cuda.current_stream()
         works = []
 
-        def issue(ranges):
+        def issue(stage, ranges):
             ev = torch.cuda.Event()
             ev.record(main)
             self.comm.wait_event(ev)
             with torch.cuda.stream(self.comm):
-                for lo, hi in ranges:
-                    works.append(dist.all_reduce(self.flat_grad[lo:hi], async_op=True))
+                for j, (lo, hi) in enumerate(ranges):
+                    if self._test_skip != (stage, j):
+                        works.append(dist.all_reduce(self.flat_grad[lo:hi], async_op=True))
 
         self.g_s1.replay()
         self.g_s1g.replay()
-        issue(self.seg_buckets[0])  # overlaps the stage-2 backward below
+        issue(0, self.seg_buckets[0])  # overlaps the stage-2 backward below
         self.g_s2.replay()
         if self.g_s2g is not None:
             self.g_s2g.replay()
-        issue(self.seg_buckets[1])
+        issue(1, self.seg_buckets[1])
         for w in works:
             w.wait()  # the compute stream waits for every bucket
         self.g_opt.replay()
@@ -378,9 +398,10 @@ class TrainStep:
             done.record(self.comm)
             return done
 
-        def exchange(ranges, done):
+        def exchange(stage, ranges, done):
             done.synchronize()  # the host waits for this stage's copies, not for the GPU
-            works = [dist.all_reduce(h[lo:hi], async_op=True) for lo, hi in ranges]
+            works = [dist.all_reduce(h[lo:hi], async_op=True)
+                     for j, (lo, hi) in enumerate(ranges) if self._test_skip != (stage, j)]
             for w in works:
                 w.wait()
             with torch.cuda.stream(self.comm):
@@ -391,10 +412,10 @@ class TrainStep:
         self.g_s1g.replay()
         d1 = copy_out(self.seg_buckets[0])
         self.g_s2.replay()  # stage 2 on the GPU while the host exchanges stage 1
-        exchange(self.seg_buckets[0], d1)
+        exchange(0, self.seg_buckets[0], d1)
         if self.g_s2g is not None:
             self.g_s2g.replay()
-        exchange(self.seg_buckets[1], copy_out(self.seg_buckets[1]))
+        exchange(1, self.seg_buckets[1], copy_out(self.seg_buckets[1]))
         main.wait_stream(self.comm)
         self.g_opt.replay()
 
@@ -428,7 +449,7 @@ class TrainStep:
                 raise _lib.E2EPError(
                     "TrainStep(graph=True) captured the lift-splat plan of the first batch's "
                     "camera rig; this batch has different intrinsics/extrinsics (build a new "
-                    "TrainStep, or pass the rig as device tensors so the plan is rebuilt)")
+                    "TrainStep, or use graph=False, which plans every batch's rig)")
             for k, v in batch.items():
                 if torch.is_tensor(v) and torch.is_tensor(self.batch.get(k)) and self.batch[k].is_cuda:
                     self.batch[k].copy_(v, non_blocking=True)

@@ -8,7 +8,7 @@ plan, and the fused outer-product pooling kernel (e2ep_amd.lss)."""
 import torch
 from torch import nn
 
-from e2ep_amd import lss, nn_ops
+from e2ep_amd import _lib, lss, nn_ops
 from model.cam_encoder import CamEncoder
 
 
@@ -41,6 +41,7 @@ class BevModel(nn.Module):
         self._consts_key = self._consts_version()
         self._plan_key = None
         self._plan = None
+        self._dev_plans = {}  # device-rig key -> plan (BevModel.plan)
 
     def create_frustum(self):
         """(D, h, w, 3) grid of (u, v, depth) — model/bev_model.py:28-43."""
@@ -65,41 +66,75 @@ class BevModel(nn.Module):
         dims = [int(v) for v in self.bev_dim.detach().cpu()]
         return lo.tolist(), res.tolist(), dims
 
+    @staticmethod
+    def _dev_rig_key(intrinsics, extrinsics, device):
+        # a device rig is identified by its storage and version counter: an in-place write
+        # (e.g. TrainStep copying a new batch into its input buffers) makes it a new rig
+        return (str(device), tuple(intrinsics.shape), tuple(extrinsics.shape),
+                intrinsics.data_ptr(), extrinsics.data_ptr(), intrinsics._version,
+                extrinsics._version)
+
     def plan(self, intrinsics, extrinsics, device):
         """Pillar plan for this batch's rig.  The plan is a pure function of (frustum, K, E).
         The rig algebra is the reference's own fp32 CPU ops (lss.rig_transforms_host,
-        model/bev_model.py:46-53), so the pillar index is the reference's bit for bit, and the
-        plan is memoised on the K / E bytes, since the CARLA rig is constant (SURVEY.md §0
-        fact 2).  Host K / E (the dataloader / agent case) are read in place; device K / E are
-        copied to the host first (one 8-matrix synchronising copy per call, then the same
-        memoised path).  Only inside a HIP-graph capture, where no host copy can run, device
-        K / E go through the fp64 device algebra (lss.rig_transforms), which the capture
-        replays from the device rig each time; its last fp32 ulp is not LAPACK's, so a few
-        points on a cell edge may land in the neighbouring pillar (tests/test_lss_gpu.py).
-        E2EP_PLAN_CACHE=0 rebuilds the plan every call."""
-        if not torch.cuda.is_current_stream_capturing():
+        model/bev_model.py:46-53), so the pillar index is the reference's bit for bit on every
+        path, and the plan is memoised on the K / E bytes, since the CARLA rig is constant
+        (SURVEY.md §0 fact 2).  Host K / E (the dataloader / agent case) are read in place;
+        device K / E are copied to the host first (one 8-matrix synchronising copy per call,
+        then the same memoised path).
+        Inside a HIP-graph capture no host copy can run: device K / E must have been planned
+        before the capture (an eager forward, or TrainStep / `prepare_capture`, which call this
+        outside it), and the capture reuses that plan's device tensors — the rig is constant
+        under a captured graph (TrainStep raises when a batch brings a different one).  A
+        device rig met first inside a capture raises instead of planning with the device
+        algebra, whose last fp32 ulp is not LAPACK's (6 of 1.18 M C4 points flipped pillar in
+        round 5).  E2EP_PLAN_CACHE=0 rebuilds the plan every (eager) call."""
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not capturing:
             key = self._consts_version()
             if key != self._consts_key:  # moved or reloaded parameters (no copy inside capture)
                 self._host_consts, self._consts_key = self._consts(), key
         lo, res, dims = self._host_consts
         on_dev = intrinsics.is_cuda or extrinsics.is_cuda
-        if on_dev and torch.cuda.is_current_stream_capturing():
-            combine, trans = lss.rig_transforms(intrinsics, extrinsics, device)
-            return lss.build_plan(self.frustum, combine, trans, lo, res, dims, device)
+        dkey = self._dev_rig_key(intrinsics, extrinsics, device) if on_dev else None
+        if on_dev and capturing:
+            plan = self._dev_plans.get(dkey)
+            if plan is None:
+                raise _lib.E2EPError(
+                    "BevModel.plan: a device intrinsics/extrinsics rig met first inside a "
+                    "HIP-graph capture; plan it before the capture (an eager forward, "
+                    "BevModel.prepare_capture or TrainStep) so the captured pillar table is "
+                    "the reference's fp32 host algebra")
+            return plan
         if on_dev:  # synchronising copy: the bit-exact host algebra below
             intrinsics, extrinsics = intrinsics.detach().cpu(), extrinsics.detach().cpu()
         key = None
+        plan = None
         if lss.plan_cache_enabled():
             key = (str(device), intrinsics.shape, extrinsics.shape,
                    intrinsics.detach().float().contiguous().numpy().tobytes(),
                    extrinsics.detach().float().contiguous().numpy().tobytes())
             if key == self._plan_key and self._plan is not None:
-                return self._plan
-        combine, trans = lss.rig_transforms_host(intrinsics, extrinsics)
-        plan = lss.build_plan(self.frustum, combine, trans, lo, res, dims, device)
-        if key is not None:
-            self._plan_key, self._plan = key, plan
+                plan = self._plan
+        if plan is None:
+            combine, trans = lss.rig_transforms_host(intrinsics, extrinsics)
+            plan = lss.build_plan(self.frustum, combine, trans, lo, res, dims, device)
+            if key is not None:
+                self._plan_key, self._plan = key, plan
+        if dkey is not None:  # the plan a capture of this device rig will reuse
+            self._dev_plans.pop(dkey, None)
+            self._dev_plans[dkey] = plan
+            while len(self._dev_plans) > 8:
+                self._dev_plans.pop(next(iter(self._dev_plans)))
         return plan
+
+    def prepare_capture(self, batch):
+        """Plan the batch's rig outside a capture (TrainStep calls this before capturing) and
+        return the plan, which the caller keeps alive as long as its graph."""
+        k, e = batch.get("intrinsics"), batch.get("extrinsics")
+        if not (torch.is_tensor(k) and torch.is_tensor(e)) or not self.frustum.is_cuda:
+            return None
+        return self.plan(k, e, self.frustum.device)  # the device the forward moves images to
 
     def encoder_forward(self, images):
         """Camera features (B*N, C, h, w) and depth distribution (B*N, D, h, w)."""

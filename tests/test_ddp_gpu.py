@@ -10,9 +10,13 @@
   without an exchange, bit for bit.
 * gloo at world 2, both ranks on cuda:0 (the one-GPU rehearsal of the N>1 path): the default
   graph-mode exchange — the segmented backward with the stage-1 buckets exchanged while stage 2
-  runs, each bucket staged through pinned host memory — of the real ParkingModel TrainStep with
-  the same batch on both ranks equals the one-process step (mean of two equal gradients) and
-  the single-graph exchange (segment=False), replay for replay.
+  runs, each bucket staged through pinned host memory — of the real ParkingModel TrainStep,
+  rank r training on its OWN batch (synthetic seed 7 + r, target noise 7 + r), equals the
+  data-parallel step computed in one process (each rank's batch through the same weights, BN
+  batch statistics per rank as DDP without SyncBN, the two flat gradients summed and one
+  FlatAdam.step(sum, 1/2)) and the single-graph exchange (segment=False), bit for bit; and the
+  check can fail: skipping the all-reduce of one stage-1 bucket (a test-only switch) breaks it.
+  Reference: pl_train.py:42-47 (DDP when num_gpus > 1).
 """
 import os
 import socket
@@ -140,14 +144,24 @@ def test_rccl_world1_exchange_is_exact(graph):
         dist.destroy_process_group()
 
 
+def _rank_batch(rank):
+    from e2ep_amd import synthetic
+    d = synthetic.synthetic_batch(1, seed=7 + rank)
+    return {k: (v if k in ("intrinsics", "extrinsics") else v.to(DEV)) for k, v in d.items()}
+
+
+_STEPS = 2  # replays after the one eager warm-up step
+
+
 def _gloo_worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from e2ep_amd.train import TrainStep
-    for segment in (True, False):
-        m = _parking_module()
-        s = TrainStep(m, _parking_batch(), world=world, graph=True, warmup=1, bucket_mb=4.0,
+    for case in ("segmented", "single", "skip"):
+        segment = case != "single"
+        m = _parking_module(seed_noise=7 + rank)
+        s = TrainStep(m, _rank_batch(rank), world=world, graph=True, warmup=1, bucket_mb=4.0,
                       segment=segment)
         assert s.buckets is None and s._host is not None
         if segment:  # the default graph-mode exchange: stage buckets between segment replays
@@ -159,28 +173,66 @@ def _gloo_worker(rank, world, port, out):
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))  # a partition
         else:
             assert not s.segmented and s.g_bwd is not None and s.g_gather is not None
-        losses = [float(s()) for _ in range(2)]
-        out[(rank, segment)] = (losses, _flat_params(m))
+        if case == "skip":
+            s._test_skip = (0, 0)  # the first stage-1 bucket is never exchanged
+        losses = [float(s()) for _ in range(_STEPS)]
+        out[(rank, case)] = (losses, _flat_params(m))
         del s, m
     dist.destroy_process_group()
 
 
-def test_gloo_two_rank_rehearsal_equals_one_process():
-    from e2ep_amd.train import TrainStep
+def _one_process_data_parallel(steps):
+    """The world-2 step in one process: both ranks' batches through the same weights (one
+    module; BN normalises each forward with its own batch statistics, as per-rank BN under
+    DDP does), each rank's gradients gathered into a flat buffer, the all-reduce's sum
+    formed, and one FlatAdam.step(sum, 1/world) — steps times, the first one eager like
+    TrainStep's warm-up.  Returns (losses per rank, flat parameters)."""
+    from e2ep_amd import synthetic
+    from e2ep_amd.optim import FlatAdam
     m = _parking_module()
-    s = TrainStep(m, _parking_batch(), graph=True, warmup=1)
-    want_losses = [float(s()) for _ in range(2)]
-    want = _flat_params(m)
-    del s, m
+    params = [p for p in m.parameters() if p.requires_grad]
+    opt = FlatAdam(params, lr=1e-4, weight_decay=1e-4)  # TrainStep's defaults
+    batches = [_rank_batch(r) for r in range(2)]
+    noises = [synthetic.target_noise(1, seed=7 + r).to(DEV) for r in range(2)]
+    flats = [torch.zeros(opt.numel, device=DEV) for _ in range(2)]
+    has = [torch.zeros(len(params), dtype=torch.int64, device=DEV) for _ in range(2)]
+    one = torch.ones((), device=DEV)
+    losses = {0: [], 1: []}
+    for _ in range(steps):
+        for r in range(2):
+            m.parking_model._noise = lambda b, device, n, z=noises[r]: z
+            opt.zero_grad(set_to_none=True)
+            loss = m.training_step(batches[r], 0)
+            loss.backward(one)
+            opt.prepare()
+            opt.gather_grads(flats[r])
+            opt.has_grad(has[r])
+            losses[r].append(float(loss))
+        opt.step(flats[0] + flats[1], 0.5, has_grad=torch.maximum(has[0], has[1]))
+    torch.cuda.synchronize()
+    return losses, _flat_params(m)
+
+
+def test_gloo_two_rank_rehearsal_equals_one_process():
+    want_losses, want = _one_process_data_parallel(1 + _STEPS)
     with mp.Manager() as man:
         out = man.dict()
         mp.spawn(_gloo_worker, args=(2, _port(), out), nprocs=2, join=True)
         res = dict(out)
-    (l0, p0), (l1, p1) = res[(0, True)], res[(1, True)]
-    (l0s, p0s), (l1s, p1s) = res[(0, False)], res[(1, False)]
+    (l0, p0), (l1, p1) = res[(0, "segmented")], res[(1, "segmented")]
+    (l0s, p0s), (l1s, p1s) = res[(0, "single")], res[(1, "single")]
+    # each rank saw its own batch: different losses, identical replicas afterwards
+    assert l0 != l1 and l0[0] != l1[0]
+    assert l0 == want_losses[0][1:] and l1 == want_losses[1][1:]
+    assert l0s == l0 and l1s == l1
     assert torch.equal(p0, p1) and torch.equal(p0s, p1s)
-    assert l0 == want_losses and l1 == want_losses and l0s == want_losses
-    # (g + g) / 2 == g in fp32: both exchanges reproduce the one-process step bit for bit
-    # (the bound the verdict asks for is 1e-6 relative)
+    # the mean of two DIFFERENT gradients, through the segmented and the single-graph
+    # exchange, equals the one-process data-parallel step (the bound asked for is 1e-6
+    # relative; the sum of two fp32 values is order-free, so it holds bit for bit)
     assert rel_l2(p0, want) <= 1e-6 and torch.equal(p0, want)
     assert torch.equal(p0, p0s)
+    # the check can fail: one stage-1 bucket not exchanged -> replicas drift apart and away
+    # from the data-parallel step
+    (_, pk0), (_, pk1) = res[(0, "skip")], res[(1, "skip")]
+    assert not torch.equal(pk0, pk1)
+    assert rel_l2(pk0, want) > 1e-6 and rel_l2(pk1, want) > 1e-6

@@ -53,12 +53,14 @@ def test_device_rig_algebra_reproduces_reference_pillars_4cam():
     assert np.array_equal(pil, g["pillar"].reshape(-1))
 
 
-def test_captured_device_rig_algebra_hires_6cam_band():
-    """The capture-only fallback (BevModel.plan inside a HIP-graph capture with K/E on the
-    GPU, where no host copy can run): the fp64 device algebra vs the reference's fp32 LAPACK
-    combine at 6-cam 512^2.  LAPACK's last ulp is not reproducible on the device and a handful
-    of the 1.18M points sit within an ulp of a cell edge; the flip count is recorded.  Every
-    other rig path is bit-exact (0 flips): the next two tests."""
+def test_device_rig_algebra_hires_6cam_band():
+    """The device rig algebra entry point (e2ep_rig_transforms, lss.rig_transforms: fp64
+    Gauss-Jordan on the GPU) vs the reference's fp32 LAPACK combine at 6-cam 512^2.  LAPACK's
+    last ulp is not reproducible on the device and a handful of the 1.18M points sit within an
+    ulp of a cell edge; the flip count is recorded.  No product path plans with it since round
+    6 — a captured step reuses a plan built with the reference's fp32 host algebra before the
+    capture (test_captured_device_rig_plan_bit_exact_c4) — so every product path is bit-exact
+    (0 flips)."""
     from test_model_b8_gpu import _record
     g = golden("geometry_6cam_512.npz")
     from oracle import geom_c
@@ -93,6 +95,51 @@ def test_device_rig_pillar_index_bit_exact_end_to_end(rig):
             else:
                 flips = int((pil[b] != g["pillar"].reshape(-1)).sum())
                 assert flips == 0, flips
+
+
+def test_captured_device_rig_plan_bit_exact_c4(monkeypatch):
+    """C4 (6 x 512^2, B = 4) with the rig on the GPU inside a HIP-graph capture (reference
+    model/bev_model.py:45-57,85-96): the capture reuses the plan BevModel.plan built outside it
+    with the reference's fp32 host algebra — the same plan object, its pillar table equal to
+    the reference golden for every sample (0 flips, recorded) — and the captured lift-splat
+    replays bitwise what the eager call computes.  A device rig met first inside a capture
+    raises instead of planning with the device algebra."""
+    from e2ep_amd import _lib, graphs, lss
+    from model.bev_model import BevModel
+    from test_model_b8_gpu import _record
+    from tool.config import default_cfg
+    g = golden("geometry_6cam_512.npz")
+    bm = BevModel(default_cfg(final_dim=[512, 512], image_crop=512)).to(DEV)
+    B = 4
+    K = torch.from_numpy(g["K"])[None].repeat(B, 1, 1, 1).to(DEV)
+    E = torch.from_numpy(g["E"])[None].repeat(B, 1, 1, 1).to(DEV)
+    with monkeypatch.context() as mp_:  # the capture branch, without a real capture
+        mp_.setattr(torch.cuda, "is_current_stream_capturing", lambda: True)
+        with pytest.raises(_lib.E2EPError, match="before the capture"):
+            bm.plan(K, E, DEV)
+    plan = bm.plan(K, E, DEV)  # outside the capture: host algebra, pinned for the capture
+    N, D, hw = 6, 48, 64 * 64
+    gl = torch.Generator().manual_seed(3)
+    prob = torch.rand(B * N, D, 64, 64, generator=gl).to(DEV)
+    feat = torch.randn(B * N, 64, 64, 64, generator=gl).to(DEV)
+    seen = []
+
+    def body():
+        p = bm.plan(K, E, DEV)
+        seen.append(p)
+        return lss.lift_splat(prob, feat, p)
+
+    want = body().clone()
+    graph, out, _ = graphs.capture(body)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert seen[-1] is plan and seen[0] is plan
+    assert torch.equal(out, want)
+    pil = plan.pillar.view(B, -1).cpu().numpy().astype(np.int32)
+    ref = meta()["geometry_6cam_512"]["pillar_sha256"]
+    flips = sum(hashlib.sha256(pil[b].tobytes()).hexdigest() != ref for b in range(B))
+    _record("rig", "captured_device_rig_c4_b4_samples_off_golden", flips=int(flips), samples=B)
+    assert flips == 0
 
 
 @pytest.mark.parametrize("rig", ["geometry_4cam_256.npz", "geometry_6cam_512.npz"])
