@@ -112,7 +112,11 @@ __device__ __forceinline__ void bstore_t(__amdgpu_buffer_rsrc_t r, int byte_off,
 // BatchNorm / depthwise / squeeze-excitation kernels, the SE gate): e^-z as v_exp_f32 of
 // -z log2(e) and the reciprocal as v_rcp_f32 (1 ulp) instead of the correctly rounded divide
 // this library is built with (-fhip-fp32-correctly-rounded-divide-sqrt: ~10 instructions per
-// divide).  Within a few ulp of the divide form; those kernels run one or two sigmoids per
+// divide).  Error: rounding -log2(e) * z to fp32 before v_exp_f32 perturbs e^-z by a relative
+// |z| * 2^-24, so sigmoid_f / swish_f are within 2^-24 * (|z| + 4) relative of the exact value
+// (~20 ulp at |z| = 20, ~90 at |z| = 87; below z = -88 e^-z overflows and the result is 0, an
+// absolute error under 1e-38) — tests/test_nn_ops_gpu.py::test_sigmoid_swish_error_bound holds
+// them to that bound against fp64 over [-90, 90].  Those kernels run one or two sigmoids per
 // element and were ALU-bound on the 128² maps.  The losses keep expf (loss.hip).
 __device__ __forceinline__ float sigmoid_f(float z) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));

@@ -980,6 +980,21 @@ int e2ep_dwconv_bwd_pair_ok(const int *dims) {
           (dw_bwd_pair_plan(g, t, off) || dw_bwd_pair_s2_plan(g, p2))) ? 1 : 0;
 }
 
+int e2ep_dwconv_bf16_ok(const int *dims) {
+  const DwGeom g = dw_geom(dims);
+  if (!(g.N > 0 && g.C > 0 && g.P > 0 && g.Q > 0 && g.st > 0)) return 0;
+  if (!dw_strip_ok(g) || !dw_wgrad_strip_ok(g)) return 0;  // forward y, weight-gradient gy
+  if ((g.H * g.W) % 4 != 0 || (g.P * g.Q) % 4 != 0) return 0;  // the BatchNorms beside it
+  if (g.st == 1) {  // the stride-1 data gradient's strip path (e2ep_dwconv_dgrad)
+    DwGeom t = g;
+    t.H = g.P; t.W = g.Q; t.P = g.H; t.Q = g.W;
+    t.pt = g.K - 1 - g.pt; t.pl = g.K - 1 - g.pl;
+    return (dw_strip_ok(t) && t.pt >= 0 && t.pl >= 0 && t.pl <= DW_PADL) ? 1 : 0;
+  }
+  DwS2 p2;
+  return dw_s2_plan(g, p2) ? 1 : 0;  // the stride-2 data gradient's strip path
+}
+
 size_t e2ep_dwconv_wgrad_workspace(const int *dims) {
   DwGeom g = dw_geom(dims);
   return (size_t)g.C * dw_wgrad_splits(g) * g.K * g.K * sizeof(float);

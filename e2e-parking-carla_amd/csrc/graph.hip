@@ -8,6 +8,7 @@
 // instantiation, every memset node is replaced here by an equivalent kernel node (same
 // dependencies, same dependents) running k_memset_node; memcpy and kernel nodes are left
 // alone.
+#include <unordered_set>
 #include <vector>
 
 #include "common.h"
@@ -111,6 +112,44 @@ int e2ep_graph_exec_launch(void *exec, void *stream) {
 
 int e2ep_graph_exec_destroy(void *exec) {
   if (exec) E2EP_HIPCHECK(hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec)));
+  return 0;
+}
+
+// An unjoined side stream at hipStreamEndCapture: the round-2 / round-4 nested-fork captures
+// segfaulted there instead of failing.  `side`'s capture frontier (the nodes its next work
+// would depend on) must lie among the ancestors of `origin`'s frontier.
+int e2ep_capture_unjoined(void *origin, void *side, int *unjoined) {
+  E2EP_REQUIRE(unjoined, E2EP_EINVAL, "e2ep_capture_unjoined: null result");
+  *unjoined = 0;
+  hipStreamCaptureStatus so = hipStreamCaptureStatusNone, ss = hipStreamCaptureStatusNone;
+  unsigned long long io = 0, is = 0;
+  hipGraph_t go = nullptr, gs = nullptr;
+  const hipGraphNode_t *d = nullptr;
+  size_t n = 0;
+  E2EP_HIPCHECK(hipStreamGetCaptureInfo_v2(as_stream(origin), &so, &io, &go, &d, &n));
+  E2EP_REQUIRE(so == hipStreamCaptureStatusActive, E2EP_EINVAL,
+               "e2ep_capture_unjoined: the origin stream is not capturing");
+  std::vector<hipGraphNode_t> frontier(d, d + n);
+  d = nullptr;
+  n = 0;
+  E2EP_HIPCHECK(hipStreamGetCaptureInfo_v2(as_stream(side), &ss, &is, &gs, &d, &n));
+  if (ss != hipStreamCaptureStatusActive || is != io || n == 0) return 0;
+  std::vector<hipGraphNode_t> tail(d, d + n);
+  std::unordered_set<hipGraphNode_t> seen(frontier.begin(), frontier.end());
+  std::vector<hipGraphNode_t> stack(frontier);
+  std::vector<hipGraphNode_t> deps;
+  while (!stack.empty()) {
+    hipGraphNode_t x = stack.back();
+    stack.pop_back();
+    size_t nd = 0;
+    E2EP_HIPCHECK(hipGraphNodeGetDependencies(x, nullptr, &nd));
+    deps.resize(nd);
+    if (nd) E2EP_HIPCHECK(hipGraphNodeGetDependencies(x, deps.data(), &nd));
+    for (size_t k = 0; k < nd; ++k)
+      if (seen.insert(deps[k]).second) stack.push_back(deps[k]);
+  }
+  for (hipGraphNode_t t : tail)
+    if (!seen.count(t)) *unjoined = 1;
   return 0;
 }
 

@@ -13,9 +13,10 @@
 // (side-stream weight gradients, several captured graphs) never share a slot; a captured
 // launch keeps its range on every replay (kernels of one graph replay never overlap
 // themselves).  Launches captured into a graph take their ranges from a region that is
-// handed out once (HANDOFF_CAPTURED counters, not reused while the process lives unless it
-// runs out, ~500 captured train steps); eager launches rotate through the other region, so an
-// eager launch never shares a slot with a live graph's launch.
+// handed out once (HANDOFF_CAPTURED counters, never reused while the process lives; once they
+// run out, ~500 captured train steps, later captures get none and use separate reduce
+// launches); eager launches rotate through the other region, so an eager launch never shares
+// a slot with a live graph's launch.
 #pragma once
 #include "common.h"
 

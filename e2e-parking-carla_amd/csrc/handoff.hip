@@ -35,7 +35,9 @@ unsigned int *handoff_slots(int n, hipStream_t stream) {
   const int len = (n + 63) & ~63;  // 256-B aligned ranges
   int at;
   if (captured) {
-    if (p.captured + len > HANDOFF_CAPTURED) p.captured = 0;  // exhausted: reuse the oldest
+    // exhausted: no range (the caller runs its separate reduce launches).  Never wrap: the
+    // oldest ranges may belong to graphs that are still alive and replay concurrently
+    if (p.captured + len > HANDOFF_CAPTURED) return nullptr;
     at = p.captured;
     p.captured += len;
   } else {

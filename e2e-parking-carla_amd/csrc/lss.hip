@@ -683,29 +683,58 @@ __global__ void k_rig(const float *__restrict__ K, const float *__restrict__ E, 
 // instead of setting the kernel's tail.  One block per sample.
 //  * B = 8 (or lane_len = 0): per sample, all of its tiles; block id -> (sample id % B, rank
 //    id / B): one sample per XCD at B = 8, where its featT (1 MB) stays in that XCD's L2.
-//  * B = 1, 2, 4 (lane schedule, lane_len = ceil(nt / G) with G = 8 / B): each sample's tiles are
-//    cut into G contiguous pillar ranges (x bands of the BEV grid, seen by a subset of the
-//    cameras), and range g of sample s is the list of lane g * B + s: tiles[lane][0..lane_len),
-//    heaviest first, padded with -1.  Block id -> (lane id % 8, entry id / 8): a lane's blocks
-//    share one XCD (workgroups are dealt round-robin over the 8 XCDs — a placement used for
-//    speed only), so an XCD's L2 holds the features of part of one sample's cameras instead of
-//    all of them (C4, B = 4: 6.3 MB of featT per sample against a 4 MB L2; round 4 measured a
-//    51 % L2 hit rate for the per-sample order).
+//  * B = 1, 2, 4 (lane schedule, G = 8 / B lanes per sample): each sample's tiles are cut into G
+//    contiguous pillar ranges (x bands of the BEV grid, seen by a subset of the cameras), and
+//    range g of sample s is the list of lane g * B + s: tiles[lane][0..lane_len), heaviest
+//    first, padded with -1.  Block id -> (lane id % 8, entry id / 8): a lane's blocks share one
+//    XCD (workgroups are dealt round-robin over the 8 XCDs — a placement used for speed only),
+//    so an XCD's L2 holds the features of part of one sample's cameras instead of all of them
+//    (C4, B = 4: 6.3 MB of featT per sample against a 4 MB L2; round 4 measured a 51 % L2 hit
+//    rate for the per-sample order).  Round 6: the range boundaries balance POINTS, not tiles —
+//    the C4 rig's front band holds 1.8x the rear band's points (554 k vs 305 k per sample), so
+//    equal tile ranges left one XCD of each pair with 65 % of the sample's work.  A tile goes to
+//    the range its point midpoint falls in; ranges stay within lane_len tiles (lss_lane_len:
+//    1.5x the even share), else the even cut is kept.
 constexpr int SCHED_MAX_TILES = 4096;
+constexpr int SCHED_MAX_G = 8;
 __global__ void __launch_bounds__(1024) k_tile_schedule(const int *__restrict__ offsets, int XYZ,
                                                         int T, int B, int lane_len,
                                                         int *__restrict__ tiles) {
   __shared__ int cnt[SCHED_MAX_TILES];
+  __shared__ int bnd[SCHED_MAX_G + 1];
   const int b = blockIdx.x, nt = (XYZ + T - 1) / T;
   const int G = lane_len ? 8 / B : 1;
   const int *off = offsets + (long long)b * (XYZ + 1);
   for (int t = threadIdx.x; t < nt; t += blockDim.x)
     cnt[t] = off[min((t + 1) * T, XYZ)] - off[t * T];
+  if ((int)threadIdx.x <= G) bnd[threadIdx.x] = 0;
+  __syncthreads();
+  if (G > 1) {
+    // point-balanced cut: tile t belongs to range floor(G * mid(t) / total), mid(t) = the
+    // points before it + half its own (offsets are the exclusive prefix of the counts);
+    // bnd[g] = number of tiles of ranges < g
+    const long long total = off[XYZ] - off[0];
+    for (int t = threadIdx.x; t < nt; t += blockDim.x) {
+      const long long mid2 = 2LL * (off[t * T] - off[0]) + cnt[t];  // 2 * midpoint
+      const int g = total > 0 ? (int)min((long long)G - 1, (mid2 * G) / (2 * total)) : 0;
+      for (int u = g + 1; u <= G; ++u) atomicAdd(&bnd[u], 1);
+    }
+    __syncthreads();
+    bool fits = bnd[G] == nt;
+    for (int g = 0; g < G; ++g) fits = fits && bnd[g + 1] - bnd[g] <= lane_len;
+    __syncthreads();
+    if (!fits && (int)threadIdx.x <= G)  // the even cut
+      bnd[threadIdx.x] = (int)(((long long)threadIdx.x * nt + G - 1) / G);
+    __syncthreads();
+  } else if (threadIdx.x == 0) {
+    bnd[1] = nt;
+  }
   __syncthreads();
   for (int t = threadIdx.x; t < nt; t += blockDim.x) {
     const int c = cnt[t];
-    const int g = (int)(((long long)t * G) / nt);
-    const int lo = (int)(((long long)g * nt + G - 1) / G), hi = (int)(((long long)(g + 1) * nt + G - 1) / G);
+    int g = 0;
+    while (g + 1 < G && t >= bnd[g + 1]) ++g;
+    const int lo = bnd[g], hi = bnd[g + 1];
     int r = 0;
     for (int u = lo; u < hi; ++u) r += cnt[u] > c || (cnt[u] == c && u < t);
     if (lane_len) tiles[(long long)(g * B + b) * lane_len + r] = t;
@@ -713,17 +742,18 @@ __global__ void __launch_bounds__(1024) k_tile_schedule(const int *__restrict__ 
   }
   if (lane_len)  // padding past each range's end
     for (int g = 0; g < G; ++g) {
-      const int lo = (int)(((long long)g * nt + G - 1) / G), hi = (int)(((long long)(g + 1) * nt + G - 1) / G);
-      for (int r = hi - lo + threadIdx.x; r < lane_len; r += blockDim.x)
+      const int len = bnd[g + 1] - bnd[g];
+      for (int r = len + threadIdx.x; r < lane_len; r += blockDim.x)
         tiles[(long long)(g * B + b) * lane_len + r] = -1;
     }
 }
 
-// lane-schedule length (0 = per-sample order): B divides 8 and B < 8
+// lane-schedule length (0 = per-sample order): B divides 8 and B < 8.  1.5x the even share of
+// tiles, so point-balanced ranges fit (k_tile_schedule)
 static int lss_lane_len(int B, int XYZ) {
   const int nt = cdiv(XYZ, E2EP_LSS_TILE);
   if (B >= 8 || 8 % B != 0) return 0;
-  return cdiv(nt, 8 / B);
+  return cdiv(3 * cdiv(nt, 8 / B), 2);
 }
 
 __global__ void k_zero_i32(int *p, long long n) {
@@ -766,12 +796,16 @@ int e2ep_debug_fwd_trace(void *dev_buf) {
   return e == hipSuccess ? 0 : (int)e;
 }
 
-int e2ep_lss_tiles(int XYZ) { return cdiv(XYZ, E2EP_LSS_TILE) + 8; }  // + lane padding
+// per sample: room for the lane schedule's 8 * lss_lane_len(B, XYZ) entries at any B
+int e2ep_lss_tiles(int XYZ) { return 2 * cdiv(XYZ, E2EP_LSS_TILE) + 16; }
 
 int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int XYZ,
                   int32_t *offsets, int32_t *order, int32_t *tiles, void *workspace,
-                  void *stream) {
+                  size_t workspace_bytes, void *stream) {
   E2EP_REQUIRE(B > 0 && XYZ > 0, E2EP_EINVAL, "e2ep_lss_plan: bad shape");
+  E2EP_REQUIRE(workspace && workspace_bytes >= e2ep_lss_plan_workspace(B, XYZ), E2EP_EINVAL,
+               "e2ep_lss_plan: workspace %zu bytes < %zu (e2ep_lss_plan_workspace)",
+               workspace_bytes, e2ep_lss_plan_workspace(B, XYZ));
   E2EP_REQUIRE(N < 128 && D < 256 && h * w < 65536, E2EP_ERANGE,
                "e2ep_lss_plan: packed point code needs N<128, D<256, h*w<65536 (got %d,%d,%d)", N,
                D, h * w);
@@ -794,6 +828,8 @@ int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int 
     E2EP_REQUIRE(cdiv(XYZ, E2EP_LSS_TILE) <= SCHED_MAX_TILES, E2EP_ERANGE,
                  "e2ep_lss_plan: %d tiles per sample exceed the scheduler's %d (pass tiles=NULL)",
                  cdiv(XYZ, E2EP_LSS_TILE), SCHED_MAX_TILES);
+    E2EP_REQUIRE(8LL * lss_lane_len(B, XYZ) <= (long long)B * e2ep_lss_tiles(XYZ), E2EP_ERANGE,
+                 "e2ep_lss_plan: lane schedule exceeds the tile buffer");
     hipLaunchKernelGGL(k_tile_schedule, dim3(B), dim3(1024), 0, s, offsets, XYZ, E2EP_LSS_TILE, B,
                        lss_lane_len(B, XYZ), tiles);
   }

@@ -157,6 +157,74 @@ __global__ void __launch_bounds__(256) k_embed_tokens_bwd(
   }
 }
 
+// Autoregressive decode step (reference model/control_predict.py:70-75): softmax of one
+// logits row, argmax of the probabilities (torch.argmax: the first index of the largest
+// value), the token written into column `pos` of the persistent sequence.  Block per row; the
+// max and the sum reduce in a fixed order (deterministic).
+__global__ void __launch_bounds__(256) k_token_argmax_append(const float *__restrict__ logits,
+                                                             long long rstride, int V,
+                                                             int64_t *__restrict__ seq,
+                                                             int seq_stride, int pos) {
+  __shared__ float sf[4];
+  __shared__ int si[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float *row = logits + (size_t)b * rstride;
+  float m = -INFINITY;
+  for (int v = tid; v < V; v += 256) m = fmaxf(m, row[v]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) sf[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(sf[0], sf[1]), fmaxf(sf[2], sf[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int v = tid; v < V; v += 256) s += expf(row[v] - m);
+  s = wave_sum(s);
+  if (lane == 0) sf[wv] = s;
+  __syncthreads();
+  s = (sf[0] + sf[1]) + (sf[2] + sf[3]);
+  __syncthreads();
+  float best = -1.f;
+  int bi = 0x7fffffff;
+  for (int v = tid; v < V; v += 256) {
+    const float p = expf(row[v] - m) / s;
+    if (p > best) {  // v ascends per thread: the first index of a tie is kept
+      best = p;
+      bi = v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    sf[wv] = best;
+    si[wv] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (sf[w] > best || (sf[w] == best && si[w] < bi)) {
+        best = sf[w];
+        bi = si[w];
+      }
+    seq[(size_t)b * seq_stride + pos] = bi;
+  }
+}
+
+// seq[b][t] = t < L ? prefix[b][t] : pad   (grid B, block 64)
+__global__ void k_tokens_init(const int64_t *__restrict__ prefix, int pstride, int L,
+                              int64_t *__restrict__ seq, int T, int64_t pad) {
+  const int b = blockIdx.x;
+  for (int t = threadIdx.x; t < T; t += blockDim.x)
+    seq[(size_t)b * T + t] = t < L ? prefix[(size_t)b * pstride + t] : pad;
+}
+
 static int tok_check(float p, const int32_t *seed, long long n, const char *who) {
   E2EP_REQUIRE(p >= 0.f && p < 1.f && (p == 0.f || seed), E2EP_EINVAL, "%s: bad dropout p / seed", who);
   E2EP_REQUIRE(n > 0 && n < 0xffffffffLL, E2EP_ERANGE, "%s: %lld elements (need 1 .. 2^32)", who, n);
@@ -202,6 +270,25 @@ int e2ep_embed_tokens_fwd(const int64_t *tok, int tok_stride, const float *table
   hipLaunchKernelGGL(k_embed_tokens_fwd, dim3(B * T), dim3(256), 0, as_stream(stream), tok,
                      tok_stride, table, V, pos, T, E, p, seed, out);
   return launch_status("e2ep_embed_tokens_fwd");
+}
+
+int e2ep_tokens_init(const int64_t *prefix, int prefix_stride, int B, int L, int64_t *seq, int T,
+                     int64_t pad, void *stream) {
+  E2EP_REQUIRE(prefix && seq && B > 0 && L > 0 && T >= L && prefix_stride >= L, E2EP_EINVAL,
+               "e2ep_tokens_init: bad arguments");
+  hipLaunchKernelGGL(k_tokens_init, dim3(B), dim3(64), 0, as_stream(stream), prefix, prefix_stride,
+                     L, seq, T, pad);
+  return launch_status("e2ep_tokens_init");
+}
+
+int e2ep_token_argmax_append(const float *logits, long long row_stride, int B, int V,
+                             int64_t *seq, int seq_stride, int pos, void *stream) {
+  E2EP_REQUIRE(logits && seq && B > 0 && V > 0 && row_stride >= V && pos >= 0 &&
+                   pos < seq_stride,
+               E2EP_EINVAL, "e2ep_token_argmax_append: bad arguments");
+  hipLaunchKernelGGL(k_token_argmax_append, dim3(B), dim3(256), 0, as_stream(stream), logits,
+                     row_stride, V, seq, seq_stride, pos);
+  return launch_status("e2ep_token_argmax_append");
 }
 
 int e2ep_embed_tokens_bwd(const float *dout, const int64_t *tok, int tok_stride, int V, int B,

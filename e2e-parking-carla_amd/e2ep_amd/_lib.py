@@ -25,7 +25,7 @@ SIGNATURES = {
     "e2ep_lss_plan_workspace": (_sz, [_i, _i]),
     "e2ep_lss_tiles": (_i, [_i]),
     "e2ep_debug_fwd_trace": (_i, [_p]),
-    "e2ep_lss_plan": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
+    "e2ep_lss_plan": (_i, [_p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _sz, _p]),
     "e2ep_lss_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _i64, _p]),
     "e2ep_lss_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p]),
     "e2ep_transpose": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
@@ -118,6 +118,10 @@ SIGNATURES = {
     "e2ep_graph_exec_create": (_i, [_p, _p]),
     "e2ep_graph_exec_launch": (_i, [_p, _p]),
     "e2ep_graph_exec_destroy": (_i, [_p]),
+    "e2ep_capture_unjoined": (_i, [_p, _p, ctypes.POINTER(_i)]),
+    "e2ep_tokens_init": (_i, [_p, _i, _i, _i, _p, _i, _i64, _p]),
+    "e2ep_token_argmax_append": (_i, [_p, _i64, _i, _i, _p, _i, _i, _p]),
+    "e2ep_dwconv_bf16_ok": (_i, [_p]),
     "e2ep_control_ce_workspace": (_sz, [_i]),
     "e2ep_control_ce_fwd": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p]),
     "e2ep_control_ce_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _p]),

@@ -80,15 +80,49 @@ class Graph:
             pass
 
 
+def _side_streams():
+    """(name, stream) of every side stream the product forks inside a capture: the model
+    branches (streams.py) and the weight-gradient forks (conv._Fork)."""
+    from . import conv, streams
+    out = [("branch '%s' (device %d)" % (k[1], k[0]), st) for k, st in streams._STREAMS.items()]
+    out += [("weight-gradient side stream of stream 0x%x (device %d)" % (k[1], k[0]), st)
+            for k, st in conv._SIDE.items()]
+    return out
+
+
+def _join_check():
+    """Inside a capture, after the captured work: every side stream that took part in the
+    capture must have rejoined the origin stream (its last work an ancestor of the origin's
+    frontier).  An unjoined one is joined here, so the capture can still end cleanly, and
+    named in the E2EPError the caller raises (a nested fork once made hipStreamEndCapture
+    segfault instead: streams.py)."""
+    origin = torch.cuda.current_stream()
+    bad = []
+    for name, st in _side_streams():
+        if st.device != origin.device or st == origin:
+            continue
+        u = ctypes.c_int(0)
+        _lib.call("e2ep_capture_unjoined", ctypes.c_void_p(origin.cuda_stream),
+                  ctypes.c_void_p(st.cuda_stream), ctypes.byref(u))
+        if u.value:
+            origin.wait_stream(st)
+            bad.append(name)
+    return bad
+
+
 def capture(fn, pool=None):
     """Capture fn() into a repaired graph with its own executable (torch's, when fn drew from
     torch's generators: Graph).  Returns (Graph, fn's result, number of memset nodes
-    rewritten)."""
+    rewritten).  Raises E2EPError when fn left a forked side stream unjoined."""
     g = torch.cuda.CUDAGraph(keep_graph=True)
     seeded = _SeededOps()
     with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_mode()):
         with seeded:
             out = fn()
+        unjoined = _join_check()
+    if unjoined:
+        raise _lib.E2EPError("graphs.capture: side stream(s) forked inside the capture never "
+                             "rejoined the capturing stream: " + "; ".join(unjoined))
     n = ctypes.c_int(0)
     _lib.call("e2ep_graph_replace_memsets", ctypes.c_void_p(g.raw_cuda_graph()), ctypes.byref(n))
     return Graph(g, seeded.seen), out, n.value

@@ -95,7 +95,7 @@ def build_plan(frustum, combine, trans, lo, res, dims, device):
     tiles = torch.empty(B * _lib.call_raw("e2ep_lss_tiles", XYZ), dtype=torch.int32, device=device)
     ws = torch.empty(B * XYZ, dtype=torch.int32, device=device)
     _lib.call("e2ep_lss_plan", _lib.ptr(pillar), B, N, D, h, w, XYZ, _lib.ptr(offsets),
-              _lib.ptr(order), _lib.ptr(tiles), _lib.ptr(ws), s)
+              _lib.ptr(order), _lib.ptr(tiles), _lib.ptr(ws), _lib.nbytes(ws), s)
     return LssPlan(pillar, offsets, order, tiles, B, N, D, h, w, X, Y, Z)
 
 

@@ -461,9 +461,11 @@ class _BnActDwConv(torch.autograd.Function):
                           _lib.ptr(stats[0]), _lib.ptr(stats[1]), _lib.ptr(stats[2]),
                           _lib.ptr(stats[3]), _lib.ptr(ws), _lib.nbytes(ws), s, 0)
         # bf16 storage of the depthwise output (C3 training, _store_bf16)
-        hb = _store_bf16(train) and (P * Q) % 4 == 0
-        y = torch.empty(N, C, P, Q, dtype=torch.bfloat16 if hb else torch.float32, device=x.device)
         d = _lib.dims(dims)
+        # every kernel on either side of this layer must take the bf16 masks, or the layer
+        # keeps fp32 storage (e2ep_dwconv_bf16_ok: forward, data / weight gradients, the BNs)
+        hb = _store_bf16(train) and _lib.call_raw("e2ep_dwconv_bf16_ok", d) == 1
+        y = torch.empty(N, C, P, Q, dtype=torch.bfloat16 if hb else torch.float32, device=x.device)
         with timing.region(timing.name("dwconv_fwd", x.shape, "_BnActDwConv")):
             _lib.call("e2ep_dwconv_fwd_stats", _lib.ptr(x), _lib.ptr(w), d, _lib.ptr(stats[2]),
                       _lib.ptr(stats[3]), act, _lib.ptr(y), _lib.ptr(ystats), _lib.nbytes(ystats), s,

@@ -6,7 +6,7 @@ output).  `forward` is the teacher-forced training path, `predict` one autoregre
 import torch
 from torch import nn
 
-from e2ep_amd import nn_ops, transformer
+from e2ep_amd import _lib, nn_ops, transformer
 
 
 class ControlPredict(nn.Module):
@@ -67,3 +67,34 @@ class ControlPredict(nn.Module):
         emb = nn_ops.embed_tokens(tgt, self.embedding.weight, self.pos_embed)
         logits = self.project(self.decoder(encoder_out, emb, mask, padm))[:, length - 1, :]
         return torch.softmax(logits, dim=-1).argmax(dim=-1).view(-1, 1)
+
+    def predict_tokens(self, encoder_out, toks, steps):
+        """`steps` autoregressive predict() calls, each appending its token — the loop of
+        reference model/parking_model.py:72-78 over model/control_predict.py:60-75 — on one
+        persistent sequence buffer: the PAD padding, softmax, argmax and torch.cat of every
+        step are two e2ep launches in all (e2ep_tokens_init once, e2ep_token_argmax_append per
+        step), no host sync, HIP-graph capturable.  Returns the (B, L + steps) tokens (a view
+        of the buffer)."""
+        B, L = toks.shape
+        T = self.cfg.tf_de_tgt_dim - 1
+        if not (toks.is_cuda and toks.dtype == torch.long and L + steps <= T and steps > 0):
+            for _ in range(steps):  # the reference's own loop (it raises where L + steps > T)
+                toks = torch.cat([toks, self.predict(encoder_out, toks)], dim=1)
+            return toks
+        seq = torch.empty((B, T), dtype=torch.long, device=toks.device)
+        s = _lib.stream()
+        _lib.call("e2ep_tokens_init", _lib.ptr(toks), toks.stride(0), B, L, _lib.ptr(seq), T,
+                  self.pad_idx, s)
+        mask = None
+        for i in range(steps):
+            length = L + i
+            mask, padm = self.create_mask(seq)
+            emb = nn_ops.embed_tokens(seq, self.embedding.weight, self.pos_embed)
+            logits = self.project(self.decoder(encoder_out, emb, mask, padm))
+            V = logits.shape[-1]
+            row = logits[:, length - 1, :]
+            if row.stride(1) != 1:
+                row = row.contiguous()
+            _lib.call("e2ep_token_argmax_append", _lib.ptr(row), row.stride(0), B, V,
+                      _lib.ptr(seq), T, length, _lib.stream())
+        return seq[:, :L + steps]

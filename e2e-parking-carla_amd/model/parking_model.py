@@ -110,7 +110,7 @@ class ParkingModel(nn.Module):
     def predict(self, data, noise=None):
         (fuse_feature, pred_segmentation, pred_depth, bev_target), br = self._encoder_async(data, noise)
         toks = data["gt_control"].to(fuse_feature.device, non_blocking=True)
-        for _ in range(3):
-            nxt = self.control_predict.predict(fuse_feature, toks)
-            toks = torch.cat([toks, nxt], dim=1)
+        # three predict() calls, each appending its token (reference :72-78), on one token
+        # buffer: two e2ep launches for the padding / softmax / argmax / cat of all three
+        toks = self.control_predict.predict_tokens(fuse_feature, toks, 3)
         return toks, br.join(pred_segmentation), pred_depth, bev_target

@@ -29,6 +29,9 @@ extern "C" {
 int e2ep_abi_version(void);
 const char *e2ep_last_error(void);
 
+/* ABI 4 (round 6): e2ep_lss_plan takes workspace_bytes; new entry points
+ * e2ep_capture_unjoined, e2ep_tokens_init / e2ep_token_argmax_append, e2ep_dwconv_bf16_ok. */
+
 /* bf16 activation storage (ABI 3; BASELINE C3, the bf16 training mode): the entry points that
  * take an `io` mask read / write the named tensors as bf16 (torch.bfloat16 bits) instead of
  * fp32; their pointers are then void*.  The arithmetic stays fp32: a bf16 element is widened on
@@ -68,7 +71,7 @@ int e2ep_geom_index(const float *frustum, const float *combine, const float *tra
 size_t e2ep_lss_plan_workspace(int B, int XYZ);
 
 /* Pillars per output tile of e2ep_lss_fwd, and the tile-schedule entries to allocate per
- * sample: ceil(XYZ / E2EP_LSS_TILE) tiles + 8 entries of lane padding. */
+ * sample: 2 * ceil(XYZ / E2EP_LSS_TILE) + 16 (room for the lane schedule's padded lanes). */
 #define E2EP_LSS_TILE 64
 int e2ep_lss_tiles(int XYZ);
 
@@ -82,13 +85,14 @@ int e2ep_lss_tiles(int XYZ);
  *   tiles   [B*e2ep_lss_tiles(XYZ)] or NULL: the forward's launch schedule (any order of the
  *           tiles is correct): B = 8 (or any B not dividing 8): per sample its tiles, heaviest
  *           first, block -> (sample id % B, rank id / B); B = 1, 2, 4: lane schedule — each
- *           sample's tiles cut into G = 8/B contiguous pillar ranges, range g of sample s =
- *           lane g*B + s = tiles[lane * L .. +L) (L = ceil(tiles / G)), heaviest first, -1
+ *           sample's tiles cut into G = 8/B contiguous pillar ranges of balanced point counts (each
+ *           at most L tiles, else the even cut), range g of sample s = lane g*B + s =
+ *           tiles[lane * L .. +L) (L = ceil(1.5 * ceil(tiles / G))), heaviest first, -1
  *           padded, block -> (lane id % 8, entry id / 8): a lane's blocks share an XCD and its L2.
  * Limits: N < 128, D < 256, h*w < 65536; with tiles, ceil(XYZ / E2EP_LSS_TILE) <= 4096. */
 int e2ep_lss_plan(const int32_t *pillar, int B, int N, int D, int h, int w, int XYZ,
                   int32_t *offsets, int32_t *order, int32_t *tiles, void *workspace,
-                  void *stream);
+                  size_t workspace_bytes, void *stream);
 
 /* Fused depth-distribution x feature outer product + pillar sum-pooling, forward.
  * Replaces encoder_forward's outer product/permute (model/bev_model.py:64-71) and
@@ -543,6 +547,12 @@ int e2ep_dwconv_dgrad(const void *gy, const float *w, const int *dims, void *dx,
  * two separately.  Workspace: e2ep_dwconv_wgrad_workspace.  Results bitwise those of the two
  * separate launches. */
 int e2ep_dwconv_bwd_pair_ok(const int *dims);
+/* 1 when every kernel on either side of this depthwise conv takes the bf16 storage masks
+ * (E2EP_IO_*): the forward strip kernel (y bf16), the data gradient (strip or stride-2 strip
+ * kernel, gy / dx bf16), the weight-gradient strip kernel (gy bf16) and the BatchNorms on
+ * its input and output planes (H*W and P*Q multiples of 4); else 0 — the caller keeps fp32
+ * storage for that layer instead of failing partway through a step. */
+int e2ep_dwconv_bf16_ok(const int *dims);
 int e2ep_dwconv_bwd(const void *gy, const float *x, const float *w, const int *dims,
                     const float *in_scale, const float *in_shift, int in_act, void *dx,
                     void *workspace, size_t workspace_bytes, float *dw, void *stream,
@@ -591,6 +601,17 @@ int e2ep_fusion_tokens_bwd(const float *dtokens, int B, int C, int S, int E, flo
 int e2ep_embed_tokens_fwd(const int64_t *tok, int tok_stride, const float *table, int V,
                           const float *pos, int B, int T, int E, float p, const int32_t *seed,
                           float *out, void *stream);
+/* Autoregressive control decoding on a persistent token buffer (reference
+ * model/parking_model.py:72-78 calling model/control_predict.py:60-75 three times: pad with
+ * PAD, softmax, argmax, torch.cat — here two kernels, no host sync, capturable):
+ *   e2ep_tokens_init: seq[b, t] = t < L ? prefix[b * prefix_stride + t] : pad   (B x T)
+ *   e2ep_token_argmax_append: seq[b, pos] = argmax_v softmax(logits[b * row_stride + v])
+ *     over v < V: the softmax values as exp(x - max) / sum, argmax = first index of the largest
+ *     probability (torch.argmax's rule).  One workgroup per row. */
+int e2ep_tokens_init(const int64_t *prefix, int prefix_stride, int B, int L, int64_t *seq, int T,
+                     int64_t pad, void *stream);
+int e2ep_token_argmax_append(const float *logits, long long row_stride, int B, int V,
+                             int64_t *seq, int seq_stride, int pos, void *stream);
 int e2ep_embed_tokens_bwd(const float *dout, const int64_t *tok, int tok_stride, int V, int B,
                           int T, int E, float p, const int32_t *seed, float *dtable, float *dpos,
                           void *stream);
@@ -797,6 +818,11 @@ int e2ep_graph_replace_memsets(void *graph, int *replaced);
  * torch.cuda.CUDAGraph.replay(), whose prologue launches int64 fill kernels to refresh torch's
  * generator states (the step's random numbers come from e2ep_rng_draw). */
 int e2ep_graph_exec_create(void *graph, void **exec);
+/* Before ending a capture on `origin`: *unjoined = 1 when `side` is part of the same capture
+ * and its last captured work is not an ancestor of origin's current capture frontier (a
+ * forked stream that was never joined back; hipStreamEndCapture would fail or crash on it),
+ * else 0.  Host-side graph inspection only (hipStreamGetCaptureInfo_v2). */
+int e2ep_capture_unjoined(void *origin, void *side, int *unjoined);
 int e2ep_graph_exec_launch(void *exec, void *stream);
 int e2ep_graph_exec_destroy(void *exec);
 

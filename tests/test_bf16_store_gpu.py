@@ -313,3 +313,36 @@ def test_bf16_store_only_in_bf16_training():
                 assert nn_ops.bn_act_depthwise_conv2d(x, bn, "swish", w, 1, (1, 1, 1, 1)).dtype == torch.float32
     finally:
         nn_ops.set_bf16_store(prev)
+
+
+@pytest.mark.parametrize("case", [(2, 32, 30, 30, 3, 1, (1, 1, 1, 1)),   # W % 4 != 0
+                                  (2, 32, 18, 18, 5, 2, (2, 2, 2, 2)),   # stride-2 output 9x9
+                                  (2, 16, 20, 20, 3, 2, (1, 1, 1, 1))])  # 10x10 output: no strip kernel
+def test_bf16_store_non_strip_geometry_keeps_fp32(case):
+    """A layer whose geometry some kernel beside it cannot store in bf16 (no strip kernel,
+    P*Q % 4 != 0, ...) keeps fp32 storage under E2EP_BF16_STORE (e2ep_dwconv_bf16_ok, ADVICE
+    r5) instead of raising E2EP_EINVAL partway through the step; forward and backward run and
+    equal the fp32-storage step bitwise."""
+    from e2ep_amd import _lib, nn_ops, precision
+    N, C, H, W, K, s, pad = case
+    dims, P, Q = _dims(case)
+    assert _lib.call_raw("e2ep_dwconv_bf16_ok", _lib.dims(dims)) == 0
+    g = _g(C + H + K)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, 1, K, K, generator=g) / K
+    res = {}
+    with precision.use("bf16"):
+        for store in (0, 2):
+            prev = nn_ops.set_bf16_store(store)
+            try:
+                bn = _bn(C, _g(C + 7))
+                xd = x.to(DEV).requires_grad_(True)
+                wd = w.to(DEV).requires_grad_(True)
+                y = nn_ops.bn_act_depthwise_conv2d(xd, bn, "swish", wd, s, pad)
+                y.backward(torch.ones_like(y))
+                res[store] = (y.detach(), xd.grad, wd.grad)
+            finally:
+                nn_ops.set_bf16_store(prev)
+    assert res[2][0].dtype == torch.float32
+    for a, b in zip(res[0], res[2]):
+        assert torch.equal(a, b)

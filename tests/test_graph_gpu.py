@@ -125,3 +125,30 @@ def test_torch_rng_in_capture_draws_fresh_values_per_replay():
     g2.replay()
     torch.cuda.synchronize()
     assert float(buf[0]) == 2.0
+
+
+def test_capture_raises_on_unjoined_side_stream():
+    """graphs.capture checks, before the capture ends, that every side stream forked into it
+    (model branches, weight-gradient forks) rejoined the capturing stream
+    (e2ep_capture_unjoined): a fork left open raises E2EPError naming the stream (joined
+    first, so the capture still ends cleanly) instead of reaching hipStreamEndCapture; a
+    joined fork captures and replays."""
+    from e2ep_amd import _lib, conv, graphs
+    dev = torch.device("cuda", torch.cuda.current_device())
+    buf = torch.zeros(1024, device="cuda")
+
+    def body(join):
+        def f():
+            with conv._Fork(dev) as side:
+                buf.add_(1)
+            if join:
+                side.join()
+            buf.mul_(2)
+        return f
+    g, _, _ = graphs.capture(body(True))
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(buf[0]) == 2.0
+    with pytest.raises(_lib.E2EPError, match="never rejoined"):
+        graphs.capture(body(False))
+    torch.cuda.synchronize()

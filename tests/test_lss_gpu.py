@@ -195,23 +195,34 @@ def test_plan_invariants_batch_of_different_rigs():
             assert np.all(np.diff(seg) > 0)
     assert not np.array_equal(pil[0], pil[1])
     # forward tile schedule at B = 2 (lane schedule, include/e2ep.h): 8 lanes; lane l holds
-    # pillar range g = l // 2 of sample l % 2 (G = 4 contiguous ranges per sample), heaviest
-    # tile first (ties by index), -1 padded; each sample's tiles appear exactly once
+    # pillar range g = l // 2 of sample l % 2: G = 4 contiguous ranges per sample that cover
+    # every tile once, with point-balanced boundaries (a tile belongs to the range its point
+    # midpoint falls in) of at most L = ceil(1.5 ceil(nt / G)) tiles, heaviest first (ties by
+    # index), -1 padded
     T, B, G = 64, 2, 4
     nt = -(-40000 // T)
-    L = -(-nt // G)
+    L = -(-3 * -(-nt // G) // 2)
     lanes = plan.tiles.cpu().numpy()[:8 * L].reshape(8, L)
     for b in range(B):
         edges = np.minimum(np.arange(nt + 1) * T, 40000)
         cnt = off[b][edges[1:]] - off[b][edges[:-1]]
+        before = off[b][edges[:-1]] - off[b][0]
+        total = int(off[b][-1] - off[b][0])
+        rng = np.minimum(G - 1, ((2 * before + cnt) * G) // (2 * total))
+        bnd = np.searchsorted(rng, np.arange(G + 1), side="left")
+        even = np.diff(bnd).max() > L
+        if even:
+            bnd = -(-np.arange(G + 1) * nt // G)  # the even cut
         seen = []
         for g in range(G):
-            lo, hi = -(-g * nt // G), -(-(g + 1) * nt // G)
+            lo, hi = bnd[g], bnd[g + 1]
             lane = lanes[g * B + b]
             want = lo + np.lexsort((np.arange(hi - lo), -cnt[lo:hi]))
             assert np.array_equal(lane[:hi - lo], want)
             assert np.all(lane[hi - lo:] == -1)
             seen.extend(lane[:hi - lo])
+            # balanced: a range's points within one tile of the even share
+            assert even or abs(int(cnt[lo:hi].sum()) - total / G) <= cnt.max()
         assert np.array_equal(np.sort(seen), np.arange(nt))
 
 
@@ -375,3 +386,22 @@ def test_lss_hires_6cam_512_vs_fp64():
     assert rel_l2(bev, ref) < 1e-5 and max_scaled(bev, ref) < 1e-5
     assert rel_l2(p.grad.reshape(N, -1), gp_ref) < 1e-5
     assert rel_l2(f.grad.reshape(N, C, h * w).transpose(1, 2), gf_ref) < 1e-5
+
+
+def test_lss_plan_refuses_short_workspace():
+    """e2ep_lss_plan checks workspace_bytes against e2ep_lss_plan_workspace (ABI 4)."""
+    from e2ep_amd import _lib
+    B, N, D, h, w, XYZ = 1, 4, 48, 32, 32, 40000
+    P = N * D * h * w
+    pillar = torch.full((B * P,), -1, dtype=torch.int32, device=DEV)
+    offsets = torch.empty(B * (XYZ + 1), dtype=torch.int32, device=DEV)
+    order = torch.empty(B * P, dtype=torch.int32, device=DEV)
+    need = _lib.call_raw("e2ep_lss_plan_workspace", B, XYZ)
+    ws = torch.empty(need // 4, dtype=torch.int32, device=DEV)
+    with pytest.raises(_lib.E2EPError, match="workspace"):
+        _lib.call("e2ep_lss_plan", _lib.ptr(pillar), B, N, D, h, w, XYZ, _lib.ptr(offsets),
+                  _lib.ptr(order), None, _lib.ptr(ws), need - 4, _lib.stream())
+    _lib.call("e2ep_lss_plan", _lib.ptr(pillar), B, N, D, h, w, XYZ, _lib.ptr(offsets),
+              _lib.ptr(order), None, _lib.ptr(ws), need, _lib.stream())
+    torch.cuda.synchronize()
+    assert int(offsets[-1]) == 0

@@ -652,3 +652,48 @@ def test_step_rng_draws():
     assert u.shape == (22, 32) and v.shape == (8, 2) and u.data_ptr() != v.data_ptr()
     rng.end_step()
     assert rng.uniform((3,), DEV).shape == (3,)
+
+
+def test_sigmoid_swish_error_bound():
+    """common.h sigmoid_f / swish_f (v_exp_f32 of the fp32-rounded -z log2(e), v_rcp_f32),
+    used by every swish, swish derivative and SE gate of the BN / depthwise / SE kernels,
+    against fp64 on the same fp32 z over [-90, 90] (the error grows with |z|, it
+    is not "a few ulp"): relative error <= 2^-24 (|z| + 5) wherever sigmoid(z) is a normal fp32
+    number (z > -87.3); below that the reciprocal's denormal result is flushed to 0, an
+    absolute error under 2^-126 (sigmoid) / 91 * 2^-126 (swish).  Probed through
+    e2ep_se_gate_fwd (x = 1: sigmoid(a)) and e2ep_act_fwd (swish); the measured worst ratio to
+    the bound is printed and recorded."""
+    import numpy as np
+    from e2ep_amd import _lib
+    from test_model_b8_gpu import _record
+    z = torch.cat([torch.linspace(-90, 90, 1 << 20), torch.tensor([0.0, -0.0, 1e-30, -1e-30,
+                   -87.2, -87.4, -87.9, -88.0, -88.7, -89.0, 87.9, 88.7])]).float()
+    zd = z.to(DEV)
+    n = z.numel()
+    sig = torch.empty_like(zd)
+    _lib.call("e2ep_se_gate_fwd", _lib.ptr(torch.ones_like(zd)), _lib.ptr(zd), n, 1,
+              _lib.ptr(sig), _lib.stream())
+    sw = torch.empty_like(zd)
+    _lib.call("e2ep_act_fwd", _lib.ptr(zd), n, 2, _lib.ptr(sw), _lib.stream())
+    z64 = z.double().numpy()
+    ref_s = 1.0 / (1.0 + np.exp(-z64))
+    ref_w = z64 * ref_s
+    got_s, got_w = sig.cpu().double().numpy(), sw.cpu().double().numpy()
+    tiny = 2.0 ** -126
+    nrm = ref_s >= tiny
+    bound = 2.0 ** -24 * (np.abs(z64) + 5.0)
+    rs = np.abs(got_s - ref_s)[nrm] / ref_s[nrm]
+    nz = nrm & (z64 != 0)
+    rw = np.abs(got_w - ref_w)[nz] / np.abs(ref_w[nz])
+    worst_s = float(np.max(rs / bound[nrm]))
+    worst_w = float(np.max(rw / bound[nz]))
+    at = float(z64[nrm][np.argmax(rs / bound[nrm])])
+    print(f"sigmoid_f worst rel err / bound {worst_s:.3f} (at z = {at:.3f}), swish_f "
+          f"{worst_w:.3f}; max rel {rs.max():.3e} / {rw.max():.3e}")
+    _record("activation", "sigmoid_swish_vs_fp64", sigmoid_worst_over_bound=worst_s,
+            swish_worst_over_bound=worst_w, sigmoid_max_rel=float(rs.max()),
+            swish_max_rel=float(rw.max()), worst_at_z=at)
+    assert worst_s <= 1.0 and worst_w <= 1.0
+    assert np.all(np.abs(got_s - ref_s)[~nrm] <= tiny)
+    assert np.all(np.abs(got_w - ref_w)[~nrm] <= 91 * tiny)
+    assert got_w[z64 == 0].tolist() == [0.0, 0.0]

@@ -120,3 +120,30 @@ def test_embed_tokens_out_of_range_raises_like_embedding():
             nn_ops.embed_tokens(tok, table, pos)
         with pytest.raises(IndexError):
             torch.nn.functional.embedding(tok.cpu(), table.cpu())
+
+
+@pytest.mark.parametrize("B,V", [(1, 204), (8, 204), (3, 1000), (2, 7)])
+def test_token_argmax_append_matches_softmax_argmax(B, V):
+    """e2ep_token_argmax_append (the AR loop's softmax + argmax + cat, reference
+    model/control_predict.py:72-75, model/parking_model.py:75-77) writes
+    torch.softmax(row).argmax() into column `pos` of the token buffer and nothing else;
+    planted exact ties pick the first index, as torch.argmax; e2ep_tokens_init pads with PAD."""
+    from e2ep_amd import _lib
+    g = torch.Generator().manual_seed(B * V)
+    T, L, pad = 14, 2, V - 1
+    logits = torch.randn(B, T, V, generator=g) * 3
+    logits[:, L - 1, V // 3] = logits[:, L - 1, 2 * V // 3] = logits[:, L - 1].max(-1).values + 1.0
+    logits = logits.to(DEV)
+    prefix = torch.randint(0, V, (B, 4), generator=g).to(DEV)
+    seq = torch.full((B, T), -5, dtype=torch.long, device=DEV)
+    s = _lib.stream()
+    _lib.call("e2ep_tokens_init", _lib.ptr(prefix), prefix.stride(0), B, L, _lib.ptr(seq), T, pad, s)
+    want = seq.clone()
+    assert torch.equal(want[:, :L], prefix[:, :L]) and bool((want[:, L:] == pad).all())
+    for pos in (L, L + 1):
+        row = logits[:, pos - 1, :]
+        _lib.call("e2ep_token_argmax_append", _lib.ptr(row), row.stride(0), B, V, _lib.ptr(seq),
+                  T, pos, s)
+        want[:, pos] = torch.softmax(row, dim=-1).argmax(dim=-1)
+    assert torch.equal(seq, want)
+    assert bool((seq[:, L] == V // 3).all())  # the first of the two tied maxima
