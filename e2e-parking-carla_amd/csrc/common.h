@@ -113,10 +113,12 @@ __device__ __forceinline__ void bstore_t(__amdgpu_buffer_rsrc_t r, int byte_off,
 // -z log2(e) and the reciprocal as v_rcp_f32 (1 ulp) instead of the correctly rounded divide
 // this library is built with (-fhip-fp32-correctly-rounded-divide-sqrt: ~10 instructions per
 // divide).  Error: rounding -log2(e) * z to fp32 before v_exp_f32 perturbs e^-z by a relative
-// |z| * 2^-24, so sigmoid_f / swish_f are within 2^-24 * (|z| + 4) relative of the exact value
-// (~20 ulp at |z| = 20, ~90 at |z| = 87; below z = -88 e^-z overflows and the result is 0, an
-// absolute error under 1e-38) — tests/test_nn_ops_gpu.py::test_sigmoid_swish_error_bound holds
-// them to that bound against fp64 over [-90, 90].  Those kernels run one or two sigmoids per
+// |z| * 2^-24 (v_exp_f32 / v_rcp_f32 add a few ulp), so sigmoid_f / swish_f are within
+// 2^-24 * (2 |z| + 8) relative of the exact value — measured worst 3.9e-6 (~65 ulp) at
+// z = -44; where sigmoid(z) is no longer a normal fp32 number (z < -87.3) the reciprocal's
+// denormal is flushed to 0, an absolute error under 2^-126.
+// tests/test_nn_ops_gpu.py::test_sigmoid_swish_error_bound holds them to that bound against
+// fp64 over [-90, 90].  Those kernels run one or two sigmoids per
 // element and were ALU-bound on the 128² maps.  The losses keep expf (loss.hip).
 __device__ __forceinline__ float sigmoid_f(float z) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));

@@ -1,7 +1,6 @@
 // Internal interface shared by the convolution kernel files (conv.hip, conv_lp.hip).
 #pragma once
 #include "common.h"
-#include "handoff.h"
 
 namespace e2ep {
 
@@ -63,17 +62,6 @@ struct TapList {
   int tap[MAXTAPS];
 };
 
-// In-launch fold of a weight gradient's split-K slabs (e2ep_tune key 34 = 2): every workgroup
-// of an output tile stores its slab write-through (handoff.h), and the tile's last arrival of
-// `gz` sums the tile's slabs in split order — k_reduce_splits4's order — straight into dw, so no
-// k_reduce_splits launch follows.  cnt == nullptr: slabs only (reduced after the launch).  Only
-// where every filter tap is live (the reduction writes a dead tap's gradient as 0) and dw is
-// overwritten, not accumulated.  One slab (gz == 1): the workgroup writes dw directly.
-struct WFold {
-  unsigned int *cnt;
-  float *dw;
-};
-
 // Implicit-GEMM forward (mode 0) / data gradient (mode 1) with 32-deep K-steps and up to
 // 128-row tiles, conv_lp.hip: bf16 / fp16 operands (op 1 / 2), and fp32 (op 0) where
 // TUNE_LP32 selects it.  lp_workspace() bytes of split-K workspace (0: none); lp_launch() returns an
@@ -95,11 +83,9 @@ int lp_stats_tiles(const ConvGeom &g, int op);
 // lp_wgrad_launch returns the slabs written.
 bool lp_wgrad_ok(const ConvGeom &g, const TapList &tl);
 int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op);
-// xb: x is bf16 (op 1 only).  fold_dw != nullptr asks for the in-launch fold into fold_dw
-// (WFold; the caller checked taps / accumulation); *folded says whether it ran folded.
+// xb: x is bf16 (op 1 only)
 int lp_wgrad_launch(const float *gout, const void *x, const ConvGeom &g, const TapList &tl,
-                    int splits, float *part, hipStream_t s, int op, bool xb = false,
-                    float *fold_dw = nullptr, bool *folded = nullptr);
+                    int splits, float *part, hipStream_t s, int op, bool xb = false);
 
 // A conv layer's data gradient on k_conv_lp (route ROUTE_LP / ROUTE_LP32 of conv.hip) and
 // weight gradient (op 1: k_wgrad_lp; op 0: the k_conv_wgrad2-equivalent 64 x 64 tile) in one
@@ -110,7 +96,6 @@ bool lp_bwd_pair_ok(const ConvGeom &g, int M, int op, const TapList &tl);
 int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void *dx,
                        long long dx_bytes, const ConvGeom &g, int M, int op, void *ws_dgrad,
                        const void *x, const TapList &tl, int wsplits, float *part2,
-                       hipStream_t s, bool xb = false, float *fold_dw = nullptr,
-                       bool *folded = nullptr);
+                       hipStream_t s, bool xb = false);
 
 }  // namespace e2ep

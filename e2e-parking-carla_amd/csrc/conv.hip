@@ -911,8 +911,7 @@ constexpr int W2_LDS_FLOATS = 2 * 2 * 64 * W2LD;  // As[2][64][W2LD] (co x pixel
 template <int OP>
 __device__ __forceinline__ void conv_wgrad2_block(
     const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
-    ConvGeom g, int pix_per_split, TapList tl, int bx, int by, int bz, int gz, float *lds,
-    WFold wf = WFold{nullptr, nullptr}, int gx = 0) {
+    ConvGeom g, int pix_per_split, TapList tl, int bx, int by, int bz, int gz, float *lds) {
   float(*As)[64][W2LD] = reinterpret_cast<float(*)[64][W2LD]>(lds);                 // As[co][pixel]
   float(*Bs)[64][W2LD] = reinterpret_cast<float(*)[64][W2LD]>(lds + 2 * 64 * W2LD);  // Bs[column][pixel]
   __shared__ int s_tap[MAXTAPS];
@@ -1048,53 +1047,21 @@ __device__ __forceinline__ void conv_wgrad2_block(
   const int lcol = n0 + 32 * wn + li;
   const int lci = lcol < Kl ? lcol / tl.n : 0;
   const int col = lci * RS + s_tap[lcol < Kl ? lcol - lci * tl.n : 0];  // dW column
-  if (wf.cnt && gz == 1) {  // one slab: the gradient itself
-#pragma unroll
-    for (int rr = 0; rr < 16; ++rr) {
-      const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-      if (co < g.Cout && lcol < Kl) wf.dw[co * Kw + col] = acc[rr];
-    }
-    return;
-  }
 #pragma unroll
   for (int rr = 0; rr < 16; ++rr) {
     const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
     const bool ok = co < g.Cout && lcol < Kl;
-    if (wf.cnt) bstore_sc1(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[rr]);
-    else bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[rr]);
-  }
-  if (!wf.cnt) return;
-  // WFold: the tile's last arrival sums the slabs in split order into dw
-  __shared__ int s_wlast;
-  handoff_drain();
-  if (!handoff_arrive(wf.cnt + bx + gx * by, gz, &s_wlast)) return;
-#pragma unroll
-  for (int rr = 0; rr < 16; ++rr) {
-    const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-    acc[rr] = bload_sc1(rp, (co < g.Cout && lcol < Kl) ? (co * Kw + col) * 4 : OOR);
-  }
-#pragma unroll 2
-  for (int k = 1; k < gz; ++k) {
-#pragma unroll
-    for (int rr = 0; rr < 16; ++rr) {
-      const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-      acc[rr] += bload_sc1(rp, (co < g.Cout && lcol < Kl) ? ((k * g.Cout + co) * Kw + col) * 4 : OOR);
-    }
-  }
-#pragma unroll
-  for (int rr = 0; rr < 16; ++rr) {
-    const int co = m0 + 32 * wm + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-    if (co < g.Cout && lcol < Kl) wf.dw[co * Kw + col] = acc[rr];
+    bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[rr]);
   }
 }
 
 template <int OP>
 __global__ void __launch_bounds__(256) k_conv_wgrad2(
     const float *__restrict__ gout, const float *__restrict__ x, float *__restrict__ part,
-    ConvGeom g, int pix_per_split, TapList tl, WFold wf) {
+    ConvGeom g, int pix_per_split, TapList tl) {
   __shared__ __attribute__((aligned(16))) float lds[W2_LDS_FLOATS];
   conv_wgrad2_block<OP>(gout, x, part, g, pix_per_split, tl, blockIdx.x, blockIdx.y, blockIdx.z,
-                        gridDim.z, lds, wf, gridDim.x);
+                        gridDim.z, lds);
 }
 
 // A conv layer's data gradient (k_conv_gemm MODE 1, fp32) and spatial / small-map weight
@@ -1108,7 +1075,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_bwd_pair(
     float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
     const float *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
-    int gx2, int gy2, int gz2, WFold wf) {
+    int gx2, int gy2, int gz2) {
   constexpr int L1 = conv_gemm_lds_floats<BNT, BMT>();
   constexpr int L = L1 > W2_LDS_FLOATS ? L1 : W2_LDS_FLOATS;
   __shared__ __attribute__((aligned(16))) float lds[L];
@@ -1123,7 +1090,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_bwd_pair(
   } else {
     id -= n1;
     conv_wgrad2_block<0>(gout, x, part2, g, pix_per_split, tl, id % gx2, (id / gx2) % gy2,
-                         id / (gx2 * gy2), gz2, lds, wf, gx2);
+                         id / (gx2 * gy2), gz2, lds);
   }
 }
 
@@ -1188,7 +1155,7 @@ __device__ __forceinline__ void wgrad1x1_block(const float *__restrict__ gout,
                                                const float *__restrict__ x,
                                                float *__restrict__ part, ConvGeom g, int splits,
                                                int groups_per_split, int bt, int split,
-                                               float (*red)[64], WFold wf = WFold{nullptr, nullptr}) {
+                                               float (*red)[64]) {
   // wave tile (32*TI co) x (32*TJ ci): TI*TJ accumulators share each loaded operand
   constexpr int NT = TI * TJ;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1269,42 +1236,13 @@ __device__ __forceinline__ void wgrad1x1_block(const float *__restrict__ gout,
   }
   // C layout: element r of lane l is (i, j) = ((r&3) + 8*(r>>2) + 4*(l>>5), l&31)
   const int Kw = g.Cin;
-  const bool direct = wf.cnt && splits == 1;  // WFold, one slab: the gradient itself
   for (int e = threadIdx.x; e < NT * 16 * 64; e += 256) {
     const int tr = e >> 6, l = e & 63;
     const int t = tr >> 4, r = tr & 15;
     const int i = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = l & 31;
     const int oc = ti * 32 * TI + 32 * (t / TJ) + i, ic = tj * 32 * TJ + 32 * (t % TJ) + j;
     if (oc < g.Cout && ic < g.Cin) {
-      if (direct) wf.dw[(long long)oc * Kw + ic] = red[tr][l];
-      else if (wf.cnt) st_sc1(&part[((long long)split * g.Cout + oc) * Kw + ic], red[tr][l]);
-      else part[((long long)split * g.Cout + oc) * Kw + ic] = red[tr][l];
-    }
-  }
-  if (!wf.cnt || direct) return;
-  // WFold: the tile's last arrival sums the slabs in split order into dw
-  __shared__ int s_wlast;
-  handoff_drain();
-  if (!handoff_arrive(wf.cnt + bt, splits, &s_wlast)) return;
-  const long long MN = (long long)g.Cout * Kw;
-  for (int e = threadIdx.x; e < NT * 16 * 64; e += 256) {
-    const int tr = e >> 6, l = e & 63;
-    const int t = tr >> 4, r = tr & 15;
-    const int i = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = l & 31;
-    const int oc = ti * 32 * TI + 32 * (t / TJ) + i, ic = tj * 32 * TJ + 32 * (t % TJ) + j;
-    if (oc < g.Cout && ic < g.Cin) {
-      const long long o = (long long)oc * Kw + ic;
-      float v = ld_sc1(&part[o]);
-      int k = 1;
-      for (; k + 8 <= splits; k += 8) {  // 8 slabs in flight, added in split order
-        float t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = ld_sc1(&part[(k + u) * MN + o]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v += t[u];
-      }
-      for (; k < splits; ++k) v += ld_sc1(&part[k * MN + o]);
-      wf.dw[o] = v;
+      part[((long long)split * g.Cout + oc) * Kw + ic] = red[tr][l];
     }
   }
 }
@@ -1313,10 +1251,10 @@ template <int TI, int TJ, int OP>
 __global__ void __launch_bounds__(256) k_wgrad_1x1(const float *__restrict__ gout,
                                                    const float *__restrict__ x,
                                                    float *__restrict__ part, ConvGeom g,
-                                                   int splits, int groups_per_split, WFold wf) {
+                                                   int splits, int groups_per_split) {
   __shared__ float red[TI * TJ * 16][64];
   wgrad1x1_block<TI, TJ, OP>(gout, x, part, g, splits, groups_per_split, blockIdx.x, blockIdx.y,
-                             red, wf);
+                             red);
 }
 
 // A 1x1 conv layer's data gradient (k_conv_gemm MODE 1, fp32) and weight gradient (the
@@ -1330,7 +1268,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_bwd_pair1x1(
     float *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
     const float *__restrict__ x, float *__restrict__ part2, int splits2, int gps, int nt2,
-    int wfirst, WFold wf) {
+    int wfirst) {
   constexpr int L1 = conv_gemm_lds_floats<BNT, BMT>();
   constexpr int L2 = TI * TJ * 16 * 64;
   __shared__ __attribute__((aligned(16))) float lds[L1 > L2 ? L1 : L2];
@@ -1344,7 +1282,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_bwd_pair1x1(
   } else {
     const int j = id - n1;
     wgrad1x1_block<TI, TJ, 0>(gout, x, part2, g, splits2, gps, j % nt2, j / nt2,
-                              reinterpret_cast<float(*)[64]>(lds), wf);
+                              reinterpret_cast<float(*)[64]>(lds));
   }
 }
 
@@ -1426,19 +1364,6 @@ static void reduce_splits(const float *part, int splits, int n, float *out, int 
   else
     hipLaunchKernelGGL(k_reduce_splits, dim3(cdiv(n, 64)), dim3(1024), 0, s, part, splits, n, out,
                        accumulate, RS, mask);
-}
-
-// The in-launch weight-gradient fold (conv.h WFold) applies: e2ep_tune key 34 = 2, every tap
-// live (a dead tap's 0 is written by the reduction only), dw overwritten (not accumulated).
-static bool wfold_ok(const ConvGeom &g, const TapList &tl, int accumulate) {
-  return g_tune[TUNE_WGRAD_FOLD] == 2 && !accumulate && tl.n == g.R * g.S;
-}
-// the fold's counters for `tiles` output tiles (none: slabs + reduce_splits)
-static WFold wfold_for(const ConvGeom &g, const TapList &tl, int accumulate, int tiles, float *dw,
-                       hipStream_t s) {
-  if (!wfold_ok(g, tl, accumulate)) return WFold{nullptr, nullptr};
-  unsigned int *cnt = handoff_slots(tiles, s);
-  return cnt ? WFold{cnt, dw} : WFold{nullptr, nullptr};
 }
 
 // per-channel bias gradient: db[c] = sum over (n, p) of g[n, c, p]  (one block per channel)
@@ -2204,11 +2129,9 @@ int e2ep_conv_wgrad(const float *gout, const void *xv, const int *dims, int spli
                    "e2ep_conv_wgrad: a bf16 x needs the bf16-operand weight gradient");
       hipStream_t s = as_stream(stream);
       float *part = static_cast<float *>(workspace);
-      bool folded = false;
       const int used = lp_wgrad_launch(gout, xv, g, tl, splits, part, s, g_conv_precision == 1 ? 1 : 0,
-                                       io != 0, wfold_ok(g, tl, accumulate) ? dw : nullptr, &folded);
-      if (!folded)
-        reduce_splits(part, used, g.Cout * g.Cin * g.R * g.S, dw, accumulate, g.R * g.S, tl.mask, s);
+                                       io != 0);
+      reduce_splits(part, used, g.Cout * g.Cin * g.R * g.S, dw, accumulate, g.R * g.S, tl.mask, s);
       return launch_status("e2ep_conv_wgrad");
     }
   }
@@ -2223,15 +2146,14 @@ int e2ep_conv_wgrad(const float *gout, const void *xv, const int *dims, int spli
     int to, tc;
     wgrad1x1_tiles(g, to, tc);
     const dim3 grid(cdiv(g.Cout, to) * cdiv(g.Cin, tc), used);
-    const WFold wf = wfold_for(g, live_taps(g), accumulate, (int)grid.x, dw, s);
 #define W1_LAUNCH(TI, TJ)                                                                      \
   do {                                                                                         \
     if (g_conv_precision == 1)                                                                 \
       hipLaunchKernelGGL((k_wgrad_1x1<TI, TJ, 1>), grid, dim3(256), 0, s, gout, x, part, g, used, \
-                         gps, wf);                                                             \
+                         gps);                                                                 \
     else                                                                                       \
       hipLaunchKernelGGL((k_wgrad_1x1<TI, TJ, 0>), grid, dim3(256), 0, s, gout, x, part, g, used, \
-                         gps, wf);                                                             \
+                         gps);                                                                 \
   } while (0)
     if (to == 64 && tc == 64) W1_LAUNCH(2, 2);
     else if (to == 64) W1_LAUNCH(2, 1);
@@ -2239,7 +2161,7 @@ int e2ep_conv_wgrad(const float *gout, const void *xv, const int *dims, int spli
     else W1_LAUNCH(1, 1);
 #undef W1_LAUNCH
     const int n = g.Cout * g.Cin;
-    if (!wf.cnt) reduce_splits(part, used, n, dw, accumulate, 1, 1ULL, s);
+    reduce_splits(part, used, n, dw, accumulate, 1, 1ULL, s);
     return launch_status("e2ep_conv_wgrad");
   }
   const int Ptot = g.N * g.P * g.Q;
@@ -2255,12 +2177,10 @@ int e2ep_conv_wgrad(const float *gout, const void *xv, const int *dims, int spli
   float *part = static_cast<float *>(workspace);
   if (tl.n > 0 && v2) {
     dim3 grid(cdiv(g.Cin * tl.n, 64), cdiv(g.Cout, 64), used);
-    const WFold wf = wfold_for(g, tl, accumulate, (int)(grid.x * grid.y), dw, s);
     if (g_conv_precision == 1)
-      hipLaunchKernelGGL((k_conv_wgrad2<1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl, wf);
+      hipLaunchKernelGGL((k_conv_wgrad2<1>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
     else
-      hipLaunchKernelGGL((k_conv_wgrad2<0>), grid, dim3(256), 0, s, gout, x, part, g, per, tl, wf);
-    if (wf.cnt) return launch_status("e2ep_conv_wgrad");
+      hipLaunchKernelGGL((k_conv_wgrad2<0>), grid, dim3(256), 0, s, gout, x, part, g, per, tl);
   } else if (tl.n > 0) {
     dim3 grid(cdiv(g.Cin * tl.n, WBN), cdiv(g.Cout, BM), used);
 #define WG_LAUNCH(OPV, KBV) \
@@ -2348,19 +2268,16 @@ int e2ep_conv_bwd(const float *gout, const void *xv, const float *w, const int *
   float *part2 = static_cast<float *>(ws_wgrad);
   int used;
   if (kind == PAIR_LP) {
-    bool folded = false;
     used = lp_bwd_pair_launch(w, gout, res, dxv, dx_bytes, g, M, g_conv_precision == 1 ? 1 : 0,
-                              ws_dgrad, xv, tl, wsplits, part2, s, xb,
-                              wfold_ok(g, tl, 0) ? dw : nullptr, &folded);
+                              ws_dgrad, xv, tl, wsplits, part2, s, xb);
     E2EP_REQUIRE(used > 0, E2EP_EINVAL, "e2ep_conv_bwd: no paired k_conv_lp plan");
-    if (!folded) reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
+    reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
     return launch_status("e2ep_conv_bwd");
   }
   // k_conv_gemm data gradient: launch_gemm's grid and fold counters
   const dim3 g1(cdiv(p.ncols, p.bnt), cdiv(M, p.bm), p.nph * p.splits);
   float *part1 = p.splits > 1 ? static_cast<float *>(ws_dgrad) : nullptr;
   unsigned int *cnt = p.splits > 1 ? handoff_slots((int)g1.x * (int)g1.y, s) : nullptr;
-  WFold wf2{nullptr, nullptr};
   if (kind == PAIR_GEMM1X1) {
     // e2ep_conv_wgrad's k_wgrad_1x1 plan
     const int groups = g.N * g.P * g.Q / 8;
@@ -2371,11 +2288,10 @@ int e2ep_conv_bwd(const float *gout, const void *xv, const float *w, const int *
     const int nt2 = cdiv(g.Cout, to) * cdiv(g.Cin, tc);
     const dim3 grid(g1.x * g1.y * g1.z + nt2 * used);
     const int wfirst = g_tune[TUNE_PAIR1X1_ORDER] == 2 ? 1 : 0;
-    const WFold wf = wfold_for(g, tl, 0, nt2, dw, s);
 #define E2EP_PAIR1(BNTV, BMTV, TIV, TJV)                                                          \
   hipLaunchKernelGGL((k_conv_bwd_pair1x1<BNTV, BMTV, TIV, TJV>), grid, dim3(256), 0, s, w, gout,  \
                      res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, (int)g1.y,  \
-                     (int)g1.z, x, part2, used, gps, nt2, wfirst, wf)
+                     (int)g1.z, x, part2, used, gps, nt2, wfirst)
 #define E2EP_PAIR1_W(BNTV, BMTV)                                          \
   do {                                                                    \
     if (to == 64 && tc == 64) E2EP_PAIR1(BNTV, BMTV, 2, 2);               \
@@ -2395,7 +2311,7 @@ int e2ep_conv_bwd(const float *gout, const void *xv, const float *w, const int *
     if (p.splits > 1 && !cnt)  // no fold counters: the data gradient's slabs reduced here
       hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s, part1,
                          p.splits, M, g.H * g.W, (int)p.ncols, nullptr, 0, res, dx);
-    if (!wf.cnt) reduce_splits(part2, used, g.Cout * g.Cin, dw, 0, 1, 1ULL, s);
+    reduce_splits(part2, used, g.Cout * g.Cin, dw, 0, 1, 1ULL, s);
     return launch_status("e2ep_conv_bwd");
   } else {
     // weight gradient grid (e2ep_conv_wgrad's k_conv_wgrad2 path)
@@ -2405,11 +2321,10 @@ int e2ep_conv_bwd(const float *gout, const void *xv, const float *w, const int *
     used = (Ptot + per - 1) / per;
     const dim3 g2(cdiv(g.Cin * tl.n, 64), cdiv(g.Cout, 64), used);
     const dim3 grid(g1.x * g1.y * g1.z + g2.x * g2.y * g2.z);
-    wf2 = wfold_for(g, tl, 0, (int)(g2.x * g2.y), dw, s);
 #define E2EP_PAIR(BNTV, BMTV)                                                                     \
   hipLaunchKernelGGL((k_conv_bwd_pair<BNTV, BMTV>), grid, dim3(256), 0, s, w, gout, res, dx,      \
                      dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, (int)g1.y,           \
-                     (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z, wf2)
+                     (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z)
     if (p.bm == 64) {
       if (p.bnt == 128) E2EP_PAIR(128, 64);
       else E2EP_PAIR(64, 64);
@@ -2422,7 +2337,7 @@ int e2ep_conv_bwd(const float *gout, const void *xv, const float *w, const int *
   if (p.splits > 1 && !cnt)  // no fold counters: the data gradient's slabs reduced here
     hipLaunchKernelGGL(k_conv_reduce, dim3(cdiv(p.ncols, 256), M), dim3(256), 0, s, part1,
                        p.splits, M, g.H * g.W, (int)p.ncols, nullptr, 0, res, dx);
-  if (!wf2.cnt) reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
+  reduce_splits(part2, used, g.Cout * g.Cin * g.R * g.S, dw, 0, g.R * g.S, tl.mask, s);
   return launch_status("e2ep_conv_bwd");
 }
 

@@ -729,8 +729,7 @@ __device__ __forceinline__ void wgrad_lp_block(
     const float *__restrict__ gout, const TX *__restrict__ x, float *__restrict__ part,
     ConvGeom g, int pix_per_split, TapList tl, int bx, int by, int bz, int gz,
     typename LpType<OP == 0 ? 0 : 1>::T (*As)[64 * WM][lld_of(OP, LKS)],
-    typename LpType<OP == 0 ? 0 : 1>::T (*Bs)[64 * WN][lld_of(OP, LKS)],
-    WFold wf = WFold{nullptr, nullptr}, int gx = 0) {
+    typename LpType<OP == 0 ? 0 : 1>::T (*Bs)[64 * WN][lld_of(OP, LKS)]) {
   constexpr int BMT = 64 * WM, BNT = 64 * WN;
   static_assert(OP != 0 || LKS == 32, "fp32: 32-pixel steps");
   constexpr int OPR = LKS / 8;             // A pixel octets per row
@@ -956,77 +955,28 @@ __device__ __forceinline__ void wgrad_lp_block(
     }
   }
   const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gz * g.Cout * Kw);
-  // this lane's (co, column) entries: byte offset in slab 0, or OOR
-  int eo[WN][WM][16];
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
     const int lcol = n0 + 32 * (WN * wn + j) + li;
     const int lci = lcol < Kl ? lcol / tl.n : 0;
     const int col = lci * RS + s_tap[lcol < Kl ? lcol - lci * tl.n : 0];  // dW column
 #pragma unroll
-    for (int i = 0; i < WM; ++i)
+    for (int i = 0; i < WM; ++i) {
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int co = m0 + 32 * (WM * wm + i) + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
-        eo[j][i][rr] = (co < g.Cout && lcol < Kl) ? (co * Kw + col) * 4 : OOR;
+        const bool ok = co < g.Cout && lcol < Kl;
+        bstore(rp, ok ? ((split * g.Cout + co) * Kw + col) * 4 : OOR, acc[i][j][rr]);
       }
+    }
   }
-  if (wf.cnt && gz == 1) {  // WFold, one slab: the gradient itself
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int rr = 0; rr < 16; ++rr)
-          if (eo[j][i][rr] != OOR) wf.dw[eo[j][i][rr] >> 2] = acc[i][j][rr];
-    return;
-  }
-  const int so = split * g.Cout * Kw * 4;  // this split's slab
-#pragma unroll
-  for (int j = 0; j < WN; ++j)
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int o = eo[j][i][rr] != OOR ? so + eo[j][i][rr] : OOR;
-        if (wf.cnt) bstore_sc1(rp, o, acc[i][j][rr]);
-        else bstore(rp, o, acc[i][j][rr]);
-      }
-  if (!wf.cnt) return;
-  // WFold: the tile's last arrival sums the slabs in split order into dw
-  __shared__ int s_wlast;
-  handoff_drain();
-  if (!handoff_arrive(wf.cnt + bx + gx * by, gz, &s_wlast)) return;
-  const int slab = g.Cout * Kw * 4;
-#pragma unroll
-  for (int j = 0; j < WN; ++j)
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) acc[i][j][rr] = bload_sc1(rp, eo[j][i][rr]);
-#pragma unroll 2
-  for (int k = 1; k < gz; ++k)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int rr = 0; rr < 16; ++rr)
-          acc[i][j][rr] += bload_sc1(rp, eo[j][i][rr] != OOR ? k * slab + eo[j][i][rr] : OOR);
-#pragma unroll
-  for (int j = 0; j < WN; ++j)
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr)
-        if (eo[j][i][rr] != OOR) wf.dw[eo[j][i][rr] >> 2] = acc[i][j][rr];
 }
 
 template <int WM, int WN, int OP, int LKS, typename TX = float>
 __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout,
                                                   const TX *__restrict__ x,
                                                   float *__restrict__ part, ConvGeom g,
-                                                  int pix_per_split, TapList tl, WFold wf) {
+                                                  int pix_per_split, TapList tl) {
   typedef typename LpType<OP == 0 ? 0 : 1>::T T;
   constexpr int LD = lld_of(OP, LKS);
   __shared__ __attribute__((aligned(16))) T As[2][64 * WM][LD];
@@ -1034,7 +984,7 @@ __global__ void __launch_bounds__(256) k_wgrad_lp(const float *__restrict__ gout
   int bx, by, bz;
   xcd_block(g.xcd != 0, bx, by, bz);
   wgrad_lp_block<WM, WN, OP, LKS, TX>(gout, x, part, g, pix_per_split, tl, bx, by, bz, gridDim.z, As,
-                                      Bs, wf, gridDim.x);
+                                      Bs);
 }
 
 // A conv layer's data gradient (k_conv_lp MODE 1) and weight gradient (k_wgrad_lp slabs) in
@@ -1049,7 +999,7 @@ __global__ void __launch_bounds__(256) k_lp_bwd_pair(
     TX *__restrict__ dx, long long dx_bytes, ConvGeom g, int M, int splits, int kper,
     float *__restrict__ part1, unsigned int *__restrict__ cnt, int gx1, int gy1, int gz1,
     const TX *__restrict__ x, float *__restrict__ part2, int pix_per_split, TapList tl,
-    int gx2, int gy2, int gz2, WFold wf) {
+    int gx2, int gy2, int gz2) {
   typedef typename LpType<OP>::T T;
   constexpr int LD = lld_of(OP, LK);
   constexpr int L1 = 2 * 64 * (DWM + DWN) * LD, L2 = 2 * 64 * (WWM + WWN) * LD;
@@ -1069,7 +1019,7 @@ __global__ void __launch_bounds__(256) k_lp_bwd_pair(
     wgrad_lp_block<WWM, WWN, OP, LK, TX>(
         gout, x, part2, g, pix_per_split, tl, id % gx2, (id / gx2) % gy2, id / (gx2 * gy2), gz2,
         reinterpret_cast<T(*)[64 * WWM][LD]>(lds),
-        reinterpret_cast<T(*)[64 * WWN][LD]>(lds + 2 * 64 * WWM * LD), wf, gx2);
+        reinterpret_cast<T(*)[64 * WWN][LD]>(lds + 2 * 64 * WWM * LD));
   }
 }
 
@@ -1120,16 +1070,8 @@ int lp_wgrad_splits(const ConvGeom &g, const TapList &tl, int op) {
   return (int)std::max(1LL, std::min(s, 256LL));
 }
 
-// the fold's counters for `tiles` output tiles when fold_dw is given (conv.h WFold)
-static WFold lp_wfold(float *fold_dw, int tiles, hipStream_t s, bool *folded) {
-  unsigned int *cnt = fold_dw ? handoff_slots(tiles, s) : nullptr;
-  if (folded) *folded = cnt != nullptr;
-  return cnt ? WFold{cnt, fold_dw} : WFold{nullptr, nullptr};
-}
-
 int lp_wgrad_launch(const float *gout, const void *xv, const ConvGeom &g, const TapList &tl,
-                    int splits, float *part, hipStream_t s, int op, bool xb, float *fold_dw,
-                    bool *folded) {
+                    int splits, float *part, hipStream_t s, int op, bool xb) {
   const float *x = static_cast<const float *>(xv);
   const bf16_t *xh = static_cast<const bf16_t *>(xv);
   int wm, wn;
@@ -1140,19 +1082,18 @@ int lp_wgrad_launch(const float *gout, const void *xv, const ConvGeom &g, const 
   per = (per + lk - 1) / lk * lk;
   const int used = (Ptot + per - 1) / per;
   const dim3 grid(cdiv(g.Cin * tl.n, 64 * wn), cdiv(g.Cout, 64 * wm), used);
-  const WFold wf = lp_wfold(fold_dw, (int)(grid.x * grid.y), s, folded);
 #define WL(WMV, WNV)                                                                             \
   do {                                                                                           \
     if (op != 1)                                                                                 \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 0, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl, wf); \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 0, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
     else if (xb && lk == 64)                                                                     \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64, bf16_t>), grid, dim3(256), 0, s, gout, xh, part, g, per, tl, wf); \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64, bf16_t>), grid, dim3(256), 0, s, gout, xh, part, g, per, tl); \
     else if (xb)                                                                                 \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 32, bf16_t>), grid, dim3(256), 0, s, gout, xh, part, g, per, tl, wf); \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 32, bf16_t>), grid, dim3(256), 0, s, gout, xh, part, g, per, tl); \
     else if (lk == 64)                                                                           \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64>), grid, dim3(256), 0, s, gout, x, part, g, per, tl, wf); \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 64>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
     else                                                                                         \
-      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl, wf); \
+      hipLaunchKernelGGL((k_wgrad_lp<WMV, WNV, 1, 32>), grid, dim3(256), 0, s, gout, x, part, g, per, tl); \
   } while (0)
   if (wm == 2 && wn == 2) WL(2, 2);
   else if (wm == 2) WL(2, 1);
@@ -1196,7 +1137,7 @@ bool lp_bwd_pair_ok(const ConvGeom &g, int M, int op, const TapList &tl) {
 int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void *dxv,
                        long long dx_bytes, const ConvGeom &g, int M, int op, void *ws_dgrad,
                        const void *xv, const TapList &tl, int wsplits, float *part2,
-                       hipStream_t s, bool xb, float *fold_dw, bool *folded) {
+                       hipStream_t s, bool xb) {
   LpPlan p;
   int wwm, wwn;
   if (!lp_pair_tiles(g, M, op, tl, p, wwm, wwn)) return -1;
@@ -1214,17 +1155,16 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void
   const int used = (Ptot + per - 1) / per;
   const dim3 g2(cdiv(g.Cin * tl.n, 64 * wwn), cdiv(g.Cout, 64 * wwm), used);
   const dim3 grid(g1.x * g1.y * g1.z + g2.x * g2.y * g2.z);
-  const WFold wf = lp_wfold(fold_dw, (int)(g2.x * g2.y), s, folded);
 #define PAIR_L(DM, DN, OPV, WMV, WNV)                                                           \
   do {                                                                                          \
     if (OPV == 1 && xb)                                                                         \
       hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV, bf16_t>), grid, dim3(256), 0, s, w, \
                          gout, res, dxh, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x, \
-                         (int)g1.y, (int)g1.z, xh, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z, wf); \
+                         (int)g1.y, (int)g1.z, xh, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z); \
     else                                                                                        \
       hipLaunchKernelGGL((k_lp_bwd_pair<DM, DN, OPV, WMV, WNV>), grid, dim3(256), 0, s, w, gout,  \
                          res, dx, dx_bytes, g, M, p.splits, p.kper, part1, cnt, (int)g1.x,       \
-                         (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z, wf); \
+                         (int)g1.y, (int)g1.z, x, part2, per, tl, (int)g2.x, (int)g2.y, (int)g2.z); \
   } while (0)
 #define PAIR_W(DM, DN)                                     \
   do {                                                     \

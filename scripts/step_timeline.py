@@ -37,6 +37,10 @@ def main():
                 ev.append((r[0], r[1], t, str(r[2])[:70], r[3:]))
         except sqlite3.Error as e:  # noqa: PERF203 - diagnostics
             print(f"# {t}: {e}")
+    if "regions" in tables:  # every graph launch of the run, relative to the step
+        for st, en, nm in c.execute("select start, end, name from regions where name like 'hipGraph%' "
+                                    "or name like 'hipStreamSynchronize%' order by start"):
+            print(f"# api {(st - t0) / 1e3:10.1f} {(en - st) / 1e3:9.1f}  {nm}")
     ev.sort()
     for s, e, t, n, x in ev:
         print(f"{(s - t0) / 1e3:10.1f} {(e - s) / 1e3:9.1f}  {t[:18]:18s} {n} {x if x else ''}")
