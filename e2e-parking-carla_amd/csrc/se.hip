@@ -157,6 +157,58 @@ __global__ void __launch_bounds__(256) k_se_excite(const TX *__restrict__ x, SeI
   }
 }
 
+// k_se_excite with k_se_logits folded in (e2ep_tune key 34 = 2): the block's planes [p0, p1]
+// (at most SE_XP) get a[p] = W2[c] . swish(hpre[n]) + b2[c] first, one wave per plane (lanes
+// over the hidden units, fixed-order wave reduction), their gates sigmoid(a) in LDS; the block
+// holding a plane's first element also writes a[p] (the backward's input).  One launch and one
+// dependent hop fewer per SE block, on the forward's critical path.
+constexpr int SE_XP = 8;
+template <typename TX, typename TY = float>
+__global__ void __launch_bounds__(256) k_se_excite_mlp(const TX *__restrict__ x, SeIn tf,
+                                                       const float *__restrict__ hpre,
+                                                       const float *__restrict__ w2,
+                                                       const float *__restrict__ b2, int sq,
+                                                       float *__restrict__ a, int HW,
+                                                       long long nvec, int vec,
+                                                       TY *__restrict__ y) {
+  __shared__ float sg[SE_XP];
+  const int per = vec ? (HW >> 2) : HW;  // vectors per plane
+  const int i0 = (int)(blockIdx.x * blockDim.x);
+  const int last = (int)min((long long)i0 + (long long)blockDim.x, nvec) - 1;
+  const int p0 = i0 / per, p1 = last / per;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int p = p0 + wv; p <= p1; p += 4) {  // wave-uniform
+    const int n = p / tf.C, c = p - n * tf.C;
+    const float *hr = hpre + (size_t)n * sq, *wr = w2 + (size_t)c * sq;
+    float acc = 0.f;
+    for (int k = lane; k < sq; k += 64) {
+      const float z = hr[k];
+      acc += wr[k] * (z * sigm(z));
+    }
+    acc = wave_sum(acc);
+    const float av = acc + (b2 ? b2[c] : 0.f);
+    if (lane == 0) {
+      sg[p - p0] = sigm(av);
+      if (p * per >= i0) a[p] = av;  // the plane starts in this block
+    }
+  }
+  __syncthreads();
+  const int i = i0 + (int)threadIdx.x;
+  if (i >= nvec) return;
+  const bool t = tf.sc != nullptr;
+  const int pl = i / per;
+  const int c = pl % tf.C;
+  const float sc = t ? tf.sc[c] : 1.f, sh = t ? tf.sh[c] : 0.f;
+  const float g = sg[pl - p0];
+  if (vec) {
+    float4 v = se_in4(ld4(x + 4 * i), sc, sh, t);
+    v.x *= g; v.y *= g; v.z *= g; v.w *= g;
+    st4(y + 4 * i, v);
+  } else {
+    st1(y + i, se_in(ld1(x + i), sc, sh, t) * g);
+  }
+}
+
 // The block's _bn1 backward sums, taken in the same pass (BNS, training BN with the SE input
 // transform): with xhat = (x - mean) invstd, zb = xhat gamma + beta (the arithmetic of
 // bn.hip's BnBwdElem) and sp = swish'(zb), the BN backward's channel sums of
@@ -411,6 +463,20 @@ int e2ep_se_fwd(const void *x, const float *x_scale, const float *x_shift, const
                        static_cast<const float *>(x), tf, planes, HW, pooled);
   hipLaunchKernelGGL(k_se_hidden, dim3(N, cdiv(sq, 4)), dim3(256), 0, s, pooled, w1, b1, C, sq,
                      hpre);
+  // the logits inside the excite launch (key 34 = 2) when a 256-thread block spans at most
+  // SE_XP planes
+  const int per = vec ? HW / 4 : HW;
+  if (g_tune[TUNE_SE_EXCITE_MLP] == 2 && cdiv(256, per) + 1 <= SE_XP) {
+#define E2EP_SEX(TXV, TYV)                                                                      \
+  hipLaunchKernelGGL((k_se_excite_mlp<TXV, TYV>), dim3(cdiv(nvec, 256)), dim3(256), 0, s,       \
+                     static_cast<const TXV *>(x), tf, hpre, w2, b2, sq, a, HW, nvec, vec,        \
+                     static_cast<TYV *>(y))
+    if (io & E2EP_IO_DX_BF16) E2EP_SEX(bf16_t, bf16_t);
+    else if (io) E2EP_SEX(bf16_t, float);
+    else E2EP_SEX(float, float);
+#undef E2EP_SEX
+    return launch_status("e2ep_se_fwd");
+  }
   hipLaunchKernelGGL(k_se_logits, dim3(cdiv(C, SE_CT), cdiv(N, SE_NT)), dim3(256),
                      (SE_CT * (sq + 1) + SE_NT * sq) * sizeof(float), s, hpre, w2, b2, N, C, sq, a);
   if (io & E2EP_IO_DX_BF16)
