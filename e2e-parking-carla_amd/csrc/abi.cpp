@@ -16,8 +16,10 @@ void set_error(const char *fmt, ...) {
 // launch-plan tunables (tune.h TUNE_*), e2ep_tune.  Defaults from in-step A/B on the replayed
 // C2 step (profiles/r02/session6/tune_ab_round*.txt): split-BN target 2048 (was 1024),
 // depthwise weight-gradient target 1024 (was 2048), 1x1 weight-gradient target 1024 (was
-// 2048) together -0.23 ms/step; the rest keep their values (no gain measured).
-int g_tune[TUNE_N] = {2048, 4096, 1024, 512, 768, 1024, 512, 1, 1, 2, 1, 2, 2, 1, 2, 1, 1, 1, 1, 1, 1, 2, 1024, 2, 2048, 2, 1, 1, 2, 1, 2, 1, 1, 1, 1};
+// 2048) together -0.23 ms/step; the rest keep their values (no gain measured).  Round 6: split-BN
+// target 8192 and 512 float4 per BN apply workgroup (was 2048 / 1024), C2 20.78 -> 20.58 ms
+// (profiles/r06/bn_split_ab.txt).
+int g_tune[TUNE_N] = {8192, 4096, 512, 512, 768, 1024, 512, 1, 1, 2, 1, 2, 2, 1, 2, 1, 1, 1, 1, 1, 1, 2, 1024, 2, 2048, 2, 1, 1, 2, 1, 2, 1, 1, 1, 1};
 }  // namespace e2ep
 
 extern "C" {
