@@ -229,9 +229,21 @@ def wgrad_overlap():
     return _OVERLAP[0]
 
 
+# E2EP_WGRAD_STREAM=cam | heads: the weight-gradient forks of the main stream run on that model
+# branch's stream (streams.py) instead of a stream of their own, so a captured train step uses
+# three streams instead of four.  With four, the replayed graph idled 0.2 - 0.45 ms per step in 50 - 90
+# us gaps between the first MBConv blocks' kernels; with either the branches or the forks off
+# (three or two streams) it did not (scripts/step_timeline.py, profiles/r06/graph_gaps.txt).  The
+# camera branch's own work (the depth head, forward and backward) and the forks are at
+# different points of the step.
+_WGRAD_STREAM = [os.environ.get("E2EP_WGRAD_STREAM", "own")]
+
+
 def side_stream(device):
     """The weight-gradient side stream of the current stream (one per stream)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
+    if _WGRAD_STREAM[0] in ("cam", "heads"):
+        return streams._side(torch.device("cuda", idx), _WGRAD_STREAM[0])
     key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     st = _SIDE.get(key)
     if st is None:
