@@ -90,3 +90,20 @@ def test_stage2_touching_a_stage1_gradient_is_detected():
         marks = segments.grad_marks(stage1)
         segments.backward_rest(rec.pairs)
         assert segments.stage2_leaves_stage1(stage1, marks) == (not share)
+
+
+def test_train_step_rig_key_compares_rig_values():
+    """TrainStep's captured-rig check (e2ep_amd.train._rig_key): a rig is identified by its
+    shapes and fp32 bytes, whatever its device or dtype, so a graph-mode step refuses a batch
+    whose rig differs from the captured one and accepts an equal one (reference rig handling:
+    model/bev_model.py:45-57; the captured plan is the rig's)."""
+    from e2ep_amd.train import _rig_key
+    K = torch.eye(3).repeat(2, 4, 1, 1)
+    E = torch.eye(4).repeat(2, 4, 1, 1)
+    k0 = _rig_key({"intrinsics": K, "extrinsics": E})
+    assert k0 == _rig_key({"intrinsics": K.clone().double(), "extrinsics": E.clone()})
+    E2 = E.clone()
+    E2[0, 0, 0, 3] += 0.25
+    assert k0 != _rig_key({"intrinsics": K, "extrinsics": E2})
+    assert k0 != _rig_key({"intrinsics": K[:1], "extrinsics": E[:1]})
+    assert _rig_key({"image": torch.zeros(1)}) is None
