@@ -237,6 +237,9 @@ def wgrad_overlap():
 # camera branch's own work (the depth head, forward and backward) and the forks are at
 # different points of the step.
 _WGRAD_STREAM = [os.environ.get("E2EP_WGRAD_STREAM", "own")]
+# diagnostics only (scripts/diag_branch_capture.py): allow the nested fork from a branch stream
+# that made the round-4 capture segfault, to see what graphs.capture's join check reports
+_FORK_FROM_BRANCH = os.environ.get("E2EP_FORK_FROM_BRANCH", "0") == "1"
 
 
 def side_stream(device):
@@ -266,7 +269,7 @@ class _Fork:
     def __init__(self, device, on=True, work_us=float("inf")):
         self.main = torch.cuda.current_stream(device)
         self.on = (on and _OVERLAP[0] and work_us >= _FORK_MIN_US[0]
-                   and not streams.is_branch_stream(self.main))
+                   and (_FORK_FROM_BRANCH or not streams.is_branch_stream(self.main)))
         self.side = side_stream(device) if self.on else self.main
 
     def __enter__(self):

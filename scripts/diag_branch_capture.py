@@ -18,6 +18,8 @@ Round 5: model_cam crashed (exit -11 in capture_end) and model_cam_nofork / mode
 replayed, so the crash needs a stream forked from a branch stream; conv._Fork no longer forks
 from a branch stream, and model_cam / model_heads are expected to replay too
 (profiles/r05/diag_branch_capture*.log).
+Round 6: with E2EP_FORK_FROM_BRANCH=1 the nested fork is allowed again, and graphs.capture's
+join check (e2ep_capture_unjoined) reports any stream left unjoined before the capture ends.
 """
 import os
 import subprocess
