@@ -5,12 +5,16 @@ ROCm stack, and PyTorch's reductions capture them (cross-block semaphores), so e
 the train step captures is kept un-instantiated, its memset nodes are rewritten into
 kernel nodes by e2ep_graph_replace_memsets, and only then instantiated."""
 import ctypes
+import os
+import sys
 
 import torch
 import torch.distributed as dist
 from torch.utils._python_dispatch import TorchDispatchMode
 
 from . import _lib
+
+_DEBUG = os.environ.get("E2EP_CAPTURE_DEBUG", "0") == "1"  # per-stream join-check report on stderr
 
 
 def capture_mode():
@@ -104,6 +108,9 @@ def _join_check():
         u = ctypes.c_int(0)
         _lib.call("e2ep_capture_unjoined", ctypes.c_void_p(origin.cuda_stream),
                   ctypes.c_void_p(st.cuda_stream), ctypes.byref(u))
+        if _DEBUG:
+            print(f"graphs.capture join check: {name}: {'UNJOINED' if u.value else 'joined / not in the capture'}",
+                  file=sys.stderr, flush=True)
         if u.value:
             origin.wait_stream(st)
             bad.append(name)
