@@ -19,7 +19,7 @@ void set_error(const char *fmt, ...) {
 // 2048) together -0.23 ms/step; the rest keep their values (no gain measured).  Round 6: split-BN
 // target 8192 and 512 float4 per BN apply workgroup (was 2048 / 1024), C2 20.78 -> 20.58 ms
 // (profiles/r06/bn_split_ab.txt).
-int g_tune[TUNE_N] = {8192, 4096, 512, 512, 768, 1024, 512, 1, 1, 2, 1, 2, 2, 1, 2, 1, 1, 1, 1, 1, 1, 2, 1024, 2, 2048, 2, 1, 1, 2, 1, 2, 1, 1, 1, 1};
+int g_tune[TUNE_N] = {8192, 4096, 512, 512, 768, 1024, 512, 1, 1, 2, 1, 2, 2, 1, 2, 1, 1, 1, 1, 1, 1, 2, 1024, 2, 2048, 2, 1, 1, 2, 1, 2, 1, 1, 1, 1, 1};
 }  // namespace e2ep
 
 extern "C" {

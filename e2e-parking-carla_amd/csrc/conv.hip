@@ -1816,6 +1816,7 @@ static int fwd_stats_tiles(const ConvGeom &g0) {
   g.xcd = g_tune[TUNE_XCD] == 2;
   if (direct_ok(g)) return 0;
   const int route = conv_route(0, g, g.Cout);
+  if (route == ROUTE_LP && stem_direct_ok(0, g, g.Cout, g_conv_precision)) return 0;  // no stats
   if (route == ROUTE_LP) return lp_stats_tiles(g, g_conv_precision);
   if (route == ROUTE_LP32) return lp_stats_tiles(g, 0);
   if (route != ROUTE_GEMM || g_conv_precision != 0) return 0;  // fp32 k_conv_gemm only
@@ -1837,6 +1838,9 @@ static int launch_gemm(int mode, int act, const float *w, const void *srcv, cons
     set_error("conv: BatchNorm statistics requested from a kernel that does not take them");
     return E2EP_EINVAL;
   }
+  if (route == ROUTE_LP && !stats && !io && stem_direct_ok(mode, g, M, g_conv_precision))
+    return stem_direct_launch(act, g_conv_precision, w, static_cast<const float *>(srcv), bias,
+                              static_cast<float *>(dstv), dst_bytes, g, workspace, s);
   if (route == ROUTE_LP)
     return lp_launch(mode, act, g_conv_precision, w, srcv, bias, dstv, dst_bytes, g, M, workspace, s,
                      stats, io);
@@ -1961,9 +1965,12 @@ size_t e2ep_conv_fwd_workspace(const int *dims) {
   if (direct_ok(g)) return 0;
   if (g_conv_precision != 0 || g_tune[TUNE_LP32] == 2) {  // w_layout unknown here: cover all
     g.wlayout = 1;
-    if (lp_ok(0, g, g.Cout, g_conv_precision))
-      return std::max(lp_workspace(0, g, g.Cout, g_conv_precision),
-                      gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout));
+    if (lp_ok(0, g, g.Cout, g_conv_precision)) {
+      size_t ws = std::max(lp_workspace(0, g, g.Cout, g_conv_precision),
+                           gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout));
+      if (stem_direct_ok(0, g, g.Cout, g_conv_precision)) ws = std::max(ws, stem_direct_workspace(g));
+      return ws;
+    }
   }
   if (conv1x1_gemm_ok(0, g)) return conv1x1_ws(0, g, g.Cout);
   return gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout);

@@ -1,0 +1,319 @@
+// Direct-convolution forward of the BEV stem with 16-bit operands: conv 7x7 / 2, pad 3,
+// 65 -> 64 channels, 256^2 -> 128^2 (reference model/bev_encoder.py:13,26) in the C3 bf16
+// training mode and the C5 fp16 inference mode (operands rounded to nearest-even as they are
+// staged, fp32 accumulate, fp32 tensors in HBM — the k_conv_lp semantics).
+//
+// The implicit GEMM (k_conv_lp) re-gathers the im2col operand for every (tap, channel chunk)
+// K-step: the 7x7/2 stem read each input value ~12 times through L2 and spent its time on
+// load issue (k_conv_lp<0,0,1,4,1,32> 290 us, 0.07 of the bf16 peak,
+// profiles/r06/step_sequence_bf16_final.txt).  Here a block owns an output tile of
+// 64 channels x 8 rows x 32 columns of one image and stages its input patch ONCE per
+// 16-channel chunk:
+//  * patch = 21 x 69 input positions x 16 channels, 16-bit, laid out [row][channel half]
+//    [column parity][column / 2][8 channels]: for tap (r, s) lane i of a wave reads output
+//    column i's 8 channels as one ds_read_b128, and the 32 lanes of a half read 32
+//    consecutive 16-B slots (the stride-2 columns de-interleaved by parity) — conflict free;
+//  * weights: k_stem_wprep first writes them once per launch as a 16-bit image in the order
+//    the blocks read them ([chunk][filter row][s][channel half][co][8], then the tail's
+//    [step][half][co][8]: 408 KB for the stem); a block copies one (chunk, filter row) —
+//    14 KB, 3.5 coalesced b128 loads per thread — into a double-buffered LDS slot, the next
+//    row's loads in flight during the current row's MFMAs (gathering them from the fp32
+//    tap-major weights, 8 scalar loads per lane 260 B apart, took the kernel to 159 us);
+//  * each wave computes 64 co x 2 output rows x 32 columns: per tap two A fragments (co
+//    0-31, 32-63) x two B fragments (its rows) = 4 v_mfma_f32_32x32x16 per 4 b128 LDS reads;
+//  * the Cin % 16 remainder channels (the stem's 65th, the target plane) run as flattened
+//    (channel, tap) K-steps over a scalar patch image: 4 steps for 1 x 49 rows, not a
+//    zero-padded 16-channel chunk (13 % of the MFMAs);
+//  * LDS 75.7 KB per block: two blocks per CU, one staging while the other computes.
+// Sum order per output: chunks in order, filter rows, filter columns, then the remainder rows
+// in (channel, tap) order — fixed, so results are deterministic run to run.
+#include <algorithm>
+
+#include "conv.h"
+
+#pragma clang fp contract(on)
+
+namespace e2ep {
+
+namespace {
+
+typedef float sd_f32x16 __attribute__((ext_vector_type(16)));
+typedef float sd_f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 sd_bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 sd_f16x8 __attribute__((ext_vector_type(8)));
+
+template <int OP> struct SdType;
+template <> struct SdType<1> { typedef __bf16 T; typedef sd_bf16x8 T8; };
+template <> struct SdType<2> { typedef _Float16 T; typedef sd_f16x8 T8; };
+
+constexpr int SD_K = 7;                        // filter rows = columns
+constexpr int SD_TH = 8, SD_TW = 32;           // output tile rows x columns (4 waves x 2 rows)
+constexpr int SD_PR = 2 * (SD_TH - 1) + SD_K;  // 21 patch rows
+constexpr int SD_PC = 2 * (SD_TW - 1) + SD_K;  // 69 patch columns
+constexpr int SD_PCH = (SD_PC + 1) / 2;        // 35 columns per parity
+constexpr int SD_PATCH8 = SD_PR * 2 * 2 * SD_PCH;  // 8-channel groups of the patch image
+constexpr int SD_PTASKS = 2 * SD_PR * SD_PC;       // (channel half, row, column) staging tasks
+constexpr int SD_WROW8 = SD_K * 2 * 64;            // 8-channel weight groups per filter row
+constexpr int SD_TAILMAX = 4;                      // remainder channels (14 flattened steps)
+
+template <int OP>
+__device__ __forceinline__ typename SdType<OP>::T8 sd_cvt8(const float *v) {
+  sd_f32x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = v[j];
+  return __builtin_convertvector(f, typename SdType<OP>::T8);
+}
+
+template <int OP>
+__device__ __forceinline__ sd_f32x16 sd_mfma(typename SdType<OP>::T8 a, typename SdType<OP>::T8 b,
+                                             sd_f32x16 c) {
+  if constexpr (OP == 1) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+}  // namespace
+
+// x [N][Cin][H][W] fp32, wimg the k_stem_wprep weight image, y [N][64][P][Q] fp32 (+ bias, relu).
+// Grid (ceil(Q / 32), ceil(P / 8), N), 256 threads; the host gate stem_direct_ok holds the
+// shape assumptions (64 output channels, 7x7, stride 2, Cin % 16 <= 4, byte offsets < 2^31).
+template <int OP, int ACT>
+__global__ void __launch_bounds__(256) k_conv_stem_lp(const float *__restrict__ x,
+                                                      const void *__restrict__ wimg,
+                                                      const float *__restrict__ bias,
+                                                      float *__restrict__ y, long long y_bytes,
+                                                      ConvGeom g) {
+  typedef typename SdType<OP>::T T;
+  typedef typename SdType<OP>::T8 T8;
+  __shared__ T8 patch[SD_PATCH8];   // [row][half][parity][column / 2]; the tail's scalar image
+  __shared__ T8 wl[2][SD_WROW8];    // [buffer][s][half][co]; the tail's [step][half][co]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int n = blockIdx.z, oy0 = blockIdx.y * SD_TH, ox0 = blockIdx.x * SD_TW;
+  const int iy0 = 2 * oy0 - g.ph, ix0 = 2 * ox0 - g.pw;
+  const int HW = g.H * g.W;
+  const int nch = g.Cin >> 4, crem = g.Cin - 16 * nch;
+  const int xbase = n * g.Cin * HW;
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
+  const int kt = crem * SD_K * SD_K;
+  const int tsteps = (kt + 15) >> 4;
+  const __amdgpu_buffer_rsrc_t rw = rsrc(wimg, 16LL * (nch * SD_K * SD_WROW8 + tsteps * 128));
+
+  // one 16-channel chunk's patch: task = (half, row, column), 8 channel loads (lanes on
+  // consecutive columns: coalesced) -> one b128 LDS write
+  auto stage_patch = [&](int c) {
+    for (int t0 = 0; t0 < SD_PTASKS; t0 += 4 * 256) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + 256 * u + tid;
+        const int pc = t % SD_PC, rest = t / SD_PC;
+        const int pr = rest % SD_PR, h = rest / SD_PR;
+        const int iy = iy0 + pr, ix = ix0 + pc;
+        const bool ok = t < SD_PTASKS && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+        const int base = xbase + (16 * c + 8 * h) * HW + iy * g.W + ix;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[u][e] = bload(rx, ok ? (base + e * HW) * 4 : OOR);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + 256 * u + tid;
+        const int pc = t % SD_PC, rest = t / SD_PC;
+        const int pr = rest % SD_PR, h = rest / SD_PR;
+        if (t < SD_PTASKS) patch[((pr * 2 + h) * 2 + (pc & 1)) * SD_PCH + (pc >> 1)] = sd_cvt8<OP>(v[u]);
+      }
+    }
+  };
+  // one (chunk, filter row) of the weight image: 896 consecutive 16-B groups
+  float4 wv[4];
+  auto load_w = [&](int c, int r) {
+    const int g0 = (c * SD_K + r) * SD_WROW8;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int task = tid + 256 * u;
+      wv[u] = bload4(rw, task < SD_WROW8 ? (g0 + task) * 16 : OOR);
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int task = tid + 256 * u;
+      if (task < SD_WROW8) wl[buf][task] = __builtin_bit_cast(T8, wv[u]);
+    }
+  };
+
+  sd_f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[a][j] = sd_f32x16{0};
+
+  auto compute_row = [&](int r, int buf) {
+#pragma unroll
+    for (int s = 0; s < SD_K; ++s) {
+      const T8 a0 = wl[buf][(s * 2 + lh) * 64 + li];
+      const T8 a1 = wl[buf][(s * 2 + lh) * 64 + 32 + li];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int pr = 2 * (2 * wave + j) + r;
+        const T8 b = patch[((pr * 2 + lh) * 2 + (s & 1)) * SD_PCH + li + (s >> 1)];
+        acc[0][j] = sd_mfma<OP>(a0, b, acc[0][j]);
+        acc[1][j] = sd_mfma<OP>(a1, b, acc[1][j]);
+      }
+    }
+  };
+
+  const int nsteps = nch * SD_K;  // (chunk, filter row) steps
+  if (nsteps > 0) {
+    stage_patch(0);
+    load_w(0, 0);
+    store_w(0);
+    __syncthreads();
+    for (int k = 0; k < nsteps; ++k) {
+      const int c = k / SD_K, r = k - SD_K * c;
+      const int kn = min(k + 1, nsteps - 1);  // the last step re-reads itself into the idle buffer
+      load_w(kn / SD_K, kn % SD_K);
+      __builtin_amdgcn_sched_barrier(0);  // weight loads first, then the row's MFMAs
+      compute_row(r, k & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      store_w((k + 1) & 1);
+      if (r == SD_K - 1 && k + 1 < nsteps) {  // chunk done by every wave: restage the patch
+        __syncthreads();
+        stage_patch(c + 1);
+      }
+      __syncthreads();
+    }
+  }
+
+  if (crem > 0) {  // remainder channels: flattened (channel, tap) rows, 16 per K-step
+    T *tp = reinterpret_cast<T *>(patch);  // [channel][row][column]
+    T8 *tw = &wl[0][0];                    // [step][half][co]
+    for (int t = tid; t < crem * SD_PR * SD_PC; t += 256) {
+      const int pc = t % SD_PC, rest = t / SD_PC;
+      const int pr = rest % SD_PR, cc = rest / SD_PR;
+      const int iy = iy0 + pr, ix = ix0 + pc;
+      const bool ok = (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      tp[t] = (T)bload(rx, ok ? (xbase + (16 * nch + cc) * HW + iy * g.W + ix) * 4 : OOR);
+    }
+    for (int t = tid; t < tsteps * 128; t += 256)
+      tw[t] = __builtin_bit_cast(T8, bload4(rw, (nch * SD_K * SD_WROW8 + t) * 16));
+    __syncthreads();
+    for (int step = 0; step < tsteps; ++step) {
+      const T8 a0 = tw[(step * 2 + lh) * 64 + li];
+      const T8 a1 = tw[(step * 2 + lh) * 64 + 32 + li];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        T8 b;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // rows past kt carry zero weights; clamp them onto a staged (finite) value
+          const int k = min(16 * step + 8 * lh + e, kt - 1);
+          const int cc = k / (SD_K * SD_K), tap = k - SD_K * SD_K * cc;
+          const int r = tap / SD_K, s = tap - SD_K * r;
+          b[e] = tp[(cc * SD_PR + 2 * (2 * wave + j) + r) * SD_PC + 2 * li + s];
+        }
+        acc[0][j] = sd_mfma<OP>(a0, b, acc[0][j]);
+        acc[1][j] = sd_mfma<OP>(a1, b, acc[1][j]);
+      }
+    }
+  }
+
+  // epilogue: C/D layout col = lane & 31 (output column), row = (r&3) + 8(r>>2) + 4(lane>>5)
+  const __amdgpu_buffer_rsrc_t ry = rsrc(y, y_bytes);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int oy = oy0 + 2 * wave + j, ox = ox0 + li;
+    const bool ok = oy < g.P && ox < g.Q;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int co = 32 * a + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+        float v = acc[a][j][rr];
+        if (bias) v += bias[co];
+        if (ACT == 1) v = fmaxf(v, 0.f);
+        bstore(ry, ok ? (((n * 64 + co) * g.P + oy) * g.Q + ox) * 4 : OOR, v);
+      }
+    }
+  }
+}
+
+// The 16-bit weight image k_conv_stem_lp reads: group i (8 values) of the full chunks is
+// (c, r, s, half, co) = the 8 input channels 16c + 8 half .. of tap (r, s), output channel co;
+// past them the tail's flattened rows k = (remainder channel, tap), 16 per step.  One thread
+// per group; wt is tap-major fp32 [49][64][Cin].
+template <int OP>
+__global__ void __launch_bounds__(256) k_stem_wprep(const float *__restrict__ wt, int Cin,
+                                                    typename SdType<OP>::T8 *__restrict__ img) {
+  const int nch = Cin >> 4, crem = Cin - 16 * nch;
+  const int kt = crem * SD_K * SD_K;
+  const int nmain = nch * SD_K * SD_WROW8, total = nmain + ((kt + 15) >> 4) * 128;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  float v[8];
+  if (i < nmain) {
+    const int c = i / (SD_K * SD_WROW8), rem = i - c * SD_K * SD_WROW8;
+    const int r = rem / SD_WROW8, task = rem - r * SD_WROW8;
+    const int s = task >> 7, h = (task >> 6) & 1, co = task & 63;
+    const float *p = wt + ((r * SD_K + s) * 64 + co) * Cin + 16 * c + 8 * h;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = p[e];
+  } else {
+    const int t = i - nmain, step = t >> 7, h = (t >> 6) & 1, co = t & 63;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 16 * step + 8 * h + e;
+      const int cc = k / (SD_K * SD_K), tap = k - SD_K * SD_K * cc;
+      v[e] = k < kt ? wt[(tap * 64 + co) * Cin + 16 * nch + cc] : 0.f;
+    }
+  }
+  img[i] = sd_cvt8<OP>(v);
+}
+
+static int stem_groups(const ConvGeom &g) {
+  const int nch = g.Cin >> 4, kt = (g.Cin - 16 * nch) * SD_K * SD_K;
+  return nch * SD_K * SD_WROW8 + ((kt + 15) >> 4) * 128;
+}
+
+size_t stem_direct_workspace(const ConvGeom &g) { return 16 * (size_t)stem_groups(g); }
+
+bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op) {
+  if (g_tune[TUNE_STEM_DIRECT] != 2) return false;
+  if (mode != 0 || (op != 1 && op != 2) || g.wlayout != 1) return false;
+  if (g.R != SD_K || g.S != SD_K || g.sh != 2 || g.sw != 2 || g.dh != 1 || g.dw != 1) return false;
+  if (g.Cout != 64 || M != 64 || g.Cin % 16 > SD_TAILMAX || g.ph < 0 || g.pw < 0) return false;
+  if (g.P != (g.H + 2 * g.ph - SD_K) / 2 + 1 || g.Q != (g.W + 2 * g.pw - SD_K) / 2 + 1) return false;
+  const long long lim = 0x7fffffffLL - 16;
+  return 4LL * g.N * g.Cin * g.H * g.W < lim && 4LL * g.N * 64 * g.P * g.Q < lim &&
+         4LL * SD_K * SD_K * 64 * g.Cin < lim && g.N <= 65535;
+}
+
+int stem_direct_launch(int act, int op, const float *w, const float *x, const float *bias, float *y,
+                       long long y_bytes, const ConvGeom &g, void *workspace, hipStream_t s) {
+  if (!stem_direct_ok(0, g, 64, op) || (act != 0 && act != 1) || !workspace) {
+    set_error("conv: the direct stem kernel does not take this geometry / needs its weight-image "
+              "workspace (stem_direct_ok, e2ep_conv_fwd_workspace)");
+    return E2EP_EINVAL;
+  }
+  const int groups = stem_groups(g);
+  const dim3 grid(cdiv(g.Q, SD_TW), cdiv(g.P, SD_TH), g.N);
+#define SD_LAUNCH(OPV, ACTV)                                                                       \
+  do {                                                                                             \
+    hipLaunchKernelGGL((k_stem_wprep<OPV>), dim3(cdiv(groups, 256)), dim3(256), 0, s, w, g.Cin,    \
+                       static_cast<typename SdType<OPV>::T8 *>(workspace));                        \
+    hipLaunchKernelGGL((k_conv_stem_lp<OPV, ACTV>), grid, dim3(256), 0, s, x, workspace, bias, y,  \
+                       y_bytes, g);                                                                \
+  } while (0)
+  if (op == 1) {
+    if (act) SD_LAUNCH(1, 1);
+    else SD_LAUNCH(1, 0);
+  } else {
+    if (act) SD_LAUNCH(2, 1);
+    else SD_LAUNCH(2, 0);
+  }
+#undef SD_LAUNCH
+  return 0;
+}
+
+}  // namespace e2ep

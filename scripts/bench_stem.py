@@ -1,0 +1,55 @@
+"""A/B of the BEV stem forward (conv 7x7/2, 65 -> 64, 256^2 -> 128^2, B = 8) on 16-bit operands:
+k_conv_stem_lp (e2ep_tune key 35 = 2, csrc/conv_stem.hip) against the implicit-GEMM k_conv_lp
+(key 35 = 1).  Mean device time per launch over --iters launches (HIP events), after warmup.
+
+    python scripts/bench_stem.py [--mode bf16|fp16] [--batch 8] [--iters 50]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "e2e-parking-carla_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="bf16")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    from e2ep_amd import _lib, conv, precision
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(a.batch, 65, 256, 256, generator=g).cuda()
+    w = (torch.randn(64, 65, 7, 7, generator=g) / 22.6).cuda()
+    flop = 2.0 * a.batch * 64 * 128 * 128 * 65 * 49
+    res = {"config": f"B={a.batch} 65x256^2 -> 64x128^2, 7x7/2, {a.mode} operands", "flop": flop}
+    outs = {}
+    for key, name in ((1, "k_conv_lp"), (2, "k_conv_stem_lp")):
+        old = _lib.call_raw("e2ep_tune", 35, key)
+        try:
+            with precision.use(a.mode), torch.no_grad():
+                for _ in range(5):
+                    y = conv.conv2d(x, w, None, (2, 2), (3, 3, 3, 3), (1, 1), 0)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    y = conv.conv2d(x, w, None, (2, 2), (3, 3, 3, 3), (1, 1), 0)
+                e1.record()
+                torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            outs[name] = y
+            res[name] = {"us": round(us, 1), "TFLOPs": round(flop / us / 1e6, 1)}
+        finally:
+            _lib.call_raw("e2ep_tune", 35, old)
+    d = (outs["k_conv_stem_lp"] - outs["k_conv_lp"]).double()
+    res["rel_l2_direct_vs_gemm"] = (d.norm() / outs["k_conv_lp"].double().norm()).item()
+    res["speedup"] = round(res["k_conv_lp"]["us"] / res["k_conv_stem_lp"]["us"], 2)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

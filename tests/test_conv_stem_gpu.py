@@ -1,0 +1,91 @@
+"""k_conv_stem_lp (csrc/conv_stem.hip): the direct-convolution forward of 7x7 / 2 convs with 64
+output channels on 16-bit operands — the BEV stem (reference model/bev_encoder.py:13,26) in C3
+(bf16) and C5 (fp16).  Against fp64 convolutions of the operands rounded to the 16-bit format
+(the products are exact, the sums fp32), against the implicit-GEMM kernel it replaces
+(k_conv_lp, e2ep_tune key 35 = 1: same rounding, another fp32 sum order), and run to run
+bitwise."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import rel_l2
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+KEY = 35  # tune.h TUNE_STEM_DIRECT
+
+# (N, Cin, H, W, bias, act): Cin % 16 = remainder channels on the flattened tail steps
+CASES = [
+    (2, 65, 256, 256, False, 0),  # the BEV stem at full size (4 tail steps)
+    (2, 65, 50, 70, False, 0),    # ragged output tiles (25 x 35)
+    (1, 64, 64, 64, False, 0),    # no remainder
+    (2, 3, 40, 36, False, 0),     # remainder only (no 16-channel chunk)
+    (1, 68, 32, 48, False, 0),    # 4 remainder channels (14 tail steps, the cap)
+    (2, 65, 64, 64, True, 1),     # bias + relu epilogue
+    (2, 21, 30, 30, False, 0),    # 5 remainder channels: stays on k_conv_lp
+]
+
+
+def _run(x, w, b, act, mode, key):
+    from e2ep_amd import _lib, conv, precision
+    old = _lib.call_raw("e2ep_tune", KEY, key)
+    try:
+        with precision.use(mode):
+            return conv.conv2d(x, w, b, (2, 2), (3, 3, 3, 3), (1, 1), act)
+    finally:
+        _lib.call_raw("e2ep_tune", KEY, old)
+
+
+@pytest.mark.parametrize("mode,dt", [("bf16", torch.bfloat16), ("fp16", torch.float16)])
+@pytest.mark.parametrize("case", CASES, ids=[str(i) for i in range(len(CASES))])
+def test_stem_direct_vs_rounded_fp64(case, mode, dt):
+    N, Cin, H, W, has_b, act = case
+    if mode == "fp16" and N * H * W > 40000:
+        pytest.skip("fp16 covered at the smaller shapes")
+    g = torch.Generator().manual_seed(7 + Cin + H)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(64, Cin, 7, 7, generator=g) / (Cin * 49) ** 0.5
+    b = torch.randn(64, generator=g) if has_b else None
+    xd, wd = x.to(DEV), w.to(DEV)
+    bd = b.to(DEV) if has_b else None
+    with torch.no_grad():
+        y = _run(xd, wd, bd, act, mode, 2)
+        y2 = _run(xd, wd, bd, act, mode, 2)
+        y_gemm = _run(xd, wd, bd, act, mode, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)  # deterministic
+    r = lambda t: t.to(dt).double()  # noqa: E731
+    ref = F.conv2d(r(x), r(w), b.double() if has_b else None, 2, 3)
+    if act:
+        ref = ref.clamp_min(0)
+    assert y.shape == ref.shape
+    assert rel_l2(y, ref) < 2e-6
+    assert rel_l2(y, y_gemm) < 2e-6
+    assert (y.cpu().double() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
+
+
+def test_stem_direct_in_bev_stem_training_step():
+    """The BEV stem op (bev_stem: resize + conv) in C3 with the direct forward: the output and
+    every gradient agree with the implicit-GEMM forward (the backward kernels are the same)."""
+    from e2ep_amd import bev_stem
+    g = torch.Generator().manual_seed(11)
+    bev = torch.randn(2, 64, 200, 200, generator=g).to(DEV)
+    tgt = torch.randn(2, 1, 200, 200, generator=g).to(DEV)
+    w = (torch.randn(64, 65, 7, 7, generator=g) / 22.6).to(DEV)
+    gy = torch.randn(2, 64, 128, 128, generator=g).to(DEV)
+    out = {}
+    for key in (2, 1):
+        from e2ep_amd import _lib, precision
+        old = _lib.call_raw("e2ep_tune", KEY, key)
+        try:
+            b = bev.clone().requires_grad_(True)
+            wd = w.clone().requires_grad_(True)
+            with precision.use("bf16"):
+                y = bev_stem.bev_stem(b, tgt, wd, (256, 256))
+                y.backward(gy)
+            out[key] = (y.detach(), b.grad, wd.grad)
+        finally:
+            _lib.call_raw("e2ep_tune", KEY, old)
+    assert rel_l2(out[2][0], out[1][0]) < 2e-6
+    assert torch.equal(out[2][1], out[1][1])  # backward does not depend on the forward kernel
+    assert torch.equal(out[2][2], out[1][2])
