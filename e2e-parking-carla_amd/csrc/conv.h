@@ -98,13 +98,17 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void
                        const void *x, const TapList &tl, int wsplits, float *part2,
                        hipStream_t s, bool xb = false);
 
-// Direct-convolution forward of a 7x7 / 2 conv with 64 output channels on 16-bit operands
-// (op 1 / 2: the BEV stem in C3 / C5), conv_stem.hip: k_conv_stem_lp stages each output
-// tile's input patch once per 16-channel chunk.  Tap-major weights; e2ep_tune key 35 = 2.
-// workspace: stem_direct_workspace(g) bytes for the 16-bit weight image (k_stem_wprep).
+// Direct convolution of a 7x7 / 2 conv with 64 output channels on 16-bit operands (op 1 / 2:
+// the BEV stem in C3 / C5), conv_stem.hip: the forward (mode 0, k_conv_stem_lp) stages each
+// output tile's input patch once per 16-channel chunk, the data gradient (mode 1, pad 3, 64
+// gradient channels, k_conv_stem_dgrad_lp) each tile's gradient patch once.  Tap-major
+// weights; e2ep_tune key 35 = 1 + mask (1 forward, 2 data gradient).  workspace:
+// stem_direct_workspace(g, mode) bytes for the 16-bit weight image (k_stem_wprep*).
 bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op);
-size_t stem_direct_workspace(const ConvGeom &g);
+size_t stem_direct_workspace(const ConvGeom &g, int mode);
 int stem_direct_launch(int act, int op, const float *w, const float *x, const float *bias, float *y,
                        long long y_bytes, const ConvGeom &g, void *workspace, hipStream_t s);
+int stem_dgrad_launch(int op, const float *w, const float *gy, float *dx, long long dx_bytes,
+                      const ConvGeom &g, void *workspace, hipStream_t s);
 
 }  // namespace e2ep

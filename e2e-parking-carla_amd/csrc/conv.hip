@@ -1838,9 +1838,12 @@ static int launch_gemm(int mode, int act, const float *w, const void *srcv, cons
     set_error("conv: BatchNorm statistics requested from a kernel that does not take them");
     return E2EP_EINVAL;
   }
-  if (route == ROUTE_LP && !stats && !io && stem_direct_ok(mode, g, M, g_conv_precision))
+  if (route == ROUTE_LP && !stats && !io && mode == 0 && stem_direct_ok(0, g, M, g_conv_precision))
     return stem_direct_launch(act, g_conv_precision, w, static_cast<const float *>(srcv), bias,
                               static_cast<float *>(dstv), dst_bytes, g, workspace, s);
+  if (route == ROUTE_LP && !io && mode == 1 && !bias && stem_direct_ok(1, g, M, g_conv_precision))
+    return stem_dgrad_launch(g_conv_precision, w, static_cast<const float *>(srcv),
+                             static_cast<float *>(dstv), dst_bytes, g, workspace, s);
   if (route == ROUTE_LP)
     return lp_launch(mode, act, g_conv_precision, w, srcv, bias, dstv, dst_bytes, g, M, workspace, s,
                      stats, io);
@@ -1968,7 +1971,7 @@ size_t e2ep_conv_fwd_workspace(const int *dims) {
     if (lp_ok(0, g, g.Cout, g_conv_precision)) {
       size_t ws = std::max(lp_workspace(0, g, g.Cout, g_conv_precision),
                            gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout));
-      if (stem_direct_ok(0, g, g.Cout, g_conv_precision)) ws = std::max(ws, stem_direct_workspace(g));
+      if (stem_direct_ok(0, g, g.Cout, g_conv_precision)) ws = std::max(ws, stem_direct_workspace(g, 0));
       return ws;
     }
   }
@@ -1980,9 +1983,12 @@ size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
   ConvGeom g = make_geom(dims);
   if (g_conv_precision != 0 || g_tune[TUNE_LP32] == 2) {
     g.wlayout = 1;
-    if (lp_ok(1, g, m_channels, g_conv_precision))
-      return std::max(lp_workspace(1, g, m_channels, g_conv_precision),
-                      gemm_workspace(plan_gemm(1, g, m_channels), m_channels));
+    if (lp_ok(1, g, m_channels, g_conv_precision)) {
+      size_t ws = std::max(lp_workspace(1, g, m_channels, g_conv_precision),
+                           gemm_workspace(plan_gemm(1, g, m_channels), m_channels));
+      if (stem_direct_ok(1, g, m_channels, g_conv_precision)) ws = std::max(ws, stem_direct_workspace(g, 1));
+      return ws;
+    }
   }
   if (conv1x1_gemm_ok(1, g)) return conv1x1_ws(1, g, m_channels);
   return gemm_workspace(plan_gemm(1, g, m_channels), m_channels);

@@ -28,6 +28,7 @@
 // Sum order per output: chunks in order, filter rows, filter columns, then the remainder rows
 // in (channel, tap) order — fixed, so results are deterministic run to run.
 #include <algorithm>
+#include <type_traits>
 
 #include "conv.h"
 
@@ -239,6 +240,161 @@ __global__ void __launch_bounds__(256) k_conv_stem_lp(const float *__restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Data gradient of the same conv (C3: the BEV stem's gradient into the 64 BEV channels,
+// bf16 operands gy and W, fp32 accumulate): dx[ci][y][x] = sum_(co, r, s) W[co][ci][r][s]
+// gy[co][(y + 3 - r) / 2][(x + 3 - s) / 2] over the taps whose parity matches (stride 2, pad 3).
+// Written per output phase (py, px) = (y & 1, x & 1), y = 2u + py: phase py takes the filter
+// rows r with r + py odd, at gradient row u + (py + 3 - r) / 2 (offset -1 .. +2).  A block
+// owns 64 ci x all four phases of a coarse 4 x 32 (u, v) tile — a 8 x 64 pixel dx tile — and
+// stages the gradient patch (7 x 35 positions x all 64 co, 31 KB) ONCE; wave w takes coarse
+// row u0 + w, all four phases (8 accumulators of 32 v x 32 ci): per tap two b128 weight
+// fragments (ci halves, the (chunk, filter row) double-buffered from a prepped
+// [chunk][r][s][co half][ci][8 co] image) and one b128 patch fragment, 2 MFMAs.  Every wave
+// runs every tap once (no phase imbalance).  Sum order: co chunk, r, s — deterministic.
+// ------------------------------------------------------------------------------------------
+constexpr int SG_TU = 4, SG_TV = 32;                  // coarse tile: 4 waves x 32 columns
+constexpr int SG_PU = SG_TU + 3, SG_PV = SG_TV + 3;   // patch rows / columns (offsets -1 .. +2)
+constexpr int SG_CH = 4;                              // 16-channel chunks of the 64 co
+constexpr int SG_PATCH8 = SG_CH * SG_PU * 2 * SG_PV;  // 8-channel groups of the patch (1960)
+
+template <int OP>
+__global__ void __launch_bounds__(256, 2) k_conv_stem_dgrad_lp(const float *__restrict__ gy,
+                                                            const void *__restrict__ wimg,
+                                                            float *__restrict__ dx,
+                                                            long long dx_bytes, ConvGeom g) {
+  typedef typename SdType<OP>::T8 T8;
+  __shared__ T8 patch[SG_PATCH8];  // [chunk][row][half][column]
+  __shared__ T8 wl[2][SD_WROW8];   // [buffer][s][half][ci]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int n = blockIdx.z, u0 = blockIdx.y * SG_TU, v0 = blockIdx.x * SG_TV;
+  const int PQ = g.P * g.Q;
+  const int gbase = n * 64 * PQ;
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gy, 4LL * g.N * 64 * PQ);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(wimg, 16LL * SG_CH * SD_K * SD_WROW8);
+
+  // the whole gradient patch: task = (chunk, row, half, column), 8 channel loads (lanes on
+  // consecutive columns) -> one b128 LDS write
+  for (int t0 = 0; t0 < SG_PATCH8; t0 += 4 * 256) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 256 * u + tid;
+      const int pv = t % SG_PV, rest = t / SG_PV;
+      const int h = rest & 1, pu = (rest >> 1) % SG_PU, c = (rest >> 1) / SG_PU;
+      const int oy = u0 - 1 + pu, ox = v0 - 1 + pv;
+      const bool ok = t < SG_PATCH8 && (unsigned)oy < (unsigned)g.P && (unsigned)ox < (unsigned)g.Q;
+      const int base = gbase + (16 * c + 8 * h) * PQ + oy * g.Q + ox;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[u][e] = bload(rg, ok ? (base + e * PQ) * 4 : OOR);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 256 * u + tid;
+      if (t < SG_PATCH8) patch[t] = sd_cvt8<OP>(v[u]);
+    }
+  }
+  float4 wv[4];
+  auto load_w = [&](int c, int r) {
+    const int g0 = (c * SD_K + r) * SD_WROW8;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int task = tid + 256 * u;
+      wv[u] = bload4(rw, task < SD_WROW8 ? (g0 + task) * 16 : OOR);
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int task = tid + 256 * u;
+      if (task < SD_WROW8) wl[buf][task] = __builtin_bit_cast(T8, wv[u]);
+    }
+  };
+
+  sd_f32x16 acc[2][2][2];  // [py][px][ci half]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      acc[i][j][0] = sd_f32x16{0};
+      acc[i][j][1] = sd_f32x16{0};
+    }
+  // filter row r of chunk c: phase py = (r + 1) & 1 (compile time in each branch)
+  auto compute = [&](auto py_c, int c, int r, int buf) {
+    constexpr int PY = decltype(py_c)::value;
+    const int dr = (PY + 3 - r) >> 1;
+    const int prow = ((c * SG_PU + wave + dr + 1) * 2 + lh) * SG_PV + li;
+#pragma unroll
+    for (int s = 0; s < SD_K; ++s) {
+      const int px = (s + 1) & 1, ds = (px + 3 - s) >> 1;
+      const T8 a0 = wl[buf][(s * 2 + lh) * 64 + li];
+      const T8 a1 = wl[buf][(s * 2 + lh) * 64 + 32 + li];
+      const T8 b = patch[prow + ds + 1];
+      if (px == 0) {
+        acc[PY][0][0] = sd_mfma<OP>(a0, b, acc[PY][0][0]);
+        acc[PY][0][1] = sd_mfma<OP>(a1, b, acc[PY][0][1]);
+      } else {
+        acc[PY][1][0] = sd_mfma<OP>(a0, b, acc[PY][1][0]);
+        acc[PY][1][1] = sd_mfma<OP>(a1, b, acc[PY][1][1]);
+      }
+      // one tap's fragments live at a time: hoisting all seven taps' LDS reads ahead of the
+      // MFMAs (hipcc's choice) needs 84 more VGPRs than 2 waves / SIMD leave next to the 128
+      // accumulator registers
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  load_w(0, 0);
+  store_w(0);
+  __syncthreads();
+  constexpr int nsteps = SG_CH * SD_K;
+  for (int k = 0; k < nsteps; ++k) {
+    const int c = k / SD_K, r = k - SD_K * c;
+    const int kn = min(k + 1, nsteps - 1);
+    load_w(kn / SD_K, kn % SD_K);
+    __builtin_amdgcn_sched_barrier(0);
+    if (r & 1) compute(std::integral_constant<int, 0>{}, c, r, k & 1);
+    else compute(std::integral_constant<int, 1>{}, c, r, k & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    store_w((k + 1) & 1);
+    __syncthreads();
+  }
+
+  const __amdgpu_buffer_rsrc_t rd = rsrc(dx, dx_bytes);
+#pragma unroll
+  for (int py = 0; py < 2; ++py)
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      const int y = 2 * (u0 + wave) + py, xx = 2 * (v0 + li) + px;
+      const bool ok = y < g.H && xx < g.W;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int ci = 32 * a + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+          bstore(rd, ok ? (((n * 64 + ci) * g.H + y) * g.W + xx) * 4 : OOR, acc[py][px][a][rr]);
+        }
+    }
+}
+
+// k_conv_stem_dgrad_lp's weight image: group (c, r, s, half, ci) = W[16c + 8 half + e][ci][r][s],
+// e = 0..7, for the 64 gradient channels ci; wt tap-major fp32 [49][64][Cin].
+template <int OP>
+__global__ void __launch_bounds__(256) k_stem_wprep_dgrad(const float *__restrict__ wt, int Cin,
+                                                          typename SdType<OP>::T8 *__restrict__ img) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= SG_CH * SD_K * SD_WROW8) return;
+  const int c = i / (SD_K * SD_WROW8), rem = i - c * SD_K * SD_WROW8;
+  const int r = rem / SD_WROW8, task = rem - r * SD_WROW8;
+  const int s = task >> 7, h = (task >> 6) & 1, ci = task & 63;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = wt[((r * SD_K + s) * 64 + 16 * c + 8 * h + e) * Cin + ci];
+  img[i] = sd_cvt8<OP>(v);
+}
+
 // The 16-bit weight image k_conv_stem_lp reads: group i (8 values) of the full chunks is
 // (c, r, s, half, co) = the 8 input channels 16c + 8 half .. of tap (r, s), output channel co;
 // past them the tail's flattened rows k = (remainder channel, tap), 16 per step.  One thread
@@ -276,13 +432,19 @@ static int stem_groups(const ConvGeom &g) {
   return nch * SD_K * SD_WROW8 + ((kt + 15) >> 4) * 128;
 }
 
-size_t stem_direct_workspace(const ConvGeom &g) { return 16 * (size_t)stem_groups(g); }
+size_t stem_direct_workspace(const ConvGeom &g, int mode) {
+  return 16 * (size_t)(mode == 0 ? stem_groups(g) : SG_CH * SD_K * SD_WROW8);
+}
 
+// e2ep_tune key 35 = 1 + mask: 1 the forward, 2 the data gradient
 bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op) {
-  if (g_tune[TUNE_STEM_DIRECT] != 2) return false;
-  if (mode != 0 || (op != 1 && op != 2) || g.wlayout != 1) return false;
+  const int mask = g_tune[TUNE_STEM_DIRECT] - 1;
+  if (mode == 0 ? !(mask & 1) : mode == 1 ? !(mask & 2) : true) return false;
+  if ((op != 1 && op != 2) || g.wlayout != 1) return false;
   if (g.R != SD_K || g.S != SD_K || g.sh != 2 || g.sw != 2 || g.dh != 1 || g.dw != 1) return false;
-  if (g.Cout != 64 || M != 64 || g.Cin % 16 > SD_TAILMAX || g.ph < 0 || g.pw < 0) return false;
+  if (g.Cout != 64 || M != 64 || g.ph < 0 || g.pw < 0) return false;
+  if (mode == 0 && g.Cin % 16 > SD_TAILMAX) return false;
+  if (mode == 1 && (g.ph != 3 || g.pw != 3 || g.Cin < 64)) return false;
   if (g.P != (g.H + 2 * g.ph - SD_K) / 2 + 1 || g.Q != (g.W + 2 * g.pw - SD_K) / 2 + 1) return false;
   const long long lim = 0x7fffffffLL - 16;
   return 4LL * g.N * g.Cin * g.H * g.W < lim && 4LL * g.N * 64 * g.P * g.Q < lim &&
@@ -313,6 +475,28 @@ int stem_direct_launch(int act, int op, const float *w, const float *x, const fl
     else SD_LAUNCH(2, 0);
   }
 #undef SD_LAUNCH
+  return 0;
+}
+
+int stem_dgrad_launch(int op, const float *w, const float *gy, float *dx, long long dx_bytes,
+                      const ConvGeom &g, void *workspace, hipStream_t s) {
+  if (!stem_direct_ok(1, g, 64, op) || !workspace) {
+    set_error("conv: the direct stem data gradient does not take this geometry / needs its "
+              "weight-image workspace (stem_direct_ok, e2ep_conv_dgrad_workspace)");
+    return E2EP_EINVAL;
+  }
+  const int groups = SG_CH * SD_K * SD_WROW8;
+  const dim3 grid(cdiv((g.W + 1) / 2, SG_TV), cdiv((g.H + 1) / 2, SG_TU), g.N);
+#define SG_LAUNCH(OPV)                                                                           \
+  do {                                                                                           \
+    hipLaunchKernelGGL((k_stem_wprep_dgrad<OPV>), dim3(cdiv(groups, 256)), dim3(256), 0, s, w,   \
+                       g.Cin, static_cast<typename SdType<OPV>::T8 *>(workspace));               \
+    hipLaunchKernelGGL((k_conv_stem_dgrad_lp<OPV>), grid, dim3(256), 0, s, gy, workspace, dx,    \
+                       dx_bytes, g);                                                             \
+  } while (0)
+  if (op == 1) SG_LAUNCH(1);
+  else SG_LAUNCH(2);
+#undef SG_LAUNCH
   return 0;
 }
 

@@ -1,6 +1,7 @@
-"""A/B of the BEV stem forward (conv 7x7/2, 65 -> 64, 256^2 -> 128^2, B = 8) on 16-bit operands:
-k_conv_stem_lp (e2ep_tune key 35 = 2, csrc/conv_stem.hip) against the implicit-GEMM k_conv_lp
-(key 35 = 1).  Mean device time per launch over --iters launches (HIP events), after warmup.
+"""A/B of the BEV stem forward and data gradient (conv 7x7/2, 65 -> 64, 256^2 -> 128^2, B = 8) on
+16-bit operands: k_conv_stem_lp / k_conv_stem_dgrad_lp (e2ep_tune key 35 = 1 + mask,
+csrc/conv_stem.hip) against the implicit-GEMM k_conv_lp (key 35 = 1).  Mean device time per
+call over --iters calls (HIP events; the weight-image prep launch included), after warmup.
 
     python scripts/bench_stem.py [--mode bf16|fp16] [--batch 8] [--iters 50]"""
 import argparse
@@ -45,6 +46,31 @@ def main():
             res[name] = {"us": round(us, 1), "TFLOPs": round(flop / us / 1e6, 1)}
         finally:
             _lib.call_raw("e2ep_tune", 35, old)
+    dims = (a.batch, 65, 256, 256, 64, 7, 7, 128, 128, 2, 2, 3, 3, 1, 1)
+    wt = conv.tap_major(w)
+    gy = torch.randn(a.batch, 64, 128, 128, generator=g).cuda()
+    dx = torch.empty(a.batch, 64, 256, 256, device="cuda")
+    for key, name in ((1, "dgrad_k_conv_lp"), (4, "dgrad_k_conv_stem_dgrad_lp")):
+        old = _lib.call_raw("e2ep_tune", 35, key)
+        try:
+            with precision.use(a.mode), torch.no_grad():
+                for _ in range(5):
+                    conv.conv_dgrad(gy, wt, dims, 64, dx, w_layout=1)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    conv.conv_dgrad(gy, wt, dims, 64, dx, w_layout=1)
+                e1.record()
+                torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            outs[name] = dx.clone()
+            res[name] = {"us": round(us, 1), "TFLOPs": round(flop * 64 / 65 / us / 1e6, 1)}
+        finally:
+            _lib.call_raw("e2ep_tune", 35, old)
+    dd = (outs["dgrad_k_conv_stem_dgrad_lp"] - outs["dgrad_k_conv_lp"]).double()
+    res["dgrad_rel_l2_direct_vs_gemm"] = (dd.norm() / outs["dgrad_k_conv_lp"].double().norm()).item()
+    res["dgrad_speedup"] = round(res["dgrad_k_conv_lp"]["us"] / res["dgrad_k_conv_stem_dgrad_lp"]["us"], 2)
     d = (outs["k_conv_stem_lp"] - outs["k_conv_lp"]).double()
     res["rel_l2_direct_vs_gemm"] = (d.norm() / outs["k_conv_lp"].double().norm()).item()
     res["speedup"] = round(res["k_conv_lp"]["us"] / res["k_conv_stem_lp"]["us"], 2)

@@ -1,9 +1,9 @@
-"""k_conv_stem_lp (csrc/conv_stem.hip): the direct-convolution forward of 7x7 / 2 convs with 64
-output channels on 16-bit operands — the BEV stem (reference model/bev_encoder.py:13,26) in C3
-(bf16) and C5 (fp16).  Against fp64 convolutions of the operands rounded to the 16-bit format
-(the products are exact, the sums fp32), against the implicit-GEMM kernel it replaces
-(k_conv_lp, e2ep_tune key 35 = 1: same rounding, another fp32 sum order), and run to run
-bitwise."""
+"""k_conv_stem_lp / k_conv_stem_dgrad_lp (csrc/conv_stem.hip): the direct-convolution forward
+and data gradient of 7x7 / 2 convs with 64 output channels on 16-bit operands — the BEV stem
+(reference model/bev_encoder.py:13,26) in C3 (bf16) and C5 (fp16).  Against fp64 convolutions
+of the operands rounded to the 16-bit format (the products are exact, the sums fp32), against
+the implicit-GEMM kernel they replace (k_conv_lp, e2ep_tune key 35 = 1: same rounding, another
+fp32 sum order), and run to run bitwise.  Key 35 = 1 + mask (1 forward, 2 data gradient)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -64,18 +64,61 @@ def test_stem_direct_vs_rounded_fp64(case, mode, dt):
     assert (y.cpu().double() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
 
 
+# (N, Cin, H, W): the data gradient into the first 64 input channels (pad 3)
+DG_CASES = [
+    (2, 65, 256, 256),  # the BEV stem at full size
+    (2, 65, 50, 70),    # ragged coarse tiles
+    (1, 64, 64, 64),    # every input channel
+    (1, 65, 33, 47),    # odd sizes: the last phase row / column partly outside
+]
+
+
+@pytest.mark.parametrize("mode,dt", [("bf16", torch.bfloat16), ("fp16", torch.float16)])
+@pytest.mark.parametrize("case", DG_CASES, ids=[str(i) for i in range(len(DG_CASES))])
+def test_stem_direct_dgrad_vs_rounded_fp64(case, mode, dt):
+    from e2ep_amd import _lib, conv, precision
+    N, Cin, H, W = case
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dims = (N, Cin, H, W, 64, 7, 7, P, Q, 2, 2, 3, 3, 1, 1)
+    g = torch.Generator().manual_seed(5 + H + W)
+    w = torch.randn(64, Cin, 7, 7, generator=g) / (Cin * 49) ** 0.5
+    gy = torch.randn(N, 64, P, Q, generator=g)
+    wt = conv.tap_major(w.to(DEV))
+    gyd = gy.to(DEV)
+    out = {}
+    for key in (4, 1):
+        old = _lib.call_raw("e2ep_tune", KEY, key)
+        try:
+            with precision.use(mode):
+                for rep in range(2 if key == 4 else 1):
+                    dx = torch.empty(N, 64, H, W, device=DEV)
+                    conv.conv_dgrad(gyd, wt, dims, 64, dx, w_layout=1)
+                    out[(key, rep)] = dx
+        finally:
+            _lib.call_raw("e2ep_tune", KEY, old)
+    torch.cuda.synchronize()
+    assert torch.equal(out[(4, 0)], out[(4, 1)])  # deterministic
+    r = lambda t: t.to(dt).double()  # noqa: E731
+    x64 = torch.zeros(N, Cin, H, W, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x64, r(w), None, 2, 3).backward(r(gy))
+    ref = x64.grad[:, :64]
+    assert rel_l2(out[(4, 0)], ref) < 2e-6
+    assert rel_l2(out[(4, 0)], out[(1, 0)]) < 2e-6
+    assert (out[(4, 0)].cpu().double() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
+
+
 def test_stem_direct_in_bev_stem_training_step():
-    """The BEV stem op (bev_stem: resize + conv) in C3 with the direct forward: the output and
-    every gradient agree with the implicit-GEMM forward (the backward kernels are the same)."""
-    from e2ep_amd import bev_stem
+    """The BEV stem op (bev_stem: resize + conv) in C3 with the direct forward and data gradient
+    (key 35 = 4) against the implicit-GEMM kernels (key 35 = 1): the output and the BEV gradient
+    agree to fp32 sum order, the weight gradient (same kernel both ways) bitwise."""
+    from e2ep_amd import _lib, bev_stem, precision
     g = torch.Generator().manual_seed(11)
     bev = torch.randn(2, 64, 200, 200, generator=g).to(DEV)
     tgt = torch.randn(2, 1, 200, 200, generator=g).to(DEV)
     w = (torch.randn(64, 65, 7, 7, generator=g) / 22.6).to(DEV)
     gy = torch.randn(2, 64, 128, 128, generator=g).to(DEV)
     out = {}
-    for key in (2, 1):
-        from e2ep_amd import _lib, precision
+    for key in (4, 1):
         old = _lib.call_raw("e2ep_tune", KEY, key)
         try:
             b = bev.clone().requires_grad_(True)
@@ -86,6 +129,6 @@ def test_stem_direct_in_bev_stem_training_step():
             out[key] = (y.detach(), b.grad, wd.grad)
         finally:
             _lib.call_raw("e2ep_tune", KEY, old)
-    assert rel_l2(out[2][0], out[1][0]) < 2e-6
-    assert torch.equal(out[2][1], out[1][1])  # backward does not depend on the forward kernel
-    assert torch.equal(out[2][2], out[1][2])
+    assert rel_l2(out[4][0], out[1][0]) < 2e-6
+    assert rel_l2(out[4][1], out[1][1]) < 2e-6
+    assert torch.equal(out[4][2], out[1][2])
