@@ -2102,6 +2102,7 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
 
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
+  if (g_conv_precision == 1 && stem_direct_ok(2, g, g.Cout, 1)) return stem_wgrad_splits(g);
   if (lp_wgrad_selected()) {  // k_wgrad_lp (conv_lp.hip): C3 bf16, or fp32 when selected
     const TapList tl = live_taps(g);
     if (lp_wgrad_ok(g, tl)) return lp_wgrad_splits(g, tl, g_conv_precision == 1 ? 1 : 0);
@@ -2135,6 +2136,14 @@ int e2ep_conv_wgrad(const float *gout, const void *xv, const int *dims, int spli
                workspace_bytes, e2ep_conv_wgrad_workspace(dims, splits), splits);
   E2EP_REQUIRE(io == 0 || io == E2EP_IO_X_BF16, E2EP_EINVAL,
                "e2ep_conv_wgrad: storage mask %d not supported (0 or X bf16)", io);
+  if (io == 0 && g_conv_precision == 1 && stem_direct_ok(2, g, g.Cout, 1)) {
+    hipStream_t s = as_stream(stream);
+    float *part = static_cast<float *>(workspace);
+    const int used = stem_wgrad_launch(gout, x, g, splits, part, s);
+    E2EP_REQUIRE(used > 0, E2EP_EINVAL, "e2ep_conv_wgrad: direct stem weight gradient refused");
+    reduce_splits(part, used, g.Cout * g.Cin * g.R * g.S, dw, accumulate, g.R * g.S, live_taps(g).mask, s);
+    return launch_status("e2ep_conv_wgrad");
+  }
   if (lp_wgrad_selected()) {
     const TapList tl = live_taps(g);
     if (lp_wgrad_ok(g, tl)) {
@@ -2223,6 +2232,11 @@ static int conv_bwd_pair_plan(ConvGeom &g, int m_channels, GemmPlan &p, TapList 
   if (!geom_ok(g) || m_channels <= 0 || m_channels > g.Cin) return PAIR_NONE;
   tl = live_taps(g);
   if (tl.n <= 0) return PAIR_NONE;
+  // the BEV stem on the direct-convolution kernels (conv_stem.hip) runs its two gradients as
+  // separate launches (both faster than the paired implicit GEMMs)
+  if (g_conv_precision != 0 && (stem_direct_ok(1, g, m_channels, g_conv_precision) ||
+                                stem_direct_ok(2, g, g.Cout, g_conv_precision)))
+    return PAIR_NONE;
   // the weight-gradient kernel e2ep_conv_wgrad would run
   const bool wg_lp = lp_wgrad_selected() && lp_wgrad_ok(g, tl);
   const bool wg_2 = !wg_lp && !wgrad1x1_ok(g) && (g.P * g.Q) % W2K == 0 &&

@@ -395,6 +395,174 @@ __global__ void __launch_bounds__(256) k_stem_wprep_dgrad(const float *__restric
   img[i] = sd_cvt8<OP>(v);
 }
 
+// ------------------------------------------------------------------------------------------
+// Weight gradient of the same conv on bf16 operands (C3): dW[co][ci][r][s] = sum over pixels of
+// gy[co][oy][ox] x[ci][2oy + r - 3][2ox + s - 3].  GEMM rows m = co (64), columns n = (ci, r, s)
+// of an 8-channel chunk (392 = 13 tiles of 32), K = output pixels.  k_wgrad_lp gathers the
+// im2col column of every (ci, tap) from L2 on its own (each x value fetched ~49 times, stride-2
+// float4 windows half discarded: 492 us for the stem in the C3 step).  Here a block walks its
+// share of 4 x 16 output-pixel tiles for one channel chunk and stages per tile
+//  * gy: 64 co x 64 pixels, 16-bit rows of 64 + 8 (144 B: conflict-free b128 reads);
+//  * x: the tile's 13 x 37 input window of the 8 channels, written once per filter column s
+//    as the stride-2 sample row X[ci][row][s][ox] = x[..][2 ox + s - 3] (16-bit rows of 16 + 8,
+//    48 B): the B fragment of column (ci, r, s) and pixel octet (oy, ox..ox+7) is then ONE
+//    aligned b128 read at row 2 oy + r — each x value loaded once (coalesced), stored 3-4 times;
+//  * wave w: rows co 32 (w & 1) .., column tiles of parity w >> 1 (7 or 6 accumulators).
+// Every block writes its chunk's columns of its split slab part[split][co][ci * 49 + tap]
+// (k_reduce_splits sums the slabs in split order: deterministic).
+// ------------------------------------------------------------------------------------------
+constexpr int SW_TH = 4, SW_TW = 16;             // output pixel tile (64 pixels: 4 K-steps)
+constexpr int SW_CC = 8;                         // channels per chunk
+constexpr int SW_NCOL = SW_CC * SD_K * SD_K;     // 392 columns (ci, r, s)
+constexpr int SW_NT = (SW_NCOL + 31) / 32;       // 13 column tiles: 7 + 6 over the two wave pairs
+static_assert(SW_NT == 13, "column tiles split 7 + 6");
+constexpr int SW_XR = 2 * SW_TH + SD_K - 2;      // 13 input rows (2 (TH - 1) + 7)
+constexpr int SW_XC = 2 * SW_TW + SD_K - 2;      // 37 input columns
+constexpr int SW_XLD = SW_TW + 8;                // X row stride (elements): 48 B, conflict-free b128
+constexpr int SW_GLD = SW_TH * SW_TW + 8;        // G row stride (elements): 144 B
+constexpr int SW_OCT = SW_TW / 8;                // pixel octets per tile row
+constexpr int SW_GG = 64 * SW_TH * SW_OCT / 256;  // gy octets per thread
+
+template <int OP>
+__global__ void __launch_bounds__(256, 2) k_conv_stem_wgrad_lp(const float *__restrict__ gy,
+                                                               const float *__restrict__ x,
+                                                               float *__restrict__ part,
+                                                               int tiles_per_split, ConvGeom g) {
+  typedef typename SdType<OP>::T T;
+  typedef typename SdType<OP>::T8 T8;
+  __shared__ __attribute__((aligned(16))) T Gs[64 * SW_GLD];                   // [co][pixel]
+  __shared__ __attribute__((aligned(16))) T Xs[SW_CC * SW_XR * SD_K * SW_XLD];  // [ci][row][s][ox]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int mt = wave & 1, np = wave >> 1;  // co half, column-tile parity
+  const int cb = blockIdx.x, sp = blockIdx.y;
+  const int tq = (g.Q + SW_TW - 1) / SW_TW, tp = (g.P + SW_TH - 1) / SW_TH;
+  const int ntiles = g.N * tp * tq;
+  const int t_beg = sp * tiles_per_split, t_end = min(ntiles, t_beg + tiles_per_split);
+  const int PQ = g.P * g.Q, HW = g.H * g.W;
+  const __amdgpu_buffer_rsrc_t rg = rsrc(gy, 4LL * g.N * 64 * PQ);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
+
+  // this lane's B column per tile j (n = 32 (2 j + np) + li): X offset of (ci, r, s)
+  int boff[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int n = min(32 * (2 * j + np) + li, SW_NCOL - 1);
+    const int ci = n / (SD_K * SD_K), tap = n - SD_K * SD_K * ci;
+    const int r = tap / SD_K, s = tap - SD_K * r;
+    boff[j] = ((ci * SW_XR + r) * SD_K + s) * SW_XLD + 8 * lh;
+  }
+  const int njt = np == 0 ? 7 : 6;  // column tiles of this wave (13 = 7 + 6)
+  sd_f32x16 acc[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) acc[j] = sd_f32x16{0};
+
+  // per-tile staging through registers, one tile ahead: the next tile's loads are in flight
+  // during this tile's MFMAs (staging in dependent rounds of loads left ~12 k cycles of
+  // latency per tile; with 4 x 32 tiles the prefetch registers spilled: 343 us)
+  constexpr int XT = SW_CC * SW_XR * SW_XC;  // 3848 window values
+  constexpr int XU = (XT + 255) / 256;       // 16 per thread
+  float4 ga[SW_GG], gb[SW_GG];
+  float xv[XU];
+  auto load_tile = [&](int t) {
+    const int img = t / (tp * tq), rem = t - img * tp * tq;
+    const int oy0 = (rem / tq) * SW_TH, ox0 = (rem % tq) * SW_TW;
+#pragma unroll
+    for (int u = 0; u < SW_GG; ++u) {  // gy: group (co, row, octet)
+      const int gi = tid + 256 * u;
+      const int j = gi % SW_OCT, oyl = (gi / SW_OCT) % SW_TH, co = gi / (SW_OCT * SW_TH);
+      const int oy = oy0 + oyl, ox = ox0 + 8 * j;
+      const bool ok = oy < g.P && ox < g.Q;  // Q % 8 == 0: an octet is all in or all out
+      const int off = ((img * 64 + co) * g.P + oy) * g.Q + ox;
+      ga[u] = bload4(rg, ok ? off * 4 : OOR);
+      gb[u] = bload4(rg, ok ? (off + 4) * 4 : OOR);
+    }
+    const int iy0 = 2 * oy0 - g.ph, ix0 = 2 * ox0 - g.pw;
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {  // x window: task (ci, row, column), lanes on columns
+      const int k = 256 * u + tid;
+      const int col = k % SW_XC, rest = k / SW_XC;
+      const int row = rest % SW_XR, cl = rest / SW_XR;
+      const int ci = SW_CC * cb + cl, iy = iy0 + row, ix = ix0 + col;
+      const bool ok = k < XT && ci < g.Cin && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+      xv[u] = bload(rx, ok ? (((img * g.Cin + ci) * g.H + iy) * g.W + ix) * 4 : OOR);
+    }
+  };
+  auto store_tile = [&]() {
+    // an opaque copy of tid: without it hipcc keeps every slot's store address (computed with
+    // the load's) live across the MFMAs and spills
+    int tid2 = tid;
+    asm volatile("" : "+v"(tid2));
+#pragma unroll
+    for (int u = 0; u < SW_GG; ++u) {
+      const int gi = tid2 + 256 * u;
+      const int j = gi % SW_OCT, oyl = (gi / SW_OCT) % SW_TH, co = gi / (SW_OCT * SW_TH);
+      const float v[8] = {ga[u].x, ga[u].y, ga[u].z, ga[u].w, gb[u].x, gb[u].y, gb[u].z, gb[u].w};
+      *reinterpret_cast<T8 *>(&Gs[co * SW_GLD + oyl * SW_TW + 8 * j]) = sd_cvt8<OP>(v);
+    }
+    // each window value into its 3-4 stride-2 sample rows (filter columns s = column mod 2,
+    // + 2, ..; ox = (column - s) / 2 in range)
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int k = 256 * u + tid2;
+      if (k < XT) {
+        const int col = k % SW_XC, rest = k / SW_XC;
+        const int row = rest % SW_XR, cl = rest / SW_XR;
+        const T h = (T)xv[u];
+        T *dst = &Xs[(cl * SW_XR + row) * SD_K * SW_XLD];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int s = (col & 1) + 2 * q;
+          const int ox2 = col - s;
+          if (s < SD_K && ox2 >= 0 && ox2 <= 2 * (SW_TW - 1)) dst[s * SW_XLD + (ox2 >> 1)] = h;
+        }
+      }
+    }
+  };
+
+  if (t_beg < t_end) load_tile(t_beg);
+  for (int t = t_beg; t < t_end; ++t) {
+    __syncthreads();  // the previous tile's fragments are read
+    store_tile();
+    __syncthreads();
+    load_tile(min(t + 1, t_end - 1));  // next tile's loads in flight during the MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    // K-steps: (output row, 16-pixel half); A = gy octet of co, B = sample-row octet
+#pragma unroll
+    for (int ks = 0; ks < SW_TH * SW_TW / 16; ++ks) {
+      const int oyl = ks / (SW_TW / 16), hx = ks % (SW_TW / 16);
+      const T8 a = *reinterpret_cast<const T8 *>(&Gs[(32 * mt + li) * SW_GLD + oyl * SW_TW + 16 * hx + 8 * lh]);
+      const int kofs = 2 * oyl * SD_K * SW_XLD + 16 * hx;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        if (j < njt) {
+          const T8 b = *reinterpret_cast<const T8 *>(&Xs[boff[j] + kofs]);
+          acc[j] = sd_mfma<OP>(a, b, acc[j]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one K-step's fragments live at a time
+    }
+  }
+
+  // slab columns of this chunk: n = ci_l * 49 + tap -> column (8 cb + ci_l) * 49 + tap
+  const int ncols = g.Cin * SD_K * SD_K;
+  const __amdgpu_buffer_rsrc_t rp = rsrc(part, 4LL * gridDim.y * 64 * ncols);
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    if (j >= njt) break;
+    const int n = 32 * (2 * j + np) + li;
+    const int col = SW_CC * cb * SD_K * SD_K + n;
+    const bool nok = n < SW_NCOL && col < ncols;
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const int co = 32 * mt + (rr & 3) + 8 * (rr >> 2) + 4 * lh;
+      bstore(rp, nok ? ((sp * 64 + co) * ncols + col) * 4 : OOR, acc[j][rr]);
+    }
+  }
+}
+
 // The 16-bit weight image k_conv_stem_lp reads: group i (8 values) of the full chunks is
 // (c, r, s, half, co) = the 8 input channels 16c + 8 half .. of tap (r, s), output channel co;
 // past them the tail's flattened rows k = (remainder channel, tap), 16 per step.  One thread
@@ -436,15 +604,16 @@ size_t stem_direct_workspace(const ConvGeom &g, int mode) {
   return 16 * (size_t)(mode == 0 ? stem_groups(g) : SG_CH * SD_K * SD_WROW8);
 }
 
-// e2ep_tune key 35 = 1 + mask: 1 the forward, 2 the data gradient
+// e2ep_tune key 35 = 1 + mask: 1 the forward, 2 the data gradient, 4 the weight gradient
 bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op) {
   const int mask = g_tune[TUNE_STEM_DIRECT] - 1;
-  if (mode == 0 ? !(mask & 1) : mode == 1 ? !(mask & 2) : true) return false;
-  if ((op != 1 && op != 2) || g.wlayout != 1) return false;
+  if (mode == 0 ? !(mask & 1) : mode == 1 ? !(mask & 2) : mode == 2 ? !(mask & 4) : true) return false;
+  if ((op != 1 && op != 2) || (mode == 2 && op != 1) || (mode != 2 && g.wlayout != 1)) return false;
   if (g.R != SD_K || g.S != SD_K || g.sh != 2 || g.sw != 2 || g.dh != 1 || g.dw != 1) return false;
   if (g.Cout != 64 || M != 64 || g.ph < 0 || g.pw < 0) return false;
   if (mode == 0 && g.Cin % 16 > SD_TAILMAX) return false;
   if (mode == 1 && (g.ph != 3 || g.pw != 3 || g.Cin < 64)) return false;
+  if (mode == 2 && (g.Q % 8 != 0 || g.Cin > 4096)) return false;
   if (g.P != (g.H + 2 * g.ph - SD_K) / 2 + 1 || g.Q != (g.W + 2 * g.pw - SD_K) / 2 + 1) return false;
   const long long lim = 0x7fffffffLL - 16;
   return 4LL * g.N * g.Cin * g.H * g.W < lim && 4LL * g.N * 64 * g.P * g.Q < lim &&
@@ -498,6 +667,27 @@ int stem_dgrad_launch(int op, const float *w, const float *gy, float *dx, long l
   else SG_LAUNCH(2);
 #undef SG_LAUNCH
   return 0;
+}
+
+// slabs of the direct weight gradient: ~2 blocks per CU over the channel chunks
+int stem_wgrad_splits(const ConvGeom &g) {
+  const int chunks = (g.Cin + SW_CC - 1) / SW_CC;
+  const int ntiles = g.N * ((g.P + SW_TH - 1) / SW_TH) * ((g.Q + SW_TW - 1) / SW_TW);
+  return std::max(1, std::min(ntiles, 512 / chunks));
+}
+
+int stem_wgrad_launch(const float *gy, const float *x, const ConvGeom &g, int splits, float *part,
+                      hipStream_t s) {
+  if (!stem_direct_ok(2, g, 64, 1) || splits < 1) {
+    set_error("conv: the direct stem weight gradient does not take this geometry (stem_direct_ok)");
+    return -1;
+  }
+  const int ntiles = g.N * ((g.P + SW_TH - 1) / SW_TH) * ((g.Q + SW_TW - 1) / SW_TW);
+  const int tps = cdiv(ntiles, splits);
+  const int used = cdiv(ntiles, tps);
+  const dim3 grid(cdiv(g.Cin, SW_CC), used);
+  hipLaunchKernelGGL((k_conv_stem_wgrad_lp<1>), grid, dim3(256), 0, s, gy, x, part, tps, g);
+  return used;
 }
 
 }  // namespace e2ep

@@ -1,6 +1,7 @@
-"""A/B of the BEV stem forward and data gradient (conv 7x7/2, 65 -> 64, 256^2 -> 128^2, B = 8) on
-16-bit operands: k_conv_stem_lp / k_conv_stem_dgrad_lp (e2ep_tune key 35 = 1 + mask,
-csrc/conv_stem.hip) against the implicit-GEMM k_conv_lp (key 35 = 1).  Mean device time per
+"""A/B of the BEV stem forward, data gradient and (bf16) weight gradient (conv 7x7/2, 65 -> 64, 256^2 -> 128^2, B = 8) on
+16-bit operands: k_conv_stem_lp / k_conv_stem_dgrad_lp / k_conv_stem_wgrad_lp (e2ep_tune key 35 = 1 + mask,
+csrc/conv_stem.hip) against the implicit GEMMs k_conv_lp / k_wgrad_lp (key 35 = 1); the weight
+gradient's time includes its split reduction.  Mean device time per
 call over --iters calls (HIP events; the weight-image prep launch included), after warmup.
 
     python scripts/bench_stem.py [--mode bf16|fp16] [--batch 8] [--iters 50]"""
@@ -71,6 +72,29 @@ def main():
     dd = (outs["dgrad_k_conv_stem_dgrad_lp"] - outs["dgrad_k_conv_lp"]).double()
     res["dgrad_rel_l2_direct_vs_gemm"] = (dd.norm() / outs["dgrad_k_conv_lp"].double().norm()).item()
     res["dgrad_speedup"] = round(res["dgrad_k_conv_lp"]["us"] / res["dgrad_k_conv_stem_dgrad_lp"]["us"], 2)
+    if a.mode == "bf16":  # the weight gradient (bf16 operands in C3 only)
+        dw = torch.empty(64, 65, 7, 7, device="cuda")
+        for key, name in ((1, "wgrad_k_wgrad_lp"), (8, "wgrad_k_conv_stem_wgrad_lp")):
+            old = _lib.call_raw("e2ep_tune", 35, key)
+            try:
+                with precision.use(a.mode), torch.no_grad():
+                    for _ in range(5):
+                        conv.conv_wgrad(gy, x, dims, dw)
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(a.iters):
+                        conv.conv_wgrad(gy, x, dims, dw)
+                    e1.record()
+                    torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / a.iters
+                outs[name] = dw.clone()
+                res[name] = {"us": round(us, 1), "TFLOPs": round(flop / us / 1e6, 1)}
+            finally:
+                _lib.call_raw("e2ep_tune", 35, old)
+        dd = (outs["wgrad_k_conv_stem_wgrad_lp"] - outs["wgrad_k_wgrad_lp"]).double()
+        res["wgrad_rel_l2_direct_vs_gemm"] = (dd.norm() / outs["wgrad_k_wgrad_lp"].double().norm()).item()
+        res["wgrad_speedup"] = round(res["wgrad_k_wgrad_lp"]["us"] / res["wgrad_k_conv_stem_wgrad_lp"]["us"], 2)
     d = (outs["k_conv_stem_lp"] - outs["k_conv_lp"]).double()
     res["rel_l2_direct_vs_gemm"] = (d.norm() / outs["k_conv_lp"].double().norm()).item()
     res["speedup"] = round(res["k_conv_lp"]["us"] / res["k_conv_stem_lp"]["us"], 2)

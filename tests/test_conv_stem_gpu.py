@@ -3,7 +3,8 @@ and data gradient of 7x7 / 2 convs with 64 output channels on 16-bit operands â€
 (reference model/bev_encoder.py:13,26) in C3 (bf16) and C5 (fp16).  Against fp64 convolutions
 of the operands rounded to the 16-bit format (the products are exact, the sums fp32), against
 the implicit-GEMM kernel they replace (k_conv_lp, e2ep_tune key 35 = 1: same rounding, another
-fp32 sum order), and run to run bitwise.  Key 35 = 1 + mask (1 forward, 2 data gradient)."""
+fp32 sum order), and run to run bitwise.  Key 35 = 1 + mask (1 forward, 2 data gradient, 4 weight
+gradient, k_conv_stem_wgrad_lp, bf16 only)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -108,9 +109,9 @@ def test_stem_direct_dgrad_vs_rounded_fp64(case, mode, dt):
 
 
 def test_stem_direct_in_bev_stem_training_step():
-    """The BEV stem op (bev_stem: resize + conv) in C3 with the direct forward and data gradient
-    (key 35 = 4) against the implicit-GEMM kernels (key 35 = 1): the output and the BEV gradient
-    agree to fp32 sum order, the weight gradient (same kernel both ways) bitwise."""
+    """The BEV stem op (bev_stem: resize + conv) in C3 on the direct kernels (key 35 = 8) against
+    the implicit-GEMM kernels (key 35 = 1): the output and both gradients agree to fp32 sum
+    order."""
     from e2ep_amd import _lib, bev_stem, precision
     g = torch.Generator().manual_seed(11)
     bev = torch.randn(2, 64, 200, 200, generator=g).to(DEV)
@@ -118,7 +119,7 @@ def test_stem_direct_in_bev_stem_training_step():
     w = (torch.randn(64, 65, 7, 7, generator=g) / 22.6).to(DEV)
     gy = torch.randn(2, 64, 128, 128, generator=g).to(DEV)
     out = {}
-    for key in (4, 1):
+    for key in (8, 1):
         old = _lib.call_raw("e2ep_tune", KEY, key)
         try:
             b = bev.clone().requires_grad_(True)
@@ -129,6 +130,46 @@ def test_stem_direct_in_bev_stem_training_step():
             out[key] = (y.detach(), b.grad, wd.grad)
         finally:
             _lib.call_raw("e2ep_tune", KEY, old)
-    assert rel_l2(out[4][0], out[1][0]) < 2e-6
-    assert rel_l2(out[4][1], out[1][1]) < 2e-6
-    assert torch.equal(out[4][2], out[1][2])
+    assert rel_l2(out[8][0], out[1][0]) < 2e-6
+    assert rel_l2(out[8][1], out[1][1]) < 2e-6
+    assert rel_l2(out[8][2], out[1][2]) < 2e-6
+
+
+# (N, Cin, H, W): weight gradient, Q % 8 == 0
+WG_CASES = [
+    (2, 65, 256, 256),  # the BEV stem at full size (9 channel chunks, the last one channel)
+    (2, 65, 50, 80),    # ragged row tiles (P = 25), Q = 40
+    (1, 64, 64, 64),    # whole chunks
+    (1, 3, 32, 48),     # one partial chunk
+    (3, 17, 40, 16),    # Q = 8: one octet of a 32-column tile
+]
+
+
+@pytest.mark.parametrize("case", WG_CASES, ids=[str(i) for i in range(len(WG_CASES))])
+def test_stem_direct_wgrad_vs_rounded_fp64(case):
+    from e2ep_amd import _lib, conv, precision
+    N, Cin, H, W = case
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dims = (N, Cin, H, W, 64, 7, 7, P, Q, 2, 2, 3, 3, 1, 1)
+    g = torch.Generator().manual_seed(9 + H + W + Cin)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    gy = torch.randn(N, 64, P, Q, generator=g)
+    xd, gyd = x.to(DEV), gy.to(DEV)
+    out = {}
+    for key in (8, 1):
+        old = _lib.call_raw("e2ep_tune", KEY, key)
+        try:
+            with precision.use("bf16"):
+                for rep in range(2 if key == 8 else 1):
+                    dw = torch.empty(64, Cin, 7, 7, device=DEV)
+                    conv.conv_wgrad(gyd, xd, dims, dw)
+                    out[(key, rep)] = dw
+        finally:
+            _lib.call_raw("e2ep_tune", KEY, old)
+    torch.cuda.synchronize()
+    assert torch.equal(out[(8, 0)], out[(8, 1)])  # deterministic
+    r = lambda t: t.to(torch.bfloat16).double()  # noqa: E731
+    w64 = torch.zeros(64, Cin, 7, 7, dtype=torch.float64, requires_grad=True)
+    F.conv2d(r(x), w64, None, 2, 3).backward(r(gy))
+    assert rel_l2(out[(8, 0)], w64.grad) < 5e-6
+    assert rel_l2(out[(8, 0)], out[(1, 0)]) < 5e-6
