@@ -102,18 +102,19 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void
 // the BEV stem in C3 / C5), conv_stem.hip: the forward (mode 0, k_conv_stem_lp) stages each
 // output tile's input patch once per 16-channel chunk, the data gradient (mode 1, pad 3, 64
 // gradient channels, k_conv_stem_dgrad_lp) each tile's gradient patch once.  Tap-major
-// weights; e2ep_tune key 35 = 1 + mask (1 forward, 2 data gradient, 4 weight gradient).  workspace:
-// stem_direct_workspace(g, mode) bytes for the 16-bit weight image (k_stem_wprep*).
+// weights; e2ep_tune key 35 = 1 + mask (1 forward, 2 data gradient, 4 weight gradient, 8 the
+// forward / data gradient on fp32 operands too, op 0).  workspace: stem_direct_workspace(g, mode,
+// op) bytes for the weight image (k_stem_wprep*).
 bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op);
-size_t stem_direct_workspace(const ConvGeom &g, int mode);
+size_t stem_direct_workspace(const ConvGeom &g, int mode, int op);
 int stem_direct_launch(int act, int op, const float *w, const float *x, const float *bias, float *y,
                        long long y_bytes, const ConvGeom &g, void *workspace, hipStream_t s);
 int stem_dgrad_launch(int op, const float *w, const float *gy, float *dx, long long dx_bytes,
                       const ConvGeom &g, void *workspace, hipStream_t s);
-// mode 2: the weight gradient on bf16 operands (k_conv_stem_wgrad_lp, op 1): split slabs
-// part[split][64][Cin * 49] for the split reduction; returns the slabs written (-1: refused)
+// mode 2: the weight gradient (k_conv_stem_wgrad_lp, op 1 bf16 / op 0 fp32 operands): split
+// slabs part[split][64][Cin * 49] for the split reduction; returns the slabs written (-1: refused)
 int stem_wgrad_splits(const ConvGeom &g);
 int stem_wgrad_launch(const float *gy, const float *x, const ConvGeom &g, int splits, float *part,
-                      hipStream_t s);
+                      hipStream_t s, int op);
 
 }  // namespace e2ep

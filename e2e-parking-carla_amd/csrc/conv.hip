@@ -1816,7 +1816,7 @@ static int fwd_stats_tiles(const ConvGeom &g0) {
   g.xcd = g_tune[TUNE_XCD] == 2;
   if (direct_ok(g)) return 0;
   const int route = conv_route(0, g, g.Cout);
-  if (route == ROUTE_LP && stem_direct_ok(0, g, g.Cout, g_conv_precision)) return 0;  // no stats
+  if (stem_direct_ok(0, g, g.Cout, g_conv_precision)) return 0;  // the direct stem takes no stats
   if (route == ROUTE_LP) return lp_stats_tiles(g, g_conv_precision);
   if (route == ROUTE_LP32) return lp_stats_tiles(g, 0);
   if (route != ROUTE_GEMM || g_conv_precision != 0) return 0;  // fp32 k_conv_gemm only
@@ -1838,10 +1838,11 @@ static int launch_gemm(int mode, int act, const float *w, const void *srcv, cons
     set_error("conv: BatchNorm statistics requested from a kernel that does not take them");
     return E2EP_EINVAL;
   }
-  if (route == ROUTE_LP && !stats && !io && mode == 0 && stem_direct_ok(0, g, M, g_conv_precision))
+  // the BEV stem's direct-convolution kernels (conv_stem.hip) whatever the route
+  if (!stats && !io && mode == 0 && stem_direct_ok(0, g, M, g_conv_precision))
     return stem_direct_launch(act, g_conv_precision, w, static_cast<const float *>(srcv), bias,
                               static_cast<float *>(dstv), dst_bytes, g, workspace, s);
-  if (route == ROUTE_LP && !io && mode == 1 && !bias && stem_direct_ok(1, g, M, g_conv_precision))
+  if (!io && mode == 1 && !bias && stem_direct_ok(1, g, M, g_conv_precision))
     return stem_dgrad_launch(g_conv_precision, w, static_cast<const float *>(srcv),
                              static_cast<float *>(dstv), dst_bytes, g, workspace, s);
   if (route == ROUTE_LP)
@@ -1963,7 +1964,15 @@ extern "C" {
 
 // (sized for the k_conv_gemm plan; the k_conv_gemm2 path needs none, so a caller may pass a
 // workspace sized by these queries whichever kernel runs)
+static size_t conv_fwd_workspace(const int *dims);
 size_t e2ep_conv_fwd_workspace(const int *dims) {
+  ConvGeom g = make_geom(dims);
+  g.wlayout = 1;  // w_layout unknown here: cover the direct stem's weight image
+  const size_t ws = conv_fwd_workspace(dims);
+  return stem_direct_ok(0, g, g.Cout, g_conv_precision)
+             ? std::max(ws, stem_direct_workspace(g, 0, g_conv_precision)) : ws;
+}
+static size_t conv_fwd_workspace(const int *dims) {
   ConvGeom g = make_geom(dims);
   if (direct_ok(g)) return 0;
   if (g_conv_precision != 0 || g_tune[TUNE_LP32] == 2) {  // w_layout unknown here: cover all
@@ -1971,7 +1980,6 @@ size_t e2ep_conv_fwd_workspace(const int *dims) {
     if (lp_ok(0, g, g.Cout, g_conv_precision)) {
       size_t ws = std::max(lp_workspace(0, g, g.Cout, g_conv_precision),
                            gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout));
-      if (stem_direct_ok(0, g, g.Cout, g_conv_precision)) ws = std::max(ws, stem_direct_workspace(g, 0));
       return ws;
     }
   }
@@ -1979,14 +1987,21 @@ size_t e2ep_conv_fwd_workspace(const int *dims) {
   return gemm_workspace(plan_gemm(0, g, g.Cout), g.Cout);
 }
 
+static size_t conv_dgrad_workspace(const int *dims, int m_channels);
 size_t e2ep_conv_dgrad_workspace(const int *dims, int m_channels) {
+  ConvGeom g = make_geom(dims);
+  g.wlayout = 1;
+  const size_t ws = conv_dgrad_workspace(dims, m_channels);
+  return stem_direct_ok(1, g, m_channels, g_conv_precision)
+             ? std::max(ws, stem_direct_workspace(g, 1, g_conv_precision)) : ws;
+}
+static size_t conv_dgrad_workspace(const int *dims, int m_channels) {
   ConvGeom g = make_geom(dims);
   if (g_conv_precision != 0 || g_tune[TUNE_LP32] == 2) {
     g.wlayout = 1;
     if (lp_ok(1, g, m_channels, g_conv_precision)) {
       size_t ws = std::max(lp_workspace(1, g, m_channels, g_conv_precision),
                            gemm_workspace(plan_gemm(1, g, m_channels), m_channels));
-      if (stem_direct_ok(1, g, m_channels, g_conv_precision)) ws = std::max(ws, stem_direct_workspace(g, 1));
       return ws;
     }
   }
@@ -2102,7 +2117,7 @@ int e2ep_conv_dgrad(const float *gout, const float *w, const int *dims, int m_ch
 
 int e2ep_conv_wgrad_splits(const int *dims) {
   ConvGeom g = make_geom(dims);
-  if (g_conv_precision == 1 && stem_direct_ok(2, g, g.Cout, 1)) return stem_wgrad_splits(g);
+  if (stem_direct_ok(2, g, g.Cout, g_conv_precision == 1 ? 1 : 0)) return stem_wgrad_splits(g);
   if (lp_wgrad_selected()) {  // k_wgrad_lp (conv_lp.hip): C3 bf16, or fp32 when selected
     const TapList tl = live_taps(g);
     if (lp_wgrad_ok(g, tl)) return lp_wgrad_splits(g, tl, g_conv_precision == 1 ? 1 : 0);
@@ -2136,10 +2151,11 @@ int e2ep_conv_wgrad(const float *gout, const void *xv, const int *dims, int spli
                workspace_bytes, e2ep_conv_wgrad_workspace(dims, splits), splits);
   E2EP_REQUIRE(io == 0 || io == E2EP_IO_X_BF16, E2EP_EINVAL,
                "e2ep_conv_wgrad: storage mask %d not supported (0 or X bf16)", io);
-  if (io == 0 && g_conv_precision == 1 && stem_direct_ok(2, g, g.Cout, 1)) {
+  // the weight gradient's operands: bf16 in C3, fp32 otherwise (C5's fp16 mode included)
+  if (io == 0 && stem_direct_ok(2, g, g.Cout, g_conv_precision == 1 ? 1 : 0)) {
     hipStream_t s = as_stream(stream);
     float *part = static_cast<float *>(workspace);
-    const int used = stem_wgrad_launch(gout, x, g, splits, part, s);
+    const int used = stem_wgrad_launch(gout, x, g, splits, part, s, g_conv_precision == 1 ? 1 : 0);
     E2EP_REQUIRE(used > 0, E2EP_EINVAL, "e2ep_conv_wgrad: direct stem weight gradient refused");
     reduce_splits(part, used, g.Cout * g.Cin * g.R * g.S, dw, accumulate, g.R * g.S, live_taps(g).mask, s);
     return launch_status("e2ep_conv_wgrad");
@@ -2234,8 +2250,7 @@ static int conv_bwd_pair_plan(ConvGeom &g, int m_channels, GemmPlan &p, TapList 
   if (tl.n <= 0) return PAIR_NONE;
   // the BEV stem on the direct-convolution kernels (conv_stem.hip) runs its two gradients as
   // separate launches (both faster than the paired implicit GEMMs)
-  if (g_conv_precision != 0 && (stem_direct_ok(1, g, m_channels, g_conv_precision) ||
-                                stem_direct_ok(2, g, g.Cout, g_conv_precision)))
+  if (stem_direct_ok(1, g, m_channels, g_conv_precision) || stem_direct_ok(2, g, g.Cout, g_conv_precision))
     return PAIR_NONE;
   // the weight-gradient kernel e2ep_conv_wgrad would run
   const bool wg_lp = lp_wgrad_selected() && lp_wgrad_ok(g, tl);

@@ -44,6 +44,7 @@ typedef __bf16 sd_bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 sd_f16x8 __attribute__((ext_vector_type(8)));
 
 template <int OP> struct SdType;
+template <> struct SdType<0> { typedef float T; typedef sd_f32x8 T8; };  // exact-f32 MFMA (C2)
 template <> struct SdType<1> { typedef __bf16 T; typedef sd_bf16x8 T8; };
 template <> struct SdType<2> { typedef _Float16 T; typedef sd_f16x8 T8; };
 
@@ -65,11 +66,36 @@ __device__ __forceinline__ typename SdType<OP>::T8 sd_cvt8(const float *v) {
   return __builtin_convertvector(f, typename SdType<OP>::T8);
 }
 
+// One 16-deep K-step of a 32 x 32 tile: one v_mfma_f32_32x32x16_{bf16,f16}; for fp32 operands
+// (OP 0, v_mfma_f32_32x32x2_f32) eight, MFMA t taking element t of each lane half's 8 values
+// (k = t and 8 + t: the same 16 k, as k_conv_gemm2 permutes them)
 template <int OP>
 __device__ __forceinline__ sd_f32x16 sd_mfma(typename SdType<OP>::T8 a, typename SdType<OP>::T8 b,
                                              sd_f32x16 c) {
-  if constexpr (OP == 1) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-  else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  if constexpr (OP == 1) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  } else if constexpr (OP == 2) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], b[t], c, 0, 0, 0);
+    return c;
+  }
+}
+
+// group `i` (8 values: 16 B, or 32 B for fp32) of a weight image; zeros when !ok
+template <int OP>
+__device__ __forceinline__ typename SdType<OP>::T8 sd_gload(__amdgpu_buffer_rsrc_t r, int i, bool ok) {
+  typedef typename SdType<OP>::T8 T8;
+  if constexpr (OP == 0) {
+    const float4 u = bload4(r, ok ? i * 32 : OOR), v = bload4(r, ok ? i * 32 + 16 : OOR);
+    T8 o;
+    o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w;
+    o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
+    return o;
+  } else {
+    return __builtin_bit_cast(T8, bload4(r, ok ? i * 16 : OOR));
+  }
 }
 
 }  // namespace
@@ -99,7 +125,7 @@ __global__ void __launch_bounds__(256) k_conv_stem_lp(const float *__restrict__ 
   const __amdgpu_buffer_rsrc_t rx = rsrc(x, 4LL * g.N * g.Cin * HW);
   const int kt = crem * SD_K * SD_K;
   const int tsteps = (kt + 15) >> 4;
-  const __amdgpu_buffer_rsrc_t rw = rsrc(wimg, 16LL * (nch * SD_K * SD_WROW8 + tsteps * 128));
+  const __amdgpu_buffer_rsrc_t rw = rsrc(wimg, (long long)sizeof(T8) * (nch * SD_K * SD_WROW8 + tsteps * 128));
 
   // one 16-channel chunk's patch: task = (half, row, column), 8 channel loads (lanes on
   // consecutive columns: coalesced) -> one b128 LDS write
@@ -127,20 +153,20 @@ __global__ void __launch_bounds__(256) k_conv_stem_lp(const float *__restrict__ 
     }
   };
   // one (chunk, filter row) of the weight image: 896 consecutive 16-B groups
-  float4 wv[4];
+  T8 wv[4];
   auto load_w = [&](int c, int r) {
     const int g0 = (c * SD_K + r) * SD_WROW8;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int task = tid + 256 * u;
-      wv[u] = bload4(rw, task < SD_WROW8 ? (g0 + task) * 16 : OOR);
+      wv[u] = sd_gload<OP>(rw, g0 + task, task < SD_WROW8);
     }
   };
   auto store_w = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int task = tid + 256 * u;
-      if (task < SD_WROW8) wl[buf][task] = __builtin_bit_cast(T8, wv[u]);
+      if (task < SD_WROW8) wl[buf][task] = wv[u];
     }
   };
 
@@ -198,7 +224,7 @@ __global__ void __launch_bounds__(256) k_conv_stem_lp(const float *__restrict__ 
       tp[t] = (T)bload(rx, ok ? (xbase + (16 * nch + cc) * HW + iy * g.W + ix) * 4 : OOR);
     }
     for (int t = tid; t < tsteps * 128; t += 256)
-      tw[t] = __builtin_bit_cast(T8, bload4(rw, (nch * SD_K * SD_WROW8 + t) * 16));
+      tw[t] = sd_gload<OP>(rw, nch * SD_K * SD_WROW8 + t, true);
     __syncthreads();
     for (int step = 0; step < tsteps; ++step) {
       const T8 a0 = tw[(step * 2 + lh) * 64 + li];
@@ -259,7 +285,7 @@ constexpr int SG_CH = 4;                              // 16-channel chunks of th
 constexpr int SG_PATCH8 = SG_CH * SG_PU * 2 * SG_PV;  // 8-channel groups of the patch (1960)
 
 template <int OP>
-__global__ void __launch_bounds__(256, 2) k_conv_stem_dgrad_lp(const float *__restrict__ gy,
+__global__ void __launch_bounds__(256, OP == 0 ? 1 : 2) k_conv_stem_dgrad_lp(const float *__restrict__ gy,
                                                             const void *__restrict__ wimg,
                                                             float *__restrict__ dx,
                                                             long long dx_bytes, ConvGeom g) {
@@ -274,7 +300,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_stem_dgrad_lp(const float *__re
   const int PQ = g.P * g.Q;
   const int gbase = n * 64 * PQ;
   const __amdgpu_buffer_rsrc_t rg = rsrc(gy, 4LL * g.N * 64 * PQ);
-  const __amdgpu_buffer_rsrc_t rw = rsrc(wimg, 16LL * SG_CH * SD_K * SD_WROW8);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(wimg, (long long)sizeof(T8) * SG_CH * SD_K * SD_WROW8);
 
   // the whole gradient patch: task = (chunk, row, half, column), 8 channel loads (lanes on
   // consecutive columns) -> one b128 LDS write
@@ -297,20 +323,20 @@ __global__ void __launch_bounds__(256, 2) k_conv_stem_dgrad_lp(const float *__re
       if (t < SG_PATCH8) patch[t] = sd_cvt8<OP>(v[u]);
     }
   }
-  float4 wv[4];
+  T8 wv[4];
   auto load_w = [&](int c, int r) {
     const int g0 = (c * SD_K + r) * SD_WROW8;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int task = tid + 256 * u;
-      wv[u] = bload4(rw, task < SD_WROW8 ? (g0 + task) * 16 : OOR);
+      wv[u] = sd_gload<OP>(rw, g0 + task, task < SD_WROW8);
     }
   };
   auto store_w = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int task = tid + 256 * u;
-      if (task < SD_WROW8) wl[buf][task] = __builtin_bit_cast(T8, wv[u]);
+      if (task < SD_WROW8) wl[buf][task] = wv[u];
     }
   };
 
@@ -424,7 +450,7 @@ constexpr int SW_OCT = SW_TW / 8;                // pixel octets per tile row
 constexpr int SW_GG = 64 * SW_TH * SW_OCT / 256;  // gy octets per thread
 
 template <int OP>
-__global__ void __launch_bounds__(256, 2) k_conv_stem_wgrad_lp(const float *__restrict__ gy,
+__global__ void __launch_bounds__(256, OP == 0 ? 1 : 2) k_conv_stem_wgrad_lp(const float *__restrict__ gy,
                                                                const float *__restrict__ x,
                                                                float *__restrict__ part,
                                                                int tiles_per_split, ConvGeom g) {
@@ -600,15 +626,19 @@ static int stem_groups(const ConvGeom &g) {
   return nch * SD_K * SD_WROW8 + ((kt + 15) >> 4) * 128;
 }
 
-size_t stem_direct_workspace(const ConvGeom &g, int mode) {
-  return 16 * (size_t)(mode == 0 ? stem_groups(g) : SG_CH * SD_K * SD_WROW8);
+size_t stem_direct_workspace(const ConvGeom &g, int mode, int op) {
+  return (op == 0 ? 32 : 16) * (size_t)(mode == 0 ? stem_groups(g) : SG_CH * SD_K * SD_WROW8);
 }
 
-// e2ep_tune key 35 = 1 + mask: 1 the forward, 2 the data gradient, 4 the weight gradient
+// e2ep_tune key 35 = 1 + mask: 1 the forward, 2 the data gradient, 4 the weight gradient (bf16
+// or fp32 operands), 8 the fp32-operand kernels too (exact-f32 MFMA: C2, and C5's fp32 weight
+// gradient)
 bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op) {
   const int mask = g_tune[TUNE_STEM_DIRECT] - 1;
   if (mode == 0 ? !(mask & 1) : mode == 1 ? !(mask & 2) : mode == 2 ? !(mask & 4) : true) return false;
-  if ((op != 1 && op != 2) || (mode == 2 && op != 1) || (mode != 2 && g.wlayout != 1)) return false;
+  if (op < 0 || op > 2 || (op == 0 && !(mask & 8)) || (mode == 2 && op == 2) ||
+      (mode != 2 && g.wlayout != 1))
+    return false;
   if (g.R != SD_K || g.S != SD_K || g.sh != 2 || g.sw != 2 || g.dh != 1 || g.dw != 1) return false;
   if (g.Cout != 64 || M != 64 || g.ph < 0 || g.pw < 0) return false;
   if (mode == 0 && g.Cin % 16 > SD_TAILMAX) return false;
@@ -639,9 +669,12 @@ int stem_direct_launch(int act, int op, const float *w, const float *x, const fl
   if (op == 1) {
     if (act) SD_LAUNCH(1, 1);
     else SD_LAUNCH(1, 0);
-  } else {
+  } else if (op == 2) {
     if (act) SD_LAUNCH(2, 1);
     else SD_LAUNCH(2, 0);
+  } else {
+    if (act) SD_LAUNCH(0, 1);
+    else SD_LAUNCH(0, 0);
   }
 #undef SD_LAUNCH
   return 0;
@@ -664,7 +697,8 @@ int stem_dgrad_launch(int op, const float *w, const float *gy, float *dx, long l
                        dx_bytes, g);                                                             \
   } while (0)
   if (op == 1) SG_LAUNCH(1);
-  else SG_LAUNCH(2);
+  else if (op == 2) SG_LAUNCH(2);
+  else SG_LAUNCH(0);
 #undef SG_LAUNCH
   return 0;
 }
@@ -677,8 +711,8 @@ int stem_wgrad_splits(const ConvGeom &g) {
 }
 
 int stem_wgrad_launch(const float *gy, const float *x, const ConvGeom &g, int splits, float *part,
-                      hipStream_t s) {
-  if (!stem_direct_ok(2, g, 64, 1) || splits < 1) {
+                      hipStream_t s, int op) {
+  if (!stem_direct_ok(2, g, 64, op) || splits < 1) {
     set_error("conv: the direct stem weight gradient does not take this geometry (stem_direct_ok)");
     return -1;
   }
@@ -686,7 +720,8 @@ int stem_wgrad_launch(const float *gy, const float *x, const ConvGeom &g, int sp
   const int tps = cdiv(ntiles, splits);
   const int used = cdiv(ntiles, tps);
   const dim3 grid(cdiv(g.Cin, SW_CC), used);
-  hipLaunchKernelGGL((k_conv_stem_wgrad_lp<1>), grid, dim3(256), 0, s, gy, x, part, tps, g);
+  if (op == 1) hipLaunchKernelGGL((k_conv_stem_wgrad_lp<1>), grid, dim3(256), 0, s, gy, x, part, tps, g);
+  else hipLaunchKernelGGL((k_conv_stem_wgrad_lp<0>), grid, dim3(256), 0, s, gy, x, part, tps, g);
   return used;
 }
 

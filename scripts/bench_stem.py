@@ -4,7 +4,8 @@ csrc/conv_stem.hip) against the implicit GEMMs k_conv_lp / k_wgrad_lp (key 35 = 
 gradient's time includes its split reduction.  Mean device time per
 call over --iters calls (HIP events; the weight-image prep launch included), after warmup.
 
-    python scripts/bench_stem.py [--mode bf16|fp16] [--batch 8] [--iters 50]"""
+    python scripts/bench_stem.py [--mode bf16|fp16|fp32] [--batch 8] [--iters 50]
+(fp32: the exact-f32 MFMA variants, key 35 mask 8, against k_conv_gemm2)"""
 import argparse
 import json
 import os
@@ -29,7 +30,8 @@ def main():
     flop = 2.0 * a.batch * 64 * 128 * 128 * 65 * 49
     res = {"config": f"B={a.batch} 65x256^2 -> 64x128^2, 7x7/2, {a.mode} operands", "flop": flop}
     outs = {}
-    for key, name in ((1, "k_conv_lp"), (2, "k_conv_stem_lp")):
+    f32 = 8 if a.mode == "fp32" else 0
+    for key, name in ((1, "k_conv_lp"), (2 + f32, "k_conv_stem_lp")):
         old = _lib.call_raw("e2ep_tune", 35, key)
         try:
             with precision.use(a.mode), torch.no_grad():
@@ -51,7 +53,7 @@ def main():
     wt = conv.tap_major(w)
     gy = torch.randn(a.batch, 64, 128, 128, generator=g).cuda()
     dx = torch.empty(a.batch, 64, 256, 256, device="cuda")
-    for key, name in ((1, "dgrad_k_conv_lp"), (4, "dgrad_k_conv_stem_dgrad_lp")):
+    for key, name in ((1, "dgrad_k_conv_lp"), (4 + f32, "dgrad_k_conv_stem_dgrad_lp")):
         old = _lib.call_raw("e2ep_tune", 35, key)
         try:
             with precision.use(a.mode), torch.no_grad():
@@ -72,9 +74,9 @@ def main():
     dd = (outs["dgrad_k_conv_stem_dgrad_lp"] - outs["dgrad_k_conv_lp"]).double()
     res["dgrad_rel_l2_direct_vs_gemm"] = (dd.norm() / outs["dgrad_k_conv_lp"].double().norm()).item()
     res["dgrad_speedup"] = round(res["dgrad_k_conv_lp"]["us"] / res["dgrad_k_conv_stem_dgrad_lp"]["us"], 2)
-    if a.mode == "bf16":  # the weight gradient (bf16 operands in C3 only)
+    if a.mode != "fp16":  # the weight gradient (bf16 operands in C3, fp32 in C2)
         dw = torch.empty(64, 65, 7, 7, device="cuda")
-        for key, name in ((1, "wgrad_k_wgrad_lp"), (8, "wgrad_k_conv_stem_wgrad_lp")):
+        for key, name in ((1, "wgrad_k_wgrad_lp"), (8 + f32, "wgrad_k_conv_stem_wgrad_lp")):
             old = _lib.call_raw("e2ep_tune", 35, key)
             try:
                 with precision.use(a.mode), torch.no_grad():

@@ -173,3 +173,70 @@ def test_stem_direct_wgrad_vs_rounded_fp64(case):
     F.conv2d(r(x), w64, None, 2, 3).backward(r(gy))
     assert rel_l2(out[(8, 0)], w64.grad) < 5e-6
     assert rel_l2(out[(8, 0)], out[(1, 0)]) < 5e-6
+
+
+# fp32 operands (C2, exact-f32 MFMA, key 35 mask 8): the same kernels with v_mfma_f32_32x32x2_f32
+F32_CASES = [(2, 65, 256, 256), (2, 65, 50, 70), (1, 64, 64, 64), (1, 68, 32, 48)]
+
+
+@pytest.mark.parametrize("case", F32_CASES, ids=[str(i) for i in range(len(F32_CASES))])
+def test_stem_direct_fp32_vs_fp64(case):
+    from e2ep_amd import _lib, conv
+    N, Cin, H, W = case
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dims = (N, Cin, H, W, 64, 7, 7, P, Q, 2, 2, 3, 3, 1, 1)
+    g = torch.Generator().manual_seed(13 + H + Cin)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(64, Cin, 7, 7, generator=g) / (Cin * 49) ** 0.5
+    gy = torch.randn(N, 64, P, Q, generator=g)
+    xd, wd, gyd = x.to(DEV), w.to(DEV), gy.to(DEV)
+    wt = conv.tap_major(wd)
+    out = {}
+    for key in (12, 1):
+        old = _lib.call_raw("e2ep_tune", KEY, key)
+        try:
+            with torch.no_grad():
+                y = conv.conv2d(xd, wd, None, (2, 2), (3, 3, 3, 3), (1, 1), 0)
+            dx = torch.empty(N, 64, H, W, device=DEV)
+            conv.conv_dgrad(gyd, wt, dims, 64, dx, w_layout=1)
+            out[key] = (y, dx)
+        finally:
+            _lib.call_raw("e2ep_tune", KEY, old)
+    torch.cuda.synchronize()
+    y64 = F.conv2d(x.double(), w.double(), None, 2, 3)
+    x64 = torch.zeros(N, Cin, H, W, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x64, w.double(), None, 2, 3).backward(gy.double())
+    # fp32 sums of up to 65 x 49 products in another order than k_conv_gemm2's: ~1e-6
+    # relative (test_conv_gpu.py holds the implicit GEMMs to 1e-5 against fp64)
+    assert rel_l2(out[12][0], y64) < 5e-6
+    assert rel_l2(out[12][1], x64.grad[:, :64]) < 5e-6
+    assert rel_l2(out[12][0], out[1][0]) < 5e-6
+    assert rel_l2(out[12][1], out[1][1]) < 5e-6
+
+
+@pytest.mark.parametrize("case", WG_CASES, ids=[str(i) for i in range(len(WG_CASES))])
+def test_stem_direct_wgrad_fp32_vs_fp64(case):
+    """k_conv_stem_wgrad_lp<0> (exact-f32 MFMA, key 35 mask 4 | 8): C2's stem weight gradient,
+    and C5's (its fp16 mode keeps the weight gradient fp32)."""
+    from e2ep_amd import _lib, conv
+    N, Cin, H, W = case
+    P, Q = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dims = (N, Cin, H, W, 64, 7, 7, P, Q, 2, 2, 3, 3, 1, 1)
+    g = torch.Generator().manual_seed(17 + H + W + Cin)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    gy = torch.randn(N, 64, P, Q, generator=g)
+    xd, gyd = x.to(DEV), gy.to(DEV)
+    out = {}
+    for key in (16, 1):
+        old = _lib.call_raw("e2ep_tune", KEY, key)
+        try:
+            dw = torch.empty(64, Cin, 7, 7, device=DEV)
+            conv.conv_wgrad(gyd, xd, dims, dw)
+            out[key] = dw
+        finally:
+            _lib.call_raw("e2ep_tune", KEY, old)
+    torch.cuda.synchronize()
+    w64 = torch.zeros(64, Cin, 7, 7, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.double(), w64, None, 2, 3).backward(gy.double())
+    assert rel_l2(out[16], w64.grad) < 5e-6
+    assert rel_l2(out[16], out[1]) < 5e-6
