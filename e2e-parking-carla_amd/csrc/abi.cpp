@@ -20,11 +20,11 @@ void set_error(const char *fmt, ...) {
 // target 8192 and 512 float4 per BN apply workgroup (was 2048 / 1024), C2 20.78 -> 20.58 ms
 // (profiles/r06/bn_split_ab.txt); key 35 = 4, the direct-conv BEV stem forward and data
 // gradient (mask 1 | 2) on 16-bit operands: C3 17.74 -> 17.53 ms (forward) -> 17.49 ms (data
-// gradient).  On fp32 operands too (mask 8, key 12) C2 measured 20.56 -> 20.44 ms, but the
-// B = 8 eval-mode gradient-norm parity (test_model_b8_gpu) moved past its bound (1.36e-4 vs
-// fp64 on one camera-encoder BN weight), so fp32 stays on the implicit GEMMs; the direct weight
-// gradient (mask 4) is neutral in C3 and slower than k_conv_wgrad2 in fp32
-// (profiles/r06/stem_direct_ab.txt).
+// gradient).  On fp32 operands the forward (mask 16) took C2 20.56 -> 20.44 ms but moved the
+// B = 8 eval-mode gradient-norm parity (test_model_b8_gpu) past its bound (1.36e-4 vs fp64 on
+// one camera-encoder BN weight), and the fp32 data gradient (mask 8) alone is neutral, so fp32
+// stays on the implicit GEMMs; the direct weight gradient (mask 4) is neutral in C3 and slower
+// than k_conv_wgrad2 in fp32 (profiles/r06/stem_direct_ab.txt).
 int g_tune[TUNE_N] = {8192, 4096, 512, 512, 768, 1024, 512, 1, 1, 2, 1, 2, 2, 1, 2, 1, 1, 1, 1, 1, 1, 2, 1024, 2, 2048, 2, 1, 1, 2, 1, 2, 1, 1, 1, 1, 4};
 }  // namespace e2ep
 

@@ -102,8 +102,8 @@ int lp_bwd_pair_launch(const float *w, const float *gout, const float *res, void
 // the BEV stem in C3 / C5), conv_stem.hip: the forward (mode 0, k_conv_stem_lp) stages each
 // output tile's input patch once per 16-channel chunk, the data gradient (mode 1, pad 3, 64
 // gradient channels, k_conv_stem_dgrad_lp) each tile's gradient patch once.  Tap-major
-// weights; e2ep_tune key 35 = 1 + mask (1 forward, 2 data gradient, 4 weight gradient, 8 the
-// forward / data gradient on fp32 operands too, op 0).  workspace: stem_direct_workspace(g, mode,
+// weights; e2ep_tune key 35 = 1 + mask (1 forward, 2 data gradient, 4 weight gradient; on fp32
+// operands, op 0, also 8 for the gradients and 16 for the forward).  workspace: stem_direct_workspace(g, mode,
 // op) bytes for the weight image (k_stem_wprep*).
 bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op);
 size_t stem_direct_workspace(const ConvGeom &g, int mode, int op);

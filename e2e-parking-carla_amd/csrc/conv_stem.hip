@@ -630,13 +630,13 @@ size_t stem_direct_workspace(const ConvGeom &g, int mode, int op) {
   return (op == 0 ? 32 : 16) * (size_t)(mode == 0 ? stem_groups(g) : SG_CH * SD_K * SD_WROW8);
 }
 
-// e2ep_tune key 35 = 1 + mask: 1 the forward, 2 the data gradient, 4 the weight gradient (bf16
-// or fp32 operands), 8 the fp32-operand kernels too (exact-f32 MFMA: C2, and C5's fp32 weight
-// gradient)
+// e2ep_tune key 35 = 1 + mask: 1 the forward, 2 the data gradient, 4 the weight gradient; on fp32
+// operands (exact-f32 MFMA: C2, and C5's fp32 weight gradient) also 8 for the gradients and 16
+// for the forward
 bool stem_direct_ok(int mode, const ConvGeom &g, int M, int op) {
   const int mask = g_tune[TUNE_STEM_DIRECT] - 1;
   if (mode == 0 ? !(mask & 1) : mode == 1 ? !(mask & 2) : mode == 2 ? !(mask & 4) : true) return false;
-  if (op < 0 || op > 2 || (op == 0 && !(mask & 8)) || (mode == 2 && op == 2) ||
+  if (op < 0 || op > 2 || (op == 0 && !(mask & (mode == 0 ? 16 : 8))) || (mode == 2 && op == 2) ||
       (mode != 2 && g.wlayout != 1))
     return false;
   if (g.R != SD_K || g.S != SD_K || g.sh != 2 || g.sw != 2 || g.dh != 1 || g.dw != 1) return false;

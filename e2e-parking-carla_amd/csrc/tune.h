@@ -38,7 +38,7 @@ enum Tune {
   TUNE_LSS_FWD = 32,          // k_lss_fwd shape: 1 = automatic (16 x 16 when a sample's featT > 4 MB, else 16 x 8), 2 = 32 groups x 8 rows in flight, 3 = 16 x 16, 4 = 32 x 16, 5 = 16 x 8
   TUNE_BN_ORDER = 33,         // split BN sweeps back to front: 1 + mask (1 bwd apply, 2 bwd reduction, 4 fwd apply); 1 = all front to back
   TUNE_SE_EXCITE_MLP = 34,    // squeeze-excitation logits inside the excite launch: 2 = on, 1 = k_se_logits + k_se_excite
-  TUNE_STEM_DIRECT = 35,      // BEV stem (7x7/2, 64 out, 16-bit operands) on the direct-conv kernels: 1 + mask (1 forward k_conv_stem_lp, 2 data gradient k_conv_stem_dgrad_lp, 4 weight gradient k_conv_stem_wgrad_lp (bf16), 8 forward / data gradient on fp32 operands too); 1 = the implicit GEMMs
+  TUNE_STEM_DIRECT = 35,      // BEV stem (7x7/2, 64 out, 16-bit operands) on the direct-conv kernels: 1 + mask (1 forward k_conv_stem_lp, 2 data gradient k_conv_stem_dgrad_lp, 4 weight gradient k_conv_stem_wgrad_lp; fp32 operands also 8 the gradients, 16 the forward); 1 = the implicit GEMMs
   TUNE_N = 36
 };
 extern int g_tune[TUNE_N];

@@ -5,7 +5,7 @@ gradient's time includes its split reduction.  Mean device time per
 call over --iters calls (HIP events; the weight-image prep launch included), after warmup.
 
     python scripts/bench_stem.py [--mode bf16|fp16|fp32] [--batch 8] [--iters 50]
-(fp32: the exact-f32 MFMA variants, key 35 mask 8, against k_conv_gemm2)"""
+(fp32: the exact-f32 MFMA variants, key 35 mask 16 / 8, against k_conv_gemm2 / k_conv_wgrad2)"""
 import argparse
 import json
 import os
@@ -30,8 +30,8 @@ def main():
     flop = 2.0 * a.batch * 64 * 128 * 128 * 65 * 49
     res = {"config": f"B={a.batch} 65x256^2 -> 64x128^2, 7x7/2, {a.mode} operands", "flop": flop}
     outs = {}
-    f32 = 8 if a.mode == "fp32" else 0
-    for key, name in ((1, "k_conv_lp"), (2 + f32, "k_conv_stem_lp")):
+    f32 = 8 if a.mode == "fp32" else 0  # key 35 mask 8: fp32 gradients, 16: fp32 forward
+    for key, name in ((1, "k_conv_lp"), (2 + 3 * f32, "k_conv_stem_lp")):
         old = _lib.call_raw("e2ep_tune", 35, key)
         try:
             with precision.use(a.mode), torch.no_grad():
