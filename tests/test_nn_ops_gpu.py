@@ -161,6 +161,28 @@ def test_resize(case):
     assert rel_l2(xd.grad, x64.grad) < 2e-5
 
 
+@pytest.mark.parametrize("shape,out", [((2, 8, 50, 60), (40, 92)), ((2, 65, 200, 200), (256, 256)),
+                                       ((1, 3, 128, 128), (200, 200))])
+def test_resize_fwd_vector_path_bitwise(shape, out):
+    """e2ep_resize_fwd's four-outputs-per-thread kernel (k_resize_fwd4: Wo % 4 == 0 and a 16-B
+    aligned y) equals the one-output kernel (taken for a y one float off alignment) bitwise."""
+    from e2ep_amd import _lib
+    N, C, Hi, Wi = shape
+    Ho, Wo = out
+    x = torch.randn(*shape, generator=_g(Hi + Wo)).to(DEV)
+    n = N * C * Ho * Wo
+    buf = torch.full((n + 4,), float("nan"), device=DEV)
+    ys = []
+    for off in (0, 1):  # aligned: k_resize_fwd4; one float off: k_resize_fwd
+        y = buf[off:off + n]
+        _lib.call("e2ep_resize_fwd", _lib.ptr(x), N, C, C * Hi * Wi, Hi, Wi, Ho, Wo, Hi / Ho, Wi / Wo,
+                  _lib.ptr(y), C * Ho * Wo, _lib.stream())
+        ys.append(y.clone())
+    assert torch.equal(ys[0], ys[1])
+    y32 = F.interpolate(x.cpu(), size=out, mode="bilinear", align_corners=False)
+    assert rel_l2(ys[0].view(N, C, Ho, Wo), y32) < 1e-6
+
+
 @pytest.mark.parametrize("case", [(4, 144, 64, 64, 3, 2, (0, 1, 0, 1)), (4, 48, 32, 32, 3, 1, (1, 1, 1, 1)),
                                   (4, 192, 32, 32, 5, 2, (2, 2, 2, 2)), (2, 672, 16, 16, 5, 1, (2, 2, 2, 2)),
                                   (3, 8, 13, 11, 3, 2, (0, 1, 0, 1)), (2, 24, 128, 128, 3, 1, (1, 1, 1, 1)),
